@@ -1,0 +1,238 @@
+#!/usr/bin/env python3
+"""bench.py -- BASELINE.json metric: GiB/s of key-value payload through the
+filter encode+decode chain, device-resident, on MI355X.
+
+Default workload (BASELINE.json configs[1]): one message
+per step carrying n = 2^27 dense float32 values (512 MiB, N(0,1), seed 1) and
+the chain [FIXING_FLOAT num_bytes=1] with min/max computed; a step encodes it on
+the worker's RemoteNode, delivers it and decodes it on the server's
+(libpsf psf_node_roundtrip: no Python per message).  Payload = 4n bytes/step.
+
+N GPUs (torchrun, one rank per GPU): rank g is server g of EvenDivide(N, g)
+and codes its own pre-placed shard (no data-path collective; weak scaling).
+Timed region: barrier + synchronize, K steps, barrier + synchronize; the max
+elapsed over ranks is the job time.  value = N * K * payload / time.
+
+roofline: per-kernel durations from HIP events recorded on the launch stream
+around every kernel inside the timed region (libpsf profiler); the dominant
+kernel's algorithmic bytes / average duration vs 8 TB/s.  traffic: PMC-derived
+HBM bytes per launch from profiles/pmc_traffic.json when it matches (see
+tools/pmc_traffic.py), else null.
+cpu_baseline: the reference's own filter code (oracle/_ref, unmodified
+headers) -- or the C restatement if that is absent -- on one host core, rank 0
+at N=1 only, over a bounded sample (2^24 values, repeated ~10 s).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+GIB = float(1 << 30)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, MI355X_MICROARCH.md
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--n", type=int, default=1 << 27, help="values per message (per GPU)")
+    ap.add_argument("--nb", type=int, default=1, help="FIXING_FLOAT num_bytes")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(n_sample: int, nb: int, seconds: float):
+    import ctypes as C
+
+    import numpy as np
+
+    import oracle
+    x = np.random.default_rng(1).standard_normal(n_sample).astype(np.float32)
+    kind = "port"
+    try:
+        R = oracle.Ref()
+        kind = "reference"
+    except Exception:
+        R = None
+    reps, t = 0, 0.0
+    if R is not None:
+        L = R.lib
+        R.set_time(12345)
+        snd, rcv = L.psref_node_new(), L.psref_node_new()
+        while t < seconds or reps == 0:
+            m = R.msg_new(request=True, push=True)
+            L.psref_msg_add_value(m, x.ctypes.data_as(C.c_void_p), x.nbytes, 9)
+            fi = L.psref_msg_add_filter(m, 3)
+            L.psref_fc_set_num_bytes(m, fi, nb)
+            t0 = time.perf_counter()
+            assert L.psref_node_encode(snd, m) == 0
+            w = L.psref_msg_clone(m)
+            assert L.psref_node_decode(rcv, w) == 0
+            t += time.perf_counter() - t0
+            L.psref_msg_free(w)
+            L.psref_msg_free(m)
+            reps += 1
+    else:
+        P = oracle.Port()
+        while t < seconds or reps == 0:
+            t0 = time.perf_counter()
+            st, codes, mn, mx = P.ff_encode(x, nb, 12345)
+            P.ff_decode(codes, nb, mn, mx)
+            t += time.perf_counter() - t0
+            reps += 1
+    return {
+        "value": round(reps * x.nbytes / t / GIB, 4),
+        "unit": "GiB/s",
+        "cores": 1,
+        "kind": kind,
+        "sample": f"{reps} x FIXING_FLOAT(nb={nb}) encode+decode of 2^{n_sample.bit_length() - 1} f32 "
+                  f"({x.nbytes >> 20} MiB), single-threaded as the reference's filters run, "
+                  f"{t:.1f} s CPU",
+        "cpu_model": _cpu_model(),
+        "nproc": os.cpu_count(),
+    }
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def pmc_traffic(kernel: str, n: int, nb: int):
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    e = d.get(kernel)
+    if not e or e.get("n") != n or e.get("nb") != nb:
+        return None
+    return e.get("hbm_bytes_per_launch")
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+
+    from parameter_server_amd import FIXING_FLOAT
+    from parameter_server_amd import filter as F
+
+    n, nb = args.n, args.nb
+    # this rank's shard of the key range (range.h:100-107 EvenDivide), pre-placed
+    g = torch.Generator(device=f"cuda:{local}")
+    g.manual_seed(1 + rank)
+    x = torch.randn(n, device=f"cuda:{local}", generator=g, dtype=torch.float32)
+
+    ctx = F.Context(local)
+    worker, server = F.RemoteNode(ctx), F.RemoteNode(ctx)
+    F.set_clock(12345)  # FIXING_FLOAT seed (time(NULL) in the reference)
+    tmpl = F.Message(request=True, push=True, key_channel=0)
+    tmpl.add_value(x)
+    tmpl.add_filter(FIXING_FLOAT, num_bytes=nb)
+
+    worker.roundtrip(server, tmpl, args.warmup)
+    torch.cuda.synchronize()
+    if not args.no_profile:
+        ctx.profile(True)
+    ctx.profile_reset()
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    worker.roundtrip(server, tmpl, args.steps)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    prof = ctx.profile_read()
+    ctx.profile(False)
+
+    if world > 1:
+        t = torch.tensor([elapsed], device=f"cuda:{local}", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    payload = 4 * n  # key bytes 0 (dense values), value bytes 4n
+    value = world * args.steps * payload / elapsed / GIB
+
+    roofline = None
+    if prof:
+        dom = max(prof, key=lambda k: prof[k][1])
+        launches, ms, alg = prof[dom]
+        per_launch_bytes = alg / launches
+        avg_s = ms / launches / 1e3
+        achieved = per_launch_bytes / avg_s / 1e9
+        traffic = pmc_traffic(dom, n, nb)
+        roofline = {
+            "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "kernel": dom,
+            "kernels": {k: {"launches": v[0], "avg_us": round(v[1] / v[0] * 1e3, 2),
+                            "alg_bytes_per_launch": int(v[2] / v[0]),
+                            "GBps": round(v[2] / v[0] / (v[1] / v[0] / 1e3) / 1e9, 1)}
+                        for k, v in prof.items()},
+        }
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(1 << 24, nb, args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": "GiB/s key-value payload through filter encode+decode, device-resident",
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: f32 N(0,1) values, seed 1+rank, FIXING_FLOAT LCG seed 12345",
+            "config": {
+                "workload": "C2 (BASELINE configs[1]): dense f32 values, chain [FIXING_FLOAT "
+                            f"num_bytes={nb}], min/max computed, encode+decode round trip per step",
+                "n_values_per_gpu": n,
+                "payload_bytes_per_step_per_gpu": payload,
+                "value_type": "float32",
+                "num_bytes": nb,
+                "parallelism": f"server key-range shards x{world} (EvenDivide), no data-path collective",
+            },
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,177 @@
+/*
+ * libpsf -- MI355X-native (HIP/gfx950) parameter_server filter codec chain.
+ *
+ * C ABI of the drop-in boundary.  Plain pointers and sizes only; `stream` is a
+ * hipStream_t passed as void* (NULL = the context's own stream).  Every entry
+ * point returns PSF_OK (0) or a negative PSF_ERR_* code; psf_last_error()
+ * describes the last failure on the calling thread.  The reference aborts the
+ * process through glog CHECK at the same points; the C++ shim in
+ * include/psf_ps_filter.h maps a non-zero status back to that fatal CHECK.
+ *
+ * Two layers:
+ *
+ *  1. Codec kernels -- what a reference Filter subclass binds
+ *     (replaces the element loops of the reference headers):
+ *       psf_ff_encode / psf_ff_decode   <- FixingFloatFilter::convert<V>
+ *                                          src/filter/fixing_float.h:50-101
+ *       psf_key_signature / psf_crc32c  <- KeyCachingFilter signature
+ *                                          src/filter/key_caching.h:18,43
+ *                                          (crc32c::Value, src/util/crc32c.h:19-21)
+ *
+ *  2. Filter plugin surface -- the reference's message path in one library:
+ *       psf_node_encode / psf_node_decode  <- RemoteNode::EncodeMessage / DecodeMessage
+ *                                             src/system/remote_node.cc:17-29, running
+ *                                             Filter::create (src/filter/filter.cc:9-23)
+ *                                             instances of KEY_CACHING, FIXING_FLOAT,
+ *                                             COMPRESSING, NOISE on HBM buffers
+ *       psf_msg_* / psf_fc_*               <- Message / Task / FilterConfig fields
+ *                                             (src/system/message.h:10-76,
+ *                                             src/system/proto/task.proto:28-39,
+ *                                             src/filter/proto/filter.proto:3-35)
+ */
+#ifndef PSF_H_
+#define PSF_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---------------------------------------------------- */
+#define PSF_OK 0
+#define PSF_ERR_ARG (-1)         /* bad argument / unknown filter type            */
+#define PSF_ERR_NBYTES (-2)      /* CHECK_GT(nbytes,0), CHECK_LT(nbytes,8)        */
+#define PSF_ERR_BIN (-3)         /* CHECK_GT(bin,0): max <= min after +1e-6        */
+#define PSF_ERR_HIP (-4)         /* HIP runtime failure                           */
+#define PSF_ERR_CHECK (-5)       /* other reference CHECK (signature mismatch ...) */
+#define PSF_ERR_UNSUPPORTED (-6)
+
+/* ---- task.proto DataType / filter.proto Type values -------------------- */
+#define PSF_DT_UINT64 8
+#define PSF_DT_FLOAT 9
+#define PSF_DT_DOUBLE 10
+#define PSF_DT_CHAR 11
+#define PSF_KEY_CACHING 1
+#define PSF_COMPRESSING 2
+#define PSF_FIXING_FLOAT 3
+#define PSF_NOISE 4
+
+/* buffer location */
+#define PSF_LOC_HOST 0
+#define PSF_LOC_DEVICE 1
+
+const char* psf_last_error(void);
+const char* psf_version(void);
+
+/* time(NULL) is FIXING_FLOAT's LCG seed in the reference (fixing_float.h:78);
+ * enable=1 pins it to `t` process-wide (parity testing), enable=0 restores it. */
+void psf_set_clock(int enable, int64_t t);
+
+/* ---- execution context (device + stream + workspace) ------------------- */
+typedef struct psf_context psf_context;
+int psf_context_create(int device, void* stream, psf_context** out);
+int psf_context_destroy(psf_context* ctx);
+int psf_context_sync(psf_context* ctx);
+
+/* ---- layer 1: codec kernels (device pointers, async unless noted) ------ */
+typedef struct {
+  int32_t has_min, has_max; /* FixedFloatConfig has-bits                      */
+  float min_value, max_value;
+} psf_fixed_point;
+
+/* FIXING_FLOAT encode of n values (value_type FLOAT/DOUBLE) into n*num_bytes
+ * bytes at d_code.  fp is in/out: preset min/max are honoured, computed ones
+ * are written back (this call then synchronises the stream once).  `seed` is
+ * the LCG seed the reference takes from time(NULL). */
+int psf_ff_encode(psf_context* ctx, const void* d_values, size_t n, int value_type,
+                  int num_bytes, psf_fixed_point* fp, int32_t seed, void* d_code);
+
+/* Fully asynchronous encode: side-info {min,max} goes to d_range (device
+ * float[2]) and the CHECK_GT(bin,0) outcome to d_status (device int32,
+ * PSF_OK or PSF_ERR_BIN); either may be NULL. */
+int psf_ff_encode_async(psf_context* ctx, const void* d_values, size_t n, int value_type,
+                        int num_bytes, const psf_fixed_point* preset, int32_t seed,
+                        void* d_code, float* d_range, int32_t* d_status);
+
+/* FIXING_FLOAT decode of n codes into n values, min/max from the received
+ * FilterConfig (psf_ff_decode) or from device memory (psf_ff_decode_async). */
+int psf_ff_decode(psf_context* ctx, const void* d_code, size_t n, int value_type,
+                  int num_bytes, float min_value, float max_value, void* d_values);
+int psf_ff_decode_async(psf_context* ctx, const void* d_code, size_t n, int value_type,
+                        int num_bytes, const float* d_range, void* d_values);
+
+/* CRC32C of d_data[0:bytes) -> *crc (host); synchronous. */
+int psf_crc32c(psf_context* ctx, const void* d_data, size_t bytes, uint32_t* crc);
+/* KEY_CACHING signature: CRC32C of the first min(bytes, 2048) key bytes. */
+int psf_key_signature(psf_context* ctx, const void* d_keys, size_t bytes, uint32_t* sig);
+
+/* ---- layer 2: messages and the filter chain ---------------------------- */
+typedef struct psf_message psf_message;
+typedef struct psf_node psf_node;
+
+/* A RemoteNode: one filter instance per type, created on first use. */
+int psf_node_create(psf_context* ctx, psf_node** out);
+int psf_node_destroy(psf_node* node);
+int psf_node_encode(psf_node* node, psf_message* msg);
+int psf_node_decode(psf_node* node, psf_message* msg);
+
+/* Task fields the filters read (task.proto:28-39; param.push = ParamCall). */
+int psf_msg_create(int request, int has_param, int push, int32_t key_channel,
+                   int has_key_range, uint64_t key_range_begin, uint64_t key_range_end,
+                   psf_message** out);
+int psf_msg_destroy(psf_message* msg);
+/* Receiver-side copy: same Task (incl. all filter side-info) and the same
+ * buffers (zero-copy), as the wire delivers it. */
+int psf_msg_clone(const psf_message* msg, psf_message** out);
+
+/* Attach caller memory (not copied, not freed; keep it alive while any
+ * message or key cache refers to it).  loc = PSF_LOC_DEVICE / PSF_LOC_HOST. */
+int psf_msg_set_key(psf_message* msg, void* ptr, size_t bytes, int key_type, int loc);
+int psf_msg_add_value(psf_message* msg, void* ptr, size_t bytes, int value_type, int loc);
+int psf_msg_key(const psf_message* msg, void** ptr, size_t* bytes, int* loc);
+int psf_msg_key_info(const psf_message* msg, int* has_key_flag, int* key_type);
+int psf_msg_num_values(const psf_message* msg);
+int psf_msg_value(const psf_message* msg, int i, void** ptr, size_t* bytes, int* loc);
+
+/* FilterConfig access; `idx` is the position in task.filter. */
+int psf_msg_add_filter(psf_message* msg, int type);  /* returns idx >= 0 or error */
+int psf_fc_set_num_bytes(psf_message* msg, int idx, int num_bytes);
+int psf_fc_set_clear_cache(psf_message* msg, int idx, int enable);
+int psf_fc_set_noise(psf_message* msg, int idx, float mean, float std);
+int psf_fc_add_fixed_point(psf_message* msg, int idx, const psf_fixed_point* fp);
+int psf_fc_num_fixed_point(const psf_message* msg, int idx);
+int psf_fc_fixed_point(const psf_message* msg, int idx, int k, psf_fixed_point* fp);
+int psf_fc_signature(const psf_message* msg, int idx, int* has_signature, uint32_t* sig);
+int psf_fc_num_uncompressed(const psf_message* msg, int idx);
+int psf_fc_uncompressed(const psf_message* msg, int idx, int i, uint64_t* size);
+
+/* Message path driver (what Executor::Submit -> remote peer -> PickActiveMsg
+ * does per message, executor.cc:131-146,178-219): `iters` times, encode a
+ * fresh copy of `tmpl` on `snd`, deliver it (Task copy + zero-copy buffers)
+ * and decode it on `rcv`.  The last decoded message is returned in *out
+ * (may be NULL).  Used by bench.py so no Python runs per message. */
+int psf_node_roundtrip(psf_node* snd, psf_node* rcv, const psf_message* tmpl, int iters,
+                       psf_message** out);
+
+/* ---- launch profiler (HIP events on the launch stream) ----------------- */
+#define PSF_K_MINMAX 0
+#define PSF_K_ENCODE 1
+#define PSF_K_DECODE 2
+#define PSF_K_CRC32C 3
+#define PSF_K_NOISE 4
+#define PSF_K_SNAPPY_COMPRESS 5
+#define PSF_K_SNAPPY_DECOMPRESS 6
+#define PSF_K_NUM 7
+int psf_profile_enable(psf_context* ctx, int enable);
+int psf_profile_reset(psf_context* ctx);
+/* launches, summed kernel milliseconds and summed algorithmic HBM bytes */
+int psf_profile_read(psf_context* ctx, int kernel, int64_t* launches, double* total_ms,
+                     double* alg_bytes);
+const char* psf_profile_kernel_name(int kernel);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PSF_H_ */

@@ -1,0 +1,111 @@
+"""ctypes binding of libpsf.so (include/psf.h).
+
+The library is built in-tree (parameter_server_amd/libpsf.so) by
+``parameter_server_amd.build``.  There is no CPU fallback: if the shared
+library is missing, loading fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpsf.so")
+
+PSF_OK = 0
+PSF_ERR_ARG = -1
+PSF_ERR_NBYTES = -2
+PSF_ERR_BIN = -3
+PSF_ERR_HIP = -4
+PSF_ERR_CHECK = -5
+PSF_ERR_UNSUPPORTED = -6
+
+DT_UINT64, DT_FLOAT, DT_DOUBLE, DT_CHAR = 8, 9, 10, 11
+KEY_CACHING, COMPRESSING, FIXING_FLOAT, NOISE = 1, 2, 3, 4
+LOC_HOST, LOC_DEVICE = 0, 1
+
+
+class PsfError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"psf error {code}: {msg}")
+        self.code = code
+
+
+class FixedPoint(C.Structure):
+    _fields_ = [("has_min", C.c_int32), ("has_max", C.c_int32),
+                ("min_value", C.c_float), ("max_value", C.c_float)]
+
+
+vp, sz, i32, u32, u64 = C.c_void_p, C.c_size_t, C.c_int32, C.c_uint32, C.c_uint64
+PI = C.POINTER(C.c_int)
+
+# name -> (argtypes, restype); the exported surface of include/psf.h
+SIGNATURES = {
+    "psf_last_error": ([], C.c_char_p),
+    "psf_version": ([], C.c_char_p),
+    "psf_set_clock": ([C.c_int, C.c_int64], None),
+    "psf_context_create": ([C.c_int, vp, C.POINTER(vp)], C.c_int),
+    "psf_context_destroy": ([vp], C.c_int),
+    "psf_context_sync": ([vp], C.c_int),
+    "psf_ff_encode": ([vp, vp, sz, C.c_int, C.c_int, C.POINTER(FixedPoint), i32, vp], C.c_int),
+    "psf_ff_encode_async": ([vp, vp, sz, C.c_int, C.c_int, C.POINTER(FixedPoint), i32, vp, vp, vp], C.c_int),
+    "psf_ff_decode": ([vp, vp, sz, C.c_int, C.c_int, C.c_float, C.c_float, vp], C.c_int),
+    "psf_ff_decode_async": ([vp, vp, sz, C.c_int, C.c_int, vp, vp], C.c_int),
+    "psf_crc32c": ([vp, vp, sz, C.POINTER(u32)], C.c_int),
+    "psf_key_signature": ([vp, vp, sz, C.POINTER(u32)], C.c_int),
+    "psf_node_create": ([vp, C.POINTER(vp)], C.c_int),
+    "psf_node_destroy": ([vp], C.c_int),
+    "psf_node_encode": ([vp, vp], C.c_int),
+    "psf_node_decode": ([vp, vp], C.c_int),
+    "psf_msg_create": ([C.c_int, C.c_int, C.c_int, i32, C.c_int, u64, u64, C.POINTER(vp)], C.c_int),
+    "psf_msg_destroy": ([vp], C.c_int),
+    "psf_msg_clone": ([vp, C.POINTER(vp)], C.c_int),
+    "psf_msg_set_key": ([vp, vp, sz, C.c_int, C.c_int], C.c_int),
+    "psf_msg_add_value": ([vp, vp, sz, C.c_int, C.c_int], C.c_int),
+    "psf_msg_key": ([vp, C.POINTER(vp), C.POINTER(sz), PI], C.c_int),
+    "psf_msg_key_info": ([vp, PI, PI], C.c_int),
+    "psf_msg_num_values": ([vp], C.c_int),
+    "psf_msg_value": ([vp, C.c_int, C.POINTER(vp), C.POINTER(sz), PI], C.c_int),
+    "psf_msg_add_filter": ([vp, C.c_int], C.c_int),
+    "psf_fc_set_num_bytes": ([vp, C.c_int, C.c_int], C.c_int),
+    "psf_fc_set_clear_cache": ([vp, C.c_int, C.c_int], C.c_int),
+    "psf_fc_set_noise": ([vp, C.c_int, C.c_float, C.c_float], C.c_int),
+    "psf_fc_add_fixed_point": ([vp, C.c_int, C.POINTER(FixedPoint)], C.c_int),
+    "psf_fc_num_fixed_point": ([vp, C.c_int], C.c_int),
+    "psf_fc_fixed_point": ([vp, C.c_int, C.c_int, C.POINTER(FixedPoint)], C.c_int),
+    "psf_fc_signature": ([vp, C.c_int, PI, C.POINTER(u32)], C.c_int),
+    "psf_fc_num_uncompressed": ([vp, C.c_int], C.c_int),
+    "psf_fc_uncompressed": ([vp, C.c_int, C.c_int, C.POINTER(u64)], C.c_int),
+    "psf_node_roundtrip": ([vp, vp, vp, C.c_int, C.POINTER(vp)], C.c_int),
+    "psf_profile_enable": ([vp, C.c_int], C.c_int),
+    "psf_profile_reset": ([vp], C.c_int),
+    "psf_profile_read": ([vp, C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_double),
+                          C.POINTER(C.c_double)], C.c_int),
+    "psf_profile_kernel_name": ([C.c_int], C.c_char_p),
+}
+
+KERNELS = ("ff_minmax_partials", "ff_encode", "ff_decode", "crc32c_chunks", "noise_add",
+           "snappy_compress", "snappy_decompress")
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load libpsf.so (once).  Raises if the HIP library was not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is missing: run `python -m parameter_server_amd.build` "
+                              "(there is no CPU fallback)")
+        L = C.CDLL(LIB_PATH)
+        for name, (args, res) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.argtypes = args
+            f.restype = res
+        _lib = L
+    return _lib
+
+
+def check(status: int) -> int:
+    if status < 0:
+        raise PsfError(status, lib().psf_last_error().decode())
+    return status

@@ -1,0 +1,353 @@
+// extern "C" boundary of libpsf (include/psf.h).
+#include "../../../include/psf.h"
+
+#include <string>
+
+#include "filter.h"
+
+struct psf_context { psf::Context* impl; };
+struct psf_node { psf::RemoteNode* impl; };
+struct psf_message { psf::Message m; };
+
+namespace {
+thread_local std::string g_last_error;
+
+template <typename F> int guarded(F&& f) {
+  try {
+    return f();
+  } catch (const psf::CheckError& e) {
+    g_last_error = e.what();
+    return e.code;
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+    return PSF_ERR_CHECK;
+  }
+}
+
+psf::FilterConfig* fc_at(psf_message* msg, int idx) {
+  if (!msg || idx < 0 || idx >= (int)msg->m.task.filter.size())
+    throw psf::CheckError(PSF_ERR_ARG, "filter index out of range");
+  return &msg->m.task.filter[idx];
+}
+const psf::FilterConfig* fc_at(const psf_message* msg, int idx) {
+  return fc_at(const_cast<psf_message*>(msg), idx);
+}
+psf::Buffer wrap(void* ptr, size_t bytes, int loc) {
+  psf::Buffer b;
+  b.ptr = static_cast<uint8_t*>(ptr);
+  b.bytes = ptr ? bytes : 0;
+  b.loc = loc == PSF_LOC_HOST ? psf::Loc::kHost : psf::Loc::kDevice;
+  return b;
+}
+}  // namespace
+
+extern "C" {
+
+const char* psf_last_error(void) { return g_last_error.c_str(); }
+const char* psf_version(void) { return "psf 0.1 gfx950"; }
+void psf_set_clock(int enable, int64_t t) { psf::set_clock_override(enable != 0, t); }
+
+int psf_context_create(int device, void* stream, psf_context** out) {
+  return guarded([&] {
+    if (!out) return PSF_ERR_ARG;
+    *out = new psf_context{new psf::Context(device, static_cast<hipStream_t>(stream))};
+    return PSF_OK;
+  });
+}
+int psf_context_destroy(psf_context* ctx) {
+  if (!ctx) return PSF_OK;
+  delete ctx->impl;
+  delete ctx;
+  return PSF_OK;
+}
+int psf_context_sync(psf_context* ctx) {
+  return guarded([&] { ctx->impl->sync(); return PSF_OK; });
+}
+
+// ---------------------------------------------------------------- kernels
+int psf_ff_encode(psf_context* ctx, const void* d_values, size_t n, int value_type,
+                  int num_bytes, psf_fixed_point* fp, int32_t seed, void* d_code) {
+  return guarded([&] {
+    if (!ctx || !fp) return PSF_ERR_ARG;
+    if (num_bytes <= 0 || num_bytes >= 8) return PSF_ERR_NBYTES;
+    if (value_type != PSF_DT_FLOAT && value_type != PSF_DT_DOUBLE) return PSF_ERR_ARG;
+    psf::Context& c = *ctx->impl;
+    psf::FixedPoint pre{fp->has_min, fp->has_max, fp->min_value, fp->max_value};
+    if (pre.has_min && pre.has_max) {
+      if (!((double)pre.max_value - (double)pre.min_value > 0)) return PSF_ERR_BIN;
+      return psf::ff_encode_launch(d_values, n, value_type, num_bytes, pre, (uint32_t)seed, d_code,
+                                   c.partials(), nullptr, nullptr, c.stream(), c.prof());
+    }
+    if (n == 0) return PSF_ERR_ARG;  // min/max of an empty array
+    psf::Slot* s = c.d_slots();
+    int st = psf::ff_encode_launch(d_values, n, value_type, num_bytes, pre, (uint32_t)seed, d_code,
+                                   c.partials(), s->range, &s->status, c.stream(), c.prof());
+    if (st != PSF_OK) return st;
+    c.fetch_slots(1);
+    const psf::Slot& h = c.h_slots()[0];
+    if (!fp->has_min) { fp->min_value = h.range[0]; fp->has_min = 1; }
+    if (!fp->has_max) { fp->max_value = h.range[1]; fp->has_max = 1; }
+    return h.status;
+  });
+}
+
+int psf_ff_encode_async(psf_context* ctx, const void* d_values, size_t n, int value_type,
+                        int num_bytes, const psf_fixed_point* preset, int32_t seed,
+                        void* d_code, float* d_range, int32_t* d_status) {
+  return guarded([&] {
+    if (!ctx) return PSF_ERR_ARG;
+    psf::FixedPoint pre{0, 0, 0.f, 0.f};
+    if (preset) pre = psf::FixedPoint{preset->has_min, preset->has_max, preset->min_value, preset->max_value};
+    psf::Context& c = *ctx->impl;
+    return psf::ff_encode_launch(d_values, n, value_type, num_bytes, pre, (uint32_t)seed, d_code,
+                                 c.partials(), d_range, d_status, c.stream(), c.prof());
+  });
+}
+
+int psf_ff_decode(psf_context* ctx, const void* d_code, size_t n, int value_type,
+                  int num_bytes, float min_value, float max_value, void* d_values) {
+  return guarded([&] {
+    if (!ctx) return PSF_ERR_ARG;
+    if (!((double)max_value - (double)min_value > 0)) return PSF_ERR_BIN;
+    return psf::ff_decode_launch(d_code, n, value_type, num_bytes, nullptr, min_value, max_value,
+                                 d_values, ctx->impl->stream(), ctx->impl->prof());
+  });
+}
+
+int psf_ff_decode_async(psf_context* ctx, const void* d_code, size_t n, int value_type,
+                        int num_bytes, const float* d_range, void* d_values) {
+  return guarded([&] {
+    if (!ctx || !d_range) return PSF_ERR_ARG;
+    return psf::ff_decode_launch(d_code, n, value_type, num_bytes, d_range, 0.f, 0.f, d_values,
+                                 ctx->impl->stream(), ctx->impl->prof());
+  });
+}
+
+int psf_crc32c(psf_context* ctx, const void* d_data, size_t bytes, uint32_t* crc) {
+  return guarded([&] {
+    if (!ctx || !crc) return PSF_ERR_ARG;
+    psf::Context& c = *ctx->impl;
+    int st = psf::crc32c_launch(d_data, bytes, &c.d_slots()[0].crc, c.stream(), c.prof());
+    if (st != PSF_OK) return st;
+    c.fetch_slots(1);
+    *crc = c.h_slots()[0].crc;
+    return PSF_OK;
+  });
+}
+
+int psf_key_signature(psf_context* ctx, const void* d_keys, size_t bytes, uint32_t* sig) {
+  return psf_crc32c(ctx, d_keys, bytes < 2048 ? bytes : 2048, sig);
+}
+
+// ---------------------------------------------------------------- chain
+int psf_node_create(psf_context* ctx, psf_node** out) {
+  return guarded([&] {
+    if (!ctx || !out) return PSF_ERR_ARG;
+    *out = new psf_node{new psf::RemoteNode(ctx->impl)};
+    return PSF_OK;
+  });
+}
+int psf_node_destroy(psf_node* node) {
+  if (!node) return PSF_OK;
+  delete node->impl;
+  delete node;
+  return PSF_OK;
+}
+int psf_node_encode(psf_node* node, psf_message* msg) {
+  return guarded([&] {
+    if (!node || !msg) return PSF_ERR_ARG;
+    node->impl->EncodeMessage(&msg->m);
+    return PSF_OK;
+  });
+}
+int psf_node_decode(psf_node* node, psf_message* msg) {
+  return guarded([&] {
+    if (!node || !msg) return PSF_ERR_ARG;
+    node->impl->DecodeMessage(&msg->m);
+    return PSF_OK;
+  });
+}
+
+int psf_msg_create(int request, int has_param, int push, int32_t key_channel,
+                   int has_key_range, uint64_t kr_begin, uint64_t kr_end, psf_message** out) {
+  return guarded([&] {
+    if (!out) return PSF_ERR_ARG;
+    auto* m = new psf_message();
+    m->m.task.request = request != 0;
+    m->m.task.has_param = has_param != 0;
+    m->m.task.push = push != 0;
+    m->m.task.key_channel = key_channel;
+    if (has_key_range) {
+      m->m.task.has_key_range = true;
+      m->m.task.key_range = psf::KeyRange{kr_begin, kr_end};
+    }
+    *out = m;
+    return PSF_OK;
+  });
+}
+int psf_msg_destroy(psf_message* msg) {
+  delete msg;
+  return PSF_OK;
+}
+int psf_msg_clone(const psf_message* msg, psf_message** out) {
+  return guarded([&] {
+    if (!msg || !out) return PSF_ERR_ARG;
+    *out = new psf_message(*msg);
+    return PSF_OK;
+  });
+}
+
+int psf_msg_set_key(psf_message* msg, void* ptr, size_t bytes, int key_type, int loc) {
+  return guarded([&] {
+    if (!msg) return PSF_ERR_ARG;
+    auto& t = msg->m.task;
+    msg->m.key = wrap(ptr, bytes, loc);
+    t.has_key = msg->m.key.bytes > 0;
+    t.key_type = key_type;
+    if (!t.has_key_range) { t.has_key_range = true; t.key_range = psf::KeyRange::All(); }
+    return PSF_OK;
+  });
+}
+int psf_msg_add_value(psf_message* msg, void* ptr, size_t bytes, int value_type, int loc) {
+  return guarded([&] {
+    if (!msg) return PSF_ERR_ARG;
+    msg->m.task.value_type.push_back(value_type);
+    msg->m.value.push_back(wrap(ptr, bytes, loc));
+    return PSF_OK;
+  });
+}
+int psf_msg_key(const psf_message* msg, void** ptr, size_t* bytes, int* loc) {
+  if (!msg) return PSF_ERR_ARG;
+  if (ptr) *ptr = msg->m.key.ptr;
+  if (bytes) *bytes = msg->m.key.bytes;
+  if (loc) *loc = (int)msg->m.key.loc;
+  return PSF_OK;
+}
+int psf_msg_key_info(const psf_message* msg, int* has_key_flag, int* key_type) {
+  if (!msg) return PSF_ERR_ARG;
+  if (has_key_flag) *has_key_flag = msg->m.task.has_key ? 1 : 0;
+  if (key_type) *key_type = msg->m.task.key_type;
+  return PSF_OK;
+}
+int psf_msg_num_values(const psf_message* msg) { return msg ? (int)msg->m.value.size() : PSF_ERR_ARG; }
+int psf_msg_value(const psf_message* msg, int i, void** ptr, size_t* bytes, int* loc) {
+  if (!msg || i < 0 || i >= (int)msg->m.value.size()) return PSF_ERR_ARG;
+  const auto& b = msg->m.value[i];
+  if (ptr) *ptr = b.ptr;
+  if (bytes) *bytes = b.bytes;
+  if (loc) *loc = (int)b.loc;
+  return PSF_OK;
+}
+
+int psf_msg_add_filter(psf_message* msg, int type) {
+  return guarded([&] {
+    if (!msg) return PSF_ERR_ARG;
+    if (type < 1 || type > 4) return PSF_ERR_ARG;
+    msg->m.task.filter.emplace_back();
+    msg->m.task.filter.back().type = (psf::FilterConfig::Type)type;
+    return (int)msg->m.task.filter.size() - 1;
+  });
+}
+int psf_fc_set_num_bytes(psf_message* msg, int idx, int nb) {
+  return guarded([&] { fc_at(msg, idx)->num_bytes = nb; return PSF_OK; });
+}
+int psf_fc_set_clear_cache(psf_message* msg, int idx, int v) {
+  return guarded([&] { fc_at(msg, idx)->clear_cache_if_done = v != 0; return PSF_OK; });
+}
+int psf_fc_set_noise(psf_message* msg, int idx, float mean, float sd) {
+  return guarded([&] {
+    auto* f = fc_at(msg, idx);
+    f->mean = mean;
+    f->std = sd;
+    return PSF_OK;
+  });
+}
+int psf_fc_add_fixed_point(psf_message* msg, int idx, const psf_fixed_point* fp) {
+  return guarded([&] {
+    auto* f = fc_at(msg, idx);
+    f->fixed_point.emplace_back();
+    auto& x = f->fixed_point.back();
+    if (fp && fp->has_min) x.set_min(fp->min_value);
+    if (fp && fp->has_max) x.set_max(fp->max_value);
+    return PSF_OK;
+  });
+}
+int psf_fc_num_fixed_point(const psf_message* msg, int idx) {
+  return guarded([&] { return (int)fc_at(msg, idx)->fixed_point.size(); });
+}
+int psf_fc_fixed_point(const psf_message* msg, int idx, int k, psf_fixed_point* fp) {
+  return guarded([&] {
+    const auto* f = fc_at(msg, idx);
+    if (!fp || k < 0 || k >= (int)f->fixed_point.size()) return PSF_ERR_ARG;
+    const auto& x = f->fixed_point[k];
+    fp->has_min = x.has_min;
+    fp->has_max = x.has_max;
+    fp->min_value = x.min_value;
+    fp->max_value = x.max_value;
+    return PSF_OK;
+  });
+}
+int psf_fc_signature(const psf_message* msg, int idx, int* has_signature, uint32_t* sig) {
+  return guarded([&] {
+    const auto* f = fc_at(msg, idx);
+    if (has_signature) *has_signature = f->has_signature ? 1 : 0;
+    if (sig) *sig = f->signature;
+    return PSF_OK;
+  });
+}
+int psf_fc_num_uncompressed(const psf_message* msg, int idx) {
+  return guarded([&] { return (int)fc_at(msg, idx)->uncompressed_size.size(); });
+}
+int psf_node_roundtrip(psf_node* snd, psf_node* rcv, const psf_message* tmpl, int iters,
+                       psf_message** out) {
+  return guarded([&] {
+    if (!snd || !rcv || !tmpl || iters < 0) return PSF_ERR_ARG;
+    psf_message* last = nullptr;
+    for (int i = 0; i < iters; ++i) {
+      psf::Message m = tmpl->m;       // fresh Task + zero-copy buffers
+      snd->impl->EncodeMessage(&m);
+      psf::Message w = m;             // delivered copy (van: Task frame + data frames)
+      rcv->impl->DecodeMessage(&w);
+      if (out && i == iters - 1) last = new psf_message{w};
+    }
+    if (out) *out = last;
+    return PSF_OK;
+  });
+}
+
+int psf_profile_enable(psf_context* ctx, int enable) {
+  if (!ctx) return PSF_ERR_ARG;
+  ctx->impl->prof()->enable(enable != 0);
+  return PSF_OK;
+}
+int psf_profile_reset(psf_context* ctx) {
+  if (!ctx) return PSF_ERR_ARG;
+  ctx->impl->prof()->reset();
+  return PSF_OK;
+}
+int psf_profile_read(psf_context* ctx, int k, int64_t* launches, double* total_ms,
+                     double* alg_bytes) {
+  if (!ctx || k < 0 || k >= psf::kKNum) return PSF_ERR_ARG;
+  psf::Profiler* p = ctx->impl->prof();
+  p->collect();
+  if (launches) *launches = p->launches[k];
+  if (total_ms) *total_ms = p->total_ms[k];
+  if (alg_bytes) *alg_bytes = p->bytes[k];
+  return PSF_OK;
+}
+const char* psf_profile_kernel_name(int k) {
+  static const char* names[] = {"ff_minmax_partials", "ff_encode", "ff_decode", "crc32c_chunks",
+                                "noise_add", "snappy_compress", "snappy_decompress"};
+  return (k >= 0 && k < psf::kKNum) ? names[k] : "?";
+}
+
+int psf_fc_uncompressed(const psf_message* msg, int idx, int i, uint64_t* size) {
+  return guarded([&] {
+    const auto* f = fc_at(msg, idx);
+    if (!size || i < 0 || i >= (int)f->uncompressed_size.size()) return PSF_ERR_ARG;
+    *size = f->uncompressed_size[i];
+    return PSF_OK;
+  });
+}
+
+}  // extern "C"

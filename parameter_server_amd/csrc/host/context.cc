@@ -1,0 +1,117 @@
+#include "context.h"
+
+#include <string.h>
+#include <time.h>
+
+#include <atomic>
+
+namespace psf {
+
+struct Context::StreamHolder {
+  int device;
+  hipStream_t stream;
+  bool own;
+  ~StreamHolder() {
+    if (own) {
+      (void)hipSetDevice(device);
+      (void)hipStreamSynchronize(stream);
+      (void)hipStreamDestroy(stream);
+    }
+  }
+};
+
+Context::Context(int device, hipStream_t stream) : device_(device), stream_(nullptr) {
+  if (device < 0) return;  // host-only context: host-resident buffers, no HIP calls
+  PSF_HIP_CHECK(hipSetDevice(device));
+  bool own = stream == nullptr;
+  if (own) PSF_HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+  stream_ = stream;
+  holder_ = std::make_shared<StreamHolder>(StreamHolder{device, stream, own});
+  // keep freed HBM in the default pool for reuse (no release at sync points)
+  hipMemPool_t pool;
+  if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
+    uint64_t thr = ~0ull;
+    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+  }
+  PSF_HIP_CHECK(hipMalloc(&d_partials_, 2 * sizeof(uint64_t) * kMaxGrid));
+  PSF_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&d_slots_), sizeof(Slot) * kSlots));
+  PSF_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_slots_), sizeof(Slot) * kSlots,
+                              hipHostMallocDefault));
+}
+
+Context::~Context() {
+  if (device_ < 0) return;
+  (void)hipSetDevice(device_);
+  (void)hipStreamSynchronize(stream_);
+  (void)hipFree(d_partials_);
+  (void)hipFree(d_slots_);
+  (void)hipHostFree(h_slots_);
+}
+
+Buffer Context::alloc(size_t bytes) {
+  Buffer b;
+  b.bytes = bytes;
+  b.loc = Loc::kDevice;
+  if (bytes == 0) return b;
+  if (device_ < 0) throw CheckError(kErrArg, "host-only context cannot hold HBM buffers");
+  void* p = nullptr;
+  PSF_HIP_CHECK(hipMallocAsync(&p, bytes, stream_));
+  auto holder = holder_;
+  b.owner = std::shared_ptr<void>(p, [holder](void* q) {
+    (void)hipSetDevice(holder->device);
+    (void)hipFreeAsync(q, holder->stream);
+  });
+  b.ptr = static_cast<uint8_t*>(p);
+  return b;
+}
+
+void Context::fetch_slots(int n) {
+  if (device_ < 0) throw CheckError(kErrArg, "host-only context has no device workspace");
+  if (n <= 0) { sync(); return; }
+  PSF_HIP_CHECK(hipMemcpyAsync(h_slots_, d_slots_, sizeof(Slot) * n, hipMemcpyDeviceToHost, stream_));
+  sync();
+}
+
+void Context::sync() {
+  if (device_ >= 0) PSF_HIP_CHECK(hipStreamSynchronize(stream_));
+}
+
+Buffer Context::to_device(const Buffer& b) {
+  if (b.loc == Loc::kDevice || b.empty()) return b;
+  Buffer d = alloc(b.bytes);
+  PSF_HIP_CHECK(hipMemcpyAsync(d.ptr, b.ptr, b.bytes, hipMemcpyHostToDevice, stream_));
+  return d;
+}
+
+// ------------------------------------------------------------ clock ------
+static std::atomic<bool> g_clock_override{false};
+static std::atomic<int64_t> g_clock_value{0};
+
+void set_clock_override(bool enable, int64_t t) {
+  g_clock_value.store(t);
+  g_clock_override.store(enable);
+}
+
+int32_t ff_clock_seed() {
+  if (g_clock_override.load()) return (int32_t)g_clock_value.load();
+  return (int32_t)time(nullptr);  // `int seed = time(NULL);`
+}
+
+// ------------------------------------------------------------ crc32c -----
+uint32_t crc32c_host(const void* p, size_t n) {
+  static uint32_t table[256];
+  static std::once_flag once;
+  std::call_once(once, [] {
+    for (uint32_t i = 0; i < 256; ++i) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
+      table[i] = c;
+    }
+  });
+  const uint8_t* b = static_cast<const uint8_t*>(p);
+  uint32_t l = 0xFFFFFFFFu;
+  for (size_t i = 0; i < n; ++i) l = table[(l ^ b[i]) & 0xFF] ^ (l >> 8);
+  return l ^ 0xFFFFFFFFu;
+}
+
+}  // namespace psf

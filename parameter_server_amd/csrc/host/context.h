@@ -1,0 +1,80 @@
+// Per-(device, stream) execution context of libpsf: the HIP stream the codec
+// kernels are ordered on, stream-ordered HBM allocation for codec outputs, a
+// small device workspace (min/max partials, per-array side-info slots) and a
+// pinned host mirror of the slots so side-info reaches the FilterConfig with one
+// D2H copy + one stream sync per message.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <memory>
+#include <mutex>
+#include <string>
+
+#include "../psf_internal.h"
+#include "message.h"
+
+namespace psf {
+
+#define PSF_HIP_CHECK(expr)                                                         \
+  do {                                                                              \
+    hipError_t _e = (expr);                                                         \
+    if (_e != hipSuccess)                                                           \
+      throw ::psf::CheckError(::psf::kErrHip, std::string(#expr) + ": " +            \
+                                                  hipGetErrorString(_e));           \
+  } while (0)
+
+// Side-info slot written by the device, mirrored to pinned host memory.
+struct Slot {
+  float range[2];
+  int32_t status;
+  uint32_t crc;
+};
+
+class Context {
+ public:
+  static constexpr int kSlots = 256;
+
+  // stream == nullptr -> a private non-blocking stream owned by the context.
+  // device < 0 -> host-only context (host-resident buffers; no HIP calls).
+  Context(int device, hipStream_t stream);
+  ~Context();
+
+  int device() const { return device_; }
+  hipStream_t stream() const { return stream_; }
+
+  // HBM buffer freed (stream-ordered) when its last reference drops.
+  Buffer alloc(size_t bytes);
+
+  void* partials() const { return d_partials_; }
+  Slot* d_slots() const { return d_slots_; }
+  Slot* h_slots() const { return h_slots_; }
+  // copy slots [0, n) device->pinned host and wait for the stream
+  void fetch_slots(int n);
+  void sync();
+  // stage a host buffer into HBM (used at the host edge)
+  Buffer to_device(const Buffer& b);
+
+  std::mutex& mu() { return mu_; }
+  Profiler* prof() { return &prof_; }
+
+ private:
+  Profiler prof_;
+  struct StreamHolder;
+  int device_;
+  hipStream_t stream_;
+  std::shared_ptr<StreamHolder> holder_;
+  void* d_partials_ = nullptr;
+  Slot* d_slots_ = nullptr;
+  Slot* h_slots_ = nullptr;
+  std::mutex mu_;
+};
+
+// time(NULL) as the reference's FIXING_FLOAT seed source (fixing_float.h:78),
+// with an override hook so parity tests can pin it (psf_set_clock).
+int32_t ff_clock_seed();
+void set_clock_override(bool enable, int64_t t);
+
+// CRC32C on the host (for KEY_CACHING on host-resident keys).
+uint32_t crc32c_host(const void* p, size_t n);
+
+}  // namespace psf

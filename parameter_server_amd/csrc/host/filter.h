@@ -1,0 +1,112 @@
+// The reference's filter plugin surface (src/filter/filter.h:9-24), restated for
+// HBM-resident messages.  Filter::create is the registration point
+// (filter.cc:9-23); each codec is a Filter subclass whose encode/decode launch
+// libpsf's HIP kernels on the owning node's Context stream.
+#pragma once
+#include <map>
+#include <mutex>
+#include <unordered_map>
+#include <utility>
+
+#include "context.h"
+#include "message.h"
+
+namespace psf {
+
+class Filter {
+ public:
+  explicit Filter(Context* ctx) : ctx_(ctx) {}
+  virtual ~Filter() {}
+
+  // filter.cc:9-23; unknown types are fatal there (CHECK), an error here.
+  static Filter* create(const FilterConfig& conf, Context* ctx);
+
+  virtual void encode(Message* msg) {}
+  virtual void decode(Message* msg) {}
+
+  // filter.cc:26-31: the first config of that type, or null.
+  static FilterConfig* find(FilterConfig::Type type, Message* msg) { return find(type, &msg->task); }
+  static FilterConfig* find(FilterConfig::Type type, Task* task);
+
+ protected:
+  Context* ctx_;
+};
+
+// KEY_CACHING, key_caching.h:6-76
+class KeyCachingFilter : public Filter {
+ public:
+  using Filter::Filter;
+  void encode(Message* msg) override;
+  void decode(Message* msg) override;
+  size_t cache_size() const { return cache_.size(); }
+
+ private:
+  struct CacheKey {
+    int32_t channel;
+    KeyRange range;
+    bool operator==(const CacheKey& o) const { return channel == o.channel && range == o.range; }
+  };
+  struct CacheKeyHash {
+    size_t operator()(const CacheKey& k) const {
+      uint64_t h = (uint64_t)(uint32_t)k.channel * 0x9E3779B97F4A7C15ull;
+      h ^= k.range.begin + 0x7F4A7C159E3779B9ull + (h << 6) + (h >> 2);
+      h ^= k.range.end + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+      return (size_t)h;
+    }
+  };
+  struct Entry {
+    uint32_t sig = 0;
+    Buffer key;  // zero-copy reference, as the reference caches the SArray
+  };
+  static bool is_done(const Task& t) { return !t.request || (t.has_param && t.push); }  // :63-67
+  uint32_t signature(const Buffer& key);
+
+  std::unordered_map<CacheKey, Entry, CacheKeyHash> cache_;
+  static constexpr size_t kMaxSigLen = 2048;  // key_caching.h:74
+  std::mutex mu_;
+};
+
+// FIXING_FLOAT, fixing_float.h:6-103
+class FixingFloatFilter : public Filter {
+ public:
+  using Filter::Filter;
+  void encode(Message* msg) override { convert(msg, true); }
+  void decode(Message* msg) override { convert(msg, false); }
+
+ private:
+  void convert(Message* msg, bool encode);
+};
+
+// COMPRESSING, compressing.h:6-38 (snappy raw format)
+class CompressingFilter : public Filter {
+ public:
+  using Filter::Filter;
+  void encode(Message* msg) override;
+  void decode(Message* msg) override;
+};
+
+// NOISE, add_noise.h:9-41
+class AddNoiseFilter : public Filter {
+ public:
+  using Filter::Filter;
+  void encode(Message* msg) override;
+};
+
+// RemoteNode's chain driver (remote_node.cc:7-29, remote_node.h:35-65): one
+// filter instance per filter type per peer, created from the first config
+// seen; encode in task.filter order, decode in reverse.
+class RemoteNode {
+ public:
+  explicit RemoteNode(Context* ctx) : ctx_(ctx) {}
+  ~RemoteNode() { for (auto& f : filters_) delete f.second; }
+  void EncodeMessage(Message* msg);
+  void DecodeMessage(Message* msg);
+  Filter* FindFilterOrCreate(const FilterConfig& conf);
+  Context* ctx() const { return ctx_; }
+
+ private:
+  Context* ctx_;
+  std::unordered_map<int, Filter*> filters_;
+};
+
+}  // namespace psf

@@ -1,0 +1,202 @@
+// Codec filters of libpsf (host side).  Each method cites the reference lines
+// whose behaviour it keeps; the element work runs in the HIP kernels of
+// ff_codec.hip / crc32c.hip / snappy.hip / noise.hip.
+#include <math.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "filter.h"
+
+namespace psf {
+
+// ------------------------------------------------------------- factory ----
+Filter* Filter::create(const FilterConfig& conf, Context* ctx) {
+  switch (conf.type) {  // filter.cc:9-23
+    case FilterConfig::KEY_CACHING: return new KeyCachingFilter(ctx);
+    case FilterConfig::COMPRESSING: return new CompressingFilter(ctx);
+    case FilterConfig::FIXING_FLOAT: return new FixingFloatFilter(ctx);
+    case FilterConfig::NOISE: return new AddNoiseFilter(ctx);
+    default: throw CheckError(kErrArg, "unknow filter type");
+  }
+}
+
+FilterConfig* Filter::find(FilterConfig::Type type, Task* task) {  // filter.cc:26-31
+  for (auto& f : task->filter)
+    if (f.type == type) return &f;
+  return nullptr;
+}
+
+// --------------------------------------------------------- KEY_CACHING ----
+uint32_t KeyCachingFilter::signature(const Buffer& key) {
+  const size_t len = std::min(key.bytes, kMaxSigLen);  // key_caching.h:18
+  if (key.loc == Loc::kHost) return crc32c_host(key.ptr, len);
+  Slot* d = ctx_->d_slots();
+  int st = crc32c_launch(key.ptr, len, &d[0].crc, ctx_->stream(), ctx_->prof());
+  if (st != kOk) throw CheckError(st, "crc32c launch failed");
+  ctx_->fetch_slots(1);
+  return ctx_->h_slots()[0].crc;
+}
+
+void KeyCachingFilter::encode(Message* msg) {  // key_caching.h:9-34
+  FilterConfig* conf = find(FilterConfig::KEY_CACHING, msg);
+  if (!conf) return;
+  if (!msg->has_key()) {
+    conf->has_signature = false;
+    conf->signature = 0;
+    return;
+  }
+  const uint32_t sig = signature(msg->key);
+  conf->has_signature = true;
+  conf->signature = sig;
+  CacheKey ck{msg->task.key_channel, msg->task.key_range};
+  std::lock_guard<std::mutex> l(mu_);
+  Entry& e = cache_[ck];
+  const bool hit = e.sig == sig && e.key.bytes == msg->key.bytes;
+  if (hit) {
+    msg->clear_key();
+  } else {
+    e.sig = sig;
+    e.key = msg->key;
+  }
+  if (conf->clear_cache_if_done && is_done(msg->task)) cache_.erase(ck);
+}
+
+void KeyCachingFilter::decode(Message* msg) {  // key_caching.h:36-60
+  FilterConfig* conf = find(FilterConfig::KEY_CACHING, msg);
+  if (!conf || !conf->has_signature) return;
+  const uint32_t sig = conf->signature;
+  if (msg->has_key()) {
+    const uint32_t got = signature(msg->key);
+    if (got != sig) throw CheckError(kErrCheck, "KEY_CACHING: key signature mismatch");
+  }
+  CacheKey ck{msg->task.key_channel, msg->task.key_range};
+  std::lock_guard<std::mutex> l(mu_);
+  Entry& e = cache_[ck];
+  if (msg->has_key()) {
+    e.sig = sig;
+    e.key = msg->key;
+  } else {
+    // "the cache is invalid... may ask the sender to resend this task"
+    if (sig != e.sig) throw CheckError(kErrCheck, "KEY_CACHING: cache miss on decode");
+    msg->set_key(e.key);
+  }
+  if (conf->clear_cache_if_done && is_done(msg->task)) cache_.erase(ck);
+}
+
+// -------------------------------------------------------- FIXING_FLOAT ----
+void FixingFloatFilter::convert(Message* msg, bool encode) {  // fixing_float.h:24-47
+  FilterConfig* conf = find(FilterConfig::FIXING_FLOAT, msg);
+  if (!conf) throw CheckError(kErrCheck, "CHECK_NOTNULL(find(FIXING_FLOAT))");
+  if (conf->num_bytes == 0) return;
+  const int n = (int)msg->value.size();
+  if (n != (int)msg->task.value_type.size())
+    throw CheckError(kErrCheck, "CHECK_EQ(value.size(), value_type_size())");
+
+  struct Job { int i; int type; FixedFloatConfig* fp; Buffer in, out; size_t elems; };
+  std::vector<Job> jobs;
+  int k = 0;
+  for (int i = 0; i < n; ++i) {
+    if (msg->value[i].empty()) continue;
+    const int type = msg->task.value_type[i];
+    if ((int)conf->fixed_point.size() <= k) conf->fixed_point.emplace_back();
+    if (type == kFloat || type == kDouble) jobs.push_back(Job{i, type, &conf->fixed_point[k++], {}, {}, 0});
+  }
+  if (jobs.empty()) return;
+  const int nb = conf->num_bytes;
+  if (nb <= 0 || nb >= 8) throw CheckError(kErrNbytes, "CHECK_GT(nbytes,0) / CHECK_LT(nbytes,8)");
+  const double ratio = ff_ratio(nb);
+  (void)ratio;
+  hipStream_t st = ctx_->stream();
+
+  if (!encode) {  // fixing_float.h:89-101
+    for (auto& j : jobs) {
+      const FixedFloatConfig& fp = *j.fp;
+      if (!fp.has_min) throw CheckError(kErrCheck, "CHECK(conf->has_min_value())");
+      if (!fp.has_max) throw CheckError(kErrCheck, "CHECK(conf->has_max_value())");
+      const double bin = (double)fp.max_value - (double)fp.min_value;
+      if (!(bin > 0)) throw CheckError(kErrBin, "CHECK_GT(bin, 0)");
+      const size_t vsz = j.type == kFloat ? 4 : 8;
+      Buffer code = ctx_->to_device(msg->value[j.i]);
+      const size_t elems = code.bytes / (size_t)nb;
+      Buffer out = ctx_->alloc(elems * vsz);
+      int s = ff_decode_launch(code.ptr, elems, j.type, nb, nullptr, fp.min_value, fp.max_value, out.ptr, st,
+                               ctx_->prof());
+      if (s != kOk) throw CheckError(s, "ff_decode launch failed");
+      msg->value[j.i] = out;
+    }
+    return;
+  }
+
+  // encode, fixing_float.h:50-88; side-info comes back through the slots
+  for (size_t base = 0; base < jobs.size(); base += Context::kSlots) {
+    const size_t end = std::min(jobs.size(), base + (size_t)Context::kSlots);
+    bool need_fetch = false;
+    for (size_t q = base; q < end; ++q) {
+      Job& j = jobs[q];
+      const size_t vsz = j.type == kFloat ? 4 : 8;
+      j.in = ctx_->to_device(msg->value[j.i]);
+      j.elems = j.in.bytes / vsz;
+      if (j.elems == 0) throw CheckError(kErrArg, "value array shorter than one element");
+      FixedPoint preset{j.fp->has_min, j.fp->has_max, j.fp->min_value, j.fp->max_value};
+      if (preset.has_min && preset.has_max) {
+        if (!((double)preset.max_value - (double)preset.min_value > 0))
+          throw CheckError(kErrBin, "CHECK_GT(bin, 0)");
+      } else {
+        need_fetch = true;
+      }
+      j.out = ctx_->alloc(j.elems * (size_t)nb);
+      Slot* slot = ctx_->d_slots() + (q - base);
+      const uint32_t seed = (uint32_t)ff_clock_seed();  // `int seed = time(NULL)`, per array
+      int s = ff_encode_launch(j.in.ptr, j.elems, j.type, nb, preset, seed, j.out.ptr,
+                               ctx_->partials(), slot->range, &slot->status, st, ctx_->prof());
+      if (s != kOk) throw CheckError(s, "ff_encode launch failed");
+    }
+    if (need_fetch) ctx_->fetch_slots((int)(end - base));
+    for (size_t q = base; q < end; ++q) {
+      Job& j = jobs[q];
+      if (need_fetch) {
+        const Slot& hs = ctx_->h_slots()[q - base];
+        if (!j.fp->has_min) j.fp->set_min(hs.range[0]);
+        if (!j.fp->has_max) j.fp->set_max(hs.range[1]);
+        if (hs.status != kOk) throw CheckError(kErrBin, "CHECK_GT(bin, 0)");
+      }
+      msg->value[j.i] = j.out;
+    }
+  }
+}
+
+// --------------------------------------------------------- COMPRESSING ----
+void CompressingFilter::encode(Message* msg) {
+  if (!find(FilterConfig::COMPRESSING, msg)) return;
+  throw CheckError(kErrUnsupported, "COMPRESSING: not built yet");
+}
+void CompressingFilter::decode(Message* msg) {
+  if (!find(FilterConfig::COMPRESSING, msg)) return;
+  throw CheckError(kErrUnsupported, "COMPRESSING: not built yet");
+}
+
+// --------------------------------------------------------------- NOISE ----
+void AddNoiseFilter::encode(Message* msg) {
+  if (!find(FilterConfig::NOISE, msg)) throw CheckError(kErrCheck, "CHECK_NOTNULL(find(NOISE))");
+  throw CheckError(kErrUnsupported, "NOISE: not built yet");
+}
+
+// ---------------------------------------------------------- RemoteNode ----
+Filter* RemoteNode::FindFilterOrCreate(const FilterConfig& conf) {  // remote_node.cc:7-15
+  auto it = filters_.find(conf.type);
+  if (it == filters_.end()) it = filters_.emplace(conf.type, Filter::create(conf, ctx_)).first;
+  return it->second;
+}
+
+void RemoteNode::EncodeMessage(Message* msg) {  // remote_node.cc:17-22
+  for (size_t i = 0; i < msg->task.filter.size(); ++i)
+    FindFilterOrCreate(msg->task.filter[i])->encode(msg);
+}
+
+void RemoteNode::DecodeMessage(Message* msg) {  // remote_node.cc:23-29, reverse order
+  for (int i = (int)msg->task.filter.size() - 1; i >= 0; --i)
+    FindFilterOrCreate(msg->task.filter[i])->decode(msg);
+}
+
+}  // namespace psf

@@ -1,0 +1,99 @@
+// Host-side message model of libpsf: the fields of the reference's Message /
+// Task / FilterConfig that the codec chain reads and writes, with buffers that
+// live in HBM (or host memory at the host edge).
+//
+//   Message     <- reference src/system/message.h:10-76 (key, value, has_key,
+//                  clear_key, set_key<char> semantics incl. key_type=CHAR and the
+//                  default key_range = Range::All())
+//   Task        <- src/system/proto/task.proto:10-57 (request, key_range,
+//                  key_channel, has_key, key_type, value_type, filter, param.push)
+//   FilterConfig<- src/filter/proto/filter.proto:3-35 (field defaults and has-bits)
+//   Buffer      <- SArray<char> (util/shared_array.h:29): a shared, zero-copy byte
+//                  view; the owner keeps the storage alive (custom deleter, as the
+//                  van's zero-copy frames do, van.cc:244-249).
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include <deque>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace psf {
+
+enum class Loc : int { kHost = 0, kDevice = 1 };
+
+struct Buffer {
+  std::shared_ptr<void> owner;  // null => caller-owned memory (caller keeps it alive)
+  uint8_t* ptr = nullptr;
+  size_t bytes = 0;
+  Loc loc = Loc::kDevice;
+  bool empty() const { return bytes == 0; }
+  void clear() { owner.reset(); ptr = nullptr; bytes = 0; }
+};
+
+// glog CHECK failures of the reference map to this exception; the C ABI turns
+// it into a status code (include/psf.h).
+struct CheckError : std::runtime_error {
+  int code;
+  CheckError(int c, const std::string& what) : std::runtime_error(what), code(c) {}
+};
+
+struct KeyRange {
+  uint64_t begin = 0, end = 0;
+  bool operator==(const KeyRange& o) const { return begin == o.begin && end == o.end; }
+  static KeyRange All() { return KeyRange{0, ~0ull}; }  // range.h:92-95
+};
+
+struct FixedFloatConfig {  // filter.proto:22-25
+  bool has_min = false, has_max = false;
+  float min_value = -1.f, max_value = 1.f;
+  void set_min(float v) { min_value = v; has_min = true; }
+  void set_max(float v) { max_value = v; has_max = true; }
+};
+
+struct FilterConfig {  // filter.proto:3-35
+  enum Type { KEY_CACHING = 1, COMPRESSING = 2, FIXING_FLOAT = 3, NOISE = 4 };
+  Type type = KEY_CACHING;
+  bool clear_cache_if_done = false;            // field 20
+  int32_t num_bytes = 3;                       // field 5, default 3
+  std::deque<FixedFloatConfig> fixed_point;    // field 4 (stable addresses)
+  float mean = 0.f, std = 0.f;                 // fields 6, 7
+  bool has_signature = false;                  // field 2
+  uint32_t signature = 0;
+  std::vector<uint64_t> uncompressed_size;     // field 3
+};
+
+struct Task {
+  bool request = false;
+  int32_t key_channel = 0;
+  bool has_key_range = false;
+  KeyRange key_range;
+  bool has_key = false;
+  int key_type = 0;
+  std::vector<int> value_type;
+  std::deque<FilterConfig> filter;
+  bool has_param = false;
+  bool push = false;  // param.push
+};
+
+struct Message {
+  Task task;
+  Buffer key;
+  std::vector<Buffer> value;
+
+  bool has_key() const { return !key.empty(); }
+  void clear_key() { task.has_key = false; key.clear(); }
+  // message.h:70-76 (set_key<char>)
+  void set_key(const Buffer& k) {
+    task.key_type = 11;  // CHAR
+    if (has_key()) clear_key();
+    task.has_key = true;
+    key = k;
+    if (!task.has_key_range) { task.has_key_range = true; task.key_range = KeyRange::All(); }
+  }
+};
+
+}  // namespace psf

@@ -1,0 +1,68 @@
+// Launch profiler: a start/stop hipEvent pair recorded on the launch stream
+// around each kernel (the bench's live per-kernel durations, cross-checked
+// against rocprofv3 --kernel-trace in profiles/).
+#include <stdlib.h>
+
+#include "../psf_internal.h"
+
+namespace psf {
+
+Profiler::~Profiler() {
+  for (int i = 0; i < npend_; ++i) {
+    (void)hipEventDestroy(pend_[i].a);
+    (void)hipEventDestroy(pend_[i].b);
+  }
+  for (int i = 0; i < npool_; ++i) (void)hipEventDestroy(pool_[i]);
+  free(pend_);
+  free(pool_);
+}
+
+hipEvent_t Profiler::take() {
+  if (npool_ > 0) return pool_[--npool_];
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+void Profiler::begin(hipStream_t st) {
+  cur_ = take();
+  (void)hipEventRecord(cur_, st);
+}
+
+void Profiler::end(KernelId id, hipStream_t st, double alg_bytes) {
+  hipEvent_t b = take();
+  (void)hipEventRecord(b, st);
+  if (npend_ == cap_) {
+    cap_ = cap_ ? 2 * cap_ : 64;
+    pend_ = static_cast<Pending*>(realloc(pend_, sizeof(Pending) * cap_));
+  }
+  pend_[npend_++] = Pending{id, cur_, b, alg_bytes};
+  cur_ = nullptr;
+  if (npend_ >= 4096) collect();
+}
+
+void Profiler::collect() {
+  for (int i = 0; i < npend_; ++i) {
+    Pending& p = pend_[i];
+    float ms = 0.f;
+    (void)hipEventSynchronize(p.b);
+    (void)hipEventElapsedTime(&ms, p.a, p.b);
+    launches[p.id] += 1;
+    total_ms[p.id] += ms;
+    bytes[p.id] += p.bytes;
+    if (npool_ + 2 > cappool_) {
+      cappool_ = cappool_ ? 2 * cappool_ : 128;
+      pool_ = static_cast<hipEvent_t*>(realloc(pool_, sizeof(hipEvent_t) * cappool_));
+    }
+    pool_[npool_++] = p.a;
+    pool_[npool_++] = p.b;
+  }
+  npend_ = 0;
+}
+
+void Profiler::reset() {
+  collect();
+  for (int k = 0; k < kKNum; ++k) { launches[k] = 0; total_ms[k] = 0; bytes[k] = 0; }
+}
+
+}  // namespace psf

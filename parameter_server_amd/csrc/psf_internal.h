@@ -1,0 +1,91 @@
+// Internal declarations shared by the HIP kernels and the C++ host layer of
+// libpsf.  The public C ABI is include/psf.h.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace psf {
+
+constexpr int kBlock = 256;     // 4 waves of 64
+constexpr int kMaxGrid = 2048;  // 256 CUs x 8 workgroups; streaming kernels grid-stride
+
+// status codes (mirrored by PSF_* in include/psf.h)
+constexpr int kOk = 0;
+constexpr int kErrArg = -1;
+constexpr int kErrNbytes = -2;
+constexpr int kErrBin = -3;
+constexpr int kErrHip = -4;
+constexpr int kErrCheck = -5;
+constexpr int kErrUnsupported = -6;
+
+// task.proto DataType values used by the codecs
+constexpr int kFloat = 9;
+constexpr int kDouble = 10;
+constexpr int kChar = 11;
+
+// boolrand LCG, fixing_float.h:18-21
+constexpr uint32_t kLcgA = 214013u;
+constexpr uint32_t kLcgC = 2531011u;
+
+struct FixedPoint {
+  int has_min, has_max;
+  float min_value, max_value;
+};
+
+// Kernel launch profiler: HIP events recorded on the launch stream around
+// each kernel, plus the kernel's algorithmic HBM bytes.
+enum KernelId { kKMinmax = 0, kKEncode, kKDecode, kKCrc, kKNoise, kKSnappyCompress,
+                kKSnappyDecompress, kKNum };
+class Profiler {
+ public:
+  ~Profiler();
+  bool on() const { return on_; }
+  void enable(bool on) { on_ = on; }
+  void begin(hipStream_t st);
+  void end(KernelId id, hipStream_t st, double alg_bytes);
+  void collect();  // waits for pending events, accumulates
+  void reset();
+  long launches[kKNum] = {0};
+  double total_ms[kKNum] = {0};
+  double bytes[kKNum] = {0};
+
+ private:
+  struct Pending { KernelId id; hipEvent_t a, b; double bytes; };
+  hipEvent_t take();
+  bool on_ = false;
+  hipEvent_t cur_ = nullptr;
+  Pending* pend_ = nullptr;
+  int npend_ = 0, cap_ = 0;
+  hipEvent_t* pool_ = nullptr;
+  int npool_ = 0, cappool_ = 0;
+};
+
+// RAII bracket around one kernel launch
+struct ProfScope {
+  Profiler* p; KernelId id; hipStream_t st; double bytes;
+  ProfScope(Profiler* p_, KernelId id_, hipStream_t st_, double bytes_)
+      : p(p_ && p_->on() ? p_ : nullptr), id(id_), st(st_), bytes(bytes_) {
+    if (p) p->begin(st);
+  }
+  ~ProfScope() { if (p) p->end(id, st, bytes); }
+};
+
+// ff_codec.hip
+double ff_ratio(int nb);
+int ff_grid(size_t work_items);
+int ff_encode_launch(const void* x, size_t n, int value_type, int nb, const FixedPoint& preset,
+                     uint32_t seed, void* out, void* partials, float* range_out, int* status_out,
+                     hipStream_t st, Profiler* prof = nullptr);
+int ff_decode_launch(const void* code, size_t n, int value_type, int nb, const float* range,
+                     float mn, float mx, void* out, hipStream_t st, Profiler* prof = nullptr);
+
+// crc32c.hip: CRC32C of d[0:n) written to *out (device).  n may be any size.
+int crc32c_launch(const void* d, size_t n, uint32_t* out, hipStream_t st,
+                  Profiler* prof = nullptr);
+
+// noise.hip
+int add_noise_launch(void* d, size_t n, int value_type, float mean, float sd, void* ws,
+                     size_t ws_bytes, hipStream_t st);
+
+}  // namespace psf

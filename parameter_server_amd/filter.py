@@ -1,0 +1,311 @@
+"""Python face of the filter plugin surface (thin ctypes wrappers over
+include/psf.h; all codec work runs in libpsf's HIP kernels).
+
+Mirrors the reference's objects so tests read like its own:
+
+* ``Context``     -- device + HIP stream (+ workspace) the kernels run on
+* ``RemoteNode``  -- RemoteNode::EncodeMessage / DecodeMessage (remote_node.cc:17-29)
+* ``Message``     -- Message/Task/FilterConfig fields (message.h:10-76,
+                     task.proto:28-39, filter.proto:3-35)
+
+Buffers are torch tensors on the context's device (or CPU tensors for the host
+edge).  Messages keep the tensors they reference alive; nodes keep alive every
+tensor a key cache may refer to.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import torch
+
+from ._lib import (DT_DOUBLE, DT_FLOAT, DT_UINT64, LOC_DEVICE, LOC_HOST, FixedPoint, PsfError,  # noqa: F401
+                   check, lib)
+
+_TORCH_DT = {DT_FLOAT: torch.float32, DT_DOUBLE: torch.float64}
+
+
+def dtype_code(t: torch.Tensor) -> int:
+    return {torch.float32: DT_FLOAT, torch.float64: DT_DOUBLE, torch.int64: DT_UINT64,
+            torch.uint8: 11}.get(t.dtype, 0)
+
+
+def set_clock(t: Optional[int]) -> None:
+    """Pin the FIXING_FLOAT seed source (time(NULL) in the reference)."""
+    lib().psf_set_clock(0 if t is None else 1, 0 if t is None else int(t))
+
+
+class Context:
+    def __init__(self, device: int = 0, stream: Optional[torch.cuda.Stream] = None):
+        self.device = device
+        self.stream = stream if stream is not None else torch.cuda.current_stream(device)
+        h = C.c_void_p()
+        check(lib().psf_context_create(device, C.c_void_p(self.stream.cuda_stream), C.byref(h)))
+        self.h = h
+
+    def sync(self):
+        check(lib().psf_context_sync(self.h))
+
+    # -- launch profiler -----------------------------------------------------
+    def profile(self, on: bool = True):
+        check(lib().psf_profile_enable(self.h, int(on)))
+
+    def profile_reset(self):
+        check(lib().psf_profile_reset(self.h))
+
+    def profile_read(self) -> dict:
+        """{kernel: (launches, total_ms, algorithmic_bytes)} for launched kernels."""
+        from ._lib import KERNELS
+        out = {}
+        for k, name in enumerate(KERNELS):
+            n, ms, b = C.c_int64(), C.c_double(), C.c_double()
+            check(lib().psf_profile_read(self.h, k, C.byref(n), C.byref(ms), C.byref(b)))
+            if n.value:
+                out[name] = (n.value, ms.value, b.value)
+        return out
+
+    def close(self):
+        if self.h:
+            lib().psf_context_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- layer 1 kernels -----------------------------------------------------
+    def ff_encode(self, x: torch.Tensor, nb: int, seed: int, mn=None, mx=None, out=None):
+        """FIXING_FLOAT encode; returns (codes uint8 tensor, min, max)."""
+        fp = FixedPoint(mn is not None, mx is not None, 0.0 if mn is None else mn,
+                        0.0 if mx is None else mx)
+        if out is None:
+            out = torch.empty(x.numel() * nb, dtype=torch.uint8, device=x.device)
+        check(lib().psf_ff_encode(self.h, C.c_void_p(x.data_ptr()), x.numel(), dtype_code(x), nb,
+                                  C.byref(fp), C.c_int32(seed), C.c_void_p(out.data_ptr())))
+        return out, fp.min_value, fp.max_value
+
+    def ff_encode_async(self, x, nb, seed, out, d_range, d_status=None, mn=None, mx=None):
+        fp = FixedPoint(mn is not None, mx is not None, 0.0 if mn is None else mn,
+                        0.0 if mx is None else mx)
+        check(lib().psf_ff_encode_async(self.h, C.c_void_p(x.data_ptr()), x.numel(), dtype_code(x), nb,
+                                        C.byref(fp), C.c_int32(seed), C.c_void_p(out.data_ptr()),
+                                        C.c_void_p(d_range.data_ptr()),
+                                        None if d_status is None else C.c_void_p(d_status.data_ptr())))
+
+    def ff_decode(self, code: torch.Tensor, nb: int, mn: float, mx: float, dtype=torch.float32, out=None):
+        n = code.numel() // nb
+        if out is None:
+            out = torch.empty(n, dtype=dtype, device=code.device)
+        check(lib().psf_ff_decode(self.h, C.c_void_p(code.data_ptr()), n, dtype_code(out), nb, mn, mx,
+                                  C.c_void_p(out.data_ptr())))
+        return out
+
+    def ff_decode_async(self, code, nb, d_range, out):
+        n = code.numel() // nb
+        check(lib().psf_ff_decode_async(self.h, C.c_void_p(code.data_ptr()), n, dtype_code(out), nb,
+                                        C.c_void_p(d_range.data_ptr()), C.c_void_p(out.data_ptr())))
+        return out
+
+    def crc32c(self, t: torch.Tensor, nbytes: Optional[int] = None) -> int:
+        v = C.c_uint32()
+        nb = t.numel() * t.element_size() if nbytes is None else nbytes
+        check(lib().psf_crc32c(self.h, C.c_void_p(t.data_ptr()), nb, C.byref(v)))
+        return v.value
+
+    def key_signature(self, t: torch.Tensor) -> int:
+        v = C.c_uint32()
+        check(lib().psf_key_signature(self.h, C.c_void_p(t.data_ptr()), t.numel() * t.element_size(),
+                                      C.byref(v)))
+        return v.value
+
+
+class HostContext(Context):
+    """Host-only context (device -1): host-resident buffers, no HIP calls.
+    KEY_CACHING on host keys runs here; codecs needing HBM report an error."""
+
+    def __init__(self):
+        self.device = -1
+        self.stream = None
+        h = C.c_void_p()
+        check(lib().psf_context_create(-1, None, C.byref(h)))
+        self.h = h
+
+
+class Message:
+    def __init__(self, request=True, push=False, has_param=True, key_channel=0, key_range=None,
+                 _handle=None, _refs=None):
+        if _handle is not None:
+            self.h = _handle
+            self._refs = list(_refs or [])
+            return
+        h = C.c_void_p()
+        kr = key_range
+        check(lib().psf_msg_create(int(request), int(has_param), int(push), int(key_channel),
+                                   int(kr is not None), 0 if kr is None else kr[0],
+                                   0 if kr is None else kr[1], C.byref(h)))
+        self.h = h
+        self._refs = []
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().psf_msg_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+    def clone(self) -> "Message":
+        """Receiver-side copy (Task + zero-copy buffers), as delivered by the wire."""
+        h = C.c_void_p()
+        check(lib().psf_msg_clone(self.h, C.byref(h)))
+        return Message(_handle=h, _refs=self._refs)
+
+    @staticmethod
+    def _loc(t: torch.Tensor) -> int:
+        return LOC_DEVICE if t.is_cuda else LOC_HOST
+
+    def set_key(self, keys: torch.Tensor, key_type: int = DT_UINT64):
+        keys = keys.contiguous()
+        self._refs.append(keys)
+        check(lib().psf_msg_set_key(self.h, C.c_void_p(keys.data_ptr()), keys.numel() * keys.element_size(),
+                                    key_type, self._loc(keys)))
+
+    def add_value(self, v: torch.Tensor, value_type: Optional[int] = None):
+        v = v.contiguous()
+        self._refs.append(v)
+        vt = dtype_code(v) if value_type is None else value_type
+        check(lib().psf_msg_add_value(self.h, C.c_void_p(v.data_ptr()), v.numel() * v.element_size(),
+                                      vt, self._loc(v)))
+
+    def add_filter(self, type_: int, num_bytes=None, clear_cache_if_done=None, fixed_point=None,
+                   noise=None) -> int:
+        idx = check(lib().psf_msg_add_filter(self.h, type_))
+        if num_bytes is not None:
+            check(lib().psf_fc_set_num_bytes(self.h, idx, num_bytes))
+        if clear_cache_if_done is not None:
+            check(lib().psf_fc_set_clear_cache(self.h, idx, int(clear_cache_if_done)))
+        if noise is not None:
+            check(lib().psf_fc_set_noise(self.h, idx, noise[0], noise[1]))
+        for fp in fixed_point or []:
+            mn, mx = fp
+            f = FixedPoint(mn is not None, mx is not None, 0.0 if mn is None else mn,
+                           0.0 if mx is None else mx)
+            check(lib().psf_fc_add_fixed_point(self.h, idx, C.byref(f)))
+        return idx
+
+    # -- inspection --------------------------------------------------------
+    def key_ptr(self):
+        p, n, loc = C.c_void_p(), C.c_size_t(), C.c_int()
+        check(lib().psf_msg_key(self.h, C.byref(p), C.byref(n), C.byref(loc)))
+        return p.value, n.value, loc.value
+
+    def key_info(self):
+        hk, kt = C.c_int(), C.c_int()
+        check(lib().psf_msg_key_info(self.h, C.byref(hk), C.byref(kt)))
+        return bool(hk.value), kt.value
+
+    def num_values(self) -> int:
+        return check(lib().psf_msg_num_values(self.h))
+
+    def value_ptr(self, i: int):
+        p, n, loc = C.c_void_p(), C.c_size_t(), C.c_int()
+        check(lib().psf_msg_value(self.h, i, C.byref(p), C.byref(n), C.byref(loc)))
+        return p.value, n.value, loc.value
+
+    def fixed_points(self, idx: int):
+        out = []
+        for k in range(check(lib().psf_fc_num_fixed_point(self.h, idx))):
+            f = FixedPoint()
+            check(lib().psf_fc_fixed_point(self.h, idx, k, C.byref(f)))
+            out.append((bool(f.has_min), f.min_value, bool(f.has_max), f.max_value))
+        return out
+
+    def signature(self, idx: int):
+        h, s = C.c_int(), C.c_uint32()
+        check(lib().psf_fc_signature(self.h, idx, C.byref(h), C.byref(s)))
+        return bool(h.value), s.value
+
+    def uncompressed_sizes(self, idx: int):
+        out = []
+        for i in range(check(lib().psf_fc_num_uncompressed(self.h, idx))):
+            v = C.c_uint64()
+            check(lib().psf_fc_uncompressed(self.h, idx, i, C.byref(v)))
+            out.append(v.value)
+        return out
+
+
+def copy_out(ptr: int, nbytes: int, loc: int, device) -> torch.Tensor:
+    """Copy a library-owned buffer into a fresh uint8 tensor (same device)."""
+    if nbytes == 0:
+        return torch.empty(0, dtype=torch.uint8, device=device if loc == LOC_DEVICE else "cpu")
+    if loc == LOC_HOST:
+        buf = (C.c_uint8 * nbytes).from_address(ptr)
+        return torch.frombuffer(bytearray(buf), dtype=torch.uint8)
+    out = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    _memcpy_d2d(out.data_ptr(), ptr, nbytes)
+    return out
+
+
+_hip = None
+
+
+def _memcpy_d2d(dst: int, src: int, n: int):
+    global _hip
+    if _hip is None:
+        _hip = C.CDLL("libamdhip64.so")
+        _hip.hipMemcpyAsync.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]
+        _hip.hipMemcpyAsync.restype = C.c_int
+    stream = torch.cuda.current_stream()
+    rc = _hip.hipMemcpyAsync(C.c_void_p(dst), C.c_void_p(src), n, 3, C.c_void_p(stream.cuda_stream))
+    if rc != 0:
+        raise RuntimeError(f"hipMemcpyAsync failed: {rc}")
+
+
+class RemoteNode:
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+        h = C.c_void_p()
+        check(lib().psf_node_create(ctx.h, C.byref(h)))
+        self.h = h
+        self._keepalive = {}
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().psf_node_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+    def _hold(self, msg: Message):
+        for t in msg._refs:
+            self._keepalive[id(t)] = t
+
+    def roundtrip(self, rcv: "RemoteNode", tmpl: Message, iters: int, keep_last: bool = False):
+        """Native loop: encode a copy of tmpl here, deliver, decode on rcv."""
+        self._hold(tmpl)
+        rcv._hold(tmpl)
+        out = C.c_void_p()
+        check(lib().psf_node_roundtrip(self.h, rcv.h, tmpl.h, iters, C.byref(out) if keep_last else None))
+        return Message(_handle=out, _refs=tmpl._refs) if keep_last else None
+
+    def encode(self, msg: Message) -> None:
+        self._hold(msg)
+        check(lib().psf_node_encode(self.h, msg.h))
+
+    def decode(self, msg: Message) -> None:
+        self._hold(msg)
+        check(lib().psf_node_decode(self.h, msg.h))
+
+    # convenience: copy results out
+    def key(self, msg: Message) -> torch.Tensor:
+        p, n, loc = msg.key_ptr()
+        self.ctx.sync()
+        return copy_out(p, n, loc, f"cuda:{self.ctx.device}")
+
+    def value(self, msg: Message, i: int) -> torch.Tensor:
+        p, n, loc = msg.value_ptr(i)
+        self.ctx.sync()
+        return copy_out(p, n, loc, f"cuda:{self.ctx.device}")

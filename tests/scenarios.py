@@ -1,0 +1,348 @@
+"""Message-sequence scenarios run identically against the reference harness
+(oracle/_ref, reference headers unmodified) and against libpsf.
+
+A scenario is a list of steps; each step builds one message, encodes it on the
+sender's RemoteNode, "sends" it (Task copy + zero-copy buffers, as the van
+delivers it) and decodes it on the receiver's node.  ``run`` returns a
+JSON-serialisable record of everything observable: side-info written into the
+FilterConfigs, which buffers survived encode, the decoded keys/values, and
+error statuses.  tests/golden/make_golden.py stores the reference's record;
+the tests compare libpsf's record with it.
+"""
+from __future__ import annotations
+
+import hashlib
+
+import numpy as np
+
+KEY_CACHING, COMPRESSING, FIXING_FLOAT, NOISE = 1, 2, 3, 4
+DT_UINT64, DT_FLOAT, DT_DOUBLE, DT_CHAR = 8, 9, 10, 11
+NP = {DT_FLOAT: np.float32, DT_DOUBLE: np.float64, DT_UINT64: np.uint64, DT_CHAR: np.uint8}
+
+
+def digest(b: np.ndarray) -> str:
+    return hashlib.sha256(np.ascontiguousarray(b).view(np.uint8).tobytes()).hexdigest()[:32]
+
+
+# --------------------------------------------------------------- data ------
+def sorted_keys(n: int, seed: int, hi: int = 10**9) -> np.ndarray:
+    rng = np.random.default_rng(seed)
+    return np.unique(rng.integers(0, hi, size=int(n * 1.1) + 16, dtype=np.uint64))[:n]
+
+
+def gauss(n: int, seed: int, dtype=np.float32) -> np.ndarray:
+    return np.random.default_rng(seed).standard_normal(n).astype(dtype)
+
+
+# ----------------------------------------------------------- scenarios ------
+def kc_scenario():
+    """KEY_CACHING state machine (key_caching.h:9-75) exercised over the async
+    SGD pull/push triple plus the edge cases."""
+    k1 = sorted_keys(3000, 11)
+    k2 = sorted_keys(3000, 12)          # different keys, same length
+    k1_tail = k1.copy()
+    k1_tail[-1] += np.uint64(1)        # same first 2 KiB, same length: false hit
+    k1_short = k1[:2000]               # same prefix, different length
+    small = sorted_keys(17, 13)        # < 2 KiB of keys
+    kc = [(KEY_CACHING, {})]
+    kc_clear = [(KEY_CACHING, {"clear_cache_if_done": True})]
+    S = []
+
+    def step(name, snd, rcv, keys, filters, request=True, push=False, channel=0, kr=(0, 10**9),
+             values=None):
+        S.append(dict(name=name, snd=snd, rcv=rcv, keys=keys, filters=filters, request=request,
+                      push=push, channel=channel, kr=kr, values=values or []))
+
+    step("pull_req_miss", "W", "S", k1, kc, push=False)
+    step("pull_resp_hit", "S", "W", k1, kc, request=False)
+    step("push_hit_clear", "W", "S", k1, kc_clear, push=True)
+    step("push_after_clear_miss", "W", "S", k1, kc, push=True)
+    step("false_hit_same_prefix", "W", "S", k1_tail, kc, push=True)
+    step("length_change_miss", "W", "S", k1_short, kc, push=True)
+    step("other_keys_miss", "W", "S", k2, kc, push=True)
+    step("other_keys_hit", "W", "S", k2, kc, push=True)
+    step("other_channel_miss", "W", "S", k2, kc, push=True, channel=7)
+    step("other_range_miss", "W", "S", k2, kc, push=True, kr=(5, 10**9))
+    step("small_keys_miss", "W", "S", small, kc, push=True, channel=3)
+    step("small_keys_hit", "W", "S", small, kc, push=True, channel=3)
+    step("no_keys_clears_signature", "W", "S", None, kc, push=True, channel=3)
+    step("no_kc_config_passthrough", "W", "S", small, [], push=True, channel=3)
+    step("clear_on_response", "S", "W", k2, kc_clear, request=False)
+    step("after_clear_on_response_miss", "S", "W", k2, kc, request=False)
+    step("request_without_push_keeps", "W", "S", small, kc_clear, push=False, channel=3)
+    step("request_without_push_hit", "W", "S", small, kc, push=False, channel=3)
+    # decode of an elided key the receiver never cached -> fatal CHECK
+    step("sender_caches", "X", "Y", small, kc, push=True, channel=9)
+    step("receiver_miss_is_fatal", "X", "Z", small, kc, push=True, channel=9)
+    return S
+
+
+def chain_scenario(nkeys=3000, seed=2):
+    """ctr online_l1lr.conf:36-53 chain [KEY_CACHING(clear on push),
+    FIXING_FLOAT nb=1] over pull-req / pull-resp / push-req per minibatch."""
+    S = []
+    push_f = [(KEY_CACHING, {"clear_cache_if_done": True}), (FIXING_FLOAT, {"num_bytes": 1})]
+    pull_f = [(KEY_CACHING, {}), (FIXING_FLOAT, {"num_bytes": 1})]
+    for mb in range(3):
+        keys = sorted_keys(nkeys, seed * 100 + mb)
+        w = gauss(nkeys, seed * 100 + mb + 50) * np.float32(0.1)
+        g = gauss(nkeys, seed * 100 + mb + 70)
+        S.append(dict(name=f"mb{mb}_pull_req", snd="W", rcv="S", keys=keys, filters=pull_f,
+                      request=True, push=False, channel=mb, kr=(0, 10**9), values=[]))
+        S.append(dict(name=f"mb{mb}_pull_resp", snd="S", rcv="W", keys=keys, filters=pull_f,
+                      request=False, push=False, channel=mb, kr=(0, 10**9), values=[w]))
+        S.append(dict(name=f"mb{mb}_push", snd="W", rcv="S", keys=keys, filters=push_f,
+                      request=True, push=True, channel=mb, kr=(0, 10**9), values=[g]))
+    return S
+
+
+def ff_message_scenario():
+    """FixingFloatFilter::convert message-level rules (fixing_float.h:24-47):
+    empty arrays skipped, non-float arrays passed through, fixed_point entries
+    consumed per float/double array, presets honoured, num_bytes == 0 no-op."""
+    a = gauss(100, 21)
+    b = gauss(50, 22, np.float64) * 3
+    c = np.arange(10, dtype=np.float32) - 4.5
+    ints = np.arange(12, dtype=np.uint64)
+    S = []
+    S.append(dict(name="mixed_arrays", snd="W", rcv="S", keys=None, request=True, push=True,
+                  channel=0, kr=(0, 10**9),
+                  values=[a, b, np.zeros(0, np.float32), ints, c],
+                  filters=[(FIXING_FLOAT, {"num_bytes": 2})]))
+    S.append(dict(name="preset_ranges", snd="W", rcv="S", keys=None, request=True, push=True,
+                  channel=0, kr=(0, 10**9), values=[a, b],
+                  filters=[(FIXING_FLOAT, {"num_bytes": 3,
+                                           "fixed_point": [(-0.5, 0.5), (None, 1.0)]})]))
+    S.append(dict(name="num_bytes_zero_noop", snd="W", rcv="S", keys=None, request=True, push=True,
+                  channel=0, kr=(0, 10**9), values=[a], filters=[(FIXING_FLOAT, {"num_bytes": 0})]))
+    S.append(dict(name="nb8_rejected", snd="W", rcv="S", keys=None, request=True, push=True,
+                  channel=0, kr=(0, 10**9), values=[a], filters=[(FIXING_FLOAT, {"num_bytes": 8})]))
+    S.append(dict(name="constant_ge32_rejected", snd="W", rcv="S", keys=None, request=True,
+                  push=True, channel=0, kr=(0, 10**9), values=[np.full(8, 40.0, np.float32)],
+                  filters=[(FIXING_FLOAT, {"num_bytes": 1})]))
+    return S
+
+
+# ---------------------------------------------------------------- runner ----
+def run(impl, steps, seed_clock=12345):
+    """Run steps through impl; returns a list of per-step records."""
+    impl.set_clock(seed_clock)
+    nodes = {}
+
+    def node(name):
+        if name not in nodes:
+            nodes[name] = impl.new_node()
+        return nodes[name]
+
+    out = []
+    for st in steps:
+        rec = {"name": st["name"]}
+        m = impl.new_msg(st["request"], st["push"], st["channel"], st["kr"])
+        if st["keys"] is not None:
+            impl.set_key(m, st["keys"])
+        for v in st["values"]:
+            impl.add_value(m, v)
+        fidx = []
+        for ftype, opts in st["filters"]:
+            fidx.append((ftype, impl.add_filter(m, ftype, **opts)))
+        rec["encode_status"] = impl.encode(node(st["snd"]), m)
+        rec["side_info_encode"] = _side(impl, m, fidx)
+        if rec["encode_status"] == 0:
+            k = impl.key(m)
+            rec["wire_key_bytes"] = int(k.size)
+            vals = impl.values(m)
+            rec["wire_values"] = [digest(v) for v in vals]
+            rec["wire_value_bytes"] = [int(v.size) for v in vals]
+            w = impl.clone(m)
+            rec["decode_status"] = impl.decode(node(st["rcv"]), w)
+            if rec["decode_status"] == 0:
+                k = impl.key(w)
+                rec["key_bytes"] = int(k.size)
+                rec["key_digest"] = digest(k)
+                rec["has_key_flag"], rec["key_type"] = impl.key_info(w)
+                vals = impl.values(w)
+                rec["values"] = [digest(v) for v in vals]
+                rec["value_bytes"] = [int(v.size) for v in vals]
+                rec["side_info_decode"] = _side(impl, w, fidx)
+            impl.free_msg(w)
+        impl.free_msg(m)
+        out.append(rec)
+    for n in nodes.values():
+        impl.free_node(n)
+    return out
+
+
+def _side(impl, m, fidx):
+    side = []
+    for ftype, idx in fidx:
+        d = {"type": ftype}
+        if ftype == KEY_CACHING:
+            d["has_signature"], d["signature"] = impl.signature(m, idx)
+        elif ftype == FIXING_FLOAT:
+            d["fixed_point"] = [[bool(a), float(b), bool(c), float(e)] for a, b, c, e in impl.fixed_points(m, idx)]
+        elif ftype == COMPRESSING:
+            d["uncompressed_size"] = impl.uncompressed(m, idx)
+        side.append(d)
+    return side
+
+
+# --------------------------------------------------------------- adapters ---
+class RefImpl:
+    """oracle/_ref (reference headers) behind the runner interface."""
+
+    def __init__(self, ref):
+        self.R = ref
+        self.L = ref.lib
+
+    def set_clock(self, t):
+        self.R.set_time(t)
+
+    def new_node(self):
+        return self.L.psref_node_new()
+
+    def free_node(self, n):
+        self.L.psref_node_free(n)
+
+    def new_msg(self, request, push, channel, kr):
+        return self.R.msg_new(request=request, push=push, has_param=True, key_channel=channel,
+                              key_range=kr)
+
+    def free_msg(self, m):
+        self.L.psref_msg_free(m)
+
+    def clone(self, m):
+        return self.L.psref_msg_clone(m)
+
+    def set_key(self, m, keys):
+        keys = np.ascontiguousarray(keys)
+        self.L.psref_msg_set_key(m, keys.ctypes.data if keys.size else None, keys.nbytes, DT_UINT64)
+
+    def add_value(self, m, v):
+        v = np.ascontiguousarray(v)
+        dt = {np.dtype(np.float32): DT_FLOAT, np.dtype(np.float64): DT_DOUBLE,
+              np.dtype(np.uint64): DT_UINT64}[v.dtype]
+        self.L.psref_msg_add_value(m, v.ctypes.data if v.size else None, v.nbytes, dt)
+
+    def add_filter(self, m, ftype, num_bytes=None, clear_cache_if_done=None, fixed_point=None,
+                   noise=None):
+        i = self.L.psref_msg_add_filter(m, ftype)
+        if num_bytes is not None:
+            self.L.psref_fc_set_num_bytes(m, i, num_bytes)
+        if clear_cache_if_done is not None:
+            self.L.psref_fc_set_clear_cache(m, i, int(clear_cache_if_done))
+        if noise is not None:
+            self.L.psref_fc_set_noise(m, i, noise[0], noise[1])
+        for mn, mx in fixed_point or []:
+            self.L.psref_fc_add_fixed_point(m, i, mn is not None, 0.0 if mn is None else mn,
+                                            mx is not None, 0.0 if mx is None else mx)
+        return i
+
+    def encode(self, n, m):
+        return 0 if self.L.psref_node_encode(n, m) == 0 else -1
+
+    def decode(self, n, m):
+        return 0 if self.L.psref_node_decode(n, m) == 0 else -1
+
+    def key(self, m):
+        return self.R.msg_key(m)
+
+    def key_info(self, m):
+        return bool(self.L.psref_msg_has_key_flag(m)), int(self.L.psref_msg_key_type(m))
+
+    def values(self, m):
+        return self.R.msg_values(m)
+
+    def signature(self, m, i):
+        return self.R.signature(m, i)
+
+    def fixed_points(self, m, i):
+        return self.R.fixed_points(m, i)
+
+    def uncompressed(self, m, i):
+        return [int(self.L.psref_fc_uncompressed(m, i, j)) for j in range(self.L.psref_fc_num_uncompressed(m, i))]
+
+
+class PsfImpl:
+    """libpsf behind the runner interface.  device=None -> host-resident
+    buffers on a host-only context (KEY_CACHING logic without a GPU)."""
+
+    def __init__(self, device=0):
+        import torch
+        from parameter_server_amd import filter as F
+        self.F, self.torch = F, torch
+        self.device = device
+        self.ctx = F.Context(device) if device is not None else F.HostContext()
+
+    def _t(self, a):
+        t = self.torch.from_numpy(np.ascontiguousarray(a).copy())
+        return t.to(f"cuda:{self.device}") if self.device is not None else t
+
+    def set_clock(self, t):
+        self.F.set_clock(t)
+
+    def new_node(self):
+        return self.F.RemoteNode(self.ctx)
+
+    def free_node(self, n):
+        pass
+
+    def new_msg(self, request, push, channel, kr):
+        return self.F.Message(request=request, push=push, has_param=True, key_channel=channel, key_range=kr)
+
+    def free_msg(self, m):
+        pass
+
+    def clone(self, m):
+        return m.clone()
+
+    def set_key(self, m, keys):
+        t = self._t(keys.view(np.int64))
+        m.set_key(t)
+
+    def add_value(self, m, v):
+        dt = {np.dtype(np.float32): DT_FLOAT, np.dtype(np.float64): DT_DOUBLE,
+              np.dtype(np.uint64): DT_UINT64}[v.dtype]
+        t = self._t(v.view(np.int64) if v.dtype == np.uint64 else v)
+        m.add_value(t, dt)
+
+    def add_filter(self, m, ftype, **opts):
+        return m.add_filter(ftype, **opts)
+
+    def encode(self, n, m):
+        try:
+            n.encode(m)
+            return 0
+        except self.F.PsfError:
+            return -1
+
+    def decode(self, n, m):
+        try:
+            n.decode(m)
+            return 0
+        except self.F.PsfError:
+            return -1
+
+    def _copy(self, p, nb, loc):
+        t = self.F.copy_out(p, nb, loc, None if self.device is None else f"cuda:{self.device}")
+        return t.cpu().numpy()
+
+    def key(self, m):
+        p, nb, loc = m.key_ptr()
+        self.ctx.sync()
+        return self._copy(p, nb, loc)
+
+    def key_info(self, m):
+        return m.key_info()
+
+    def values(self, m):
+        self.ctx.sync()
+        return [self._copy(*m.value_ptr(i)) for i in range(m.num_values())]
+
+    def signature(self, m, i):
+        return m.signature(i)
+
+    def fixed_points(self, m, i):
+        return m.fixed_points(i)
+
+    def uncompressed(self, m, i):
+        return m.uncompressed_sizes(i)
