@@ -2,7 +2,7 @@
  * libpsf -- MI355X-native (HIP/gfx950) parameter_server filter codec chain.
  *
  * C ABI of the drop-in boundary.  Plain pointers and sizes only; `stream` is a
- * hipStream_t passed as void* (NULL = the context's own stream).  Every entry
+ * hipStream_t passed as void* (see psf_context_create).  Every entry
  * point returns PSF_OK (0) or a negative PSF_ERR_* code; psf_last_error()
  * describes the last failure on the calling thread.  The reference aborts the
  * process through glog CHECK at the same points; the C++ shim in
@@ -71,7 +71,10 @@ void psf_set_clock(int enable, int64_t t);
 
 /* ---- execution context (device + stream + workspace) ------------------- */
 typedef struct psf_context psf_context;
-int psf_context_create(int device, void* stream, psf_context** out);
+/* own_stream=1: a private non-blocking stream; own_stream=0: kernels go on
+ * `stream` as given (NULL = the legacy default stream).  device < 0 gives a
+ * host-only context (host-resident buffers; codecs needing HBM fail). */
+int psf_context_create(int device, void* stream, int own_stream, psf_context** out);
 int psf_context_destroy(psf_context* ctx);
 int psf_context_sync(psf_context* ctx);
 

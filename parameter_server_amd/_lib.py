@@ -43,7 +43,7 @@ SIGNATURES = {
     "psf_last_error": ([], C.c_char_p),
     "psf_version": ([], C.c_char_p),
     "psf_set_clock": ([C.c_int, C.c_int64], None),
-    "psf_context_create": ([C.c_int, vp, C.POINTER(vp)], C.c_int),
+    "psf_context_create": ([C.c_int, vp, C.c_int, C.POINTER(vp)], C.c_int),
     "psf_context_destroy": ([vp], C.c_int),
     "psf_context_sync": ([vp], C.c_int),
     "psf_ff_encode": ([vp, vp, sz, C.c_int, C.c_int, C.POINTER(FixedPoint), i32, vp], C.c_int),

@@ -110,7 +110,7 @@ int crc32c_launch(const void* d, size_t n, uint32_t* out, hipStream_t st, Profil
   ProfScope ps(prof, kKCrc, st, (double)n);
   hipLaunchKernelGGL(crc32c_chunks, dim3((unsigned)blocks), dim3(kBlock), 0, st,
                      static_cast<const uint8_t*>(d), n, chunk, out, tbl);
-  return kOk;
+  return launch_status();
 }
 
 }  // namespace psf

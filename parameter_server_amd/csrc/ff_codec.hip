@@ -511,10 +511,12 @@ static int encode_typed(const V* x, size_t n, int nb, const FixedPoint& preset, 
       hipLaunchKernelGGL((ff_minmax_partials<V, false>), dim3(grid), dim3(kBlock), 0, st, x, n, partials);
     p.partials = partials;
     p.nparts = grid;
+    if (launch_status() != kOk) return kErrHip;
   }
   ProfScope ps(prof, kKEncode, st, (double)n * (sizeof(V) + nb));
-  return vec ? dispatch_encode_nb<V, true>(x, n, nb, out, p, st)
-             : dispatch_encode_nb<V, false>(x, n, nb, out, p, st);
+  int s = vec ? dispatch_encode_nb<V, true>(x, n, nb, out, p, st)
+              : dispatch_encode_nb<V, false>(x, n, nb, out, p, st);
+  return s == kOk ? launch_status() : s;
 }
 
 int ff_encode_launch(const void* x, size_t n, int value_type, int nb, const FixedPoint& preset,
@@ -566,14 +568,17 @@ int ff_decode_launch(const void* code, size_t n, int value_type, int nb, const f
   const uint8_t* c = static_cast<const uint8_t*>(code);
   const size_t vsz = value_type == kFloat ? 4 : 8;
   ProfScope ps(prof, kKDecode, st, (double)n * (nb + vsz));
+  int s;
   if (value_type == kFloat) {
     float* o = static_cast<float*>(out);
-    return vec ? dispatch_decode_nb<float, true>(c, n, nb, o, p, st)
-               : dispatch_decode_nb<float, false>(c, n, nb, o, p, st);
+    s = vec ? dispatch_decode_nb<float, true>(c, n, nb, o, p, st)
+            : dispatch_decode_nb<float, false>(c, n, nb, o, p, st);
+  } else {
+    double* o = static_cast<double*>(out);
+    s = vec ? dispatch_decode_nb<double, true>(c, n, nb, o, p, st)
+            : dispatch_decode_nb<double, false>(c, n, nb, o, p, st);
   }
-  double* o = static_cast<double*>(out);
-  return vec ? dispatch_decode_nb<double, true>(c, n, nb, o, p, st)
-             : dispatch_decode_nb<double, false>(c, n, nb, o, p, st);
+  return s == kOk ? launch_status() : s;
 }
 
 }  // namespace psf

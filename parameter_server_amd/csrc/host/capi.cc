@@ -47,10 +47,10 @@ const char* psf_last_error(void) { return g_last_error.c_str(); }
 const char* psf_version(void) { return "psf 0.1 gfx950"; }
 void psf_set_clock(int enable, int64_t t) { psf::set_clock_override(enable != 0, t); }
 
-int psf_context_create(int device, void* stream, psf_context** out) {
+int psf_context_create(int device, void* stream, int own_stream, psf_context** out) {
   return guarded([&] {
     if (!out) return PSF_ERR_ARG;
-    *out = new psf_context{new psf::Context(device, static_cast<hipStream_t>(stream))};
+    *out = new psf_context{new psf::Context(device, static_cast<hipStream_t>(stream), own_stream != 0)};
     return PSF_OK;
   });
 }

@@ -20,13 +20,14 @@ struct Context::StreamHolder {
   }
 };
 
-Context::Context(int device, hipStream_t stream) : device_(device), stream_(nullptr) {
+Context::Context(int device, hipStream_t stream, bool own) : device_(device), stream_(nullptr) {
   if (device < 0) return;  // host-only context: host-resident buffers, no HIP calls
   PSF_HIP_CHECK(hipSetDevice(device));
-  bool own = stream == nullptr;
+  if (own) stream = nullptr;
   if (own) PSF_HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
   stream_ = stream;
-  holder_ = std::make_shared<StreamHolder>(StreamHolder{device, stream, own});
+  // constructed in place: a temporary StreamHolder would destroy the stream
+  holder_ = std::shared_ptr<StreamHolder>(new StreamHolder{device, stream, own});
   // keep freed HBM in the default pool for reuse (no release at sync points)
   hipMemPool_t pool;
   if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {

@@ -34,9 +34,10 @@ class Context {
  public:
   static constexpr int kSlots = 256;
 
-  // stream == nullptr -> a private non-blocking stream owned by the context.
+  // own_stream -> a private non-blocking stream owned by the context; else
+  // `stream` as given (nullptr = the legacy default stream).
   // device < 0 -> host-only context (host-resident buffers; no HIP calls).
-  Context(int device, hipStream_t stream);
+  Context(int device, hipStream_t stream, bool own_stream);
   ~Context();
 
   int device() const { return device_; }

@@ -28,6 +28,9 @@ constexpr int kChar = 11;
 constexpr uint32_t kLcgA = 214013u;
 constexpr uint32_t kLcgC = 2531011u;
 
+// status of the most recent launch(es) on this thread
+inline int launch_status() { return hipGetLastError() == hipSuccess ? kOk : kErrHip; }
+
 struct FixedPoint {
   int has_min, has_max;
   float min_value, max_value;

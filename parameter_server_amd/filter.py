@@ -40,7 +40,7 @@ class Context:
         self.device = device
         self.stream = stream if stream is not None else torch.cuda.current_stream(device)
         h = C.c_void_p()
-        check(lib().psf_context_create(device, C.c_void_p(self.stream.cuda_stream), C.byref(h)))
+        check(lib().psf_context_create(device, C.c_void_p(self.stream.cuda_stream), 0, C.byref(h)))
         self.h = h
 
     def sync(self):
@@ -129,7 +129,7 @@ class HostContext(Context):
         self.device = -1
         self.stream = None
         h = C.c_void_p()
-        check(lib().psf_context_create(-1, None, C.byref(h)))
+        check(lib().psf_context_create(-1, None, 0, C.byref(h)))
         self.h = h
 
 
