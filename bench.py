@@ -44,6 +44,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--n", type=int, default=1 << 27, help="values per message (per GPU)")
     ap.add_argument("--nb", type=int, default=1, help="FIXING_FLOAT num_bytes")
+    ap.add_argument("--bufs", type=int, default=3, help="distinct messages cycled through")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
@@ -141,17 +142,25 @@ def main():
     from parameter_server_amd import filter as F
 
     n, nb = args.n, args.nb
-    # this rank's shard of the key range (range.h:100-107 EvenDivide), pre-placed
+    # this rank's shard of the key range (range.h:100-107 EvenDivide), pre-placed.
+    # Consecutive steps use different messages (args.bufs distinct arrays whose
+    # total exceeds the 256 MiB Infinity Cache), so no step reads data a
+    # previous step left on chip.
     g = torch.Generator(device=f"cuda:{local}")
     g.manual_seed(1 + rank)
-    x = torch.randn(n, device=f"cuda:{local}", generator=g, dtype=torch.float32)
+    xs = [torch.randn(n, device=f"cuda:{local}", generator=g, dtype=torch.float32)
+          for _ in range(args.bufs)]
 
     ctx = F.Context(local)
     worker, server = F.RemoteNode(ctx), F.RemoteNode(ctx)
     F.set_clock(12345)  # FIXING_FLOAT seed (time(NULL) in the reference)
-    tmpl = F.Message(request=True, push=True, key_channel=0)
-    tmpl.add_value(x)
-    tmpl.add_filter(FIXING_FLOAT, num_bytes=nb)
+    tmpls = []
+    for x in xs:
+        t = F.Message(request=True, push=True, key_channel=0)
+        t.add_value(x)
+        t.add_filter(FIXING_FLOAT, num_bytes=nb)
+        tmpls.append(t)
+    tmpl = tmpls
 
     worker.roundtrip(server, tmpl, args.warmup)
     torch.cuda.synchronize()

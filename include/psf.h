@@ -151,12 +151,12 @@ int psf_fc_num_uncompressed(const psf_message* msg, int idx);
 int psf_fc_uncompressed(const psf_message* msg, int idx, int i, uint64_t* size);
 
 /* Message path driver (what Executor::Submit -> remote peer -> PickActiveMsg
- * does per message, executor.cc:131-146,178-219): `iters` times, encode a
- * fresh copy of `tmpl` on `snd`, deliver it (Task copy + zero-copy buffers)
- * and decode it on `rcv`.  The last decoded message is returned in *out
- * (may be NULL).  Used by bench.py so no Python runs per message. */
-int psf_node_roundtrip(psf_node* snd, psf_node* rcv, const psf_message* tmpl, int iters,
-                       psf_message** out);
+ * does per message, executor.cc:131-146,178-219): for i in [0, iters), encode
+ * a fresh copy of tmpls[i % ntmpl] on `snd`, deliver it (Task copy + zero-copy
+ * buffers) and decode it on `rcv`.  The last decoded message is returned in
+ * *out (may be NULL).  Used by bench.py so no Python runs per message. */
+int psf_node_roundtrip(psf_node* snd, psf_node* rcv, const psf_message* const* tmpls, int ntmpl,
+                       int iters, psf_message** out);
 
 /* ---- launch profiler (HIP events on the launch stream) ----------------- */
 #define PSF_K_MINMAX 0

@@ -43,7 +43,7 @@ __device__ static inline uint32_t x2nmodp(uint64_t n, unsigned k, const X2nTable
 
 __global__ __launch_bounds__(kBlock) void crc32c_chunks(const uint8_t* __restrict__ d, size_t n,
                                                          size_t chunk, uint32_t* __restrict__ out,
-                                                         X2nTable tbl) {
+                                                         X2nTable tbl, PubSlot* pub, uint32_t ticket) {
   __shared__ uint32_t table[256];
   __shared__ uint32_t wave_acc[kBlock / 64];
   {
@@ -83,7 +83,15 @@ __global__ __launch_bounds__(kBlock) void crc32c_chunks(const uint8_t* __restric
     uint32_t acc = 0;
 #pragma unroll
     for (int w = 0; w < kBlock / 64; ++w) acc ^= wave_acc[w];
-    atomicXor(out, acc);
+    if (gridDim.x == 1) {  // whole message in this workgroup: final value
+      *out = acc;
+      if (pub) {
+        pub->crc = acc;
+        publish_ticket(pub, ticket);
+      }
+    } else {
+      atomicXor(out, acc);
+    }
   }
 }
 
@@ -95,10 +103,18 @@ static X2nTable make_x2n_table() {
   return t;
 }
 
-int crc32c_launch(const void* d, size_t n, uint32_t* out, hipStream_t st, Profiler* prof) {
+int crc32c_launch(const void* d, size_t n, uint32_t* out, hipStream_t st, Profiler* prof,
+                  PubSlot* pub, uint32_t ticket) {
   static const X2nTable tbl = make_x2n_table();
+  if (n == 0) return kErrArg;  // crc32c("") == 0: callers answer that on the host
+  if (n <= kCrcSingleBlock) {
+    size_t chunk = ((n + kBlock - 1) / kBlock + 3) & ~(size_t)3;
+    ProfScope ps(prof, kKCrc, st, (double)n);
+    hipLaunchKernelGGL(crc32c_chunks, dim3(1), dim3(kBlock), 0, st, static_cast<const uint8_t*>(d),
+                       n, chunk, out, tbl, pub, ticket);
+    return launch_status();
+  }
   if (hipMemsetAsync(out, 0, sizeof(uint32_t), st) != hipSuccess) return kErrHip;
-  if (n == 0) return kOk;  // crc32c("") == 0
   // >= 8 bytes per lane, chunks a multiple of 4 bytes, at most kMaxGrid blocks
   size_t lanes = (n + 7) / 8;
   size_t blocks = (lanes + kBlock - 1) / kBlock;
@@ -109,7 +125,7 @@ int crc32c_launch(const void* d, size_t n, uint32_t* out, hipStream_t st, Profil
   blocks = ((n + chunk - 1) / chunk + kBlock - 1) / kBlock;
   ProfScope ps(prof, kKCrc, st, (double)n);
   hipLaunchKernelGGL(crc32c_chunks, dim3((unsigned)blocks), dim3(kBlock), 0, st,
-                     static_cast<const uint8_t*>(d), n, chunk, out, tbl);
+                     static_cast<const uint8_t*>(d), n, chunk, out, tbl, nullptr, 0u);
   return launch_status();
 }
 

@@ -6,13 +6,20 @@
 //   ff_minmax_partials  pass 1 of encode when min/max are not preset
 //                       (fixing_float.h:57-64): per-workgroup min/max of the
 //                       value array as order-preserving integer keys.
-//   ff_encode           pass 2 (fixing_float.h:73-88): every workgroup first folds
-//                       the <= kMaxGrid partials (8-16 KiB, L2-resident), derives
-//                       min/max/bin exactly as the reference, then quantises
-//                       4 values per lane with the stochastic-rounding LCG bit
+//   ff_encode           pass 2 (fixing_float.h:73-88): every workgroup folds the
+//                       <= kMinmaxGrid partials (L2-resident), derives min/max/bin
+//                       exactly as the reference, then quantises 4 values per lane
+//                       per group with the stochastic-rounding LCG bit
 //                       (fixing_float.h:18-21) reproduced by affine jump-ahead.
 //   ff_decode           fixing_float.h:89-101; nb==1 uses a 256-entry LDS table
 //                       built with the same double formula (bit-identical).
+//
+// Data layout: the value array is cut into tiles of kTileGroups groups of 4
+// values (16 KiB of f32); a workgroup owns a contiguous run of tiles and walks
+// it front to back (block-contiguous streams measured 6.1 TB/s read vs 5.2 TB/s
+// for a grid-stride walk on MI355X, tools/bw_probe*.hip).  Inside a tile lane l
+// handles groups l, l+256, l+512, l+768, so every load/store instruction of a
+// wave is one contiguous 1 KiB (f32 in) / 256 B (nb=1 codes out) span.
 //
 // Bit-exactness rules: IEEE double division (hipcc's
 // default f64 fdiv lowering is correctly rounded), NO FMA contraction (this file
@@ -24,6 +31,12 @@
 #include "psf_internal.h"
 
 namespace psf {
+
+constexpr int kTileGroups = 4 * kBlock;  // groups of 4 values per tile
+constexpr int kMinmaxGrid = 1024;        // partials the encode kernel folds
+constexpr int kStreamGrid = 4096;        // workgroups for the store-heavy passes
+constexpr uint32_t kMask17 = 0x1FFFFu;   // LCG state kept mod 2^17 (see quant_group)
+struct Lcg17 { uint32_t a[4], c[4]; };   // affine maps for 1..4 LCG steps, mod 2^17
 
 // ------------------------------------------------------------ helpers ------
 __device__ __forceinline__ uint32_t f32_key(float f) {
@@ -92,88 +105,95 @@ __device__ __forceinline__ void block_minmax(K& lo, K& hi) {
   __syncthreads();
 }
 
-// 4-element vector load of V.
+// 4-element vector access of V.  Cache policy (tools/bw_probe3.hip, emulated
+// round trip, MI355X): the value array is streamed with non-temporal loads in
+// both encode passes and the decoded array is written with non-temporal
+// stores, which keeps the 256 MiB Infinity Cache for the codes the decode pass
+// re-reads and stops the decoded output's write-back from landing on the next
+// message's min/max pass (369 -> 298 us per 2^27-value step).
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
 template <typename V> struct Vec4;
 template <> struct Vec4<float> {
   __device__ static void load(const float* p, float v[4]) {
-    float4 t = *reinterpret_cast<const float4*>(p);
+    f32x4 t = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
     v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
   }
   __device__ static void store(float* p, const float v[4]) {
-    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    f32x4 t = {v[0], v[1], v[2], v[3]};
+    __builtin_nontemporal_store(t, reinterpret_cast<f32x4*>(p));
   }
 };
 template <> struct Vec4<double> {
   __device__ static void load(const double* p, double v[4]) {
-    double2 a = reinterpret_cast<const double2*>(p)[0];
-    double2 b = reinterpret_cast<const double2*>(p)[1];
+    f64x2 a = __builtin_nontemporal_load(reinterpret_cast<const f64x2*>(p));
+    f64x2 b = __builtin_nontemporal_load(reinterpret_cast<const f64x2*>(p) + 1);
     v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
   }
   __device__ static void store(double* p, const double v[4]) {
-    reinterpret_cast<double2*>(p)[0] = make_double2(v[0], v[1]);
-    reinterpret_cast<double2*>(p)[1] = make_double2(v[2], v[3]);
+    f64x2 a = {v[0], v[1]}, b = {v[2], v[3]};
+    __builtin_nontemporal_store(a, reinterpret_cast<f64x2*>(p));
+    __builtin_nontemporal_store(b, reinterpret_cast<f64x2*>(p) + 1);
   }
 };
 
+// tiles [t0, t1) owned by this workgroup
+__device__ __forceinline__ void tile_range(size_t ntiles, size_t& t0, size_t& t1) {
+  const size_t per = (ntiles + gridDim.x - 1) / gridDim.x;
+  t0 = (size_t)blockIdx.x * per;
+  t1 = t0 + per < ntiles ? t0 + per : ntiles;
+}
+
 // ------------------------------------------------------ pass 1: min/max ----
+template <typename V, typename K>
+__device__ __forceinline__ void acc_minmax(V e, K& lo, K& hi) {
+  if (e == e) {  // NaNs are skipped (documented divergence)
+    K k = KeyOf<V>::key(e);
+    lo = k < lo ? k : lo;
+    hi = k > hi ? k : hi;
+  }
+}
+
 // partials layout: K lo[grid], K hi[grid].
 template <typename V, bool kVec>
 __global__ __launch_bounds__(kBlock) void ff_minmax_partials(const V* __restrict__ x, size_t n,
                                                               void* __restrict__ partials) {
   typedef typename KeyOf<V>::K K;
   K lo = KeyOf<V>::kLoId, hi = KeyOf<V>::kHiId;
-  const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
-  const size_t nthreads = (size_t)gridDim.x * kBlock;
   if (kVec) {
     const size_t ngroups = n >> 2;
-    size_t g = tid;
-    // 4 groups (16 values) in flight per lane per iteration
-    for (; g + 3 * nthreads < ngroups; g += 4 * nthreads) {
-      V v[4][4];
+    const size_t ntiles = (ngroups + kTileGroups - 1) / kTileGroups;
+    size_t t0, t1;
+    tile_range(ntiles, t0, t1);
+    for (size_t t = t0; t < t1; ++t) {
+      const size_t gb = t * kTileGroups + threadIdx.x;
+      if ((t + 1) * kTileGroups <= ngroups) {
+        V v[4][4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) Vec4<V>::load(x + 4 * (g + u * nthreads), v[u]);
+        for (int u = 0; u < 4; ++u) Vec4<V>::load(x + 4 * (gb + u * kBlock), v[u]);
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < 4; ++u)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          V e = v[u][j];
-          if (e == e) {
-            K k = KeyOf<V>::key(e);
-            lo = k < lo ? k : lo;
-            hi = k > hi ? k : hi;
+          for (int j = 0; j < 4; ++j) acc_minmax<V, K>(v[u][j], lo, hi);
+      } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const size_t g = gb + u * kBlock;
+          if (g < ngroups) {
+            V v[4];
+            Vec4<V>::load(x + 4 * g, v);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc_minmax<V, K>(v[j], lo, hi);
           }
         }
-    }
-    for (; g < ngroups; g += nthreads) {
-      V v[4];
-      Vec4<V>::load(x + 4 * g, v);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        V e = v[j];
-        if (e == e) {
-          K k = KeyOf<V>::key(e);
-          lo = k < lo ? k : lo;
-          hi = k > hi ? k : hi;
-        }
       }
     }
-    for (size_t i = (ngroups << 2) + tid; i < n; i += nthreads) {
-      V e = x[i];
-      if (e == e) {
-        K k = KeyOf<V>::key(e);
-        lo = k < lo ? k : lo;
-        hi = k > hi ? k : hi;
-      }
-    }
+    if (blockIdx.x == 0)
+      for (size_t i = (ngroups << 2) + threadIdx.x; i < n; i += kBlock) acc_minmax<V, K>(x[i], lo, hi);
   } else {
-    for (size_t i = tid; i < n; i += nthreads) {
-      V e = x[i];
-      if (e == e) {
-        K k = KeyOf<V>::key(e);
-        lo = k < lo ? k : lo;
-        hi = k > hi ? k : hi;
-      }
-    }
+    const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const size_t nthreads = (size_t)gridDim.x * kBlock;
+    for (size_t i = tid; i < n; i += nthreads) acc_minmax<V, K>(x[i], lo, hi);
   }
   block_minmax(lo, hi);
   if (threadIdx.x == 0) {
@@ -183,9 +203,9 @@ __global__ __launch_bounds__(kBlock) void ff_minmax_partials(const V* __restrict
   }
 }
 
-// Fold the partials (every workgroup of the encode kernel does this; the
-// partials are <= 2*kMaxGrid keys and stay in L2).  Returns min/max in the
-// reference's FilterConfig representation (float), fixing_float.h:57-64.
+// Fold the partials (every workgroup of the encode kernel does this; <= 1024
+// pairs, L2-resident).  Returns min/max in the reference's FilterConfig
+// representation (float), fixing_float.h:57-64.
 template <typename V>
 __device__ __forceinline__ void fold_partials(const void* partials, int nparts, float& mn_f,
                                               float& mx_f) {
@@ -225,13 +245,18 @@ struct EncodeParams {
   int has_min, has_max;
   float preset_min, preset_max;
   uint32_t seed;
-  uint32_t jump_a, jump_c;  // LCG affine map for 4*nthreads steps
+  uint32_t a_lane, c_lane;  // LCG affine map (mod 2^17) advancing one group-row (kBlock groups)
+  uint32_t a_tile, c_tile;  // ... one tile (kTileGroups groups)
+  uint32_t a_thr, c_thr;    // scalar path (full 32-bit): nthreads elements
+  Lcg17 k17;                // 1..4 steps, mod 2^17
   double ratio;
-  float* range_out;       // device float[2] side-info, may be null
-  int* status_out;        // device int, may be null
+  float* range_out;         // side-info float[2] (device), may be null
+  int* status_out;          // CHECK_GT(bin,0) outcome (device), may be null
+  PubSlot* pub;             // host-mapped publish slot, may be null
+  uint32_t ticket;
 };
 
-// s -> a*s + c, composed k times, k < 2^63.
+// s -> a*s + c, composed k times.
 __device__ __forceinline__ uint32_t lcg_jump(uint32_t s, uint64_t k) {
   uint32_t a = kLcgA, c = kLcgC;
   while (k) {
@@ -248,7 +273,7 @@ __device__ __forceinline__ void store_codes(uint8_t* __restrict__ out, size_t g,
   if (NB == 1) {
     uint32_t w = (uint32_t)(r[0] & 0xFF) | ((uint32_t)(r[1] & 0xFF) << 8) |
                  ((uint32_t)(r[2] & 0xFF) << 16) | ((uint32_t)(r[3] & 0xFF) << 24);
-    __builtin_nontemporal_store(w, reinterpret_cast<uint32_t*>(out) + g);
+    reinterpret_cast<uint32_t*>(out)[g] = w;
   } else if (NB == 2) {
     uint32_t w0 = (uint32_t)(r[0] & 0xFFFF) | ((uint32_t)(r[1] & 0xFFFF) << 16);
     uint32_t w1 = (uint32_t)(r[2] & 0xFFFF) | ((uint32_t)(r[3] & 0xFFFF) << 16);
@@ -271,28 +296,85 @@ __device__ __forceinline__ void store_codes(uint8_t* __restrict__ out, size_t g,
   }
 }
 
+// The quantiser.  Reference (fixing_float.h:80-82):
+//   tmp = (proj - min_v) / bin * ratio;  r = (uint64)floor(tmp) + boolrand
+// Only floor(tmp) matters, so the f64 division is skipped unless it can change
+// the floor:
+//  * f64 fast path (nb <= 3): t' = d * (ratio/bin) differs from tmp by
+//    < 5e-16 * tmp <= 8.4e-9; floor(t') == floor(tmp) whenever frac(t') is
+//    farther than kGuard64 = 2^-26 from an integer.
+//  * f32 fast path (f32 values, nb == 1): d and the product in f32 carry
+//    <= 3 * 2^-24 relative error, |t' - tmp| <= 4.6e-5 for tmp <= 254, so the
+//    guard is kGuard32 = 2^-13.  (tests/test_oracle.py checks both bounds.)
+// Anything inside a guard band, NaN inputs (the min/max clamp sends them to a
+// band edge) and an infinite bin take the reference's exact double sequence.
+constexpr double kGuard64 = 1.4901161193847656e-08;  // 2^-26
+constexpr float kGuard32 = 1.220703125e-04f;         // 2^-13
+
+struct QuantParams {
+  double min_v, max_v, bin, ratio, scale;
+  float min_f, max_f, scale_f;
+  bool fast;  // bin finite (an infinite bin makes inf/inf NaNs the fast path misses)
+};
+
+// the reference's exact sequence, NaN -> 0 (x86 cast)
+__device__ __forceinline__ uint32_t quant_exact(double x, const QuantParams& q) {
+  const double proj = x > q.max_v ? q.max_v : (x < q.min_v ? q.min_v : x);
+  const double tmp = (proj - q.min_v) / q.bin * q.ratio;
+  return (tmp == tmp) ? (uint32_t)floor(tmp) : 0u;
+}
+
 template <typename V, int NB>
-__device__ __forceinline__ uint64_t quantize(V xv, double min_v, double max_v, double bin,
-                                            double ratio, uint32_t& s) {
-  double x = (double)xv;
-  double proj = x > max_v ? max_v : (x < min_v ? min_v : x);
-  double tmp = (proj - min_v) / bin * ratio;
-  s = kLcgA * s + kLcgC;
-  uint64_t bit = ((s >> 16) & 1u) == 0u ? 1u : 0u;
-  uint64_t q;
-  if (NB <= 3) {
-    // ratio > 0 and proj >= min_v: tmp is in [0, ratio] or NaN
-    q = (tmp == tmp) ? (uint64_t)(uint32_t)floor(tmp) : 0;
-  } else {
-    q = x86_d2u64(floor(tmp));
+__device__ __forceinline__ uint64_t quant_floor(V xv, const QuantParams& q) {
+  if (NB >= 4) {  // degenerate int-shift ratios: always the exact sequence
+    const double x = (double)xv;
+    const double proj = x > q.max_v ? q.max_v : (x < q.min_v ? q.min_v : x);
+    return x86_d2u64(floor((proj - q.min_v) / q.bin * q.ratio));
   }
-  return q + bit;
+  if (!q.fast) return quant_exact((double)xv, q);
+  if (NB == 1 && sizeof(V) == 4) {
+    const float x = (float)xv;
+    const float t = (fminf(fmaxf(x, q.min_f), q.max_f) - q.min_f) * q.scale_f;
+    const float f = floorf(t);
+    const float fr = t - f;
+    if (__builtin_expect(fr > kGuard32 && fr < 1.0f - kGuard32, 1)) return (uint32_t)f;
+    return quant_exact((double)xv, q);
+  }
+  const double x = (double)xv;
+  const double t = (fmin(fmax(x, q.min_v), q.max_v) - q.min_v) * q.scale;
+  const double f = floor(t);
+  const double fr = t - f;
+  if (__builtin_expect(fr > kGuard64 && fr < 1.0 - kGuard64, 1)) return (uint32_t)f;
+  return quant_exact(x, q);
+}
+
+// Only bit 16 of the LCG state is ever observed, and (a*s + c) mod 2^17 depends
+// only on s mod 2^17, so the vector path carries the state mod 2^17 and steps
+// it with full-rate 24-bit multiplies.  k17[k] = affine map for k+1 steps.
+
+__device__ __forceinline__ uint32_t step17(uint32_t a, uint32_t c, uint32_t s) {
+  return (__umul24(a, s) + c) & kMask17;
+}
+
+template <typename V, int NB>
+__device__ __forceinline__ void quant_group(const V v[4], const QuantParams& q, uint32_t s17,
+                                            const Lcg17& k17, uint64_t r[4]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t sj = step17(k17.a[j], k17.c[j], s17);  // state s_{4g+j+1}
+    r[j] = quant_floor<V, NB>(v[j], q) + (uint64_t)((~sj >> 16) & 1u);
+  }
+}
+
+// full 32-bit state step (scalar and tail paths)
+__device__ __forceinline__ uint64_t lcg_bit(uint32_t& s) {
+  s = kLcgA * s + kLcgC;
+  return ((s >> 16) & 1u) == 0u ? 1u : 0u;
 }
 
 template <typename V, int NB, bool kVec>
 __global__ __launch_bounds__(kBlock) void ff_encode(const V* __restrict__ x, size_t n,
                                                      uint8_t* __restrict__ out, EncodeParams p) {
-  __shared__ float s_range[2];
   float mn_f = p.preset_min, mx_f = p.preset_max;
   if (p.partials != nullptr) {
     float cmn, cmx;
@@ -300,50 +382,85 @@ __global__ __launch_bounds__(kBlock) void ff_encode(const V* __restrict__ x, siz
     if (!p.has_min) mn_f = cmn;
     if (!p.has_max) mx_f = cmx;
   }
-  (void)s_range;
-  const double min_v = (double)mn_f, max_v = (double)mx_f;
-  const double bin = max_v - min_v;
+  QuantParams q;
+  q.min_v = (double)mn_f;
+  q.max_v = (double)mx_f;
+  q.bin = q.max_v - q.min_v;
+  q.ratio = p.ratio;
+  q.scale = q.ratio / q.bin;
+  q.min_f = mn_f;
+  q.max_f = mx_f;
+  q.scale_f = (float)q.scale;
+  q.fast = q.bin < __builtin_huge_val();
   if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const int status = (q.bin > 0) ? kOk : kErrBin;
     if (p.range_out) { p.range_out[0] = mn_f; p.range_out[1] = mx_f; }
-    if (p.status_out) *p.status_out = (bin > 0) ? kOk : kErrBin;
+    if (p.status_out) *p.status_out = status;
+    if (p.pub) {  // side-info to the host while the grid keeps streaming
+      p.pub->range[0] = mn_f;
+      p.pub->range[1] = mx_f;
+      p.pub->status = status;
+      publish_ticket(p.pub, p.ticket);
+    }
   }
-  if (!(bin > 0)) return;  // CHECK_GT(bin, 0), fixing_float.h:71
-  const double ratio = p.ratio;
+  if (!(q.bin > 0)) return;  // CHECK_GT(bin, 0), fixing_float.h:71
 
-  const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
-  const size_t nthreads = (size_t)gridDim.x * kBlock;
   if (kVec) {
     const size_t ngroups = n >> 2;
+    const size_t ntiles = (ngroups + kTileGroups - 1) / kTileGroups;
+    size_t t0, t1;
+    tile_range(ntiles, t0, t1);
     // state before element 4g is s_{4g}; element i consumes s_{i+1}
-    uint32_t s = lcg_jump(p.seed, 4 * tid);
-    for (size_t g = tid; g < ngroups; g += nthreads) {
-      V v[4];
-      Vec4<V>::load(x + 4 * g, v);
-      uint64_t r[4];
-      uint32_t t = s;
+    uint32_t s = lcg_jump(p.seed, 4ull * (t0 * kTileGroups + threadIdx.x)) & kMask17;
+    for (size_t t = t0; t < t1; ++t) {
+      const size_t gb = t * kTileGroups + threadIdx.x;
+      uint32_t su = s;
+      if ((t + 1) * kTileGroups <= ngroups) {
+        V v[4][4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) r[j] = quantize<V, NB>(v[j], min_v, max_v, bin, ratio, t);
-      store_codes<NB>(out, g, r);
-      s = p.jump_a * s + p.jump_c;
+        for (int u = 0; u < 4; ++u) Vec4<V>::load(x + 4 * (gb + u * kBlock), v[u]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          uint64_t r[4];
+          quant_group<V, NB>(v[u], q, su, p.k17, r);
+          store_codes<NB>(out, gb + u * kBlock, r);
+          su = step17(p.a_lane, p.c_lane, su);
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const size_t g = gb + u * kBlock;
+          if (g < ngroups) {
+            V v[4];
+            Vec4<V>::load(x + 4 * g, v);
+            uint64_t r[4];
+            quant_group<V, NB>(v, q, su, p.k17, r);
+            store_codes<NB>(out, g, r);
+          }
+          su = step17(p.a_lane, p.c_lane, su);
+        }
+      }
+      s = step17(p.a_tile, p.c_tile, s);
     }
-    // ragged tail (< 4 elements): one thread
+    // ragged tail (< 4 values): one thread
     const size_t tail = ngroups << 2;
-    if (tid == 0 && tail < n) {
-      uint32_t t = lcg_jump(p.seed, tail);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && tail < n) {
+      uint32_t st = lcg_jump(p.seed, tail);
       for (size_t i = tail; i < n; ++i) {
-        uint64_t r = quantize<V, NB>(x[i], min_v, max_v, bin, ratio, t);
+        uint64_t r = quant_floor<V, NB>(x[i], q) + lcg_bit(st);
         for (int j = 0; j < NB; ++j) { out[i * NB + j] = (uint8_t)(r & 0xFF); r >>= 8; }
       }
     }
   } else {
-    // unaligned input: scalar path, one element per lane per step
+    // unaligned buffers: scalar grid-stride path, one value per lane per step
+    const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const size_t nthreads = (size_t)gridDim.x * kBlock;
     uint32_t s = lcg_jump(p.seed, tid);
-    const uint32_t ja = p.jump_a, jc = p.jump_c;  // here: affine map for nthreads steps
     for (size_t i = tid; i < n; i += nthreads) {
-      uint32_t t = s;
-      uint64_t r = quantize<V, NB>(x[i], min_v, max_v, bin, ratio, t);
+      uint32_t st = s;
+      uint64_t r = quant_floor<V, NB>(x[i], q) + lcg_bit(st);
       for (int j = 0; j < NB; ++j) { out[i * NB + j] = (uint8_t)(r & 0xFF); r >>= 8; }
-      s = ja * s + jc;
+      s = p.a_thr * s + p.c_thr;
     }
   }
 }
@@ -361,6 +478,21 @@ __device__ __forceinline__ V dequant(uint64_t code, double ratio, double bin, do
   return (V)(r / ratio * bin + min_v);
 }
 
+template <int NB>
+__device__ __forceinline__ void load_codes(const uint8_t* __restrict__ code, size_t g, uint64_t r[4]) {
+  if (NB == 2) {
+    uint2 w = reinterpret_cast<const uint2*>(code)[g];
+    r[0] = w.x & 0xFFFF; r[1] = w.x >> 16; r[2] = w.y & 0xFFFF; r[3] = w.y >> 16;
+  } else {
+    const uint32_t* c = reinterpret_cast<const uint32_t*>(code) + 3 * g;
+    uint32_t a = c[0], b = c[1], d = c[2];
+    r[0] = a & 0xFFFFFF;
+    r[1] = (a >> 24) | ((b & 0xFFFF) << 8);
+    r[2] = (b >> 16) | ((d & 0xFF) << 16);
+    r[3] = d >> 8;
+  }
+}
+
 template <typename V, int NB, bool kVec>
 __global__ __launch_bounds__(kBlock) void ff_decode(const uint8_t* __restrict__ code, size_t n,
                                                      V* __restrict__ out, DecodeParams p) {
@@ -369,65 +501,70 @@ __global__ __launch_bounds__(kBlock) void ff_decode(const uint8_t* __restrict__ 
   const double min_v = (double)mn_f, max_v = (double)mx_f;
   const double bin = max_v - min_v;
   const double ratio = p.ratio;
-  const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
-  const size_t nthreads = (size_t)gridDim.x * kBlock;
 
-  if (NB == 1 && kVec) {
-    // 256-entry table, same formula => bit-identical to the per-element path
+  if (kVec && NB <= 3) {
+    const size_t ngroups = n >> 2;
+    const size_t ntiles = (ngroups + kTileGroups - 1) / kTileGroups;
+    size_t t0, t1;
+    tile_range(ntiles, t0, t1);
     __shared__ V lut[256];
-    lut[threadIdx.x] = dequant<V>((uint64_t)threadIdx.x, ratio, bin, min_v);
-    __syncthreads();
-    const size_t ngroups = n >> 2;
-    const uint32_t* c32 = reinterpret_cast<const uint32_t*>(code);
-    size_t g = tid;
-    for (; g + 3 * nthreads < ngroups; g += 4 * nthreads) {
-      uint32_t w[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) w[u] = __builtin_nontemporal_load(c32 + g + u * nthreads);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        V v[4] = {lut[w[u] & 0xFF], lut[(w[u] >> 8) & 0xFF], lut[(w[u] >> 16) & 0xFF], lut[w[u] >> 24]};
-        Vec4<V>::store(out + 4 * (g + u * nthreads), v);
-      }
+    if (NB == 1) {
+      // 256-entry table, same formula => bit-identical to the per-element path
+      lut[threadIdx.x] = dequant<V>((uint64_t)threadIdx.x, ratio, bin, min_v);
+      __syncthreads();
     }
-    for (; g < ngroups; g += nthreads) {
-      uint32_t w = c32[g];
-      V v[4] = {lut[w & 0xFF], lut[(w >> 8) & 0xFF], lut[(w >> 16) & 0xFF], lut[w >> 24]};
-      Vec4<V>::store(out + 4 * g, v);
-    }
-    for (size_t i = (ngroups << 2) + tid; i < n; i += nthreads) out[i] = lut[code[i]];
-    return;
-  }
-
-  if (kVec && (NB == 2 || NB == 3)) {
-    const size_t ngroups = n >> 2;
-    for (size_t g = tid; g < ngroups; g += nthreads) {
-      uint64_t r[4];
-      if (NB == 2) {
-        uint2 w = reinterpret_cast<const uint2*>(code)[g];
-        r[0] = w.x & 0xFFFF; r[1] = w.x >> 16; r[2] = w.y & 0xFFFF; r[3] = w.y >> 16;
+    for (size_t t = t0; t < t1; ++t) {
+      const size_t gb = t * kTileGroups + threadIdx.x;
+      const bool full = (t + 1) * kTileGroups <= ngroups;
+      if (NB == 1) {
+        const uint32_t* c32 = reinterpret_cast<const uint32_t*>(code);
+        uint32_t w[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const size_t g = gb + u * kBlock;
+          w[u] = (full || g < ngroups) ? c32[g] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const size_t g = gb + u * kBlock;
+          if (full || g < ngroups) {
+            V v[4] = {lut[w[u] & 0xFF], lut[(w[u] >> 8) & 0xFF], lut[(w[u] >> 16) & 0xFF],
+                      lut[w[u] >> 24]};
+            Vec4<V>::store(out + 4 * g, v);
+          }
+        }
       } else {
-        const uint32_t* c = reinterpret_cast<const uint32_t*>(code) + 3 * g;
-        uint32_t a = c[0], b = c[1], d = c[2];
-        r[0] = a & 0xFFFFFF;
-        r[1] = (a >> 24) | ((b & 0xFFFF) << 8);
-        r[2] = (b >> 16) | ((d & 0xFF) << 16);
-        r[3] = d >> 8;
-      }
-      V v[4];
+        uint64_t r[4][4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = dequant<V>(r[j], ratio, bin, min_v);
-      Vec4<V>::store(out + 4 * g, v);
+        for (int u = 0; u < 4; ++u) {
+          const size_t g = gb + u * kBlock;
+          if (full || g < ngroups) load_codes<NB>(code, g, r[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const size_t g = gb + u * kBlock;
+          if (full || g < ngroups) {
+            V v[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = dequant<V>(r[u][j], ratio, bin, min_v);
+            Vec4<V>::store(out + 4 * g, v);
+          }
+        }
+      }
     }
-    for (size_t i = (ngroups << 2) + tid; i < n; i += nthreads) {
-      uint64_t r = 0;
-      for (int j = 0; j < NB; ++j) r |= (uint64_t)code[i * NB + j] << (8 * j);
-      out[i] = dequant<V>(r, ratio, bin, min_v);
+    if (blockIdx.x == 0) {
+      for (size_t i = (ngroups << 2) + threadIdx.x; i < n; i += kBlock) {
+        uint64_t r = 0;
+        for (int j = 0; j < NB; ++j) r |= (uint64_t)code[i * NB + j] << (8 * j);
+        out[i] = dequant<V>(r, ratio, bin, min_v);
+      }
     }
     return;
   }
 
   // generic byte path (nb >= 4, or unaligned buffers)
+  const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  const size_t nthreads = (size_t)gridDim.x * kBlock;
   for (size_t i = tid; i < n; i += nthreads) {
     uint64_t r = 0;
     for (int j = 0; j < NB; ++j) r |= (uint64_t)code[i * NB + j] << (8 * j);
@@ -460,12 +597,26 @@ int ff_grid(size_t work_items) {
   return (int)g;
 }
 
+static int tile_grid(size_t n, int cap) {
+  const size_t ntiles = ((n >> 2) + kTileGroups - 1) / kTileGroups;
+  size_t g = ntiles < 1 ? 1 : ntiles;
+  if (g > (size_t)cap) g = cap;
+  return (int)g;
+}
+
 template <typename V, int NB, bool kVec>
 static void launch_encode(const V* x, size_t n, uint8_t* out, EncodeParams p, hipStream_t st) {
-  const size_t items = kVec ? (n >> 2) : n;
-  const int grid = ff_grid(items);
-  const uint64_t stride = (uint64_t)grid * kBlock * (kVec ? 4 : 1);
-  lcg_affine_pow(stride, p.jump_a, p.jump_c);
+  const int grid = kVec ? tile_grid(n, kStreamGrid) : ff_grid(n);
+  lcg_affine_pow(4ull * kBlock, p.a_lane, p.c_lane);
+  lcg_affine_pow(4ull * kTileGroups, p.a_tile, p.c_tile);
+  lcg_affine_pow((uint64_t)grid * kBlock, p.a_thr, p.c_thr);
+  p.a_lane &= kMask17; p.c_lane &= kMask17;
+  p.a_tile &= kMask17; p.c_tile &= kMask17;
+  for (int k = 0; k < 4; ++k) {
+    lcg_affine_pow((uint64_t)k + 1, p.k17.a[k], p.k17.c[k]);
+    p.k17.a[k] &= kMask17;
+    p.k17.c[k] &= kMask17;
+  }
   hipLaunchKernelGGL((ff_encode<V, NB, kVec>), dim3(grid), dim3(kBlock), 0, st, x, n, out, p);
 }
 
@@ -488,8 +639,10 @@ static int dispatch_encode_nb(const V* x, size_t n, int nb, uint8_t* out, const 
 template <typename V>
 static int encode_typed(const V* x, size_t n, int nb, const FixedPoint& preset, uint32_t seed,
                         uint8_t* out, void* partials, float* range_out, int* status_out,
-                        hipStream_t st, Profiler* prof) {
+                        hipStream_t st, Profiler* prof, PubSlot* pub, uint32_t ticket) {
   EncodeParams p{};
+  p.pub = pub;
+  p.ticket = ticket;
   p.has_min = preset.has_min;
   p.has_max = preset.has_max;
   p.preset_min = preset.min_value;
@@ -498,12 +651,11 @@ static int encode_typed(const V* x, size_t n, int nb, const FixedPoint& preset, 
   p.ratio = ff_ratio(nb);
   p.range_out = range_out;
   p.status_out = status_out;
-  // 16-byte alignment of the input and 4-byte alignment of the output
+  // 16-byte aligned values, 4-byte (nb=2: 8-byte) aligned codes
   const bool vec = ((reinterpret_cast<uintptr_t>(x) & 15) == 0) &&
                    ((reinterpret_cast<uintptr_t>(out) & (nb == 2 ? 7 : 3)) == 0);
   if (!(preset.has_min && preset.has_max)) {
-    const size_t items = vec ? (n >> 2) : n;
-    const int grid = ff_grid(items);
+    const int grid = vec ? tile_grid(n, kMinmaxGrid) : (ff_grid(n) < kMinmaxGrid ? ff_grid(n) : kMinmaxGrid);
     ProfScope ps(prof, kKMinmax, st, (double)n * sizeof(V));
     if (vec)
       hipLaunchKernelGGL((ff_minmax_partials<V, true>), dim3(grid), dim3(kBlock), 0, st, x, n, partials);
@@ -521,23 +673,24 @@ static int encode_typed(const V* x, size_t n, int nb, const FixedPoint& preset, 
 
 int ff_encode_launch(const void* x, size_t n, int value_type, int nb, const FixedPoint& preset,
                      uint32_t seed, void* out, void* partials, float* range_out, int* status_out,
-                     hipStream_t st, Profiler* prof) {
+                     hipStream_t st, Profiler* prof, PubSlot* pub, uint32_t ticket) {
   if (nb <= 0 || nb >= 8) return kErrNbytes;
   if (n == 0) return kOk;
   if (value_type == kFloat)
     return encode_typed<float>(static_cast<const float*>(x), n, nb, preset, seed,
-                               static_cast<uint8_t*>(out), partials, range_out, status_out, st, prof);
+                               static_cast<uint8_t*>(out), partials, range_out, status_out, st, prof,
+                               pub, ticket);
   if (value_type == kDouble)
     return encode_typed<double>(static_cast<const double*>(x), n, nb, preset, seed,
-                                static_cast<uint8_t*>(out), partials, range_out, status_out, st, prof);
+                                static_cast<uint8_t*>(out), partials, range_out, status_out, st, prof,
+                                pub, ticket);
   return kErrArg;
 }
 
 template <typename V, int NB, bool kVec>
 static void launch_decode(const uint8_t* code, size_t n, V* out, const DecodeParams& p,
                           hipStream_t st) {
-  const size_t items = kVec ? (n >> 2) : n;
-  const int grid = ff_grid(items);
+  const int grid = (kVec && NB <= 3) ? tile_grid(n, kStreamGrid) : ff_grid(n);
   hipLaunchKernelGGL((ff_decode<V, NB, kVec>), dim3(grid), dim3(kBlock), 0, st, code, n, out, p);
 }
 

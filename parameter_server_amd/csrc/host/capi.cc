@@ -79,12 +79,13 @@ int psf_ff_encode(psf_context* ctx, const void* d_values, size_t n, int value_ty
                                    c.partials(), nullptr, nullptr, c.stream(), c.prof());
     }
     if (n == 0) return PSF_ERR_ARG;  // min/max of an empty array
-    psf::Slot* s = c.d_slots();
+    const uint32_t ticket = c.next_ticket();
     int st = psf::ff_encode_launch(d_values, n, value_type, num_bytes, pre, (uint32_t)seed, d_code,
-                                   c.partials(), s->range, &s->status, c.stream(), c.prof());
+                                   c.partials(), nullptr, nullptr, c.stream(), c.prof(),
+                                   c.pub_dev(0), ticket);
     if (st != PSF_OK) return st;
-    c.fetch_slots(1);
-    const psf::Slot& h = c.h_slots()[0];
+    c.wait_ticket(0, ticket);
+    const psf::Slot& h = *c.pub_host(0);
     if (!fp->has_min) { fp->min_value = h.range[0]; fp->has_min = 1; }
     if (!fp->has_max) { fp->max_value = h.range[1]; fp->has_max = 1; }
     return h.status;
@@ -127,10 +128,12 @@ int psf_crc32c(psf_context* ctx, const void* d_data, size_t bytes, uint32_t* crc
   return guarded([&] {
     if (!ctx || !crc) return PSF_ERR_ARG;
     psf::Context& c = *ctx->impl;
-    int st = psf::crc32c_launch(d_data, bytes, &c.d_slots()[0].crc, c.stream(), c.prof());
+    if (bytes == 0) { *crc = 0; return PSF_OK; }  // crc32c("") == 0
+    uint32_t* d_out = &c.d_slots()[0].crc;
+    int st = psf::crc32c_launch(d_data, bytes, d_out, c.stream(), c.prof());
     if (st != PSF_OK) return st;
-    c.fetch_slots(1);
-    *crc = c.h_slots()[0].crc;
+    PSF_HIP_CHECK(hipMemcpyAsync(crc, d_out, sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream()));
+    c.sync();
     return PSF_OK;
   });
 }
@@ -298,13 +301,13 @@ int psf_fc_signature(const psf_message* msg, int idx, int* has_signature, uint32
 int psf_fc_num_uncompressed(const psf_message* msg, int idx) {
   return guarded([&] { return (int)fc_at(msg, idx)->uncompressed_size.size(); });
 }
-int psf_node_roundtrip(psf_node* snd, psf_node* rcv, const psf_message* tmpl, int iters,
-                       psf_message** out) {
+int psf_node_roundtrip(psf_node* snd, psf_node* rcv, const psf_message* const* tmpls, int ntmpl,
+                       int iters, psf_message** out) {
   return guarded([&] {
-    if (!snd || !rcv || !tmpl || iters < 0) return PSF_ERR_ARG;
+    if (!snd || !rcv || !tmpls || ntmpl <= 0 || iters < 0) return PSF_ERR_ARG;
     psf_message* last = nullptr;
     for (int i = 0; i < iters; ++i) {
-      psf::Message m = tmpl->m;       // fresh Task + zero-copy buffers
+      psf::Message m = tmpls[i % ntmpl]->m;  // fresh Task + zero-copy buffers
       snd->impl->EncodeMessage(&m);
       psf::Message w = m;             // delivered copy (van: Task frame + data frames)
       rcv->impl->DecodeMessage(&w);

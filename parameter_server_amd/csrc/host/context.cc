@@ -1,5 +1,6 @@
 #include "context.h"
 
+#include <sched.h>
 #include <string.h>
 #include <time.h>
 
@@ -37,7 +38,9 @@ Context::Context(int device, hipStream_t stream, bool own) : device_(device), st
   PSF_HIP_CHECK(hipMalloc(&d_partials_, 2 * sizeof(uint64_t) * kMaxGrid));
   PSF_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&d_slots_), sizeof(Slot) * kSlots));
   PSF_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_slots_), sizeof(Slot) * kSlots,
-                              hipHostMallocDefault));
+                              hipHostMallocMapped | hipHostMallocCoherent));
+  memset(h_slots_, 0, sizeof(Slot) * kSlots);
+  PSF_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&m_slots_), h_slots_, 0));
 }
 
 Context::~Context() {
@@ -66,11 +69,22 @@ Buffer Context::alloc(size_t bytes) {
   return b;
 }
 
-void Context::fetch_slots(int n) {
+void Context::wait_ticket(int i, uint32_t ticket) {
   if (device_ < 0) throw CheckError(kErrArg, "host-only context has no device workspace");
-  if (n <= 0) { sync(); return; }
-  PSF_HIP_CHECK(hipMemcpyAsync(h_slots_, d_slots_, sizeof(Slot) * n, hipMemcpyDeviceToHost, stream_));
-  sync();
+  const Slot* s = h_slots_ + i;
+  for (uint64_t spin = 0;; ++spin) {
+    if (__atomic_load_n(&s->ticket, __ATOMIC_ACQUIRE) == ticket) return;
+    if ((spin & 255) == 255) {
+      hipError_t q = hipStreamQuery(stream_);
+      if (q == hipSuccess) {  // stream drained: the publish must be visible now
+        if (__atomic_load_n(&s->ticket, __ATOMIC_ACQUIRE) == ticket) return;
+        throw CheckError(kErrHip, "kernel finished without publishing its side-info");
+      }
+      if (q != hipErrorNotReady)
+        throw CheckError(kErrHip, std::string("stream failed: ") + hipGetErrorString(q));
+      if (spin > (1u << 16)) sched_yield();
+    }
+  }
 }
 
 void Context::sync() {

@@ -23,12 +23,7 @@ namespace psf {
                                                   hipGetErrorString(_e));           \
   } while (0)
 
-// Side-info slot written by the device, mirrored to pinned host memory.
-struct Slot {
-  float range[2];
-  int32_t status;
-  uint32_t crc;
-};
+typedef PubSlot Slot;
 
 class Context {
  public:
@@ -48,9 +43,14 @@ class Context {
 
   void* partials() const { return d_partials_; }
   Slot* d_slots() const { return d_slots_; }
-  Slot* h_slots() const { return h_slots_; }
-  // copy slots [0, n) device->pinned host and wait for the stream
-  void fetch_slots(int n);
+  // host-mapped, coherent publish slots: kernels write through pub_dev(i),
+  // the host reads pub_host(i)
+  Slot* pub_dev(int i) const { return m_slots_ + i; }
+  Slot* pub_host(int i) const { return h_slots_ + i; }
+  uint32_t next_ticket() { return ++ticket_; }
+  // Wait until slot i carries `ticket` (spins on host memory; falls back to
+  // the stream state so a kernel that never publishes cannot hang the host).
+  void wait_ticket(int i, uint32_t ticket);
   void sync();
   // stage a host buffer into HBM (used at the host edge)
   Buffer to_device(const Buffer& b);
@@ -67,6 +67,8 @@ class Context {
   void* d_partials_ = nullptr;
   Slot* d_slots_ = nullptr;
   Slot* h_slots_ = nullptr;
+  Slot* m_slots_ = nullptr;
+  uint32_t ticket_ = 0;
   std::mutex mu_;
 };
 

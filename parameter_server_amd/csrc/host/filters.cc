@@ -31,11 +31,13 @@ FilterConfig* Filter::find(FilterConfig::Type type, Task* task) {  // filter.cc:
 uint32_t KeyCachingFilter::signature(const Buffer& key) {
   const size_t len = std::min(key.bytes, kMaxSigLen);  // key_caching.h:18
   if (key.loc == Loc::kHost) return crc32c_host(key.ptr, len);
-  Slot* d = ctx_->d_slots();
-  int st = crc32c_launch(key.ptr, len, &d[0].crc, ctx_->stream(), ctx_->prof());
+  // <= 2 KiB: one workgroup, result published straight to host-mapped memory
+  const uint32_t ticket = ctx_->next_ticket();
+  int st = crc32c_launch(key.ptr, len, &ctx_->d_slots()[0].crc, ctx_->stream(), ctx_->prof(),
+                         ctx_->pub_dev(0), ticket);
   if (st != kOk) throw CheckError(st, "crc32c launch failed");
-  ctx_->fetch_slots(1);
-  return ctx_->h_slots()[0].crc;
+  ctx_->wait_ticket(0, ticket);
+  return ctx_->pub_host(0)->crc;
 }
 
 void KeyCachingFilter::encode(Message* msg) {  // key_caching.h:9-34
@@ -128,10 +130,13 @@ void FixingFloatFilter::convert(Message* msg, bool encode) {  // fixing_float.h:
     return;
   }
 
-  // encode, fixing_float.h:50-88; side-info comes back through the slots
+  // encode, fixing_float.h:50-88.  Computed min/max (and the CHECK_GT(bin,0)
+  // outcome) are published by workgroup 0 of each encode kernel to a
+  // host-mapped slot as soon as it has folded the partials; the FilterConfig is
+  // filled from there while the rest of the grid is still streaming.
   for (size_t base = 0; base < jobs.size(); base += Context::kSlots) {
     const size_t end = std::min(jobs.size(), base + (size_t)Context::kSlots);
-    bool need_fetch = false;
+    std::vector<uint32_t> tickets(end - base, 0);
     for (size_t q = base; q < end; ++q) {
       Job& j = jobs[q];
       const size_t vsz = j.type == kFloat ? 4 : 8;
@@ -139,24 +144,26 @@ void FixingFloatFilter::convert(Message* msg, bool encode) {  // fixing_float.h:
       j.elems = j.in.bytes / vsz;
       if (j.elems == 0) throw CheckError(kErrArg, "value array shorter than one element");
       FixedPoint preset{j.fp->has_min, j.fp->has_max, j.fp->min_value, j.fp->max_value};
+      PubSlot* pub = nullptr;
       if (preset.has_min && preset.has_max) {
         if (!((double)preset.max_value - (double)preset.min_value > 0))
           throw CheckError(kErrBin, "CHECK_GT(bin, 0)");
       } else {
-        need_fetch = true;
+        tickets[q - base] = ctx_->next_ticket();
+        pub = ctx_->pub_dev((int)(q - base));
       }
       j.out = ctx_->alloc(j.elems * (size_t)nb);
-      Slot* slot = ctx_->d_slots() + (q - base);
       const uint32_t seed = (uint32_t)ff_clock_seed();  // `int seed = time(NULL)`, per array
       int s = ff_encode_launch(j.in.ptr, j.elems, j.type, nb, preset, seed, j.out.ptr,
-                               ctx_->partials(), slot->range, &slot->status, st, ctx_->prof());
+                               ctx_->partials(), nullptr, nullptr, st, ctx_->prof(), pub,
+                               tickets[q - base]);
       if (s != kOk) throw CheckError(s, "ff_encode launch failed");
     }
-    if (need_fetch) ctx_->fetch_slots((int)(end - base));
     for (size_t q = base; q < end; ++q) {
       Job& j = jobs[q];
-      if (need_fetch) {
-        const Slot& hs = ctx_->h_slots()[q - base];
+      if (tickets[q - base]) {
+        ctx_->wait_ticket((int)(q - base), tickets[q - base]);
+        const Slot& hs = *ctx_->pub_host((int)(q - base));
         if (!j.fp->has_min) j.fp->set_min(hs.range[0]);
         if (!j.fp->has_max) j.fp->set_max(hs.range[1]);
         if (hs.status != kOk) throw CheckError(kErrBin, "CHECK_GT(bin, 0)");

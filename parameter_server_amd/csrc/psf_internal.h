@@ -36,6 +36,23 @@ struct FixedPoint {
   float min_value, max_value;
 };
 
+// Side-info a kernel publishes to host-mapped coherent memory as soon as it is
+// known (FIXING_FLOAT min/max + CHECK_GT(bin,0) outcome, KEY_CACHING CRC);
+// `ticket` is written last, behind a system-scope fence, so the host can act on
+// it while the rest of the kernel is still streaming.
+struct PubSlot {
+  float range[2];
+  int32_t status;
+  uint32_t crc;
+  uint32_t ticket;
+  uint32_t pad[3];
+};
+
+__device__ __forceinline__ void publish_ticket(PubSlot* s, uint32_t ticket) {
+  __threadfence_system();
+  __hip_atomic_store(&s->ticket, ticket, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // Kernel launch profiler: HIP events recorded on the launch stream around
 // each kernel, plus the kernel's algorithmic HBM bytes.
 enum KernelId { kKMinmax = 0, kKEncode, kKDecode, kKCrc, kKNoise, kKSnappyCompress,
@@ -77,15 +94,21 @@ struct ProfScope {
 // ff_codec.hip
 double ff_ratio(int nb);
 int ff_grid(size_t work_items);
+// range_out/status_out: optional device pointers (async API); pub: optional
+// host-mapped slot published with `ticket` once min/max/status are known.
 int ff_encode_launch(const void* x, size_t n, int value_type, int nb, const FixedPoint& preset,
                      uint32_t seed, void* out, void* partials, float* range_out, int* status_out,
-                     hipStream_t st, Profiler* prof = nullptr);
+                     hipStream_t st, Profiler* prof = nullptr, PubSlot* pub = nullptr,
+                     uint32_t ticket = 0);
 int ff_decode_launch(const void* code, size_t n, int value_type, int nb, const float* range,
                      float mn, float mx, void* out, hipStream_t st, Profiler* prof = nullptr);
 
 // crc32c.hip: CRC32C of d[0:n) written to *out (device).  n may be any size.
+// When the message fits one workgroup (n <= kCrcSingleBlock) the result is also
+// published to `pub` with `ticket`.
+constexpr size_t kCrcSingleBlock = 8 * kBlock;
 int crc32c_launch(const void* d, size_t n, uint32_t* out, hipStream_t st,
-                  Profiler* prof = nullptr);
+                  Profiler* prof = nullptr, PubSlot* pub = nullptr, uint32_t ticket = 0);
 
 // noise.hip
 int add_noise_launch(void* d, size_t n, int value_type, float mean, float sd, void* ws,

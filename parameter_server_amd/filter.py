@@ -283,13 +283,17 @@ class RemoteNode:
         for t in msg._refs:
             self._keepalive[id(t)] = t
 
-    def roundtrip(self, rcv: "RemoteNode", tmpl: Message, iters: int, keep_last: bool = False):
-        """Native loop: encode a copy of tmpl here, deliver, decode on rcv."""
-        self._hold(tmpl)
-        rcv._hold(tmpl)
+    def roundtrip(self, rcv: "RemoteNode", tmpls, iters: int, keep_last: bool = False):
+        """Native loop: encode a copy of tmpls[i % len] here, deliver, decode on rcv."""
+        tmpls = tmpls if isinstance(tmpls, (list, tuple)) else [tmpls]
+        for t in tmpls:
+            self._hold(t)
+            rcv._hold(t)
+        arr = (C.c_void_p * len(tmpls))(*[t.h.value for t in tmpls])
         out = C.c_void_p()
-        check(lib().psf_node_roundtrip(self.h, rcv.h, tmpl.h, iters, C.byref(out) if keep_last else None))
-        return Message(_handle=out, _refs=tmpl._refs) if keep_last else None
+        check(lib().psf_node_roundtrip(self.h, rcv.h, arr, len(tmpls), iters,
+                                       C.byref(out) if keep_last else None))
+        return Message(_handle=out, _refs=tmpls[-1]._refs) if keep_last else None
 
     def encode(self, msg: Message) -> None:
         self._hold(msg)

@@ -58,6 +58,28 @@ def test_ff_random_vs_port(ctx, port, dtype, nb):
         assert dec.cpu().numpy().tobytes() == pd.tobytes()
 
 
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("nb", [1, 2, 3])
+def test_ff_quantisation_boundaries(ctx, port, dtype, nb):
+    """Values on and next to the quantisation grid, where floor() of the
+    reference's tmp flips: exercises the exact-division fallback of the HIP
+    quantiser, with preset and with computed min/max."""
+    rng = np.random.default_rng(100 + nb)
+    ratio = float(2 ** (8 * nb) - 2)
+    for mn, mx in ((-1.0, 1.0), (0.1, 0.7), (-3.5, 12.25)):
+        k = rng.integers(0, int(ratio) + 1, 20000)
+        g = (np.float64(mn) + k * ((np.float64(mx) - np.float64(mn)) / ratio)).astype(dtype)
+        x = np.concatenate([g, np.nextafter(g, dtype(np.inf)), np.nextafter(g, dtype(-np.inf)),
+                            np.array([mn, mx, mn - 1, mx + 1], dtype)]).astype(dtype)
+        xt = torch.from_numpy(x).to(DEV)
+        for preset in (True, False):
+            a, b = (mn, mx) if preset else (None, None)
+            codes, cmn, cmx = ctx.ff_encode(xt, nb, 4321, a, b)
+            st, pc, pmn, pmx = port.ff_encode(x, nb, 4321, a, b)
+            assert st == 0
+            assert np.array_equal(codes.cpu().numpy(), pc), (mn, mx, preset)
+
+
 def test_ff_unaligned_and_preset(ctx, port):
     n = 100003
     x = np.random.default_rng(3).standard_normal(n + 1).astype(np.float32)

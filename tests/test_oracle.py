@@ -87,6 +87,37 @@ def test_minmax_tie_rule(port):
     assert st == 0 and np.signbit(mn) and mn == 0.0
 
 
+def test_fast_floor_guard_is_sound():
+    """The HIP encoder skips the f64 division when d*(ratio/bin) is farther
+    than 2^-26 from an integer (ff_codec.hip quant_floor).  Check, in IEEE
+    double without FMA (numpy), that the guard never lets a floor differ from
+    the reference's floor(d / bin * ratio)."""
+    rng = np.random.default_rng(0)
+    guard = 2.0 ** -26
+    for nb in (1, 2, 3):
+        ratio = float(2 ** (8 * nb) - 2)
+        for trial in range(20):
+            lo = np.float32(rng.standard_normal() * 10.0 ** rng.integers(-3, 4))
+            hi = np.float32(lo + abs(rng.standard_normal()) * 10.0 ** rng.integers(-6, 4) + 1e-30)
+            if not hi > lo:
+                continue
+            mn, mx = np.float64(lo), np.float64(hi)
+            bin_ = mx - mn
+            x = rng.uniform(mn, mx, 200_000)
+            # adversarial: exact grid points and their float32 neighbours
+            k = rng.integers(0, int(ratio) + 1, 50_000)
+            g = (mn + k * (bin_ / ratio)).astype(np.float32).astype(np.float64)
+            x = np.concatenate([x, g, np.nextafter(g, np.inf), np.nextafter(g, -np.inf)])
+            proj = np.clip(x, mn, mx)
+            d = proj - mn
+            exact = np.floor(d / bin_ * ratio)
+            t = d * (ratio / bin_)
+            fr = t - np.floor(t)
+            fast_ok = (fr > guard) & (fr < 1 - guard)
+            assert np.array_equal(np.floor(t)[fast_ok], exact[fast_ok]), (nb, trial)
+            assert fast_ok.mean() > 0.5
+
+
 def _ref():
     import oracle
     if not os.path.exists(oracle.REF_SO):
