@@ -167,7 +167,8 @@ int psf_node_roundtrip(psf_node* snd, psf_node* rcv, const psf_message* const* t
 #define PSF_K_SNAPPY_COMPRESS 5
 #define PSF_K_SNAPPY_DECOMPRESS 6
 #define PSF_K_NUM 7
-int psf_profile_enable(psf_context* ctx, int enable);
+/* kernel_mask: bit k times kernel PSF_K_k (-1 = all, 0 = off) */
+int psf_profile_enable(psf_context* ctx, int kernel_mask);
 int psf_profile_reset(psf_context* ctx);
 /* launches, summed kernel milliseconds and summed algorithmic HBM bytes */
 int psf_profile_read(psf_context* ctx, int kernel, int64_t* launches, double* total_ms,

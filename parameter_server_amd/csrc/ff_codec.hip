@@ -324,6 +324,59 @@ __device__ __forceinline__ uint32_t quant_exact(double x, const QuantParams& q) 
   return (tmp == tmp) ? (uint32_t)floor(tmp) : 0u;
 }
 
+// Branch-free fast floor for nb <= 3; `ok` is false when the value sits in a
+// guard band (or is NaN / the bin is infinite) and needs quant_exact.
+template <typename V, int NB>
+__device__ __forceinline__ uint32_t quant_fast(V xv, const QuantParams& q, bool& ok) {
+  if (NB == 1 && sizeof(V) == 4) {
+    const float x = (float)xv;
+    const float t = (fminf(fmaxf(x, q.min_f), q.max_f) - q.min_f) * q.scale_f;
+    const float f = floorf(t);
+    const float fr = t - f;
+    ok = q.fast && fr > kGuard32 && fr < 1.0f - kGuard32;
+    return (uint32_t)f;
+  }
+  const double x = (double)xv;
+  const double t = (fmin(fmax(x, q.min_v), q.max_v) - q.min_v) * q.scale;
+  const double f = floor(t);
+  const double fr = t - f;
+  ok = q.fast && fr > kGuard64 && fr < 1.0 - kGuard64;
+  return (uint32_t)f;
+}
+
+// 4 groups x 4 values of one lane: fast floors, then one (rare) divergent
+// pass over the values that need the exact sequence.
+template <typename V, int NB>
+__device__ __forceinline__ void quant_tile(const V v[4][4], const QuantParams& q, uint32_t fl[4][4]) {
+  if (NB >= 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const double x = (double)v[u][j];
+        const double proj = x > q.max_v ? q.max_v : (x < q.min_v ? q.min_v : x);
+        fl[u][j] = (uint32_t)x86_d2u64(floor((proj - q.min_v) / q.bin * q.ratio));
+      }
+    return;
+  }
+  uint32_t slow = 0;
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bool ok;
+      fl[u][j] = quant_fast<V, NB>(v[u][j], q, ok);
+      slow |= (ok ? 0u : 1u) << (4 * u + j);
+    }
+  if (__builtin_expect(slow != 0, 0)) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (slow & (1u << (4 * u + j))) fl[u][j] = quant_exact((double)v[u][j], q);
+  }
+}
+
 template <typename V, int NB>
 __device__ __forceinline__ uint64_t quant_floor(V xv, const QuantParams& q) {
   if (NB >= 4) {  // degenerate int-shift ratios: always the exact sequence
@@ -353,7 +406,11 @@ __device__ __forceinline__ uint64_t quant_floor(V xv, const QuantParams& q) {
 // it with full-rate 24-bit multiplies.  k17[k] = affine map for k+1 steps.
 
 __device__ __forceinline__ uint32_t step17(uint32_t a, uint32_t c, uint32_t s) {
-  return (__umul24(a, s) + c) & kMask17;
+  // hipcc lowers a*s to the quarter-rate v_mul_lo_u32 even when both operands
+  // are known to fit 17 bits; v_mul_u32_u24 is full rate and exact here.
+  uint32_t r;
+  asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(s));
+  return (r + c) & kMask17;
 }
 
 template <typename V, int NB>
@@ -419,10 +476,16 @@ __global__ __launch_bounds__(kBlock) void ff_encode(const V* __restrict__ x, siz
         V v[4][4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) Vec4<V>::load(x + 4 * (gb + u * kBlock), v[u]);
+        uint32_t fl[4][4];
+        quant_tile<V, NB>(v, q, fl);
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           uint64_t r[4];
-          quant_group<V, NB>(v[u], q, su, p.k17, r);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const uint32_t sj = step17(p.k17.a[j], p.k17.c[j], su);  // s_{4g+j+1}
+            r[j] = (uint64_t)(uint32_t)(fl[u][j] + ((~sj >> 16) & 1u));
+          }
           store_codes<NB>(out, gb + u * kBlock, r);
           su = step17(p.a_lane, p.c_lane, su);
         }

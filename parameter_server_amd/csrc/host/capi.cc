@@ -318,9 +318,9 @@ int psf_node_roundtrip(psf_node* snd, psf_node* rcv, const psf_message* const* t
   });
 }
 
-int psf_profile_enable(psf_context* ctx, int enable) {
+int psf_profile_enable(psf_context* ctx, int kernel_mask) {
   if (!ctx) return PSF_ERR_ARG;
-  ctx->impl->prof()->enable(enable != 0);
+  ctx->impl->prof()->enable((uint32_t)kernel_mask);
   return PSF_OK;
 }
 int psf_profile_reset(psf_context* ctx) {

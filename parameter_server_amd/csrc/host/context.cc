@@ -5,19 +5,58 @@
 #include <time.h>
 
 #include <atomic>
+#include <unordered_map>
+#include <vector>
 
 namespace psf {
 
+// The stream plus a stream-ordered caching allocator for codec outputs.  A
+// buffer whose last reference drops goes back on a free list of its size class
+// and is handed to a later allocation on the same stream, so stream order
+// alone protects it (no per-message hipMallocAsync/hipFreeAsync packets in the
+// queue).  Shared by every Buffer the context allocates, so it outlives the
+// Context if buffers do.
 struct Context::StreamHolder {
   int device;
   hipStream_t stream;
   bool own;
+  std::mutex mu;
+  std::unordered_map<size_t, std::vector<void*>> free_lists;
+
+  StreamHolder(int d, hipStream_t s, bool o) : device(d), stream(s), own(o) {}
   ~StreamHolder() {
-    if (own) {
-      (void)hipSetDevice(device);
-      (void)hipStreamSynchronize(stream);
-      (void)hipStreamDestroy(stream);
+    (void)hipSetDevice(device);
+    (void)hipStreamSynchronize(stream);
+    for (auto& kv : free_lists)
+      for (void* p : kv.second) (void)hipFree(p);
+    if (own) (void)hipStreamDestroy(stream);
+  }
+  static size_t size_class(size_t bytes) {
+    if (bytes <= 4096) return 4096;
+    if (bytes <= (1u << 20)) {  // next power of two
+      size_t c = 8192;
+      while (c < bytes) c <<= 1;
+      return c;
     }
+    return (bytes + (1u << 20) - 1) & ~(size_t)((1u << 20) - 1);  // 1 MiB granules
+  }
+  void* get(size_t cls) {
+    {
+      std::lock_guard<std::mutex> l(mu);
+      auto it = free_lists.find(cls);
+      if (it != free_lists.end() && !it->second.empty()) {
+        void* p = it->second.back();
+        it->second.pop_back();
+        return p;
+      }
+    }
+    void* p = nullptr;
+    PSF_HIP_CHECK(hipMalloc(&p, cls));
+    return p;
+  }
+  void put(size_t cls, void* p) {
+    std::lock_guard<std::mutex> l(mu);
+    free_lists[cls].push_back(p);
   }
 };
 
@@ -28,13 +67,7 @@ Context::Context(int device, hipStream_t stream, bool own) : device_(device), st
   if (own) PSF_HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
   stream_ = stream;
   // constructed in place: a temporary StreamHolder would destroy the stream
-  holder_ = std::shared_ptr<StreamHolder>(new StreamHolder{device, stream, own});
-  // keep freed HBM in the default pool for reuse (no release at sync points)
-  hipMemPool_t pool;
-  if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
-    uint64_t thr = ~0ull;
-    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
-  }
+  holder_ = std::shared_ptr<StreamHolder>(new StreamHolder(device, stream, own));
   PSF_HIP_CHECK(hipMalloc(&d_partials_, 2 * sizeof(uint64_t) * kMaxGrid));
   PSF_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&d_slots_), sizeof(Slot) * kSlots));
   PSF_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_slots_), sizeof(Slot) * kSlots,
@@ -58,13 +91,10 @@ Buffer Context::alloc(size_t bytes) {
   b.loc = Loc::kDevice;
   if (bytes == 0) return b;
   if (device_ < 0) throw CheckError(kErrArg, "host-only context cannot hold HBM buffers");
-  void* p = nullptr;
-  PSF_HIP_CHECK(hipMallocAsync(&p, bytes, stream_));
+  const size_t cls = StreamHolder::size_class(bytes);
+  void* p = holder_->get(cls);
   auto holder = holder_;
-  b.owner = std::shared_ptr<void>(p, [holder](void* q) {
-    (void)hipSetDevice(holder->device);
-    (void)hipFreeAsync(q, holder->stream);
-  });
+  b.owner = std::shared_ptr<void>(p, [holder, cls](void* q) { holder->put(cls, q); });
   b.ptr = static_cast<uint8_t*>(p);
   return b;
 }

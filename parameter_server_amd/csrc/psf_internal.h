@@ -60,8 +60,8 @@ enum KernelId { kKMinmax = 0, kKEncode, kKDecode, kKCrc, kKNoise, kKSnappyCompre
 class Profiler {
  public:
   ~Profiler();
-  bool on() const { return on_; }
-  void enable(bool on) { on_ = on; }
+  bool on(KernelId id) const { return (mask_ >> id) & 1u; }
+  void enable(uint32_t kernel_mask) { mask_ = kernel_mask; }
   void begin(hipStream_t st);
   void end(KernelId id, hipStream_t st, double alg_bytes);
   void collect();  // waits for pending events, accumulates
@@ -73,7 +73,7 @@ class Profiler {
  private:
   struct Pending { KernelId id; hipEvent_t a, b; double bytes; };
   hipEvent_t take();
-  bool on_ = false;
+  uint32_t mask_ = 0;
   hipEvent_t cur_ = nullptr;
   Pending* pend_ = nullptr;
   int npend_ = 0, cap_ = 0;
@@ -85,7 +85,7 @@ class Profiler {
 struct ProfScope {
   Profiler* p; KernelId id; hipStream_t st; double bytes;
   ProfScope(Profiler* p_, KernelId id_, hipStream_t st_, double bytes_)
-      : p(p_ && p_->on() ? p_ : nullptr), id(id_), st(st_), bytes(bytes_) {
+      : p(p_ && p_->on(id_) ? p_ : nullptr), id(id_), st(st_), bytes(bytes_) {
     if (p) p->begin(st);
   }
   ~ProfScope() { if (p) p->end(id, st, bytes); }
