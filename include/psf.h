@@ -77,6 +77,9 @@ typedef struct psf_context psf_context;
 int psf_context_create(int device, void* stream, int own_stream, psf_context** out);
 int psf_context_destroy(psf_context* ctx);
 int psf_context_sync(psf_context* ctx);
+/* Ordered on the context's stream, then synchronous: copy `bytes` from a
+ * buffer the library returned (device or host) into host memory. */
+int psf_copy_to_host(psf_context* ctx, void* dst, const void* src, size_t bytes);
 
 /* ---- layer 1: codec kernels (device pointers, async unless noted) ------ */
 typedef struct {

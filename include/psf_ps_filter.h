@@ -1,0 +1,126 @@
+// psf_ps_filter.h -- drop-in adapter between the reference's filter plugin
+// surface and libpsf (include/psf.h).
+//
+// Header-only C++ written against the reference's own types: PS::Filter
+// (src/filter/filter.h:9-24), PS::Message (src/system/message.h:10-67),
+// PS::SArray (src/util/shared_array.h:29) and the protobuf-generated
+// FilterConfig / Task accessors (src/filter/proto/filter.proto:3-35,
+// src/system/proto/task.proto:28-39).  A maintainer adds one line to
+// Filter::create (src/filter/filter.cc:9-23), see INTEGRATION.md:
+//
+//     if (Filter* f = psf_hip::CreateFilter(conf)) return f;
+//
+// The reference's messages live in host memory (ZeroMQ frames,
+// src/system/van.cc:244-255), so this adapter is the host edge: each array is
+// staged into HBM, coded by libpsf's kernels, and the result comes back as a
+// new SArray<char> -- exactly where the reference's filter would put its output
+// (fixing_float.h:37-44).  Side-info (fixed_point min/max) is written into the
+// message's own FilterConfig as the reference does.  libpsf status codes map to
+// the reference's fatal CHECK.
+//
+// Filters adapted: FIXING_FLOAT.  KEY_CACHING on host-resident keys is 2 KiB
+// of CRC plus a hash map -- libpsf runs it on the host too -- so CreateFilter
+// returns nullptr for it (and for types libpsf does not accelerate yet) and
+// the reference's own class is used.
+#pragma once
+#include <stdint.h>
+#include <string.h>
+
+#include <mutex>
+
+#include "psf.h"
+
+namespace PS {
+namespace psf_hip {
+
+// one libpsf context (device 0, private stream) per process, created lazily
+inline psf_context* Context() {
+  static psf_context* ctx = [] {
+    psf_context* c = nullptr;
+    int st = psf_context_create(0, nullptr, 1, &c);
+    CHECK_EQ(st, PSF_OK) << "libpsf: " << psf_last_error();
+    return c;
+  }();
+  return ctx;
+}
+
+inline void Check(int st) { CHECK_EQ(st, PSF_OK) << "libpsf: " << psf_last_error(); }
+
+// FixingFloatFilter (src/filter/fixing_float.h:6-103) on MI355X.
+class FixingFloatFilter : public Filter {
+ public:
+  FixingFloatFilter() {
+    Check(psf_node_create(Context(), &node_));
+  }
+  ~FixingFloatFilter() { psf_node_destroy(node_); }
+  void encode(Message* msg) { convert(msg, true); }
+  void decode(Message* msg) { convert(msg, false); }
+
+ private:
+  void convert(Message* msg, bool encode) {
+    FilterConfig* conf = CHECK_NOTNULL(find(FilterConfig::FIXING_FLOAT, msg));
+    if (conf->num_bytes() == 0) return;
+    std::lock_guard<std::mutex> l(mu_);
+    // Task + values as libpsf messages (host buffers, not copied)
+    psf_message* m = nullptr;
+    const Task& t = msg->task;
+    Check(psf_msg_create(t.request(), t.has_param(), t.has_param() && t.param().push(),
+                         t.key_channel(), t.has_key_range(), t.key_range().begin(),
+                         t.key_range().end(), &m));
+    for (size_t i = 0; i < msg->value.size(); ++i) {
+      int vt = i < (size_t)t.value_type_size() ? (int)t.value_type(i) : 0;
+      Check(psf_msg_add_value(m, msg->value[i].data(), msg->value[i].size(), vt, PSF_LOC_HOST));
+    }
+    int fi = psf_msg_add_filter(m, PSF_FIXING_FLOAT);
+    Check(fi < 0 ? fi : PSF_OK);
+    Check(psf_fc_set_num_bytes(m, fi, conf->num_bytes()));
+    for (int k = 0; k < conf->fixed_point_size(); ++k) {
+      const auto& f = conf->fixed_point(k);
+      psf_fixed_point p = {f.has_min_value(), f.has_max_value(), f.min_value(), f.max_value()};
+      Check(psf_fc_add_fixed_point(m, fi, &p));
+    }
+    const int st = encode ? psf_node_encode(node_, m) : psf_node_decode(node_, m);
+    if (st != PSF_OK) {
+      std::string err = psf_last_error();
+      psf_msg_destroy(m);
+      CHECK(false) << "libpsf FIXING_FLOAT: " << err;
+    }
+    // outputs back into the reference's message (new SArray<char>, as
+    // fixing_float.h:37-44 replaces msg->value[i])
+    for (size_t i = 0; i < msg->value.size(); ++i) {
+      void* p = nullptr;
+      size_t bytes = 0;
+      int loc = 0;
+      Check(psf_msg_value(m, (int)i, &p, &bytes, &loc));
+      if (p == msg->value[i].data() && bytes == msg->value[i].size()) continue;  // untouched
+      SArray<char> out(bytes);
+      Check(psf_copy_to_host(Context(), out.data(), p, bytes));
+      msg->value[i] = out;
+    }
+    // side-info: the fixed_point list as libpsf left it
+    const int nfp = psf_fc_num_fixed_point(m, fi);
+    for (int k = 0; k < nfp; ++k) {
+      psf_fixed_point p;
+      Check(psf_fc_fixed_point(m, fi, k, &p));
+      auto* f = k < conf->fixed_point_size() ? conf->mutable_fixed_point(k) : conf->add_fixed_point();
+      if (p.has_min) f->set_min_value(p.min_value);
+      if (p.has_max) f->set_max_value(p.max_value);
+    }
+    psf_msg_destroy(m);
+  }
+
+  psf_node* node_ = nullptr;
+  std::mutex mu_;
+};
+
+// Registration hook for Filter::create (filter.cc:9-23): a libpsf filter, or
+// nullptr to fall through to the reference's own switch.
+inline Filter* CreateFilter(const FilterConfig& conf) {
+  switch (conf.type()) {
+    case FilterConfig::FIXING_FLOAT: return new FixingFloatFilter();
+    default: return nullptr;
+  }
+}
+
+}  // namespace psf_hip
+}  // namespace PS

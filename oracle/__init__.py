@@ -40,6 +40,8 @@ def build(ref: bool | None = None) -> None:
         ref = os.path.isdir("/root/reference/src/filter")
     if ref:
         subprocess.check_call(["make", "-s", "-C", HERE, "ref"])
+        if os.path.exists(os.path.join(os.path.dirname(HERE), "parameter_server_amd", "libpsf.so")):
+            subprocess.check_call(["make", "-s", "-C", HERE, "adapter"])
 
 
 def _np_dtype(dt: int):

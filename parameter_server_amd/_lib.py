@@ -46,6 +46,7 @@ SIGNATURES = {
     "psf_context_create": ([C.c_int, vp, C.c_int, C.POINTER(vp)], C.c_int),
     "psf_context_destroy": ([vp], C.c_int),
     "psf_context_sync": ([vp], C.c_int),
+    "psf_copy_to_host": ([vp, vp, vp, sz], C.c_int),
     "psf_ff_encode": ([vp, vp, sz, C.c_int, C.c_int, C.POINTER(FixedPoint), i32, vp], C.c_int),
     "psf_ff_encode_async": ([vp, vp, sz, C.c_int, C.c_int, C.POINTER(FixedPoint), i32, vp, vp, vp], C.c_int),
     "psf_ff_decode": ([vp, vp, sz, C.c_int, C.c_int, C.c_float, C.c_float, vp], C.c_int),

@@ -1,6 +1,8 @@
 // extern "C" boundary of libpsf (include/psf.h).
 #include "../../../include/psf.h"
 
+#include <string.h>
+
 #include <string>
 
 #include "filter.h"
@@ -62,6 +64,17 @@ int psf_context_destroy(psf_context* ctx) {
 }
 int psf_context_sync(psf_context* ctx) {
   return guarded([&] { ctx->impl->sync(); return PSF_OK; });
+}
+int psf_copy_to_host(psf_context* ctx, void* dst, const void* src, size_t bytes) {
+  return guarded([&] {
+    if (!ctx || (bytes && (!dst || !src))) return PSF_ERR_ARG;
+    if (bytes == 0) return PSF_OK;
+    psf::Context& c = *ctx->impl;
+    if (c.device() < 0) { memcpy(dst, src, bytes); return PSF_OK; }
+    PSF_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, c.stream()));
+    c.sync();
+    return PSF_OK;
+  });
 }
 
 // ---------------------------------------------------------------- kernels
