@@ -128,6 +128,22 @@ Buffer Context::to_device(const Buffer& b) {
   return d;
 }
 
+const void* Context::noise_table(int value_type, size_t n) {
+  if (device_ < 0) throw CheckError(kErrArg, "host-only context has no device workspace");
+  Buffer& t = value_type == kFloat ? noise_f32_ : noise_f64_;
+  const size_t vsz = value_type == kFloat ? 4 : 8;
+  if (t.bytes / vsz >= n) return t.ptr;
+  size_t len = t.bytes / vsz * 2;
+  if (len < n) len = n;
+  if (len < (1u << 16)) len = 1u << 16;
+  Buffer nt = alloc(len * vsz);
+  Buffer scratch = alloc(noise_scratch_bytes(len));
+  int s = noise_build_table(value_type, nt.ptr, len, scratch.ptr, scratch.bytes, stream_, &prof_);
+  if (s != kOk) throw CheckError(s, "NOISE table build failed");
+  t = nt;
+  return t.ptr;
+}
+
 // ------------------------------------------------------------ clock ------
 static std::atomic<bool> g_clock_override{false};
 static std::atomic<int64_t> g_clock_value{0};

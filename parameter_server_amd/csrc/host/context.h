@@ -54,6 +54,8 @@ class Context {
   void sync();
   // stage a host buffer into HBM (used at the host edge)
   Buffer to_device(const Buffer& b);
+  // NOISE: device table of the reference engine's standard normals, >= n long
+  const void* noise_table(int value_type, size_t n);
 
   std::mutex& mu() { return mu_; }
   Profiler* prof() { return &prof_; }
@@ -69,6 +71,7 @@ class Context {
   Slot* h_slots_ = nullptr;
   Slot* m_slots_ = nullptr;
   uint32_t ticket_ = 0;
+  Buffer noise_f32_, noise_f64_;
   std::mutex mu_;
 };
 

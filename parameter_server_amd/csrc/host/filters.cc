@@ -184,9 +184,31 @@ void CompressingFilter::decode(Message* msg) {
 }
 
 // --------------------------------------------------------------- NOISE ----
-void AddNoiseFilter::encode(Message* msg) {
-  if (!find(FilterConfig::NOISE, msg)) throw CheckError(kErrCheck, "CHECK_NOTNULL(find(NOISE))");
-  throw CheckError(kErrUnsupported, "NOISE: not built yet");
+void AddNoiseFilter::encode(Message* msg) {  // add_noise.h:11-25
+  FilterConfig* conf = find(FilterConfig::NOISE, msg);
+  if (!conf) throw CheckError(kErrCheck, "CHECK_NOTNULL(find(NOISE))");
+  const int n = (int)msg->value.size();
+  if (n != (int)msg->task.value_type.size())
+    throw CheckError(kErrCheck, "CHECK_EQ(value.size(), value_type_size())");
+  hipStream_t st = ctx_->stream();
+  for (int i = 0; i < n; ++i) {
+    Buffer& v = msg->value[i];
+    if (v.empty()) continue;
+    const int type = msg->task.value_type[i];
+    if (type != kFloat && type != kDouble) continue;
+    const size_t elems = v.bytes / (type == kFloat ? 4 : 8);
+    if (elems == 0) continue;
+    const void* z = ctx_->noise_table(type, elems);
+    // in place on the caller's buffer, as the reference (add_noise.h:33-37)
+    Buffer d = ctx_->to_device(v);
+    int s = noise_apply_launch(d.ptr, z, elems, type, conf->mean, conf->std, st, ctx_->prof());
+    if (s != kOk) throw CheckError(s, "noise launch failed");
+    if (v.loc == Loc::kHost) {
+      PSF_HIP_CHECK(hipMemcpyAsync(v.ptr, d.ptr, elems * (type == kFloat ? 4 : 8),
+                                   hipMemcpyDeviceToHost, st));
+      ctx_->sync();
+    }
+  }
 }
 
 // ---------------------------------------------------------- RemoteNode ----

@@ -110,8 +110,12 @@ constexpr size_t kCrcSingleBlock = 8 * kBlock;
 int crc32c_launch(const void* d, size_t n, uint32_t* out, hipStream_t st,
                   Profiler* prof = nullptr, PubSlot* pub = nullptr, uint32_t ticket = 0);
 
-// noise.hip
-int add_noise_launch(void* d, size_t n, int value_type, float mean, float sd, void* ws,
-                     size_t ws_bytes, hipStream_t st);
+// noise.hip: the standard-normal sequence of add_noise.h's default-seeded
+// engine (built once, on the device) and the per-message in-place apply.
+size_t noise_scratch_bytes(uint64_t nz);
+int noise_build_table(int value_type, void* z, uint64_t nz, void* scratch, size_t scratch_bytes,
+                      hipStream_t st, Profiler* prof = nullptr);
+int noise_apply_launch(void* v, const void* z, size_t n, int value_type, float mean, float sd,
+                       hipStream_t st, Profiler* prof = nullptr);
 
 }  // namespace psf

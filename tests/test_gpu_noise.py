@@ -1,0 +1,96 @@
+"""GPU parity for NOISE (add_noise.h:11-39) through the message path.
+
+The engine draws, uniforms, polar coordinates and acceptance decisions are
+exact IEEE operations reproduced bit for bit, and f32 uses glibc's own logf
+algorithm, so f32 NOISE must be bit-identical to the reference.  f64 uses the
+device's double log, which may differ from glibc's log in the last bit: the
+tolerance written here is >= 95 % bit-identical (measured ~98.8 %) and every
+value within 4 ulp of the z * std term."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+def _ulp_diff(a, b):
+    a = np.ascontiguousarray(a)
+    b = np.ascontiguousarray(b)
+    it = np.int32 if a.dtype == np.float32 else np.int64
+    ai, bi = a.view(it).astype(np.int64), b.view(it).astype(np.int64)
+    return np.abs(ai - bi)
+
+
+def _noise_via_node(ctx, x, mean, sd):
+    from parameter_server_amd import NOISE
+    from parameter_server_amd import filter as F
+    node = F.RemoteNode(ctx)
+    t = torch.from_numpy(x.copy()).cuda()
+    m = F.Message(request=True, push=True)
+    m.add_value(t)
+    m.add_filter(NOISE, noise=(mean, sd))
+    node.encode(m)
+    ctx.sync()
+    return t.cpu().numpy()  # in place on the caller's buffer, as the reference
+
+
+def _check(got, want, x, mean=0.0):
+    """f32: bit-identical (the kernel uses glibc's own logf algorithm).
+    f64: >= 95 % bit-identical, the rest within 4 ulp of z*std (a 1-ulp log
+    difference moves mult by <= 1 ulp and z = y*mult by <= 2)."""
+    d = _ulp_diff(got, want)
+    exact = float((d == 0).mean())
+    if want.dtype == np.float32:
+        assert exact == 1.0, exact
+        return
+    # device log(double) differs from glibc's log in the last bit on ~2.7 % of
+    # inputs (tools/debug_ops64.hip); each accepted attempt yields 2 values
+    assert exact >= 0.95, exact
+    noise = want.astype(np.float64) - x.astype(np.float64)
+    zsd = np.abs(noise - mean)  # |z * std|: where a last-bit difference in z lands
+    tol = 4 * (np.spacing(zsd.astype(want.dtype)).astype(np.float64) +
+               np.spacing(np.abs(noise).astype(want.dtype)).astype(np.float64) +
+               np.spacing(np.abs(want)).astype(np.float64))
+    err = np.abs(got.astype(np.float64) - want.astype(np.float64))
+    assert (err <= tol).all(), float((err / np.maximum(tol, 1e-300)).max())
+
+
+def test_noise_golden(ctx):
+    g = np.load(os.path.join(GOLDEN, "noise.npz"))
+    for tag in ("f32", "f64"):
+        for j in range(3):
+            mean, sd = g[f"{tag}_{j}_param"]
+            x = g[f"{tag}_{j}_in"]
+            got = _noise_via_node(ctx, x, float(mean), float(sd))
+            _check(got, g[f"{tag}_{j}_out"], x, float(mean))
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_noise_large_vs_port(ctx, port, dtype):
+    n = (1 << 21) + 7
+    x = np.random.default_rng(5).standard_normal(n).astype(dtype)
+    got = _noise_via_node(ctx, x, 0.5, 3.0)
+    want = port.add_noise(x, 0.5, 3.0)
+    _check(got, want, x, 0.5)
+    # a second, shorter array reuses the cached sequence prefix
+    got2 = _noise_via_node(ctx, x[:1000], -1.0, 0.25)
+    _check(got2, port.add_noise(x[:1000], -1.0, 0.25), x[:1000], -1.0)
+
+
+def test_noise_host_buffer(port):
+    """Host-resident value array (host edge): staged, noised, written back in place."""
+    from parameter_server_amd import NOISE
+    from parameter_server_amd import filter as F
+    ctx = F.Context(0)
+    node = F.RemoteNode(ctx)
+    x = np.linspace(-2, 2, 4097).astype(np.float32)
+    t = torch.from_numpy(x.copy())
+    m = F.Message()
+    m.add_value(t)
+    m.add_filter(NOISE, noise=(0.0, 1.0))
+    node.encode(m)
+    _check(t.numpy(), port.add_noise(x, 0.0, 1.0), x)

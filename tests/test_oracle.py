@@ -118,6 +118,20 @@ def test_fast_floor_guard_is_sound():
             assert fast_ok.mean() > 0.5
 
 
+def test_noise_logf_matches_libm():
+    """The NOISE kernel's logf (csrc/glibc_logf.h) equals this libm's logf
+    (the reference's std::log(float)); exhaustive check: run logf_check
+    without arguments."""
+    import subprocess
+
+    import oracle
+    exe = os.path.join(oracle.HERE, "_port", "logf_check")
+    if not os.path.exists(exe):
+        oracle.build(ref=False)
+    out = subprocess.run([exe, "3000000"], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout
+
+
 def _ref():
     import oracle
     if not os.path.exists(oracle.REF_SO):
