@@ -153,6 +153,21 @@ int psf_fc_signature(const psf_message* msg, int idx, int* has_signature, uint32
 int psf_fc_num_uncompressed(const psf_message* msg, int idx);
 int psf_fc_uncompressed(const psf_message* msg, int idx, int i, uint64_t* size);
 
+/* ---- key-range partition and slicing (multi-server / multi-GPU split) --
+ * Range<Key>::EvenDivide(n, i) (src/util/range.h:100-107): the i-th of n
+ * server ranges of [begin, end), computed in long double as the reference. */
+int psf_range_even_divide(uint64_t begin, uint64_t end, uint64_t n, uint64_t i,
+                          uint64_t* out_begin, uint64_t* out_end);
+/* SliceKOFVMessage<K> (src/system/message.h:107-147): split `msg` (sorted keys
+ * of key_bytes = sizeof(K), 8 or 4) at the contiguous ranges
+ * [bounds[i], bounds[i+1]), i < nranges.  outs[i] receives a new message
+ * (the original Task, zero-copy key/value segments; free with
+ * psf_msg_destroy) and valid[i] = 0 when range i misses the message's key
+ * range (the reference does not send those).  Device keys: lower_bound runs
+ * on the GPU. */
+int psf_msg_slice(psf_context* ctx, const psf_message* msg, const uint64_t* bounds, int nranges,
+                  int key_bytes, psf_message** outs, int* valid);
+
 /* Message path driver (what Executor::Submit -> remote peer -> PickActiveMsg
  * does per message, executor.cc:131-146,178-219): for i in [0, iters), encode
  * a fresh copy of tmpls[i % ntmpl] on `snd`, deliver it (Task copy + zero-copy

@@ -6,6 +6,7 @@
 #include <string>
 
 #include "filter.h"
+#include "slice.h"
 
 struct psf_context { psf::Context* impl; };
 struct psf_node { psf::RemoteNode* impl; };
@@ -314,6 +315,33 @@ int psf_fc_signature(const psf_message* msg, int idx, int* has_signature, uint32
 int psf_fc_num_uncompressed(const psf_message* msg, int idx) {
   return guarded([&] { return (int)fc_at(msg, idx)->uncompressed_size.size(); });
 }
+int psf_range_even_divide(uint64_t begin, uint64_t end, uint64_t n, uint64_t i,
+                          uint64_t* out_begin, uint64_t* out_end) {
+  return guarded([&] {
+    psf::KeyRange r = psf::even_divide(psf::KeyRange{begin, end}, n, i);
+    if (out_begin) *out_begin = r.begin;
+    if (out_end) *out_end = r.end;
+    return PSF_OK;
+  });
+}
+
+int psf_msg_slice(psf_context* ctx, const psf_message* msg, const uint64_t* bounds, int nranges,
+                  int key_bytes, psf_message** outs, int* valid) {
+  return guarded([&] {
+    if (!ctx || !msg || nranges < 0 || (nranges && (!bounds || !outs || !valid))) return PSF_ERR_ARG;
+    std::vector<psf::KeyRange> krs(nranges);
+    for (int i = 0; i < nranges; ++i) krs[i] = psf::KeyRange{bounds[i], bounds[i + 1]};
+    std::vector<psf::Message> parts;
+    std::vector<bool> ok;
+    psf::slice_message(ctx->impl, msg->m, krs, key_bytes, &parts, &ok);
+    for (int i = 0; i < nranges; ++i) {
+      outs[i] = new psf_message{parts[i]};
+      valid[i] = ok[i] ? 1 : 0;
+    }
+    return PSF_OK;
+  });
+}
+
 int psf_node_roundtrip(psf_node* snd, psf_node* rcv, const psf_message* const* tmpls, int ntmpl,
                        int iters, psf_message** out) {
   return guarded([&] {

@@ -1,0 +1,106 @@
+"""The multi-GPU split of the filter path.
+
+GPU g is server g and owns Range<Key>(key_start, key_end).EvenDivide(N, g)
+(src/system/assigner.h:17-28, src/util/range.h:100-107).  A push/pull message
+is sliced at those ranges (SliceKOFVMessage, src/system/message.h:107-147),
+each slice is encoded by the sender's per-peer RemoteNode (executor.cc:131-146)
+and delivered to its owner, where the owner's RemoteNode decodes it.
+
+The only data-path collective is the cross-range spill: slices whose owner is
+another GPU travel in one all-to-all-v per step (RCCL over xGMI with the
+"nccl" backend; gloo for the CPU tests).  What travels is the ENCODED slice --
+the reference's wire frames [Task][key][value...] (van.cc:122-191) -- so
+KEY_CACHING hits and FIXING_FLOAT's 4x shrink cut the xGMI bytes too.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Optional, Sequence
+
+import torch
+
+from ._lib import check, lib
+
+KEY_ALL = (0, (1 << 64) - 1)  # Range<Key>::All(), range.h:92-95
+
+
+def even_divide(key_range, n: int, i: int):
+    """Range<Key>(key_range).EvenDivide(n, i), exactly (long double)."""
+    b, e = C.c_uint64(), C.c_uint64()
+    check(lib().psf_range_even_divide(key_range[0], key_range[1], n, i, C.byref(b), C.byref(e)))
+    return b.value, e.value
+
+
+def server_ranges(nservers: int, key_range=KEY_ALL):
+    """The key ranges of servers 0..nservers-1 (manager.cc:36-37 + assigner.h:21)."""
+    return [even_divide(key_range, nservers, g) for g in range(nservers)]
+
+
+def slice_message(ctx, msg, ranges: Sequence, key_bytes: int = 8):
+    """SliceKOFVMessage: returns one Message per range, or None where the range
+    misses the message's key range (the reference marks those invalid and
+    does not send them)."""
+    from .filter import Message
+    n = len(ranges)
+    for i in range(1, n):
+        if ranges[i - 1][1] != ranges[i][0]:
+            raise ValueError("ranges must be contiguous (message.h:120)")
+    bounds = (C.c_uint64 * (n + 1))(*([r[0] for r in ranges[:1]] + [r[1] for r in ranges]))
+    outs = (C.c_void_p * n)()
+    valid = (C.c_int * n)()
+    check(lib().psf_msg_slice(ctx.h, msg.h, bounds, n, key_bytes, outs, valid))
+    res: List[Optional[Message]] = []
+    for i in range(n):
+        m = Message(_handle=C.c_void_p(outs[i]), _refs=msg._refs)
+        res.append(m if valid[i] else None)
+    return res
+
+
+class SpillExchange:
+    """All-to-all-v of byte frames between ranks (one collective per step).
+
+    send[dst] is a list of uint8 tensors (frames) for rank dst; the result
+    recv[src] is the list of frames rank src sent here, in order.  Frame
+    lengths travel first (one small all-to-all), then all bytes in one
+    all_to_all_single with per-peer split sizes."""
+
+    def __init__(self, group=None, device=None):
+        import torch.distributed as dist
+        self.dist = dist
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.device = device
+
+    def exchange(self, send: List[List[torch.Tensor]]) -> List[List[torch.Tensor]]:
+        dist, W = self.dist, self.world
+        dev = self.device if self.device is not None else "cpu"
+        counts = torch.tensor([len(f) for f in send], dtype=torch.int64, device=dev)
+        counts_in = torch.empty_like(counts)
+        dist.all_to_all_single(counts_in, counts, group=self.group)
+        # every rank must use the same row width for the lens all-to-all
+        maxf_t = torch.tensor([max(1, int(counts.max()))], dtype=torch.int64, device=dev)
+        dist.all_reduce(maxf_t, op=dist.ReduceOp.MAX, group=self.group)
+        maxf = int(maxf_t.item())
+        lens = torch.zeros(W, maxf, dtype=torch.int64, device=dev)
+        for d, frames in enumerate(send):
+            for j, f in enumerate(frames):
+                lens[d, j] = f.numel()
+        lens_in = torch.empty_like(lens)
+        dist.all_to_all_single(lens_in.view(-1), lens.view(-1), group=self.group)
+        in_splits = [int(lens[d].sum()) for d in range(W)]
+        out_splits = [int(lens_in[s].sum()) for s in range(W)]
+        flat = [f.reshape(-1) for frames in send for f in frames]
+        sendbuf = torch.cat(flat) if flat else torch.empty(0, dtype=torch.uint8, device=dev)
+        recvbuf = torch.empty(sum(out_splits), dtype=torch.uint8, device=dev)
+        dist.all_to_all_single(recvbuf, sendbuf, out_splits, in_splits, group=self.group)
+        recv, off = [], 0
+        counts_l = counts_in.tolist()
+        lens_l = lens_in.tolist()
+        for s in range(W):
+            frames = []
+            for j in range(counts_l[s]):
+                ln = lens_l[s][j]
+                frames.append(recvbuf[off:off + ln])
+                off += ln
+            recv.append(frames)
+        return recv

@@ -13,6 +13,7 @@ disagreement aborts.  The fixtures are data only (inputs + expected outputs):
   snappy.npz                     snappy 1.1.8 RawCompress outputs (COMPRESSING)
   scenarios.json                 message-sequence records (KEY_CACHING, chain,
                                  FIXING_FLOAT message rules) from tests/scenarios.py
+  even_divide.json               Range<Key>::EvenDivide server ranges (range.h)
 """
 from __future__ import annotations
 
@@ -164,6 +165,32 @@ def gen_snappy(R):
     print(f"snappy: {len(inputs)} vectors (snappy 1.1.8)")
 
 
+def gen_even_divide():
+    """Range<Key>::EvenDivide from the reference's own range.h
+    (oracle/_ref/libpsrange.so), checked against oracle/slicing.py."""
+    import ctypes as C
+
+    from oracle import slicing
+    L = C.CDLL(os.path.join(ROOT, "oracle", "_ref", "libpsrange.so"))
+    L.psref_even_divide.argtypes = [C.c_uint64] * 4 + [C.POINTER(C.c_uint64)] * 2
+    rng = np.random.default_rng(9)
+    spaces = [(0, (1 << 64) - 1), (0, 10**9), (5, 5 + 7), (123456789, 1 << 63), ((1 << 64) - 1000, (1 << 64) - 1)]
+    for _ in range(20):
+        a, b = sorted(int(v) for v in rng.integers(0, 2**63, 2, dtype=np.uint64))
+        spaces.append((a, b * 2))
+    rows = []
+    for (b, e) in spaces:
+        for n in (1, 2, 3, 4, 5, 7, 8, 16, 64):
+            for i in range(n):
+                ob, oe = C.c_uint64(), C.c_uint64()
+                assert L.psref_even_divide(b, e, n, i, C.byref(ob), C.byref(oe)) == 0
+                assert slicing.even_divide(b, e, n, i) == (ob.value, oe.value), (b, e, n, i)
+                rows.append([str(b), str(e), n, i, str(ob.value), str(oe.value)])
+    with open(os.path.join(HERE, "even_divide.json"), "w") as f:
+        json.dump(rows, f)
+    print(f"even_divide: {len(rows)} rows")
+
+
 def gen_scenarios(R):
     impl = scenarios.RefImpl(R)
     out = {
@@ -184,6 +211,7 @@ def main():
     gen_noise(R, P)
     gen_snappy(R)
     gen_scenarios(R)
+    gen_even_divide()
 
 
 if __name__ == "__main__":

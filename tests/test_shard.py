@@ -1,0 +1,123 @@
+"""CPU: the multi-server / multi-GPU split.
+
+* Range<Key>::EvenDivide in libpsf == the reference's own range.h (fixture)
+* SliceKOFVMessage in libpsf (host keys) == the numpy restatement
+* the all-to-all-v spill exchange over world_size 2 with gloo
+"""
+import json
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+
+def test_even_divide_matches_reference_fixture():
+    from oracle import slicing
+    from parameter_server_amd import shard
+    rows = json.load(open(os.path.join(GOLDEN, "even_divide.json")))
+    assert len(rows) > 2000
+    for b, e, n, i, ob, oe in rows:
+        want = (int(ob), int(oe))
+        assert shard.even_divide((int(b), int(e)), n, i) == want
+        assert slicing.even_divide(int(b), int(e), n, i) == want
+    # the reference's defect is reproduced: 7 servers over Range::All()
+    assert shard.even_divide(shard.KEY_ALL, 7, 6)[1] == 0
+
+
+def _keys(n, seed, hi=1 << 64):
+    rng = np.random.default_rng(seed)
+    k = np.unique(rng.integers(0, hi - 1, size=n + 64, dtype=np.uint64))[:n]
+    return k
+
+
+@pytest.mark.parametrize("nserv", [1, 2, 3, 7, 8])
+@pytest.mark.parametrize("mrange", ["all", "part", "narrow"])
+def test_slice_host_keys_matches_restatement(nserv, mrange):
+    from oracle import slicing
+    from parameter_server_amd import filter as F
+    from parameter_server_amd import shard
+    keys = _keys(5000, nserv)
+    v1 = np.random.default_rng(1).standard_normal(keys.size).astype(np.float32)
+    v3 = np.random.default_rng(2).standard_normal(keys.size * 3).astype(np.float32)  # dim 3 rows
+    mr = {"all": shard.KEY_ALL, "part": (int(keys[100]), int(keys[4000])),
+          "narrow": (int(keys[10]), int(keys[12]))}[mrange]
+    ctx = F.HostContext()
+    m = F.Message(request=True, push=True, key_range=mr)
+    m.set_key(torch.from_numpy(keys.view(np.int64).copy()))
+    m.add_value(torch.from_numpy(v1))
+    m.add_value(torch.from_numpy(v3))
+    ranges = shard.server_ranges(nserv)
+    if nserv == 7:
+        ranges[-1] = (ranges[-1][0], (1 << 64) - 1)  # contiguous stand-in for the end=0 defect
+    parts = shard.slice_message(ctx, m, ranges)
+    want = slicing.slice_kofv(keys, [v1, v3], mr, ranges)
+    assert len(parts) == len(want) == nserv
+    total = 0
+    for p, w in zip(parts, want):
+        if w is None:
+            assert p is None
+            continue
+        assert p is not None
+        ptr, nb, loc = p.key_ptr()
+        got = np.ctypeslib.as_array((np.ctypeslib.ctypes.c_uint8 * nb).from_address(ptr)) if nb else np.zeros(0, np.uint8)
+        assert got.tobytes() == w[0].tobytes()
+        total += w[0].size
+        for j, wv in enumerate(w[1]):
+            vp, vb, _ = p.value_ptr(j)
+            gv = np.ctypeslib.as_array((np.ctypeslib.ctypes.c_uint8 * vb).from_address(vp)) if vb else np.zeros(0, np.uint8)
+            assert gv.tobytes() == wv.tobytes()
+        assert p.key_info()[1] == 8  # key_type = UINT64 (EncodeType<K>)
+    if mrange == "all":
+        assert total == keys.size
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _exchange_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    from parameter_server_amd.shard import SpillExchange
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ex = SpillExchange()
+        send = []
+        for d in range(world):
+            frames = [torch.full((10 * rank + d + j,), 16 * rank + d, dtype=torch.uint8) for j in range(d + 1)]
+            if rank == 0 and d == 1:
+                frames = []  # a peer with nothing to send
+            send.append(frames)
+        recv = ex.exchange(send)
+        ok = True
+        for s in range(world):
+            exp = 0 if (s == 0 and rank == 1) else rank + 1
+            ok &= len(recv[s]) == exp
+            for j, f in enumerate(recv[s]):
+                ok &= f.numel() == 10 * s + rank + j and bool((f == 16 * s + rank).all())
+        q.put((rank, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_spill_exchange_gloo_world2():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_exchange_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: True, 1: True}
