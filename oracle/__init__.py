@@ -52,6 +52,20 @@ def _ptr(a: np.ndarray):
     return a.ctypes.data_as(C.c_void_p)
 
 
+def _uncompress(fn, b, cap):
+    a = np.frombuffer(bytes(b) + b"\0", dtype=np.uint8)  # never hand out a NULL pointer
+    n = C.c_size_t(0)
+    hdr = np.empty(0, np.uint8)
+    st = fn(_ptr(a), a.size - 1, _ptr(hdr), 0, C.byref(n))
+    if st != -2:
+        return st, b""
+    if n.value > cap:
+        return -2, b""
+    out = np.empty(max(n.value, 1), dtype=np.uint8)
+    st = fn(_ptr(a), a.size - 1, _ptr(out), n.value, C.byref(n))
+    return st, (out[:n.value].tobytes() if st == 0 else b"")
+
+
 class Port:
     """ctypes view of oracle/psf_port.c."""
 
@@ -76,6 +90,11 @@ class Port:
         L.port_lcg_state.restype = C.c_uint32
         L.port_add_noise.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.c_float, C.c_float]
         L.port_add_noise.restype = C.c_int
+        L.port_snappy_compress.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p]
+        L.port_snappy_compress.restype = C.c_size_t
+        L.port_snappy_uncompress.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
+                                             C.POINTER(C.c_size_t)]
+        L.port_snappy_uncompress.restype = C.c_int
 
     def ff_encode(self, x: np.ndarray, nb: int, seed: int, mn=None, mx=None):
         """Returns (status, codes:uint8[n*nb], min, max)."""
@@ -116,6 +135,17 @@ class Port:
         st = self.lib.port_add_noise(_ptr(y), y.size, dt, mean, sd)
         assert st == 0
         return y
+
+    def snappy_compress(self, b) -> bytes:
+        """snappy 1.1.8 RawCompress restated (oracle/snappy_port.c)."""
+        a = np.frombuffer(bytes(b), dtype=np.uint8)
+        out = np.empty(32 + a.size + a.size // 6, dtype=np.uint8)
+        n = self.lib.port_snappy_compress(_ptr(a) if a.size else None, a.size, _ptr(out))
+        return out[:n].tobytes()
+
+    def snappy_uncompress(self, b, cap: int = 1 << 26):
+        """(status, bytes): 0 ok, -1 bad header, -2 declared length > cap, -3 bad body."""
+        return _uncompress(self.lib.port_snappy_uncompress, b, cap)
 
 
 class Ref:
@@ -162,6 +192,7 @@ class Ref:
             "psref_node_decode": ([vp, vp], C.c_int),
             "psref_snappy_max": ([sz], sz),
             "psref_snappy_compress": ([vp, sz, vp], sz),
+            "psref_snappy_uncompress": ([vp, sz, vp, sz, C.POINTER(sz)], C.c_int),
         }
         for name, (a, r) in sig.items():
             f = getattr(L, name)
@@ -181,6 +212,9 @@ class Ref:
         out = np.empty(self.lib.psref_snappy_max(a.size), dtype=np.uint8)
         n = self.lib.psref_snappy_compress(_ptr(a) if a.size else None, a.size, _ptr(out))
         return out[:n].tobytes()
+
+    def snappy_uncompress(self, b, cap: int = 1 << 26):
+        return _uncompress(self.lib.psref_snappy_uncompress, b, cap)
 
     def last_error(self) -> str:
         return self.lib.psref_last_error().decode()

@@ -192,5 +192,13 @@ size_t psref_snappy_compress(const void* src, size_t n, void* dst) {
   snappy::RawCompress(static_cast<const char*>(src), n, static_cast<char*>(dst), &out);
   return out;
 }
+// -1: GetUncompressedLength fails; -2: length > cap; -3: RawUncompress fails.
+int psref_snappy_uncompress(const void* src, size_t n, void* dst, size_t cap, size_t* out_len) {
+  size_t d = 0;
+  if (!snappy::GetUncompressedLength(static_cast<const char*>(src), n, &d)) return -1;
+  *out_len = d;
+  if (d > cap) return -2;
+  return snappy::RawUncompress(static_cast<const char*>(src), n, static_cast<char*>(dst)) ? 0 : -3;
+}
 
 }  // extern "C"

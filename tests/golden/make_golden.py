@@ -11,6 +11,8 @@ disagreement aborts.  The fixtures are data only (inputs + expected outputs):
   crc32c.npz                     CRC32C vectors
   noise.npz                      NOISE outputs (f32, f64)
   snappy.npz                     snappy 1.1.8 RawCompress outputs (COMPRESSING)
+  snappy_dec.npz                 snappy 1.1.8 RawUncompress verdicts + outputs on
+                                 valid and mutated streams
   scenarios.json                 message-sequence records (KEY_CACHING, chain,
                                  FIXING_FLOAT message rules) from tests/scenarios.py
   even_divide.json               Range<Key>::EvenDivide server ranges (range.h)
@@ -157,12 +159,65 @@ def gen_snappy(R):
         "one": b"\x00",
         "long_run_after_literal": b"xy" + bytes(70000) + b"z" * 10,
     }
+    for n in (15, 16, 4096, 65535, 65536, 65537, 131072 + 100):
+        inputs[f"keys_{n}"] = scenarios.sorted_keys(n // 8 + 1, n).tobytes()[:n]
+        if n in (15, 16, 4096, 65537):
+            inputs[f"random_{n}"] = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+    inputs["runs"] = np.repeat(rng.integers(0, 256, 3000, dtype=np.uint8), rng.integers(1, 200, 3000)).tobytes()
+    P = oracle.Port()
     arrays = {}
     for k, v in inputs.items():
+        out = R.snappy_compress(v)
+        assert P.snappy_compress(v) == out, k
         arrays[f"{k}_in"] = np.frombuffer(v, np.uint8)
-        arrays[f"{k}_out"] = np.frombuffer(R.snappy_compress(v), np.uint8)
+        arrays[f"{k}_out"] = np.frombuffer(out, np.uint8)
     np.savez_compressed(os.path.join(HERE, "snappy.npz"), **arrays)
     print(f"snappy: {len(inputs)} vectors (snappy 1.1.8)")
+    gen_snappy_malformed(R, P)
+
+
+def gen_snappy_malformed(R, P):
+    """RawUncompress verdicts of the reference's snappy on mutated streams
+    (the decoder's CHECK paths: shared_array_inl.h:236,240)."""
+    rng = np.random.default_rng(11)
+    streams, status, outs = [], [], []
+    srcs = [lambda n: rng.integers(0, 256, n, dtype=np.uint8).tobytes(),
+            lambda n: scenarios.sorted_keys(n // 8 + 1, n).tobytes()[:n],
+            lambda n: np.repeat(rng.integers(0, 4, n // 9 + 1, dtype=np.uint8), 9).tobytes()[:n]]
+    hand = [b"", b"\x80", b"\xff\xff\xff\xff\x1f", b"\xff\xff\xff\xff\x0f", b"\x05\x10abcde",
+            b"\x05\x10abcd", b"\x04\x01\x00", b"\x04\x00a\x01\x00", b"\x04\x00a\x01\x01",
+            b"\x05\x00a\x0d\x01", b"\x02\x00a", b"\x01\x04ab", b"\x03\xf0\x02\x00\x00abc",
+            b"\x0a\x00a\x0a\x01\x00", b"\x08\x00a\x12\x01\x00\x00\x00"]
+    for h in hand:
+        streams.append(h)
+    for t in range(400):
+        b = srcs[t % 3](int(rng.integers(0, 2500)))
+        r = bytearray(R.snappy_compress(b))
+        for _ in range(int(rng.integers(0, 3))):
+            if not r:
+                break
+            i, op = int(rng.integers(0, len(r))), int(rng.integers(0, 4))
+            if op == 0:
+                r[i] = int(rng.integers(0, 256))
+            elif op == 1:
+                del r[i]
+            elif op == 2:
+                r.insert(i, int(rng.integers(0, 256)))
+            else:
+                del r[i:]
+        streams.append(bytes(r))
+    for s in streams:
+        st, out = R.snappy_uncompress(s, cap=1 << 20)
+        assert (st, out) == P.snappy_uncompress(s, cap=1 << 20), s[:16]
+        status.append(st)
+        outs.append(out)
+    off = np.cumsum([0] + [len(s) for s in streams])
+    ooff = np.cumsum([0] + [len(o) for o in outs])
+    np.savez_compressed(os.path.join(HERE, "snappy_dec.npz"),
+                        data=np.frombuffer(b"".join(streams), np.uint8), offsets=off.astype(np.int64),
+                        status=np.array(status, np.int32),
+                        out=np.frombuffer(b"".join(outs), np.uint8), out_offsets=ooff.astype(np.int64))
+    print(f"snappy_dec: {len(streams)} streams, {sum(1 for s in status if s == 0)} valid")
 
 
 def gen_even_divide():

@@ -159,3 +159,48 @@ def test_reference_scenarios_stable(scenario_golden):
     R = _ref()
     got = scenarios.run(scenarios.RefImpl(R), scenarios.kc_scenario())
     assert got == scenario_golden["key_caching"]
+
+
+# ---- COMPRESSING: snappy 1.1.8 restated (oracle/snappy_port.c) -------------
+def _snappy_fixtures():
+    a = np.load(os.path.join(GOLDEN, "snappy.npz"), allow_pickle=False)
+    names = sorted(k[:-3] for k in a.files if k.endswith("_in"))
+    return [(k, a[f"{k}_in"].tobytes(), a[f"{k}_out"].tobytes()) for k in names]
+
+
+def _snappy_dec_fixtures():
+    a = np.load(os.path.join(GOLDEN, "snappy_dec.npz"), allow_pickle=False)
+    d, off, st, out, ooff = a["data"], a["offsets"], a["status"], a["out"], a["out_offsets"]
+    return [(d[off[i]:off[i + 1]].tobytes(), int(st[i]), out[ooff[i]:ooff[i + 1]].tobytes())
+            for i in range(len(st))]
+
+
+def test_snappy_port_compress_matches_1_1_8(port):
+    fx = _snappy_fixtures()
+    assert len(fx) >= 20
+    for name, x, want in fx:
+        assert port.snappy_compress(x) == want, name
+        st, back = port.snappy_uncompress(want)
+        assert st == 0 and back == x, name
+
+
+def test_snappy_port_decoder_verdicts(port):
+    fx = _snappy_dec_fixtures()
+    assert sum(1 for _, s, _ in fx if s != 0) > 100
+    for s, st, out in fx:
+        assert port.snappy_uncompress(s, cap=1 << 20) == (st, out), s[:16]
+
+
+def test_snappy_reference_random(port):
+    R = _ref()
+    rng = np.random.default_rng(123)
+    for t in range(60):
+        n = int(rng.integers(0, 200000))
+        kind = t % 3
+        if kind == 0:
+            b = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        elif kind == 1:
+            b = np.sort(rng.integers(0, 10**9, n // 8 + 1, dtype=np.uint64)).tobytes()[:n]
+        else:
+            b = np.repeat(rng.integers(0, 8, n // 5 + 1, dtype=np.uint8), 5).tobytes()[:n]
+        assert port.snappy_compress(b) == R.snappy_compress(b), (t, n)
