@@ -17,6 +17,10 @@
  *       psf_key_signature / psf_crc32c  <- KeyCachingFilter signature
  *                                          src/filter/key_caching.h:18,43
  *                                          (crc32c::Value, src/util/crc32c.h:19-21)
+ *       psf_snappy_*                    <- CompressingFilter's SArray::CompressTo /
+ *                                          UncompressFrom, src/util/shared_array_inl.h:
+ *                                          232-255 (snappy::RawCompress /
+ *                                          GetUncompressedLength / RawUncompress, 1.1.8)
  *
  *  2. Filter plugin surface -- the reference's message path in one library:
  *       psf_node_encode / psf_node_decode  <- RemoteNode::EncodeMessage / DecodeMessage
@@ -112,6 +116,19 @@ int psf_ff_decode_async(psf_context* ctx, const void* d_code, size_t n, int valu
 int psf_crc32c(psf_context* ctx, const void* d_data, size_t bytes, uint32_t* crc);
 /* KEY_CACHING signature: CRC32C of the first min(bytes, 2048) key bytes. */
 int psf_key_signature(psf_context* ctx, const void* d_keys, size_t bytes, uint32_t* sig);
+
+/* COMPRESSING codec: the snappy raw format, byte-identical to snappy 1.1.8.
+ * snappy::MaxCompressedLength(n) = 32 + n + n/6. */
+size_t psf_snappy_max_compressed_length(size_t n);
+/* snappy::RawCompress: d_out holds >= psf_snappy_max_compressed_length(n)
+ * bytes; *out_len = stream length.  Synchronous.  n < 2^32. */
+int psf_snappy_compress(psf_context* ctx, const void* d_in, size_t n, void* d_out, size_t* out_len);
+/* snappy::GetUncompressedLength: PSF_ERR_CHECK when the header is malformed. */
+int psf_snappy_uncompressed_length(psf_context* ctx, const void* d_in, size_t n, size_t* out_len);
+/* snappy::RawUncompress into d_out (out_cap >= the declared length, else
+ * PSF_ERR_ARG); PSF_ERR_CHECK when RawUncompress would return false. */
+int psf_snappy_uncompress(psf_context* ctx, const void* d_in, size_t n, void* d_out, size_t out_cap,
+                          size_t* out_len);
 
 /* ---- layer 2: messages and the filter chain ---------------------------- */
 typedef struct psf_message psf_message;

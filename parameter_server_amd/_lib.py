@@ -53,6 +53,10 @@ SIGNATURES = {
     "psf_ff_decode_async": ([vp, vp, sz, C.c_int, C.c_int, vp, vp], C.c_int),
     "psf_crc32c": ([vp, vp, sz, C.POINTER(u32)], C.c_int),
     "psf_key_signature": ([vp, vp, sz, C.POINTER(u32)], C.c_int),
+    "psf_snappy_max_compressed_length": ([sz], sz),
+    "psf_snappy_compress": ([vp, vp, sz, vp, C.POINTER(sz)], C.c_int),
+    "psf_snappy_uncompressed_length": ([vp, vp, sz, C.POINTER(sz)], C.c_int),
+    "psf_snappy_uncompress": ([vp, vp, sz, vp, sz, C.POINTER(sz)], C.c_int),
     "psf_node_create": ([vp, C.POINTER(vp)], C.c_int),
     "psf_node_destroy": ([vp], C.c_int),
     "psf_node_encode": ([vp, vp], C.c_int),

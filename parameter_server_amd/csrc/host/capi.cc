@@ -7,6 +7,7 @@
 
 #include "filter.h"
 #include "slice.h"
+#include "snappy_host.h"
 
 struct psf_context { psf::Context* impl; };
 struct psf_node { psf::RemoteNode* impl; };
@@ -157,6 +158,70 @@ int psf_key_signature(psf_context* ctx, const void* d_keys, size_t bytes, uint32
 }
 
 // ---------------------------------------------------------------- chain
+size_t psf_snappy_max_compressed_length(size_t n) { return psf::snappy_max_compressed(n); }
+
+int psf_snappy_compress(psf_context* ctx, const void* d_in, size_t n, void* d_out, size_t* out_len) {
+  return guarded([&] {
+    if (!ctx || !d_out || !out_len || (n && !d_in) || n > 0xffffffffull) return PSF_ERR_ARG;
+    psf::Context& c = *ctx->impl;
+    if (c.device() < 0) return PSF_ERR_ARG;
+    if (n == 0) {  // RawCompress of nothing: the one-byte header
+      PSF_HIP_CHECK(hipMemsetAsync(d_out, 0, 1, c.stream()));
+      PSF_HIP_CHECK(hipStreamSynchronize(c.stream()));
+      *out_len = 1;
+      return PSF_OK;
+    }
+    psf::Buffer scratch = c.alloc(psf::snappy_compress_scratch(n));
+    const uint32_t ticket = c.next_ticket();
+    int st = psf::snappy_compress_launch(d_in, n, d_out, scratch.ptr, c.stream(), c.prof(), c.pub_dev(0), ticket);
+    if (st != PSF_OK) return st;
+    c.wait_ticket(0, ticket);
+    *out_len = c.pub_host(0)->size;
+    return PSF_OK;
+  });
+}
+
+static psf::Buffer device_view(const void* p, size_t n) {
+  psf::Buffer b;
+  b.ptr = static_cast<uint8_t*>(const_cast<void*>(p));
+  b.bytes = n;
+  b.loc = psf::Loc::kDevice;
+  return b;
+}
+
+int psf_snappy_uncompressed_length(psf_context* ctx, const void* d_in, size_t n, size_t* out_len) {
+  return guarded([&] {
+    if (!ctx || !out_len || (n && !d_in)) return PSF_ERR_ARG;
+    psf::Context& c = *ctx->impl;
+    if (c.device() < 0) return PSF_ERR_ARG;
+    uint64_t d = 0;
+    if (!psf::snappy_read_header(c, device_view(d_in, n), &d)) return PSF_ERR_CHECK;
+    *out_len = d;
+    return PSF_OK;
+  });
+}
+
+int psf_snappy_uncompress(psf_context* ctx, const void* d_in, size_t n, void* d_out, size_t out_cap,
+                          size_t* out_len) {
+  return guarded([&] {
+    if (!ctx || !out_len || (n && !d_in)) return PSF_ERR_ARG;
+    psf::Context& c = *ctx->impl;
+    if (c.device() < 0) return PSF_ERR_ARG;
+    uint64_t d = 0;
+    const uint32_t hdr = psf::snappy_read_header(c, device_view(d_in, n), &d);
+    if (!hdr) return PSF_ERR_CHECK;
+    *out_len = d;
+    if (d > out_cap || (d && !d_out)) return PSF_ERR_ARG;
+    psf::Buffer scratch = c.alloc(psf::snappy_uncompress_scratch(n, d));
+    const uint32_t ticket = c.next_ticket();
+    int st = psf::snappy_uncompress_launch(d_in, n, hdr, d, d_out, scratch.ptr, c.stream(), c.prof(), c.pub_dev(0),
+                                           ticket);
+    if (st != PSF_OK) return st;
+    c.wait_ticket(0, ticket);
+    return c.pub_host(0)->status;
+  });
+}
+
 int psf_node_create(psf_context* ctx, psf_node** out) {
   return guarded([&] {
     if (!ctx || !out) return PSF_ERR_ARG;

@@ -7,6 +7,7 @@
 #include <vector>
 
 #include "filter.h"
+#include "snappy_host.h"
 
 namespace psf {
 
@@ -174,13 +175,32 @@ void FixingFloatFilter::convert(Message* msg, bool encode) {  // fixing_float.h:
 }
 
 // --------------------------------------------------------- COMPRESSING ----
-void CompressingFilter::encode(Message* msg) {
-  if (!find(FilterConfig::COMPRESSING, msg)) return;
-  throw CheckError(kErrUnsupported, "COMPRESSING: not built yet");
+void CompressingFilter::encode(Message* msg) {  // compressing.h:8-19
+  FilterConfig* conf = find(FilterConfig::COMPRESSING, msg);
+  if (!conf) return;
+  conf->uncompressed_size.clear();
+  SnappyBatch batch(*ctx_);
+  if (msg->has_key()) {
+    conf->uncompressed_size.push_back(msg->key.bytes);
+    batch.compress(msg->key, &msg->key);
+  }
+  for (auto& v : msg->value) {
+    conf->uncompressed_size.push_back(v.bytes);
+    batch.compress(v, &v);
+  }
+  batch.flush();
 }
-void CompressingFilter::decode(Message* msg) {
-  if (!find(FilterConfig::COMPRESSING, msg)) return;
-  throw CheckError(kErrUnsupported, "COMPRESSING: not built yet");
+
+void CompressingFilter::decode(Message* msg) {  // compressing.h:20-37
+  FilterConfig* conf = find(FilterConfig::COMPRESSING, msg);
+  if (!conf) return;
+  const int has_key = msg->has_key() ? 1 : 0;
+  if (conf->uncompressed_size.size() != msg->value.size() + has_key)
+    throw CheckError(kErrCheck, "CHECK_EQ(conf->uncompressed_size_size(), msg->value.size() + has_key)");
+  SnappyBatch batch(*ctx_);
+  if (has_key) batch.uncompress(msg->key, &msg->key);
+  for (auto& v : msg->value) batch.uncompress(v, &v);
+  batch.flush();
 }
 
 // --------------------------------------------------------------- NOISE ----

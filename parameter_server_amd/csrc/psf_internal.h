@@ -45,7 +45,8 @@ struct PubSlot {
   int32_t status;
   uint32_t crc;
   uint32_t ticket;
-  uint32_t pad[3];
+  uint32_t pad;
+  uint64_t size;  // COMPRESSING: stream / output length
 };
 
 __device__ __forceinline__ void publish_ticket(PubSlot* s, uint32_t ticket) {
@@ -117,5 +118,19 @@ int noise_build_table(int value_type, void* z, uint64_t nz, void* scratch, size_
                       hipStream_t st, Profiler* prof = nullptr);
 int noise_apply_launch(void* v, const void* z, size_t n, int value_type, float mean, float sd,
                        hipStream_t st, Profiler* prof = nullptr);
+
+// snappy.hip: COMPRESSING (snappy 1.1.8 raw format).  `out` holds at least
+// snappy_max_compressed(n) bytes; the stream length is published to pub->size.
+constexpr uint32_t kSnappyFragOut = 76544;  // >= MaxCompressedLength(64 KiB), 256-aligned
+size_t snappy_max_compressed(size_t n);
+size_t snappy_compress_scratch(size_t n);
+int snappy_compress_launch(const void* in, size_t n, void* out, void* scratch, hipStream_t st,
+                           Profiler* prof, PubSlot* pub, uint32_t ticket);
+// `hdr` = bytes of the varint32 header (parsed on the host), dsize = its value;
+// the verdict of RawUncompress (kOk / kErrCheck) is published to pub->status.
+size_t snappy_uncompress_scratch(size_t c, size_t dsize);
+int snappy_uncompress_launch(const void* in, size_t c, uint32_t hdr, size_t dsize, void* out,
+                             void* scratch, hipStream_t st, Profiler* prof, PubSlot* pub,
+                             uint32_t ticket);
 
 }  // namespace psf

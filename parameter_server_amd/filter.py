@@ -125,6 +125,29 @@ class Context:
                                       C.byref(v)))
         return v.value
 
+    # -- COMPRESSING codec (snappy 1.1.8 raw format) ------------------------
+    def snappy_compress(self, t: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """snappy::RawCompress of t's bytes -> uint8 tensor (a view of `out`)."""
+        n = t.numel() * t.element_size()
+        cap = lib().psf_snappy_max_compressed_length(n)
+        if out is None:
+            out = torch.empty(cap, dtype=torch.uint8, device=t.device)
+        assert out.numel() >= cap
+        ln = C.c_size_t()
+        check(lib().psf_snappy_compress(self.h, C.c_void_p(t.data_ptr()), n, C.c_void_p(out.data_ptr()),
+                                        C.byref(ln)))
+        return out[:ln.value]
+
+    def snappy_uncompress(self, s: torch.Tensor) -> torch.Tensor:
+        """snappy::RawUncompress -> uint8 tensor; PsfError(PSF_ERR_CHECK) on a bad stream."""
+        n = s.numel() * s.element_size()
+        ln = C.c_size_t()
+        check(lib().psf_snappy_uncompressed_length(self.h, C.c_void_p(s.data_ptr()), n, C.byref(ln)))
+        out = torch.empty(max(ln.value, 1), dtype=torch.uint8, device=s.device)
+        check(lib().psf_snappy_uncompress(self.h, C.c_void_p(s.data_ptr()), n, C.c_void_p(out.data_ptr()),
+                                          out.numel(), C.byref(ln)))
+        return out[:ln.value]
+
 
 class HostContext(Context):
     """Host-only context (device -1): host-resident buffers, no HIP calls.

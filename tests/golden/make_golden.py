@@ -252,6 +252,7 @@ def gen_scenarios(R):
         "key_caching": scenarios.run(impl, scenarios.kc_scenario()),
         "chain_ctr": scenarios.run(impl, scenarios.chain_scenario()),
         "ff_message": scenarios.run(impl, scenarios.ff_message_scenario()),
+        "compressing": scenarios.run(impl, scenarios.compress_scenario()),
     }
     with open(os.path.join(HERE, "scenarios.json"), "w") as f:
         json.dump(out, f, indent=1)

@@ -123,6 +123,33 @@ def ff_message_scenario():
     return S
 
 
+def compress_scenario():
+    """CompressingFilter (compressing.h:8-37) alone and at the end of the ctr
+    chain: keys + values compressed, uncompressed_size side-info, empty arrays
+    kept empty, several 64 KiB snappy fragments, keys elided by KEY_CACHING
+    before compression."""
+    keys = sorted_keys(3000, 31)
+    big = sorted_keys(100000, 32)
+    w = gauss(3000, 33) * np.float32(0.1)
+    g = gauss(100000, 34)
+    cmp_ = [(COMPRESSING, {})]
+    chain = [(KEY_CACHING, {}), (FIXING_FLOAT, {"num_bytes": 1}), (COMPRESSING, {})]
+    S = []
+
+    def step(name, snd, rcv, keys, values, filters, request=True, push=True, channel=0):
+        S.append(dict(name=name, snd=snd, rcv=rcv, keys=keys, filters=filters, request=request,
+                      push=push, channel=channel, kr=(0, 10**9), values=values))
+
+    step("keys_and_values", "W", "S", keys, [w], cmp_)
+    step("values_only_with_empty", "W", "S", None, [w, np.zeros(0, np.float32), g[:777]], cmp_)
+    step("multi_fragment", "W", "S", big, [g, g.astype(np.float64)], cmp_)
+    step("keys_only", "W", "S", big[:5], [], cmp_)
+    step("chain_pull_req_miss", "W", "S", big, [], chain, push=False, channel=1)
+    step("chain_pull_resp_hit", "S", "W", big, [g * np.float32(0.01)], chain, request=False, channel=1)
+    step("chain_push_hit", "W", "S", big, [g], chain, push=True, channel=1)
+    return S
+
+
 # ---------------------------------------------------------------- runner ----
 def run(impl, steps, seed_clock=12345):
     """Run steps through impl; returns a list of per-step records."""

@@ -151,11 +151,12 @@ def test_key_signature_prefix(ctx, port):
     assert ctx.key_signature(keys) == port.key_signature(keys[:256].cpu().numpy())
 
 
-@pytest.mark.parametrize("which", ["key_caching", "chain_ctr", "ff_message"])
+@pytest.mark.parametrize("which", ["key_caching", "chain_ctr", "ff_message", "compressing"])
 def test_scenarios_match_reference(scenario_golden, which):
     import scenarios
     steps = {"key_caching": scenarios.kc_scenario, "chain_ctr": scenarios.chain_scenario,
-             "ff_message": scenarios.ff_message_scenario}[which]()
+             "ff_message": scenarios.ff_message_scenario,
+             "compressing": scenarios.compress_scenario}[which]()
     got = scenarios.run(scenarios.PsfImpl(device=0), steps)
     want = scenario_golden[which]
     for g, w in zip(got, want):

@@ -1,0 +1,179 @@
+"""GPU: the COMPRESSING codec (snappy 1.1.8 raw format) through the C ABI.
+
+Compress must be byte-identical to snappy 1.1.8 (tests/golden/snappy.npz from
+the reference's libsnappy; the C restatement oracle/snappy_port.c for larger
+seeded inputs).  Uncompress must reproduce RawUncompress's verdict and output
+on valid and mutated streams (tests/golden/snappy_dec.npz), including valid
+streams that no 1.1.8 encoder writes (literals and copies across 64 KiB output
+fragments: the one-lane path)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev(b: bytes, offset: int = 0) -> torch.Tensor:
+    a = np.frombuffer(b"\0" * offset + b, dtype=np.uint8).copy()
+    return torch.from_numpy(a).cuda()[offset:]
+
+
+def _inputs(rng, n, kind):
+    if kind == "random":
+        return rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+    if kind == "keys":
+        return np.sort(rng.integers(0, 10**9, n // 8 + 1, dtype=np.uint64)).tobytes()[:n]
+    if kind == "codes":
+        return np.clip(rng.standard_normal(n) * 30 + 128, 0, 255).astype(np.uint8).tobytes()
+    if kind == "runs":
+        return np.repeat(rng.integers(0, 256, n // 50 + 1, dtype=np.uint8),
+                         50).tobytes()[:n]
+    if kind == "zeros":
+        return bytes(n)
+    if kind == "text":
+        words = [b"param", b"server", b"filter", b"key", b"value", b"  ", b"\n"]
+        return b"".join(words[i] for i in rng.integers(0, len(words), n // 4 + 1))[:n]
+    raise ValueError(kind)
+
+
+def test_compress_matches_snappy_1_1_8_fixtures(ctx):
+    a = np.load(os.path.join(GOLDEN, "snappy.npz"), allow_pickle=False)
+    names = sorted(k[:-3] for k in a.files if k.endswith("_in"))
+    assert len(names) >= 20
+    for k in names:
+        x, want = a[f"{k}_in"].tobytes(), a[f"{k}_out"].tobytes()
+        got = ctx.snappy_compress(_dev(x)).cpu().numpy().tobytes()
+        assert got == want, k
+        back = ctx.snappy_uncompress(_dev(want)).cpu().numpy().tobytes()
+        assert back == x, k
+
+
+@pytest.mark.parametrize("kind", ["random", "keys", "codes", "runs", "zeros", "text"])
+def test_compress_random_sizes_vs_port(ctx, port, kind):
+    rng = np.random.default_rng(len(kind) * 7 + ord(kind[0]))
+    for n in [1, 14, 15, 16, 17, 63, 64, 65, 255, 256, 257, 4095, 65535, 65536, 65537, 300001, 3 << 20]:
+        x = _inputs(rng, n, kind)
+        want = port.snappy_compress(x)
+        got = ctx.snappy_compress(_dev(x)).cpu().numpy().tobytes()
+        assert got == want, (kind, n)
+        back = ctx.snappy_uncompress(_dev(want)).cpu().numpy().tobytes()
+        assert back == x, (kind, n)
+
+
+def test_compress_unaligned_input(ctx, port):
+    rng = np.random.default_rng(5)
+    x = _inputs(rng, 200003, "keys")
+    for off in (1, 3, 4, 8, 13):
+        got = ctx.snappy_compress(_dev(x, off)).cpu().numpy().tobytes()
+        assert got == port.snappy_compress(x), off
+
+
+def test_decoder_verdicts_match_reference(ctx):
+    from parameter_server_amd._lib import PSF_ERR_CHECK, PsfError
+    a = np.load(os.path.join(GOLDEN, "snappy_dec.npz"), allow_pickle=False)
+    d, off, st, out, ooff = a["data"], a["offsets"], a["status"], a["out"], a["out_offsets"]
+    nbad = 0
+    for i in range(len(st)):
+        s = d[off[i]:off[i + 1]].tobytes()
+        want = out[ooff[i]:ooff[i + 1]].tobytes()
+        if st[i] == -2:
+            continue  # declared length beyond the fixture's cap: not a verdict
+        try:
+            got = ctx.snappy_uncompress(_dev(s)).cpu().numpy().tobytes()
+            ok = True
+        except PsfError as e:
+            assert e.code == PSF_ERR_CHECK
+            ok = False
+        assert ok == (st[i] == 0), (i, s[:12], st[i])
+        if ok:
+            assert got == want, i
+        else:
+            nbad += 1
+    assert nbad > 100
+
+
+def _varint(n):
+    out = bytearray()
+    while n >= 128:
+        out.append((n & 127) | 128)
+        n >>= 7
+    out.append(n)
+    return bytes(out)
+
+
+def _lit(b):
+    n = len(b) - 1
+    if n < 60:
+        return bytes([n << 2]) + b
+    k = (n.bit_length() + 7) // 8
+    return bytes([(59 + k) << 2]) + n.to_bytes(k, "little") + b
+
+
+def _copy2(off, ln):
+    return bytes([2 | ((ln - 1) << 2), off & 255, off >> 8])
+
+
+def _copy4(off, ln):
+    return bytes([3 | ((ln - 1) << 2)]) + off.to_bytes(4, "little")
+
+
+def test_valid_streams_across_fragments(ctx, port):
+    """Valid streams a 1.1.8 encoder never writes: a literal straddling the
+    64 KiB output boundary, a copy reaching into the previous fragment, a
+    copy-4 tag, an overlapping copy (offset 1)."""
+    rng = np.random.default_rng(9)
+    blob = rng.integers(0, 256, 70000, dtype=np.uint8).tobytes()
+    streams = []
+    body = _lit(blob) + _copy2(65000, 64) + _copy4(1, 64) + _copy2(3, 60)
+    streams.append(body)
+    body = _lit(blob[:65530]) + _copy2(60000, 64) + _lit(b"xyz") + _copy4(65000, 30)
+    streams.append(body)
+    body = _lit(b"a") + b"".join(_copy2(1, 64) for _ in range(3000))
+    streams.append(body)
+    for body in streams:
+        total = _count(body)
+        s = _varint(total) + body
+        st, want = port.snappy_uncompress(s, cap=1 << 24)
+        assert st == 0
+        got = ctx.snappy_uncompress(_dev(s)).cpu().numpy().tobytes()
+        assert got == want
+
+
+def _count(body):
+    p, o = 0, 0
+    while p < len(body):
+        c = body[p]
+        if c & 3 == 0:
+            ln = (c >> 2) + 1
+            h = 1
+            if ln > 60:
+                k = ln - 60
+                ln = int.from_bytes(body[p + 1:p + 1 + k], "little") + 1
+                h += k
+            p += h + ln
+        else:
+            ln = 4 + ((c >> 2) & 7) if c & 3 == 1 else (c >> 2) + 1
+            p += {1: 2, 2: 3, 3: 5}[c & 3]
+        o += ln
+    return o
+
+
+def test_large_roundtrip_properties(ctx):
+    """64 MiB of sorted keys: decode(encode(x)) == x and the stream parses."""
+    n = 8 << 20
+    keys = torch.sort(torch.randint(0, 10**12, (n,), dtype=torch.int64, device="cuda"))[0]
+    s = ctx.snappy_compress(keys)
+    assert s.numel() < keys.numel() * 8
+    back = ctx.snappy_uncompress(s)
+    assert torch.equal(back.view(torch.int64), keys)
+
+
+def test_header_errors(ctx):
+    from parameter_server_amd._lib import PsfError
+    for bad in (b"\x80", b"\xff\xff\xff\xff\x1f", b"\x03ab", b"\x02\x00\x00"):
+        with pytest.raises(PsfError):
+            ctx.snappy_uncompress(_dev(bad))
