@@ -169,6 +169,7 @@ int psf_fc_fixed_point(const psf_message* msg, int idx, int k, psf_fixed_point* 
 int psf_fc_signature(const psf_message* msg, int idx, int* has_signature, uint32_t* sig);
 int psf_fc_num_uncompressed(const psf_message* msg, int idx);
 int psf_fc_uncompressed(const psf_message* msg, int idx, int i, uint64_t* size);
+int psf_fc_add_uncompressed(psf_message* msg, int idx, uint64_t size);
 
 /* ---- key-range partition and slicing (multi-server / multi-GPU split) --
  * Range<Key>::EvenDivide(n, i) (src/util/range.h:100-107): the i-th of n

@@ -18,15 +18,16 @@
 // message's own FilterConfig as the reference does.  libpsf status codes map to
 // the reference's fatal CHECK.
 //
-// Filters adapted: FIXING_FLOAT.  KEY_CACHING on host-resident keys is 2 KiB
-// of CRC plus a hash map -- libpsf runs it on the host too -- so CreateFilter
-// returns nullptr for it (and for types libpsf does not accelerate yet) and
-// the reference's own class is used.
+// Filters adapted: FIXING_FLOAT, COMPRESSING (snappy 1.1.8-identical streams)
+// and NOISE.  KEY_CACHING on host-resident keys is 2 KiB of CRC plus a hash
+// map -- libpsf runs it on the host too -- so CreateFilter returns nullptr for
+// it and the reference's own class is used.
 #pragma once
 #include <stdint.h>
 #include <string.h>
 
 #include <mutex>
+#include <string>
 
 #include "psf.h"
 
@@ -113,11 +114,90 @@ class FixingFloatFilter : public Filter {
   std::mutex mu_;
 };
 
+// One libpsf filter of `type` over the whole message: key (when present) and
+// values travel as host buffers, the FilterConfig fields that type reads are
+// copied in, outputs and side-info come back.
+//   COMPRESSING  <- src/filter/compressing.h:8-37 (uncompressed_size side-info)
+//   NOISE        <- src/filter/add_noise.h:11-39 (in place on the value arrays)
+class MessageFilter : public Filter {
+ public:
+  explicit MessageFilter(FilterConfig::Type type) : type_(type) {
+    Check(psf_node_create(Context(), &node_));
+  }
+  ~MessageFilter() { psf_node_destroy(node_); }
+  void encode(Message* msg) { run(msg, true); }
+  void decode(Message* msg) { run(msg, false); }
+
+ private:
+  void run(Message* msg, bool encode) {
+    FilterConfig* conf = find(type_, msg);
+    if (!conf) {
+      if (type_ == FilterConfig::NOISE && encode) CHECK_NOTNULL(conf);  // add_noise.h:13
+      return;
+    }
+    std::lock_guard<std::mutex> l(mu_);
+    const Task& t = msg->task;
+    psf_message* m = nullptr;
+    Check(psf_msg_create(t.request(), t.has_param(), t.has_param() && t.param().push(),
+                         t.key_channel(), t.has_key_range(), t.key_range().begin(),
+                         t.key_range().end(), &m));
+    const bool had_key = msg->has_key();
+    if (had_key) Check(psf_msg_set_key(m, msg->key.data(), msg->key.size(), PSF_DT_CHAR, PSF_LOC_HOST));
+    for (size_t i = 0; i < msg->value.size(); ++i) {
+      int vt = i < (size_t)t.value_type_size() ? (int)t.value_type(i) : 0;
+      Check(psf_msg_add_value(m, msg->value[i].data(), msg->value[i].size(), vt, PSF_LOC_HOST));
+    }
+    int fi = psf_msg_add_filter(m, type_);
+    Check(fi < 0 ? fi : PSF_OK);
+    if (type_ == FilterConfig::NOISE) Check(psf_fc_set_noise(m, fi, conf->mean(), conf->std()));
+    if (type_ == FilterConfig::COMPRESSING)
+      for (int i = 0; i < conf->uncompressed_size_size(); ++i)
+        Check(psf_fc_add_uncompressed(m, fi, conf->uncompressed_size(i)));
+    const int st = encode ? psf_node_encode(node_, m) : psf_node_decode(node_, m);
+    if (st != PSF_OK) {
+      std::string err = psf_last_error();
+      psf_msg_destroy(m);
+      CHECK(false) << "libpsf filter " << (int)type_ << ": " << err;
+    }
+    if (had_key) msg->key = take(m, -1, msg->key);
+    for (size_t i = 0; i < msg->value.size(); ++i) msg->value[i] = take(m, (int)i, msg->value[i]);
+    if (type_ == FilterConfig::COMPRESSING) {
+      conf->clear_uncompressed_size();
+      const int nu = psf_fc_num_uncompressed(m, fi);
+      for (int i = 0; i < nu; ++i) {
+        uint64_t v = 0;
+        Check(psf_fc_uncompressed(m, fi, i, &v));
+        conf->add_uncompressed_size(v);
+      }
+    }
+    psf_msg_destroy(m);
+  }
+
+  // array i (-1 = key) of the libpsf message as an SArray<char>; the input
+  // array itself when libpsf left it in place
+  static SArray<char> take(psf_message* m, int i, const SArray<char>& in) {
+    void* p = nullptr;
+    size_t bytes = 0;
+    int loc = 0;
+    Check(i < 0 ? psf_msg_key(m, &p, &bytes, &loc) : psf_msg_value(m, i, &p, &bytes, &loc));
+    if (p == in.data() && bytes == in.size()) return in;
+    SArray<char> out(bytes);
+    if (bytes) Check(psf_copy_to_host(Context(), out.data(), p, bytes));
+    return out;
+  }
+
+  FilterConfig::Type type_;
+  psf_node* node_ = nullptr;
+  std::mutex mu_;
+};
+
 // Registration hook for Filter::create (filter.cc:9-23): a libpsf filter, or
 // nullptr to fall through to the reference's own switch.
 inline Filter* CreateFilter(const FilterConfig& conf) {
   switch (conf.type()) {
     case FilterConfig::FIXING_FLOAT: return new FixingFloatFilter();
+    case FilterConfig::COMPRESSING: return new MessageFilter(FilterConfig::COMPRESSING);
+    case FilterConfig::NOISE: return new MessageFilter(FilterConfig::NOISE);
     default: return nullptr;
   }
 }

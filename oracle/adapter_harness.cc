@@ -9,7 +9,10 @@
 // Built by `make -C oracle adapter` into oracle/_ref/libpsadapter.so.
 #include "filter/filter.h"
 #include "filter/fixing_float.h"
+#include "filter/compressing.h"
+#include "filter/add_noise.h"
 #include "psf_ps_filter.h"
+#include "snappy_glue.h"
 
 #include <string>
 #include <vector>
@@ -99,6 +102,85 @@ int psadapter_compare_ff(const void* x, size_t bytes, int value_type, int nb, in
       g_err = e.what();
       rc = 5;
     }
+  }
+  delete a;
+  delete b;
+  return rc;
+}
+
+// COMPRESSING: reference CompressingFilter vs the adapter on one message with
+// keys (if kbytes) and one value array.  0 = identical wire bytes, identical
+// uncompressed_size and both cross decodes restore the input.
+int psadapter_compare_compress(const void* key, size_t kbytes, const void* val, size_t vbytes, int vt) {
+  auto mk = [&] {
+    auto* m = new Message();
+    if (kbytes) {
+      SArray<char> k(kbytes);
+      memcpy(k.data(), key, kbytes);
+      m->set_key(k);
+    }
+    SArray<char> v(vbytes);
+    if (vbytes) memcpy(v.data(), val, vbytes);
+    m->task.value_type_.push_back((DataType)vt);
+    m->value.push_back(v);
+    m->task.add_filter()->set_type(FilterConfig::COMPRESSING);
+    return m;
+  };
+  Message *a = mk(), *b = mk(), *orig = mk();
+  PS::CompressingFilter ref;
+  psf_hip::MessageFilter hip(FilterConfig::COMPRESSING);
+  int rc = 0;
+  try {
+    ref.encode(a);
+    hip.encode(b);
+    const auto &fa = a->task.filter(0), &fb = b->task.filter(0);
+    if (!same_bytes(a->key, b->key) || !same_bytes(a->value[0], b->value[0])) rc = 2;
+    else if (fa.uncompressed_size_size() != fb.uncompressed_size_size()) rc = 3;
+    for (int i = 0; rc == 0 && i < fa.uncompressed_size_size(); ++i)
+      if (fa.uncompressed_size(i) != fb.uncompressed_size(i)) rc = 3;
+    if (rc == 0) {
+      Message a2 = *b, b2 = *a;
+      ref.decode(&a2);
+      hip.decode(&b2);
+      if (!same_bytes(a2.key, orig->key) || !same_bytes(b2.key, orig->key) ||
+          !same_bytes(a2.value[0], orig->value[0]) || !same_bytes(b2.value[0], orig->value[0]))
+        rc = 4;
+    }
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    rc = 5;
+  }
+  delete a;
+  delete b;
+  delete orig;
+  return rc;
+}
+
+// NOISE: reference AddNoiseFilter vs the adapter (in place); 0 = identical bytes
+int psadapter_compare_noise(const void* val, size_t vbytes, int vt, float mean, float sd) {
+  auto mk = [&] {
+    auto* m = new Message();
+    SArray<char> v(vbytes);
+    memcpy(v.data(), val, vbytes);
+    m->task.value_type_.push_back((DataType)vt);
+    m->value.push_back(v);
+    auto* f = m->task.add_filter();
+    f->set_type(FilterConfig::NOISE);
+    f->mean_ = mean;
+    f->std_ = sd;
+    return m;
+  };
+  Message *a = mk(), *b = mk();
+  PS::AddNoiseFilter ref;
+  psf_hip::MessageFilter hip(FilterConfig::NOISE);
+  int rc = 0;
+  try {
+    ref.encode(a);
+    hip.encode(b);
+    if (!same_bytes(a->value[0], b->value[0])) rc = 2;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    rc = 5;
   }
   delete a;
   delete b;

@@ -17,7 +17,6 @@
 #include "filter/compressing.h"
 #include "filter/add_noise.h"
 #include "util/crc32c.h"
-#include "/opt/conda/include/snappy.h"
 
 #include <map>
 #include <string>
@@ -30,27 +29,7 @@ extern "C" time_t __wrap_time(time_t* t) {
   return g_time;
 }
 
-// snappy glue restated from shared_array_inl.h:232-255
-namespace PS {
-template <typename V> SArray<char> SArray<V>::CompressTo() const {
-  if (empty()) return SArray<char>();
-  size_t ssize = size_ * sizeof(V);
-  size_t dsize = snappy::MaxCompressedLength(ssize);
-  SArray<char> dest(dsize);
-  snappy::RawCompress(reinterpret_cast<const char*>(data()), ssize, dest.data(), &dsize);
-  dest.resize(dsize);
-  return dest;
-}
-template <typename V> void SArray<V>::UncompressFrom(const char* src, size_t src_size) {
-  if (src_size == 0) { clear(); return; }
-  size_t dsize = 0;
-  CHECK(snappy::GetUncompressedLength(src, src_size, &dsize));
-  CHECK_EQ(dsize / sizeof(V) * sizeof(V), dsize);
-  resize(dsize / sizeof(V));
-  CHECK(snappy::RawUncompress(src, src_size, reinterpret_cast<char*>(data())));
-}
-template class SArray<char>;
-}  // namespace PS
+#include "snappy_glue.h"
 
 namespace {
 thread_local std::string g_err;

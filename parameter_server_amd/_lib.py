@@ -80,6 +80,7 @@ SIGNATURES = {
     "psf_fc_signature": ([vp, C.c_int, PI, C.POINTER(u32)], C.c_int),
     "psf_fc_num_uncompressed": ([vp, C.c_int], C.c_int),
     "psf_fc_uncompressed": ([vp, C.c_int, C.c_int, C.POINTER(u64)], C.c_int),
+    "psf_fc_add_uncompressed": ([vp, C.c_int, u64], C.c_int),
     "psf_node_roundtrip": ([vp, vp, C.POINTER(vp), C.c_int, C.c_int, C.POINTER(vp)], C.c_int),
     "psf_range_even_divide": ([u64, u64, u64, u64, C.POINTER(u64), C.POINTER(u64)], C.c_int),
     "psf_msg_slice": ([vp, vp, C.POINTER(u64), C.c_int, C.c_int, C.POINTER(vp), PI], C.c_int),

@@ -450,6 +450,13 @@ const char* psf_profile_kernel_name(int k) {
   return (k >= 0 && k < psf::kKNum) ? names[k] : "?";
 }
 
+int psf_fc_add_uncompressed(psf_message* msg, int idx, uint64_t size) {
+  return guarded([&] {
+    fc_at(msg, idx)->uncompressed_size.push_back(size);
+    return PSF_OK;
+  });
+}
+
 int psf_fc_uncompressed(const psf_message* msg, int idx, int i, uint64_t* size) {
   return guarded([&] {
     const auto* f = fc_at(msg, idx);

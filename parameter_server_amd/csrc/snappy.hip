@@ -33,7 +33,7 @@ namespace {
 constexpr uint32_t kFrag = 65536;     // snappy kBlockSize
 constexpr uint32_t kMaxTable = 16384;  // kMaxHashTableSize
 constexpr uint32_t kMul = 0x1e35a7bdu;
-constexpr int kSkipN = 5 * 64 + 1;
+constexpr int kSkipN = 6 * 64 + 1;  // a skip loop ends before probe 270
 
 // cum[k]: offset of probe k from the start of a skip loop (skip starts at 32,
 // each probe advances by skip>>5 and then skip += skip>>5).
@@ -61,10 +61,13 @@ __device__ __forceinline__ uint32_t ld32(const uint32_t* s, uint32_t p) {
 
 __device__ __forceinline__ uint32_t hash(uint32_t v, int shift) { return (v * kMul) >> shift; }
 
+constexpr uint32_t kMinSlots = 4096;
+
 struct CompressLds {
+  uint32_t skip[kSkipN + 3];  // kSkip, read from LDS: no vector-memory wait in the loop
   uint32_t src[kFrag / 4 + 8];
   uint16_t table[kMaxTable];
-  uint8_t dedup[kMaxTable];
+  uint32_t minlane[kMinSlots];  // per hash slot: lowest lane of the step that probed it
 };
 
 __device__ uint32_t emit_literal(uint8_t* out, uint32_t op, const uint8_t* srcb, uint32_t lit,
@@ -136,7 +139,6 @@ __global__ __launch_bounds__(64) void snappy_compress_frags(const uint8_t* __res
   const uint8_t* g = in + start;
   uint8_t* out = scratch + (size_t)f * kSnappyFragOut;
   uint8_t* srcb = reinterpret_cast<uint8_t*>(L.src);
-  volatile uint8_t* dd = L.dedup;  // lanes read back another lane's write
 
   if ((reinterpret_cast<uintptr_t>(g) & 15) == 0) {
     const uint32_t nv = len >> 4;
@@ -148,6 +150,8 @@ __global__ __launch_bounds__(64) void snappy_compress_frags(const uint8_t* __res
     for (uint32_t i = lane; i < len; i += 64) srcb[i] = g[i];
   }
   if (lane < 16) srcb[len + lane] = 0;
+  for (uint32_t i = lane; i < (uint32_t)kSkipN; i += 64) L.skip[i] = kSkip.v[i];
+  for (uint32_t i = lane; i < kMinSlots; i += 64) L.minlane[i] = 0xffffffffu;
   uint32_t tsize = 256;
   while (tsize < kMaxTable && tsize < len) tsize <<= 1;
   const int shift = __builtin_clz(tsize) + 1;  // 32 - log2(tsize)
@@ -160,44 +164,55 @@ __global__ __launch_bounds__(64) void snappy_compress_frags(const uint8_t* __res
     const uint32_t ip_limit = len - 15;
     uint32_t ip = 1;
     for (;;) {
-      // ---- skip loop: 64 probes per step, first match wins
+      // ---- skip loop: up to 64 probes per step, first match wins.  Probes are
+      // exact up to the first lane jc whose hash slot an earlier lane of the
+      // step also probed: lanes < jc see the table as it was, and lane jc either
+      // sees that lane's write (same hash; it is the only earlier one, a second
+      // would itself have been jc) or the table (slot alias).  Later lanes are
+      // dropped and the next step starts after jc.
       uint32_t cand = 0, kbase = 0;
       for (;;) {
         const uint32_t k = kbase + lane;
-        const uint32_t pos = ip + kSkip.v[k];
-        const bool valid = ip + kSkip.v[k + 1] <= ip_limit;  // else "goto emit_remainder"
-        uint32_t v = 0, h = 0;
+        const uint32_t pos = ip + L.skip[k];
+        const bool valid = ip + L.skip[k + 1] <= ip_limit;  // else "goto emit_remainder"
+        uint32_t v = 0, h = 0, slot = 0;
         if (valid) {
           v = ld32(L.src, pos);
           h = hash(v, shift);
-          dd[h] = (uint8_t)lane;
+          slot = h & (kMinSlots - 1);
+          atomicMin(&L.minlane[slot], lane);
         }
-        const bool coll = valid && dd[h] != (uint8_t)lane;
-        uint32_t c = valid ? L.table[h] : 0;
-        uint32_t next_same = 64;
+        asm volatile("" ::: "memory");
+        uint32_t first = valid ? L.minlane[slot] : lane;
+        asm volatile("" ::: "memory");
+        if (valid) L.minlane[slot] = 0xffffffffu;  // clean for the next step
         const uint64_t vm = __ballot(valid);
-        if (__ballot(coll)) {  // same hash twice in this step: later probes see earlier writes
-          for (uint32_t j = 0; j < 64 && ((vm >> j) & 1); ++j) {
-            const uint32_t hj = __builtin_amdgcn_readlane(h, j);
-            const uint32_t pj = __builtin_amdgcn_readlane(pos, j);
-            if (valid && hj == h) {
-              if (j < lane) c = pj;
-              else if (j > lane && next_same == 64) next_same = j;
-            }
-          }
+        const uint64_t em = __ballot(valid && first < lane);
+        int limit = 63;  // last exact lane
+        int jc = 64, jm = 0;
+        bool exact_pair = false;
+        if (em) {
+          jc = __builtin_ctzll(em);
+          jm = (int)__builtin_amdgcn_readlane(first, jc);
+          exact_pair = __builtin_amdgcn_readlane(h, jm) == __builtin_amdgcn_readlane(h, jc);
+          limit = jc;
         }
-        const bool m = valid && v == ld32(L.src, c);
+        uint32_t c = valid ? L.table[h] : 0;
+        if (exact_pair && (int)lane == jc) c = __builtin_amdgcn_readlane(pos, jm);
+        const bool m = valid && (int)lane <= limit && v == ld32(L.src, c);
         const uint64_t mm = __ballot(m);
-        const int last = mm ? __builtin_ctzll(mm) : (vm ? 63 - __builtin_clzll(vm) : -1);
-        if (valid && (int)lane <= last && (int)next_same > last) L.table[h] = (uint16_t)pos;
+        const uint64_t lim_mask = limit >= 63 ? ~0ull : ((1ull << (limit + 1)) - 1);
+        const int last = mm ? __builtin_ctzll(mm) : limit;
+        const bool overwritten = exact_pair && (int)lane == jm && jc <= last;
+        if (valid && (int)lane <= last && !overwritten) L.table[h] = (uint16_t)pos;
         if (mm) {
           const int ks = __builtin_ctzll(mm);
           ip = __builtin_amdgcn_readlane(pos, ks);
           cand = __builtin_amdgcn_readlane(c, ks);
           break;
         }
-        if (vm != ~0ull) goto remainder;
-        kbase += 64;
+        if ((vm & lim_mask) != lim_mask) goto remainder;
+        kbase += (uint32_t)limit + 1;
       }
       op = emit_literal(out, op, srcb, next_emit, ip - next_emit, lane);
       // ---- emit copies while the next position matches immediately
@@ -340,37 +355,61 @@ __device__ __forceinline__ Tag parse_tag(const uint8_t* b, uint64_t p) {
   return t;
 }
 
-// stage in[base, base+want) into lds (zero past the end of the input)
-__device__ __forceinline__ void stage(uint8_t* lds, const uint8_t* in, uint64_t C, uint64_t base, uint32_t want,
-                                      uint32_t lane, uint32_t nthreads) {
-  const uint64_t avail = base < C ? C - base : 0;
-  for (uint32_t i = lane; i < want; i += nthreads) lds[i] = i < avail ? in[base + i] : 0;
+// Stage in[base, base+want) into LDS: aligned dword loads where the whole word
+// lies inside the input, bytes at the edges (0 past the end).  Returns s with
+// lds[s + i] == in[base + i].
+__device__ __forceinline__ uint32_t stage(uint32_t* lds, const uint8_t* in, uint64_t C, uint64_t base, uint32_t want,
+                                          uint32_t lane) {
+  const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(in + base) & 3);
+  const int64_t r0 = (int64_t)base - (int64_t)s;  // input offset of lds byte 0 (dword aligned)
+  const uint32_t nw = (s + want + 3) >> 2;
+  for (uint32_t j = lane; j < nw; j += 64) {
+    const int64_t r = r0 + 4 * (int64_t)j;
+    uint32_t v = 0;
+    if (r >= 0 && r + 4 <= (int64_t)C) {
+      v = *reinterpret_cast<const uint32_t*>(in + r);
+    } else {
+      for (int q = 0; q < 4; ++q)
+        if (r + q >= 0 && r + q < (int64_t)C) v |= (uint32_t)in[r + q] << (8 * q);
+    }
+    lds[j] = v;
+  }
+  return s;
 }
 
-// K1: speculative parse of each window from its first byte
+constexpr uint32_t kStarts = 64;  // K1 parses from each of the first 64 offsets of a window
+
+// K1: speculative parse of each window from each of its first 64 byte offsets
+// (lane l from offset l).  A window's true entry is one of them unless a literal
+// carried the chain further in; for those K2 walks until it meets lane 0's chain.
 __global__ __launch_bounds__(64) void snappy_dscan(const uint8_t* __restrict__ in, uint64_t C, uint32_t hdr,
                                                    uint32_t* __restrict__ bitmap, uint32_t* __restrict__ cum,
                                                    uint64_t* __restrict__ wexit, uint64_t* __restrict__ wtotal) {
-  __shared__ uint8_t b[kWin + 16];
+  __shared__ uint32_t b32[(kWin + 32) / 4];
   __shared__ uint32_t bm[kWin / 32];
   const uint32_t lane = threadIdx.x, w = blockIdx.x;
   const uint64_t base = hdr + (uint64_t)w * kWin;
   const uint32_t wl = (uint32_t)min((uint64_t)kWin, C - base);
-  stage(b, in, C, base, wl + 16, lane, 64);
+  const uint32_t s = stage(b32, in, C, base, wl + 16, lane);
   for (uint32_t i = lane; i < kWin / 32; i += 64) bm[i] = 0;
   __syncthreads();
-  if (lane == 0) {
-    uint64_t p = 0, o = 0;
-    while (p < wl) {
-      bm[p >> 5] |= 1u << (p & 31);
-      cum[base + p] = (uint32_t)o;
+  const uint8_t* b = reinterpret_cast<const uint8_t*>(b32) + s;
+  uint64_t p = lane, o = 0;
+  bool alive = p < wl;
+  while (__ballot(alive)) {
+    if (alive) {
+      if (lane == 0) {
+        atomicOr(&bm[p >> 5], 1u << (p & 31));
+        cum[base + p] = (uint32_t)o;
+      }
       const Tag t = parse_tag(b + p, p);
       o += t.len;
       p = t.next;
+      alive = p < wl;
     }
-    wexit[w] = base + p;
-    wtotal[w] = o;
   }
+  wexit[(size_t)w * kStarts + lane] = base + p;
+  wtotal[(size_t)w * kStarts + lane] = o;
   __syncthreads();
   uint32_t* gb = bitmap + (size_t)w * (kWin / 32);
   for (uint32_t i = lane; i < kWin / 32; i += 64) gb[i] = bm[i];
@@ -392,20 +431,23 @@ __global__ __launch_bounds__(64) void snappy_dlink(const uint8_t* __restrict__ i
   while (p < C) {
     const uint64_t rel = p - hdr;
     const uint32_t w = (uint32_t)(rel / kWin);
-    wentry[w] = p;
-    woff[w] = o;
-    if ((bitmap[rel >> 5] >> (rel & 31)) & 1) {
-      o += wtotal[w] - cum[p];
-      p = wexit[w];
-    } else {  // entry off the speculative chain: walk this window here
-      const uint64_t wend = hdr + (uint64_t)(w + 1) * kWin;
+    const uint64_t off = rel - (uint64_t)w * kWin;
+    if (wentry[w] == kNone) {
+      wentry[w] = p;
+      woff[w] = o;
+    }
+    if (off < kStarts) {  // parsed exactly by K1's lane `off`
+      o += wtotal[(size_t)w * kStarts + off];
+      p = wexit[(size_t)w * kStarts + off];
+    } else if ((bitmap[rel >> 5] >> (rel & 31)) & 1) {  // met lane 0's chain
+      o += wtotal[(size_t)w * kStarts] - cum[p];
+      p = wexit[(size_t)w * kStarts];
+    } else {  // one tag, then look again
       uint8_t tb[5];
-      while (p < wend && p < C) {
-        for (int i = 0; i < 5; ++i) tb[i] = p + i < C ? in[p + i] : 0;
-        const Tag t = parse_tag(tb, p);
-        o += t.len;
-        p = t.next;
-      }
+      for (int i = 0; i < 5; ++i) tb[i] = p + i < C ? in[p + i] : 0;
+      const Tag t = parse_tag(tb, p);
+      o += t.len;
+      p = t.next;
     }
     if (o > dsize) {
       bad = true;
@@ -421,15 +463,16 @@ __global__ __launch_bounds__(64) void snappy_dindex(const uint8_t* __restrict__ 
                                                     const uint64_t* __restrict__ wentry,
                                                     const uint64_t* __restrict__ woff,
                                                     uint64_t* __restrict__ fragpos, uint32_t* __restrict__ flags) {
-  __shared__ uint8_t b[kWin + 16];
+  __shared__ uint32_t b32[(kWin + 32) / 4];
   const uint32_t lane = threadIdx.x, w = blockIdx.x;
   const uint64_t e = wentry[w];
   if (e == kNone || (*flags & kFlagInvalid)) return;
   const uint64_t base = hdr + (uint64_t)w * kWin;
   const uint32_t wl = (uint32_t)min((uint64_t)kWin, C - base);
-  stage(b, in, C, base, wl + 16, lane, 64);
+  const uint32_t s = stage(b32, in, C, base, wl + 16, lane);
   __syncthreads();
   if (lane != 0) return;
+  const uint8_t* b = reinterpret_cast<const uint8_t*>(b32) + s;
   uint64_t p = e - base, o = woff[w];
   uint32_t fl = 0;
   while (p < wl) {
@@ -446,30 +489,43 @@ __global__ __launch_bounds__(64) void snappy_dindex(const uint8_t* __restrict__ 
   if (fl) atomicOr(flags, fl);
 }
 
-// K4: one wave per 64 KiB output fragment, decoded in LDS
+// K4: one wave per 64 KiB output fragment, decoded in LDS; tags and short
+// literals are read from a staged window of the compressed bytes
 __global__ __launch_bounds__(64) void snappy_dfrag(const uint8_t* __restrict__ in, uint64_t C, uint64_t dsize,
                                                    const uint64_t* __restrict__ fragpos,
                                                    const uint32_t* __restrict__ flags, uint8_t* __restrict__ out) {
-  __shared__ uint8_t ob[kFrag];
-  __shared__ uint8_t ib[kInWin + 16];
+  __shared__ uint32_t ob32[kFrag / 4];
+  __shared__ uint32_t ib32[(kInWin + 32) / 4];
   if (*flags) return;
+  uint8_t* ob = reinterpret_cast<uint8_t*>(ob32);
+  const uint8_t* ibb = reinterpret_cast<const uint8_t*>(ib32);
   const uint32_t lane = threadIdx.x, k = blockIdx.x;
   const uint64_t o0 = (uint64_t)k * kFrag;
   const uint32_t end = (uint32_t)min((uint64_t)kFrag, dsize - o0);
+  constexpr uint32_t kSpan = kInWin + 16;  // staged bytes [wb, wb + kSpan)
   uint64_t p = fragpos[k];
   uint64_t wb = p;
-  stage(ib, in, C, wb, kInWin + 16, lane, 64);
+  uint32_t s = stage(ib32, in, C, wb, kSpan, lane);
   uint32_t o = 0;
   while (o < end) {
-    if (p + 8 > wb + kInWin + 16) {
+    if (p + 8 > wb + kSpan) {
       wb = p;
-      stage(ib, in, C, wb, kInWin + 16, lane, 64);
+      s = stage(ib32, in, C, wb, kSpan, lane);
     }
-    const Tag t = parse_tag(ib + (p - wb), p);
+    const Tag t = parse_tag(ibb + s + (p - wb), p);
     const uint32_t L = (uint32_t)t.len;
     if (t.lit) {
-      const uint64_t s = p + t.hl;
-      for (uint32_t i = lane; i < L; i += 64) ob[o + i] = in[s + i];
+      const uint64_t src = p + t.hl;
+      if (src + L > wb + kSpan && L <= kInWin) {
+        wb = src;
+        s = stage(ib32, in, C, wb, kSpan, lane);
+      }
+      if (src + L <= wb + kSpan) {
+        const uint8_t* q = ibb + s + (src - wb);
+        for (uint32_t i = lane; i < L; i += 64) ob[o + i] = q[i];
+      } else {
+        for (uint32_t i = lane; i < L; i += 64) ob[o + i] = in[src + i];
+      }
     } else if (t.off >= L) {
       for (uint32_t i = lane; i < L; i += 64) ob[o + i] = ob[o - t.off + i];
     } else {
@@ -483,7 +539,7 @@ __global__ __launch_bounds__(64) void snappy_dfrag(const uint8_t* __restrict__ i
   if ((reinterpret_cast<uintptr_t>(d) & 15) == 0) {
     const uint32_t nv = end >> 4;
     for (uint32_t i = lane; i < nv; i += 64)
-      reinterpret_cast<uint4*>(d)[i] = reinterpret_cast<const uint4*>(ob)[i];
+      reinterpret_cast<uint4*>(d)[i] = reinterpret_cast<const uint4*>(ob32)[i];
     for (uint32_t i = (nv << 4) + lane; i < end; i += 64) d[i] = ob[i];
   } else {
     for (uint32_t i = lane; i < end; i += 64) d[i] = ob[i];
@@ -550,7 +606,7 @@ int snappy_compress_launch(const void* in, size_t n, void* out, void* scratch, h
 size_t snappy_uncompress_scratch(size_t C, size_t dsize) {
   const size_t nwin = (C + kWin - 1) / kWin + 1;
   const size_t nfo = (dsize + kFrag - 1) / kFrag + 1;
-  return nwin * (kWin / 8) + C * 4 + nwin * 8 * 4 + nfo * 8 + 256;
+  return nwin * (kWin / 8) + C * 4 + nwin * 8 * (2 * kStarts + 2) + nfo * 8 + 256;
 }
 
 int snappy_uncompress_launch(const void* in, size_t C, uint32_t hdr, size_t dsize, void* out, void* scratch,
@@ -562,8 +618,8 @@ int snappy_uncompress_launch(const void* in, size_t C, uint32_t hdr, size_t dsiz
   uint8_t* s = static_cast<uint8_t*>(scratch);
   uint32_t* flags = reinterpret_cast<uint32_t*>(s);
   uint64_t* wexit = reinterpret_cast<uint64_t*>(s + 64);
-  uint64_t* wtotal = wexit + (nwin + 1);
-  uint64_t* wentry = wtotal + (nwin + 1);
+  uint64_t* wtotal = wexit + (size_t)(nwin + 1) * kStarts;
+  uint64_t* wentry = wtotal + (size_t)(nwin + 1) * kStarts;
   uint64_t* woff = wentry + (nwin + 1);
   uint64_t* fragpos = woff + (nwin + 1);
   uint32_t* bitmap = reinterpret_cast<uint32_t*>(fragpos + (nfo + 1));

@@ -48,3 +48,33 @@ def test_adapter_matches_reference_filter(harness, dtype, nb):
 def test_adapter_rejects_like_reference(harness):
     x = np.full(64, 40.0, np.float32)  # fixing_float.h:71 CHECK_GT(bin, 0)
     assert _run(harness, x, 1, 1) == -1
+
+
+def _sig(L):
+    L.psadapter_compare_compress.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_int]
+    L.psadapter_compare_compress.restype = C.c_int
+    L.psadapter_compare_noise.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.c_float, C.c_float]
+    L.psadapter_compare_noise.restype = C.c_int
+
+
+@pytest.mark.parametrize("nkeys", [0, 5, 3000, 200_000])
+def test_adapter_compressing_matches_reference(harness, nkeys):
+    """CompressingFilter (compressing.h:8-37): same snappy bytes for keys and
+    values, same uncompressed_size, each side decodes the other's output."""
+    _sig(harness)
+    rng = np.random.default_rng(nkeys)
+    keys = np.sort(rng.choice(10**9, size=nkeys, replace=False)).astype(np.uint64)
+    for vals in (rng.standard_normal(nkeys + 7).astype(np.float32),
+                 np.clip(rng.standard_normal(70_000) * 20 + 128, 0, 255).astype(np.uint8),
+                 np.zeros(0, np.float32)):
+        rc = harness.psadapter_compare_compress(keys.ctypes.data if nkeys else None, keys.nbytes,
+                                                vals.ctypes.data if vals.size else None, vals.nbytes, 9)
+        assert rc == 0, (rc, harness.psadapter_last_error())
+
+
+@pytest.mark.parametrize("dtype", [np.float32])
+def test_adapter_noise_matches_reference(harness, dtype):
+    _sig(harness)
+    x = np.linspace(-1, 1, 5001).astype(dtype)
+    rc = harness.psadapter_compare_noise(x.ctypes.data, x.nbytes, 9, 0.5, 2.0)
+    assert rc == 0, (rc, harness.psadapter_last_error())
