@@ -37,6 +37,17 @@ GIB = float(1 << 30)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, MI355X_MICROARCH.md
 
 
+WORKLOADS = {
+    "c2": "C2 (BASELINE configs[1]): dense f32 values, chain [FIXING_FLOAT num_bytes={nb}], "
+          "min/max computed, encode+decode round trip per step",
+    "c3": "C3 (BASELINE configs[2]): 10M uint64 keys @1% of [0,1e9) + f32 values, chain "
+          "[KEY_CACHING, FIXING_FLOAT num_bytes={nb}], repeat send (key cache hit: keys elided)",
+    "c3miss": "C3 (BASELINE configs[2]) first-send path: 10M uint64 keys @1% of [0,1e9) + f32 "
+              "values, chain [KEY_CACHING(clear_cache_if_done), FIXING_FLOAT num_bytes={nb}], "
+              "every send a key cache miss",
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -48,16 +59,28 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c3miss"],
+                    help="c2: dense f32 values (default, the headline); c3: 10M sorted uint64 "
+                         "keys from [0,1e9) + f32 values, [KEY_CACHING, FIXING_FLOAT] repeat "
+                         "sends (cache hits); c3miss: same with clear_cache_if_done (every send "
+                         "a miss)")
+    ap.add_argument("--m", type=int, default=10_000_000, help="c3: keys per message")
     return ap.parse_args()
 
 
-def cpu_baseline(n_sample: int, nb: int, seconds: float):
+def cpu_baseline(n_sample: int, nb: int, seconds: float, config: str = "c2"):
     import ctypes as C
 
     import numpy as np
 
     import oracle
     x = np.random.default_rng(1).standard_normal(n_sample).astype(np.float32)
+    keys = None
+    if config != "c2":  # C3 sample: sorted unique keys from [0, 1e9), KEY_CACHING first
+        keys = np.unique(np.random.default_rng(3).integers(0, 10**9, n_sample + n_sample // 8,
+                                                            dtype=np.uint64))[:n_sample]
+        keys = np.ascontiguousarray(keys[:x.size])
+        x = x[:keys.size]
     kind = "port"
     try:
         R = oracle.Ref()
@@ -70,7 +93,11 @@ def cpu_baseline(n_sample: int, nb: int, seconds: float):
         R.set_time(12345)
         snd, rcv = L.psref_node_new(), L.psref_node_new()
         while t < seconds or reps == 0:
-            m = R.msg_new(request=True, push=True)
+            m = R.msg_new(request=True, push=True, key_range=(0, 10**9))
+            if keys is not None:
+                L.psref_msg_set_key(m, keys.ctypes.data_as(C.c_void_p), keys.nbytes, 8)
+                kf = L.psref_msg_add_filter(m, 1)
+                L.psref_fc_set_clear_cache(m, kf, int(config == "c3miss"))
             L.psref_msg_add_value(m, x.ctypes.data_as(C.c_void_p), x.nbytes, 9)
             fi = L.psref_msg_add_filter(m, 3)
             L.psref_fc_set_num_bytes(m, fi, nb)
@@ -90,13 +117,15 @@ def cpu_baseline(n_sample: int, nb: int, seconds: float):
             P.ff_decode(codes, nb, mn, mx)
             t += time.perf_counter() - t0
             reps += 1
+    payload = x.nbytes + (keys.nbytes if keys is not None else 0)
+    chain = "FIXING_FLOAT" if keys is None else "KEY_CACHING+FIXING_FLOAT"
     return {
-        "value": round(reps * x.nbytes / t / GIB, 4),
+        "value": round(reps * payload / t / GIB, 4),
         "unit": "GiB/s",
         "cores": 1,
         "kind": kind,
-        "sample": f"{reps} x FIXING_FLOAT(nb={nb}) encode+decode of 2^{n_sample.bit_length() - 1} f32 "
-                  f"({x.nbytes >> 20} MiB), single-threaded as the reference's filters run, "
+        "sample": f"{reps} x {chain}(nb={nb}) encode+decode of 2^{n_sample.bit_length() - 1} f32 "
+                  f"({payload >> 20} MiB payload), single-threaded as the reference's filters run, "
                   f"{t:.1f} s CPU",
         "cpu_model": _cpu_model(),
         "nproc": os.cpu_count(),
@@ -138,28 +167,48 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
 
-    from parameter_server_amd import FIXING_FLOAT
+    from parameter_server_amd import FIXING_FLOAT, KEY_CACHING
     from parameter_server_amd import filter as F
 
     n, nb = args.n, args.nb
-    # this rank's shard of the key range (range.h:100-107 EvenDivide), pre-placed.
-    # Consecutive steps use different messages (args.bufs distinct arrays whose
-    # total exceeds the 256 MiB Infinity Cache), so no step reads data a
-    # previous step left on chip.
-    g = torch.Generator(device=f"cuda:{local}")
+    dev = f"cuda:{local}"
+    g = torch.Generator(device=dev)
     g.manual_seed(1 + rank)
-    xs = [torch.randn(n, device=f"cuda:{local}", generator=g, dtype=torch.float32)
-          for _ in range(args.bufs)]
-
     ctx = F.Context(local)
     worker, server = F.RemoteNode(ctx), F.RemoteNode(ctx)
     F.set_clock(12345)  # FIXING_FLOAT seed (time(NULL) in the reference)
     tmpls = []
-    for x in xs:
-        t = F.Message(request=True, push=True, key_channel=0)
-        t.add_value(x)
-        t.add_filter(FIXING_FLOAT, num_bytes=nb)
-        tmpls.append(t)
+    if args.config == "c2":
+        # this rank's shard of the key range (range.h:100-107 EvenDivide),
+        # pre-placed.  Consecutive steps use different messages (args.bufs
+        # distinct arrays whose total exceeds the 256 MiB Infinity Cache), so no
+        # step reads data a previous step left on chip.
+        xs = [torch.randn(n, device=dev, generator=g, dtype=torch.float32) for _ in range(args.bufs)]
+        for x in xs:
+            t = F.Message(request=True, push=True, key_channel=0)
+            t.add_value(x)
+            t.add_filter(FIXING_FLOAT, num_bytes=nb)
+            tmpls.append(t)
+        payload = 4 * n  # key bytes 0 (dense values), value bytes 4n
+    else:
+        # C3: m sorted unique keys sampled without replacement from [0, 1e9)
+        # (SURVEY.md §8(d)), one f32 value per key; the worker's push stream
+        # repeats the key set (KEY_CACHING hit) or clears it after every
+        # send (c3miss: clear_cache_if_done on push, key_caching.h:30-33)
+        m = args.m
+        keys = torch.unique(torch.randint(0, 10**9, (m + m // 8,), device=dev, generator=g))
+        keys = torch.sort(keys[torch.randperm(keys.numel(), device=dev, generator=g)[:m]])[0]
+        assert keys.numel() == m
+        n = m
+        xs = [torch.randn(m, device=dev, generator=g, dtype=torch.float32) for _ in range(args.bufs)]
+        for x in xs:
+            t = F.Message(request=True, push=True, key_channel=0, key_range=(0, 10**9))
+            t.set_key(keys)
+            t.add_value(x)
+            t.add_filter(KEY_CACHING, clear_cache_if_done=(args.config == "c3miss"))
+            t.add_filter(FIXING_FLOAT, num_bytes=nb)
+            tmpls.append(t)
+        payload = 12 * m  # 8m key bytes + 4m value bytes
     tmpl = tmpls
 
     worker.roundtrip(server, tmpl, args.warmup)
@@ -198,7 +247,6 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    payload = 4 * n  # key bytes 0 (dense values), value bytes 4n
     value = world * args.steps * payload / elapsed / GIB
 
     roofline = None
@@ -225,7 +273,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(1 << 24, nb, args.cpu_seconds)
+        cpu = cpu_baseline(1 << 24 if args.config == "c2" else 1 << 22, nb, args.cpu_seconds, args.config)
 
     if rank == 0:
         line = {
@@ -240,10 +288,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic: f32 N(0,1) values, seed 1+rank, FIXING_FLOAT LCG seed 12345",
+            "data": "synthetic: f32 N(0,1) values, seed 1+rank, FIXING_FLOAT LCG seed 12345"
+                    + ("" if args.config == "c2" else "; sorted unique uint64 keys from [0,1e9)"),
             "config": {
-                "workload": "C2 (BASELINE configs[1]): dense f32 values, chain [FIXING_FLOAT "
-                            f"num_bytes={nb}], min/max computed, encode+decode round trip per step",
+                "workload": WORKLOADS[args.config].format(nb=nb),
                 "n_values_per_gpu": n,
                 "payload_bytes_per_step_per_gpu": payload,
                 "value_type": "float32",

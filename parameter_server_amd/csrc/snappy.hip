@@ -302,7 +302,7 @@ __global__ __launch_bounds__(256) void snappy_pack(const uint8_t* __restrict__ s
 }
 
 // ------------------------------------------------------------------ uncompress
-constexpr uint32_t kWin = 65536;   // compressed bytes per parse window
+constexpr uint32_t kWin = 16384;   // compressed bytes per parse window (16 KiB: ~8 waves per CU)
 constexpr uint32_t kInWin = 8192;  // staged compressed bytes in the fragment decoder
 constexpr uint64_t kNone = ~0ull;
 constexpr uint32_t kFlagInvalid = 1, kFlagSerial = 2;
@@ -355,6 +355,31 @@ __device__ __forceinline__ Tag parse_tag(const uint8_t* b, uint64_t p) {
   return t;
 }
 
+// Branch-free decode of the tag whose first 5 bytes are x (little endian).
+__device__ __forceinline__ Tag decode_tag(uint64_t x, uint64_t p) {
+  Tag t;
+  const uint32_t c = (uint32_t)x & 0xff;
+  const uint32_t ty = c & 3;
+  const uint32_t k = (c >> 2) + 1 > 60 ? (c >> 2) + 1 - 60 : 0;  // literal length bytes
+  const uint64_t litlen = k ? ((x >> 8) & ((1ull << (8 * k)) - 1)) + 1 : (c >> 2) + 1;
+  const uint32_t off1 = ((c >> 5) << 8) | (uint32_t)((x >> 8) & 0xff);
+  const uint32_t off2 = (uint32_t)((x >> 8) & 0xffff);
+  const uint32_t off4 = (uint32_t)(x >> 8);
+  t.lit = ty == 0;
+  t.hl = ty == 0 ? 1 + k : ty == 1 ? 2 : ty == 2 ? 3 : 5;
+  t.len = ty == 0 ? litlen : ty == 1 ? 4 + ((c >> 2) & 7) : (c >> 2) + 1;
+  t.off = ty == 0 ? 0 : ty == 1 ? off1 : ty == 2 ? off2 : off4;
+  t.next = p + t.hl + (ty == 0 ? litlen : 0);
+  return t;
+}
+
+// tag at LDS byte q of w (one two-dword read; q + 8 bytes must be staged)
+__device__ __forceinline__ Tag lds_tag(const uint32_t* w, uint64_t q, uint64_t p) {
+  const uint32_t i = (uint32_t)(q >> 2);
+  const uint64_t x = (((uint64_t)w[i + 1] << 32) | w[i]) >> (8 * (q & 3));
+  return decode_tag(x, p);
+}
+
 // Stage in[base, base+want) into LDS: aligned dword loads where the whole word
 // lies inside the input, bytes at the edges (0 past the end).  Returns s with
 // lds[s + i] == in[base + i].
@@ -393,7 +418,6 @@ __global__ __launch_bounds__(64) void snappy_dscan(const uint8_t* __restrict__ i
   const uint32_t s = stage(b32, in, C, base, wl + 16, lane);
   for (uint32_t i = lane; i < kWin / 32; i += 64) bm[i] = 0;
   __syncthreads();
-  const uint8_t* b = reinterpret_cast<const uint8_t*>(b32) + s;
   uint64_t p = lane, o = 0;
   bool alive = p < wl;
   while (__ballot(alive)) {
@@ -402,7 +426,7 @@ __global__ __launch_bounds__(64) void snappy_dscan(const uint8_t* __restrict__ i
         atomicOr(&bm[p >> 5], 1u << (p & 31));
         cum[base + p] = (uint32_t)o;
       }
-      const Tag t = parse_tag(b + p, p);
+      const Tag t = lds_tag(b32, s + p, p);
       o += t.len;
       p = t.next;
       alive = p < wl;
@@ -472,11 +496,10 @@ __global__ __launch_bounds__(64) void snappy_dindex(const uint8_t* __restrict__ 
   const uint32_t s = stage(b32, in, C, base, wl + 16, lane);
   __syncthreads();
   if (lane != 0) return;
-  const uint8_t* b = reinterpret_cast<const uint8_t*>(b32) + s;
   uint64_t p = e - base, o = woff[w];
   uint32_t fl = 0;
   while (p < wl) {
-    const Tag t = parse_tag(b + p, p);
+    const Tag t = lds_tag(b32, s + p, p);
     if (!t.lit) {
       if (t.off == 0 || t.off > o) fl |= kFlagInvalid;
       else if (o - t.off < (o & ~(uint64_t)(kFrag - 1))) fl |= kFlagSerial;
@@ -512,7 +535,7 @@ __global__ __launch_bounds__(64) void snappy_dfrag(const uint8_t* __restrict__ i
       wb = p;
       s = stage(ib32, in, C, wb, kSpan, lane);
     }
-    const Tag t = parse_tag(ibb + s + (p - wb), p);
+    const Tag t = lds_tag(ib32, s + (p - wb), p);
     const uint32_t L = (uint32_t)t.len;
     if (t.lit) {
       const uint64_t src = p + t.hl;
