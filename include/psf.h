@@ -153,6 +153,17 @@ int psf_msg_clone(const psf_message* msg, psf_message** out);
  * message or key cache refers to it).  loc = PSF_LOC_DEVICE / PSF_LOC_HOST. */
 int psf_msg_set_key(psf_message* msg, void* ptr, size_t bytes, int key_type, int loc);
 int psf_msg_add_value(psf_message* msg, void* ptr, size_t bytes, int value_type, int loc);
+/* The Task frame of the wire (van.cc:122-191: [Task][key][value...]): the
+ * fields the filter path reads and writes, protobuf wire format with the
+ * reference's field numbers (task.proto, filter.proto).  serialize: buf = NULL
+ * asks for the length; has_key is set from the key as Van::Send does.  parse:
+ * a new message with that Task and no buffers (attach the key / value frames
+ * with psf_msg_set_key / psf_msg_add_value); PSF_ERR_CHECK where protobuf's
+ * ParseFromArray fails. */
+int psf_task_serialize(const psf_message* msg, void* buf, size_t cap, size_t* len);
+int psf_task_parse(const void* buf, size_t len, psf_message** out);
+/* Replace value array i by a caller buffer (e.g. a received frame, van.cc:244-255). */
+int psf_msg_set_value(psf_message* msg, int i, void* ptr, size_t bytes, int loc);
 int psf_msg_key(const psf_message* msg, void** ptr, size_t* bytes, int* loc);
 int psf_msg_key_info(const psf_message* msg, int* has_key_flag, int* key_type);
 int psf_msg_num_values(const psf_message* msg);

@@ -66,6 +66,9 @@ SIGNATURES = {
     "psf_msg_clone": ([vp, C.POINTER(vp)], C.c_int),
     "psf_msg_set_key": ([vp, vp, sz, C.c_int, C.c_int], C.c_int),
     "psf_msg_add_value": ([vp, vp, sz, C.c_int, C.c_int], C.c_int),
+    "psf_msg_set_value": ([vp, C.c_int, vp, sz, C.c_int], C.c_int),
+    "psf_task_serialize": ([vp, vp, sz, C.POINTER(sz)], C.c_int),
+    "psf_task_parse": ([vp, sz, C.POINTER(vp)], C.c_int),
     "psf_msg_key": ([vp, C.POINTER(vp), C.POINTER(sz), PI], C.c_int),
     "psf_msg_key_info": ([vp, PI, PI], C.c_int),
     "psf_msg_num_values": ([vp], C.c_int),

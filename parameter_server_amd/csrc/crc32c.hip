@@ -95,6 +95,97 @@ __global__ __launch_bounds__(kBlock) void crc32c_chunks(const uint8_t* __restric
   }
 }
 
+// ---- single-workgroup path (KEY_CACHING: <= 2 KiB, latency-bound) ----------
+// Lane t CRCs the 8 bytes [n - 8(256-t), n - 8(255-t)) (clipped at 0, so the
+// short chunk is lane 0's), then a shift-and-XOR tree combines neighbours; every
+// right-hand block at level j is 8*2^j bytes long, so the operator x^(64*2^j)
+// is a compile-time constant, applied as eight nibble-table lookups.
+constexpr uint32_t multmodp_c(uint32_t a, uint32_t b) {
+  uint32_t p = 0;
+  for (int i = 31; i >= 0; --i) {
+    if (a & (1u << i)) p ^= b;
+    b = (b & 1u) ? (b >> 1) ^ kCrcPoly : (b >> 1);
+  }
+  return p;
+}
+struct NibbleOps {
+  uint32_t t[8][8][16];  // [level j][nibble q][value v] = (v << 4q) * x^(64*2^j) mod P
+};
+constexpr NibbleOps make_nibble_ops() {
+  NibbleOps o{};
+  uint32_t k = 1u << 31;  // x^0
+  uint32_t x8 = 1u << 23;  // x^8
+  // x^64 = (x^8)^8
+  uint32_t x64 = 1u << 31;
+  for (int i = 0; i < 8; ++i) x64 = multmodp_c(x64, x8);
+  k = x64;
+  for (int j = 0; j < 8; ++j) {
+    for (int q = 0; q < 8; ++q)
+      for (uint32_t v = 0; v < 16; ++v) o.t[j][q][v] = multmodp_c(v << (4 * q), k);
+    k = multmodp_c(k, k);  // x^(64*2^(j+1))
+  }
+  return o;
+}
+__constant__ NibbleOps kNibbleOps = make_nibble_ops();
+
+__device__ __forceinline__ uint32_t shift_op(const uint32_t (*t)[16], uint32_t a) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) r ^= t[q][(a >> (4 * q)) & 15];
+  return r;
+}
+
+__global__ __launch_bounds__(kBlock) void crc32c_small(const uint8_t* __restrict__ d, uint32_t n,
+                                                        uint32_t* __restrict__ out, PubSlot* pub,
+                                                        uint32_t ticket) {
+  __shared__ uint32_t table[256];
+  __shared__ uint32_t ops[8][8][16];
+  __shared__ uint32_t wave_acc[kBlock / 64];
+  const uint32_t t = threadIdx.x;
+  // the 8 bytes of this lane (issued first: the longest latency)
+  const int64_t e = (int64_t)n - 8 * (int64_t)(kBlock - 1 - t);
+  const int64_t b = e - 8;
+  uint8_t bytes[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) bytes[i] = (b + i >= 0 && b + i < e) ? d[b + i] : 0;
+  {
+    uint32_t c = t;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (kCrcPoly & (0u - (c & 1u)));
+    table[t] = c;
+    const uint32_t* src = &kNibbleOps.t[0][0][0];
+    uint32_t* dst = &ops[0][0][0];
+    for (uint32_t i = t; i < 8 * 8 * 16; i += kBlock) dst[i] = src[i];
+  }
+  __syncthreads();
+  uint32_t v = 0;  // crc32c of this lane's bytes ("" -> 0)
+  if (e > 0) {
+    uint32_t l = 0xFFFFFFFFu;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (b + i >= 0) l = table[(l ^ bytes[i]) & 0xFF] ^ (l >> 8);
+    v = l ^ 0xFFFFFFFFu;
+  }
+  // crc(L || R) = shift(crc(L), |R|) ^ crc(R), |R| = 8 * 2^j at level j
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    const uint32_t r = __shfl_down(v, 1u << j, 64);
+    if ((t & ((2u << j) - 1)) == 0) v = shift_op(ops[j], v) ^ r;
+  }
+  if ((t & 63) == 0) wave_acc[t >> 6] = v;
+  __syncthreads();
+  if (t == 0) {
+    uint32_t acc = wave_acc[0];
+#pragma unroll
+    for (int w = 1; w < kBlock / 64; ++w) acc = shift_op(ops[6], acc) ^ wave_acc[w];  // 512-byte blocks
+    *out = acc;
+    if (pub) {
+      pub->crc = acc;
+      publish_ticket(pub, ticket);
+    }
+  }
+}
+
 static X2nTable make_x2n_table() {
   X2nTable t;
   uint32_t p = 1u << 30;  // x^1
@@ -108,10 +199,9 @@ int crc32c_launch(const void* d, size_t n, uint32_t* out, hipStream_t st, Profil
   static const X2nTable tbl = make_x2n_table();
   if (n == 0) return kErrArg;  // crc32c("") == 0: callers answer that on the host
   if (n <= kCrcSingleBlock) {
-    size_t chunk = ((n + kBlock - 1) / kBlock + 3) & ~(size_t)3;
     ProfScope ps(prof, kKCrc, st, (double)n);
-    hipLaunchKernelGGL(crc32c_chunks, dim3(1), dim3(kBlock), 0, st, static_cast<const uint8_t*>(d),
-                       n, chunk, out, tbl, pub, ticket);
+    hipLaunchKernelGGL(crc32c_small, dim3(1), dim3(kBlock), 0, st, static_cast<const uint8_t*>(d),
+                       (uint32_t)n, out, pub, ticket);
     return launch_status();
   }
   if (hipMemsetAsync(out, 0, sizeof(uint32_t), st) != hipSuccess) return kErrHip;

@@ -8,6 +8,7 @@
 #include "filter.h"
 #include "slice.h"
 #include "snappy_host.h"
+#include "wire.h"
 
 struct psf_context { psf::Context* impl; };
 struct psf_node { psf::RemoteNode* impl; };
@@ -286,6 +287,7 @@ int psf_msg_set_key(psf_message* msg, void* ptr, size_t bytes, int key_type, int
     msg->m.key = wrap(ptr, bytes, loc);
     t.has_key = msg->m.key.bytes > 0;
     t.key_type = key_type;
+    t.has_key_type = true;
     if (!t.has_key_range) { t.has_key_range = true; t.key_range = psf::KeyRange::All(); }
     return PSF_OK;
   });
@@ -295,6 +297,39 @@ int psf_msg_add_value(psf_message* msg, void* ptr, size_t bytes, int value_type,
     if (!msg) return PSF_ERR_ARG;
     msg->m.task.value_type.push_back(value_type);
     msg->m.value.push_back(wrap(ptr, bytes, loc));
+    return PSF_OK;
+  });
+}
+int psf_msg_set_value(psf_message* msg, int i, void* ptr, size_t bytes, int loc) {
+  return guarded([&] {
+    if (!msg || i < 0 || i >= (int)msg->m.value.size()) return PSF_ERR_ARG;
+    msg->m.value[i] = wrap(ptr, bytes, loc);
+    return PSF_OK;
+  });
+}
+int psf_task_serialize(const psf_message* msg, void* buf, size_t cap, size_t* len) {
+  return guarded([&] {
+    if (!msg || !len) return PSF_ERR_ARG;
+    psf::Task t = msg->m.task;
+    t.has_key = !msg->m.key.empty();  // van.cc:131-137 double check
+    const std::string s = psf::serialize_task(t);
+    *len = s.size();
+    if (!buf || cap < s.size()) return buf ? PSF_ERR_ARG : PSF_OK;
+    memcpy(buf, s.data(), s.size());
+    return PSF_OK;
+  });
+}
+int psf_task_parse(const void* buf, size_t len, psf_message** out) {
+  return guarded([&] {
+    if (!out || (len && !buf)) return PSF_ERR_ARG;
+    auto* m = new psf_message();
+    try {
+      psf::parse_task(static_cast<const uint8_t*>(buf), len, &m->m.task);
+    } catch (...) {
+      delete m;
+      throw;
+    }
+    *out = m;
     return PSF_OK;
   });
 }
@@ -331,16 +366,27 @@ int psf_msg_add_filter(psf_message* msg, int type) {
   });
 }
 int psf_fc_set_num_bytes(psf_message* msg, int idx, int nb) {
-  return guarded([&] { fc_at(msg, idx)->num_bytes = nb; return PSF_OK; });
+  return guarded([&] {
+    auto* f = fc_at(msg, idx);
+    f->num_bytes = nb;
+    f->has_num_bytes = true;
+    return PSF_OK;
+  });
 }
 int psf_fc_set_clear_cache(psf_message* msg, int idx, int v) {
-  return guarded([&] { fc_at(msg, idx)->clear_cache_if_done = v != 0; return PSF_OK; });
+  return guarded([&] {
+    auto* f = fc_at(msg, idx);
+    f->clear_cache_if_done = v != 0;
+    f->has_clear_cache_if_done = true;
+    return PSF_OK;
+  });
 }
 int psf_fc_set_noise(psf_message* msg, int idx, float mean, float sd) {
   return guarded([&] {
     auto* f = fc_at(msg, idx);
     f->mean = mean;
     f->std = sd;
+    f->has_mean = f->has_std = true;
     return PSF_OK;
   });
 }

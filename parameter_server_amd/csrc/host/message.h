@@ -64,6 +64,8 @@ struct FilterConfig {  // filter.proto:3-35
   bool has_signature = false;                  // field 2
   uint32_t signature = 0;
   std::vector<uint64_t> uncompressed_size;     // field 3
+  // proto2 has-bits of the optional fields above (what the wire carries)
+  bool has_clear_cache_if_done = false, has_num_bytes = false, has_mean = false, has_std = false;
 };
 
 struct Task {
@@ -72,6 +74,7 @@ struct Task {
   bool has_key_range = false;
   KeyRange key_range;
   bool has_key = false;
+  bool has_key_type = false;
   int key_type = 0;
   std::vector<int> value_type;
   std::deque<FilterConfig> filter;
@@ -89,6 +92,7 @@ struct Message {
   // message.h:70-76 (set_key<char>)
   void set_key(const Buffer& k) {
     task.key_type = 11;  // CHAR
+    task.has_key_type = true;
     if (has_key()) clear_key();
     task.has_key = true;
     key = k;

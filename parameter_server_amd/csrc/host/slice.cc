@@ -85,6 +85,7 @@ void slice_message(Context* ctx, const Message& msg, const std::vector<KeyRange>
     const size_t lo = pos[i], hi = pos[i + 1];
     ret.set_key(segment(msg.key, lo * key_bytes, (hi - lo) * key_bytes));
     ret.task.key_type = key_bytes == 8 ? 8 : 7;  // EncodeType<K>: UINT64 / UINT32
+    ret.task.has_key_type = true;
     for (const Buffer& v : msg.value) {
       const size_t k = v.bytes / nkeys;  // bytes per key
       if (nkeys * k != v.bytes) throw CheckError(kErrCheck, "CHECK_EQ(key.size() * k, v.size())");

@@ -190,6 +190,33 @@ class Message:
         check(lib().psf_msg_clone(self.h, C.byref(h)))
         return Message(_handle=h, _refs=self._refs)
 
+    # -- wire (van.cc:122-269) ------------------------------------------------
+    def task_bytes(self) -> bytes:
+        """The Task frame: protobuf wire format, the reference's field numbers."""
+        n = C.c_size_t()
+        check(lib().psf_task_serialize(self.h, None, 0, C.byref(n)))
+        buf = (C.c_uint8 * max(n.value, 1))()
+        check(lib().psf_task_serialize(self.h, buf, n.value, C.byref(n)))
+        return bytes(buf[:n.value])
+
+    @classmethod
+    def from_task_bytes(cls, b: bytes) -> "Message":
+        """A received message: the parsed Task, no key/value frames yet."""
+        h = C.c_void_p()
+        raw = (C.c_uint8 * max(len(b), 1)).from_buffer_copy(b + b"\0")
+        check(lib().psf_task_parse(raw, len(b), C.byref(h)))
+        return cls(_handle=h)
+
+    def frames(self, device=None):
+        """[Task][key][value...] as Van::Send emits them (van.cc:122-191); the
+        key frame only when the key is non-empty.  Buffers are copied to host."""
+        out = [self.task_bytes()]
+        p, n, loc = self.key_ptr()
+        arrays = ([(p, n, loc)] if n else []) + [self.value_ptr(i) for i in range(self.num_values())]
+        for p, n, loc in arrays:
+            out.append(copy_out(p, n, loc, device).cpu().numpy().tobytes() if n else b"")
+        return out
+
     @staticmethod
     def _loc(t: torch.Tensor) -> int:
         return LOC_DEVICE if t.is_cuda else LOC_HOST
