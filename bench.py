@@ -45,7 +45,21 @@ WORKLOADS = {
     "c3miss": "C3 (BASELINE configs[2]) first-send path: 10M uint64 keys @1% of [0,1e9) + f32 "
               "values, chain [KEY_CACHING(clear_cache_if_done), FIXING_FLOAT num_bytes={nb}], "
               "every send a key cache miss",
+    "c5": "C5 (BASELINE configs[4]) per GPU: 2^20 uint64 keys spread over 2^64 (splitmix64) + "
+          "embedding rows dim=128 f32 (512 MiB, one min/max per array), chain [KEY_CACHING, "
+          "FIXING_FLOAT num_bytes={nb}{cmp}], repeat send (key cache hit)",
 }
+
+
+def splitmix64_keys(m: int, seed: int):
+    """m sorted unique uint64 keys splitmix64(seed + i)."""
+    import numpy as np
+    with np.errstate(over="ignore"):
+        z = (np.arange(m, dtype=np.uint64) + np.uint64(seed)) * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return np.unique(z)
 
 
 def parse():
@@ -59,12 +73,13 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
-    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c3miss"],
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c3miss", "c5"],
                     help="c2: dense f32 values (default, the headline); c3: 10M sorted uint64 "
                          "keys from [0,1e9) + f32 values, [KEY_CACHING, FIXING_FLOAT] repeat "
                          "sends (cache hits); c3miss: same with clear_cache_if_done (every send "
                          "a miss)")
-    ap.add_argument("--m", type=int, default=10_000_000, help="c3: keys per message")
+    ap.add_argument("--m", type=int, default=None, help="keys per message (c3: 10M, c5: 2^20)")
+    ap.add_argument("--compress", action="store_true", help="append COMPRESSING to the chain (c5)")
     return ap.parse_args()
 
 
@@ -167,7 +182,7 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
 
-    from parameter_server_amd import FIXING_FLOAT, KEY_CACHING
+    from parameter_server_amd import COMPRESSING, FIXING_FLOAT, KEY_CACHING
     from parameter_server_amd import filter as F
 
     n, nb = args.n, args.nb
@@ -190,12 +205,28 @@ def main():
             t.add_filter(FIXING_FLOAT, num_bytes=nb)
             tmpls.append(t)
         payload = 4 * n  # key bytes 0 (dense values), value bytes 4n
+    elif args.config == "c5":
+        m = args.m or (1 << 20)
+        keys = torch.from_numpy(splitmix64_keys(m, 4 + rank).view("int64")).to(dev)
+        m = keys.numel()
+        n = m * 128
+        xs = [torch.randn(n, device=dev, generator=g, dtype=torch.float32) for _ in range(args.bufs)]
+        for x in xs:
+            t = F.Message(request=True, push=True, key_channel=0)
+            t.set_key(keys)
+            t.add_value(x)
+            t.add_filter(KEY_CACHING)
+            t.add_filter(FIXING_FLOAT, num_bytes=nb)
+            if args.compress:
+                t.add_filter(COMPRESSING)
+            tmpls.append(t)
+        payload = 8 * m + 4 * n
     else:
         # C3: m sorted unique keys sampled without replacement from [0, 1e9)
         # (SURVEY.md §8(d)), one f32 value per key; the worker's push stream
         # repeats the key set (KEY_CACHING hit) or clears it after every
         # send (c3miss: clear_cache_if_done on push, key_caching.h:30-33)
-        m = args.m
+        m = args.m or 10_000_000
         keys = torch.unique(torch.randint(0, 10**9, (m + m // 8,), device=dev, generator=g))
         keys = torch.sort(keys[torch.randperm(keys.numel(), device=dev, generator=g)[:m]])[0]
         assert keys.numel() == m
@@ -272,7 +303,7 @@ def main():
         }
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config != "c5":
         cpu = cpu_baseline(1 << 24 if args.config == "c2" else 1 << 22, nb, args.cpu_seconds, args.config)
 
     if rank == 0:
@@ -289,9 +320,10 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic: f32 N(0,1) values, seed 1+rank, FIXING_FLOAT LCG seed 12345"
-                    + ("" if args.config == "c2" else "; sorted unique uint64 keys from [0,1e9)"),
+                    + {"c2": "", "c5": "; sorted unique uint64 keys splitmix64(4+rank+i)"}.get(
+                        args.config, "; sorted unique uint64 keys from [0,1e9)"),
             "config": {
-                "workload": WORKLOADS[args.config].format(nb=nb),
+                "workload": WORKLOADS[args.config].format(nb=nb, cmp=", COMPRESSING" if args.compress else ""),
                 "n_values_per_gpu": n,
                 "payload_bytes_per_step_per_gpu": payload,
                 "value_type": "float32",

@@ -330,17 +330,18 @@ template <typename V, int NB>
 __device__ __forceinline__ uint32_t quant_fast(V xv, const QuantParams& q, bool& ok) {
   if (NB == 1 && sizeof(V) == 4) {
     const float x = (float)xv;
-    const float t = (fminf(fmaxf(x, q.min_f), q.max_f) - q.min_f) * q.scale_f;
+    // clamp in one v_med3 (min < max here); NaNs go to the exact path
+    const float t = (__builtin_amdgcn_fmed3f(x, q.min_f, q.max_f) - q.min_f) * q.scale_f;
     const float f = floorf(t);
-    const float fr = t - f;
-    ok = q.fast && fr > kGuard32 && fr < 1.0f - kGuard32;
+    // frac in (g, 1-g) as one compare: |frac - 1/2| < 1/2 - g (conservative
+    // where 1/2 - frac rounds; those values just take the exact path)
+    ok = q.fast & (fabsf((t - f) - 0.5f) < 0.5f - kGuard32) & (x == x);  // no branches
     return (uint32_t)f;
   }
   const double x = (double)xv;
   const double t = (fmin(fmax(x, q.min_v), q.max_v) - q.min_v) * q.scale;
   const double f = floor(t);
-  const double fr = t - f;
-  ok = q.fast && fr > kGuard64 && fr < 1.0 - kGuard64;
+  ok = q.fast & (fabs((t - f) - 0.5) < 0.5 - kGuard64);  // NaN t: false
   return (uint32_t)f;
 }
 
@@ -407,9 +408,10 @@ __device__ __forceinline__ uint64_t quant_floor(V xv, const QuantParams& q) {
 
 __device__ __forceinline__ uint32_t step17(uint32_t a, uint32_t c, uint32_t s) {
   // hipcc lowers a*s to the quarter-rate v_mul_lo_u32 even when both operands
-  // are known to fit 17 bits; v_mul_u32_u24 is full rate and exact here.
+  // are known to fit 17 bits; v_mul_u32_u24 is full rate and exact here.  `a`
+  // is wave-uniform (a kernel parameter) and is read straight from its SGPR.
   uint32_t r;
-  asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(s));
+  asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "s"(a), "v"(s));
   return (r + c) & kMask17;
 }
 
