@@ -19,8 +19,9 @@ step() {  # step <name> <seconds> <cmd...>
 }
 for s in "$@"; do
   case $s in
-    pytest) step pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
-    pytestall) step pytest_gpu 900 python -m pytest tests -m gpu -q ;;
+    pytest) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
+    pytestall) step pytest_gpu 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread ;;
+    hostedge) step host_edge 300 python tools/host_edge.py ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ;;
     benchq) step bench 600 python bench.py --no-cpu-baseline --steps 20 ;;
