@@ -205,6 +205,74 @@ int psf_msg_slice(psf_context* ctx, const psf_message* msg, const uint64_t* boun
 int psf_node_roundtrip(psf_node* snd, psf_node* rcv, const psf_message* const* tmpls, int ntmpl,
                        int iters, psf_message** out);
 
+/* ---- server-side consumers ------------------------
+ * What the receiving server does with a decoded message, fused with the
+ * FIXING_FLOAT dequantise: psf_node_set_defer_dequant(server, 1) makes
+ * FIXING_FLOAT's decode leave its codes pending (only where every filter
+ * listed before it is KEY_CACHING, so nothing decoded later reads values);
+ * the consumers below then dequantise in-register with ff_decode's exact
+ * arithmetic (fixing_float.h:89-101) and never materialise the float array. */
+int psf_node_set_defer_dequant(psf_node* node, int enable);
+/* value i still holds FIXING_FLOAT codes: *num_bytes > 0 and the range, else 0 */
+int psf_msg_pending(const psf_message* msg, int i, int* num_bytes, float* min_value, float* max_value);
+/* run the pending dequantise(s) now (what DecodeMessage would have produced) */
+int psf_msg_materialize(psf_context* ctx, psf_message* msg);
+
+/* AssignOpType (src/util/proto/assign_op.proto:4-13), the float subset
+ * AssignOp handles (src/util/assign_op.h:10-26) */
+#define PSF_OP_ASSIGN 0
+#define PSF_OP_PLUS 1
+#define PSF_OP_MINUS 2
+#define PSF_OP_TIMES 3
+#define PSF_OP_DIVIDE 4
+
+/* ParallelOrderedMatch (src/util/parallel_ordered_match.h:7-83): for every key
+ * of the sorted d_src_key also in the sorted d_dst_key,
+ * d_dst_val[j*k + i] op= d_src_val[s*k + i] (value_type FLOAT / DOUBLE); the
+ * r-th copy of a repeated key pairs with the r-th copy in dst, as the
+ * reference's two cursors do.  *n = matched keys * k (the reference's return
+ * value).  d_dst_val must hold ndst*k values (the reference zero-fills an
+ * empty one first, parallel_ordered_match.h:69-72).  Synchronous. */
+int psf_ordered_match(psf_context* ctx, const uint64_t* d_src_key, size_t nsrc, const void* d_src_val,
+                      const uint64_t* d_dst_key, size_t ndst, void* d_dst_val, int k, int value_type,
+                      int op, size_t* n);
+/* The same with the src values given as FIXING_FLOAT codes (num_bytes per
+ * value, range [min_value, max_value]); value_type FLOAT. */
+int psf_ff_decode_match(psf_context* ctx, const uint64_t* d_src_key, size_t nsrc, const void* d_code,
+                        int num_bytes, float min_value, float max_value, const uint64_t* d_dst_key,
+                        size_t ndst, void* d_dst_val, int k, int op, size_t* n);
+/* KVVector::SetValue's merge of value array i of a received message
+ * (src/parameter/kv_vector.h:182-183 / 205-207): src keys = the message's key;
+ * a pending FIXING_FLOAT array is dequantised in-register. */
+int psf_msg_ordered_match(psf_context* ctx, const psf_message* msg, int i, const uint64_t* d_dst_key,
+                          size_t ndst, void* d_dst_val, int k, int value_type, int op, size_t* n);
+
+/* KVMap<Key, float, FTRLEntry, SGDState> (src/parameter/kv_map.h:32-91,
+ * src/app/linear_method/async_sgd.h:42-154): the async-SGD server's model as a
+ * hash table in HBM (grows 2x on the device at load 1/2).  lr_type 1 CONSTANT /
+ * 2 DECAY with alpha, beta (LearningRateConfig, linear.proto:93-101); penalty
+ * ElasticNet(lambda1, lambda2) (penalty.h:41-91: L1 = (lambda[0], lambda[1] or
+ * 0), L2 = (0, lambda[0])).  CHECKs of LearningRate / ElasticNet ->
+ * PSF_ERR_CHECK.  `capacity` = expected number of keys (a hint). */
+typedef struct psf_kvmap psf_kvmap;
+int psf_kvmap_create(psf_context* ctx, size_t capacity, int lr_type, double alpha, double beta,
+                     double lambda1, double lambda2, psf_kvmap** out);
+int psf_kvmap_destroy(psf_kvmap* map);
+/* KVMap::SetValue on a push message: FTRLEntry::Set for every key (pending
+ * FIXING_FLOAT codes dequantised in-register).  Asynchronous; a failed
+ * CHECK_GT(eta, 0) is reported by the next psf_kvmap_stats. */
+int psf_kvmap_set_value(psf_kvmap* map, const psf_message* msg);
+/* KVMap::GetValue on a pull message: appends the FLOAT array of w. */
+int psf_kvmap_get_value(psf_kvmap* map, psf_message* msg);
+/* raw device arrays */
+int psf_kvmap_push(psf_kvmap* map, const uint64_t* d_keys, size_t n, const float* d_grad);
+int psf_kvmap_pull(psf_kvmap* map, const uint64_t* d_keys, size_t n, float* d_w);
+/* SGDState counters (async_sgd.h:106-125): nnz exactly; weight_sum and
+ * delta_sum accumulated in double (the reference sums the same float terms
+ * serially in float); size = stored keys.  Synchronous. */
+int psf_kvmap_stats(psf_kvmap* map, int64_t* nnz, double* weight_sum, double* delta_sum,
+                    uint64_t* size);
+
 /* ---- launch profiler (HIP events on the launch stream) ----------------- */
 #define PSF_K_MINMAX 0
 #define PSF_K_ENCODE 1
@@ -213,7 +281,10 @@ int psf_node_roundtrip(psf_node* snd, psf_node* rcv, const psf_message* const* t
 #define PSF_K_NOISE 4
 #define PSF_K_SNAPPY_COMPRESS 5
 #define PSF_K_SNAPPY_DECOMPRESS 6
-#define PSF_K_NUM 7
+#define PSF_K_MATCH 7
+#define PSF_K_KV_PUSH 8
+#define PSF_K_KV_GET 9
+#define PSF_K_NUM 10
 /* kernel_mask: bit k times kernel PSF_K_k (-1 = all, 0 = off) */
 int psf_profile_enable(psf_context* ctx, int kernel_mask);
 int psf_profile_reset(psf_context* ctx);

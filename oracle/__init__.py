@@ -95,6 +95,13 @@ class Port:
         L.port_snappy_uncompress.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
                                              C.POINTER(C.c_size_t)]
         L.port_snappy_uncompress.restype = C.c_int
+        L.port_ordered_match.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_size_t,
+                                         C.c_void_p, C.c_int, C.c_int, C.c_int]
+        L.port_ordered_match.restype = C.c_size_t
+        L.port_ftrl_update.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p,
+                                       C.c_void_p, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float,
+                                       C.POINTER(C.c_int64), C.POINTER(C.c_float), C.POINTER(C.c_float)]
+        L.port_ftrl_update.restype = C.c_int
 
     def ff_encode(self, x: np.ndarray, nb: int, seed: int, mn=None, mx=None):
         """Returns (status, codes:uint8[n*nb], min, max)."""
@@ -146,6 +153,68 @@ class Port:
     def snappy_uncompress(self, b, cap: int = 1 << 26):
         """(status, bytes): 0 ok, -1 bad header, -2 declared length > cap, -3 bad body."""
         return _uncompress(self.lib.port_snappy_uncompress, b, cap)
+
+    def ordered_match(self, src_key, src_val, dst_key, dst_val, k=1, op=0) -> int:
+        """ParallelOrderedMatch; dst_val is updated in place; returns *n."""
+        sk = np.ascontiguousarray(src_key, np.uint64)
+        dk = np.ascontiguousarray(dst_key, np.uint64)
+        sv = np.ascontiguousarray(src_val)
+        assert dst_val.flags.c_contiguous and dst_val.dtype == sv.dtype
+        dt = DT_FLOAT if sv.dtype == np.float32 else DT_DOUBLE
+        return int(self.lib.port_ordered_match(_ptr(sk), sk.size, _ptr(sv), _ptr(dk), dk.size,
+                                               _ptr(dst_val), k, dt, op))
+
+
+class FtrlModel:
+    """KVMap<Key, float, FTRLEntry, SGDState> restated for tests: a key ->
+    entry map (the reference's unordered_map, kv_map.h:65) in numpy arrays,
+    updated by oracle/psf_port.c's port_ftrl_update (async_sgd.h:137-151)."""
+
+    def __init__(self, port: "Port", lr_type=2, alpha=0.01, beta=10.0, lambda1=0.0, lambda2=0.0):
+        self.port = port
+        self.decay = 0 if lr_type == 1 else 1
+        self.alpha, self.beta = np.float32(alpha), np.float32(beta)
+        self.l1, self.l2 = np.float32(lambda1), np.float32(lambda2)
+        self.index = {}
+        cap = 1 << 10
+        self.w = np.zeros(cap, np.float32)
+        self.z = np.zeros(cap, np.float32)
+        self.sqrt_n = np.zeros(cap, np.float32)
+        self.nnz = C.c_int64(0)
+        self.weight_sum = C.c_float(0)
+        self.delta_sum = C.c_float(0)
+
+    def _entries(self, keys):
+        idx = np.empty(len(keys), np.int64)
+        for i, k in enumerate(keys.tolist()):
+            e = self.index.get(k)
+            if e is None:
+                e = self.index[k] = len(self.index)
+            idx[i] = e
+        if len(self.index) > self.w.size:
+            cap = 1 << (len(self.index) - 1).bit_length()
+            for a in ("w", "z", "sqrt_n"):
+                old = getattr(self, a)
+                new = np.zeros(cap, np.float32)
+                new[:old.size] = old
+                setattr(self, a, new)
+        return idx
+
+    def push(self, keys: np.ndarray, grad: np.ndarray) -> int:
+        idx = self._entries(np.asarray(keys, np.uint64))
+        g = np.ascontiguousarray(grad, np.float32)
+        return self.port.lib.port_ftrl_update(_ptr(idx), idx.size, _ptr(g), _ptr(self.w), _ptr(self.z),
+                                              _ptr(self.sqrt_n), self.decay, self.alpha, self.beta,
+                                              self.l1, self.l2, C.byref(self.nnz),
+                                              C.byref(self.weight_sum), C.byref(self.delta_sum))
+
+    def pull(self, keys: np.ndarray) -> np.ndarray:
+        out = np.zeros(len(keys), np.float32)
+        for i, k in enumerate(np.asarray(keys, np.uint64).tolist()):
+            e = self.index.get(k)
+            if e is not None:
+                out[i] = self.w[e]
+        return out
 
 
 class Ref:

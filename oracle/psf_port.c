@@ -245,3 +245,84 @@ int port_add_noise(void* data, size_t n, int dtype, float mean, float sd) {
   }
   return PORT_ERR_ARG;
 }
+
+/* ---- server-side consumers -------------------------- */
+
+/* AssignOp, src/util/assign_op.h:10-26 (ASSIGN..DIVIDE) */
+#define ASSIGN_OP(T, right, left, op)          \
+  do {                                         \
+    switch (op) {                              \
+      case 0: (right) = (left); break;         \
+      case 1: (right) += (left); break;        \
+      case 2: (right) -= (left); break;        \
+      case 3: (right) *= (left); break;        \
+      case 4: (right) /= (left); break;        \
+    }                                          \
+  } while (0)
+
+/* ParallelOrderedMatch, src/util/parallel_ordered_match.h:7-34 and 57-83, run
+ * on one thread (the grainsize split only partitions dst): skip the src
+ * prefix below dst[0] (lower_bound), then walk both sorted arrays with two
+ * cursors, applying op on equal keys and advancing both.  Returns *n (matched
+ * keys * k). */
+size_t port_ordered_match(const uint64_t* sk, size_t ns, const void* sv, const uint64_t* dk, size_t nd,
+                          void* dv, int k, int dtype, int op) {
+  if (nd == 0 || ns == 0) return 0;
+  size_t lo = 0, hi = ns;
+  while (lo < hi) {
+    size_t mid = lo + ((hi - lo) >> 1);
+    if (sk[mid] < dk[0]) lo = mid + 1; else hi = mid;
+  }
+  size_t s = lo, d = 0, n = 0;
+  while (d < nd && s < ns) {
+    if (sk[s] < dk[d]) {
+      ++s;
+    } else {
+      if (!(dk[d] < sk[s])) {
+        for (int i = 0; i < k; ++i) {
+          if (dtype == DT_FLOAT) ASSIGN_OP(float, ((float*)dv)[d * k + i], ((const float*)sv)[s * k + i], op);
+          else ASSIGN_OP(double, ((double*)dv)[d * k + i], ((const double*)sv)[s * k + i], op);
+        }
+        ++s;
+        n += (size_t)k;
+      }
+      ++d;
+    }
+  }
+  return n;
+}
+
+/* FTRLEntry::Set, src/app/linear_method/async_sgd.h:137-151, with
+ * LearningRate<float>::eval (learning_rate.h:15-22), ElasticNet<float>::proximal
+ * (penalty.h:51-56) and SGDState::UpdateWeight (async_sgd.h:106-116), applied
+ * serially to entries idx[0..n) of the state arrays (the caller maps keys to
+ * entries, as the reference's unordered_map does).  float arithmetic, one
+ * operation at a time.  Returns -1 where the reference's CHECK_GT(eta, 0)
+ * fails, else 0. */
+int port_ftrl_update(const int64_t* idx, size_t n, const float* grad, float* w, float* z, float* sqrt_n,
+                     int lr_decay, float alpha, float beta, float lambda1, float lambda2, int64_t* nnz,
+                     float* weight_sum, float* delta_sum) {
+  for (size_t i = 0; i < n; ++i) {
+    const int64_t e = idx[i];
+    const float w_old = w[e];
+    const float g = grad[i];
+    const float sqrt_n_new = (float)sqrt((double)(sqrt_n[e] * sqrt_n[e] + g * g));
+    const float sigma = (sqrt_n_new - sqrt_n[e]) / alpha;
+    z[e] += g - sigma * w[e];
+    sqrt_n[e] = sqrt_n_new;
+    const float eta = lr_decay ? alpha / (sqrt_n[e] + beta) : alpha;
+    const float zz = -z[e] * eta;
+    if (!(eta > 0)) return -1;
+    const float leta = lambda1 * eta;
+    float nw;
+    if (zz <= leta && zz >= -leta) nw = 0;
+    else nw = zz > 0 ? (zz - leta) / (1 + lambda2 * eta) : (zz + leta) / (1 + lambda2 * eta);
+    w[e] = nw;
+    if (nw == 0 && w_old != 0) --*nnz;
+    else if (nw != 0 && w_old == 0) ++*nnz;
+    *weight_sum += nw * nw;
+    const float delta = nw - w_old;
+    *delta_sum += delta * delta;
+  }
+  return 0;
+}

@@ -15,7 +15,7 @@ __all__ = ["lib", "PsfError", "FIXING_FLOAT", "KEY_CACHING", "COMPRESSING", "NOI
 def __getattr__(name):
     # torch-dependent wrappers load lazily so `import parameter_server_amd`
     # stays cheap for the C-ABI symbol checks
-    if name in ("Context", "Message", "RemoteNode", "set_clock", "copy_out"):
+    if name in ("Context", "Message", "RemoteNode", "KVMap", "set_clock", "copy_out"):
         from . import filter as _f
         return getattr(_f, name)
     raise AttributeError(name)

@@ -87,6 +87,23 @@ SIGNATURES = {
     "psf_node_roundtrip": ([vp, vp, C.POINTER(vp), C.c_int, C.c_int, C.POINTER(vp)], C.c_int),
     "psf_range_even_divide": ([u64, u64, u64, u64, C.POINTER(u64), C.POINTER(u64)], C.c_int),
     "psf_msg_slice": ([vp, vp, C.POINTER(u64), C.c_int, C.c_int, C.POINTER(vp), PI], C.c_int),
+    "psf_node_set_defer_dequant": ([vp, C.c_int], C.c_int),
+    "psf_msg_pending": ([vp, C.c_int, PI, C.POINTER(C.c_float), C.POINTER(C.c_float)], C.c_int),
+    "psf_msg_materialize": ([vp, vp], C.c_int),
+    "psf_ordered_match": ([vp, vp, sz, vp, vp, sz, vp, C.c_int, C.c_int, C.c_int, C.POINTER(sz)], C.c_int),
+    "psf_ff_decode_match": ([vp, vp, sz, vp, C.c_int, C.c_float, C.c_float, vp, sz, vp, C.c_int, C.c_int,
+                             C.POINTER(sz)], C.c_int),
+    "psf_msg_ordered_match": ([vp, vp, C.c_int, vp, sz, vp, C.c_int, C.c_int, C.c_int, C.POINTER(sz)],
+                              C.c_int),
+    "psf_kvmap_create": ([vp, sz, C.c_int, C.c_double, C.c_double, C.c_double, C.c_double, C.POINTER(vp)],
+                         C.c_int),
+    "psf_kvmap_destroy": ([vp], C.c_int),
+    "psf_kvmap_set_value": ([vp, vp], C.c_int),
+    "psf_kvmap_get_value": ([vp, vp], C.c_int),
+    "psf_kvmap_push": ([vp, vp, sz, vp], C.c_int),
+    "psf_kvmap_pull": ([vp, vp, sz, vp], C.c_int),
+    "psf_kvmap_stats": ([vp, C.POINTER(C.c_int64), C.POINTER(C.c_double), C.POINTER(C.c_double),
+                         C.POINTER(u64)], C.c_int),
     "psf_profile_enable": ([vp, C.c_int], C.c_int),
     "psf_profile_reset": ([vp], C.c_int),
     "psf_profile_read": ([vp, C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_double),
@@ -95,7 +112,8 @@ SIGNATURES = {
 }
 
 KERNELS = ("ff_minmax_partials", "ff_encode", "ff_decode", "crc32c_chunks", "noise_add",
-           "snappy_compress", "snappy_decompress")
+           "snappy_compress", "snappy_decompress", "ordered_match", "kvmap_push", "kvmap_get")
+OP_ASSIGN, OP_PLUS, OP_MINUS, OP_TIMES, OP_DIVIDE = 0, 1, 2, 3, 4
 
 _lib = None
 

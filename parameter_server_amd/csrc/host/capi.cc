@@ -6,6 +6,7 @@
 #include <string>
 
 #include "filter.h"
+#include "kvstore.h"
 #include "slice.h"
 #include "snappy_host.h"
 #include "wire.h"
@@ -13,6 +14,7 @@
 struct psf_context { psf::Context* impl; };
 struct psf_node { psf::RemoteNode* impl; };
 struct psf_message { psf::Message m; };
+struct psf_kvmap { psf::KvMapFtrl* impl; psf::Context* ctx; };
 
 namespace {
 thread_local std::string g_last_error;
@@ -492,7 +494,8 @@ int psf_profile_read(psf_context* ctx, int k, int64_t* launches, double* total_m
 }
 const char* psf_profile_kernel_name(int k) {
   static const char* names[] = {"ff_minmax_partials", "ff_encode", "ff_decode", "crc32c_chunks",
-                                "noise_add", "snappy_compress", "snappy_decompress"};
+                                "noise_add", "snappy_compress", "snappy_decompress", "ordered_match",
+                                "kvmap_push", "kvmap_get"};
   return (k >= 0 && k < psf::kKNum) ? names[k] : "?";
 }
 
@@ -508,6 +511,122 @@ int psf_fc_uncompressed(const psf_message* msg, int idx, int i, uint64_t* size) 
     const auto* f = fc_at(msg, idx);
     if (!size || i < 0 || i >= (int)f->uncompressed_size.size()) return PSF_ERR_ARG;
     *size = f->uncompressed_size[i];
+    return PSF_OK;
+  });
+}
+
+// ------------------------------------------------- server-side consumers
+int psf_node_set_defer_dequant(psf_node* node, int enable) {
+  return guarded([&] {
+    if (!node) return PSF_ERR_ARG;
+    node->impl->set_defer_dequant(enable != 0);
+    return PSF_OK;
+  });
+}
+int psf_msg_pending(const psf_message* msg, int i, int* num_bytes, float* min_value, float* max_value) {
+  if (!msg || i < 0 || i >= (int)msg->m.value.size()) return PSF_ERR_ARG;
+  const psf::PendingDequant pd = msg->m.is_pending(i) ? msg->m.pending[i] : psf::PendingDequant{};
+  if (num_bytes) *num_bytes = pd.nb;
+  if (min_value) *min_value = pd.min_value;
+  if (max_value) *max_value = pd.max_value;
+  return PSF_OK;
+}
+int psf_msg_materialize(psf_context* ctx, psf_message* msg) {
+  return guarded([&] {
+    if (!ctx || !msg) return PSF_ERR_ARG;
+    psf::materialize(ctx->impl, &msg->m);
+    return PSF_OK;
+  });
+}
+int psf_ordered_match(psf_context* ctx, const uint64_t* d_src_key, size_t nsrc, const void* d_src_val,
+                      const uint64_t* d_dst_key, size_t ndst, void* d_dst_val, int k, int value_type,
+                      int op, size_t* n) {
+  return guarded([&] {
+    if (!ctx || !n || k <= 0 || op < 0 || op > 4) return PSF_ERR_ARG;
+    if (value_type != PSF_DT_FLOAT && value_type != PSF_DT_DOUBLE) return PSF_ERR_ARG;
+    *n = psf::ordered_match_raw(ctx->impl, d_src_key, nsrc, d_src_val, psf::PendingDequant{}, d_dst_key,
+                                ndst, d_dst_val, value_type, k, op);
+    return PSF_OK;
+  });
+}
+int psf_ff_decode_match(psf_context* ctx, const uint64_t* d_src_key, size_t nsrc, const void* d_code,
+                        int num_bytes, float min_value, float max_value, const uint64_t* d_dst_key,
+                        size_t ndst, void* d_dst_val, int k, int op, size_t* n) {
+  return guarded([&] {
+    if (!ctx || !n || k <= 0 || op < 0 || op > 4) return PSF_ERR_ARG;
+    if (num_bytes <= 0 || num_bytes >= 8) return PSF_ERR_NBYTES;
+    if (!((double)max_value - (double)min_value > 0)) return PSF_ERR_BIN;
+    psf::PendingDequant pd{num_bytes, min_value, max_value};
+    *n = psf::ordered_match_raw(ctx->impl, d_src_key, nsrc, d_code, pd, d_dst_key, ndst, d_dst_val,
+                                PSF_DT_FLOAT, k, op);
+    return PSF_OK;
+  });
+}
+int psf_msg_ordered_match(psf_context* ctx, const psf_message* msg, int i, const uint64_t* d_dst_key,
+                          size_t ndst, void* d_dst_val, int k, int value_type, int op, size_t* n) {
+  return guarded([&] {
+    if (!ctx || !msg || !n || op < 0 || op > 4) return PSF_ERR_ARG;
+    if (value_type != PSF_DT_FLOAT && value_type != PSF_DT_DOUBLE) return PSF_ERR_ARG;
+    *n = psf::ordered_match(ctx->impl, msg->m, i, d_dst_key, ndst, d_dst_val, value_type, k, op);
+    return PSF_OK;
+  });
+}
+int psf_kvmap_create(psf_context* ctx, size_t capacity, int lr_type, double alpha, double beta,
+                     double lambda1, double lambda2, psf_kvmap** out) {
+  return guarded([&] {
+    if (!ctx || !out || (lr_type != 1 && lr_type != 2)) return PSF_ERR_ARG;
+    psf::FtrlConfig c;
+    c.lr_type = lr_type;
+    c.alpha = alpha;
+    c.beta = beta;
+    c.lambda1 = lambda1;
+    c.lambda2 = lambda2;
+    *out = new psf_kvmap{new psf::KvMapFtrl(ctx->impl, capacity, c), ctx->impl};
+    return PSF_OK;
+  });
+}
+int psf_kvmap_destroy(psf_kvmap* map) {
+  if (!map) return PSF_OK;
+  delete map->impl;
+  delete map;
+  return PSF_OK;
+}
+int psf_kvmap_set_value(psf_kvmap* map, const psf_message* msg) {
+  return guarded([&] {
+    if (!map || !msg) return PSF_ERR_ARG;
+    map->impl->set_value(msg->m);
+    return PSF_OK;
+  });
+}
+int psf_kvmap_get_value(psf_kvmap* map, psf_message* msg) {
+  return guarded([&] {
+    if (!map || !msg) return PSF_ERR_ARG;
+    map->impl->get_value(&msg->m);
+    return PSF_OK;
+  });
+}
+int psf_kvmap_push(psf_kvmap* map, const uint64_t* d_keys, size_t n, const float* d_grad) {
+  return guarded([&] {
+    if (!map || (n && (!d_keys || !d_grad))) return PSF_ERR_ARG;
+    map->impl->push(d_keys, n, d_grad, psf::PendingDequant{});
+    return PSF_OK;
+  });
+}
+int psf_kvmap_pull(psf_kvmap* map, const uint64_t* d_keys, size_t n, float* d_w) {
+  return guarded([&] {
+    if (!map || (n && (!d_keys || !d_w))) return PSF_ERR_ARG;
+    map->impl->pull(d_keys, n, d_w);
+    return PSF_OK;
+  });
+}
+int psf_kvmap_stats(psf_kvmap* map, int64_t* nnz, double* weight_sum, double* delta_sum, uint64_t* size) {
+  return guarded([&] {
+    if (!map) return PSF_ERR_ARG;
+    const psf::KvMapFtrl::Stats s = map->impl->stats();
+    if (nnz) *nnz = s.nnz;
+    if (weight_sum) *weight_sum = s.weight_sum;
+    if (delta_sum) *delta_sum = s.delta_sum;
+    if (size) *size = s.size;
     return PSF_OK;
   });
 }

@@ -23,6 +23,9 @@ class Filter {
 
   virtual void encode(Message* msg) {}
   virtual void decode(Message* msg) {}
+  // FIXING_FLOAT decode may leave its codes for the consumer to dequantise
+  // (see PendingDequant); set by RemoteNode::set_defer_dequant.
+  void set_defer_dequant(bool v) { defer_dequant_ = v; }
 
   // filter.cc:26-31: the first config of that type, or null.
   static FilterConfig* find(FilterConfig::Type type, Message* msg) { return find(type, &msg->task); }
@@ -30,6 +33,7 @@ class Filter {
 
  protected:
   Context* ctx_;
+  bool defer_dequant_ = false;
 };
 
 // KEY_CACHING, key_caching.h:6-76
@@ -103,10 +107,19 @@ class RemoteNode {
   void DecodeMessage(Message* msg);
   Filter* FindFilterOrCreate(const FilterConfig& conf);
   Context* ctx() const { return ctx_; }
+  // Server side: let FIXING_FLOAT's decode hand its codes to the consumer
+  // (KvMapFtrl / ordered match dequantise them in-register).
+  void set_defer_dequant(bool v);
 
  private:
   Context* ctx_;
+  bool defer_dequant_ = false;
   std::unordered_map<int, Filter*> filters_;
 };
+
+// Run the dequantise a deferred FIXING_FLOAT decode left pending (every
+// pending value array of msg becomes decoded data, as DecodeMessage would
+// have produced).
+void materialize(Context* ctx, Message* msg);
 
 }  // namespace psf

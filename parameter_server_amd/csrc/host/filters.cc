@@ -113,12 +113,25 @@ void FixingFloatFilter::convert(Message* msg, bool encode) {  // fixing_float.h:
   hipStream_t st = ctx_->stream();
 
   if (!encode) {  // fixing_float.h:89-101
+    // Deferral is only sound when nothing decoded after this filter reads the
+    // values: decode runs in reverse order, so every filter listed before
+    // FIXING_FLOAT must be KEY_CACHING (keys only).
+    bool defer = defer_dequant_;
+    for (const auto& f : msg->task.filter) {
+      if (f.type == FilterConfig::FIXING_FLOAT) break;
+      if (f.type != FilterConfig::KEY_CACHING) defer = false;
+    }
     for (auto& j : jobs) {
       const FixedFloatConfig& fp = *j.fp;
       if (!fp.has_min) throw CheckError(kErrCheck, "CHECK(conf->has_min_value())");
       if (!fp.has_max) throw CheckError(kErrCheck, "CHECK(conf->has_max_value())");
       const double bin = (double)fp.max_value - (double)fp.min_value;
       if (!(bin > 0)) throw CheckError(kErrBin, "CHECK_GT(bin, 0)");
+      if (defer && j.type == kFloat) {
+        if (msg->pending.size() < msg->value.size()) msg->pending.resize(msg->value.size());
+        msg->pending[j.i] = PendingDequant{nb, fp.min_value, fp.max_value};
+        continue;
+      }
       const size_t vsz = j.type == kFloat ? 4 : 8;
       Buffer code = ctx_->to_device(msg->value[j.i]);
       const size_t elems = code.bytes / (size_t)nb;
@@ -234,7 +247,10 @@ void AddNoiseFilter::encode(Message* msg) {  // add_noise.h:11-25
 // ---------------------------------------------------------- RemoteNode ----
 Filter* RemoteNode::FindFilterOrCreate(const FilterConfig& conf) {  // remote_node.cc:7-15
   auto it = filters_.find(conf.type);
-  if (it == filters_.end()) it = filters_.emplace(conf.type, Filter::create(conf, ctx_)).first;
+  if (it == filters_.end()) {
+    it = filters_.emplace(conf.type, Filter::create(conf, ctx_)).first;
+    it->second->set_defer_dequant(defer_dequant_);
+  }
   return it->second;
 }
 
@@ -246,6 +262,28 @@ void RemoteNode::EncodeMessage(Message* msg) {  // remote_node.cc:17-22
 void RemoteNode::DecodeMessage(Message* msg) {  // remote_node.cc:23-29, reverse order
   for (int i = (int)msg->task.filter.size() - 1; i >= 0; --i)
     FindFilterOrCreate(msg->task.filter[i])->decode(msg);
+}
+
+void RemoteNode::set_defer_dequant(bool v) {
+  defer_dequant_ = v;
+  for (auto& f : filters_) f.second->set_defer_dequant(v);
+}
+
+void materialize(Context* ctx, Message* msg) {
+  for (size_t i = 0; i < msg->pending.size(); ++i) {
+    const PendingDequant pd = msg->pending[i];
+    if (pd.nb == 0) continue;
+    const int type = msg->task.value_type[i];
+    const size_t vsz = type == kFloat ? 4 : 8;
+    Buffer code = ctx->to_device(msg->value[i]);
+    const size_t elems = code.bytes / (size_t)pd.nb;
+    Buffer out = ctx->alloc(elems * vsz);
+    int s = ff_decode_launch(code.ptr, elems, type, pd.nb, nullptr, pd.min_value, pd.max_value, out.ptr,
+                             ctx->stream(), ctx->prof());
+    if (s != kOk) throw CheckError(s, "ff_decode launch failed");
+    msg->value[i] = out;
+    msg->pending[i] = PendingDequant{};
+  }
 }
 
 }  // namespace psf

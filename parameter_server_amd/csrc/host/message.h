@@ -82,10 +82,22 @@ struct Task {
   bool push = false;  // param.push
 };
 
+// A value array left FIXING_FLOAT-encoded by a decode that deferred the
+// dequantise to its consumer (RemoteNode::set_defer_dequant): the codes stay in
+// `value[i]`, and this records what ff_decode would have used
+// (fixing_float.h:89-101).  nb == 0: the array holds decoded data.
+struct PendingDequant {
+  int nb = 0;
+  float min_value = 0.f, max_value = 0.f;
+};
+
 struct Message {
   Task task;
   Buffer key;
   std::vector<Buffer> value;
+  std::vector<PendingDequant> pending;  // empty, or one entry per value array
+
+  bool is_pending(size_t i) const { return i < pending.size() && pending[i].nb != 0; }
 
   bool has_key() const { return !key.empty(); }
   void clear_key() { task.has_key = false; key.clear(); }

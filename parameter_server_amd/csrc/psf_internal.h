@@ -57,7 +57,7 @@ __device__ __forceinline__ void publish_ticket(PubSlot* s, uint32_t ticket) {
 // Kernel launch profiler: HIP events recorded on the launch stream around
 // each kernel, plus the kernel's algorithmic HBM bytes.
 enum KernelId { kKMinmax = 0, kKEncode, kKDecode, kKCrc, kKNoise, kKSnappyCompress,
-                kKSnappyDecompress, kKNum };
+                kKSnappyDecompress, kKMatch, kKKvPush, kKKvGet, kKNum };
 class Profiler {
  public:
   ~Profiler();
@@ -132,5 +132,23 @@ size_t snappy_uncompress_scratch(size_t c, size_t dsize);
 int snappy_uncompress_launch(const void* in, size_t c, uint32_t hdr, size_t dsize, void* out,
                              void* scratch, hipStream_t st, Profiler* prof, PubSlot* pub,
                              uint32_t ticket);
+
+// kv_store.hip: server-side consumers.  `code` != null
+// makes the source a FIXING_FLOAT code array (nb bytes, range [mn, mx]) that
+// is dequantised in-register exactly as ff_decode would.
+int ordered_match_launch(const uint64_t* src_key, size_t nsrc, const void* src_val, const void* code,
+                         int nb, float mn, float mx, const uint64_t* dst_key, size_t ndst, void* dst_val,
+                         int k, int value_type, int op, int64_t* match_scratch,
+                         unsigned long long* d_matched, hipStream_t st, Profiler* prof);
+size_t kvmap_slot_bytes();
+size_t kvmap_stats_bytes();
+int kvmap_init_launch(void* table, size_t cap, hipStream_t st);
+int kvmap_rehash_launch(const void* from, size_t nfrom, void* to, size_t cap_to, hipStream_t st);
+int kvmap_push_launch(void* table, size_t cap, const uint64_t* keys, size_t n, const float* grad,
+                      const void* code, int nb, float mn, float mx, float alpha, float beta,
+                      int lr_decay, float lambda1, float lambda2, void* stats, hipStream_t st,
+                      Profiler* prof);
+int kvmap_get_launch(const void* table, size_t cap, const uint64_t* keys, size_t n, float* out,
+                     hipStream_t st, Profiler* prof);
 
 }  // namespace psf

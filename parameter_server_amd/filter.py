@@ -149,6 +149,71 @@ class Context:
         return out[:ln.value]
 
 
+    # -- server-side consumers ---------------------------
+    def ordered_match(self, src_key, src_val, dst_key, dst_val, k=1, op=0) -> int:
+        """ParallelOrderedMatch: dst_val op= src_val on equal keys; returns *n."""
+        n = C.c_size_t()
+        check(lib().psf_ordered_match(self.h, C.c_void_p(src_key.data_ptr()), src_key.numel(),
+                                      C.c_void_p(src_val.data_ptr()), C.c_void_p(dst_key.data_ptr()),
+                                      dst_key.numel(), C.c_void_p(dst_val.data_ptr()), k,
+                                      dtype_code(dst_val), op, C.byref(n)))
+        return n.value
+
+    def ff_decode_match(self, src_key, codes, nb, mn, mx, dst_key, dst_val, k=1, op=0) -> int:
+        """ordered_match with FIXING_FLOAT codes as the source (dequantised in-register)."""
+        n = C.c_size_t()
+        check(lib().psf_ff_decode_match(self.h, C.c_void_p(src_key.data_ptr()), src_key.numel(),
+                                        C.c_void_p(codes.data_ptr()), nb, mn, mx,
+                                        C.c_void_p(dst_key.data_ptr()), dst_key.numel(),
+                                        C.c_void_p(dst_val.data_ptr()), k, op, C.byref(n)))
+        return n.value
+
+
+class KVMap:
+    """KVMap<Key, float, FTRLEntry, SGDState> in HBM (kv_map.h:32-91,
+    async_sgd.h:42-154)."""
+
+    def __init__(self, ctx: Context, capacity=1 << 20, lr_type=2, alpha=0.01, beta=10.0, lambda1=0.0,
+                 lambda2=0.0):
+        self.ctx = ctx
+        h = C.c_void_p()
+        check(lib().psf_kvmap_create(ctx.h, capacity, lr_type, alpha, beta, lambda1, lambda2, C.byref(h)))
+        self.h = h
+        self._keepalive = []
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().psf_kvmap_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+    def set_value(self, msg: "Message"):
+        self._keepalive.append(msg._refs)
+        check(lib().psf_kvmap_set_value(self.h, msg.h))
+
+    def get_value(self, msg: "Message"):
+        check(lib().psf_kvmap_get_value(self.h, msg.h))
+
+    def push(self, keys: torch.Tensor, grad: torch.Tensor):
+        check(lib().psf_kvmap_push(self.h, C.c_void_p(keys.data_ptr()), keys.numel(),
+                                   C.c_void_p(grad.data_ptr())))
+
+    def pull(self, keys: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        if out is None:
+            out = torch.empty(keys.numel(), dtype=torch.float32, device=keys.device)
+        check(lib().psf_kvmap_pull(self.h, C.c_void_p(keys.data_ptr()), keys.numel(),
+                                   C.c_void_p(out.data_ptr())))
+        return out
+
+    def stats(self):
+        """(nnz, weight_sum, delta_sum, size)"""
+        a, b, c, d = C.c_int64(), C.c_double(), C.c_double(), C.c_uint64()
+        check(lib().psf_kvmap_stats(self.h, C.byref(a), C.byref(b), C.byref(c), C.byref(d)))
+        return a.value, b.value, c.value, d.value
+
+
 class HostContext(Context):
     """Host-only context (device -1): host-resident buffers, no HIP calls.
     KEY_CACHING on host keys runs here; codecs needing HBM report an error."""
@@ -282,6 +347,24 @@ class Message:
         check(lib().psf_fc_signature(self.h, idx, C.byref(h), C.byref(s)))
         return bool(h.value), s.value
 
+    def pending(self, i: int):
+        """(num_bytes, min, max) of a value array left FIXING_FLOAT-encoded by a
+        deferred decode, or None."""
+        nb, mn, mx = C.c_int(), C.c_float(), C.c_float()
+        check(lib().psf_msg_pending(self.h, i, C.byref(nb), C.byref(mn), C.byref(mx)))
+        return (nb.value, mn.value, mx.value) if nb.value else None
+
+    def materialize(self, ctx: Context):
+        check(lib().psf_msg_materialize(ctx.h, self.h))
+
+    def ordered_match(self, ctx: Context, i: int, dst_key, dst_val, k=1, op=0) -> int:
+        """KVVector::SetValue's merge of value array i into (dst_key, dst_val)."""
+        n = C.c_size_t()
+        check(lib().psf_msg_ordered_match(ctx.h, self.h, i, C.c_void_p(dst_key.data_ptr()), dst_key.numel(),
+                                          C.c_void_p(dst_val.data_ptr()), k, dtype_code(dst_val), op,
+                                          C.byref(n)))
+        return n.value
+
     def uncompressed_sizes(self, idx: int):
         out = []
         for i in range(check(lib().psf_fc_num_uncompressed(self.h, idx))):
@@ -349,6 +432,10 @@ class RemoteNode:
         check(lib().psf_node_roundtrip(self.h, rcv.h, arr, len(tmpls), iters,
                                        C.byref(out) if keep_last else None))
         return Message(_handle=out, _refs=tmpls[-1]._refs) if keep_last else None
+
+    def set_defer_dequant(self, on: bool = True) -> None:
+        """Server side: FIXING_FLOAT decode leaves codes for the consumer."""
+        check(lib().psf_node_set_defer_dequant(self.h, int(on)))
 
     def encode(self, msg: Message) -> None:
         self._hold(msg)
