@@ -69,19 +69,42 @@ __device__ __forceinline__ size_t upper_bound_u64(const uint64_t* a, size_t lo, 
   return lo;
 }
 
+// Wave-cooperative bound: every lane of the wave calls it with the same
+// arguments; 64 pivots per step narrow [lo, hi) 64-fold, so a search over 10^8
+// keys takes 5 dependent loads instead of 27.  Returns the first index in
+// [lo, hi) with a[idx] >= key (upper: > key), or hi.
+__device__ __forceinline__ size_t wave_bound(const uint64_t* a, size_t lo, size_t hi, uint64_t key,
+                                             bool upper) {
+  const int lane = threadIdx.x & 63;
+  while (hi - lo > 64) {
+    const size_t step = (hi - lo + 63) / 64;
+    const size_t idx = lo + (size_t)lane * step;
+    const bool less = idx < hi && (upper ? a[idx] <= key : a[idx] < key);
+    const int c = __popcll(__ballot(less));  // pivots below key: a prefix (sorted)
+    const size_t nlo = c > 0 ? lo + (size_t)(c - 1) * step + 1 : lo;
+    size_t nhi = lo + (size_t)c * step;
+    if (nhi > hi) nhi = hi;
+    lo = nlo;
+    hi = nhi;
+  }
+  const size_t idx = lo + lane;
+  const bool less = idx < hi && (upper ? a[idx] <= key : a[idx] < key);
+  return lo + (size_t)__popcll(__ballot(less));
+}
+
 // ------------------------------------------------------ ordered match ------
 // Pairing rule (parallel_ordered_match.h:20-34): both cursors advance on a
 // match, so the r-th copy of key K in src pairs with the r-th copy of K in
 // dst.  For unique keys (every KVVector key array) r = 0.
 //
 // A workgroup owns kMatchChunk consecutive src keys.  Thread 0 narrows dst to
-// [lower_bound(first), upper_bound(last)); when that window fits in LDS it is
-// staged there (one coalesced pass) and every lane binary-searches LDS, else
-// every lane searches the window in global memory (L2-resident after the
-// first lanes touch it).
+// the window [lower_bound(first), upper_bound(last)); the window is streamed
+// through LDS in chunks of kMatchLds keys (coalesced loads), and every src key
+// binary-searches the one chunk that holds its lower_bound -- the chunk whose
+// last key is >= it and whose predecessor's last key is < it.
 constexpr int kMatchPer = 4;
 constexpr int kMatchChunk = kBlock * kMatchPer;
-constexpr int kMatchLds = 4096;  // dst keys staged per workgroup (32 KiB)
+constexpr int kMatchLds = 4096;  // dst keys staged per chunk (32 KiB)
 
 struct MatchParams {
   const uint64_t* src_key;
@@ -109,41 +132,62 @@ __global__ __launch_bounds__(kBlock) void ordered_match_kernel(MatchParams p) {
   __shared__ unsigned s_cnt;
   const size_t c0 = (size_t)blockIdx.x * kMatchChunk;
   const size_t c1 = c0 + kMatchChunk < p.nsrc ? c0 + kMatchChunk : p.nsrc;
-  if (threadIdx.x == 0) {
-    const size_t lo = lower_bound_u64(p.dst_key, 0, p.ndst, p.src_key[c0]);
-    s_win[0] = lo;
-    s_win[1] = upper_bound_u64(p.dst_key, lo, p.ndst, p.src_key[c1 - 1]);
-    s_cnt = 0;
+  // wave 0: window start, wave 1: window end (two 64-ary searches in parallel)
+  if (threadIdx.x < 128) {
+    const bool upper = threadIdx.x >= 64;
+    const size_t b = wave_bound(p.dst_key, 0, p.ndst, p.src_key[upper ? c1 - 1 : c0], upper);
+    if ((threadIdx.x & 63) == 0) s_win[upper ? 1 : 0] = b;
   }
+  if (threadIdx.x == 0) s_cnt = 0;
   __syncthreads();
   const size_t w0 = s_win[0], w1 = s_win[1];
-  const bool staged = w1 - w0 <= (size_t)kMatchLds;
-  if (staged) {
-    for (size_t j = w0 + threadIdx.x; j < w1; j += kBlock) s_dst[j - w0] = p.dst_key[j];
+  uint64_t key[kMatchPer];
+  size_t pos[kMatchPer];  // global lower_bound of key in dst (w1: beyond the window)
+#pragma unroll
+  for (int u = 0; u < kMatchPer; ++u) {
+    const size_t s = c0 + (size_t)u * kBlock + threadIdx.x;
+    key[u] = s < c1 ? p.src_key[s] : ~0ull;
+    pos[u] = w1;
   }
-  __syncthreads();
+  for (size_t b0 = w0; b0 < w1; b0 += kMatchLds) {
+    const size_t b1 = b0 + kMatchLds < w1 ? b0 + kMatchLds : w1;
+    {  // all loads in flight before the LDS stores (one memory latency per chunk)
+      uint64_t t[kMatchLds / kBlock];
+#pragma unroll
+      for (int q = 0; q < kMatchLds / kBlock; ++q) {
+        const size_t j = b0 + (size_t)q * kBlock + threadIdx.x;
+        t[q] = j < b1 ? p.dst_key[j] : 0;
+      }
+#pragma unroll
+      for (int q = 0; q < kMatchLds / kBlock; ++q) s_dst[q * kBlock + threadIdx.x] = t[q];
+    }
+    __syncthreads();
+    const uint64_t last = s_dst[b1 - b0 - 1];
+    const bool first = b0 == w0;
+    const uint64_t prev = first ? 0 : p.dst_key[b0 - 1];
+#pragma unroll
+    for (int u = 0; u < kMatchPer; ++u) {
+      if (key[u] <= last && (first || key[u] > prev)) {
+        size_t lo = 0, hi = b1 - b0;
+        while (lo < hi) {
+          const size_t mid = (lo + hi) >> 1;
+          if (s_dst[mid] < key[u]) lo = mid + 1; else hi = mid;
+        }
+        pos[u] = b0 + lo;
+      }
+    }
+    __syncthreads();
+  }
   unsigned cnt = 0;
 #pragma unroll
   for (int u = 0; u < kMatchPer; ++u) {
     const size_t s = c0 + (size_t)u * kBlock + threadIdx.x;
     if (s >= c1) break;
-    const uint64_t key = p.src_key[s];
-    // rank of this copy of `key` among equal src keys (0 for unique keys)
+    // rank of this copy of the key among equal src keys (0 for unique keys)
     size_t r = 0;
-    if (s > 0 && p.src_key[s - 1] == key) r = s - lower_bound_u64(p.src_key, 0, s, key);
-    size_t j;
-    if (staged) {
-      size_t lo = 0, hi = w1 - w0;
-      while (lo < hi) {
-        const size_t mid = (lo + hi) >> 1;
-        if (s_dst[mid] < key) lo = mid + 1; else hi = mid;
-      }
-      j = w0 + lo;
-    } else {
-      j = lower_bound_u64(p.dst_key, w0, w1, key);
-    }
-    j += r;
-    const bool hit = j < w1 && p.dst_key[j] == key;
+    if (s > 0 && p.src_key[s - 1] == key[u]) r = s - lower_bound_u64(p.src_key, 0, s, key[u]);
+    const size_t j = pos[u] + r;
+    const bool hit = j < w1 && p.dst_key[j] == key[u];
     if (p.k == 1) {
       if (hit) assign_op<V>(static_cast<V*>(p.dst_val)[j], src_value<V, kCodes>(p, s), p.op);
     } else {
