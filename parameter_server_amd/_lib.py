@@ -10,6 +10,8 @@ import ctypes as C
 import os
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpsf.so")
+# tuning experiments only (tools/build_variants.sh): load an in-tree variant build
+LIB_PATH = os.environ.get("PSF_LIBRARY_VARIANT") or LIB_PATH
 
 PSF_OK = 0
 PSF_ERR_ARG = -1

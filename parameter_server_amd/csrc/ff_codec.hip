@@ -28,13 +28,26 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <map>
+#include <mutex>
+#include <vector>
+
 #include "psf_internal.h"
 
 namespace psf {
 
 constexpr int kTileGroups = 4 * kBlock;  // groups of 4 values per tile
-constexpr int kMinmaxGrid = 1024;        // partials the encode kernel folds
-constexpr int kStreamGrid = 4096;        // workgroups for the store-heavy passes
+#ifndef PSF_MINMAX_GRID
+#define PSF_MINMAX_GRID 1024
+#endif
+constexpr int kMinmaxGrid = PSF_MINMAX_GRID;  // partials the encode kernel folds
+// workgroups for the store-heavy passes: 8192 (4 tiles each at 2^27 values)
+// measured 1.5-5 % faster than 4096 for encode, equal for decode; larger grids
+// lose to per-workgroup setup (tools/build_variants.sh, r01)
+#ifndef PSF_STREAM_GRID
+#define PSF_STREAM_GRID 8192
+#endif
+constexpr int kStreamGrid = PSF_STREAM_GRID;
 constexpr uint32_t kMask17 = 0x1FFFFu;   // LCG state kept mod 2^17 (see quant_group)
 struct Lcg17 { uint32_t a[4], c[4]; };   // affine maps for 1..4 LCG steps, mod 2^17
 
@@ -116,7 +129,11 @@ typedef double f64x2 __attribute__((ext_vector_type(2)));
 template <typename V> struct Vec4;
 template <> struct Vec4<float> {
   __device__ static void load(const float* p, float v[4]) {
+#ifdef PSF_PLAIN_LOADS
+    f32x4 t = *reinterpret_cast<const f32x4*>(p);
+#else
     f32x4 t = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+#endif
     v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
   }
   __device__ static void store(float* p, const float v[4]) {
@@ -249,6 +266,8 @@ struct EncodeParams {
   uint32_t a_tile, c_tile;  // ... one tile (kTileGroups groups)
   uint32_t a_thr, c_thr;    // scalar path (full 32-bit): nthreads elements
   Lcg17 k17;                // 1..4 steps, mod 2^17
+  const uint32_t* lcg_bits; // bit k = !bit16(x_k), x_k the k-th state of the mod-2^17 cycle from 0
+  uint32_t lcg_pos;         // position of the seed on that cycle: seed = x_pos (mod 2^17)
   double ratio;
   float* range_out;         // side-info float[2] (device), may be null
   int* status_out;          // CHECK_GT(bin,0) outcome (device), may be null
@@ -303,13 +322,14 @@ __device__ __forceinline__ void store_codes(uint8_t* __restrict__ out, size_t g,
 //  * f64 fast path (nb <= 3): t' = d * (ratio/bin) differs from tmp by
 //    < 5e-16 * tmp <= 8.4e-9; floor(t') == floor(tmp) whenever frac(t') is
 //    farther than kGuard64 = 2^-26 from an integer.
-//  * f32 fast path (f32 values, nb == 1): d and the product in f32 carry
-//    <= 3 * 2^-24 relative error, |t' - tmp| <= 4.6e-5 for tmp <= 254, so the
-//    guard is kGuard32 = 2^-13.  (tests/test_oracle.py checks both bounds.)
+//  * f32 fast path (f32 values, nb == 1): d, ratio/bin and the product in
+//    f32 carry <= 3 * 2^-24 relative error together, so |t' - tmp| <= 4.6e-5
+//    for tmp <= 254.0001 and the guard is kGuard32 = 2^-14 = 6.1e-5.
+//    (tests/test_oracle.py checks both bounds on adversarial inputs.)
 // Anything inside a guard band, NaN inputs (the min/max clamp sends them to a
 // band edge) and an infinite bin take the reference's exact double sequence.
 constexpr double kGuard64 = 1.4901161193847656e-08;  // 2^-26
-constexpr float kGuard32 = 1.220703125e-04f;         // 2^-13
+constexpr float kGuard32 = 6.103515625e-05f;         // 2^-14
 
 struct QuantParams {
   double min_v, max_v, bin, ratio, scale;
@@ -360,21 +380,22 @@ __device__ __forceinline__ void quant_tile(const V v[4][4], const QuantParams& q
       }
     return;
   }
-  uint32_t slow = 0;
+  // one flag per lane (the per-value flags combine in scalar masks); a lane
+  // with any value in a guard band redoes its 16 values exactly (rare)
+  bool all_ok = true;
 #pragma unroll
   for (int u = 0; u < 4; ++u)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       bool ok;
       fl[u][j] = quant_fast<V, NB>(v[u][j], q, ok);
-      slow |= (ok ? 0u : 1u) << (4 * u + j);
+      all_ok = all_ok & ok;
     }
-  if (__builtin_expect(slow != 0, 0)) {
+  if (__builtin_expect(!all_ok, 0)) {
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (slow & (1u << (4 * u + j))) fl[u][j] = quant_exact((double)v[u][j], q);
+      for (int j = 0; j < 4; ++j) fl[u][j] = quant_exact((double)v[u][j], q);
   }
 }
 
@@ -431,6 +452,59 @@ __device__ __forceinline__ uint64_t lcg_bit(uint32_t& s) {
   return ((s >> 16) & 1u) == 0u ? 1u : 0u;
 }
 
+// f32 values, num_bytes = 1: one lane's full tile (4 groups x 4 values).
+// Fast floor in f32 (the guard band of quant_fast), with the band test folded
+// into two lane-wide accumulators of frac = t - floor(t) compared as u32 bit
+// patterns (frac >= 0, so the order is the float order, and a NaN frac sorts
+// above 1): the lane is fast when g < min frac and max frac < 1 - g.  NaN and
+// infinite values need no test of their own: med3 returns min_f or max_f for
+// them, whose t is 0 or within 1e-4 of ratio, inside the band.  Codes <=
+// ratio = 254, so the packed LCG bits add without carries.  A lane that fails
+// redoes its 16 values with the reference's double sequence.
+__device__ __forceinline__ void encode_tile_f32_nb1(const float v[4][4], const QuantParams& q,
+                                                    const uint32_t b4[4], uint32_t* __restrict__ out) {
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  const f32x2 mn2 = {q.min_f, q.min_f}, sc2 = {q.scale_f, q.scale_f};
+  uint32_t lo = 0x7F800000u, hi = 0u;
+  uint32_t w[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j += 2) {  // value pairs: packed f32 sub/mul (exact per element)
+      const f32x2 c = {__builtin_amdgcn_fmed3f(v[u][j], q.min_f, q.max_f),
+                       __builtin_amdgcn_fmed3f(v[u][j + 1], q.min_f, q.max_f)};
+      const f32x2 t = (c - mn2) * sc2;
+      const f32x2 f = {floorf(t.x), floorf(t.y)};
+      const f32x2 fr = t - f;
+      const uint32_t a = __float_as_uint(fr.x), b = __float_as_uint(fr.y);
+      lo = __builtin_elementwise_min(__builtin_elementwise_min(lo, a), b);
+      hi = __builtin_elementwise_max(__builtin_elementwise_max(hi, a), b);
+      acc = __builtin_amdgcn_cvt_pk_u8_f32(f.x, j, acc);
+      acc = __builtin_amdgcn_cvt_pk_u8_f32(f.y, j + 1, acc);
+    }
+    w[u] = acc;
+  }
+  const bool fast = q.fast && (lo > __float_as_uint(kGuard32)) && (hi < __float_as_uint(1.0f - kGuard32));
+  if (__builtin_expect(!fast, 0)) {
+    // rare (~0.4 % of lanes): find the values inside the band again and give
+    // only those the exact sequence (an f64 divide each)
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bool ok;
+        (void)quant_fast<float, 1>(v[u][j], q, ok);
+        if (!ok) {
+          const uint32_t c = quant_exact((double)v[u][j], q);
+          w[u] = (w[u] & ~(0xFFu << (8 * j))) | (c << (8 * j));
+        }
+      }
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) out[u * kBlock] = w[u] + ((b4[u] * 0x204081u) & 0x01010101u);
+}
+
 template <typename V, int NB, bool kVec>
 __global__ __launch_bounds__(kBlock) void ff_encode(const V* __restrict__ x, size_t n,
                                                      uint8_t* __restrict__ out, EncodeParams p) {
@@ -478,18 +552,30 @@ __global__ __launch_bounds__(kBlock) void ff_encode(const V* __restrict__ x, siz
         V v[4][4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) Vec4<V>::load(x + 4 * (gb + u * kBlock), v[u]);
+        // the LCG bits of this lane's 4 groups from the cycle table: group g
+        // (elements 4g..4g+3) uses states s_{4g+1..4g+4} = x_{pos+4g+1..4}, four
+        // consecutive table bits (one 8-byte L1/L2-hit load + a funnel shift)
+        uint32_t b4[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const uint32_t k = (p.lcg_pos + 1u + 4u * (uint32_t)(gb + u * kBlock)) & kMask17;
+          const uint2 w = *reinterpret_cast<const uint2*>(p.lcg_bits + (k >> 5));
+          b4[u] = __builtin_amdgcn_alignbit(w.y, w.x, k & 31u) & 0xFu;
+        }
+        if (NB == 1 && sizeof(V) == 4) {
+          encode_tile_f32_nb1(reinterpret_cast<const float(*)[4]>(v), q, b4,
+                              reinterpret_cast<uint32_t*>(out) + gb);
+          s = step17(p.a_tile, p.c_tile, s);
+          continue;
+        }
         uint32_t fl[4][4];
         quant_tile<V, NB>(v, q, fl);
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           uint64_t r[4];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const uint32_t sj = step17(p.k17.a[j], p.k17.c[j], su);  // s_{4g+j+1}
-            r[j] = (uint64_t)(uint32_t)(fl[u][j] + ((~sj >> 16) & 1u));
-          }
+          for (int j = 0; j < 4; ++j) r[j] = (uint64_t)(uint32_t)(fl[u][j] + ((b4[u] >> j) & 1u));
           store_codes<NB>(out, gb + u * kBlock, r);
-          su = step17(p.a_lane, p.c_lane, su);
         }
       } else {
 #pragma unroll
@@ -649,6 +735,52 @@ static inline void lcg_affine_pow(uint64_t k, uint32_t& A, uint32_t& Cc) {
   }
 }
 
+// The LCG modulo 2^17 (all the encoder observes, see step17) is one cycle of
+// length 2^17 (a = 1 mod 4, c odd).  Host side: the cycle x_0 = 0,
+// x_{k+1} = a x_k + c, the position of every residue on it, and per device a
+// bit table T[k] = !bit16(x_k) for k < 2^17 + 64 (wrapped), 16 KiB.
+namespace {
+struct LcgCycle {
+  std::vector<uint32_t> pos;   // pos[x] = k with x_k = x
+  std::vector<uint32_t> bits;  // T, packed 32 per word, LSB first
+  LcgCycle() : pos(1u << 17), bits(((1u << 17) + 64) / 32, 0u) {
+    uint32_t x = 0;
+    for (uint32_t k = 0; k < (1u << 17); ++k) {
+      pos[x] = k;
+      x = (kLcgA * x + kLcgC) & kMask17;
+    }
+    x = 0;
+    for (uint32_t k = 0; k < (1u << 17) + 64; ++k) {
+      if (((~x) >> 16) & 1u) bits[k >> 5] |= 1u << (k & 31);
+      x = (kLcgA * x + kLcgC) & kMask17;
+    }
+  }
+};
+const LcgCycle& lcg_cycle() {
+  static const LcgCycle c;
+  return c;
+}
+std::mutex g_lcg_mu;
+std::map<int, uint32_t*> g_lcg_dev;  // per device, allocated once, never freed
+}  // namespace
+
+static const uint32_t* lcg_bits_device() {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> l(g_lcg_mu);
+  auto it = g_lcg_dev.find(dev);
+  if (it != g_lcg_dev.end()) return it->second;
+  const LcgCycle& c = lcg_cycle();
+  uint32_t* d = nullptr;
+  if (hipMalloc(&d, c.bits.size() * sizeof(uint32_t)) != hipSuccess) return nullptr;
+  if (hipMemcpy(d, c.bits.data(), c.bits.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipFree(d);
+    return nullptr;
+  }
+  g_lcg_dev[dev] = d;
+  return d;
+}
+
 double ff_ratio(int nb) {
   // fixing_float.h:55 -- 32-bit int shift, count masked to 5 bits on x86
   int32_t one_shifted = (int32_t)(1u << ((unsigned)(nb * 8) & 31u));
@@ -682,12 +814,15 @@ static void launch_encode(const V* x, size_t n, uint8_t* out, EncodeParams p, hi
     p.k17.a[k] &= kMask17;
     p.k17.c[k] &= kMask17;
   }
+  p.lcg_pos = lcg_cycle().pos[p.seed & kMask17];
   hipLaunchKernelGGL((ff_encode<V, NB, kVec>), dim3(grid), dim3(kBlock), 0, st, x, n, out, p);
 }
 
 template <typename V, bool kVec>
-static int dispatch_encode_nb(const V* x, size_t n, int nb, uint8_t* out, const EncodeParams& p,
+static int dispatch_encode_nb(const V* x, size_t n, int nb, uint8_t* out, EncodeParams p,
                               hipStream_t st) {
+  p.lcg_bits = lcg_bits_device();
+  if (!p.lcg_bits) return kErrHip;
   switch (nb) {
     case 1: launch_encode<V, 1, kVec>(x, n, out, p, st); break;
     case 2: launch_encode<V, 2, kVec>(x, n, out, p, st); break;

@@ -118,6 +118,43 @@ def test_fast_floor_guard_is_sound():
             assert fast_ok.mean() > 0.5
 
 
+def test_fast_floor_f32_guard_is_sound():
+    """The f32 / num_bytes=1 encoder (ff_codec.hip encode_tile_f32_nb1)
+    computes t = (med3(x, min, max) - min) * float(ratio / bin) in float32 and
+    takes floor(t) when frac(t) is farther than 2^-14 from an integer (tested
+    on the u32 bit pattern of frac); numpy float32 arithmetic (IEEE, no FMA)
+    replays it here against the reference's double floor((proj - min) / bin *
+    ratio) on random and adversarial (grid point +- 1 ulp) values."""
+    rng = np.random.default_rng(1)
+    f = np.float32
+    guard_bits = np.array([2.0 ** -14], np.float32).view(np.uint32)[0]
+    one_minus = np.array([1 - 2.0 ** -14], np.float32).view(np.uint32)[0]
+    ratio = 254.0
+    checked = 0
+    for trial in range(40):
+        lo = f(rng.standard_normal() * 10.0 ** rng.integers(-3, 4))
+        hi = f(lo + abs(rng.standard_normal()) * 10.0 ** rng.integers(-5, 4) + 1e-30)
+        if not hi > lo:
+            continue
+        mn, mx = np.float64(lo), np.float64(hi)
+        bin_ = mx - mn
+        x = rng.uniform(mn, mx, 100_000).astype(np.float32)
+        k = rng.integers(0, 255, 50_000)
+        g = (mn + k * (bin_ / ratio)).astype(np.float32)
+        x = np.concatenate([x, g, np.nextafter(g, f(np.inf)), np.nextafter(g, f(-np.inf)),
+                            np.array([lo, hi], np.float32)])
+        c = np.clip(x, lo, hi).astype(np.float32)
+        scale = f(ratio / bin_)
+        t = ((c - lo).astype(np.float32) * scale).astype(np.float32)
+        fl = np.floor(t)
+        fb = (t - fl).astype(np.float32).view(np.uint32)
+        fast_ok = (fb > guard_bits) & (fb < one_minus)
+        exact = np.floor((np.clip(x.astype(np.float64), mn, mx) - mn) / bin_ * ratio)
+        assert np.array_equal(fl[fast_ok].astype(np.float64), exact[fast_ok]), trial
+        checked += int(fast_ok.sum())
+    assert checked > 1_000_000
+
+
 def test_noise_logf_matches_libm():
     """The NOISE kernel's logf (csrc/glibc_logf.h) equals this libm's logf
     (the reference's std::log(float)); exhaustive check: run logf_check
