@@ -505,9 +505,52 @@ __device__ __forceinline__ void encode_tile_f32_nb1(const float v[4][4], const Q
   for (int u = 0; u < 4; ++u) out[u * kBlock] = w[u] + ((b4[u] * 0x204081u) & 0x01010101u);
 }
 
+// One full tile of this lane (groups gb, gb+256, gb+512, gb+768): LCG bits
+// from the cycle table -- group g (elements 4g..4g+3) uses the states
+// s_{4g+1..4g+4} = x_{pos+4g+1..4}, four consecutive table bits (one 8-byte
+// L1/L2-hit load and a funnel shift) -- then quantise, add, pack, store.
+template <typename V, int NB>
+__device__ __forceinline__ void encode_full_tile(const V v[4][4], const QuantParams& q, const EncodeParams& p,
+                                                 uint8_t* __restrict__ out, size_t gb) {
+  uint32_t b4[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const uint32_t k = (p.lcg_pos + 1u + 4u * (uint32_t)(gb + u * kBlock)) & kMask17;
+    const uint2 w = *reinterpret_cast<const uint2*>(p.lcg_bits + (k >> 5));
+    b4[u] = __builtin_amdgcn_alignbit(w.y, w.x, k & 31u) & 0xFu;
+  }
+  if (NB == 1 && sizeof(V) == 4) {
+    encode_tile_f32_nb1(reinterpret_cast<const float(*)[4]>(v), q, b4, reinterpret_cast<uint32_t*>(out) + gb);
+    return;
+  }
+  uint32_t fl[4][4];
+  quant_tile<V, NB>(v, q, fl);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    uint64_t r[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r[j] = (uint64_t)(uint32_t)(fl[u][j] + ((b4[u] >> j) & 1u));
+    store_codes<NB>(out, gb + u * kBlock, r);
+  }
+}
+
 template <typename V, int NB, bool kVec>
 __global__ __launch_bounds__(kBlock) void ff_encode(const V* __restrict__ x, size_t n,
                                                      uint8_t* __restrict__ out, EncodeParams p) {
+  // tiles of this workgroup; the first full tile's loads are issued before
+  // the min/max fold so that its latency hides behind them
+  const size_t ngroups = n >> 2;
+  const size_t ntiles = (ngroups + kTileGroups - 1) / kTileGroups;
+  const size_t nfull = ngroups / kTileGroups;
+  size_t t0 = 0, t1 = 0;
+  if (kVec) tile_range(ntiles, t0, t1);
+  const size_t tf = t1 < nfull ? t1 : nfull;  // full tiles are [t0, tf)
+  V first[4][4];
+  if (kVec && t0 < tf) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) Vec4<V>::load(x + 4 * (t0 * kTileGroups + threadIdx.x + u * kBlock), first[u]);
+  }
+
   float mn_f = p.preset_min, mx_f = p.preset_max;
   if (p.partials != nullptr) {
     float cmn, cmx;
@@ -539,59 +582,33 @@ __global__ __launch_bounds__(kBlock) void ff_encode(const V* __restrict__ x, siz
   if (!(q.bin > 0)) return;  // CHECK_GT(bin, 0), fixing_float.h:71
 
   if (kVec) {
-    const size_t ngroups = n >> 2;
-    const size_t ntiles = (ngroups + kTileGroups - 1) / kTileGroups;
-    size_t t0, t1;
-    tile_range(ntiles, t0, t1);
-    // state before element 4g is s_{4g}; element i consumes s_{i+1}
-    uint32_t s = lcg_jump(p.seed, 4ull * (t0 * kTileGroups + threadIdx.x)) & kMask17;
-    for (size_t t = t0; t < t1; ++t) {
-      const size_t gb = t * kTileGroups + threadIdx.x;
-      uint32_t su = s;
-      if ((t + 1) * kTileGroups <= ngroups) {
+    if (t0 < tf) {
+      encode_full_tile<V, NB>(first, q, p, out, t0 * kTileGroups + threadIdx.x);
+      for (size_t t = t0 + 1; t < tf; ++t) {
+        const size_t gb = t * kTileGroups + threadIdx.x;
         V v[4][4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) Vec4<V>::load(x + 4 * (gb + u * kBlock), v[u]);
-        // the LCG bits of this lane's 4 groups from the cycle table: group g
-        // (elements 4g..4g+3) uses states s_{4g+1..4g+4} = x_{pos+4g+1..4}, four
-        // consecutive table bits (one 8-byte L1/L2-hit load + a funnel shift)
-        uint32_t b4[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const uint32_t k = (p.lcg_pos + 1u + 4u * (uint32_t)(gb + u * kBlock)) & kMask17;
-          const uint2 w = *reinterpret_cast<const uint2*>(p.lcg_bits + (k >> 5));
-          b4[u] = __builtin_amdgcn_alignbit(w.y, w.x, k & 31u) & 0xFu;
-        }
-        if (NB == 1 && sizeof(V) == 4) {
-          encode_tile_f32_nb1(reinterpret_cast<const float(*)[4]>(v), q, b4,
-                              reinterpret_cast<uint32_t*>(out) + gb);
-          s = step17(p.a_tile, p.c_tile, s);
-          continue;
-        }
-        uint32_t fl[4][4];
-        quant_tile<V, NB>(v, q, fl);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          uint64_t r[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) r[j] = (uint64_t)(uint32_t)(fl[u][j] + ((b4[u] >> j) & 1u));
-          store_codes<NB>(out, gb + u * kBlock, r);
-        }
-      } else {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const size_t g = gb + u * kBlock;
-          if (g < ngroups) {
-            V v[4];
-            Vec4<V>::load(x + 4 * g, v);
-            uint64_t r[4];
-            quant_group<V, NB>(v, q, su, p.k17, r);
-            store_codes<NB>(out, g, r);
-          }
-          su = step17(p.a_lane, p.c_lane, su);
-        }
+        encode_full_tile<V, NB>(v, q, p, out, gb);
       }
-      s = step17(p.a_tile, p.c_tile, s);
+    }
+    // the partial last tile of the array, if this workgroup owns it: the LCG
+    // state jumps to this lane's first group and steps mod 2^17
+    for (size_t t = (t0 > tf ? t0 : tf); t < t1; ++t) {
+      const size_t gb = t * kTileGroups + threadIdx.x;
+      uint32_t su = lcg_jump(p.seed, 4ull * gb) & kMask17;  // state before element 4gb
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const size_t g = gb + u * kBlock;
+        if (g < ngroups) {
+          V v[4];
+          Vec4<V>::load(x + 4 * g, v);
+          uint64_t r[4];
+          quant_group<V, NB>(v, q, su, p.k17, r);
+          store_codes<NB>(out, g, r);
+        }
+        su = step17(p.a_lane, p.c_lane, su);
+      }
     }
     // ragged tail (< 4 values): one thread
     const size_t tail = ngroups << 2;
