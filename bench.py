@@ -45,6 +45,10 @@ WORKLOADS = {
     "c3miss": "C3 (BASELINE configs[2]) first-send path: 10M uint64 keys @1% of [0,1e9) + f32 "
               "values, chain [KEY_CACHING(clear_cache_if_done), FIXING_FLOAT num_bytes={nb}], "
               "every send a key cache miss",
+    "c4": "C4 (BASELINE configs[3]): {streams} push streams in total (stream s on rank s % N), each "
+          "{m} sorted unique uint64 keys spread over 2^64 (splitmix64) + f32 values, sliced at the "
+          "EvenDivide(N) server ranges, per-(stream, server) [KEY_CACHING, FIXING_FLOAT num_bytes={nb}], "
+          "cross-range slices spilled in one all-to-all-v per step (RCCL), repeat sends (key cache hit)",
     "c5": "C5 (BASELINE configs[4]) per GPU: 2^20 uint64 keys spread over 2^64 (splitmix64) + "
           "embedding rows dim=128 f32 (512 MiB, one min/max per array), chain [KEY_CACHING, "
           "FIXING_FLOAT num_bytes={nb}{cmp}], repeat send (key cache hit)",
@@ -73,7 +77,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
-    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c3miss", "c5"],
+    ap.add_argument("--streams", type=int, default=64, help="c4: push streams in total")
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c3miss", "c4", "c5"],
                     help="c2: dense f32 values (default, the headline); c3: 10M sorted uint64 "
                          "keys from [0,1e9) + f32 values, [KEY_CACHING, FIXING_FLOAT] repeat "
                          "sends (cache hits); c3miss: same with clear_cache_if_done (every send "
@@ -157,14 +162,15 @@ def _cpu_model():
     return "unknown"
 
 
-def pmc_traffic(kernel: str, n: int, nb: int):
+def pmc_traffic(kernel: str, n: int, nb: int, config: str):
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         d = json.load(open(path))
     except (OSError, ValueError):
         return None
     e = d.get(kernel)
-    if not e or e.get("n") != n or e.get("nb") != nb:
+    # profiles/pmc_traffic.json holds the C2 passes (tools/gpu_profile.sh)
+    if config != "c2" or not e or e.get("n") != n or e.get("nb") != nb:
         return None
     return e.get("hbm_bytes_per_launch")
 
@@ -178,9 +184,17 @@ def main():
     import torch
     import torch.distributed as dist
 
+    # rehearsal knobs (never set by the driver): PSF_DIST_BACKEND=gloo and
+    # PSF_SAME_GPU=1 run N ranks on one GPU with a host-staged exchange
+    backend = os.environ.get("PSF_DIST_BACKEND", "nccl")
+    if os.environ.get("PSF_SAME_GPU") == "1":
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group(backend)
 
     from parameter_server_amd import COMPRESSING, FIXING_FLOAT, KEY_CACHING
     from parameter_server_amd import filter as F
@@ -193,7 +207,28 @@ def main():
     worker, server = F.RemoteNode(ctx), F.RemoteNode(ctx)
     F.set_clock(12345)  # FIXING_FLOAT seed (time(NULL) in the reference)
     tmpls = []
-    if args.config == "c2":
+    router = None
+    if args.config == "c4":
+        # stream s lives on rank s % N; every step slices,
+        # encodes per destination server, spills and decodes (shard.PushRouter)
+        from parameter_server_amd import shard
+        m = args.m or (1 << 21)
+        ex = shard.SpillExchange(device=dev) if world > 1 else None
+        router = shard.PushRouter(ctx, shard.server_ranges(world), rank, world, ex)
+        streams = {}
+        nloc = 0
+        for sid in range(rank, args.streams, world):
+            keys = torch.from_numpy(splitmix64_keys(m, 4 + sid).view("int64")).to(dev)
+            t = F.Message(request=True, push=True, key_channel=sid, key_range=shard.KEY_ALL)
+            t.set_key(keys)
+            t.add_value(torch.randn(keys.numel(), device=dev, generator=g, dtype=torch.float32))
+            t.add_filter(KEY_CACHING)
+            t.add_filter(FIXING_FLOAT, num_bytes=nb)
+            streams[sid] = t
+            nloc += keys.numel()
+        n = nloc
+        payload = 12 * nloc  # this rank's streams: 8 key + 4 value bytes per key
+    elif args.config == "c2":
         # this rank's shard of the key range (range.h:100-107 EvenDivide),
         # pre-placed.  Consecutive steps use different messages (args.bufs
         # distinct arrays whose total exceeds the 256 MiB Infinity Cache), so no
@@ -242,7 +277,14 @@ def main():
         payload = 12 * m  # 8m key bytes + 4m value bytes
     tmpl = tmpls
 
-    worker.roundtrip(server, tmpl, args.warmup)
+    def run(k):
+        if router is not None:
+            for _ in range(k):
+                router.step(streams)
+        else:
+            worker.roundtrip(server, tmpl, k)
+
+    run(args.warmup)
     torch.cuda.synchronize()
 
     # diagnostic pass (not timed): every kernel bracketed by HIP events, to
@@ -251,7 +293,7 @@ def main():
     if not args.no_profile:
         ctx.profile(True)
         ctx.profile_reset()
-        worker.roundtrip(server, tmpl, min(args.steps, 20))
+        run(min(args.steps, 20))
         torch.cuda.synchronize()
         diag = ctx.profile_read()
         ctx.profile(False)
@@ -265,7 +307,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    worker.roundtrip(server, tmpl, args.steps)
+    run(args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -274,7 +316,7 @@ def main():
     ctx.profile(False)
 
     if world > 1:
-        t = torch.tensor([elapsed], device=f"cuda:{local}", dtype=torch.float64)
+        t = torch.tensor([elapsed], device=f"cuda:{local}" if backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -286,7 +328,7 @@ def main():
         per_launch_bytes = alg / launches
         avg_s = ms / launches / 1e3
         achieved = per_launch_bytes / avg_s / 1e9
-        traffic = pmc_traffic(dom, n, nb)
+        traffic = pmc_traffic(dom, n, nb, args.config)
         roofline = {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -303,7 +345,7 @@ def main():
         }
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config != "c5":
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config not in ("c4", "c5"):
         cpu = cpu_baseline(1 << 24 if args.config == "c2" else 1 << 22, nb, args.cpu_seconds, args.config)
 
     if rank == 0:
@@ -316,19 +358,23 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.config == "c4" else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic: f32 N(0,1) values, seed 1+rank, FIXING_FLOAT LCG seed 12345"
-                    + {"c2": "", "c5": "; sorted unique uint64 keys splitmix64(4+rank+i)"}.get(
+                    + {"c2": "", "c5": "; sorted unique uint64 keys splitmix64(4+rank+i)",
+                       "c4": "; sorted unique uint64 keys splitmix64(4+stream+i)"}.get(
                         args.config, "; sorted unique uint64 keys from [0,1e9)"),
             "config": {
-                "workload": WORKLOADS[args.config].format(nb=nb, cmp=", COMPRESSING" if args.compress else ""),
+                "workload": WORKLOADS[args.config].format(nb=nb, cmp=", COMPRESSING" if args.compress else "",
+                                                          streams=args.streams, m=args.m or (1 << 21)),
                 "n_values_per_gpu": n,
                 "payload_bytes_per_step_per_gpu": payload,
                 "value_type": "float32",
                 "num_bytes": nb,
-                "parallelism": f"server key-range shards x{world} (EvenDivide), no data-path collective",
+                "parallelism": f"server key-range shards x{world} (EvenDivide), " + (
+                    "cross-range spill: one all-to-all-v per step" if args.config == "c4" and world > 1
+                    else "no data-path collective"),
             },
             "roofline": roofline,
             "cpu_baseline": cpu,

@@ -162,9 +162,17 @@ int psf_msg_add_value(psf_message* msg, void* ptr, size_t bytes, int value_type,
  * ParseFromArray fails. */
 int psf_task_serialize(const psf_message* msg, void* buf, size_t cap, size_t* len);
 int psf_task_parse(const void* buf, size_t len, psf_message** out);
+/* Van::Recv's data frames (van.cc:240-255): the first data frame of a message
+ * whose Task has has_key becomes the key, every other frame is appended as a
+ * value array; the Task (key_type, value_type, filters) is left as parsed. */
+int psf_msg_recv_frame(psf_message* msg, void* ptr, size_t bytes, int loc);
 /* Replace value array i by a caller buffer (e.g. a received frame, van.cc:244-255). */
 int psf_msg_set_value(psf_message* msg, int i, void* ptr, size_t bytes, int loc);
 int psf_msg_key(const psf_message* msg, void** ptr, size_t* bytes, int* loc);
+/* task.key_channel and the number of task.value_type entries (a parsed Task's
+ * value frames) */
+int psf_msg_key_channel(const psf_message* msg, int32_t* key_channel);
+int psf_task_value_count(const psf_message* msg, int* n);
 int psf_msg_key_info(const psf_message* msg, int* has_key_flag, int* key_type);
 int psf_msg_num_values(const psf_message* msg);
 int psf_msg_value(const psf_message* msg, int i, void** ptr, size_t* bytes, int* loc);

@@ -69,10 +69,13 @@ SIGNATURES = {
     "psf_msg_set_key": ([vp, vp, sz, C.c_int, C.c_int], C.c_int),
     "psf_msg_add_value": ([vp, vp, sz, C.c_int, C.c_int], C.c_int),
     "psf_msg_set_value": ([vp, C.c_int, vp, sz, C.c_int], C.c_int),
+    "psf_msg_recv_frame": ([vp, vp, sz, C.c_int], C.c_int),
     "psf_task_serialize": ([vp, vp, sz, C.POINTER(sz)], C.c_int),
     "psf_task_parse": ([vp, sz, C.POINTER(vp)], C.c_int),
     "psf_msg_key": ([vp, C.POINTER(vp), C.POINTER(sz), PI], C.c_int),
     "psf_msg_key_info": ([vp, PI, PI], C.c_int),
+    "psf_msg_key_channel": ([vp, C.POINTER(i32)], C.c_int),
+    "psf_task_value_count": ([vp, PI], C.c_int),
     "psf_msg_num_values": ([vp], C.c_int),
     "psf_msg_value": ([vp, C.c_int, C.POINTER(vp), C.POINTER(sz), PI], C.c_int),
     "psf_msg_add_filter": ([vp, C.c_int], C.c_int),

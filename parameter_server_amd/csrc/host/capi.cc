@@ -302,6 +302,20 @@ int psf_msg_add_value(psf_message* msg, void* ptr, size_t bytes, int value_type,
     return PSF_OK;
   });
 }
+int psf_msg_recv_frame(psf_message* msg, void* ptr, size_t bytes, int loc) {
+  return guarded([&] {
+    if (!msg || (bytes && !ptr)) return PSF_ERR_ARG;
+    psf::Message& m = msg->m;
+    if (m.task.has_key && m.key.empty() && m.value.empty() && !m.key_frame_seen) {
+      m.key = wrap(ptr, bytes, loc);
+      m.key_frame_seen = true;
+    } else {
+      m.value.push_back(wrap(ptr, bytes, loc));
+      if (!m.pending.empty()) m.pending.resize(m.value.size());
+    }
+    return PSF_OK;
+  });
+}
 int psf_msg_set_value(psf_message* msg, int i, void* ptr, size_t bytes, int loc) {
   return guarded([&] {
     if (!msg || i < 0 || i >= (int)msg->m.value.size()) return PSF_ERR_ARG;
@@ -340,6 +354,16 @@ int psf_msg_key(const psf_message* msg, void** ptr, size_t* bytes, int* loc) {
   if (ptr) *ptr = msg->m.key.ptr;
   if (bytes) *bytes = msg->m.key.bytes;
   if (loc) *loc = (int)msg->m.key.loc;
+  return PSF_OK;
+}
+int psf_msg_key_channel(const psf_message* msg, int32_t* key_channel) {
+  if (!msg || !key_channel) return PSF_ERR_ARG;
+  *key_channel = msg->m.task.key_channel;
+  return PSF_OK;
+}
+int psf_task_value_count(const psf_message* msg, int* n) {
+  if (!msg || !n) return PSF_ERR_ARG;
+  *n = (int)msg->m.task.value_type.size();
   return PSF_OK;
 }
 int psf_msg_key_info(const psf_message* msg, int* has_key_flag, int* key_type) {

@@ -96,6 +96,7 @@ struct Message {
   Buffer key;
   std::vector<Buffer> value;
   std::vector<PendingDequant> pending;  // empty, or one entry per value array
+  bool key_frame_seen = false;          // Van::Recv bookkeeping (psf_msg_recv_frame)
 
   bool is_pending(size_t i) const { return i < pending.size() && pending[i].nb != 0; }
 

@@ -282,6 +282,24 @@ class Message:
             out.append(copy_out(p, n, loc, device).cpu().numpy().tobytes() if n else b"")
         return out
 
+    def recv_frame(self, t: torch.Tensor):
+        """Attach a received data frame as Van::Recv does (van.cc:240-255)."""
+        t = t.contiguous()
+        self._refs.append(t)
+        check(lib().psf_msg_recv_frame(self.h, C.c_void_p(t.data_ptr()), t.numel() * t.element_size(),
+                                       self._loc(t)))
+
+    def device_frames(self, device) -> list:
+        """[Task][key][value...] as uint8 tensors on `device` (the Task frame
+        copied up from the host, key / value frames copied on the device)."""
+        tb = self.task_bytes()
+        out = [torch.frombuffer(bytearray(tb), dtype=torch.uint8).to(device)]
+        p, n, loc = self.key_ptr()
+        arrays = ([(p, n, loc)] if n else []) + [self.value_ptr(i) for i in range(self.num_values())]
+        for p, n, loc in arrays:
+            out.append(copy_out(p, n, loc, device))
+        return out
+
     @staticmethod
     def _loc(t: torch.Tensor) -> int:
         return LOC_DEVICE if t.is_cuda else LOC_HOST

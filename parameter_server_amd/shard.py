@@ -56,6 +56,92 @@ def slice_message(ctx, msg, ranges: Sequence, key_bytes: int = 8):
     return res
 
 
+def parse_frames(frames: List[torch.Tensor]):
+    """Split a flat list of received frames into messages: each is a Task frame
+    followed by its key frame (when the Task has has_key) and one frame per
+    value_type entry (van.cc:193-255)."""
+    from .filter import Message
+    out, i = [], 0
+    while i < len(frames):
+        m = Message.from_task_bytes(frames[i].cpu().numpy().tobytes())
+        i += 1
+        has_key, _ = m.key_info()
+        nval = task_value_count(m)
+        for _ in range(int(has_key) + nval):
+            m.recv_frame(frames[i])
+            i += 1
+        out.append(m)
+    return out
+
+
+def task_value_count(m) -> int:
+    """number of value_type entries of a parsed Task (its value frames)."""
+    n = C.c_int()
+    check(lib().psf_task_value_count(m.h, C.byref(n)))
+    return n.value
+
+
+class PushRouter:
+    """The multi-server push path of one rank: every
+    local stream's message is sliced at the server key ranges
+    (SliceKOFVMessage), each slice is encoded by the sender's per-(stream,
+    server) RemoteNode (executor.cc:131-146); slices owned by this rank are
+    decoded here, the others travel as wire frames in ONE all-to-all-v per step
+    (the cross-range spill) and are decoded by their owner's per-stream node.
+    The stream id travels as the Task's key_channel."""
+
+    def __init__(self, ctx, ranges, rank: int, world: int, exchange=None):
+        from .filter import RemoteNode
+        self.ctx, self.ranges, self.rank, self.world = ctx, ranges, rank, world
+        self.exchange = exchange
+        self._RemoteNode = RemoteNode
+        self.senders, self.receivers = {}, {}
+        self.device = f"cuda:{ctx.device}" if ctx.device >= 0 else "cpu"
+
+    def _sender(self, s, d):
+        if (s, d) not in self.senders:
+            self.senders[(s, d)] = self._RemoteNode(self.ctx)
+        return self.senders[(s, d)]
+
+    def _receiver(self, s):
+        if s not in self.receivers:
+            self.receivers[s] = self._RemoteNode(self.ctx)
+        return self.receivers[s]
+
+    def step(self, streams) -> list:
+        """streams: {stream id: template Message (key_channel = stream id)} of
+        this rank.  Returns the decoded messages this rank received."""
+        send = [[] for _ in range(self.world)]
+        decoded = []
+        for sid, tmpl in streams.items():
+            m = tmpl.clone()
+            parts = slice_message(self.ctx, m, self.ranges)
+            for d, part in enumerate(parts):
+                if part is None:
+                    continue
+                self._sender(sid, d).encode(part)
+                if d == self.rank:
+                    w = part.clone()
+                    self._receiver(sid).decode(w)
+                    decoded.append(w)
+                else:
+                    send[d].extend(part.device_frames(self.device))
+        if self.world > 1:
+            recv = self.exchange.exchange(send)
+            for src in range(self.world):
+                for w in parse_frames(recv[src]):
+                    sid = w_channel(w)
+                    self._receiver(sid).decode(w)
+                    decoded.append(w)
+        return decoded
+
+
+def w_channel(m) -> int:
+    ch = C.c_int32()
+    check(lib().psf_msg_key_channel(m.h, C.byref(ch)))
+    return ch.value
+
+
 class SpillExchange:
     """All-to-all-v of byte frames between ranks (one collective per step).
 
@@ -74,6 +160,15 @@ class SpillExchange:
     def exchange(self, send: List[List[torch.Tensor]]) -> List[List[torch.Tensor]]:
         dist, W = self.dist, self.world
         dev = self.device if self.device is not None else "cpu"
+        if dist.get_backend(self.group) == "gloo" and str(dev).startswith("cuda"):
+            # gloo moves host memory only: stage through the host (CPU tests /
+            # single-GPU rehearsals; RCCL moves HBM directly)
+            self.device = "cpu"
+            try:
+                recv = self.exchange([[f.cpu() for f in frames] for frames in send])
+            finally:
+                self.device = dev
+            return [[f.to(dev) for f in frames] for frames in recv]
         counts = torch.tensor([len(f) for f in send], dtype=torch.int64, device=dev)
         counts_in = torch.empty_like(counts)
         dist.all_to_all_single(counts_in, counts, group=self.group)
