@@ -305,7 +305,9 @@ __global__ __launch_bounds__(256) void snappy_pack(const uint8_t* __restrict__ s
 constexpr uint32_t kWin = 16384;   // compressed bytes per parse window (16 KiB: ~8 waves per CU)
 constexpr uint32_t kInWin = 8192;  // staged compressed bytes in the fragment decoder
 constexpr uint64_t kNone = ~0ull;
-constexpr uint32_t kFlagInvalid = 1, kFlagSerial = 2;
+constexpr uint32_t kFlagInvalid = 1, kFlagSerial = 2, kFlagScan = 4;
+constexpr uint64_t kFullLit = 65536 + 3;  // a 64 KiB fragment stored as one literal (tag 0xF4 + 2 length bytes)
+constexpr uint32_t kLitBudget = 512;      // K0's single steps before it hands the stream to K1/K2
 
 struct Tag {
   uint64_t next;  // position after the tag (literal data included)
@@ -402,6 +404,85 @@ __device__ __forceinline__ uint32_t stage(uint32_t* lds, const uint8_t* in, uint
   return s;
 }
 
+// the 5 tag bytes at input offset p (zero past the end): three aligned dwords
+__device__ __forceinline__ uint64_t tag_bytes(const uint8_t* in, uint64_t C, uint64_t p) {
+  const uintptr_t ia = reinterpret_cast<uintptr_t>(in);
+  const uint64_t a = (ia + p) & ~(uintptr_t)3;
+  const uint64_t ai = a - ia;
+  uint32_t d[3] = {0, 0, 0};
+  if (ai + 12 <= C) {
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(a);
+    d[0] = q[0];
+    d[1] = q[1];
+    d[2] = q[2];
+  } else {
+    for (int i = 0; i < 12; ++i) {
+      const uint64_t r = ai + i;
+      if (r < C) d[i >> 2] |= (uint32_t)in[r] << (8 * (i & 3));
+    }
+  }
+  const uint32_t sh = (uint32_t)(p - ai) * 8;
+  const uint64_t lo = ((uint64_t)d[1] << 32) | d[0];
+  return sh ? (lo >> sh) | ((uint64_t)d[2] << (64 - sh)) : lo;
+}
+
+// K0: link the chain directly when the stream is mostly 64 KiB fragments
+// stored as single literals (what a snappy 1.1.8 encoder emits for
+// incompressible fragments, e.g. FIXING_FLOAT codes): lane k decodes the tag
+// at p + k * kFullLit, and the run of lanes that find a full literal there is
+// consumed in one step (64 fragments per memory latency); other tags take a
+// single step.  After kLitBudget single steps the stream is handed to the
+// window scan (K1) and its linker (K2) through kFlagScan.
+__global__ __launch_bounds__(64) void snappy_dlit(const uint8_t* __restrict__ in, uint64_t C, uint32_t hdr,
+                                                  uint64_t dsize, uint32_t nwin, uint64_t* __restrict__ wentry,
+                                                  uint64_t* __restrict__ woff, uint32_t* __restrict__ flags) {
+  const uint32_t lane = threadIdx.x;
+  for (uint32_t i = lane; i < nwin; i += 64) wentry[i] = kNone;
+  __syncthreads();
+  uint64_t p = hdr, o = 0;
+  int64_t last_w = -1;
+  uint32_t singles = 0;
+  bool bad = false;
+  while (p < C) {
+    const uint64_t pk = p + (uint64_t)lane * kFullLit;
+    const Tag t = decode_tag(tag_bytes(in, C, pk), pk);
+    const bool full = pk < C && t.lit && t.len == 65536 && t.hl == 3;
+    const uint64_t m = __ballot(full);
+    const uint32_t c = m == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~m);  // leading run of full literals
+    if (c > 0) {
+      if (lane < c) {
+        const int64_t wk = (int64_t)((pk - hdr) / kWin);
+        if (wk > last_w) {
+          wentry[wk] = pk;
+          woff[wk] = o + (uint64_t)lane * 65536;
+        }
+      }
+      last_w = (int64_t)((p + (uint64_t)(c - 1) * kFullLit - hdr) / kWin);
+      p += (uint64_t)c * kFullLit;
+      o += (uint64_t)c * 65536;
+    } else {
+      const uint64_t t0next = __shfl(t.next, 0, 64), t0len = __shfl(t.len, 0, 64);
+      const int64_t w0 = (int64_t)((p - hdr) / kWin);
+      if (lane == 0 && w0 > last_w) {
+        wentry[w0] = p;
+        woff[w0] = o;
+      }
+      if (w0 > last_w) last_w = w0;
+      p = t0next;
+      o += t0len;
+      if (++singles > kLitBudget) {
+        if (lane == 0) *flags = kFlagScan;
+        return;
+      }
+    }
+    if (o > dsize) {
+      bad = true;
+      break;
+    }
+  }
+  if (lane == 0) *flags = (bad || p != C || o != dsize) ? kFlagInvalid : 0u;
+}
+
 constexpr uint32_t kStarts = 64;  // K1 parses from each of the first 64 offsets of a window
 
 // K1: speculative parse of each window from each of its first 64 byte offsets
@@ -409,9 +490,11 @@ constexpr uint32_t kStarts = 64;  // K1 parses from each of the first 64 offsets
 // carried the chain further in; for those K2 walks until it meets lane 0's chain.
 __global__ __launch_bounds__(64) void snappy_dscan(const uint8_t* __restrict__ in, uint64_t C, uint32_t hdr,
                                                    uint32_t* __restrict__ bitmap, uint32_t* __restrict__ cum,
-                                                   uint64_t* __restrict__ wexit, uint64_t* __restrict__ wtotal) {
+                                                   uint64_t* __restrict__ wexit, uint64_t* __restrict__ wtotal,
+                                                   const uint32_t* __restrict__ flags) {
   __shared__ uint32_t b32[(kWin + 32) / 4];
   __shared__ uint32_t bm[kWin / 32];
+  if (!(*flags & kFlagScan)) return;  // K0 linked the stream already
   const uint32_t lane = threadIdx.x, w = blockIdx.x;
   const uint64_t base = hdr + (uint64_t)w * kWin;
   const uint32_t wl = (uint32_t)min((uint64_t)kWin, C - base);
@@ -439,7 +522,10 @@ __global__ __launch_bounds__(64) void snappy_dscan(const uint8_t* __restrict__ i
   for (uint32_t i = lane; i < kWin / 32; i += 64) gb[i] = bm[i];
 }
 
-// K2: link the windows along the true chain (one lane)
+// K2: link the windows along the true chain (one lane).  Every step costs
+// one memory latency: windows are entered in increasing order, so the
+// first-entry bookkeeping stays in registers, and the bitmap word and the
+// next tag's bytes (two aligned dwords) are loaded together.
 __global__ __launch_bounds__(64) void snappy_dlink(const uint8_t* __restrict__ in, uint64_t C, uint32_t hdr,
                                                    uint64_t dsize, const uint32_t* __restrict__ bitmap,
                                                    const uint32_t* __restrict__ cum,
@@ -447,31 +533,55 @@ __global__ __launch_bounds__(64) void snappy_dlink(const uint8_t* __restrict__ i
                                                    const uint64_t* __restrict__ wtotal, uint32_t nwin,
                                                    uint64_t* __restrict__ wentry, uint64_t* __restrict__ woff,
                                                    uint32_t* __restrict__ flags) {
+  if (!(*flags & kFlagScan)) return;  // K0 linked the stream already
   for (uint32_t i = threadIdx.x; i < nwin; i += 64) wentry[i] = kNone;
   __syncthreads();
   if (threadIdx.x != 0) return;
   uint64_t p = hdr, o = 0;
+  int64_t last_w = -1;  // highest window whose entry is recorded
   bool bad = false;
+  const uintptr_t ia = reinterpret_cast<uintptr_t>(in);
   while (p < C) {
     const uint64_t rel = p - hdr;
     const uint32_t w = (uint32_t)(rel / kWin);
     const uint64_t off = rel - (uint64_t)w * kWin;
-    if (wentry[w] == kNone) {
+    if ((int64_t)w > last_w) {
       wentry[w] = p;
       woff[w] = o;
+      last_w = w;
     }
     if (off < kStarts) {  // parsed exactly by K1's lane `off`
       o += wtotal[(size_t)w * kStarts + off];
       p = wexit[(size_t)w * kStarts + off];
-    } else if ((bitmap[rel >> 5] >> (rel & 31)) & 1) {  // met lane 0's chain
-      o += wtotal[(size_t)w * kStarts] - cum[p];
-      p = wexit[(size_t)w * kStarts];
-    } else {  // one tag, then look again
-      uint8_t tb[5];
-      for (int i = 0; i < 5; ++i) tb[i] = p + i < C ? in[p + i] : 0;
-      const Tag t = parse_tag(tb, p);
-      o += t.len;
-      p = t.next;
+    } else {
+      // bitmap word and the 8 bytes at p, loaded together
+      const uint32_t bw = bitmap[rel >> 5];
+      const uint64_t a = (ia + p) & ~(uintptr_t)3;  // aligned dword address
+      const uint64_t ai = a - ia;                    // its input offset (may be < p)
+      uint32_t d0 = 0, d1 = 0, d2 = 0;
+      if (ai + 12 <= C) {
+        const uint32_t* q = reinterpret_cast<const uint32_t*>(a);
+        d0 = q[0];
+        d1 = q[1];
+        d2 = q[2];
+      } else {
+        for (int i = 0; i < 12; ++i) {
+          const uint64_t r = ai + i;
+          const uint32_t b = r < C ? in[r] : 0;
+          if (i < 4) d0 |= b << (8 * i); else if (i < 8) d1 |= b << (8 * (i - 4)); else d2 |= b << (8 * (i - 8));
+        }
+      }
+      if ((bw >> (rel & 31)) & 1) {  // met lane 0's chain
+        o += wtotal[(size_t)w * kStarts] - cum[p];
+        p = wexit[(size_t)w * kStarts];
+      } else {  // one tag, then look again
+        const uint32_t sh = (uint32_t)(p - ai) * 8;  // 0..24
+        const uint64_t lo = ((uint64_t)d1 << 32) | d0;
+        const uint64_t x = sh ? (lo >> sh) | ((uint64_t)d2 << (64 - sh)) : lo;
+        const Tag t = decode_tag(x, p);
+        o += t.len;
+        p = t.next;
+      }
     }
     if (o > dsize) {
       bad = true;
@@ -650,9 +760,11 @@ int snappy_uncompress_launch(const void* in, size_t C, uint32_t hdr, size_t dsiz
   const uint8_t* src = static_cast<const uint8_t*>(in);
   uint8_t* dst = static_cast<uint8_t*>(out);
   ProfScope ps(prof, kKSnappyDecompress, st, (double)C + (double)dsize);
+  hipLaunchKernelGGL(snappy_dlit, dim3(1), dim3(64), 0, st, src, (uint64_t)C, hdr, (uint64_t)dsize, nwin, wentry,
+                     woff, flags);
   if (nwin) {
     hipLaunchKernelGGL(snappy_dscan, dim3(nwin), dim3(64), 0, st, src, (uint64_t)C, hdr, bitmap, cum, wexit,
-                       wtotal);
+                       wtotal, flags);
   }
   hipLaunchKernelGGL(snappy_dlink, dim3(1), dim3(64), 0, st, src, (uint64_t)C, hdr, (uint64_t)dsize, bitmap, cum,
                      wexit, wtotal, nwin, wentry, woff, flags);
