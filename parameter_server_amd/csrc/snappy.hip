@@ -70,6 +70,7 @@ struct CompressLds {
   uint32_t minlane[kMinSlots];  // per hash slot: lowest lane of the step that probed it
 };
 
+template <uint32_t kLanes = 64>
 __device__ uint32_t emit_literal(uint8_t* out, uint32_t op, const uint8_t* srcb, uint32_t lit,
                                  uint32_t len, uint32_t lane) {
   const uint32_t n = len - 1;
@@ -82,8 +83,20 @@ __device__ uint32_t emit_literal(uint8_t* out, uint32_t op, const uint8_t* srcb,
     if (lane >= 1 && lane <= count) out[op + lane] = (uint8_t)(n >> (8 * (lane - 1)));
     hl += count;
   }
-  for (uint32_t i = lane; i < len; i += 64) out[op + hl + i] = srcb[lit + i];
-  return op + hl + len;
+  // the literal bytes: byte stores up to the first 4-aligned output position,
+  // then whole dwords composed from LDS (ld32 reads unaligned), then the tail
+  const uint32_t d0 = op + hl, d1 = d0 + len;
+  const uint32_t a0 = (d0 + 3) & ~3u, a1 = d1 & ~3u;
+  if (a0 >= a1) {
+    for (uint32_t i = lane; i < len; i += kLanes) out[d0 + i] = srcb[lit + i];
+    return d1;
+  }
+  if (lane < a0 - d0) out[d0 + lane] = srcb[lit + lane];
+  const uint32_t* s32 = reinterpret_cast<const uint32_t*>(srcb);
+  uint32_t* o32 = reinterpret_cast<uint32_t*>(out);
+  for (uint32_t j = (a0 >> 2) + lane; j < (a1 >> 2); j += kLanes) o32[j] = ld32(s32, lit + (4 * j - d0));
+  if (lane < d1 - a1) out[a1 + lane] = srcb[lit + (a1 - d0) + lane];
+  return d1;
 }
 
 __device__ __forceinline__ void put_copy2(uint8_t* out, uint32_t op, uint32_t offset, uint32_t len) {
@@ -128,11 +141,17 @@ __device__ __forceinline__ uint32_t match_len(const uint8_t* b, uint32_t s1, uin
   }
 }
 
-__global__ __launch_bounds__(64) void snappy_compress_frags(const uint8_t* __restrict__ in, size_t n,
-                                                            uint8_t* __restrict__ scratch,
-                                                            uint32_t* __restrict__ lens) {
+// One workgroup of 4 waves per 64 KiB fragment (the LDS footprint allows one
+// workgroup per CU): all 256 lanes stage the fragment, wave 0 runs the serial
+// 1.1.8 parse, and the final literal (all of an incompressible fragment) is
+// copied out by all 256 lanes again.
+__global__ __launch_bounds__(256) void snappy_compress_frags(const uint8_t* __restrict__ in, size_t n,
+                                                             uint8_t* __restrict__ scratch,
+                                                             uint32_t* __restrict__ lens) {
   __shared__ CompressLds L;
-  const uint32_t lane = threadIdx.x;
+  __shared__ uint32_t s_op, s_next;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = tid;  // wave 0's lanes in the parse (tid < 64 there)
   const uint32_t f = blockIdx.x;
   const size_t start = (size_t)f * kFrag;
   const uint32_t len = (uint32_t)min((size_t)kFrag, n - start);
@@ -144,23 +163,35 @@ __global__ __launch_bounds__(64) void snappy_compress_frags(const uint8_t* __res
     const uint32_t nv = len >> 4;
     const uint4* g4 = reinterpret_cast<const uint4*>(g);
     uint4* s4 = reinterpret_cast<uint4*>(L.src);
-    for (uint32_t i = lane; i < nv; i += 64) s4[i] = g4[i];
-    for (uint32_t i = (nv << 4) + lane; i < len; i += 64) srcb[i] = g[i];
+    for (uint32_t i0 = 0; i0 < nv; i0 += 4 * 256) {  // 4 loads in flight per lane
+      uint4 t[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t i = i0 + u * 256 + tid;
+        if (i < nv) t[u] = g4[i];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t i = i0 + u * 256 + tid;
+        if (i < nv) s4[i] = t[u];
+      }
+    }
+    for (uint32_t i = (nv << 4) + tid; i < len; i += 256) srcb[i] = g[i];
   } else {
-    for (uint32_t i = lane; i < len; i += 64) srcb[i] = g[i];
+    for (uint32_t i = tid; i < len; i += 256) srcb[i] = g[i];
   }
-  if (lane < 16) srcb[len + lane] = 0;
-  for (uint32_t i = lane; i < (uint32_t)kSkipN; i += 64) L.skip[i] = kSkip.v[i];
-  for (uint32_t i = lane; i < kMinSlots; i += 64) L.minlane[i] = 0xffffffffu;
+  if (tid < 16) srcb[len + tid] = 0;
+  for (uint32_t i = tid; i < (uint32_t)kSkipN; i += 256) L.skip[i] = kSkip.v[i];
+  for (uint32_t i = tid; i < kMinSlots; i += 256) L.minlane[i] = 0xffffffffu;
   uint32_t tsize = 256;
   while (tsize < kMaxTable && tsize < len) tsize <<= 1;
   const int shift = __builtin_clz(tsize) + 1;  // 32 - log2(tsize)
   uint32_t* t32 = reinterpret_cast<uint32_t*>(L.table);
-  for (uint32_t i = lane; i < tsize / 2; i += 64) t32[i] = 0;
+  for (uint32_t i = tid; i < tsize / 2; i += 256) t32[i] = 0;
   __syncthreads();
 
   uint32_t op = 0, next_emit = 0;
-  if (len >= 15) {
+  if (tid < 64 && len >= 15) {
     const uint32_t ip_limit = len - 15;
     uint32_t ip = 1;
     for (;;) {
@@ -236,8 +267,15 @@ __global__ __launch_bounds__(64) void snappy_compress_frags(const uint8_t* __res
     }
   }
 remainder:
-  if (next_emit < len) op = emit_literal(out, op, srcb, next_emit, len - next_emit, lane);
-  if (lane == 0) lens[f] = op;
+  if (tid == 0) {
+    s_op = op;
+    s_next = next_emit;
+  }
+  __syncthreads();
+  op = s_op;
+  next_emit = s_next;
+  if (next_emit < len) op = emit_literal<256>(out, op, srcb, next_emit, len - next_emit, tid);
+  if (tid == 0) lens[f] = op;
 }
 
 // exclusive scan of fragment lengths (+ the varint header) -> offs; total -> pub
@@ -286,19 +324,31 @@ __global__ __launch_bounds__(256) void snappy_pack(const uint8_t* __restrict__ s
     }
     out[i] = (uint8_t)v;
   }
-  const uint8_t* s = scratch + (size_t)f * kSnappyFragOut;
-  uint8_t* d = out + offs[f];
+  const uint8_t* s = scratch + (size_t)f * kSnappyFragOut;  // 256-aligned slot
+  const uint64_t o = offs[f];
   const uint32_t len = lens[f];
-  // 4-byte reads from the (aligned) scratch slot, byte-aligned writes
-  const uint32_t n4 = len >> 2;
-  for (uint32_t i = threadIdx.x; i < n4; i += 256) {
-    const uint32_t w = reinterpret_cast<const uint32_t*>(s)[i];
-    d[4 * i] = (uint8_t)w;
-    d[4 * i + 1] = (uint8_t)(w >> 8);
-    d[4 * i + 2] = (uint8_t)(w >> 16);
-    d[4 * i + 3] = (uint8_t)(w >> 24);
+  // destination dwords that lie wholly inside [o, o+len), each composed from
+  // the two aligned scratch dwords it straddles; byte stores at the edges.
+  // The scratch slot has room past len (kSnappyFragOut >= max fragment
+  // output + 8), so the second dword read stays inside the slot.
+  const uintptr_t ob = reinterpret_cast<uintptr_t>(out);
+  const uint64_t a0 = ((ob + o + 3) & ~(uintptr_t)3) - ob, a1 = ((ob + o + len) & ~(uintptr_t)3) - ob;
+  if (a0 >= a1) {
+    for (uint32_t i = threadIdx.x; i < len; i += 256) out[o + i] = s[i];
+    return;
   }
-  for (uint32_t i = (n4 << 2) + threadIdx.x; i < len; i += 256) d[i] = s[i];
+  const uint32_t head = (uint32_t)(a0 - o);
+  if (threadIdx.x < head) out[o + threadIdx.x] = s[threadIdx.x];
+  const uint32_t* s32 = reinterpret_cast<const uint32_t*>(s);
+  uint32_t* d32 = reinterpret_cast<uint32_t*>(out + a0);
+  const uint32_t nw = (uint32_t)((a1 - a0) >> 2);
+  for (uint32_t j = threadIdx.x; j < nw; j += 256) {
+    // destination bytes a0+4j.. come from scratch bytes head+4j..
+    const uint32_t lo = s32[j], hi = s32[j + 1];
+    d32[j] = head ? __builtin_amdgcn_alignbyte(hi, lo, head) : lo;
+  }
+  const uint32_t tail0 = (uint32_t)(a1 - o);
+  for (uint32_t i = tail0 + threadIdx.x; i < len; i += 256) out[o + i] = s[i];
 }
 
 // ------------------------------------------------------------------ uncompress
@@ -390,16 +440,29 @@ __device__ __forceinline__ uint32_t stage(uint32_t* lds, const uint8_t* in, uint
   const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(in + base) & 3);
   const int64_t r0 = (int64_t)base - (int64_t)s;  // input offset of lds byte 0 (dword aligned)
   const uint32_t nw = (s + want + 3) >> 2;
-  for (uint32_t j = lane; j < nw; j += 64) {
-    const int64_t r = r0 + 4 * (int64_t)j;
-    uint32_t v = 0;
-    if (r >= 0 && r + 4 <= (int64_t)C) {
-      v = *reinterpret_cast<const uint32_t*>(in + r);
-    } else {
-      for (int q = 0; q < 4; ++q)
-        if (r + q >= 0 && r + q < (int64_t)C) v |= (uint32_t)in[r + q] << (8 * q);
+  // 8 loads in flight per lane before their LDS stores (one memory latency
+  // per 2 KiB instead of one per 256 B)
+  for (uint32_t j0 = 0; j0 < nw; j0 += 8 * 64) {
+    uint32_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint32_t j = j0 + u * 64 + lane;
+      const int64_t r = r0 + 4 * (int64_t)j;
+      v[u] = 0;
+      if (j < nw) {
+        if (r >= 0 && r + 4 <= (int64_t)C) {
+          v[u] = *reinterpret_cast<const uint32_t*>(in + r);
+        } else {
+          for (int q = 0; q < 4; ++q)
+            if (r + q >= 0 && r + q < (int64_t)C) v[u] |= (uint32_t)in[r + q] << (8 * q);
+        }
+      }
     }
-    lds[j] = v;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint32_t j = j0 + u * 64 + lane;
+      if (j < nw) lds[j] = v[u];
+    }
   }
   return s;
 }
@@ -637,6 +700,10 @@ __global__ __launch_bounds__(64) void snappy_dfrag(const uint8_t* __restrict__ i
   const uint32_t end = (uint32_t)min((uint64_t)kFrag, dsize - o0);
   constexpr uint32_t kSpan = kInWin + 16;  // staged bytes [wb, wb + kSpan)
   uint64_t p = fragpos[k];
+  {  // a fragment stored as one literal was copied by snappy_dstored
+    const Tag t0 = decode_tag(tag_bytes(in, C, p), p);
+    if (t0.lit && t0.len == end) return;
+  }
   uint64_t wb = p;
   uint32_t s = stage(ib32, in, C, wb, kSpan, lane);
   uint32_t o = 0;
@@ -677,6 +744,41 @@ __global__ __launch_bounds__(64) void snappy_dfrag(const uint8_t* __restrict__ i
   } else {
     for (uint32_t i = lane; i < end; i += 64) d[i] = ob[i];
   }
+}
+
+// K4a: fragments stored as one literal: a straight copy from the compressed
+// stream, 256 lanes x 16 B per step, unaligned source realigned with funnel
+// shifts (aligned dword loads only)
+__global__ __launch_bounds__(256) void snappy_dstored(const uint8_t* __restrict__ in, uint64_t C, uint64_t dsize,
+                                                      const uint64_t* __restrict__ fragpos,
+                                                      const uint32_t* __restrict__ flags, uint8_t* __restrict__ out) {
+  if (*flags) return;
+  const uint32_t k = blockIdx.x;
+  const uint64_t o0 = (uint64_t)k * kFrag;
+  const uint32_t end = (uint32_t)min((uint64_t)kFrag, dsize - o0);
+  const uint64_t p = fragpos[k];
+  const Tag t = decode_tag(tag_bytes(in, C, p), p);
+  if (!(t.lit && t.len == end)) return;
+  const uint64_t src = p + t.hl;
+  uint8_t* d = out + o0;
+  const uintptr_t ia = reinterpret_cast<uintptr_t>(in);
+  const uint32_t sh = (uint32_t)((ia + src) & 3) * 8;
+  const uint32_t* a = reinterpret_cast<const uint32_t*>((ia + src) & ~(uintptr_t)3);
+  const uint32_t nv = ((reinterpret_cast<uintptr_t>(d) & 15) == 0) ? end >> 4 : 0;
+  for (uint32_t i = threadIdx.x; i < nv; i += 256) {
+    // 16 output bytes from the 5 aligned dwords that cover them; the fifth is
+    // only read when the source is misaligned (then it lies inside the stream)
+    const uint32_t* q = a + 4 * i;
+    const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3];
+    const uint32_t w4 = sh ? q[4] : 0u;
+    uint4 v;
+    v.x = sh ? __builtin_amdgcn_alignbit(w1, w0, sh) : w0;
+    v.y = sh ? __builtin_amdgcn_alignbit(w2, w1, sh) : w1;
+    v.z = sh ? __builtin_amdgcn_alignbit(w3, w2, sh) : w2;
+    v.w = sh ? __builtin_amdgcn_alignbit(w4, w3, sh) : w3;
+    reinterpret_cast<uint4*>(d)[i] = v;
+  }
+  for (uint32_t i = (nv << 4) + threadIdx.x; i < end; i += 256) d[i] = in[src + i];
 }
 
 // K5: the verdict; one-lane decode of valid streams K4 could not split
@@ -728,7 +830,7 @@ int snappy_compress_launch(const void* in, size_t n, void* out, void* scratch, h
   for (uint64_t v = n; v >= 128; v >>= 7) ++hdr;
   {
     ProfScope ps(prof, kKSnappyCompress, st, (double)n);
-    hipLaunchKernelGGL(snappy_compress_frags, dim3(nfrag), dim3(64), 0, st,
+    hipLaunchKernelGGL(snappy_compress_frags, dim3(nfrag), dim3(256), 0, st,
                        static_cast<const uint8_t*>(in), n, s, lens);
   }
   hipLaunchKernelGGL(snappy_scan, dim3(1), dim3(1024), 0, st, lens, nfrag, hdr, offs, pub, ticket);
@@ -773,6 +875,8 @@ int snappy_uncompress_launch(const void* in, size_t C, uint32_t hdr, size_t dsiz
                        flags);
   }
   if (nfo) {
+    hipLaunchKernelGGL(snappy_dstored, dim3(nfo), dim3(256), 0, st, src, (uint64_t)C, (uint64_t)dsize, fragpos,
+                       flags, dst);
     hipLaunchKernelGGL(snappy_dfrag, dim3(nfo), dim3(64), 0, st, src, (uint64_t)C, (uint64_t)dsize, fragpos, flags,
                        dst);
   }
