@@ -281,6 +281,20 @@ int psf_kvmap_pull(psf_kvmap* map, const uint64_t* d_keys, size_t n, float* d_w)
 int psf_kvmap_stats(psf_kvmap* map, int64_t* nnz, double* weight_sum, double* delta_sum,
                     uint64_t* size);
 
+/* ---- many messages at once --------------------------------------------
+ * RemoteNode::EncodeMessage / DecodeMessage of n messages, message i on
+ * nodes[i]: every message runs its own chain in its own order on its own
+ * node's filter instances (stateful filters see their messages in array
+ * order), with FIXING_FLOAT's element work batched into one launch per kernel
+ * for up to 32 arrays (the async-SGD minibatch messages and the per-server
+ * slices of SURVEY.md §8(d) C1/C4 are latency-bound one at a time). */
+int psf_nodes_encode(psf_node* const* nodes, psf_message* const* msgs, int n);
+int psf_nodes_decode(psf_node* const* nodes, psf_message* const* msgs, int n);
+/* psf_node_roundtrip for n streams at once: for i in [0, iters), encode fresh
+ * copies of tmpls[0..n) on snd[0..n), deliver, decode on rcv[0..n). */
+int psf_nodes_roundtrip(psf_node* const* snd, psf_node* const* rcv, const psf_message* const* tmpls, int n,
+                        int iters);
+
 /* ---- launch profiler (HIP events on the launch stream) ----------------- */
 #define PSF_K_MINMAX 0
 #define PSF_K_ENCODE 1

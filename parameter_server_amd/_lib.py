@@ -109,6 +109,9 @@ SIGNATURES = {
     "psf_kvmap_pull": ([vp, vp, sz, vp], C.c_int),
     "psf_kvmap_stats": ([vp, C.POINTER(C.c_int64), C.POINTER(C.c_double), C.POINTER(C.c_double),
                          C.POINTER(u64)], C.c_int),
+    "psf_nodes_encode": ([C.POINTER(vp), C.POINTER(vp), C.c_int], C.c_int),
+    "psf_nodes_decode": ([C.POINTER(vp), C.POINTER(vp), C.c_int], C.c_int),
+    "psf_nodes_roundtrip": ([C.POINTER(vp), C.POINTER(vp), C.POINTER(vp), C.c_int, C.c_int], C.c_int),
     "psf_profile_enable": ([vp, C.c_int], C.c_int),
     "psf_profile_reset": ([vp], C.c_int),
     "psf_profile_read": ([vp, C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_double),

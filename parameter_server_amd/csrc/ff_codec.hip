@@ -740,6 +740,238 @@ __global__ __launch_bounds__(kBlock) void ff_decode(const uint8_t* __restrict__ 
   }
 }
 
+// ------------------------------------------------- batched (many arrays) ---
+// Many small messages (the async-SGD minibatches, the C4 slices) make the
+// per-array launches latency-bound.  The batched kernels take a table of up
+// to kBatchJobs arrays in their kernel arguments; a workgroup finds its array
+// by its index in the batch grid and runs the same tile code as the
+// single-array kernels on its share of that array's tiles.  Aligned f32/f64
+// arrays with num_bytes 1..3 only (the launcher routes the rest to the
+// single-array kernels).
+struct FfJob {
+  const void* x;
+  void* out;         // codes (encode) / values (decode)
+  uint64_t n;
+  float mn, mx;      // encode: preset range; decode: the received range
+  int32_t has_min, has_max;
+  uint32_t seed, lcg_pos;
+  uint32_t mm_wg0, mm_nwg;   // encode: min/max workgroups (mm_nwg 0: both preset)
+  uint32_t wg0, nwg;         // encode / decode workgroups
+  int32_t slot;              // publish slot (encode), -1: none
+  uint32_t ticket;
+};
+constexpr int kBatchJobs = 32;
+struct FfBatch {
+  FfJob job[kBatchJobs];
+  int njobs;
+  uint32_t mm_total;        // workgroups of the min/max kernel (partials count)
+  void* partials;           // K lo[mm_total], K hi[mm_total]
+  PubSlot* pub;             // slot base
+  const uint32_t* lcg_bits;
+  Lcg17 k17;
+  uint32_t a_lane, c_lane;
+  double ratio;
+};
+
+// the job whose [first, first + count) workgroup range holds b
+__device__ __forceinline__ int batch_job(const FfBatch& B, uint32_t b, bool mm) {
+  int j = 0;
+  for (int i = 1; i < B.njobs; ++i)
+    if ((mm ? B.job[i].mm_wg0 : B.job[i].wg0) <= b) j = i;
+  return j;
+}
+
+__device__ __forceinline__ void tile_range_of(size_t ntiles, uint32_t wg, uint32_t nwg, size_t& t0,
+                                              size_t& t1) {
+  const size_t per = (ntiles + nwg - 1) / nwg;
+  t0 = (size_t)wg * per;
+  t1 = t0 + per < ntiles ? t0 + per : ntiles;
+}
+
+template <typename V>
+__global__ __launch_bounds__(kBlock) void ff_minmax_batch(FfBatch B) {
+  typedef typename KeyOf<V>::K K;
+  const int jb = batch_job(B, blockIdx.x, true);
+  const FfJob& J = B.job[jb];
+  const V* __restrict__ x = static_cast<const V*>(J.x);
+  const size_t n = J.n;
+  const uint32_t wg = blockIdx.x - J.mm_wg0;
+  K lo = KeyOf<V>::kLoId, hi = KeyOf<V>::kHiId;
+  const size_t ngroups = n >> 2;
+  const size_t ntiles = (ngroups + kTileGroups - 1) / kTileGroups;
+  size_t t0, t1;
+  tile_range_of(ntiles, wg, J.mm_nwg, t0, t1);
+  for (size_t t = t0; t < t1; ++t) {
+    const size_t gb = t * kTileGroups + threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const size_t g = gb + u * kBlock;
+      if (g < ngroups) {
+        V v[4];
+        Vec4<V>::load(x + 4 * g, v);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc_minmax<V, K>(v[j], lo, hi);
+      }
+    }
+  }
+  if (wg == 0)
+    for (size_t i = (ngroups << 2) + threadIdx.x; i < n; i += kBlock) acc_minmax<V, K>(x[i], lo, hi);
+  block_minmax(lo, hi);
+  if (threadIdx.x == 0) {
+    K* pp = reinterpret_cast<K*>(B.partials);
+    pp[blockIdx.x] = lo;
+    pp[B.mm_total + blockIdx.x] = hi;
+  }
+}
+
+template <typename V, int NB>
+__global__ __launch_bounds__(kBlock) void ff_encode_batch(FfBatch B) {
+  const int jb = batch_job(B, blockIdx.x, false);
+  const FfJob& J = B.job[jb];
+  const V* __restrict__ x = static_cast<const V*>(J.x);
+  uint8_t* __restrict__ out = static_cast<uint8_t*>(J.out);
+  const size_t n = J.n;
+  const uint32_t wg = blockIdx.x - J.wg0;
+  float mn_f = J.mn, mx_f = J.mx;
+  if (J.mm_nwg) {
+    typedef typename KeyOf<V>::K K;
+    const K* pp = reinterpret_cast<const K*>(B.partials);
+    K lo = KeyOf<V>::kLoId, hi = KeyOf<V>::kHiId;
+    for (uint32_t i = threadIdx.x; i < J.mm_nwg; i += kBlock) {
+      const K a = pp[J.mm_wg0 + i], b = pp[B.mm_total + J.mm_wg0 + i];
+      lo = a < lo ? a : lo;
+      hi = b > hi ? b : hi;
+    }
+    block_minmax(lo, hi);
+    float cmn, cmx;
+    if (sizeof(V) == 4) {
+      const float lo_v = key_f32((uint32_t)lo), hi_v = key_f32((uint32_t)hi);
+      cmn = lo_v;
+      cmx = (float)((double)hi_v + 1e-6);
+    } else {
+      const double lo_v = key_f64((uint64_t)lo), hi_v = key_f64((uint64_t)hi);
+      cmn = (float)lo_v;
+      cmx = (float)(hi_v + 1e-6);
+    }
+    if (!J.has_min) mn_f = cmn;
+    if (!J.has_max) mx_f = cmx;
+  }
+  QuantParams q;
+  q.min_v = (double)mn_f;
+  q.max_v = (double)mx_f;
+  q.bin = q.max_v - q.min_v;
+  q.ratio = B.ratio;
+  q.scale = q.ratio / q.bin;
+  q.min_f = mn_f;
+  q.max_f = mx_f;
+  q.scale_f = (float)q.scale;
+  q.fast = q.bin < __builtin_huge_val();
+  if (wg == 0 && threadIdx.x == 0 && J.slot >= 0) {
+    PubSlot* ps = B.pub + J.slot;
+    ps->range[0] = mn_f;
+    ps->range[1] = mx_f;
+    ps->status = (q.bin > 0) ? kOk : kErrBin;
+    publish_ticket(ps, J.ticket);
+  }
+  if (!(q.bin > 0)) return;  // CHECK_GT(bin, 0), fixing_float.h:71
+
+  EncodeParams p{};  // the per-launch constants the tile code reads
+  p.lcg_bits = B.lcg_bits;
+  p.lcg_pos = J.lcg_pos;
+  p.k17 = B.k17;
+  p.a_lane = B.a_lane;
+  p.c_lane = B.c_lane;
+  const size_t ngroups = n >> 2;
+  const size_t ntiles = (ngroups + kTileGroups - 1) / kTileGroups;
+  const size_t nfull = ngroups / kTileGroups;
+  size_t t0, t1;
+  tile_range_of(ntiles, wg, J.nwg, t0, t1);
+  const size_t tf = t1 < nfull ? t1 : nfull;
+  for (size_t t = t0; t < tf; ++t) {
+    const size_t gb = t * kTileGroups + threadIdx.x;
+    V v[4][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) Vec4<V>::load(x + 4 * (gb + u * kBlock), v[u]);
+    encode_full_tile<V, NB>(v, q, p, out, gb);
+  }
+  for (size_t t = (t0 > tf ? t0 : tf); t < t1; ++t) {
+    const size_t gb = t * kTileGroups + threadIdx.x;
+    uint32_t su = lcg_jump(J.seed, 4ull * gb) & kMask17;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const size_t g = gb + u * kBlock;
+      if (g < ngroups) {
+        V v[4];
+        Vec4<V>::load(x + 4 * g, v);
+        uint64_t r[4];
+        quant_group<V, NB>(v, q, su, p.k17, r);
+        store_codes<NB>(out, g, r);
+      }
+      su = step17(p.a_lane, p.c_lane, su);
+    }
+  }
+  const size_t tail = ngroups << 2;
+  if (wg == 0 && threadIdx.x == 0 && tail < n) {
+    uint32_t st = lcg_jump(J.seed, tail);
+    for (size_t i = tail; i < n; ++i) {
+      uint64_t r = quant_floor<V, NB>(x[i], q) + lcg_bit(st);
+      for (int j = 0; j < NB; ++j) { out[i * NB + j] = (uint8_t)(r & 0xFF); r >>= 8; }
+    }
+  }
+}
+
+template <typename V, int NB>
+__global__ __launch_bounds__(kBlock) void ff_decode_batch(FfBatch B) {
+  const int jb = batch_job(B, blockIdx.x, false);
+  const FfJob& J = B.job[jb];
+  const uint8_t* __restrict__ code = static_cast<const uint8_t*>(J.x);
+  V* __restrict__ out = static_cast<V*>(J.out);
+  const size_t n = J.n;
+  const uint32_t wg = blockIdx.x - J.wg0;
+  const double min_v = (double)J.mn, max_v = (double)J.mx;
+  const double bin = max_v - min_v;
+  const double ratio = B.ratio;
+  const size_t ngroups = n >> 2;
+  const size_t ntiles = (ngroups + kTileGroups - 1) / kTileGroups;
+  size_t t0, t1;
+  tile_range_of(ntiles, wg, J.nwg, t0, t1);
+  __shared__ V lut[256];
+  if (NB == 1) {
+    lut[threadIdx.x] = dequant<V>((uint64_t)threadIdx.x, ratio, bin, min_v);
+    __syncthreads();
+  }
+  for (size_t t = t0; t < t1; ++t) {
+    const size_t gb = t * kTileGroups + threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const size_t g = gb + u * kBlock;
+      if (g < ngroups) {
+        V v[4];
+        if (NB == 1) {
+          const uint32_t w = reinterpret_cast<const uint32_t*>(code)[g];
+          v[0] = lut[w & 0xFF];
+          v[1] = lut[(w >> 8) & 0xFF];
+          v[2] = lut[(w >> 16) & 0xFF];
+          v[3] = lut[w >> 24];
+        } else {
+          uint64_t r[4];
+          load_codes<NB>(code, g, r);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = dequant<V>(r[j], ratio, bin, min_v);
+        }
+        Vec4<V>::store(out + 4 * g, v);
+      }
+    }
+  }
+  if (wg == 0) {
+    for (size_t i = (ngroups << 2) + threadIdx.x; i < n; i += kBlock) {
+      uint64_t r = 0;
+      for (int j = 0; j < NB; ++j) r |= (uint64_t)code[i * NB + j] << (8 * j);
+      out[i] = dequant<V>(r, ratio, bin, min_v);
+    }
+  }
+}
+
 // ------------------------------------------------------------ launchers ----
 static inline void lcg_affine_pow(uint64_t k, uint32_t& A, uint32_t& Cc) {
   uint32_t a = kLcgA, c = kLcgC;
@@ -949,6 +1181,135 @@ int ff_decode_launch(const void* code, size_t n, int value_type, int nb, const f
             : dispatch_decode_nb<double, false>(c, n, nb, o, p, st);
   }
   return s == kOk ? launch_status() : s;
+}
+
+
+// ------------------------------------------------------ batched launchers ---
+bool ff_batchable(const void* x, const void* out, size_t n, int nb, bool encode) {
+  if (nb < 1 || nb > 3 || n == 0) return false;
+  const uintptr_t xa = reinterpret_cast<uintptr_t>(x), oa = reinterpret_cast<uintptr_t>(out);
+  const uintptr_t code_align = nb == 2 ? 7 : 3;
+  return encode ? ((xa & 15) == 0 && (oa & code_align) == 0) : ((oa & 15) == 0 && (xa & code_align) == 0);
+}
+
+template <typename V, int NB>
+static void launch_encode_batch(FfBatch& B, uint32_t enc_total, hipStream_t st, Profiler* prof, double bytes_mm,
+                                double bytes_enc) {
+  if (B.mm_total) {
+    ProfScope ps(prof, kKMinmax, st, bytes_mm);
+    hipLaunchKernelGGL((ff_minmax_batch<V>), dim3(B.mm_total), dim3(kBlock), 0, st, B);
+  }
+  ProfScope pe(prof, kKEncode, st, bytes_enc);
+  hipLaunchKernelGGL((ff_encode_batch<V, NB>), dim3(enc_total), dim3(kBlock), 0, st, B);
+}
+
+size_t ff_batch_partials_bytes(const FfArray* arrs, int count) {
+  size_t wgs = 0;
+  for (int i = 0; i < count; ++i)
+    if (!(arrs[i].preset.has_min && arrs[i].preset.has_max)) wgs += tile_grid(arrs[i].n, kMinmaxGrid);
+  return 2 * sizeof(uint64_t) * (wgs + 1);
+}
+
+int ff_encode_batch_launch(int value_type, int nb, const FfArray* arrs, int count, void* partials,
+                           PubSlot* pub_base, hipStream_t st, Profiler* prof) {
+  if (count <= 0) return kOk;
+  if (count > kBatchJobs) return kErrArg;
+  if (value_type != kFloat && value_type != kDouble) return kErrArg;
+  FfBatch B{};
+  B.njobs = count;
+  B.partials = partials;
+  B.pub = pub_base;
+  B.lcg_bits = lcg_bits_device();
+  if (!B.lcg_bits) return kErrHip;
+  B.ratio = ff_ratio(nb);
+  lcg_affine_pow(4ull * kBlock, B.a_lane, B.c_lane);
+  B.a_lane &= kMask17;
+  B.c_lane &= kMask17;
+  for (int k = 0; k < 4; ++k) {
+    lcg_affine_pow((uint64_t)k + 1, B.k17.a[k], B.k17.c[k]);
+    B.k17.a[k] &= kMask17;
+    B.k17.c[k] &= kMask17;
+  }
+  uint32_t mm = 0, enc = 0;
+  double bytes_mm = 0, bytes_enc = 0;
+  const size_t vsz = value_type == kFloat ? 4 : 8;
+  for (int i = 0; i < count; ++i) {
+    const FfArray& a = arrs[i];
+    FfJob& J = B.job[i];
+    J.x = a.x;
+    J.out = a.out;
+    J.n = a.n;
+    J.mn = a.preset.min_value;
+    J.mx = a.preset.max_value;
+    J.has_min = a.preset.has_min;
+    J.has_max = a.preset.has_max;
+    J.seed = a.seed;
+    J.lcg_pos = lcg_cycle().pos[a.seed & kMask17];
+    J.slot = a.slot;
+    J.ticket = a.ticket;
+    J.mm_wg0 = mm;
+    J.mm_nwg = (a.preset.has_min && a.preset.has_max) ? 0u : (uint32_t)tile_grid(a.n, kMinmaxGrid);
+    mm += J.mm_nwg;
+    J.wg0 = enc;
+    J.nwg = (uint32_t)tile_grid(a.n, kStreamGrid);
+    enc += J.nwg;
+    if (J.mm_nwg) bytes_mm += (double)a.n * vsz;
+    bytes_enc += (double)a.n * (vsz + nb);
+  }
+  B.mm_total = mm;
+  if (value_type == kFloat) {
+    switch (nb) {
+      case 1: launch_encode_batch<float, 1>(B, enc, st, prof, bytes_mm, bytes_enc); break;
+      case 2: launch_encode_batch<float, 2>(B, enc, st, prof, bytes_mm, bytes_enc); break;
+      default: launch_encode_batch<float, 3>(B, enc, st, prof, bytes_mm, bytes_enc); break;
+    }
+  } else {
+    switch (nb) {
+      case 1: launch_encode_batch<double, 1>(B, enc, st, prof, bytes_mm, bytes_enc); break;
+      case 2: launch_encode_batch<double, 2>(B, enc, st, prof, bytes_mm, bytes_enc); break;
+      default: launch_encode_batch<double, 3>(B, enc, st, prof, bytes_mm, bytes_enc); break;
+    }
+  }
+  return launch_status();
+}
+
+int ff_decode_batch_launch(int value_type, int nb, const FfDecArray* arrs, int count, hipStream_t st,
+                           Profiler* prof) {
+  if (count <= 0) return kOk;
+  if (count > kBatchJobs) return kErrArg;
+  FfBatch B{};
+  B.njobs = count;
+  B.ratio = ff_ratio(nb);
+  uint32_t wg = 0;
+  double bytes = 0;
+  const size_t vsz = value_type == kFloat ? 4 : 8;
+  for (int i = 0; i < count; ++i) {
+    FfJob& J = B.job[i];
+    J.x = arrs[i].code;
+    J.out = arrs[i].out;
+    J.n = arrs[i].n;
+    J.mn = arrs[i].mn;
+    J.mx = arrs[i].mx;
+    J.wg0 = wg;
+    J.nwg = (uint32_t)tile_grid(arrs[i].n, kStreamGrid);
+    wg += J.nwg;
+    bytes += (double)arrs[i].n * (vsz + nb);
+  }
+  ProfScope ps(prof, kKDecode, st, bytes);
+  if (value_type == kFloat) {
+    switch (nb) {
+      case 1: hipLaunchKernelGGL((ff_decode_batch<float, 1>), dim3(wg), dim3(kBlock), 0, st, B); break;
+      case 2: hipLaunchKernelGGL((ff_decode_batch<float, 2>), dim3(wg), dim3(kBlock), 0, st, B); break;
+      default: hipLaunchKernelGGL((ff_decode_batch<float, 3>), dim3(wg), dim3(kBlock), 0, st, B); break;
+    }
+  } else {
+    switch (nb) {
+      case 1: hipLaunchKernelGGL((ff_decode_batch<double, 1>), dim3(wg), dim3(kBlock), 0, st, B); break;
+      case 2: hipLaunchKernelGGL((ff_decode_batch<double, 2>), dim3(wg), dim3(kBlock), 0, st, B); break;
+      default: hipLaunchKernelGGL((ff_decode_batch<double, 3>), dim3(wg), dim3(kBlock), 0, st, B); break;
+    }
+  }
+  return launch_status();
 }
 
 }  // namespace psf

@@ -496,6 +496,61 @@ int psf_node_roundtrip(psf_node* snd, psf_node* rcv, const psf_message* const* t
   });
 }
 
+int psf_nodes_encode(psf_node* const* nodes, psf_message* const* msgs, int n) {
+  return guarded([&] {
+    if (n < 0 || (n && (!nodes || !msgs))) return PSF_ERR_ARG;
+    std::vector<psf::RemoteNode*> nd(n);
+    std::vector<psf::Message*> ms(n);
+    for (int i = 0; i < n; ++i) {
+      if (!nodes[i] || !msgs[i]) return PSF_ERR_ARG;
+      nd[i] = nodes[i]->impl;
+      ms[i] = &msgs[i]->m;
+    }
+    psf::encode_batch(nd.data(), ms.data(), n);
+    return PSF_OK;
+  });
+}
+int psf_nodes_decode(psf_node* const* nodes, psf_message* const* msgs, int n) {
+  return guarded([&] {
+    if (n < 0 || (n && (!nodes || !msgs))) return PSF_ERR_ARG;
+    std::vector<psf::RemoteNode*> nd(n);
+    std::vector<psf::Message*> ms(n);
+    for (int i = 0; i < n; ++i) {
+      if (!nodes[i] || !msgs[i]) return PSF_ERR_ARG;
+      nd[i] = nodes[i]->impl;
+      ms[i] = &msgs[i]->m;
+    }
+    psf::decode_batch(nd.data(), ms.data(), n);
+    return PSF_OK;
+  });
+}
+int psf_nodes_roundtrip(psf_node* const* snd, psf_node* const* rcv, const psf_message* const* tmpls, int n,
+                        int iters) {
+  return guarded([&] {
+    if (n <= 0 || iters < 0 || !snd || !rcv || !tmpls) return PSF_ERR_ARG;
+    std::vector<psf::RemoteNode*> s(n), r(n);
+    for (int i = 0; i < n; ++i) {
+      s[i] = snd[i]->impl;
+      r[i] = rcv[i]->impl;
+    }
+    std::vector<psf::Message> m(n), w(n);
+    std::vector<psf::Message*> mp(n), wp(n);
+    for (int it = 0; it < iters; ++it) {
+      for (int i = 0; i < n; ++i) {
+        m[i] = tmpls[i]->m;  // fresh Task + zero-copy buffers
+        mp[i] = &m[i];
+      }
+      psf::encode_batch(s.data(), mp.data(), n);
+      for (int i = 0; i < n; ++i) {
+        w[i] = m[i];  // delivered copy
+        wp[i] = &w[i];
+      }
+      psf::decode_batch(r.data(), wp.data(), n);
+    }
+    return PSF_OK;
+  });
+}
+
 int psf_profile_enable(psf_context* ctx, int kernel_mask) {
   if (!ctx) return PSF_ERR_ARG;
   ctx->impl->prof()->enable((uint32_t)kernel_mask);

@@ -26,6 +26,7 @@ class Filter {
   // FIXING_FLOAT decode may leave its codes for the consumer to dequantise
   // (see PendingDequant); set by RemoteNode::set_defer_dequant.
   void set_defer_dequant(bool v) { defer_dequant_ = v; }
+  bool defer_dequant() const { return defer_dequant_; }
 
   // filter.cc:26-31: the first config of that type, or null.
   static FilterConfig* find(FilterConfig::Type type, Message* msg) { return find(type, &msg->task); }
@@ -71,11 +72,18 @@ class KeyCachingFilter : public Filter {
 };
 
 // FIXING_FLOAT, fixing_float.h:6-103
+struct FfMessage {
+  Message* msg;
+  bool defer;  // the decoding node defers the dequantise (see PendingDequant)
+};
 class FixingFloatFilter : public Filter {
  public:
   using Filter::Filter;
   void encode(Message* msg) override { convert(msg, true); }
   void decode(Message* msg) override { convert(msg, false); }
+  // the element work of many messages at once (FIXING_FLOAT is stateless)
+  static void encode_messages(Context* ctx, std::vector<FfMessage>& msgs);
+  static void decode_messages(Context* ctx, std::vector<FfMessage>& msgs);
 
  private:
   void convert(Message* msg, bool encode);
@@ -116,6 +124,13 @@ class RemoteNode {
   bool defer_dequant_ = false;
   std::unordered_map<int, Filter*> filters_;
 };
+
+// RemoteNode::EncodeMessage / DecodeMessage of n messages at once, message i
+// on nodes[i] (each message still runs its own chain, in its own order, on its
+// own node's filter instances; stateful filters see their messages in array
+// order).  FIXING_FLOAT's element work is batched across the messages.
+void encode_batch(RemoteNode* const* nodes, Message* const* msgs, int n);
+void decode_batch(RemoteNode* const* nodes, Message* const* msgs, int n);
 
 // Run the dequantise a deferred FIXING_FLOAT decode left pending (every
 // pending value array of msg becomes decoded data, as DecodeMessage would

@@ -4,6 +4,8 @@
 #include <math.h>
 
 #include <algorithm>
+#include <functional>
+#include <map>
 #include <vector>
 
 #include "filter.h"
@@ -89,102 +91,198 @@ void KeyCachingFilter::decode(Message* msg) {  // key_caching.h:36-60
 
 // -------------------------------------------------------- FIXING_FLOAT ----
 void FixingFloatFilter::convert(Message* msg, bool encode) {  // fixing_float.h:24-47
-  FilterConfig* conf = find(FilterConfig::FIXING_FLOAT, msg);
+  std::vector<FfMessage> one{FfMessage{msg, defer_dequant_}};
+  if (encode) encode_messages(ctx_, one);
+  else decode_messages(ctx_, one);
+}
+
+namespace {
+struct FfJob {
+  Message* msg;
+  int i;     // value index
+  int type;  // FLOAT / DOUBLE
+  int nb;
+  FixedFloatConfig* fp;
+  Buffer in, out;
+  size_t elems;
+};
+
+// the value arrays FixingFloatFilter::convert touches in one message
+// (fixing_float.h:24-47); false when num_bytes == 0 (the filter does nothing)
+bool collect_jobs(Message* msg, std::vector<FfJob>* jobs) {
+  FilterConfig* conf = Filter::find(FilterConfig::FIXING_FLOAT, msg);
   if (!conf) throw CheckError(kErrCheck, "CHECK_NOTNULL(find(FIXING_FLOAT))");
-  if (conf->num_bytes == 0) return;
+  if (conf->num_bytes == 0) return false;
   const int n = (int)msg->value.size();
   if (n != (int)msg->task.value_type.size())
     throw CheckError(kErrCheck, "CHECK_EQ(value.size(), value_type_size())");
-
-  struct Job { int i; int type; FixedFloatConfig* fp; Buffer in, out; size_t elems; };
-  std::vector<Job> jobs;
+  const size_t first = jobs->size();
   int k = 0;
   for (int i = 0; i < n; ++i) {
     if (msg->value[i].empty()) continue;
     const int type = msg->task.value_type[i];
     if ((int)conf->fixed_point.size() <= k) conf->fixed_point.emplace_back();
-    if (type == kFloat || type == kDouble) jobs.push_back(Job{i, type, &conf->fixed_point[k++], {}, {}, 0});
+    if (type == kFloat || type == kDouble)
+      jobs->push_back(FfJob{msg, i, type, conf->num_bytes, &conf->fixed_point[k++], {}, {}, 0});
   }
-  if (jobs.empty()) return;
-  const int nb = conf->num_bytes;
-  if (nb <= 0 || nb >= 8) throw CheckError(kErrNbytes, "CHECK_GT(nbytes,0) / CHECK_LT(nbytes,8)");
-  const double ratio = ff_ratio(nb);
-  (void)ratio;
-  hipStream_t st = ctx_->stream();
+  if (jobs->size() > first) {
+    const int nb = conf->num_bytes;
+    if (nb <= 0 || nb >= 8) throw CheckError(kErrNbytes, "CHECK_GT(nbytes,0) / CHECK_LT(nbytes,8)");
+  }
+  return true;
+}
 
-  if (!encode) {  // fixing_float.h:89-101
-    // Deferral is only sound when nothing decoded after this filter reads the
-    // values: decode runs in reverse order, so every filter listed before
-    // FIXING_FLOAT must be KEY_CACHING (keys only).
-    bool defer = defer_dequant_;
-    for (const auto& f : msg->task.filter) {
+// jobs [b, e) grouped for batched launches: same (type, nb), batchable
+template <typename F>
+void for_each_batch(std::vector<FfJob>& jobs, size_t b, size_t e, bool encode, F&& launch_one,
+                    std::function<void(std::vector<size_t>&)> launch_batch) {
+  std::map<std::pair<int, int>, std::vector<size_t>> groups;
+  for (size_t q = b; q < e; ++q) {
+    FfJob& j = jobs[q];
+    if (e - b > 1 && ff_batchable(j.in.ptr, j.out.ptr, j.elems, j.nb, encode))
+      groups[{j.type, j.nb}].push_back(q);
+    else
+      launch_one(q);
+  }
+  for (auto& g : groups) {
+    for (size_t k = 0; k < g.second.size(); k += kFfBatchMax) {
+      std::vector<size_t> part(g.second.begin() + k,
+                               g.second.begin() + std::min(g.second.size(), k + (size_t)kFfBatchMax));
+      if (part.size() == 1) launch_one(part[0]);
+      else launch_batch(part);
+    }
+  }
+}
+}  // namespace
+
+// FIXING_FLOAT encode (fixing_float.h:50-88) of every value array of `msgs`.
+// Computed min/max (and the CHECK_GT(bin,0) outcome) are published by
+// workgroup 0 of each array's encode to a host-mapped slot as soon as it has
+// folded the partials; the FilterConfigs are filled from there while the
+// grids are still streaming.  One array: the single-array kernels; several:
+// batched launches of up to kFfBatchMax arrays (one launch per kernel for a
+// whole batch of small messages).
+void FixingFloatFilter::encode_messages(Context* ctx, std::vector<FfMessage>& msgs) {
+  std::vector<FfJob> jobs;
+  for (auto& m : msgs) collect_jobs(m.msg, &jobs);
+  if (jobs.empty()) return;
+  hipStream_t st = ctx->stream();
+  for (size_t base = 0; base < jobs.size(); base += Context::kSlots) {
+    const size_t end = std::min(jobs.size(), base + (size_t)Context::kSlots);
+    std::vector<uint32_t> tickets(end - base, 0);
+    std::vector<FixedPoint> presets(end - base);
+    std::vector<uint32_t> seeds(end - base);
+    for (size_t q = base; q < end; ++q) {
+      FfJob& j = jobs[q];
+      const size_t vsz = j.type == kFloat ? 4 : 8;
+      j.in = ctx->to_device(j.msg->value[j.i]);
+      j.elems = j.in.bytes / vsz;
+      if (j.elems == 0) throw CheckError(kErrArg, "value array shorter than one element");
+      FixedPoint& preset = presets[q - base];
+      preset = FixedPoint{j.fp->has_min, j.fp->has_max, j.fp->min_value, j.fp->max_value};
+      if (preset.has_min && preset.has_max) {
+        if (!((double)preset.max_value - (double)preset.min_value > 0))
+          throw CheckError(kErrBin, "CHECK_GT(bin, 0)");
+      } else {
+        tickets[q - base] = ctx->next_ticket();
+      }
+      j.out = ctx->alloc(j.elems * (size_t)j.nb);
+      seeds[q - base] = (uint32_t)ff_clock_seed();  // `int seed = time(NULL)`, per array
+    }
+    auto one = [&](size_t q) {
+      FfJob& j = jobs[q];
+      const uint32_t t = tickets[q - base];
+      int s = ff_encode_launch(j.in.ptr, j.elems, j.type, j.nb, presets[q - base], seeds[q - base], j.out.ptr,
+                               ctx->partials(), nullptr, nullptr, st, ctx->prof(),
+                               t ? ctx->pub_dev((int)(q - base)) : nullptr, t);
+      if (s != kOk) throw CheckError(s, "ff_encode launch failed");
+    };
+    auto batch = [&](std::vector<size_t>& part) {
+      std::vector<FfArray> arrs;
+      for (size_t q : part) {
+        const FfJob& j = jobs[q];
+        const uint32_t t = tickets[q - base];
+        arrs.push_back(FfArray{j.in.ptr, j.out.ptr, j.elems, presets[q - base], seeds[q - base],
+                               t ? (int)(q - base) : -1, t});
+      }
+      Buffer scratch = ctx->alloc(ff_batch_partials_bytes(arrs.data(), (int)arrs.size()));
+      int s = ff_encode_batch_launch(jobs[part[0]].type, jobs[part[0]].nb, arrs.data(), (int)arrs.size(),
+                                     scratch.ptr, ctx->pub_dev(0), st, ctx->prof());
+      if (s != kOk) throw CheckError(s, "ff_encode batch launch failed");
+    };
+    for_each_batch(jobs, base, end, true, one, batch);
+    for (size_t q = base; q < end; ++q) {
+      FfJob& j = jobs[q];
+      if (tickets[q - base]) {
+        ctx->wait_ticket((int)(q - base), tickets[q - base]);
+        const Slot& hs = *ctx->pub_host((int)(q - base));
+        if (!j.fp->has_min) j.fp->set_min(hs.range[0]);
+        if (!j.fp->has_max) j.fp->set_max(hs.range[1]);
+        if (hs.status != kOk) throw CheckError(kErrBin, "CHECK_GT(bin, 0)");
+      }
+      j.msg->value[j.i] = j.out;
+    }
+  }
+}
+
+// FIXING_FLOAT decode (fixing_float.h:89-101) of every value array of `msgs`;
+// a message whose node defers the dequantise keeps its codes pending
+// (only where every filter listed before FIXING_FLOAT is KEY_CACHING, so
+// nothing decoded after it reads values).
+void FixingFloatFilter::decode_messages(Context* ctx, std::vector<FfMessage>& msgs) {
+  std::vector<FfJob> jobs;
+  for (auto& m : msgs) {
+    const size_t first = jobs.size();
+    if (!collect_jobs(m.msg, &jobs)) continue;
+    bool defer = m.defer;
+    for (const auto& f : m.msg->task.filter) {
       if (f.type == FilterConfig::FIXING_FLOAT) break;
       if (f.type != FilterConfig::KEY_CACHING) defer = false;
     }
-    for (auto& j : jobs) {
+    size_t keep = first;
+    for (size_t q = first; q < jobs.size(); ++q) {
+      FfJob& j = jobs[q];
       const FixedFloatConfig& fp = *j.fp;
       if (!fp.has_min) throw CheckError(kErrCheck, "CHECK(conf->has_min_value())");
       if (!fp.has_max) throw CheckError(kErrCheck, "CHECK(conf->has_max_value())");
       const double bin = (double)fp.max_value - (double)fp.min_value;
       if (!(bin > 0)) throw CheckError(kErrBin, "CHECK_GT(bin, 0)");
       if (defer && j.type == kFloat) {
+        Message* msg = j.msg;
         if (msg->pending.size() < msg->value.size()) msg->pending.resize(msg->value.size());
-        msg->pending[j.i] = PendingDequant{nb, fp.min_value, fp.max_value};
+        msg->pending[j.i] = PendingDequant{j.nb, fp.min_value, fp.max_value};
         continue;
       }
-      const size_t vsz = j.type == kFloat ? 4 : 8;
-      Buffer code = ctx_->to_device(msg->value[j.i]);
-      const size_t elems = code.bytes / (size_t)nb;
-      Buffer out = ctx_->alloc(elems * vsz);
-      int s = ff_decode_launch(code.ptr, elems, j.type, nb, nullptr, fp.min_value, fp.max_value, out.ptr, st,
-                               ctx_->prof());
-      if (s != kOk) throw CheckError(s, "ff_decode launch failed");
-      msg->value[j.i] = out;
+      jobs[keep++] = j;
     }
-    return;
+    jobs.resize(keep);
   }
-
-  // encode, fixing_float.h:50-88.  Computed min/max (and the CHECK_GT(bin,0)
-  // outcome) are published by workgroup 0 of each encode kernel to a
-  // host-mapped slot as soon as it has folded the partials; the FilterConfig is
-  // filled from there while the rest of the grid is still streaming.
-  for (size_t base = 0; base < jobs.size(); base += Context::kSlots) {
-    const size_t end = std::min(jobs.size(), base + (size_t)Context::kSlots);
-    std::vector<uint32_t> tickets(end - base, 0);
-    for (size_t q = base; q < end; ++q) {
-      Job& j = jobs[q];
-      const size_t vsz = j.type == kFloat ? 4 : 8;
-      j.in = ctx_->to_device(msg->value[j.i]);
-      j.elems = j.in.bytes / vsz;
-      if (j.elems == 0) throw CheckError(kErrArg, "value array shorter than one element");
-      FixedPoint preset{j.fp->has_min, j.fp->has_max, j.fp->min_value, j.fp->max_value};
-      PubSlot* pub = nullptr;
-      if (preset.has_min && preset.has_max) {
-        if (!((double)preset.max_value - (double)preset.min_value > 0))
-          throw CheckError(kErrBin, "CHECK_GT(bin, 0)");
-      } else {
-        tickets[q - base] = ctx_->next_ticket();
-        pub = ctx_->pub_dev((int)(q - base));
-      }
-      j.out = ctx_->alloc(j.elems * (size_t)nb);
-      const uint32_t seed = (uint32_t)ff_clock_seed();  // `int seed = time(NULL)`, per array
-      int s = ff_encode_launch(j.in.ptr, j.elems, j.type, nb, preset, seed, j.out.ptr,
-                               ctx_->partials(), nullptr, nullptr, st, ctx_->prof(), pub,
-                               tickets[q - base]);
-      if (s != kOk) throw CheckError(s, "ff_encode launch failed");
-    }
-    for (size_t q = base; q < end; ++q) {
-      Job& j = jobs[q];
-      if (tickets[q - base]) {
-        ctx_->wait_ticket((int)(q - base), tickets[q - base]);
-        const Slot& hs = *ctx_->pub_host((int)(q - base));
-        if (!j.fp->has_min) j.fp->set_min(hs.range[0]);
-        if (!j.fp->has_max) j.fp->set_max(hs.range[1]);
-        if (hs.status != kOk) throw CheckError(kErrBin, "CHECK_GT(bin, 0)");
-      }
-      msg->value[j.i] = j.out;
-    }
+  if (jobs.empty()) return;
+  hipStream_t st = ctx->stream();
+  for (auto& j : jobs) {
+    const size_t vsz = j.type == kFloat ? 4 : 8;
+    j.in = ctx->to_device(j.msg->value[j.i]);
+    j.elems = j.in.bytes / (size_t)j.nb;
+    j.out = ctx->alloc(j.elems * vsz);
   }
+  auto one = [&](size_t q) {
+    FfJob& j = jobs[q];
+    int s = ff_decode_launch(j.in.ptr, j.elems, j.type, j.nb, nullptr, j.fp->min_value, j.fp->max_value,
+                             j.out.ptr, st, ctx->prof());
+    if (s != kOk) throw CheckError(s, "ff_decode launch failed");
+  };
+  auto batch = [&](std::vector<size_t>& part) {
+    std::vector<FfDecArray> arrs;
+    for (size_t q : part) {
+      const FfJob& j = jobs[q];
+      arrs.push_back(FfDecArray{j.in.ptr, j.out.ptr, j.elems, j.fp->min_value, j.fp->max_value});
+    }
+    int s = ff_decode_batch_launch(jobs[part[0]].type, jobs[part[0]].nb, arrs.data(), (int)arrs.size(), st,
+                                   ctx->prof());
+    if (s != kOk) throw CheckError(s, "ff_decode batch launch failed");
+  };
+  for_each_batch(jobs, 0, jobs.size(), false, one, batch);
+  for (auto& j : jobs) j.msg->value[j.i] = j.out;
 }
 
 // --------------------------------------------------------- COMPRESSING ----
@@ -262,6 +360,41 @@ void RemoteNode::EncodeMessage(Message* msg) {  // remote_node.cc:17-22
 void RemoteNode::DecodeMessage(Message* msg) {  // remote_node.cc:23-29, reverse order
   for (int i = (int)msg->task.filter.size() - 1; i >= 0; --i)
     FindFilterOrCreate(msg->task.filter[i])->decode(msg);
+}
+
+void encode_batch(RemoteNode* const* nodes, Message* const* msgs, int n) {
+  size_t maxlen = 0;
+  for (int i = 0; i < n; ++i) maxlen = std::max(maxlen, msgs[i]->task.filter.size());
+  for (size_t pos = 0; pos < maxlen; ++pos) {  // filter position pos of every chain
+    std::map<Context*, std::vector<FfMessage>> ff;
+    for (int i = 0; i < n; ++i) {
+      if (pos >= msgs[i]->task.filter.size()) continue;
+      const FilterConfig& conf = msgs[i]->task.filter[pos];
+      Filter* f = nodes[i]->FindFilterOrCreate(conf);
+      if (conf.type == FilterConfig::FIXING_FLOAT) ff[nodes[i]->ctx()].push_back(FfMessage{msgs[i], false});
+      else f->encode(msgs[i]);
+    }
+    for (auto& kv : ff) FixingFloatFilter::encode_messages(kv.first, kv.second);
+  }
+}
+
+void decode_batch(RemoteNode* const* nodes, Message* const* msgs, int n) {
+  size_t maxlen = 0;
+  for (int i = 0; i < n; ++i) maxlen = std::max(maxlen, msgs[i]->task.filter.size());
+  for (size_t r = 0; r < maxlen; ++r) {  // r-th filter from the end of every chain
+    std::map<Context*, std::vector<FfMessage>> ff;
+    for (int i = 0; i < n; ++i) {
+      const size_t len = msgs[i]->task.filter.size();
+      if (r >= len) continue;
+      const FilterConfig& conf = msgs[i]->task.filter[len - 1 - r];
+      Filter* f = nodes[i]->FindFilterOrCreate(conf);
+      if (conf.type == FilterConfig::FIXING_FLOAT)
+        ff[nodes[i]->ctx()].push_back(FfMessage{msgs[i], f->defer_dequant()});
+      else
+        f->decode(msgs[i]);
+    }
+    for (auto& kv : ff) FixingFloatFilter::decode_messages(kv.first, kv.second);
+  }
 }
 
 void RemoteNode::set_defer_dequant(bool v) {

@@ -103,6 +103,31 @@ int ff_encode_launch(const void* x, size_t n, int value_type, int nb, const Fixe
                      uint32_t ticket = 0);
 int ff_decode_launch(const void* code, size_t n, int value_type, int nb, const float* range,
                      float mn, float mx, void* out, hipStream_t st, Profiler* prof = nullptr);
+// Batched launches over up to kFfBatchMax arrays of one value type and
+// num_bytes (aligned, nb 1..3: ff_batchable); encode publishes each array's
+// side-info to pub_base[slot] with its ticket.
+constexpr int kFfBatchMax = 32;
+struct FfArray {
+  const void* x;
+  void* out;
+  size_t n;
+  FixedPoint preset;
+  uint32_t seed;
+  int slot;
+  uint32_t ticket;
+};
+struct FfDecArray {
+  const void* code;
+  void* out;
+  size_t n;
+  float mn, mx;
+};
+bool ff_batchable(const void* x, const void* out, size_t n, int nb, bool encode);
+size_t ff_batch_partials_bytes(const FfArray* arrs, int count);
+int ff_encode_batch_launch(int value_type, int nb, const FfArray* arrs, int count, void* partials,
+                           PubSlot* pub_base, hipStream_t st, Profiler* prof);
+int ff_decode_batch_launch(int value_type, int nb, const FfDecArray* arrs, int count, hipStream_t st,
+                           Profiler* prof);
 
 // crc32c.hip: CRC32C of d[0:n) written to *out (device).  n may be any size.
 // When the message fits one workgroup (n <= kCrcSingleBlock) the result is also

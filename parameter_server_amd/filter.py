@@ -455,6 +455,33 @@ class RemoteNode:
         """Server side: FIXING_FLOAT decode leaves codes for the consumer."""
         check(lib().psf_node_set_defer_dequant(self.h, int(on)))
 
+    @staticmethod
+    def encode_many(nodes, msgs) -> None:
+        """psf_nodes_encode: msgs[i] through nodes[i]'s chain, FIXING_FLOAT batched."""
+        for nd, m in zip(nodes, msgs):
+            nd._hold(m)
+        n = len(msgs)
+        check(lib().psf_nodes_encode((C.c_void_p * n)(*[nd.h.value for nd in nodes]),
+                                     (C.c_void_p * n)(*[m.h.value for m in msgs]), n))
+
+    @staticmethod
+    def decode_many(nodes, msgs) -> None:
+        for nd, m in zip(nodes, msgs):
+            nd._hold(m)
+        n = len(msgs)
+        check(lib().psf_nodes_decode((C.c_void_p * n)(*[nd.h.value for nd in nodes]),
+                                     (C.c_void_p * n)(*[m.h.value for m in msgs]), n))
+
+    @staticmethod
+    def roundtrip_many(snd, rcv, tmpls, iters: int) -> None:
+        n = len(tmpls)
+        for nd in list(snd) + list(rcv):
+            for t in tmpls:
+                nd._hold(t)
+        check(lib().psf_nodes_roundtrip((C.c_void_p * n)(*[nd.h.value for nd in snd]),
+                                        (C.c_void_p * n)(*[nd.h.value for nd in rcv]),
+                                        (C.c_void_p * n)(*[t.h.value for t in tmpls]), n, iters))
+
     def encode(self, msg: Message) -> None:
         self._hold(msg)
         check(lib().psf_node_encode(self.h, msg.h))

@@ -1,0 +1,126 @@
+"""GPU: many messages through psf_nodes_encode / psf_nodes_decode (FIXING_FLOAT
+batched across messages) give exactly what one-at-a-time RemoteNode calls and
+the C restatement give: codes, side-info and decoded values bit-exact, for
+mixed sizes (tiny, ragged, partial tiles), num_bytes 1-3, f32 / f64, preset
+and computed ranges, chains with KEY_CACHING and COMPRESSING, deferred
+dequantise."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+def _cases():
+    rng = np.random.default_rng(42)
+    sizes = [1, 3, 4, 5, 1023, 4096, 4099, 100_003, 262_144, 70_001]
+    out = []
+    for k in range(48):
+        n = sizes[k % len(sizes)] + (k // len(sizes))
+        dt = np.float64 if k % 7 == 3 else np.float32
+        nb = 1 + k % 3
+        preset = [None, (-1.5, 1.5), (None, 2.0)][k % 3 if k % 5 else 0]
+        x = (rng.standard_normal(n) * (1 + k)).astype(dt)
+        keys = np.unique(rng.integers(0, 10**9, n + 16).astype(np.uint64))[:n] if k % 4 else None
+        out.append((x, nb, preset, keys))
+    return out
+
+
+def _message(F, x, nb, preset, keys, ch, compress=False):
+    from parameter_server_amd import COMPRESSING, FIXING_FLOAT, KEY_CACHING
+    m = F.Message(request=True, push=True, key_channel=ch, key_range=(0, 10**9))
+    if keys is not None:
+        m.set_key(torch.from_numpy(keys.view(np.int64)).to(DEV))
+        m.add_filter(KEY_CACHING)
+    m.add_value(torch.from_numpy(x).to(DEV))
+    fp = None if preset is None else [preset]
+    m.add_filter(FIXING_FLOAT, num_bytes=nb, fixed_point=fp)
+    if compress:
+        m.add_filter(COMPRESSING)
+    return m
+
+
+@pytest.mark.parametrize("compress", [False, True])
+def test_batch_matches_single_and_port(ctx, port, compress):
+    from parameter_server_amd import filter as F
+    F.set_clock(987654)
+    try:
+        cases = _cases()
+        snd_b = [F.RemoteNode(ctx) for _ in cases]
+        rcv_b = [F.RemoteNode(ctx) for _ in cases]
+        snd_s = [F.RemoteNode(ctx) for _ in cases]
+        rcv_s = [F.RemoteNode(ctx) for _ in cases]
+        mb = [_message(F, *c, ch=i, compress=compress) for i, c in enumerate(cases)]
+        ms = [_message(F, *c, ch=i, compress=compress) for i, c in enumerate(cases)]
+        F.RemoteNode.encode_many(snd_b, mb)
+        for nd, m in zip(snd_s, ms):
+            nd.encode(m)
+        wb = [m.clone() for m in mb]
+        ws = [m.clone() for m in ms]
+        F.RemoteNode.decode_many(rcv_b, wb)
+        for nd, m in zip(rcv_s, ws):
+            nd.decode(m)
+        ctx.sync()
+        for i, (x, nb, preset, keys) in enumerate(cases):
+            fi = 1 if keys is not None else 0
+            assert mb[i].fixed_points(fi) == ms[i].fixed_points(fi), i
+            vb, vs = snd_b[i].value(mb[i], 0), snd_s[i].value(ms[i], 0)
+            assert vb.cpu().numpy().tobytes() == vs.cpu().numpy().tobytes(), i
+            db, ds = rcv_b[i].value(wb[i], 0), rcv_s[i].value(ws[i], 0)
+            assert db.cpu().numpy().tobytes() == ds.cpu().numpy().tobytes(), i
+            # and the C restatement of the reference
+            mn = None if preset is None else preset[0]
+            mx = None if preset is None else preset[1]
+            st, codes, pmn, pmx = port.ff_encode(x, nb, 987654, mn, mx)
+            assert st == 0
+            st, dec = port.ff_decode(codes, nb, pmn, pmx, x.dtype)
+            assert db.cpu().numpy().tobytes() == dec.tobytes(), i
+            if not compress:
+                assert vb.cpu().numpy().tobytes() == codes.tobytes(), i
+            if keys is not None:
+                assert rcv_b[i].key(wb[i]).cpu().numpy().view(np.uint64).tobytes() == keys.tobytes(), i
+    finally:
+        F.set_clock(None)
+
+
+def test_batch_deferred_decode(ctx, port):
+    from parameter_server_amd import filter as F
+    F.set_clock(55)
+    try:
+        cases = _cases()[:20]
+        snd = [F.RemoteNode(ctx) for _ in cases]
+        rcv = [F.RemoteNode(ctx) for _ in cases]
+        for r in rcv:
+            r.set_defer_dequant(True)
+        ms = [_message(F, *c, ch=i) for i, c in enumerate(cases)]
+        F.RemoteNode.encode_many(snd, ms)
+        ws = [m.clone() for m in ms]
+        F.RemoteNode.decode_many(rcv, ws)
+        for i, (x, nb, preset, keys) in enumerate(cases):
+            pend = ws[i].pending(0)
+            assert (pend is not None) == (x.dtype == np.float32), i
+            ws[i].materialize(ctx)
+            mn = None if preset is None else preset[0]
+            mx = None if preset is None else preset[1]
+            st, codes, pmn, pmx = port.ff_encode(x, nb, 55, mn, mx)
+            st, dec = port.ff_decode(codes, nb, pmn, pmx, x.dtype)
+            assert rcv[i].value(ws[i], 0).cpu().numpy().tobytes() == dec.tobytes(), i
+    finally:
+        F.set_clock(None)
+
+
+def test_batch_roundtrip_driver(ctx):
+    from parameter_server_amd import FIXING_FLOAT
+    from parameter_server_amd import filter as F
+    tm = []
+    for i in range(40):
+        m = F.Message(request=True, push=True, key_channel=i)
+        m.add_value(torch.randn(100_000 + i, device=DEV))
+        m.add_filter(FIXING_FLOAT, num_bytes=1)
+        tm.append(m)
+    snd = [F.RemoteNode(ctx) for _ in tm]
+    rcv = [F.RemoteNode(ctx) for _ in tm]
+    F.RemoteNode.roundtrip_many(snd, rcv, tm, 3)
+    ctx.sync()
