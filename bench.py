@@ -49,6 +49,10 @@ WORKLOADS = {
           "{m} sorted unique uint64 keys spread over 2^64 (splitmix64) + f32 values, sliced at the "
           "EvenDivide(N) server ranges, per-(stream, server) [KEY_CACHING, FIXING_FLOAT num_bytes={nb}], "
           "cross-range slices spilled in one all-to-all-v per step (RCCL), repeat sends (key cache hit)",
+    "c1": "C1 (BASELINE configs[0]) on the device: the ctr example's push stream "
+          "(example/linear/ctr/online_l1lr.conf: [KEY_CACHING(clear_cache_if_done), FIXING_FLOAT "
+          "num_bytes={nb}]), {streams} concurrent minibatch streams of {m} sorted unique keys + f32 "
+          "gradients, all streams' messages of a step encoded / decoded in one batched call (repeat sends)",
     "c5": "C5 (BASELINE configs[4]) per GPU: 2^20 uint64 keys spread over 2^64 (splitmix64) + "
           "embedding rows dim=128 f32 (512 MiB, one min/max per array), chain [KEY_CACHING, "
           "FIXING_FLOAT num_bytes={nb}{cmp}], repeat send (key cache hit)",
@@ -78,7 +82,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--streams", type=int, default=64, help="c4: push streams in total")
-    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c3miss", "c4", "c5"],
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c3miss", "c4", "c5"],
                     help="c2: dense f32 values (default, the headline); c3: 10M sorted uint64 "
                          "keys from [0,1e9) + f32 values, [KEY_CACHING, FIXING_FLOAT] repeat "
                          "sends (cache hits); c3miss: same with clear_cache_if_done (every send "
@@ -208,7 +212,24 @@ def main():
     F.set_clock(12345)  # FIXING_FLOAT seed (time(NULL) in the reference)
     tmpls = []
     router = None
-    if args.config == "c4":
+    streams_batch = None
+    if args.config == "c1":
+        # async SGD pushes (async_sgd.h:264-296): every minibatch stream pushes
+        # its ~10^5 keys with gradients, [KEY_CACHING, FIXING_FLOAT nb=1]
+        m = args.m or 100_000
+        nstreams = args.streams
+        for sid in range(nstreams):
+            keys = torch.unique(torch.randint(0, 10**9, (m + m // 8,), device=dev, generator=g))[:m]
+            t = F.Message(request=True, push=True, key_channel=sid, key_range=(0, 10**9))
+            t.set_key(torch.sort(keys)[0])
+            t.add_value(torch.randn(m, device=dev, generator=g, dtype=torch.float32))
+            t.add_filter(KEY_CACHING)
+            t.add_filter(FIXING_FLOAT, num_bytes=nb)
+            tmpls.append(t)
+        streams_batch = ([F.RemoteNode(ctx) for _ in tmpls], [F.RemoteNode(ctx) for _ in tmpls])
+        n = m * nstreams
+        payload = 12 * n
+    elif args.config == "c4":
         # stream s lives on rank s % N; every step slices,
         # encodes per destination server, spills and decodes (shard.PushRouter)
         from parameter_server_amd import shard
@@ -281,6 +302,8 @@ def main():
         if router is not None:
             for _ in range(k):
                 router.step(streams)
+        elif streams_batch is not None:
+            F.RemoteNode.roundtrip_many(streams_batch[0], streams_batch[1], tmpl, k)
         else:
             worker.roundtrip(server, tmpl, k)
 
@@ -345,7 +368,7 @@ def main():
         }
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config not in ("c4", "c5"):
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config not in ("c1", "c4", "c5"):
         cpu = cpu_baseline(1 << 24 if args.config == "c2" else 1 << 22, nb, args.cpu_seconds, args.config)
 
     if rank == 0:
@@ -363,11 +386,13 @@ def main():
             "dtype": "f64",
             "data": "synthetic: f32 N(0,1) values, seed 1+rank, FIXING_FLOAT LCG seed 12345"
                     + {"c2": "", "c5": "; sorted unique uint64 keys splitmix64(4+rank+i)",
-                       "c4": "; sorted unique uint64 keys splitmix64(4+stream+i)"}.get(
+                       "c4": "; sorted unique uint64 keys splitmix64(4+stream+i)",
+                       "c1": "; sorted unique uint64 keys from [0,1e9) per stream"}.get(
                         args.config, "; sorted unique uint64 keys from [0,1e9)"),
             "config": {
                 "workload": WORKLOADS[args.config].format(nb=nb, cmp=", COMPRESSING" if args.compress else "",
-                                                          streams=args.streams, m=args.m or (1 << 21)),
+                                                          streams=args.streams,
+                                                          m=args.m or (100_000 if args.config == "c1" else 1 << 21)),
                 "n_values_per_gpu": n,
                 "payload_bytes_per_step_per_gpu": payload,
                 "value_type": "float32",

@@ -135,9 +135,9 @@ __device__ __forceinline__ uint32_t shift_op(const uint32_t (*t)[16], uint32_t a
   return r;
 }
 
-__global__ __launch_bounds__(kBlock) void crc32c_small(const uint8_t* __restrict__ d, uint32_t n,
-                                                        uint32_t* __restrict__ out, PubSlot* pub,
-                                                        uint32_t ticket) {
+// CRC32C of d[0:n), n <= kCrcSingleBlock, by the whole workgroup; the value
+// is valid in thread 0
+__device__ __forceinline__ uint32_t crc_small_block(const uint8_t* __restrict__ d, uint32_t n) {
   __shared__ uint32_t table[256];
   __shared__ uint32_t ops[8][8][16];
   __shared__ uint32_t wave_acc[kBlock / 64];
@@ -174,16 +174,63 @@ __global__ __launch_bounds__(kBlock) void crc32c_small(const uint8_t* __restrict
   }
   if ((t & 63) == 0) wave_acc[t >> 6] = v;
   __syncthreads();
+  uint32_t acc = 0;
   if (t == 0) {
-    uint32_t acc = wave_acc[0];
+    acc = wave_acc[0];
 #pragma unroll
     for (int w = 1; w < kBlock / 64; ++w) acc = shift_op(ops[6], acc) ^ wave_acc[w];  // 512-byte blocks
+  }
+  return acc;
+}
+
+__global__ __launch_bounds__(kBlock) void crc32c_small(const uint8_t* __restrict__ d, uint32_t n,
+                                                        uint32_t* __restrict__ out, PubSlot* pub,
+                                                        uint32_t ticket) {
+  const uint32_t acc = crc_small_block(d, n);
+  if (threadIdx.x == 0) {
     *out = acc;
     if (pub) {
       pub->crc = acc;
       publish_ticket(pub, ticket);
     }
   }
+}
+
+// many short messages (KEY_CACHING signatures of a batch): workgroup b CRCs
+// job b and publishes it to pub[job.slot]
+struct CrcBatch {
+  const uint8_t* d[kCrcBatchMax];
+  uint32_t n[kCrcBatchMax];
+  int32_t slot[kCrcBatchMax];
+  uint32_t ticket[kCrcBatchMax];
+};
+__global__ __launch_bounds__(kBlock) void crc32c_small_batch(CrcBatch B, PubSlot* pub) {
+  const uint32_t b = blockIdx.x;
+  const uint32_t acc = crc_small_block(B.d[b], B.n[b]);
+  if (threadIdx.x == 0) {
+    PubSlot* ps = pub + B.slot[b];
+    ps->crc = acc;
+    publish_ticket(ps, B.ticket[b]);
+  }
+}
+
+int crc32c_batch_launch(const void* const* d, const uint32_t* n, const int* slot, const uint32_t* ticket,
+                        int count, PubSlot* pub, hipStream_t st, Profiler* prof) {
+  if (count <= 0) return kOk;
+  if (count > kCrcBatchMax) return kErrArg;
+  CrcBatch B{};
+  double bytes = 0;
+  for (int i = 0; i < count; ++i) {
+    if (n[i] == 0 || n[i] > kCrcSingleBlock) return kErrArg;
+    B.d[i] = static_cast<const uint8_t*>(d[i]);
+    B.n[i] = n[i];
+    B.slot[i] = slot[i];
+    B.ticket[i] = ticket[i];
+    bytes += n[i];
+  }
+  ProfScope ps(prof, kKCrc, st, bytes);
+  hipLaunchKernelGGL(crc32c_small_batch, dim3(count), dim3(kBlock), 0, st, B, pub);
+  return launch_status();
 }
 
 static X2nTable make_x2n_table() {

@@ -43,6 +43,10 @@ class KeyCachingFilter : public Filter {
   using Filter::Filter;
   void encode(Message* msg) override;
   void decode(Message* msg) override;
+  // the same with the key signature computed by the caller (batched CRCs)
+  void encode_with(Message* msg, uint32_t sig);
+  void decode_with(Message* msg, uint32_t sig);
+  static bool needs_signature(Message* msg, bool encode);
   size_t cache_size() const { return cache_.size(); }
 
  private:

@@ -46,12 +46,23 @@ uint32_t KeyCachingFilter::signature(const Buffer& key) {
 void KeyCachingFilter::encode(Message* msg) {  // key_caching.h:9-34
   FilterConfig* conf = find(FilterConfig::KEY_CACHING, msg);
   if (!conf) return;
+  encode_with(msg, msg->has_key() ? signature(msg->key) : 0u);
+}
+
+bool KeyCachingFilter::needs_signature(Message* msg, bool encode) {
+  FilterConfig* conf = find(FilterConfig::KEY_CACHING, msg);
+  if (!conf || !msg->has_key()) return false;
+  return encode || conf->has_signature;
+}
+
+void KeyCachingFilter::encode_with(Message* msg, uint32_t sig) {
+  FilterConfig* conf = find(FilterConfig::KEY_CACHING, msg);
+  if (!conf) return;
   if (!msg->has_key()) {
     conf->has_signature = false;
     conf->signature = 0;
     return;
   }
-  const uint32_t sig = signature(msg->key);
   conf->has_signature = true;
   conf->signature = sig;
   CacheKey ck{msg->task.key_channel, msg->task.key_range};
@@ -70,9 +81,14 @@ void KeyCachingFilter::encode(Message* msg) {  // key_caching.h:9-34
 void KeyCachingFilter::decode(Message* msg) {  // key_caching.h:36-60
   FilterConfig* conf = find(FilterConfig::KEY_CACHING, msg);
   if (!conf || !conf->has_signature) return;
+  decode_with(msg, msg->has_key() ? signature(msg->key) : 0u);
+}
+
+void KeyCachingFilter::decode_with(Message* msg, uint32_t got) {
+  FilterConfig* conf = find(FilterConfig::KEY_CACHING, msg);
+  if (!conf || !conf->has_signature) return;
   const uint32_t sig = conf->signature;
   if (msg->has_key()) {
-    const uint32_t got = signature(msg->key);
     if (got != sig) throw CheckError(kErrCheck, "KEY_CACHING: key signature mismatch");
   }
   CacheKey ck{msg->task.key_channel, msg->task.key_range};
@@ -362,17 +378,74 @@ void RemoteNode::DecodeMessage(Message* msg) {  // remote_node.cc:23-29, reverse
     FindFilterOrCreate(msg->task.filter[i])->decode(msg);
 }
 
+// KEY_CACHING signatures (CRC32C of the first min(bytes, 2048) key bytes,
+// key_caching.h:18) of many messages: device keys in batched launches, one
+// wait per batch; host keys on the host.  sigs[i] for the listed messages.
+static void batch_signatures(RemoteNode* const* nodes, Message* const* msgs, const std::vector<int>& idx,
+                             std::vector<uint32_t>* sigs) {
+  sigs->assign(idx.size(), 0u);
+  std::map<Context*, std::vector<size_t>> dev;
+  for (size_t k = 0; k < idx.size(); ++k) {
+    const Buffer& key = msgs[idx[k]]->key;
+    const size_t len = std::min(key.bytes, (size_t)2048);
+    if (key.loc == Loc::kHost || nodes[idx[k]]->ctx()->device() < 0) (*sigs)[k] = crc32c_host(key.ptr, len);
+    else dev[nodes[idx[k]]->ctx()].push_back(k);
+  }
+  for (auto& kv : dev) {
+    Context* ctx = kv.first;
+    const std::vector<size_t>& ks = kv.second;
+    const size_t chunk = std::min((size_t)kCrcBatchMax, (size_t)Context::kSlots);
+    for (size_t b = 0; b < ks.size(); b += chunk) {
+      const size_t e = std::min(ks.size(), b + chunk);
+      std::vector<const void*> d;
+      std::vector<uint32_t> n, tk;
+      std::vector<int> slot;
+      for (size_t q = b; q < e; ++q) {
+        const Buffer& key = msgs[idx[ks[q]]]->key;
+        d.push_back(key.ptr);
+        n.push_back((uint32_t)std::min(key.bytes, (size_t)2048));
+        slot.push_back((int)(q - b));
+        tk.push_back(ctx->next_ticket());
+      }
+      int s = crc32c_batch_launch(d.data(), n.data(), slot.data(), tk.data(), (int)d.size(), ctx->pub_dev(0),
+                                  ctx->stream(), ctx->prof());
+      if (s != kOk) throw CheckError(s, "crc32c batch launch failed");
+      for (size_t q = b; q < e; ++q) {
+        ctx->wait_ticket((int)(q - b), tk[q - b]);
+        (*sigs)[ks[q]] = ctx->pub_host((int)(q - b))->crc;
+      }
+    }
+  }
+}
+
 void encode_batch(RemoteNode* const* nodes, Message* const* msgs, int n) {
   size_t maxlen = 0;
   for (int i = 0; i < n; ++i) maxlen = std::max(maxlen, msgs[i]->task.filter.size());
   for (size_t pos = 0; pos < maxlen; ++pos) {  // filter position pos of every chain
     std::map<Context*, std::vector<FfMessage>> ff;
+    std::vector<int> kc, kc_sig;
     for (int i = 0; i < n; ++i) {
       if (pos >= msgs[i]->task.filter.size()) continue;
       const FilterConfig& conf = msgs[i]->task.filter[pos];
       Filter* f = nodes[i]->FindFilterOrCreate(conf);
-      if (conf.type == FilterConfig::FIXING_FLOAT) ff[nodes[i]->ctx()].push_back(FfMessage{msgs[i], false});
-      else f->encode(msgs[i]);
+      if (conf.type == FilterConfig::FIXING_FLOAT) {
+        ff[nodes[i]->ctx()].push_back(FfMessage{msgs[i], false});
+      } else if (conf.type == FilterConfig::KEY_CACHING) {
+        kc.push_back(i);
+        if (KeyCachingFilter::needs_signature(msgs[i], true)) kc_sig.push_back(i);
+      } else {
+        f->encode(msgs[i]);
+      }
+    }
+    if (!kc.empty()) {  // signatures batched, then the caches in message order
+      std::vector<uint32_t> sigs;
+      batch_signatures(nodes, msgs, kc_sig, &sigs);
+      size_t k = 0;
+      for (int i : kc) {
+        const uint32_t sig = (k < kc_sig.size() && kc_sig[k] == i) ? sigs[k++] : 0u;
+        static_cast<KeyCachingFilter*>(nodes[i]->FindFilterOrCreate(msgs[i]->task.filter[pos]))
+            ->encode_with(msgs[i], sig);
+      }
     }
     for (auto& kv : ff) FixingFloatFilter::encode_messages(kv.first, kv.second);
   }
@@ -383,15 +456,31 @@ void decode_batch(RemoteNode* const* nodes, Message* const* msgs, int n) {
   for (int i = 0; i < n; ++i) maxlen = std::max(maxlen, msgs[i]->task.filter.size());
   for (size_t r = 0; r < maxlen; ++r) {  // r-th filter from the end of every chain
     std::map<Context*, std::vector<FfMessage>> ff;
+    std::vector<int> kc, kc_sig;
     for (int i = 0; i < n; ++i) {
       const size_t len = msgs[i]->task.filter.size();
       if (r >= len) continue;
       const FilterConfig& conf = msgs[i]->task.filter[len - 1 - r];
       Filter* f = nodes[i]->FindFilterOrCreate(conf);
-      if (conf.type == FilterConfig::FIXING_FLOAT)
+      if (conf.type == FilterConfig::FIXING_FLOAT) {
         ff[nodes[i]->ctx()].push_back(FfMessage{msgs[i], f->defer_dequant()});
-      else
+      } else if (conf.type == FilterConfig::KEY_CACHING) {
+        kc.push_back(i);
+        if (KeyCachingFilter::needs_signature(msgs[i], false)) kc_sig.push_back(i);
+      } else {
         f->decode(msgs[i]);
+      }
+    }
+    if (!kc.empty()) {
+      std::vector<uint32_t> sigs;
+      batch_signatures(nodes, msgs, kc_sig, &sigs);
+      size_t k = 0;
+      for (int i : kc) {
+        const size_t len = msgs[i]->task.filter.size();
+        const uint32_t sig = (k < kc_sig.size() && kc_sig[k] == i) ? sigs[k++] : 0u;
+        static_cast<KeyCachingFilter*>(nodes[i]->FindFilterOrCreate(msgs[i]->task.filter[len - 1 - r]))
+            ->decode_with(msgs[i], sig);
+      }
     }
     for (auto& kv : ff) FixingFloatFilter::decode_messages(kv.first, kv.second);
   }

@@ -135,6 +135,11 @@ int ff_decode_batch_launch(int value_type, int nb, const FfDecArray* arrs, int c
 constexpr size_t kCrcSingleBlock = 8 * kBlock;
 int crc32c_launch(const void* d, size_t n, uint32_t* out, hipStream_t st,
                   Profiler* prof = nullptr, PubSlot* pub = nullptr, uint32_t ticket = 0);
+// up to kCrcBatchMax buffers of 1..kCrcSingleBlock bytes, one workgroup each,
+// each CRC published to pub[slot[i]] with ticket[i]
+constexpr int kCrcBatchMax = 64;
+int crc32c_batch_launch(const void* const* d, const uint32_t* n, const int* slot, const uint32_t* ticket,
+                        int count, PubSlot* pub, hipStream_t st, Profiler* prof);
 
 // noise.hip: the standard-normal sequence of add_noise.h's default-seeded
 // engine (built once, on the device) and the per-message in-place apply.

@@ -110,30 +110,38 @@ class PushRouter:
 
     def step(self, streams) -> list:
         """streams: {stream id: template Message (key_channel = stream id)} of
-        this rank.  Returns the decoded messages this rank received."""
+        this rank.  Returns the decoded messages this rank received.  All
+        slices of the step are encoded in one batched call (psf_nodes_encode)
+        and all received ones decoded in one (psf_nodes_decode)."""
+        from .filter import RemoteNode
         send = [[] for _ in range(self.world)]
-        decoded = []
+        enc_nodes, enc_msgs, dest = [], [], []
         for sid, tmpl in streams.items():
             m = tmpl.clone()
-            parts = slice_message(self.ctx, m, self.ranges)
-            for d, part in enumerate(parts):
+            for d, part in enumerate(slice_message(self.ctx, m, self.ranges)):
                 if part is None:
                     continue
-                self._sender(sid, d).encode(part)
-                if d == self.rank:
-                    w = part.clone()
-                    self._receiver(sid).decode(w)
-                    decoded.append(w)
-                else:
-                    send[d].extend(part.device_frames(self.device))
+                enc_nodes.append(self._sender(sid, d))
+                enc_msgs.append(part)
+                dest.append((sid, d))
+        if enc_msgs:
+            RemoteNode.encode_many(enc_nodes, enc_msgs)
+        dec_nodes, dec_msgs = [], []
+        for (sid, d), part in zip(dest, enc_msgs):
+            if d == self.rank:
+                dec_nodes.append(self._receiver(sid))
+                dec_msgs.append(part.clone())
+            else:
+                send[d].extend(part.device_frames(self.device))
         if self.world > 1:
             recv = self.exchange.exchange(send)
             for src in range(self.world):
                 for w in parse_frames(recv[src]):
-                    sid = w_channel(w)
-                    self._receiver(sid).decode(w)
-                    decoded.append(w)
-        return decoded
+                    dec_nodes.append(self._receiver(w_channel(w)))
+                    dec_msgs.append(w)
+        if dec_msgs:
+            RemoteNode.decode_many(dec_nodes, dec_msgs)
+        return dec_msgs
 
 
 def w_channel(m) -> int:

@@ -124,3 +124,26 @@ def test_batch_roundtrip_driver(ctx):
     rcv = [F.RemoteNode(ctx) for _ in tm]
     F.RemoteNode.roundtrip_many(snd, rcv, tm, 3)
     ctx.sync()
+
+
+def test_batch_key_caching_order(ctx, port):
+    """Two messages with the same keys and channel on ONE node in one batch:
+    the first misses and caches, the second hits and drops its keys -- as
+    sequential EncodeMessage calls would; a second batch hits for both; the
+    receiver restores the keys."""
+    from parameter_server_amd import filter as F
+    rng = np.random.default_rng(9)
+    keys = np.unique(rng.integers(0, 10**9, 5000).astype(np.uint64))
+    snd, rcv = F.RemoteNode(ctx), F.RemoteNode(ctx)
+    for rnd in range(2):
+        ms = []
+        for j in range(3):
+            x = rng.standard_normal(keys.size).astype(np.float32)
+            ms.append(_message(F, x, 1, None, keys, ch=7))
+        F.RemoteNode.encode_many([snd] * 3, ms)
+        has = [m.key_info()[0] for m in ms]
+        assert has == ([True, False, False] if rnd == 0 else [False, False, False]), (rnd, has)
+        ws = [m.clone() for m in ms]
+        F.RemoteNode.decode_many([rcv] * 3, ws)
+        for w in ws:
+            assert rcv.key(w).cpu().numpy().view(np.uint64).tobytes() == keys.tobytes()
