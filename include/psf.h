@@ -205,6 +205,11 @@ int psf_range_even_divide(uint64_t begin, uint64_t end, uint64_t n, uint64_t i,
 int psf_msg_slice(psf_context* ctx, const psf_message* msg, const uint64_t* bounds, int nranges,
                   int key_bytes, psf_message** outs, int* valid);
 
+/* psf_msg_slice for nmsgs messages (outs / valid: nmsgs x nranges, row-major),
+ * with one device synchronisation for all of them. */
+int psf_msgs_slice(psf_context* ctx, const psf_message* const* msgs, int nmsgs, const uint64_t* bounds,
+                   int nranges, int key_bytes, psf_message** outs, int* valid);
+
 /* Message path driver (what Executor::Submit -> remote peer -> PickActiveMsg
  * does per message, executor.cc:131-146,178-219): for i in [0, iters), encode
  * a fresh copy of tmpls[i % ntmpl] on `snd`, deliver it (Task copy + zero-copy

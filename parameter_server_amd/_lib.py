@@ -92,6 +92,8 @@ SIGNATURES = {
     "psf_node_roundtrip": ([vp, vp, C.POINTER(vp), C.c_int, C.c_int, C.POINTER(vp)], C.c_int),
     "psf_range_even_divide": ([u64, u64, u64, u64, C.POINTER(u64), C.POINTER(u64)], C.c_int),
     "psf_msg_slice": ([vp, vp, C.POINTER(u64), C.c_int, C.c_int, C.POINTER(vp), PI], C.c_int),
+    "psf_msgs_slice": ([vp, C.POINTER(vp), C.c_int, C.POINTER(u64), C.c_int, C.c_int, C.POINTER(vp), PI],
+                       C.c_int),
     "psf_node_set_defer_dequant": ([vp, C.c_int], C.c_int),
     "psf_msg_pending": ([vp, C.c_int, PI, C.POINTER(C.c_float), C.POINTER(C.c_float)], C.c_int),
     "psf_msg_materialize": ([vp, vp], C.c_int),

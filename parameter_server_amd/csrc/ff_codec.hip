@@ -762,6 +762,9 @@ struct FfJob {
 };
 constexpr int kBatchJobs = 32;
 struct FfBatch {
+  uint32_t first[kBatchJobs];     // wg0 of each job (decode / encode grid), unused entries ~0u
+  uint32_t mm_first[kBatchJobs];  // mm_wg0 of the k-th job with a min/max pass, unused ~0u
+  int32_t mm_job[kBatchJobs];     // ... and its job index
   FfJob job[kBatchJobs];
   int njobs;
   uint32_t mm_total;        // workgroups of the min/max kernel (partials count)
@@ -773,12 +776,15 @@ struct FfBatch {
   double ratio;
 };
 
-// the job whose [first, first + count) workgroup range holds b
+// the job whose [first, first + count) workgroup range holds b: a fully
+// unrolled count over the contiguous first-workgroup table (wide scalar loads
+// issued together, no dependent loop)
 __device__ __forceinline__ int batch_job(const FfBatch& B, uint32_t b, bool mm) {
-  int j = 0;
-  for (int i = 1; i < B.njobs; ++i)
-    if ((mm ? B.job[i].mm_wg0 : B.job[i].wg0) <= b) j = i;
-  return j;
+  const uint32_t* f = mm ? B.mm_first : B.first;
+  int j = -1;
+#pragma unroll
+  for (int i = 0; i < kBatchJobs; ++i) j += f[i] <= b ? 1 : 0;
+  return mm ? B.mm_job[j] : j;
 }
 
 __device__ __forceinline__ void tile_range_of(size_t ntiles, uint32_t wg, uint32_t nwg, size_t& t0,
@@ -1216,6 +1222,7 @@ int ff_encode_batch_launch(int value_type, int nb, const FfArray* arrs, int coun
   if (count > kBatchJobs) return kErrArg;
   if (value_type != kFloat && value_type != kDouble) return kErrArg;
   FfBatch B{};
+  for (int i = 0; i < kBatchJobs; ++i) B.first[i] = B.mm_first[i] = ~0u;
   B.njobs = count;
   B.partials = partials;
   B.pub = pub_base;
@@ -1231,6 +1238,7 @@ int ff_encode_batch_launch(int value_type, int nb, const FfArray* arrs, int coun
     B.k17.c[k] &= kMask17;
   }
   uint32_t mm = 0, enc = 0;
+  int kmm = 0;
   double bytes_mm = 0, bytes_enc = 0;
   const size_t vsz = value_type == kFloat ? 4 : 8;
   for (int i = 0; i < count; ++i) {
@@ -1249,8 +1257,14 @@ int ff_encode_batch_launch(int value_type, int nb, const FfArray* arrs, int coun
     J.ticket = a.ticket;
     J.mm_wg0 = mm;
     J.mm_nwg = (a.preset.has_min && a.preset.has_max) ? 0u : (uint32_t)tile_grid(a.n, kMinmaxGrid);
+    if (J.mm_nwg) {
+      B.mm_first[kmm] = mm;
+      B.mm_job[kmm] = i;
+      ++kmm;
+    }
     mm += J.mm_nwg;
     J.wg0 = enc;
+    B.first[i] = enc;
     J.nwg = (uint32_t)tile_grid(a.n, kStreamGrid);
     enc += J.nwg;
     if (J.mm_nwg) bytes_mm += (double)a.n * vsz;
@@ -1278,6 +1292,7 @@ int ff_decode_batch_launch(int value_type, int nb, const FfDecArray* arrs, int c
   if (count <= 0) return kOk;
   if (count > kBatchJobs) return kErrArg;
   FfBatch B{};
+  for (int i = 0; i < kBatchJobs; ++i) B.first[i] = B.mm_first[i] = ~0u;
   B.njobs = count;
   B.ratio = ff_ratio(nb);
   uint32_t wg = 0;
@@ -1291,6 +1306,7 @@ int ff_decode_batch_launch(int value_type, int nb, const FfDecArray* arrs, int c
     J.mn = arrs[i].mn;
     J.mx = arrs[i].mx;
     J.wg0 = wg;
+    B.first[i] = wg;
     J.nwg = (uint32_t)tile_grid(arrs[i].n, kStreamGrid);
     wg += J.nwg;
     bytes += (double)arrs[i].n * (vsz + nb);

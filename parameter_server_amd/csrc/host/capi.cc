@@ -479,6 +479,30 @@ int psf_msg_slice(psf_context* ctx, const psf_message* msg, const uint64_t* boun
   });
 }
 
+int psf_msgs_slice(psf_context* ctx, const psf_message* const* msgs, int nmsgs, const uint64_t* bounds,
+                   int nranges, int key_bytes, psf_message** outs, int* valid) {
+  return guarded([&] {
+    if (!ctx || nmsgs < 0 || nranges < 0 || (nmsgs && !msgs) || (nranges && (!bounds || !outs || !valid)))
+      return PSF_ERR_ARG;
+    std::vector<psf::KeyRange> krs(nranges);
+    for (int i = 0; i < nranges; ++i) krs[i] = psf::KeyRange{bounds[i], bounds[i + 1]};
+    std::vector<const psf::Message*> ms(nmsgs);
+    for (int m = 0; m < nmsgs; ++m) {
+      if (!msgs[m]) return PSF_ERR_ARG;
+      ms[m] = &msgs[m]->m;
+    }
+    std::vector<std::vector<psf::Message>> parts;
+    std::vector<std::vector<bool>> ok;
+    psf::slice_messages(ctx->impl, ms, krs, key_bytes, &parts, &ok);
+    for (int m = 0; m < nmsgs; ++m)
+      for (int i = 0; i < nranges; ++i) {
+        outs[(size_t)m * nranges + i] = new psf_message{parts[m][i]};
+        valid[(size_t)m * nranges + i] = ok[m][i] ? 1 : 0;
+      }
+    return PSF_OK;
+  });
+}
+
 int psf_node_roundtrip(psf_node* snd, psf_node* rcv, const psf_message* const* tmpls, int ntmpl,
                        int iters, psf_message** out) {
   return guarded([&] {

@@ -56,6 +56,29 @@ def slice_message(ctx, msg, ranges: Sequence, key_bytes: int = 8):
     return res
 
 
+def slice_messages(ctx, msgs, ranges: Sequence, key_bytes: int = 8):
+    """slice_message for many messages with one device synchronisation;
+    returns one list per message."""
+    from .filter import Message
+    n, M = len(ranges), len(msgs)
+    for i in range(1, n):
+        if ranges[i - 1][1] != ranges[i][0]:
+            raise ValueError("ranges must be contiguous (message.h:120)")
+    bounds = (C.c_uint64 * (n + 1))(*([r[0] for r in ranges[:1]] + [r[1] for r in ranges]))
+    outs = (C.c_void_p * (n * M))()
+    valid = (C.c_int * (n * M))()
+    hs = (C.c_void_p * M)(*[m.h.value for m in msgs])
+    check(lib().psf_msgs_slice(ctx.h, hs, M, bounds, n, key_bytes, outs, valid))
+    res = []
+    for j, msg in enumerate(msgs):
+        row = []
+        for i in range(n):
+            m = Message(_handle=C.c_void_p(outs[j * n + i]), _refs=msg._refs)
+            row.append(m if valid[j * n + i] else None)
+        res.append(row)
+    return res
+
+
 def parse_frames(frames: List[torch.Tensor]):
     """Split a flat list of received frames into messages: each is a Task frame
     followed by its key frame (when the Task has has_key) and one frame per
@@ -116,9 +139,10 @@ class PushRouter:
         from .filter import RemoteNode
         send = [[] for _ in range(self.world)]
         enc_nodes, enc_msgs, dest = [], [], []
-        for sid, tmpl in streams.items():
-            m = tmpl.clone()
-            for d, part in enumerate(slice_message(self.ctx, m, self.ranges)):
+        sids = list(streams)
+        clones = [streams[sid].clone() for sid in sids]
+        for sid, parts in zip(sids, slice_messages(self.ctx, clones, self.ranges)):
+            for d, part in enumerate(parts):
                 if part is None:
                     continue
                 enc_nodes.append(self._sender(sid, d))

@@ -121,3 +121,30 @@ def test_spill_exchange_gloo_world2():
     for p in procs:
         p.join(timeout=60)
     assert res == {0: True, 1: True}
+
+
+def test_slice_many_host_keys_matches_restatement():
+    """psf_msgs_slice (many messages, one synchronisation) == the restatement."""
+    from oracle import slicing
+    from parameter_server_amd import filter as F
+    from parameter_server_amd import shard
+    ctx = F.HostContext()
+    ranges = shard.server_ranges(4)
+    msgs, data = [], []
+    for j in range(5):
+        keys = _keys(1000 + 37 * j, 100 + j)
+        v = np.random.default_rng(j).standard_normal(keys.size * 2).astype(np.float32)
+        m = F.Message(request=True, push=True, key_range=shard.KEY_ALL)
+        m.set_key(torch.from_numpy(keys.view(np.int64).copy()))
+        m.add_value(torch.from_numpy(v))
+        msgs.append(m)
+        data.append((keys, v))
+    for parts, (keys, v) in zip(shard.slice_messages(ctx, msgs, ranges), data):
+        want = slicing.slice_kofv(keys, [v], shard.KEY_ALL, ranges)
+        for p, w in zip(parts, want):
+            assert (p is None) == (w is None)
+            if w is None:
+                continue
+            ptr, nb, loc = p.key_ptr()
+            got = np.ctypeslib.as_array((np.ctypeslib.ctypes.c_uint8 * nb).from_address(ptr)) if nb else np.zeros(0, np.uint8)
+            assert got.tobytes() == w[0].tobytes()
