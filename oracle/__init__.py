@@ -102,6 +102,8 @@ class Port:
                                        C.c_void_p, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float,
                                        C.POINTER(C.c_int64), C.POINTER(C.c_float), C.POINTER(C.c_float)]
         L.port_ftrl_update.restype = C.c_int
+        L.port_decode_quotient_mismatches.argtypes = [C.c_int]
+        L.port_decode_quotient_mismatches.restype = C.c_long
 
     def ff_encode(self, x: np.ndarray, nb: int, seed: int, mn=None, mx=None):
         """Returns (status, codes:uint8[n*nb], min, max)."""
@@ -135,6 +137,11 @@ class Port:
 
     def ratio(self, nb: int) -> float:
         return float(self.lib.port_ff_ratio(nb))
+
+    def decode_quotient_mismatches(self, nb: int) -> int:
+        """Codes of num_bytes nb where the device decode's fma-corrected
+        quotient differs from r / ratio (exhaustive over all 2^(8nb) codes)."""
+        return int(self.lib.port_decode_quotient_mismatches(nb))
 
     def add_noise(self, x: np.ndarray, mean: float, sd: float) -> np.ndarray:
         y = np.array(x, copy=True)

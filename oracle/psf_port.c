@@ -144,6 +144,23 @@ int port_ff_decode(const uint8_t* code, size_t code_bytes, int dtype, int nb,
   return PORT_OK;
 }
 
+/* Checker for the device decode's quotient (ff_codec.hip dequant_q): counts
+ * the codes r in [0, 2^(8nb)) where the fma-corrected reciprocal product
+ * q0 = r * RN(1/ratio); q = fma(fma(-q0, ratio, r), RN(1/ratio), q0)
+ * differs from the IEEE quotient r / ratio the reference computes
+ * (fixing_float.h:97).  Not a restatement of the reference. */
+long port_decode_quotient_mismatches(int nb) {
+  if (nb <= 0 || nb > 3) return -1;
+  const double ratio = port_ff_ratio(nb), inv = 1.0 / ratio;
+  long bad = 0;
+  for (uint32_t r = 0; r < (1u << (8 * nb)); ++r) {
+    const double a = (double)r, q0 = a * inv;
+    const double q = fma(fma(-q0, ratio, a), inv, q0);
+    bad += q != a / ratio;
+  }
+  return bad;
+}
+
 /* CRC-32C (Castagnoli, reflected polynomial 0x82F63B78, init/final ~0) --
  * the function util/crc32c.cc:292-335 computes (slicing-by-4 there, a plain
  * byte table here; the value is alignment- and slicing-independent). */

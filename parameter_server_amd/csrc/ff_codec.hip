@@ -646,18 +646,83 @@ __device__ __forceinline__ V dequant(uint64_t code, double ratio, double bin, do
   return (V)(r / ratio * bin + min_v);
 }
 
+// The same value with the quotient r / ratio formed from inv = RN(1/ratio):
+// q0 = RN(r * inv), e = r - q0 * ratio (exact, one fma), q = RN(q0 + e * inv).
+// Markstein's correction; checked exhaustively to equal the IEEE quotient for
+// every code of num_bytes 1..3 (tests/test_oracle.py::test_decode_quotient),
+// so the decoded values stay bit-identical at a third of the f64 work of the
+// division sequence, which bounded the nb=2/3 decode.
+template <typename V>
+__device__ __forceinline__ V dequant_q(uint64_t code, double ratio, double inv, double bin, double min_v) {
+  const double r = (double)code;
+  const double q0 = r * inv;
+  const double q = __builtin_fma(__builtin_fma(-q0, ratio, r), inv, q0);
+  return (V)(q * bin + min_v);
+}
+
+struct __attribute__((aligned(4))) CodeWords3 { uint32_t a, b, d; };  // one group of four nb=3 codes
+
+__device__ __forceinline__ void unpack_codes3(uint32_t a, uint32_t b, uint32_t d, uint64_t r[4]) {
+  r[0] = a & 0xFFFFFF;
+  r[1] = (a >> 24) | ((b & 0xFFFF) << 8);
+  r[2] = (b >> 16) | ((d & 0xFF) << 16);
+  r[3] = d >> 8;
+}
+
+
 template <int NB>
 __device__ __forceinline__ void load_codes(const uint8_t* __restrict__ code, size_t g, uint64_t r[4]) {
   if (NB == 2) {
     uint2 w = reinterpret_cast<const uint2*>(code)[g];
     r[0] = w.x & 0xFFFF; r[1] = w.x >> 16; r[2] = w.y & 0xFFFF; r[3] = w.y >> 16;
   } else {
-    const uint32_t* c = reinterpret_cast<const uint32_t*>(code) + 3 * g;
-    uint32_t a = c[0], b = c[1], d = c[2];
-    r[0] = a & 0xFFFFFF;
-    r[1] = (a >> 24) | ((b & 0xFFFF) << 8);
-    r[2] = (b >> 16) | ((d & 0xFF) << 16);
-    r[3] = d >> 8;
+    const CodeWords3 c = reinterpret_cast<const CodeWords3*>(code)[g];
+    unpack_codes3(c.a, c.b, c.d, r);
+  }
+}
+
+// One tile (kTileGroups groups of four values) of the decode.  All four code
+// loads are issued before any dequantise: lanes past the array's last group
+// load that group again (in bounds, branch-free) and skip the store, so the
+// loads of a partial tile are not serialised behind per-group branches.
+template <typename V, int NB>
+__device__ __forceinline__ void decode_tile(const uint8_t* __restrict__ code, V* __restrict__ out, size_t gb,
+                                            size_t ngroups, const V* lut, double ratio,
+                                            double bin, double min_v) {
+  const double inv = 1.0 / ratio;  // IEEE division: RN(1/ratio)
+  if (NB == 1) {
+    const uint32_t* c32 = reinterpret_cast<const uint32_t*>(code);
+    uint32_t w[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const size_t g = gb + u * kBlock;
+      w[u] = c32[g < ngroups ? g : ngroups - 1];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const size_t g = gb + u * kBlock;
+      if (g < ngroups) {
+        V v[4] = {lut[w[u] & 0xFF], lut[(w[u] >> 8) & 0xFF], lut[(w[u] >> 16) & 0xFF], lut[w[u] >> 24]};
+        Vec4<V>::store(out + 4 * g, v);
+      }
+    }
+  } else {
+    uint64_t r[4][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const size_t g = gb + u * kBlock;
+      load_codes<NB>(code, g < ngroups ? g : ngroups - 1, r[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const size_t g = gb + u * kBlock;
+      if (g < ngroups) {
+        V v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = dequant_q<V>(r[u][j], ratio, inv, bin, min_v);
+        Vec4<V>::store(out + 4 * g, v);
+      }
+    }
   }
 }
 
@@ -681,45 +746,8 @@ __global__ __launch_bounds__(kBlock) void ff_decode(const uint8_t* __restrict__ 
       lut[threadIdx.x] = dequant<V>((uint64_t)threadIdx.x, ratio, bin, min_v);
       __syncthreads();
     }
-    for (size_t t = t0; t < t1; ++t) {
-      const size_t gb = t * kTileGroups + threadIdx.x;
-      const bool full = (t + 1) * kTileGroups <= ngroups;
-      if (NB == 1) {
-        const uint32_t* c32 = reinterpret_cast<const uint32_t*>(code);
-        uint32_t w[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const size_t g = gb + u * kBlock;
-          w[u] = (full || g < ngroups) ? c32[g] : 0u;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const size_t g = gb + u * kBlock;
-          if (full || g < ngroups) {
-            V v[4] = {lut[w[u] & 0xFF], lut[(w[u] >> 8) & 0xFF], lut[(w[u] >> 16) & 0xFF],
-                      lut[w[u] >> 24]};
-            Vec4<V>::store(out + 4 * g, v);
-          }
-        }
-      } else {
-        uint64_t r[4][4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const size_t g = gb + u * kBlock;
-          if (full || g < ngroups) load_codes<NB>(code, g, r[u]);
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const size_t g = gb + u * kBlock;
-          if (full || g < ngroups) {
-            V v[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = dequant<V>(r[u][j], ratio, bin, min_v);
-            Vec4<V>::store(out + 4 * g, v);
-          }
-        }
-      }
-    }
+    for (size_t t = t0; t < t1; ++t)
+      decode_tile<V, NB>(code, out, t * kTileGroups + threadIdx.x, ngroups, lut, ratio, bin, min_v);
     if (blockIdx.x == 0) {
       for (size_t i = (ngroups << 2) + threadIdx.x; i < n; i += kBlock) {
         uint64_t r = 0;
@@ -946,29 +974,8 @@ __global__ __launch_bounds__(kBlock) void ff_decode_batch(FfBatch B) {
     lut[threadIdx.x] = dequant<V>((uint64_t)threadIdx.x, ratio, bin, min_v);
     __syncthreads();
   }
-  for (size_t t = t0; t < t1; ++t) {
-    const size_t gb = t * kTileGroups + threadIdx.x;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const size_t g = gb + u * kBlock;
-      if (g < ngroups) {
-        V v[4];
-        if (NB == 1) {
-          const uint32_t w = reinterpret_cast<const uint32_t*>(code)[g];
-          v[0] = lut[w & 0xFF];
-          v[1] = lut[(w >> 8) & 0xFF];
-          v[2] = lut[(w >> 16) & 0xFF];
-          v[3] = lut[w >> 24];
-        } else {
-          uint64_t r[4];
-          load_codes<NB>(code, g, r);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] = dequant<V>(r[j], ratio, bin, min_v);
-        }
-        Vec4<V>::store(out + 4 * g, v);
-      }
-    }
-  }
+  for (size_t t = t0; t < t1; ++t)
+    decode_tile<V, NB>(code, out, t * kTileGroups + threadIdx.x, ngroups, lut, ratio, bin, min_v);
   if (wg == 0) {
     for (size_t i = (ngroups << 2) + threadIdx.x; i < n; i += kBlock) {
       uint64_t r = 0;

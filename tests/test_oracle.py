@@ -241,3 +241,11 @@ def test_snappy_reference_random(port):
         else:
             b = np.repeat(rng.integers(0, 8, n // 5 + 1, dtype=np.uint8), 5).tobytes()[:n]
         assert port.snappy_compress(b) == R.snappy_compress(b), (t, n)
+
+
+@pytest.mark.parametrize("nb", [1, 2, 3])
+def test_decode_quotient(port, nb):
+    """The device decode forms r / ratio as fma(fma(-q0, ratio, r), inv, q0)
+    with q0 = r * inv, inv = RN(1/ratio) (ff_codec.hip dequant_q); it must
+    equal the IEEE quotient of fixing_float.h:97 for every possible code."""
+    assert port.decode_quotient_mismatches(nb) == 0
