@@ -27,7 +27,12 @@ typedef PubSlot Slot;
 
 class Context {
  public:
-  static constexpr int kSlots = 256;
+  static constexpr int kSlots = 512;
+  // slots [0, kSyncSlots) serve launches whose results the host waits for
+  // before returning; [kSyncSlots, kSlots) the KEY_CACHING signatures that a
+  // batched encode leaves in flight while later filters launch
+  static constexpr int kSyncSlots = 256;
+  static constexpr int kDeferSlot0 = kSyncSlots;
 
   // own_stream -> a private non-blocking stream owned by the context; else
   // `stream` as given (nullptr = the legacy default stream).

@@ -183,8 +183,8 @@ void FixingFloatFilter::encode_messages(Context* ctx, std::vector<FfMessage>& ms
   for (auto& m : msgs) collect_jobs(m.msg, &jobs);
   if (jobs.empty()) return;
   hipStream_t st = ctx->stream();
-  for (size_t base = 0; base < jobs.size(); base += Context::kSlots) {
-    const size_t end = std::min(jobs.size(), base + (size_t)Context::kSlots);
+  for (size_t base = 0; base < jobs.size(); base += Context::kSyncSlots) {
+    const size_t end = std::min(jobs.size(), base + (size_t)Context::kSyncSlots);
     std::vector<uint32_t> tickets(end - base, 0);
     std::vector<FixedPoint> presets(end - base);
     std::vector<uint32_t> seeds(end - base);
@@ -379,49 +379,105 @@ void RemoteNode::DecodeMessage(Message* msg) {  // remote_node.cc:23-29, reverse
 }
 
 // KEY_CACHING signatures (CRC32C of the first min(bytes, 2048) key bytes,
-// key_caching.h:18) of many messages: device keys in batched launches, one
-// wait per batch; host keys on the host.  sigs[i] for the listed messages.
-static void batch_signatures(RemoteNode* const* nodes, Message* const* msgs, const std::vector<int>& idx,
-                             std::vector<uint32_t>* sigs) {
-  sigs->assign(idx.size(), 0u);
+// key_caching.h:18) of many messages: device keys in batched launches whose
+// results land in publish slots, host keys on the host.  finish() waits and
+// fills sigs[k] for idx[k].  With `defer`, the batches use the context's
+// deferred slot range, so the caller can launch further work (FIXING_FLOAT of
+// the next chain position) before waiting; otherwise each batch is waited
+// for before the next reuses the slots.
+namespace {
+struct SigBatch {
+  struct Chunk {
+    Context* ctx;
+    int slot0;
+    std::vector<size_t> ks;
+    std::vector<uint32_t> tk;
+  };
+  std::vector<uint32_t> sigs;
+  std::vector<Chunk> chunks;
+  void finish_chunk(const Chunk& c) {
+    for (size_t q = 0; q < c.ks.size(); ++q) {
+      c.ctx->wait_ticket(c.slot0 + (int)q, c.tk[q]);
+      sigs[c.ks[q]] = c.ctx->pub_host(c.slot0 + (int)q)->crc;
+    }
+  }
+  void finish() {
+    for (const Chunk& c : chunks) finish_chunk(c);
+    chunks.clear();
+  }
+};
+}  // namespace
+
+static void launch_signatures(RemoteNode* const* nodes, Message* const* msgs, const std::vector<int>& idx,
+                              bool defer, SigBatch* sb) {
+  sb->sigs.assign(idx.size(), 0u);
+  sb->chunks.clear();
   std::map<Context*, std::vector<size_t>> dev;
   for (size_t k = 0; k < idx.size(); ++k) {
     const Buffer& key = msgs[idx[k]]->key;
     const size_t len = std::min(key.bytes, (size_t)2048);
-    if (key.loc == Loc::kHost || nodes[idx[k]]->ctx()->device() < 0) (*sigs)[k] = crc32c_host(key.ptr, len);
+    if (key.loc == Loc::kHost || nodes[idx[k]]->ctx()->device() < 0) sb->sigs[k] = crc32c_host(key.ptr, len);
     else dev[nodes[idx[k]]->ctx()].push_back(k);
   }
+  constexpr size_t kDeferCap = (size_t)(Context::kSlots - Context::kDeferSlot0);
   for (auto& kv : dev) {
     Context* ctx = kv.first;
     const std::vector<size_t>& ks = kv.second;
-    const size_t chunk = std::min((size_t)kCrcBatchMax, (size_t)Context::kSlots);
-    for (size_t b = 0; b < ks.size(); b += chunk) {
-      const size_t e = std::min(ks.size(), b + chunk);
+    const bool keep = defer && ks.size() <= kDeferCap;  // all of this context's batches in flight at once
+    for (size_t b = 0; b < ks.size(); b += (size_t)kCrcBatchMax) {
+      const size_t e = std::min(ks.size(), b + (size_t)kCrcBatchMax);
+      SigBatch::Chunk c{ctx, keep ? Context::kDeferSlot0 + (int)b : 0, {}, {}};
       std::vector<const void*> d;
-      std::vector<uint32_t> n, tk;
+      std::vector<uint32_t> n;
       std::vector<int> slot;
       for (size_t q = b; q < e; ++q) {
         const Buffer& key = msgs[idx[ks[q]]]->key;
         d.push_back(key.ptr);
         n.push_back((uint32_t)std::min(key.bytes, (size_t)2048));
         slot.push_back((int)(q - b));
-        tk.push_back(ctx->next_ticket());
+        c.ks.push_back(ks[q]);
+        c.tk.push_back(ctx->next_ticket());
       }
-      int s = crc32c_batch_launch(d.data(), n.data(), slot.data(), tk.data(), (int)d.size(), ctx->pub_dev(0),
-                                  ctx->stream(), ctx->prof());
+      int s = crc32c_batch_launch(d.data(), n.data(), slot.data(), c.tk.data(), (int)d.size(),
+                                  ctx->pub_dev(c.slot0), ctx->stream(), ctx->prof());
       if (s != kOk) throw CheckError(s, "crc32c batch launch failed");
-      for (size_t q = b; q < e; ++q) {
-        ctx->wait_ticket((int)(q - b), tk[q - b]);
-        (*sigs)[ks[q]] = ctx->pub_host((int)(q - b))->crc;
-      }
+      if (keep) sb->chunks.push_back(std::move(c));
+      else sb->finish_chunk(c);
     }
   }
 }
 
+// Encode in filter order, position by position over all chains.  The
+// KEY_CACHING signatures of a position stay in flight while a following
+// all-FIXING_FLOAT position launches (the two touch disjoint parts of a
+// message: keys vs values); the cache logic then runs in message order, so
+// the result equals sequential EncodeMessage calls.
 void encode_batch(RemoteNode* const* nodes, Message* const* msgs, int n) {
   size_t maxlen = 0;
   for (int i = 0; i < n; ++i) maxlen = std::max(maxlen, msgs[i]->task.filter.size());
+  struct PendingKc {
+    bool active = false;
+    size_t pos = 0;
+    std::vector<int> kc, kc_sig;
+    SigBatch sb;
+  } pend;
+  auto finish_kc = [&] {
+    if (!pend.active) return;
+    pend.active = false;
+    pend.sb.finish();
+    size_t k = 0;
+    for (int i : pend.kc) {
+      const uint32_t sig = (k < pend.kc_sig.size() && pend.kc_sig[k] == i) ? pend.sb.sigs[k++] : 0u;
+      static_cast<KeyCachingFilter*>(nodes[i]->FindFilterOrCreate(msgs[i]->task.filter[pend.pos]))
+          ->encode_with(msgs[i], sig);
+    }
+  };
   for (size_t pos = 0; pos < maxlen; ++pos) {  // filter position pos of every chain
+    bool only_ff = true;
+    for (int i = 0; i < n && only_ff; ++i)
+      if (pos < msgs[i]->task.filter.size() && msgs[i]->task.filter[pos].type != FilterConfig::FIXING_FLOAT)
+        only_ff = false;
+    if (!only_ff) finish_kc();
     std::map<Context*, std::vector<FfMessage>> ff;
     std::vector<int> kc, kc_sig;
     for (int i = 0; i < n; ++i) {
@@ -437,18 +493,16 @@ void encode_batch(RemoteNode* const* nodes, Message* const* msgs, int n) {
         f->encode(msgs[i]);
       }
     }
-    if (!kc.empty()) {  // signatures batched, then the caches in message order
-      std::vector<uint32_t> sigs;
-      batch_signatures(nodes, msgs, kc_sig, &sigs);
-      size_t k = 0;
-      for (int i : kc) {
-        const uint32_t sig = (k < kc_sig.size() && kc_sig[k] == i) ? sigs[k++] : 0u;
-        static_cast<KeyCachingFilter*>(nodes[i]->FindFilterOrCreate(msgs[i]->task.filter[pos]))
-            ->encode_with(msgs[i], sig);
-      }
+    if (!kc.empty()) {  // signatures launched now, the caches after the next position's launches
+      pend.pos = pos;
+      pend.kc = std::move(kc);
+      pend.kc_sig = std::move(kc_sig);
+      launch_signatures(nodes, msgs, pend.kc_sig, true, &pend.sb);
+      pend.active = true;
     }
     for (auto& kv : ff) FixingFloatFilter::encode_messages(kv.first, kv.second);
   }
+  finish_kc();
 }
 
 void decode_batch(RemoteNode* const* nodes, Message* const* msgs, int n) {
@@ -472,12 +526,12 @@ void decode_batch(RemoteNode* const* nodes, Message* const* msgs, int n) {
       }
     }
     if (!kc.empty()) {
-      std::vector<uint32_t> sigs;
-      batch_signatures(nodes, msgs, kc_sig, &sigs);
+      SigBatch sb;
+      launch_signatures(nodes, msgs, kc_sig, false, &sb);
       size_t k = 0;
       for (int i : kc) {
         const size_t len = msgs[i]->task.filter.size();
-        const uint32_t sig = (k < kc_sig.size() && kc_sig[k] == i) ? sigs[k++] : 0u;
+        const uint32_t sig = (k < kc_sig.size() && kc_sig[k] == i) ? sb.sigs[k++] : 0u;
         static_cast<KeyCachingFilter*>(nodes[i]->FindFilterOrCreate(msgs[i]->task.filter[len - 1 - r]))
             ->decode_with(msgs[i], sig);
       }

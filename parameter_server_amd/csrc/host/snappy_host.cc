@@ -42,7 +42,7 @@ void SnappyBatch::compress(const Buffer& src, Buffer* dst) {
     return;
   }
   if (src.bytes > 0xffffffffull) throw CheckError(kErrArg, "snappy: input longer than 4 GiB");
-  if (jobs_.size() == (size_t)Context::kSlots) flush();
+  if (jobs_.size() == (size_t)Context::kSyncSlots) flush();
   Job j;
   j.in = c_.to_device(src);
   j.dst = dst;
@@ -64,7 +64,7 @@ void SnappyBatch::uncompress(const Buffer& src, Buffer* dst) {
   uint64_t dsize = 0;
   const uint32_t hdr = snappy_read_header(c_, src, &dsize);
   if (!hdr) throw CheckError(kErrCheck, "CHECK(snappy::GetUncompressedLength(src, src_size, &dsize))");
-  if (jobs_.size() == (size_t)Context::kSlots) flush();
+  if (jobs_.size() == (size_t)Context::kSyncSlots) flush();
   Job j;
   j.in = c_.to_device(src);
   j.dst = dst;

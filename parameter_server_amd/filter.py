@@ -475,9 +475,9 @@ class RemoteNode:
     @staticmethod
     def roundtrip_many(snd, rcv, tmpls, iters: int) -> None:
         n = len(tmpls)
-        for nd in list(snd) + list(rcv):
-            for t in tmpls:
-                nd._hold(t)
+        for a, b, t in zip(snd, rcv, tmpls):  # node i only ever sees tmpls[i]
+            a._hold(t)
+            b._hold(t)
         check(lib().psf_nodes_roundtrip((C.c_void_p * n)(*[nd.h.value for nd in snd]),
                                         (C.c_void_p * n)(*[nd.h.value for nd in rcv]),
                                         (C.c_void_p * n)(*[t.h.value for t in tmpls]), n, iters))
