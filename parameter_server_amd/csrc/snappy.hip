@@ -491,45 +491,88 @@ __device__ __forceinline__ uint64_t tag_bytes(const uint8_t* in, uint64_t C, uin
 
 // K0: link the chain directly when the stream is mostly 64 KiB fragments
 // stored as single literals (what a snappy 1.1.8 encoder emits for
-// incompressible fragments, e.g. FIXING_FLOAT codes): lane k decodes the tag
-// at p + k * kFullLit, and the run of lanes that find a full literal there is
-// consumed in one step (64 fragments per memory latency); other tags take a
-// single step.  After kLitBudget single steps the stream is handed to the
-// window scan (K1) and its linker (K2) through kFlagScan.
+// incompressible fragments, e.g. FIXING_FLOAT codes): lane k decodes the tags
+// at p + (k + 64 j) * kFullLit for j < kLitRows, and the leading run of
+// positions that hold a full literal is consumed in one step (512 fragments
+// per memory latency); other tags take a single step.  After kLitBudget
+// single steps the stream is handed to the window scan (K1) and its linker
+// (K2) through kFlagScan.  While every tag so far is a literal starting on a
+// 64 KiB output boundary and ending on the next one (or at the end of the
+// output), K0 also records each output fragment's first tag; if that holds to
+// the end, flags[1] = 1 tells K3 the stream is indexed and has no copies to
+// validate.
+constexpr int kLitRows = 8;
 __global__ __launch_bounds__(64) void snappy_dlit(const uint8_t* __restrict__ in, uint64_t C, uint32_t hdr,
                                                   uint64_t dsize, uint32_t nwin, uint64_t* __restrict__ wentry,
-                                                  uint64_t* __restrict__ woff, uint32_t* __restrict__ flags) {
+                                                  uint64_t* __restrict__ woff, uint64_t* __restrict__ fragpos,
+                                                  uint32_t* __restrict__ flags) {
   const uint32_t lane = threadIdx.x;
   for (uint32_t i = lane; i < nwin; i += 64) wentry[i] = kNone;
+  if (lane == 0) flags[1] = 0;
   __syncthreads();
   uint64_t p = hdr, o = 0;
   int64_t last_w = -1;
   uint32_t singles = 0;
-  bool bad = false;
+  bool bad = false, pure = true, wide = true;
   while (p < C) {
-    const uint64_t pk = p + (uint64_t)lane * kFullLit;
-    const Tag t = decode_tag(tag_bytes(in, C, pk), pk);
-    const bool full = pk < C && t.lit && t.len == 65536 && t.hl == 3;
-    const uint64_t m = __ballot(full);
-    const uint32_t c = m == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~m);  // leading run of full literals
+    bool full[kLitRows];
+    uint64_t pk[kLitRows];
+    Tag t0;
+#pragma unroll
+    for (int j = 0; j < kLitRows; ++j) {
+      pk[j] = p + (uint64_t)(lane + 64 * j) * kFullLit;
+      full[j] = false;
+      if (j == 0 || wide) {  // after a single step, probe one row only
+        const Tag t = decode_tag(tag_bytes(in, C, pk[j]), pk[j]);
+        full[j] = pk[j] < C && t.lit && t.len == 65536 && t.hl == 3;
+        if (j == 0) t0 = t;
+      }
+    }
+    uint32_t c = 0;  // leading run of full literals over rows 0, 1, ...
+    bool open = true;
+#pragma unroll
+    for (int j = 0; j < kLitRows; ++j) {
+      const uint64_t m = __ballot(full[j]);
+      if (open) {
+        const uint32_t r = m == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~m);
+        c += r;
+        open = r == 64;
+      }
+    }
     if (c > 0) {
-      if (lane < c) {
-        const int64_t wk = (int64_t)((pk - hdr) / kWin);
-        if (wk > last_w) {
-          wentry[wk] = pk;
-          woff[wk] = o + (uint64_t)lane * 65536;
+      const bool aligned = (o & (kFrag - 1)) == 0;
+      pure = pure && aligned;
+#pragma unroll
+      for (int j = 0; j < kLitRows; ++j) {
+        const uint32_t idx = lane + 64 * j;
+        if (idx < c) {
+          const int64_t wk = (int64_t)((pk[j] - hdr) / kWin);
+          if (idx > 0 || wk > last_w) {  // full literals are > kWin apart: one per window
+            wentry[wk] = pk[j];
+            woff[wk] = o + (uint64_t)idx * 65536;
+          }
+          if (aligned) fragpos[o / kFrag + idx] = pk[j];
         }
       }
       last_w = (int64_t)((p + (uint64_t)(c - 1) * kFullLit - hdr) / kWin);
       p += (uint64_t)c * kFullLit;
       o += (uint64_t)c * 65536;
+      wide = true;
     } else {
-      const uint64_t t0next = __shfl(t.next, 0, 64), t0len = __shfl(t.len, 0, 64);
+      wide = false;
+      const uint64_t t0next = __shfl(t0.next, 0, 64), t0len = __shfl(t0.len, 0, 64);
+      const bool t0lit = __shfl((int)t0.lit, 0, 64) != 0;
       const int64_t w0 = (int64_t)((p - hdr) / kWin);
-      if (lane == 0 && w0 > last_w) {
-        wentry[w0] = p;
-        woff[w0] = o;
+      // still indexed: a literal from a fragment boundary to the next one or to the end
+      const bool keep = t0lit && (o & (kFrag - 1)) == 0 && t0len <= kFrag && (t0len == kFrag || o + t0len == dsize);
+      if (lane == 0) {
+        if (w0 > last_w) {
+          wentry[w0] = p;
+          woff[w0] = o;
+        }
+        if (pure && keep) fragpos[o / kFrag] = p;
       }
+      pure = pure && keep;
       if (w0 > last_w) last_w = w0;
       p = t0next;
       o += t0len;
@@ -543,7 +586,11 @@ __global__ __launch_bounds__(64) void snappy_dlit(const uint8_t* __restrict__ in
       break;
     }
   }
-  if (lane == 0) *flags = (bad || p != C || o != dsize) ? kFlagInvalid : 0u;
+  const bool ok = !(bad || p != C || o != dsize);
+  if (lane == 0) {
+    *flags = ok ? 0u : kFlagInvalid;
+    flags[1] = ok && pure ? 1u : 0u;
+  }
 }
 
 constexpr uint32_t kStarts = 64;  // K1 parses from each of the first 64 offsets of a window
@@ -662,10 +709,24 @@ __global__ __launch_bounds__(64) void snappy_dindex(const uint8_t* __restrict__ 
                                                     uint64_t* __restrict__ fragpos, uint32_t* __restrict__ flags) {
   __shared__ uint32_t b32[(kWin + 32) / 4];
   const uint32_t lane = threadIdx.x, w = blockIdx.x;
+  if (flags[1]) return;  // K0 indexed a stream of whole-fragment literals
   const uint64_t e = wentry[w];
   if (e == kNone || (*flags & kFlagInvalid)) return;
   const uint64_t base = hdr + (uint64_t)w * kWin;
   const uint32_t wl = (uint32_t)min((uint64_t)kWin, C - base);
+  {  // the entry tag is a literal that leaves the window (a stored fragment): no staging
+    const uint64_t o = woff[w];
+    const Tag t = decode_tag(tag_bytes(in, C, e), e);
+    if (t.lit && t.next >= base + wl) {
+      if (lane == 0) {
+        uint32_t fl = 0;
+        if ((o & (kFrag - 1)) == 0) fragpos[o / kFrag] = e;
+        if (o / kFrag != (o + t.len - 1) / kFrag) fl |= kFlagSerial;
+        if (fl) atomicOr(flags, fl);
+      }
+      return;
+    }
+  }
   const uint32_t s = stage(b32, in, C, base, wl + 16, lane);
   __syncthreads();
   if (lane != 0) return;
@@ -694,7 +755,6 @@ __global__ __launch_bounds__(64) void snappy_dfrag(const uint8_t* __restrict__ i
   __shared__ uint32_t ib32[(kInWin + 32) / 4];
   if (*flags) return;
   uint8_t* ob = reinterpret_cast<uint8_t*>(ob32);
-  const uint8_t* ibb = reinterpret_cast<const uint8_t*>(ib32);
   const uint32_t lane = threadIdx.x, k = blockIdx.x;
   const uint64_t o0 = (uint64_t)k * kFrag;
   const uint32_t end = (uint32_t)min((uint64_t)kFrag, dsize - o0);
@@ -721,7 +781,7 @@ __global__ __launch_bounds__(64) void snappy_dfrag(const uint8_t* __restrict__ i
         s = stage(ib32, in, C, wb, kSpan, lane);
       }
       if (src + L <= wb + kSpan) {
-        const uint8_t* q = ibb + s + (src - wb);
+        const uint8_t* q = reinterpret_cast<const uint8_t*>(ib32) + s + (src - wb);
         for (uint32_t i = lane; i < L; i += 64) ob[o + i] = q[i];
       } else {
         for (uint32_t i = lane; i < L; i += 64) ob[o + i] = in[src + i];
@@ -863,7 +923,7 @@ int snappy_uncompress_launch(const void* in, size_t C, uint32_t hdr, size_t dsiz
   uint8_t* dst = static_cast<uint8_t*>(out);
   ProfScope ps(prof, kKSnappyDecompress, st, (double)C + (double)dsize);
   hipLaunchKernelGGL(snappy_dlit, dim3(1), dim3(64), 0, st, src, (uint64_t)C, hdr, (uint64_t)dsize, nwin, wentry,
-                     woff, flags);
+                     woff, fragpos, flags);
   if (nwin) {
     hipLaunchKernelGGL(snappy_dscan, dim3(nwin), dim3(64), 0, st, src, (uint64_t)C, hdr, bitmap, cum, wexit,
                        wtotal, flags);
