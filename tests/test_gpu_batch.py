@@ -147,3 +147,39 @@ def test_batch_key_caching_order(ctx, port):
         F.RemoteNode.decode_many([rcv] * 3, ws)
         for w in ws:
             assert rcv.key(w).cpu().numpy().view(np.uint64).tobytes() == keys.tobytes()
+
+
+def test_batch_many_messages_slot_chunks(ctx, port):
+    """300 messages [KEY_CACHING, FIXING_FLOAT] in one batch: more signatures
+    than the deferred publish-slot range holds (the signatures are then waited
+    for batch by batch) and more FIXING_FLOAT arrays than one slot chunk;
+    results equal one-at-a-time encodes and the C restatement, and a second
+    batch hits the key cache for every message."""
+    from parameter_server_amd import filter as F
+    F.set_clock(4242)
+    try:
+        rng = np.random.default_rng(11)
+        cases = []
+        for k in range(300):
+            n = 50 + 37 * (k % 13)
+            keys = np.unique(rng.integers(0, 10**9, n + 8).astype(np.uint64))[:n]
+            cases.append((rng.standard_normal(keys.size).astype(np.float32), keys))
+        snd_b = [F.RemoteNode(ctx) for _ in cases]
+        snd_s = [F.RemoteNode(ctx) for _ in cases]
+        for rnd in range(2):
+            mb = [_message(F, x, 1, None, keys, ch=i) for i, (x, keys) in enumerate(cases)]
+            ms = [_message(F, x, 1, None, keys, ch=i) for i, (x, keys) in enumerate(cases)]
+            F.RemoteNode.encode_many(snd_b, mb)
+            for nd, m in zip(snd_s, ms):
+                nd.encode(m)
+            ctx.sync()
+            for i, (x, keys) in enumerate(cases):
+                assert mb[i].key_info()[0] == ms[i].key_info()[0] == (rnd == 0), (rnd, i)
+                assert mb[i].fixed_points(1) == ms[i].fixed_points(1), i
+                vb = snd_b[i].value(mb[i], 0).cpu().numpy().tobytes()
+                assert vb == snd_s[i].value(ms[i], 0).cpu().numpy().tobytes(), i
+                if rnd == 0 and i % 37 == 0:
+                    st, codes, _, _ = port.ff_encode(x, 1, 4242)
+                    assert vb == codes.tobytes(), i
+    finally:
+        F.set_clock(None)
