@@ -80,6 +80,9 @@ typedef struct psf_context psf_context;
  * host-only context (host-resident buffers; codecs needing HBM fail). */
 int psf_context_create(int device, void* stream, int own_stream, psf_context** out);
 int psf_context_destroy(psf_context* ctx);
+/* Waits for the context's stream; also resolves the min/max a batched encode
+ * left on the device (psf_nodes_encode) and returns PSF_ERR_BIN if any of
+ * them failed CHECK_GT(bin, 0) (fixing_float.h:71) since the last check. */
 int psf_context_sync(psf_context* ctx);
 /* Ordered on the context's stream, then synchronous: copy `bytes` from a
  * buffer the library returned (device or host) into host memory. */
@@ -292,7 +295,12 @@ int psf_kvmap_stats(psf_kvmap* map, int64_t* nnz, double* weight_sum, double* de
  * node's filter instances (stateful filters see their messages in array
  * order), with FIXING_FLOAT's element work batched into one launch per kernel
  * for up to 32 arrays (the async-SGD minibatch messages and the per-server
- * slices of SURVEY.md §8(d) C1/C4 are latency-bound one at a time). */
+ * slices of SURVEY.md §8(d) C1/C4 are latency-bound one at a time).
+ * Computed FIXING_FLOAT min/max are not waited for: a decode of the message
+ * on the same context reads them on the device, and any host reader
+ * (psf_fc_fixed_point, psf_task_serialize, a decode elsewhere) resolves them
+ * first -- CHECK_GT(bin, 0) is reported there, by psf_context_sync, or at the
+ * end of psf_nodes_roundtrip, instead of at encode time. */
 int psf_nodes_encode(psf_node* const* nodes, psf_message* const* msgs, int n);
 int psf_nodes_decode(psf_node* const* nodes, psf_message* const* msgs, int n);
 /* psf_node_roundtrip for n streams at once: for i in [0, iters), encode fresh

@@ -271,6 +271,7 @@ struct EncodeParams {
   double ratio;
   float* range_out;         // side-info float[2] (device), may be null
   int* status_out;          // CHECK_GT(bin,0) outcome (device), may be null
+  float* range_host;        // {min, max, status} into host-mapped memory, may be null
   PubSlot* pub;             // host-mapped publish slot, may be null
   uint32_t ticket;
 };
@@ -572,6 +573,11 @@ __global__ __launch_bounds__(kBlock) void ff_encode(const V* __restrict__ x, siz
     const int status = (q.bin > 0) ? kOk : kErrBin;
     if (p.range_out) { p.range_out[0] = mn_f; p.range_out[1] = mx_f; }
     if (p.status_out) *p.status_out = status;
+    if (p.range_host) {  // read by the host after a stream sync
+      p.range_host[0] = mn_f;
+      p.range_host[1] = mx_f;
+      reinterpret_cast<int32_t*>(p.range_host)[2] = status;
+    }
     if (p.pub) {  // side-info to the host while the grid keeps streaming
       p.pub->range[0] = mn_f;
       p.pub->range[1] = mx_f;
@@ -787,6 +793,8 @@ struct FfJob {
   uint32_t wg0, nwg;         // encode / decode workgroups
   int32_t slot;              // publish slot (encode), -1: none
   uint32_t ticket;
+  float* range;              // encode: device {min, max, status} out; decode: device {min, max} in; or null
+  float* range_host;         // encode: {min, max, status} into host-mapped memory, or null
 };
 constexpr int kBatchJobs = 32;
 struct FfBatch {
@@ -803,6 +811,8 @@ struct FfBatch {
   uint32_t a_lane, c_lane;
   double ratio;
 };
+static_assert(sizeof(FfBatch) <= 4096, "FfBatch must fit the 4 KiB kernel-argument segment");
+
 
 // the job whose [first, first + count) workgroup range holds b: a fully
 // unrolled count over the contiguous first-workgroup table (wide scalar loads
@@ -900,12 +910,25 @@ __global__ __launch_bounds__(kBlock) void ff_encode_batch(FfBatch B) {
   q.max_f = mx_f;
   q.scale_f = (float)q.scale;
   q.fast = q.bin < __builtin_huge_val();
-  if (wg == 0 && threadIdx.x == 0 && J.slot >= 0) {
-    PubSlot* ps = B.pub + J.slot;
-    ps->range[0] = mn_f;
-    ps->range[1] = mx_f;
-    ps->status = (q.bin > 0) ? kOk : kErrBin;
-    publish_ticket(ps, J.ticket);
+  if (wg == 0 && threadIdx.x == 0) {
+    const int status = (q.bin > 0) ? kOk : kErrBin;
+    if (J.range) {  // read by a later decode on this stream
+      J.range[0] = mn_f;
+      J.range[1] = mx_f;
+      reinterpret_cast<int32_t*>(J.range)[2] = status;
+    }
+    if (J.range_host) {  // read by the host after a stream sync
+      J.range_host[0] = mn_f;
+      J.range_host[1] = mx_f;
+      reinterpret_cast<int32_t*>(J.range_host)[2] = status;
+    }
+    if (J.slot >= 0) {
+      PubSlot* ps = B.pub + J.slot;
+      ps->range[0] = mn_f;
+      ps->range[1] = mx_f;
+      ps->status = status;
+      publish_ticket(ps, J.ticket);
+    }
   }
   if (!(q.bin > 0)) return;  // CHECK_GT(bin, 0), fixing_float.h:71
 
@@ -962,7 +985,9 @@ __global__ __launch_bounds__(kBlock) void ff_decode_batch(FfBatch B) {
   V* __restrict__ out = static_cast<V*>(J.out);
   const size_t n = J.n;
   const uint32_t wg = blockIdx.x - J.wg0;
-  const double min_v = (double)J.mn, max_v = (double)J.mx;
+  float mn_f = J.mn, mx_f = J.mx;
+  if (J.range) { mn_f = J.range[0]; mx_f = J.range[1]; }
+  const double min_v = (double)mn_f, max_v = (double)mx_f;
   const double bin = max_v - min_v;
   const double ratio = B.ratio;
   const size_t ngroups = n >> 2;
@@ -1101,8 +1126,9 @@ static int dispatch_encode_nb(const V* x, size_t n, int nb, uint8_t* out, Encode
 template <typename V>
 static int encode_typed(const V* x, size_t n, int nb, const FixedPoint& preset, uint32_t seed,
                         uint8_t* out, void* partials, float* range_out, int* status_out,
-                        hipStream_t st, Profiler* prof, PubSlot* pub, uint32_t ticket) {
+                        hipStream_t st, Profiler* prof, PubSlot* pub, uint32_t ticket, float* range_host) {
   EncodeParams p{};
+  p.range_host = range_host;
   p.pub = pub;
   p.ticket = ticket;
   p.has_min = preset.has_min;
@@ -1135,17 +1161,17 @@ static int encode_typed(const V* x, size_t n, int nb, const FixedPoint& preset, 
 
 int ff_encode_launch(const void* x, size_t n, int value_type, int nb, const FixedPoint& preset,
                      uint32_t seed, void* out, void* partials, float* range_out, int* status_out,
-                     hipStream_t st, Profiler* prof, PubSlot* pub, uint32_t ticket) {
+                     hipStream_t st, Profiler* prof, PubSlot* pub, uint32_t ticket, float* range_host) {
   if (nb <= 0 || nb >= 8) return kErrNbytes;
   if (n == 0) return kOk;
   if (value_type == kFloat)
     return encode_typed<float>(static_cast<const float*>(x), n, nb, preset, seed,
                                static_cast<uint8_t*>(out), partials, range_out, status_out, st, prof,
-                               pub, ticket);
+                               pub, ticket, range_host);
   if (value_type == kDouble)
     return encode_typed<double>(static_cast<const double*>(x), n, nb, preset, seed,
                                 static_cast<uint8_t*>(out), partials, range_out, status_out, st, prof,
-                                pub, ticket);
+                                pub, ticket, range_host);
   return kErrArg;
 }
 
@@ -1262,6 +1288,8 @@ int ff_encode_batch_launch(int value_type, int nb, const FfArray* arrs, int coun
     J.lcg_pos = lcg_cycle().pos[a.seed & kMask17];
     J.slot = a.slot;
     J.ticket = a.ticket;
+    J.range = a.range;
+    J.range_host = a.range_host;
     J.mm_wg0 = mm;
     J.mm_nwg = (a.preset.has_min && a.preset.has_max) ? 0u : (uint32_t)tile_grid(a.n, kMinmaxGrid);
     if (J.mm_nwg) {
@@ -1312,6 +1340,7 @@ int ff_decode_batch_launch(int value_type, int nb, const FfDecArray* arrs, int c
     J.n = arrs[i].n;
     J.mn = arrs[i].mn;
     J.mx = arrs[i].mx;
+    J.range = const_cast<float*>(arrs[i].range);
     J.wg0 = wg;
     B.first[i] = wg;
     J.nwg = (uint32_t)tile_grid(arrs[i].n, kStreamGrid);

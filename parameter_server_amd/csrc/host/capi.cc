@@ -1,3 +1,4 @@
+#include <set>
 // extern "C" boundary of libpsf (include/psf.h).
 #include "../../../include/psf.h"
 
@@ -68,7 +69,7 @@ int psf_context_destroy(psf_context* ctx) {
   return PSF_OK;
 }
 int psf_context_sync(psf_context* ctx) {
-  return guarded([&] { ctx->impl->sync(); return PSF_OK; });
+  return guarded([&] { ctx->impl->sync_checked(); return PSF_OK; });
 }
 int psf_copy_to_host(psf_context* ctx, void* dst, const void* src, size_t bytes) {
   return guarded([&] {
@@ -433,7 +434,8 @@ int psf_fc_fixed_point(const psf_message* msg, int idx, int k, psf_fixed_point* 
   return guarded([&] {
     const auto* f = fc_at(msg, idx);
     if (!fp || k < 0 || k >= (int)f->fixed_point.size()) return PSF_ERR_ARG;
-    const auto& x = f->fixed_point[k];
+    auto& x = const_cast<psf::FixedFloatConfig&>(f->fixed_point[k]);
+    x.settle();  // computed min/max a batched encode left on the device
     fp->has_min = x.has_min;
     fp->has_max = x.has_max;
     fp->min_value = x.min_value;
@@ -571,6 +573,9 @@ int psf_nodes_roundtrip(psf_node* const* snd, psf_node* const* rcv, const psf_me
       }
       psf::decode_batch(r.data(), wp.data(), n);
     }
+    std::set<psf::Context*> ctxs;  // CHECK_GT(bin, 0) of the lazily encoded ranges
+    for (int i = 0; i < n; ++i) ctxs.insert(s[i]->ctx());
+    for (psf::Context* c : ctxs) c->check_ranges();
     return PSF_OK;
   });
 }

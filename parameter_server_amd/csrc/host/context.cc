@@ -74,12 +74,26 @@ Context::Context(int device, hipStream_t stream, bool own) : device_(device), st
                               hipHostMallocMapped | hipHostMallocCoherent));
   memset(h_slots_, 0, sizeof(Slot) * kSlots);
   PSF_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&m_slots_), h_slots_, 0));
+  PSF_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&lazy_h_), 16 * kLazyRing,
+                              hipHostMallocMapped | hipHostMallocCoherent));
+  memset(lazy_h_, 0, 16 * kLazyRing);
+  PSF_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&lazy_m_), lazy_h_, 0));
 }
 
 Context::~Context() {
   if (device_ < 0) return;
   (void)hipSetDevice(device_);
   (void)hipStreamSynchronize(stream_);
+  for (auto& u : ring_uses_) {  // messages may outlive the context: leave their ranges on the host
+    auto rb = u.rb.lock();
+    if (rb && !rb->done) {
+      memcpy(rb->host.data(), rb->ring, rb->host.size() * 4);
+      rb->done = true;
+    }
+  }
+  ring_uses_.clear();
+  tracked_.clear();
+  (void)hipHostFree(lazy_h_);
   (void)hipFree(d_partials_);
   (void)hipFree(d_slots_);
   (void)hipHostFree(h_slots_);
@@ -119,6 +133,53 @@ void Context::wait_ticket(int i, uint32_t ticket) {
 
 void Context::sync() {
   if (device_ >= 0) PSF_HIP_CHECK(hipStreamSynchronize(stream_));
+}
+
+void RangeBatch::resolve(bool synced) {
+  if (done) return;
+  if (!synced) ctx->sync();  // the kernels' host-mapped stores are visible after it
+  memcpy(host.data(), ring, host.size() * 4);
+  done = true;
+}
+
+float* Context::claim_lazy(const std::shared_ptr<RangeBatch>& rb, int n) {
+  if (n <= 0 || (uint64_t)n > kLazyRing) throw CheckError(kErrArg, "lazy side-info batch too large");
+  uint64_t start = lazy_next_;
+  const uint64_t pos = start % kLazyRing;
+  if (pos + (uint64_t)n > kLazyRing) start += kLazyRing - pos;  // records stay contiguous
+  // this claim overwrites the records of absolute indices [start - R, start + n - R)
+  bool synced = false;
+  while (!ring_uses_.empty() && ring_uses_.front().start + kLazyRing < start + (uint64_t)n) {
+    auto old = ring_uses_.front().rb.lock();
+    ring_uses_.pop_front();
+    if (old && !old->done) {
+      if (!synced) sync();
+      synced = true;
+      old->resolve(true);
+    }
+  }
+  lazy_next_ = start + (uint64_t)n;
+  ring_uses_.push_back(RingUse{rb, start, (uint64_t)n});
+  const uint64_t at = start % kLazyRing;
+  rb->ring = lazy_h_ + 4 * at;
+  return reinterpret_cast<float*>(lazy_m_ + 4 * at);
+}
+
+void Context::track(std::shared_ptr<RangeBatch> rb) {
+  tracked_.push_back(std::move(rb));
+  if (tracked_.size() >= kMaxTracked) check_ranges();
+}
+
+void Context::check_ranges() {
+  std::vector<std::shared_ptr<RangeBatch>> t;
+  t.swap(tracked_);
+  bool bad = false;
+  if (!t.empty()) sync();
+  for (auto& rb : t) {
+    rb->resolve(true);
+    for (size_t i = 2; i < rb->host.size(); i += 4) bad |= (int32_t)rb->host[i] != kOk;
+  }
+  if (bad) throw CheckError(kErrBin, "CHECK_GT(bin, 0)");
 }
 
 Buffer Context::to_device(const Buffer& b) {

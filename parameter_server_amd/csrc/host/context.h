@@ -6,7 +6,9 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <deque>
 #include <memory>
+#include <vector>
 #include <mutex>
 #include <string>
 
@@ -24,6 +26,19 @@ namespace psf {
   } while (0)
 
 typedef PubSlot Slot;
+
+class Context;
+// FIXING_FLOAT side-info of one lazy encode batch: the kernels write
+// {min, max, status, 0} (16 bytes) per array into `dev`; resolve() brings
+// them to the host with one stream sync when a host reader needs them.
+struct RangeBatch {
+  Context* ctx = nullptr;
+  Buffer dev;                      // read by decodes on ctx's stream
+  const uint32_t* ring = nullptr;  // the same records in ctx's host-mapped ring
+  std::vector<uint32_t> host;      // 4 words per array, valid once done
+  bool done = false;
+  void resolve(bool synced = false);
+};
 
 class Context {
  public:
@@ -62,11 +77,33 @@ class Context {
   // NOISE: device table of the reference engine's standard normals, >= n long
   const void* noise_table(int value_type, size_t n);
 
+  // lazy side-info batches not yet checked: check_ranges() resolves them all
+  // and reports a CHECK_GT(bin, 0) failure among them (called by sync_checked
+  // and by the batched round trip; also once the list reaches kMaxTracked)
+  void track(std::shared_ptr<RangeBatch> rb);
+  // n consecutive 16-byte records of the host-mapped ring for rb (sets
+  // rb->ring; returns their device address).  Records are reused after the
+  // ring wraps; a batch still unresolved then is resolved first.
+  static constexpr uint64_t kLazyRing = 1u << 15;
+  float* claim_lazy(const std::shared_ptr<RangeBatch>& rb, int n);
+  void check_ranges();
+  void sync_checked() { sync(); check_ranges(); }
+
   std::mutex& mu() { return mu_; }
   Profiler* prof() { return &prof_; }
 
  private:
   Profiler prof_;
+  static constexpr size_t kMaxTracked = 1024;
+  std::vector<std::shared_ptr<RangeBatch>> tracked_;
+  uint32_t* lazy_h_ = nullptr;  // host view of the ring
+  uint32_t* lazy_m_ = nullptr;  // device view
+  uint64_t lazy_next_ = 0;      // absolute index of the next record
+  struct RingUse {
+    std::weak_ptr<RangeBatch> rb;
+    uint64_t start, n;
+  };
+  std::deque<RingUse> ring_uses_;
   struct StreamHolder;
   int device_;
   hipStream_t stream_;

@@ -86,7 +86,9 @@ class FixingFloatFilter : public Filter {
   void encode(Message* msg) override { convert(msg, true); }
   void decode(Message* msg) override { convert(msg, false); }
   // the element work of many messages at once (FIXING_FLOAT is stateless)
-  static void encode_messages(Context* ctx, std::vector<FfMessage>& msgs);
+  // lazy: computed min/max stay on the device (FixedFloatConfig::pending)
+  // instead of a host wait per batch
+  static void encode_messages(Context* ctx, std::vector<FfMessage>& msgs, bool lazy = false);
   static void decode_messages(Context* ctx, std::vector<FfMessage>& msgs);
 
  private:

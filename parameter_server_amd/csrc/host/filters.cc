@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "filter.h"
+#include <cstring>
 #include "snappy_host.h"
 
 namespace psf {
@@ -121,6 +122,7 @@ struct FfJob {
   FixedFloatConfig* fp;
   Buffer in, out;
   size_t elems;
+  const float* range = nullptr;  // decode: the encode's device {min, max}
 };
 
 // the value arrays FixingFloatFilter::convert touches in one message
@@ -139,7 +141,7 @@ bool collect_jobs(Message* msg, std::vector<FfJob>* jobs) {
     const int type = msg->task.value_type[i];
     if ((int)conf->fixed_point.size() <= k) conf->fixed_point.emplace_back();
     if (type == kFloat || type == kDouble)
-      jobs->push_back(FfJob{msg, i, type, conf->num_bytes, &conf->fixed_point[k++], {}, {}, 0});
+      jobs->push_back(FfJob{msg, i, type, conf->num_bytes, &conf->fixed_point[k++], {}, {}, 0, nullptr});
   }
   if (jobs->size() > first) {
     const int nb = conf->num_bytes;
@@ -178,18 +180,22 @@ void for_each_batch(std::vector<FfJob>& jobs, size_t b, size_t e, bool encode, F
 // grids are still streaming.  One array: the single-array kernels; several:
 // batched launches of up to kFfBatchMax arrays (one launch per kernel for a
 // whole batch of small messages).
-void FixingFloatFilter::encode_messages(Context* ctx, std::vector<FfMessage>& msgs) {
+void FixingFloatFilter::encode_messages(Context* ctx, std::vector<FfMessage>& msgs, bool lazy) {
   std::vector<FfJob> jobs;
   for (auto& m : msgs) collect_jobs(m.msg, &jobs);
   if (jobs.empty()) return;
+  if (ctx->device() < 0) lazy = false;
   hipStream_t st = ctx->stream();
   for (size_t base = 0; base < jobs.size(); base += Context::kSyncSlots) {
     const size_t end = std::min(jobs.size(), base + (size_t)Context::kSyncSlots);
     std::vector<uint32_t> tickets(end - base, 0);
     std::vector<FixedPoint> presets(end - base);
     std::vector<uint32_t> seeds(end - base);
+    std::vector<int> lazy_idx(end - base, -1);
+    int nlazy = 0;
     for (size_t q = base; q < end; ++q) {
       FfJob& j = jobs[q];
+      j.fp->settle();  // a config still pending from an earlier encode
       const size_t vsz = j.type == kFloat ? 4 : 8;
       j.in = ctx->to_device(j.msg->value[j.i]);
       j.elems = j.in.bytes / vsz;
@@ -199,18 +205,38 @@ void FixingFloatFilter::encode_messages(Context* ctx, std::vector<FfMessage>& ms
       if (preset.has_min && preset.has_max) {
         if (!((double)preset.max_value - (double)preset.min_value > 0))
           throw CheckError(kErrBin, "CHECK_GT(bin, 0)");
+      } else if (lazy) {
+        lazy_idx[q - base] = nlazy++;
       } else {
         tickets[q - base] = ctx->next_ticket();
       }
       j.out = ctx->alloc(j.elems * (size_t)j.nb);
       seeds[q - base] = (uint32_t)ff_clock_seed();  // `int seed = time(NULL)`, per array
     }
+    std::shared_ptr<RangeBatch> rb;
+    float* ring_dev = nullptr;
+    if (nlazy) {
+      rb = std::make_shared<RangeBatch>();
+      rb->ctx = ctx;
+      rb->dev = ctx->alloc(16 * (size_t)nlazy);
+      rb->host.assign(4 * (size_t)nlazy, 0u);
+      ring_dev = ctx->claim_lazy(rb, nlazy);
+    }
+    auto range_of = [&](size_t q) -> float* {
+      const int k = lazy_idx[q - base];
+      return k < 0 ? nullptr : reinterpret_cast<float*>(rb->dev.ptr + 16 * (size_t)k);
+    };
+    auto ring_of = [&](size_t q) -> float* {
+      const int k = lazy_idx[q - base];
+      return k < 0 ? nullptr : ring_dev + 4 * k;
+    };
     auto one = [&](size_t q) {
       FfJob& j = jobs[q];
       const uint32_t t = tickets[q - base];
+      float* r = range_of(q);
       int s = ff_encode_launch(j.in.ptr, j.elems, j.type, j.nb, presets[q - base], seeds[q - base], j.out.ptr,
-                               ctx->partials(), nullptr, nullptr, st, ctx->prof(),
-                               t ? ctx->pub_dev((int)(q - base)) : nullptr, t);
+                               ctx->partials(), r, r ? reinterpret_cast<int*>(r + 2) : nullptr, st, ctx->prof(),
+                               t ? ctx->pub_dev((int)(q - base)) : nullptr, t, ring_of(q));
       if (s != kOk) throw CheckError(s, "ff_encode launch failed");
     };
     auto batch = [&](std::vector<size_t>& part) {
@@ -219,7 +245,7 @@ void FixingFloatFilter::encode_messages(Context* ctx, std::vector<FfMessage>& ms
         const FfJob& j = jobs[q];
         const uint32_t t = tickets[q - base];
         arrs.push_back(FfArray{j.in.ptr, j.out.ptr, j.elems, presets[q - base], seeds[q - base],
-                               t ? (int)(q - base) : -1, t});
+                               t ? (int)(q - base) : -1, t, range_of(q), ring_of(q)});
       }
       Buffer scratch = ctx->alloc(ff_batch_partials_bytes(arrs.data(), (int)arrs.size()));
       int s = ff_encode_batch_launch(jobs[part[0]].type, jobs[part[0]].nb, arrs.data(), (int)arrs.size(),
@@ -227,6 +253,7 @@ void FixingFloatFilter::encode_messages(Context* ctx, std::vector<FfMessage>& ms
       if (s != kOk) throw CheckError(s, "ff_encode batch launch failed");
     };
     for_each_batch(jobs, base, end, true, one, batch);
+    if (rb) ctx->track(rb);
     for (size_t q = base; q < end; ++q) {
       FfJob& j = jobs[q];
       if (tickets[q - base]) {
@@ -235,10 +262,36 @@ void FixingFloatFilter::encode_messages(Context* ctx, std::vector<FfMessage>& ms
         if (!j.fp->has_min) j.fp->set_min(hs.range[0]);
         if (!j.fp->has_max) j.fp->set_max(hs.range[1]);
         if (hs.status != kOk) throw CheckError(kErrBin, "CHECK_GT(bin, 0)");
+      } else if (lazy_idx[q - base] >= 0) {
+        j.fp->pending = rb;
+        j.fp->pending_idx = lazy_idx[q - base];
+        j.fp->pending_min = !j.fp->has_min;
+        j.fp->pending_max = !j.fp->has_max;
       }
       j.msg->value[j.i] = j.out;
     }
   }
+}
+
+// Host side of a lazily encoded range (see FixedFloatConfig::pending).
+void FixedFloatConfig::settle() {
+  if (!pending) return;
+  std::shared_ptr<RangeBatch> rb = std::move(pending);
+  pending.reset();
+  rb->resolve();
+  const uint32_t* r = &rb->host[4 * (size_t)pending_idx];
+  float mn, mx;
+  memcpy(&mn, r, 4);
+  memcpy(&mx, r + 1, 4);
+  if (pending_min) set_min(mn);
+  if (pending_max) set_max(mx);
+  pending_idx = -1;
+  pending_min = pending_max = false;
+  if ((int32_t)r[2] != kOk) throw CheckError(kErrBin, "CHECK_GT(bin, 0)");
+}
+
+const float* FixedFloatConfig::device_range() const {
+  return pending ? reinterpret_cast<const float*>(pending->dev.ptr + 16 * (size_t)pending_idx) : nullptr;
 }
 
 // FIXING_FLOAT decode (fixing_float.h:89-101) of every value array of `msgs`;
@@ -258,7 +311,15 @@ void FixingFloatFilter::decode_messages(Context* ctx, std::vector<FfMessage>& ms
     size_t keep = first;
     for (size_t q = first; q < jobs.size(); ++q) {
       FfJob& j = jobs[q];
-      const FixedFloatConfig& fp = *j.fp;
+      FixedFloatConfig& fp = *j.fp;
+      if (fp.pending && fp.pending->ctx == ctx && !fp.pending->done && !(defer && j.type == kFloat)) {
+        // encoded on this context's stream: the kernel reads {min, max} where
+        // the encode left them (CHECK_GT(bin, 0) is reported when settled)
+        j.range = fp.device_range();
+        jobs[keep++] = j;
+        continue;
+      }
+      fp.settle();
       if (!fp.has_min) throw CheckError(kErrCheck, "CHECK(conf->has_min_value())");
       if (!fp.has_max) throw CheckError(kErrCheck, "CHECK(conf->has_max_value())");
       const double bin = (double)fp.max_value - (double)fp.min_value;
@@ -283,7 +344,7 @@ void FixingFloatFilter::decode_messages(Context* ctx, std::vector<FfMessage>& ms
   }
   auto one = [&](size_t q) {
     FfJob& j = jobs[q];
-    int s = ff_decode_launch(j.in.ptr, j.elems, j.type, j.nb, nullptr, j.fp->min_value, j.fp->max_value,
+    int s = ff_decode_launch(j.in.ptr, j.elems, j.type, j.nb, j.range, j.fp->min_value, j.fp->max_value,
                              j.out.ptr, st, ctx->prof());
     if (s != kOk) throw CheckError(s, "ff_decode launch failed");
   };
@@ -291,7 +352,7 @@ void FixingFloatFilter::decode_messages(Context* ctx, std::vector<FfMessage>& ms
     std::vector<FfDecArray> arrs;
     for (size_t q : part) {
       const FfJob& j = jobs[q];
-      arrs.push_back(FfDecArray{j.in.ptr, j.out.ptr, j.elems, j.fp->min_value, j.fp->max_value});
+      arrs.push_back(FfDecArray{j.in.ptr, j.out.ptr, j.elems, j.fp->min_value, j.fp->max_value, j.range});
     }
     int s = ff_decode_batch_launch(jobs[part[0]].type, jobs[part[0]].nb, arrs.data(), (int)arrs.size(), st,
                                    ctx->prof());
@@ -500,7 +561,7 @@ void encode_batch(RemoteNode* const* nodes, Message* const* msgs, int n) {
       launch_signatures(nodes, msgs, pend.kc_sig, true, &pend.sb);
       pend.active = true;
     }
-    for (auto& kv : ff) FixingFloatFilter::encode_messages(kv.first, kv.second);
+    for (auto& kv : ff) FixingFloatFilter::encode_messages(kv.first, kv.second, /*lazy=*/true);
   }
   finish_kc();
 }

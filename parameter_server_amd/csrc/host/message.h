@@ -47,11 +47,22 @@ struct KeyRange {
   static KeyRange All() { return KeyRange{0, ~0ull}; }  // range.h:92-95
 };
 
+struct RangeBatch;  // context.h
+
 struct FixedFloatConfig {  // filter.proto:22-25
   bool has_min = false, has_max = false;
   float min_value = -1.f, max_value = 1.f;
   void set_min(float v) { min_value = v; has_min = true; }
   void set_max(float v) { max_value = v; has_max = true; }
+  // A batched encode leaves computed min/max on the device: entry `pending_idx`
+  // of `pending` holds {min, max, status}.  A decode on the same context reads
+  // them there; every host reader calls settle() first, which brings them over
+  // (and reports CHECK_GT(bin, 0) then).
+  std::shared_ptr<RangeBatch> pending;
+  int pending_idx = -1;
+  bool pending_min = false, pending_max = false;
+  void settle();                      // filters.cc
+  const float* device_range() const;  // filters.cc
 };
 
 struct FilterConfig {  // filter.proto:3-35

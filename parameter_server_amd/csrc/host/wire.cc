@@ -57,7 +57,9 @@ std::string serialize_filter(const FilterConfig& f) {
   put_int32(&o, 1, (int32_t)f.type);
   if (f.has_signature) put_uint(&o, 2, f.signature);
   for (uint64_t u : f.uncompressed_size) put_uint(&o, 3, u);
-  for (const auto& fp : f.fixed_point) {
+  for (const auto& fp0 : f.fixed_point) {
+    auto& fp = const_cast<FixedFloatConfig&>(fp0);
+    fp.settle();  // computed min/max a batched encode left on the device
     std::string m;
     if (fp.has_min) put_float(&m, 1, fp.min_value);
     if (fp.has_max) put_float(&m, 2, fp.max_value);

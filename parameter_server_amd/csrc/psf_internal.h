@@ -100,7 +100,7 @@ int ff_grid(size_t work_items);
 int ff_encode_launch(const void* x, size_t n, int value_type, int nb, const FixedPoint& preset,
                      uint32_t seed, void* out, void* partials, float* range_out, int* status_out,
                      hipStream_t st, Profiler* prof = nullptr, PubSlot* pub = nullptr,
-                     uint32_t ticket = 0);
+                     uint32_t ticket = 0, float* range_host = nullptr);
 int ff_decode_launch(const void* code, size_t n, int value_type, int nb, const float* range,
                      float mn, float mx, void* out, hipStream_t st, Profiler* prof = nullptr);
 // Batched launches over up to kFfBatchMax arrays of one value type and
@@ -115,12 +115,15 @@ struct FfArray {
   uint32_t seed;
   int slot;
   uint32_t ticket;
+  float* range;       // device {min, max, status} for a lazy reader, or null
+  float* range_host;  // the same into host-mapped memory, or null
 };
 struct FfDecArray {
   const void* code;
   void* out;
   size_t n;
   float mn, mx;
+  const float* range;  // device {min, max} written by the encode, or null (use mn, mx)
 };
 bool ff_batchable(const void* x, const void* out, size_t n, int nb, bool encode);
 size_t ff_batch_partials_bytes(const FfArray* arrs, int count);

@@ -183,3 +183,62 @@ def test_batch_many_messages_slot_chunks(ctx, port):
                     assert vb == codes.tobytes(), i
     finally:
         F.set_clock(None)
+
+
+def test_batch_lazy_range_bin_check(ctx):
+    """A batched encode leaves computed min/max on the device; the
+    CHECK_GT(bin, 0) of an array whose max rounds onto its min is reported
+    when the range is settled (a host read of the FilterConfig) or at the
+    context's sync, not lost."""
+    from parameter_server_amd import filter as F
+    from parameter_server_amd import FIXING_FLOAT, PsfError
+    def msgs():
+        out = []
+        for v in (1.0e4, None):
+            m = F.Message(request=True, push=True, key_channel=0)
+            x = torch.full((4096,), v, device=DEV) if v is not None else torch.randn(4096, device=DEV)
+            m.add_value(x)
+            m.add_filter(FIXING_FLOAT, num_bytes=1)
+            out.append(m)
+        return out
+    ms = msgs()
+    F.RemoteNode.encode_many([F.RemoteNode(ctx), F.RemoteNode(ctx)], ms)
+    assert ms[1].fixed_points(0)[0][0]  # the good array settles fine
+    with pytest.raises(PsfError):
+        ms[0].fixed_points(0)
+    ctx_err = None
+    try:
+        ctx.sync()
+    except PsfError as e:  # the same batch is also reported once at sync
+        ctx_err = e
+    assert ctx_err is not None
+    ctx.sync()  # reported once
+
+
+def test_batch_lazy_ring_wraps(ctx, port):
+    """More lazily encoded arrays than the host-mapped record ring holds
+    (2^15): older batches are resolved before their records are reused, and
+    every message's settled range equals the C restatement's."""
+    from parameter_server_amd import FIXING_FLOAT
+    from parameter_server_amd import filter as F
+    rng = np.random.default_rng(5)
+    node = F.RemoteNode(ctx)
+    kept = []
+    total = 0
+    while total < (1 << 15) + 4096:
+        xs = [rng.standard_normal(8).astype(np.float32) * (1 + i % 7) for i in range(256)]
+        ms = []
+        for x in xs:
+            m = F.Message(request=True, push=True, key_channel=0)
+            m.add_value(torch.from_numpy(x).to(DEV))
+            m.add_filter(FIXING_FLOAT, num_bytes=1)
+            ms.append(m)
+        F.RemoteNode.encode_many([node] * len(ms), ms)
+        kept.append((xs[::37], ms[::37]))
+        total += len(ms)
+    for xs, ms in kept:
+        for x, m in zip(xs, ms):
+            _, mn, _, mx = m.fixed_points(0)[0]
+            _, _, pmn, pmx = port.ff_encode(x, 1, 1)
+            assert (np.float32(mn), np.float32(mx)) == (np.float32(pmn), np.float32(pmx))
+    ctx.sync()
