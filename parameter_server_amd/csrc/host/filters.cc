@@ -385,9 +385,12 @@ void CompressingFilter::decode(Message* msg) {  // compressing.h:20-37
   const int has_key = msg->has_key() ? 1 : 0;
   if (conf->uncompressed_size.size() != msg->value.size() + has_key)
     throw CheckError(kErrCheck, "CHECK_EQ(conf->uncompressed_size_size(), msg->value.size() + has_key)");
+  // the recorded sizes size the launches (the device checks them against each
+  // stream's header; snappy_host.cc)
   SnappyBatch batch(*ctx_);
-  if (has_key) batch.uncompress(msg->key, &msg->key);
-  for (auto& v : msg->value) batch.uncompress(v, &v);
+  size_t k = 0;
+  if (has_key) batch.uncompress(msg->key, &msg->key, &conf->uncompressed_size[k++]);
+  for (auto& v : msg->value) batch.uncompress(v, &v, &conf->uncompressed_size[k++]);
   batch.flush();
 }
 

@@ -56,26 +56,46 @@ void SnappyBatch::compress(const Buffer& src, Buffer* dst) {
   jobs_.push_back(std::move(j));
 }
 
-void SnappyBatch::uncompress(const Buffer& src, Buffer* dst) {
+static uint32_t varint_len(uint64_t v) {
+  uint32_t n = 1;
+  for (; v >= 128; v >>= 7) ++n;
+  return n;
+}
+
+void SnappyBatch::launch_uncompress(Job& j, const Buffer& src, uint32_t hdr, uint64_t dsize) {
+  j.in = c_.to_device(src);
+  j.out = dsize ? c_.alloc(dsize) : Buffer{};
+  j.out.bytes = dsize;
+  Buffer scratch = c_.alloc(snappy_uncompress_scratch(src.bytes, dsize));
+  j.ticket = c_.next_ticket();
+  int st = snappy_uncompress_launch(j.in.ptr, j.in.bytes, hdr, dsize, j.out.ptr, scratch.ptr, c_.stream(),
+                                    c_.prof(), c_.pub_dev(j.slot), j.ticket);
+  if (st != kOk) throw CheckError(st, "snappy uncompress launch failed");
+}
+
+void SnappyBatch::uncompress(const Buffer& src, Buffer* dst, const uint64_t* size_hint) {
   if (src.empty()) {  // UncompressFrom: src_size == 0 -> clear()
     dst->clear();
     return;
   }
   uint64_t dsize = 0;
-  const uint32_t hdr = snappy_read_header(c_, src, &dsize);
-  if (!hdr) throw CheckError(kErrCheck, "CHECK(snappy::GetUncompressedLength(src, src_size, &dsize))");
+  uint32_t hdr = 0;
+  const bool hinted = size_hint && src.loc == Loc::kDevice && *size_hint <= 0xffffffffull &&
+                      varint_len(*size_hint) <= src.bytes;
+  if (hinted) {
+    dsize = *size_hint;
+    hdr = varint_len(dsize);
+  } else {
+    hdr = snappy_read_header(c_, src, &dsize);
+    if (!hdr) throw CheckError(kErrCheck, "CHECK(snappy::GetUncompressedLength(src, src_size, &dsize))");
+  }
   if (jobs_.size() == (size_t)Context::kSyncSlots) flush();
   Job j;
-  j.in = c_.to_device(src);
   j.dst = dst;
-  j.out = dsize ? c_.alloc(dsize) : Buffer{};
-  j.out.bytes = dsize;
-  Buffer scratch = c_.alloc(snappy_uncompress_scratch(src.bytes, dsize));
   j.slot = (int)jobs_.size();
-  j.ticket = c_.next_ticket();
-  int st = snappy_uncompress_launch(j.in.ptr, j.in.bytes, hdr, dsize, j.out.ptr, scratch.ptr, c_.stream(),
-                                    c_.prof(), c_.pub_dev(j.slot), j.ticket);
-  if (st != kOk) throw CheckError(st, "snappy uncompress launch failed");
+  j.hinted = hinted;
+  if (hinted) j.src = src;
+  launch_uncompress(j, src, hdr, dsize);
   jobs_.push_back(std::move(j));
 }
 
@@ -83,6 +103,18 @@ void SnappyBatch::flush() {
   int bad = kOk;
   for (auto& j : jobs_) {
     c_.wait_ticket(j.slot, j.ticket);
+    if (j.hinted && c_.pub_host(j.slot)->status == kErrHeaderHint) {
+      // the stream's header disagrees with the size hint: decode by the
+      // header, as UncompressFrom does (the slot is this job's own)
+      uint64_t dsize = 0;
+      const uint32_t hdr = snappy_read_header(c_, j.src, &dsize);
+      if (!hdr) {
+        bad = kErrCheck;
+        continue;
+      }
+      launch_uncompress(j, j.src, hdr, dsize);
+      c_.wait_ticket(j.slot, j.ticket);
+    }
     const Slot& h = *c_.pub_host(j.slot);
     if (h.status != kOk) {
       bad = h.status;

@@ -17,18 +17,25 @@ class SnappyBatch {
   explicit SnappyBatch(Context& c) : c_(c) {}
   // *dst is assigned at flush(); src must stay alive until then
   void compress(const Buffer& src, Buffer* dst);
-  void uncompress(const Buffer& src, Buffer* dst);
+  // size_hint: the uncompressed length the sender recorded (COMPRESSING's
+  // FilterConfig); the launch is sized from it without reading the stream's
+  // header to the host, the device checks the header against it, and a
+  // mismatch is redone from the header at flush()
+  void uncompress(const Buffer& src, Buffer* dst, const uint64_t* size_hint = nullptr);
   void flush();
 
  private:
   struct Job {
     Buffer in, out;
     Buffer* dst = nullptr;
+    Buffer src;      // uncompress with a size hint: redone from the header on mismatch
+    bool hinted = false;
     int slot = 0;
     uint32_t ticket = 0;
   };
   Context& c_;
   std::vector<Job> jobs_;
+  void launch_uncompress(Job& j, const Buffer& src, uint32_t hdr, uint64_t dsize);
 };
 
 }  // namespace psf

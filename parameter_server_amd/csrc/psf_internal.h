@@ -18,6 +18,7 @@ constexpr int kErrBin = -3;
 constexpr int kErrHip = -4;
 constexpr int kErrCheck = -5;
 constexpr int kErrUnsupported = -6;
+constexpr int kErrHeaderHint = -100;  // internal: a snappy stream's header differs from the size hint
 
 // task.proto DataType values used by the codecs
 constexpr int kFloat = 9;

@@ -355,7 +355,7 @@ __global__ __launch_bounds__(256) void snappy_pack(const uint8_t* __restrict__ s
 constexpr uint32_t kWin = 16384;   // compressed bytes per parse window (16 KiB: ~8 waves per CU)
 constexpr uint32_t kInWin = 8192;  // staged compressed bytes in the fragment decoder
 constexpr uint64_t kNone = ~0ull;
-constexpr uint32_t kFlagInvalid = 1, kFlagSerial = 2, kFlagScan = 4;
+constexpr uint32_t kFlagInvalid = 1, kFlagSerial = 2, kFlagScan = 4, kFlagHeader = 8;
 constexpr uint64_t kFullLit = 65536 + 3;  // a 64 KiB fragment stored as one literal (tag 0xF4 + 2 length bytes)
 constexpr uint32_t kLitBudget = 512;      // K0's single steps before it hands the stream to K1/K2
 
@@ -510,6 +510,26 @@ __global__ __launch_bounds__(64) void snappy_dlit(const uint8_t* __restrict__ in
   for (uint32_t i = lane; i < nwin; i += 64) wentry[i] = kNone;
   if (lane == 0) flags[1] = 0;
   __syncthreads();
+  {  // the host sized the launch from a hint (the FilterConfig's uncompressed
+     // size): the stream's own varint header must say the same, else the host
+     // redoes the call from the header (Varint::Parse32WithLimit)
+    const uint64_t h = tag_bytes(in, C, 0);
+    uint64_t v = 0;
+    uint32_t len = 0;
+    for (uint32_t i = 0; i < 5 && i < C; ++i) {
+      const uint32_t b = (uint32_t)(h >> (8 * i)) & 0xff;
+      if (i == 4 && b >= 16) break;
+      v |= (uint64_t)(b & 127u) << (7 * i);
+      if (b < 128) {
+        len = i + 1;
+        break;
+      }
+    }
+    if (len != hdr || v != dsize) {
+      if (lane == 0) *flags = kFlagHeader;
+      return;
+    }
+  }
   uint64_t p = hdr, o = 0;
   int64_t last_w = -1;
   uint32_t singles = 0;
@@ -863,7 +883,7 @@ __global__ __launch_bounds__(64) void snappy_dfinish(const uint8_t* __restrict__
     }
   }
   if (pub) {
-    pub->status = (f & kFlagInvalid) ? kErrCheck : kOk;
+    pub->status = (f & kFlagHeader) ? kErrHeaderHint : (f & kFlagInvalid) ? kErrCheck : kOk;
     pub->size = dsize;
     publish_ticket(pub, ticket);
   }

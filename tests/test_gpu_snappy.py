@@ -177,3 +177,33 @@ def test_header_errors(ctx):
     for bad in (b"\x80", b"\xff\xff\xff\xff\x1f", b"\x03ab", b"\x02\x00\x00"):
         with pytest.raises(PsfError):
             ctx.snappy_uncompress(_dev(bad))
+
+
+def test_decode_size_hint_vs_header(ctx, port):
+    """COMPRESSING's decode sizes the launch from the FilterConfig's recorded
+    uncompressed size; the stream's own header decides (UncompressFrom reads
+    GetUncompressedLength), so a record that disagrees with the header still
+    decodes by the header, and a malformed stream is still rejected."""
+    from parameter_server_amd import COMPRESSING, PsfError, lib
+    from parameter_server_amd import filter as F
+    data = np.random.default_rng(3).integers(0, 256, 100_003, dtype=np.uint8)
+    data[:40000] = 7  # partly compressible
+    s = port.snappy_compress(data.tobytes())
+    for hint in (data.size, data.size - 1, data.size + 5, 7, 1 << 31):
+        m = F.Message(request=True, push=True)
+        m.add_value(_dev(s))
+        idx = m.add_filter(COMPRESSING)
+        assert lib().psf_fc_add_uncompressed(m.h, idx, hint) == 0
+        node = F.RemoteNode(ctx)
+        node.decode(m)
+        p, n, loc = m.value_ptr(0)
+        ctx.sync()
+        got = F.copy_out(p, n, loc, "cuda:0").cpu().numpy().tobytes()
+        assert got == data.tobytes(), hint
+    bad = b"\xff\xff\xff\xff\xff" + s[5:]
+    m = F.Message(request=True, push=True)
+    m.add_value(_dev(bad))
+    idx = m.add_filter(COMPRESSING)
+    lib().psf_fc_add_uncompressed(m.h, idx, data.size)
+    with pytest.raises(PsfError):
+        F.RemoteNode(ctx).decode(m)
