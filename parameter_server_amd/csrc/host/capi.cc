@@ -1,9 +1,9 @@
-#include <set>
 // extern "C" boundary of libpsf (include/psf.h).
 #include "../../../include/psf.h"
 
 #include <string.h>
 
+#include <set>
 #include <string>
 
 #include "filter.h"
@@ -510,13 +510,18 @@ int psf_node_roundtrip(psf_node* snd, psf_node* rcv, const psf_message* const* t
   return guarded([&] {
     if (!snd || !rcv || !tmpls || ntmpl <= 0 || iters < 0) return PSF_ERR_ARG;
     psf_message* last = nullptr;
+    psf::RemoteNode* s = snd->impl;
+    psf::RemoteNode* r = rcv->impl;
     for (int i = 0; i < iters; ++i) {
       psf::Message m = tmpls[i % ntmpl]->m;  // fresh Task + zero-copy buffers
-      snd->impl->EncodeMessage(&m);
+      psf::Message* mp = &m;
+      psf::encode_batch(&s, &mp, 1);  // = EncodeMessage, side-info left on the device
       psf::Message w = m;             // delivered copy (van: Task frame + data frames)
-      rcv->impl->DecodeMessage(&w);
+      psf::Message* wp = &w;
+      psf::decode_batch(&r, &wp, 1);  // = DecodeMessage
       if (out && i == iters - 1) last = new psf_message{w};
     }
+    s->ctx()->check_ranges();  // CHECK_GT(bin, 0) of the computed ranges
     if (out) *out = last;
     return PSF_OK;
   });
