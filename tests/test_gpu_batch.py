@@ -242,3 +242,30 @@ def test_batch_lazy_ring_wraps(ctx, port):
             _, _, pmn, pmx = port.ff_encode(x, 1, 1)
             assert (np.float32(mn), np.float32(mx)) == (np.float32(pmn), np.float32(pmx))
     ctx.sync()
+
+
+def test_batch_lazy_range_cross_context(ctx, port):
+    """Encoded on one context (stream), decoded on another: the decoding
+    context cannot read the encode's device record in stream order, so it
+    settles the range first (a sync of the encoding context); the decoded
+    values equal the C restatement's."""
+    from parameter_server_amd import filter as F
+    F.set_clock(777)
+    try:
+        other = F.Context(0)
+        cases = _cases()[:12]
+        snd = [F.RemoteNode(ctx) for _ in cases]
+        rcv = [F.RemoteNode(other) for _ in cases]
+        ms = [_message(F, *c, ch=i) for i, c in enumerate(cases)]
+        F.RemoteNode.encode_many(snd, ms)
+        ws = [m.clone() for m in ms]
+        F.RemoteNode.decode_many(rcv, ws)
+        other.sync()
+        for i, (x, nb, preset, keys) in enumerate(cases):
+            mn = None if preset is None else preset[0]
+            mx = None if preset is None else preset[1]
+            st, codes, pmn, pmx = port.ff_encode(x, nb, 777, mn, mx)
+            st, dec = port.ff_decode(codes, nb, pmn, pmx, x.dtype)
+            assert rcv[i].value(ws[i], 0).cpu().numpy().tobytes() == dec.tobytes(), i
+    finally:
+        F.set_clock(None)
