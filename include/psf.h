@@ -74,6 +74,9 @@ const char* psf_version(void);
 void psf_set_clock(int enable, int64_t t);
 
 /* ---- execution context (device + stream + workspace) ------------------- */
+/* A context (and the nodes and messages that use it) is not thread-safe:
+ * callers serialise its use, as the reference serialises one Customer's
+ * filter calls under Executor::node_mu_ (executor.cc:110,143,170). */
 typedef struct psf_context psf_context;
 /* own_stream=1: a private non-blocking stream; own_stream=0: kernels go on
  * `stream` as given (NULL = the legacy default stream).  device < 0 gives a

@@ -45,6 +45,14 @@ inline psf_context* Context() {
   return ctx;
 }
 
+// The context's stream, publish slots and caching allocator are not
+// thread-safe, and filters of different Customers run on different executor
+// threads: every adapter call holds this one lock.
+inline std::mutex& ContextMutex() {
+  static std::mutex mu;
+  return mu;
+}
+
 inline void Check(int st) { CHECK_EQ(st, PSF_OK) << "libpsf: " << psf_last_error(); }
 
 // FixingFloatFilter (src/filter/fixing_float.h:6-103) on MI355X.
@@ -61,7 +69,7 @@ class FixingFloatFilter : public Filter {
   void convert(Message* msg, bool encode) {
     FilterConfig* conf = CHECK_NOTNULL(find(FilterConfig::FIXING_FLOAT, msg));
     if (conf->num_bytes() == 0) return;
-    std::lock_guard<std::mutex> l(mu_);
+    std::lock_guard<std::mutex> l(ContextMutex());
     // Task + values as libpsf messages (host buffers, not copied)
     psf_message* m = nullptr;
     const Task& t = msg->task;
@@ -111,7 +119,6 @@ class FixingFloatFilter : public Filter {
   }
 
   psf_node* node_ = nullptr;
-  std::mutex mu_;
 };
 
 // One libpsf filter of `type` over the whole message: key (when present) and
@@ -135,7 +142,7 @@ class MessageFilter : public Filter {
       if (type_ == FilterConfig::NOISE && encode) CHECK_NOTNULL(conf);  // add_noise.h:13
       return;
     }
-    std::lock_guard<std::mutex> l(mu_);
+    std::lock_guard<std::mutex> l(ContextMutex());
     const Task& t = msg->task;
     psf_message* m = nullptr;
     Check(psf_msg_create(t.request(), t.has_param(), t.has_param() && t.param().push(),
@@ -188,7 +195,6 @@ class MessageFilter : public Filter {
 
   FilterConfig::Type type_;
   psf_node* node_ = nullptr;
-  std::mutex mu_;
 };
 
 // Registration hook for Filter::create (filter.cc:9-23): a libpsf filter, or
