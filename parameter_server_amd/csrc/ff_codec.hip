@@ -1242,6 +1242,22 @@ static void launch_encode_batch(FfBatch& B, uint32_t enc_total, hipStream_t st, 
   hipLaunchKernelGGL((ff_encode_batch<V, NB>), dim3(enc_total), dim3(kBlock), 0, st, B);
 }
 
+static size_t tiles_of(size_t n) { return ((n >> 2) + kTileGroups - 1) / kTileGroups; }
+
+// Workgroups of one array in a batched launch: its share (by tiles) of the
+// grid the single-array kernel would use, at least one.  A batch of large
+// arrays then runs several tiles per workgroup as the single kernels do
+// instead of one workgroup per tile (C4: 32 x 2^21 values).
+static int share_grid(size_t n, size_t tiles_total, int cap) {
+  const size_t t = tiles_of(n);
+  size_t c = tiles_total ? ((size_t)cap * t + tiles_total - 1) / tiles_total : (size_t)cap;
+  if (c < 1) c = 1;
+  if (c > (size_t)cap) c = cap;
+  return tile_grid(n, (int)c);
+}
+
+// an upper bound of the min/max workgroups of ff_encode_batch_launch (each
+// array's share_grid is at most its tile_grid)
 size_t ff_batch_partials_bytes(const FfArray* arrs, int count) {
   size_t wgs = 0;
   for (int i = 0; i < count; ++i)
@@ -1274,6 +1290,11 @@ int ff_encode_batch_launch(int value_type, int nb, const FfArray* arrs, int coun
   int kmm = 0;
   double bytes_mm = 0, bytes_enc = 0;
   const size_t vsz = value_type == kFloat ? 4 : 8;
+  size_t tiles_mm = 0, tiles_all = 0;
+  for (int i = 0; i < count; ++i) {
+    tiles_all += tiles_of(arrs[i].n);
+    if (!(arrs[i].preset.has_min && arrs[i].preset.has_max)) tiles_mm += tiles_of(arrs[i].n);
+  }
   for (int i = 0; i < count; ++i) {
     const FfArray& a = arrs[i];
     FfJob& J = B.job[i];
@@ -1291,7 +1312,7 @@ int ff_encode_batch_launch(int value_type, int nb, const FfArray* arrs, int coun
     J.range = a.range;
     J.range_host = a.range_host;
     J.mm_wg0 = mm;
-    J.mm_nwg = (a.preset.has_min && a.preset.has_max) ? 0u : (uint32_t)tile_grid(a.n, kMinmaxGrid);
+    J.mm_nwg = (a.preset.has_min && a.preset.has_max) ? 0u : (uint32_t)share_grid(a.n, tiles_mm, kMinmaxGrid);
     if (J.mm_nwg) {
       B.mm_first[kmm] = mm;
       B.mm_job[kmm] = i;
@@ -1300,7 +1321,7 @@ int ff_encode_batch_launch(int value_type, int nb, const FfArray* arrs, int coun
     mm += J.mm_nwg;
     J.wg0 = enc;
     B.first[i] = enc;
-    J.nwg = (uint32_t)tile_grid(a.n, kStreamGrid);
+    J.nwg = (uint32_t)share_grid(a.n, tiles_all, kStreamGrid);
     enc += J.nwg;
     if (J.mm_nwg) bytes_mm += (double)a.n * vsz;
     bytes_enc += (double)a.n * (vsz + nb);
@@ -1343,7 +1364,7 @@ int ff_decode_batch_launch(int value_type, int nb, const FfDecArray* arrs, int c
     J.range = const_cast<float*>(arrs[i].range);
     J.wg0 = wg;
     B.first[i] = wg;
-    J.nwg = (uint32_t)tile_grid(arrs[i].n, kStreamGrid);
+    J.nwg = (uint32_t)tile_grid(arrs[i].n, kStreamGrid);  // one tile per workgroup measured best here
     wg += J.nwg;
     bytes += (double)arrs[i].n * (vsz + nb);
   }
