@@ -297,7 +297,7 @@ int psf_kvmap_stats(psf_kvmap* map, int64_t* nnz, double* weight_sum, double* de
  * nodes[i]: every message runs its own chain in its own order on its own
  * node's filter instances (stateful filters see their messages in array
  * order), with FIXING_FLOAT's element work batched into one launch per kernel
- * for up to 32 arrays (the async-SGD minibatch messages and the per-server
+ * for up to 64 arrays (the async-SGD minibatch messages and the per-server
  * slices of SURVEY.md §8(d) C1/C4 are latency-bound one at a time).
  * Computed FIXING_FLOAT min/max are not waited for: a decode of the message
  * on the same context reads them on the device, and any host reader

@@ -784,34 +784,42 @@ __global__ __launch_bounds__(kBlock) void ff_decode(const uint8_t* __restrict__ 
 // single-array kernels).
 struct FfJob {
   const void* x;
-  void* out;         // codes (encode) / values (decode)
-  uint64_t n;
-  float mn, mx;      // encode: preset range; decode: the received range
-  int32_t has_min, has_max;
-  uint32_t seed, lcg_pos;
-  uint32_t mm_wg0, mm_nwg;   // encode: min/max workgroups (mm_nwg 0: both preset)
-  uint32_t wg0, nwg;         // encode / decode workgroups
-  int32_t slot;              // publish slot (encode), -1: none
-  uint32_t ticket;
-  float* range;              // encode: device {min, max, status} out; decode: device {min, max} in; or null
-  float* range_host;         // encode: {min, max, status} into host-mapped memory, or null
+  void* out;                 // codes (encode) / values (decode)
+  union {
+    struct { uint32_t seed, lcg_pos; } e;  // encode: LCG seed and its position on the mod-2^17 cycle
+    const float* range;                    // decode: device {min, max} written by the encode, or null
+  } u;
+  uint32_t n;                // elements (ff_batchable admits n < 2^32 only)
+  float mn, mx;              // encode: preset range; decode: the received range
+  uint32_t ticket;           // encode: publish ticket
+  uint16_t mm_nwg;           // encode: min/max workgroups (0: both preset)
+  uint16_t lazy;             // encode: index k of {min, max, status} at range_base / ring_base + 4k, or kNoLazy
+  uint32_t flags;            // encode: bit 0 has_min, bit 1 has_max, bits 16-31 publish slot + 1 (0: none)
 };
-constexpr int kBatchJobs = 32;
+static_assert(sizeof(FfJob) == 48, "FfJob layout");
+constexpr uint16_t kNoLazy = 0xFFFFu;
+constexpr int kBatchJobs = kFfBatchMax;
 struct FfBatch {
-  uint32_t first[kBatchJobs];     // wg0 of each job (decode / encode grid), unused entries ~0u
-  uint32_t mm_first[kBatchJobs];  // mm_wg0 of the k-th job with a min/max pass, unused ~0u
-  int32_t mm_job[kBatchJobs];     // ... and its job index
+  // a job's workgroups are [first[i], first[i + 1]) (the last ends at the
+  // grid); mm_first likewise for the min/max kernel, where a job without a
+  // min/max pass has an empty range.  Unused entries ~0u.
+  uint32_t first[kBatchJobs];
+  uint32_t mm_first[kBatchJobs];
   FfJob job[kBatchJobs];
   int njobs;
+  uint32_t total;           // workgroups of the encode / decode grid
   uint32_t mm_total;        // workgroups of the min/max kernel (partials count)
   void* partials;           // K lo[mm_total], K hi[mm_total]
   PubSlot* pub;             // slot base
+  float* range_base;        // encode: device {min, max, status} records of the lazy jobs
+  float* ring_base;         // encode: the same records in host-mapped memory
   const uint32_t* lcg_bits;
   Lcg17 k17;
   uint32_t a_lane, c_lane;
   double ratio;
 };
 static_assert(sizeof(FfBatch) <= 4096, "FfBatch must fit the 4 KiB kernel-argument segment");
+static_assert(kMinmaxGrid <= 0xFFFF, "FfJob::mm_nwg is 16 bits");
 
 
 // the job whose [first, first + count) workgroup range holds b: a fully
@@ -822,7 +830,12 @@ __device__ __forceinline__ int batch_job(const FfBatch& B, uint32_t b, bool mm) 
   int j = -1;
 #pragma unroll
   for (int i = 0; i < kBatchJobs; ++i) j += f[i] <= b ? 1 : 0;
-  return mm ? B.mm_job[j] : j;
+  return j;
+}
+
+// workgroups of job j in the encode / decode grid
+__device__ __forceinline__ uint32_t batch_nwg(const FfBatch& B, int j) {
+  return (j + 1 < B.njobs ? B.first[j + 1] : B.total) - B.first[j];
 }
 
 __device__ __forceinline__ void tile_range_of(size_t ntiles, uint32_t wg, uint32_t nwg, size_t& t0,
@@ -839,7 +852,7 @@ __global__ __launch_bounds__(kBlock) void ff_minmax_batch(FfBatch B) {
   const FfJob& J = B.job[jb];
   const V* __restrict__ x = static_cast<const V*>(J.x);
   const size_t n = J.n;
-  const uint32_t wg = blockIdx.x - J.mm_wg0;
+  const uint32_t wg = blockIdx.x - B.mm_first[jb];
   K lo = KeyOf<V>::kLoId, hi = KeyOf<V>::kHiId;
   const size_t ngroups = n >> 2;
   const size_t ntiles = (ngroups + kTileGroups - 1) / kTileGroups;
@@ -875,14 +888,16 @@ __global__ __launch_bounds__(kBlock) void ff_encode_batch(FfBatch B) {
   const V* __restrict__ x = static_cast<const V*>(J.x);
   uint8_t* __restrict__ out = static_cast<uint8_t*>(J.out);
   const size_t n = J.n;
-  const uint32_t wg = blockIdx.x - J.wg0;
+  const uint32_t wg = blockIdx.x - B.first[jb];
+  const uint32_t nwg = batch_nwg(B, jb);
+  const uint32_t mm_wg0 = B.mm_first[jb];
   float mn_f = J.mn, mx_f = J.mx;
   if (J.mm_nwg) {
     typedef typename KeyOf<V>::K K;
     const K* pp = reinterpret_cast<const K*>(B.partials);
     K lo = KeyOf<V>::kLoId, hi = KeyOf<V>::kHiId;
     for (uint32_t i = threadIdx.x; i < J.mm_nwg; i += kBlock) {
-      const K a = pp[J.mm_wg0 + i], b = pp[B.mm_total + J.mm_wg0 + i];
+      const K a = pp[mm_wg0 + i], b = pp[B.mm_total + mm_wg0 + i];
       lo = a < lo ? a : lo;
       hi = b > hi ? b : hi;
     }
@@ -897,8 +912,8 @@ __global__ __launch_bounds__(kBlock) void ff_encode_batch(FfBatch B) {
       cmn = (float)lo_v;
       cmx = (float)(hi_v + 1e-6);
     }
-    if (!J.has_min) mn_f = cmn;
-    if (!J.has_max) mx_f = cmx;
+    if (!(J.flags & 1u)) mn_f = cmn;
+    if (!(J.flags & 2u)) mx_f = cmx;
   }
   QuantParams q;
   q.min_v = (double)mn_f;
@@ -912,18 +927,20 @@ __global__ __launch_bounds__(kBlock) void ff_encode_batch(FfBatch B) {
   q.fast = q.bin < __builtin_huge_val();
   if (wg == 0 && threadIdx.x == 0) {
     const int status = (q.bin > 0) ? kOk : kErrBin;
-    if (J.range) {  // read by a later decode on this stream
-      J.range[0] = mn_f;
-      J.range[1] = mx_f;
-      reinterpret_cast<int32_t*>(J.range)[2] = status;
+    if (J.lazy != kNoLazy) {
+      float* r = B.range_base + 4 * (uint32_t)J.lazy;  // read by a later decode on this stream
+      r[0] = mn_f;
+      r[1] = mx_f;
+      reinterpret_cast<int32_t*>(r)[2] = status;
+      if (B.ring_base) {  // read by the host when it settles the FilterConfig
+        float* h = B.ring_base + 4 * (uint32_t)J.lazy;
+        h[0] = mn_f;
+        h[1] = mx_f;
+        reinterpret_cast<int32_t*>(h)[2] = status;
+      }
     }
-    if (J.range_host) {  // read by the host after a stream sync
-      J.range_host[0] = mn_f;
-      J.range_host[1] = mx_f;
-      reinterpret_cast<int32_t*>(J.range_host)[2] = status;
-    }
-    if (J.slot >= 0) {
-      PubSlot* ps = B.pub + J.slot;
+    if (J.flags >> 16) {
+      PubSlot* ps = B.pub + ((J.flags >> 16) - 1);
       ps->range[0] = mn_f;
       ps->range[1] = mx_f;
       ps->status = status;
@@ -934,7 +951,7 @@ __global__ __launch_bounds__(kBlock) void ff_encode_batch(FfBatch B) {
 
   EncodeParams p{};  // the per-launch constants the tile code reads
   p.lcg_bits = B.lcg_bits;
-  p.lcg_pos = J.lcg_pos;
+  p.lcg_pos = J.u.e.lcg_pos;
   p.k17 = B.k17;
   p.a_lane = B.a_lane;
   p.c_lane = B.c_lane;
@@ -942,7 +959,7 @@ __global__ __launch_bounds__(kBlock) void ff_encode_batch(FfBatch B) {
   const size_t ntiles = (ngroups + kTileGroups - 1) / kTileGroups;
   const size_t nfull = ngroups / kTileGroups;
   size_t t0, t1;
-  tile_range_of(ntiles, wg, J.nwg, t0, t1);
+  tile_range_of(ntiles, wg, nwg, t0, t1);
   const size_t tf = t1 < nfull ? t1 : nfull;
   for (size_t t = t0; t < tf; ++t) {
     const size_t gb = t * kTileGroups + threadIdx.x;
@@ -953,7 +970,7 @@ __global__ __launch_bounds__(kBlock) void ff_encode_batch(FfBatch B) {
   }
   for (size_t t = (t0 > tf ? t0 : tf); t < t1; ++t) {
     const size_t gb = t * kTileGroups + threadIdx.x;
-    uint32_t su = lcg_jump(J.seed, 4ull * gb) & kMask17;
+    uint32_t su = lcg_jump(J.u.e.seed, 4ull * gb) & kMask17;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const size_t g = gb + u * kBlock;
@@ -969,7 +986,7 @@ __global__ __launch_bounds__(kBlock) void ff_encode_batch(FfBatch B) {
   }
   const size_t tail = ngroups << 2;
   if (wg == 0 && threadIdx.x == 0 && tail < n) {
-    uint32_t st = lcg_jump(J.seed, tail);
+    uint32_t st = lcg_jump(J.u.e.seed, tail);
     for (size_t i = tail; i < n; ++i) {
       uint64_t r = quant_floor<V, NB>(x[i], q) + lcg_bit(st);
       for (int j = 0; j < NB; ++j) { out[i * NB + j] = (uint8_t)(r & 0xFF); r >>= 8; }
@@ -984,16 +1001,16 @@ __global__ __launch_bounds__(kBlock) void ff_decode_batch(FfBatch B) {
   const uint8_t* __restrict__ code = static_cast<const uint8_t*>(J.x);
   V* __restrict__ out = static_cast<V*>(J.out);
   const size_t n = J.n;
-  const uint32_t wg = blockIdx.x - J.wg0;
+  const uint32_t wg = blockIdx.x - B.first[jb];
   float mn_f = J.mn, mx_f = J.mx;
-  if (J.range) { mn_f = J.range[0]; mx_f = J.range[1]; }
+  if (J.u.range) { mn_f = J.u.range[0]; mx_f = J.u.range[1]; }
   const double min_v = (double)mn_f, max_v = (double)mx_f;
   const double bin = max_v - min_v;
   const double ratio = B.ratio;
   const size_t ngroups = n >> 2;
   const size_t ntiles = (ngroups + kTileGroups - 1) / kTileGroups;
   size_t t0, t1;
-  tile_range_of(ntiles, wg, J.nwg, t0, t1);
+  tile_range_of(ntiles, wg, batch_nwg(B, jb), t0, t1);
   __shared__ V lut[256];
   if (NB == 1) {
     lut[threadIdx.x] = dequant<V>((uint64_t)threadIdx.x, ratio, bin, min_v);
@@ -1225,7 +1242,7 @@ int ff_decode_launch(const void* code, size_t n, int value_type, int nb, const f
 
 // ------------------------------------------------------ batched launchers ---
 bool ff_batchable(const void* x, const void* out, size_t n, int nb, bool encode) {
-  if (nb < 1 || nb > 3 || n == 0) return false;
+  if (nb < 1 || nb > 3 || n == 0 || n >= (1ull << 32)) return false;
   const uintptr_t xa = reinterpret_cast<uintptr_t>(x), oa = reinterpret_cast<uintptr_t>(out);
   const uintptr_t code_align = nb == 2 ? 7 : 3;
   return encode ? ((xa & 15) == 0 && (oa & code_align) == 0) : ((oa & 15) == 0 && (xa & code_align) == 0);
@@ -1287,7 +1304,6 @@ int ff_encode_batch_launch(int value_type, int nb, const FfArray* arrs, int coun
     B.k17.c[k] &= kMask17;
   }
   uint32_t mm = 0, enc = 0;
-  int kmm = 0;
   double bytes_mm = 0, bytes_enc = 0;
   const size_t vsz = value_type == kFloat ? 4 : 8;
   size_t tiles_mm = 0, tiles_all = 0;
@@ -1295,37 +1311,49 @@ int ff_encode_batch_launch(int value_type, int nb, const FfArray* arrs, int coun
     tiles_all += tiles_of(arrs[i].n);
     if (!(arrs[i].preset.has_min && arrs[i].preset.has_max)) tiles_mm += tiles_of(arrs[i].n);
   }
+  // the lazy jobs' records are 16-byte entries of one device array and one
+  // host-mapped ring (one RangeBatch per encode call, filters.cc): kept as a
+  // base pointer each plus a per-job index
+  for (int i = 0; i < count; ++i) {
+    if (arrs[i].range && (!B.range_base || arrs[i].range < B.range_base)) {
+      B.range_base = arrs[i].range;
+      B.ring_base = arrs[i].range_host;
+    }
+  }
   for (int i = 0; i < count; ++i) {
     const FfArray& a = arrs[i];
     FfJob& J = B.job[i];
+    if (a.n >= (1ull << 32) || a.slot < -1 || a.slot >= 0xFFFF) return kErrArg;
     J.x = a.x;
     J.out = a.out;
-    J.n = a.n;
+    J.n = (uint32_t)a.n;
     J.mn = a.preset.min_value;
     J.mx = a.preset.max_value;
-    J.has_min = a.preset.has_min;
-    J.has_max = a.preset.has_max;
-    J.seed = a.seed;
-    J.lcg_pos = lcg_cycle().pos[a.seed & kMask17];
-    J.slot = a.slot;
+    J.flags = (a.preset.has_min ? 1u : 0u) | (a.preset.has_max ? 2u : 0u) | ((uint32_t)(a.slot + 1) << 16);
+    J.u.e.seed = a.seed;
+    J.u.e.lcg_pos = lcg_cycle().pos[a.seed & kMask17];
     J.ticket = a.ticket;
-    J.range = a.range;
-    J.range_host = a.range_host;
-    J.mm_wg0 = mm;
-    J.mm_nwg = (a.preset.has_min && a.preset.has_max) ? 0u : (uint32_t)share_grid(a.n, tiles_mm, kMinmaxGrid);
-    if (J.mm_nwg) {
-      B.mm_first[kmm] = mm;
-      B.mm_job[kmm] = i;
-      ++kmm;
+    J.lazy = kNoLazy;
+    if (a.range) {
+      const ptrdiff_t k = a.range - B.range_base;
+      if (k % 4 || k / 4 >= kNoLazy) return kErrArg;
+      const bool ring_ok = B.ring_base ? a.range_host == B.ring_base + k : a.range_host == nullptr;
+      if (!ring_ok) return kErrArg;
+      J.lazy = (uint16_t)(k / 4);
+    } else if (a.range_host) {
+      return kErrArg;
     }
-    mm += J.mm_nwg;
-    J.wg0 = enc;
+    const uint32_t mm_nwg =
+        (a.preset.has_min && a.preset.has_max) ? 0u : (uint32_t)share_grid(a.n, tiles_mm, kMinmaxGrid);
+    J.mm_nwg = (uint16_t)mm_nwg;
+    B.mm_first[i] = mm;
+    mm += mm_nwg;
     B.first[i] = enc;
-    J.nwg = (uint32_t)share_grid(a.n, tiles_all, kStreamGrid);
-    enc += J.nwg;
-    if (J.mm_nwg) bytes_mm += (double)a.n * vsz;
+    enc += (uint32_t)share_grid(a.n, tiles_all, kStreamGrid);
+    if (mm_nwg) bytes_mm += (double)a.n * vsz;
     bytes_enc += (double)a.n * (vsz + nb);
   }
+  B.total = enc;
   B.mm_total = mm;
   if (value_type == kFloat) {
     switch (nb) {
@@ -1355,19 +1383,19 @@ int ff_decode_batch_launch(int value_type, int nb, const FfDecArray* arrs, int c
   double bytes = 0;
   const size_t vsz = value_type == kFloat ? 4 : 8;
   for (int i = 0; i < count; ++i) {
+    if (arrs[i].n >= (1ull << 32)) return kErrArg;
     FfJob& J = B.job[i];
     J.x = arrs[i].code;
     J.out = arrs[i].out;
-    J.n = arrs[i].n;
+    J.n = (uint32_t)arrs[i].n;
     J.mn = arrs[i].mn;
     J.mx = arrs[i].mx;
-    J.range = const_cast<float*>(arrs[i].range);
-    J.wg0 = wg;
+    J.u.range = arrs[i].range;
     B.first[i] = wg;
-    J.nwg = (uint32_t)tile_grid(arrs[i].n, kStreamGrid);  // one tile per workgroup measured best here
-    wg += J.nwg;
+    wg += (uint32_t)tile_grid(arrs[i].n, kStreamGrid);  // one tile per workgroup measured best here
     bytes += (double)arrs[i].n * (vsz + nb);
   }
+  B.total = wg;
   ProfScope ps(prof, kKDecode, st, bytes);
   if (value_type == kFloat) {
     switch (nb) {

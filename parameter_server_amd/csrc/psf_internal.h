@@ -107,7 +107,7 @@ int ff_decode_launch(const void* code, size_t n, int value_type, int nb, const f
 // Batched launches over up to kFfBatchMax arrays of one value type and
 // num_bytes (aligned, nb 1..3: ff_batchable); encode publishes each array's
 // side-info to pub_base[slot] with its ticket.
-constexpr int kFfBatchMax = 32;
+constexpr int kFfBatchMax = 64;
 struct FfArray {
   const void* x;
   void* out;

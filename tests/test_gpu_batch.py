@@ -269,3 +269,43 @@ def test_batch_lazy_range_cross_context(ctx, port):
             assert rcv[i].value(ws[i], 0).cpu().numpy().tobytes() == dec.tobytes(), i
     finally:
         F.set_clock(None)
+
+
+@pytest.mark.parametrize("count", [64, 70])
+def test_batch_full_job_table(ctx, port, count):
+    """A full 64-array job table (and one spilling into a second launch) of one
+    (f32, num_bytes=1) group, with fully preset arrays (no min/max pass: empty
+    ranges in the min/max workgroup table) between computed and half-preset
+    ones and ragged sizes: codes, side-info and decoded values equal the
+    one-at-a-time path and the C restatement."""
+    from parameter_server_amd import filter as F
+    F.set_clock(31337)
+    try:
+        rng = np.random.default_rng(count)
+        cases = []
+        for k in range(count):
+            n = [1, 5, 4096, 4099, 65_537, 100_003][k % 6] + k
+            preset = [None, (-2.0, 2.0), (None, 3.0), (-1.0, None)][k % 4] if k % 5 else (-0.5, 0.5)
+            cases.append((rng.standard_normal(n).astype(np.float32) * (1 + k % 9), preset))
+        snd_b = [F.RemoteNode(ctx) for _ in cases]
+        rcv_b = [F.RemoteNode(ctx) for _ in cases]
+        snd_s = [F.RemoteNode(ctx) for _ in cases]
+        mb = [_message(F, x, 1, p, None, ch=i) for i, (x, p) in enumerate(cases)]
+        ms = [_message(F, x, 1, p, None, ch=i) for i, (x, p) in enumerate(cases)]
+        F.RemoteNode.encode_many(snd_b, mb)
+        for nd, m in zip(snd_s, ms):
+            nd.encode(m)
+        wb = [m.clone() for m in mb]
+        F.RemoteNode.decode_many(rcv_b, wb)
+        ctx.sync()
+        for i, (x, p) in enumerate(cases):
+            assert mb[i].fixed_points(0) == ms[i].fixed_points(0), i
+            vb = snd_b[i].value(mb[i], 0).cpu().numpy().tobytes()
+            assert vb == snd_s[i].value(ms[i], 0).cpu().numpy().tobytes(), i
+            mn, mx = (None, None) if p is None else p
+            st, codes, pmn, pmx = port.ff_encode(x, 1, 31337, mn, mx)
+            assert st == 0 and vb == codes.tobytes(), i
+            st, dec = port.ff_decode(codes, 1, pmn, pmx, x.dtype)
+            assert rcv_b[i].value(wb[i], 0).cpu().numpy().tobytes() == dec.tobytes(), i
+    finally:
+        F.set_clock(None)
