@@ -17,11 +17,85 @@
 
 #include <deque>
 #include <memory>
+#include <new>
 #include <stdexcept>
 #include <string>
+#include <utility>
 #include <vector>
 
 namespace psf {
+
+// An append-only sequence whose elements never move while it grows (pointers
+// to them stay valid across emplace_back, as std::deque's do), with the first
+// N elements stored inline: copying a Task of a few filters allocates nothing,
+// where a std::deque allocates a map and a node even when empty (the batched
+// drivers copy a Task per message per step).
+template <typename T, size_t N>
+class StableList {
+ public:
+  template <typename L, typename R>
+  class Iter {
+   public:
+    Iter(L* l, size_t i) : l_(l), i_(i) {}
+    R& operator*() const { return (*l_)[i_]; }
+    R* operator->() const { return &(*l_)[i_]; }
+    Iter& operator++() { ++i_; return *this; }
+    bool operator==(const Iter& o) const { return i_ == o.i_; }
+    bool operator!=(const Iter& o) const { return i_ != o.i_; }
+   private:
+    L* l_;
+    size_t i_;
+  };
+  typedef Iter<StableList, T> iterator;
+  typedef Iter<const StableList, const T> const_iterator;
+
+  StableList() = default;
+  StableList(const StableList& o) { append(o); }
+  StableList& operator=(const StableList& o) {
+    if (this != &o) { clear(); append(o); }
+    return *this;
+  }
+  ~StableList() { clear(); }
+
+  size_t size() const { return n_; }
+  bool empty() const { return n_ == 0; }
+  T& operator[](size_t i) { return i < N ? inl()[i] : (*extra_)[i - N]; }
+  const T& operator[](size_t i) const { return i < N ? inl()[i] : (*extra_)[i - N]; }
+  T& back() { return (*this)[n_ - 1]; }
+  const T& back() const { return (*this)[n_ - 1]; }
+  iterator begin() { return iterator(this, 0); }
+  iterator end() { return iterator(this, n_); }
+  const_iterator begin() const { return const_iterator(this, 0); }
+  const_iterator end() const { return const_iterator(this, n_); }
+
+  template <typename... A>
+  T& emplace_back(A&&... a) {
+    if (n_ < N) {
+      T* p = new (inl() + n_) T(std::forward<A>(a)...);
+      ++n_;
+      return *p;
+    }
+    if (!extra_) extra_.reset(new std::deque<T>());
+    extra_->emplace_back(std::forward<A>(a)...);
+    ++n_;
+    return extra_->back();
+  }
+  void clear() {
+    for (size_t i = 0; i < n_ && i < N; ++i) inl()[i].~T();
+    extra_.reset();
+    n_ = 0;
+  }
+
+ private:
+  void append(const StableList& o) {
+    for (size_t i = 0; i < o.n_; ++i) emplace_back(o[i]);
+  }
+  T* inl() { return std::launder(reinterpret_cast<T*>(buf_)); }
+  const T* inl() const { return std::launder(reinterpret_cast<const T*>(buf_)); }
+  alignas(T) unsigned char buf_[N * sizeof(T)];
+  size_t n_ = 0;
+  std::unique_ptr<std::deque<T>> extra_;
+};
 
 enum class Loc : int { kHost = 0, kDevice = 1 };
 
@@ -70,7 +144,7 @@ struct FilterConfig {  // filter.proto:3-35
   Type type = KEY_CACHING;
   bool clear_cache_if_done = false;            // field 20
   int32_t num_bytes = 3;                       // field 5, default 3
-  std::deque<FixedFloatConfig> fixed_point;    // field 4 (stable addresses)
+  StableList<FixedFloatConfig, 2> fixed_point;  // field 4 (stable addresses)
   float mean = 0.f, std = 0.f;                 // fields 6, 7
   bool has_signature = false;                  // field 2
   uint32_t signature = 0;
@@ -88,7 +162,7 @@ struct Task {
   bool has_key_type = false;
   int key_type = 0;
   std::vector<int> value_type;
-  std::deque<FilterConfig> filter;
+  StableList<FilterConfig, 4> filter;  // stable addresses
   bool has_param = false;
   bool push = false;  // param.push
 };
