@@ -150,6 +150,30 @@ bool collect_jobs(Message* msg, std::vector<FfJob>* jobs) {
   return true;
 }
 
+// Outputs of jobs [b, e): one HBM block carved into 256-byte aligned
+// sub-buffers that share its owner when there are several (one allocator call
+// per batch instead of one per message), a plain buffer for one.
+void alloc_outputs(Context* ctx, std::vector<FfJob>& jobs, size_t b, size_t e,
+                   const std::vector<size_t>& bytes) {
+  if (e - b == 1) {
+    jobs[b].out = ctx->alloc(bytes[0]);
+    return;
+  }
+  auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  size_t total = 0;
+  for (size_t q = b; q < e; ++q) total += up(bytes[q - b]);
+  Buffer blk = ctx->alloc(total);
+  size_t off = 0;
+  for (size_t q = b; q < e; ++q) {
+    Buffer& o = jobs[q].out;
+    o.owner = blk.owner;
+    o.ptr = blk.ptr + off;
+    o.bytes = bytes[q - b];
+    o.loc = Loc::kDevice;
+    off += up(bytes[q - b]);
+  }
+}
+
 // jobs [b, e) grouped for batched launches: same (type, nb), batchable
 template <typename F>
 void for_each_batch(std::vector<FfJob>& jobs, size_t b, size_t e, bool encode, F&& launch_one,
@@ -182,6 +206,7 @@ void for_each_batch(std::vector<FfJob>& jobs, size_t b, size_t e, bool encode, F
 // whole batch of small messages).
 void FixingFloatFilter::encode_messages(Context* ctx, std::vector<FfMessage>& msgs, bool lazy) {
   std::vector<FfJob> jobs;
+  jobs.reserve(msgs.size());
   for (auto& m : msgs) collect_jobs(m.msg, &jobs);
   if (jobs.empty()) return;
   if (ctx->device() < 0) lazy = false;
@@ -192,6 +217,7 @@ void FixingFloatFilter::encode_messages(Context* ctx, std::vector<FfMessage>& ms
     std::vector<FixedPoint> presets(end - base);
     std::vector<uint32_t> seeds(end - base);
     std::vector<int> lazy_idx(end - base, -1);
+    std::vector<size_t> out_bytes(end - base);
     int nlazy = 0;
     for (size_t q = base; q < end; ++q) {
       FfJob& j = jobs[q];
@@ -210,9 +236,10 @@ void FixingFloatFilter::encode_messages(Context* ctx, std::vector<FfMessage>& ms
       } else {
         tickets[q - base] = ctx->next_ticket();
       }
-      j.out = ctx->alloc(j.elems * (size_t)j.nb);
+      out_bytes[q - base] = j.elems * (size_t)j.nb;
       seeds[q - base] = (uint32_t)ff_clock_seed();  // `int seed = time(NULL)`, per array
     }
+    alloc_outputs(ctx, jobs, base, end, out_bytes);
     std::shared_ptr<RangeBatch> rb;
     float* ring_dev = nullptr;
     if (nlazy) {
@@ -241,6 +268,7 @@ void FixingFloatFilter::encode_messages(Context* ctx, std::vector<FfMessage>& ms
     };
     auto batch = [&](std::vector<size_t>& part) {
       std::vector<FfArray> arrs;
+      arrs.reserve(part.size());
       for (size_t q : part) {
         const FfJob& j = jobs[q];
         const uint32_t t = tickets[q - base];
@@ -300,6 +328,7 @@ const float* FixedFloatConfig::device_range() const {
 // nothing decoded after it reads values).
 void FixingFloatFilter::decode_messages(Context* ctx, std::vector<FfMessage>& msgs) {
   std::vector<FfJob> jobs;
+  jobs.reserve(msgs.size());
   for (auto& m : msgs) {
     const size_t first = jobs.size();
     if (!collect_jobs(m.msg, &jobs)) continue;
@@ -336,12 +365,14 @@ void FixingFloatFilter::decode_messages(Context* ctx, std::vector<FfMessage>& ms
   }
   if (jobs.empty()) return;
   hipStream_t st = ctx->stream();
-  for (auto& j : jobs) {
-    const size_t vsz = j.type == kFloat ? 4 : 8;
+  std::vector<size_t> out_bytes(jobs.size());
+  for (size_t q = 0; q < jobs.size(); ++q) {
+    FfJob& j = jobs[q];
     j.in = ctx->to_device(j.msg->value[j.i]);
     j.elems = j.in.bytes / (size_t)j.nb;
-    j.out = ctx->alloc(j.elems * vsz);
+    out_bytes[q] = j.elems * (j.type == kFloat ? 4 : 8);
   }
+  alloc_outputs(ctx, jobs, 0, jobs.size(), out_bytes);
   auto one = [&](size_t q) {
     FfJob& j = jobs[q];
     int s = ff_decode_launch(j.in.ptr, j.elems, j.type, j.nb, j.range, j.fp->min_value, j.fp->max_value,
@@ -350,6 +381,7 @@ void FixingFloatFilter::decode_messages(Context* ctx, std::vector<FfMessage>& ms
   };
   auto batch = [&](std::vector<size_t>& part) {
     std::vector<FfDecArray> arrs;
+    arrs.reserve(part.size());
     for (size_t q : part) {
       const FfJob& j = jobs[q];
       arrs.push_back(FfDecArray{j.in.ptr, j.out.ptr, j.elems, j.fp->min_value, j.fp->max_value, j.range});
