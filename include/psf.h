@@ -325,6 +325,10 @@ int psf_nodes_roundtrip(psf_node* const* snd, psf_node* const* rcv, const psf_me
 #define PSF_K_NUM 10
 /* kernel_mask: bit k times kernel PSF_K_k (-1 = all, 0 = off) */
 int psf_profile_enable(psf_context* ctx, int kernel_mask);
+/* time only every stride-th launch of each profiled kernel (1 = every launch;
+ * resets the launch counts): keeps the event pairs from dominating a step of
+ * many short kernels */
+int psf_profile_stride(psf_context* ctx, int stride);
 int psf_profile_reset(psf_context* ctx);
 /* launches, summed kernel milliseconds and summed algorithmic HBM bytes */
 int psf_profile_read(psf_context* ctx, int kernel, int64_t* launches, double* total_ms,

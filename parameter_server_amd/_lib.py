@@ -115,6 +115,7 @@ SIGNATURES = {
     "psf_nodes_decode": ([C.POINTER(vp), C.POINTER(vp), C.c_int], C.c_int),
     "psf_nodes_roundtrip": ([C.POINTER(vp), C.POINTER(vp), C.POINTER(vp), C.c_int, C.c_int], C.c_int),
     "psf_profile_enable": ([vp, C.c_int], C.c_int),
+    "psf_profile_stride": ([vp, C.c_int], C.c_int),
     "psf_profile_reset": ([vp], C.c_int),
     "psf_profile_read": ([vp, C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_double),
                           C.POINTER(C.c_double)], C.c_int),

@@ -590,6 +590,11 @@ int psf_profile_enable(psf_context* ctx, int kernel_mask) {
   ctx->impl->prof()->enable((uint32_t)kernel_mask);
   return PSF_OK;
 }
+int psf_profile_stride(psf_context* ctx, int stride) {
+  if (!ctx || stride < 1) return PSF_ERR_ARG;
+  ctx->impl->prof()->set_stride((uint32_t)stride);
+  return PSF_OK;
+}
 int psf_profile_reset(psf_context* ctx) {
   if (!ctx) return PSF_ERR_ARG;
   ctx->impl->prof()->reset();

@@ -63,7 +63,13 @@ class Profiler {
  public:
   ~Profiler();
   bool on(KernelId id) const { return (mask_ >> id) & 1u; }
+  // on(id), and this launch is one of every `stride` launches of kernel id
+  bool sample(KernelId id) { return on(id) && seen_[id]++ % stride_ == 0; }
   void enable(uint32_t kernel_mask) { mask_ = kernel_mask; }
+  void set_stride(uint32_t stride) {
+    stride_ = stride ? stride : 1;
+    for (auto& s : seen_) s = 0;
+  }
   void begin(hipStream_t st);
   void end(KernelId id, hipStream_t st, double alg_bytes);
   void collect();  // waits for pending events, accumulates
@@ -76,6 +82,8 @@ class Profiler {
   struct Pending { KernelId id; hipEvent_t a, b; double bytes; };
   hipEvent_t take();
   uint32_t mask_ = 0;
+  uint32_t stride_ = 1;
+  uint64_t seen_[kKNum] = {0};
   hipEvent_t cur_ = nullptr;
   Pending* pend_ = nullptr;
   int npend_ = 0, cap_ = 0;
@@ -87,7 +95,7 @@ class Profiler {
 struct ProfScope {
   Profiler* p; KernelId id; hipStream_t st; double bytes;
   ProfScope(Profiler* p_, KernelId id_, hipStream_t st_, double bytes_)
-      : p(p_ && p_->on(id_) ? p_ : nullptr), id(id_), st(st_), bytes(bytes_) {
+      : p(p_ && p_->sample(id_) ? p_ : nullptr), id(id_), st(st_), bytes(bytes_) {
     if (p) p->begin(st);
   }
   ~ProfScope() { if (p) p->end(id, st, bytes); }

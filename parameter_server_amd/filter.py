@@ -47,13 +47,14 @@ class Context:
         check(lib().psf_context_sync(self.h))
 
     # -- launch profiler -----------------------------------------------------
-    def profile(self, on: bool = True, kernels=None):
+    def profile(self, on: bool = True, kernels=None, stride: int = 1):
         """Time kernel launches with HIP events: all kernels, or only `kernels`
-        (names from _lib.KERNELS)."""
+        (names from _lib.KERNELS); every `stride`-th launch of each."""
         from ._lib import KERNELS
         mask = 0 if not on else (-1 if kernels is None else
                                  sum(1 << KERNELS.index(k) for k in kernels))
         check(lib().psf_profile_enable(self.h, mask))
+        check(lib().psf_profile_stride(self.h, stride))
 
     def profile_reset(self):
         check(lib().psf_profile_reset(self.h))
