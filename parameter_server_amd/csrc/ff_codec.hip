@@ -858,7 +858,19 @@ __global__ __launch_bounds__(kBlock) void ff_minmax_batch(FfBatch B) {
   const size_t ntiles = (ngroups + kTileGroups - 1) / kTileGroups;
   size_t t0, t1;
   tile_range_of(ntiles, wg, J.mm_nwg, t0, t1);
-  for (size_t t = t0; t < t1; ++t) {
+  const size_t nfull = ngroups / kTileGroups;
+  const size_t tf = t1 < nfull ? t1 : nfull;
+  for (size_t t = t0; t < tf; ++t) {  // full tiles: all four loads in flight before the folds
+    const size_t gb = t * kTileGroups + threadIdx.x;
+    V v[4][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) Vec4<V>::load(x + 4 * (gb + u * kBlock), v[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc_minmax<V, K>(v[u][j], lo, hi);
+  }
+  for (size_t t = (t0 > tf ? t0 : tf); t < t1; ++t) {  // the partial last tile
     const size_t gb = t * kTileGroups + threadIdx.x;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
