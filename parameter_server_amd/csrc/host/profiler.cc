@@ -20,7 +20,10 @@ Profiler::~Profiler() {
 hipEvent_t Profiler::take() {
   if (npool_ > 0) return pool_[--npool_];
   hipEvent_t e = nullptr;
-  (void)hipEventCreate(&e);
+  // timing only: no system-scope fence at record (it wrote back and
+  // invalidated the caches inside the timed bracket: +1.5 us per encode
+  // launch, +4 us per C2 step, measured A/B on one box)
+  (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
   return e;
 }
 
