@@ -141,18 +141,51 @@ __device__ __forceinline__ uint32_t match_len(const uint8_t* b, uint32_t s1, uin
   }
 }
 
+// dst[o, o+len) = s[0, len) for a 256-aligned source with 8 readable bytes
+// past len (a scratch slot): destination dwords wholly inside the range are
+// composed from the two aligned source dwords they straddle, byte stores at
+// the edges
+__device__ void place_bytes(uint8_t* __restrict__ dst, uint64_t o, const uint8_t* __restrict__ s, uint32_t len,
+                            uint32_t tid) {
+  const uintptr_t ob = reinterpret_cast<uintptr_t>(dst);
+  const uint64_t a0 = ((ob + o + 3) & ~(uintptr_t)3) - ob, a1 = ((ob + o + len) & ~(uintptr_t)3) - ob;
+  if (a0 >= a1) {
+    for (uint32_t i = tid; i < len; i += 256) dst[o + i] = s[i];
+    return;
+  }
+  const uint32_t head = (uint32_t)(a0 - o);
+  if (tid < head) dst[o + tid] = s[tid];
+  const uint32_t* s32 = reinterpret_cast<const uint32_t*>(s);
+  uint32_t* d32 = reinterpret_cast<uint32_t*>(dst + a0);
+  const uint32_t nw = (uint32_t)((a1 - a0) >> 2);
+  for (uint32_t j = tid; j < nw; j += 256) {  // destination bytes a0+4j.. are source bytes head+4j..
+    const uint32_t lo = s32[j], hi = s32[j + 1];
+    d32[j] = head ? __builtin_amdgcn_alignbyte(hi, lo, head) : lo;
+  }
+  const uint32_t tail0 = (uint32_t)(a1 - o);
+  for (uint32_t i = tail0 + tid; i < len; i += 256) dst[o + i] = s[i];
+}
+
 // One workgroup of 4 waves per 64 KiB fragment (the LDS footprint allows one
 // workgroup per CU): all 256 lanes stage the fragment, wave 0 runs the serial
 // 1.1.8 parse, and the final literal (all of an incompressible fragment) is
 // copied out by all 256 lanes again.
 __global__ __launch_bounds__(256) void snappy_compress_frags(const uint8_t* __restrict__ in, size_t n,
                                                              uint8_t* __restrict__ scratch,
-                                                             uint32_t* __restrict__ lens) {
+                                                             uint8_t* __restrict__ dst, uint32_t hdr,
+                                                             uint64_t* __restrict__ state,
+                                                             uint32_t* __restrict__ ctr, uint32_t nfrag,
+                                                             PubSlot* pub, uint32_t ticket) {
   __shared__ CompressLds L;
-  __shared__ uint32_t s_op, s_next;
+  __shared__ uint32_t s_op, s_next, s_f;
+  __shared__ uint64_t s_off;
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid;  // wave 0's lanes in the parse (tid < 64 there)
-  const uint32_t f = blockIdx.x;
+  // fragments are taken in the order workgroups start, so every fragment a
+  // workgroup's look-back waits on belongs to a workgroup already running
+  if (tid == 0) s_f = atomicAdd(ctr, 1u);
+  __syncthreads();
+  const uint32_t f = s_f;
   const size_t start = (size_t)f * kFrag;
   const uint32_t len = (uint32_t)min((size_t)kFrag, n - start);
   const uint8_t* g = in + start;
@@ -274,81 +307,44 @@ remainder:
   __syncthreads();
   op = s_op;
   next_emit = s_next;
-  if (next_emit < len) op = emit_literal<256>(out, op, srcb, next_emit, len - next_emit, tid);
-  if (tid == 0) lens[f] = op;
-}
-
-// exclusive scan of fragment lengths (+ the varint header) -> offs; total -> pub
-__global__ __launch_bounds__(1024) void snappy_scan(const uint32_t* __restrict__ lens, uint32_t nfrag,
-                                                    uint32_t hdr, uint64_t* __restrict__ offs,
-                                                    PubSlot* pub, uint32_t ticket) {
-  __shared__ uint64_t part[1024];
-  const uint32_t t = threadIdx.x;
-  const uint32_t per = (nfrag + 1023) / 1024;
-  const uint32_t b = t * per, e = min(nfrag, b + per);
-  uint64_t s = 0;
-  for (uint32_t i = b; i < e; ++i) s += lens[i];
-  part[t] = s;
-  __syncthreads();
-  for (uint32_t d = 1; d < 1024; d <<= 1) {
-    const uint64_t v = t >= d ? part[t - d] : 0;
-    __syncthreads();
-    part[t] += v;
-    __syncthreads();
+  // this fragment's length: the tags emitted so far plus the final literal
+  uint32_t flen = op;
+  if (next_emit < len) {
+    const uint32_t m = len - next_emit - 1;
+    flen += 1 + m + 1 + (m < 60 ? 0 : ((31 - __builtin_clz(m)) >> 3) + 1);
   }
-  uint64_t run = hdr + (t ? part[t - 1] : 0);
-  for (uint32_t i = b; i < e; ++i) {
-    offs[i] = run;
-    run += lens[i];
-  }
-  if (t == 1023) {
-    offs[nfrag] = hdr + part[1023];
-    if (pub) {
-      pub->size = hdr + part[1023];
+  // its offset in the stream: decoupled look-back over the fragments before
+  // it (state word = flag << 62 | bytes; flag 1: this fragment's length, 2:
+  // the inclusive prefix with the varint header); device-scope atomics only
+  if (tid == 0) {
+    uint64_t excl = hdr;
+    if (f > 0) {
+      atomicAdd(&state[f], (1ull << 62) | flen);
+      uint64_t sum = 0;
+      for (uint32_t j = f - 1;; --j) {
+        uint64_t w;
+        while (((w = atomicAdd(&state[j], 0ull)) >> 62) == 0) __builtin_amdgcn_s_sleep(1);
+        sum += w & ((1ull << 62) - 1);
+        if ((w >> 62) == 2) break;
+      }
+      excl = sum;
+    }
+    atomicExch(reinterpret_cast<unsigned long long*>(&state[f]), (2ull << 62) | (excl + flen));
+    s_off = excl;
+    if (f + 1 == nfrag && pub) {
+      pub->size = excl + flen;
       pub->status = kOk;
       publish_ticket(pub, ticket);
     }
   }
-}
-
-__global__ __launch_bounds__(256) void snappy_pack(const uint8_t* __restrict__ scratch,
-                                                   const uint32_t* __restrict__ lens,
-                                                   const uint64_t* __restrict__ offs, size_t n,
-                                                   uint8_t* __restrict__ out) {
-  const uint32_t f = blockIdx.x;
-  if (f == 0 && threadIdx.x == 0) {
-    uint32_t v = (uint32_t)n, i = 0;
-    while (v >= 128) {
-      out[i++] = (uint8_t)(v | 128);
-      v >>= 7;
-    }
-    out[i] = (uint8_t)v;
+  __syncthreads();
+  const uint64_t off = s_off;
+  if (f == 0 && tid < hdr) dst[tid] = (uint8_t)(((uint32_t)n >> (7 * tid)) | (tid + 1 < hdr ? 128u : 0u));
+  if (op) place_bytes(dst, off, out, op, tid);  // the tags written to the scratch slot
+  if (next_emit < len) {  // emit_literal composes dwords relative to a 4-aligned base
+    const uint64_t at = off + op;
+    emit_literal<256>(dst + (at & ~3ull), (uint32_t)(at & 3), srcb, next_emit, len - next_emit, tid);
   }
-  const uint8_t* s = scratch + (size_t)f * kSnappyFragOut;  // 256-aligned slot
-  const uint64_t o = offs[f];
-  const uint32_t len = lens[f];
-  // destination dwords that lie wholly inside [o, o+len), each composed from
-  // the two aligned scratch dwords it straddles; byte stores at the edges.
-  // The scratch slot has room past len (kSnappyFragOut >= max fragment
-  // output + 8), so the second dword read stays inside the slot.
-  const uintptr_t ob = reinterpret_cast<uintptr_t>(out);
-  const uint64_t a0 = ((ob + o + 3) & ~(uintptr_t)3) - ob, a1 = ((ob + o + len) & ~(uintptr_t)3) - ob;
-  if (a0 >= a1) {
-    for (uint32_t i = threadIdx.x; i < len; i += 256) out[o + i] = s[i];
-    return;
-  }
-  const uint32_t head = (uint32_t)(a0 - o);
-  if (threadIdx.x < head) out[o + threadIdx.x] = s[threadIdx.x];
-  const uint32_t* s32 = reinterpret_cast<const uint32_t*>(s);
-  uint32_t* d32 = reinterpret_cast<uint32_t*>(out + a0);
-  const uint32_t nw = (uint32_t)((a1 - a0) >> 2);
-  for (uint32_t j = threadIdx.x; j < nw; j += 256) {
-    // destination bytes a0+4j.. come from scratch bytes head+4j..
-    const uint32_t lo = s32[j], hi = s32[j + 1];
-    d32[j] = head ? __builtin_amdgcn_alignbyte(hi, lo, head) : lo;
-  }
-  const uint32_t tail0 = (uint32_t)(a1 - o);
-  for (uint32_t i = tail0 + threadIdx.x; i < len; i += 256) out[o + i] = s[i];
 }
 
 // ------------------------------------------------------------------ uncompress
@@ -895,7 +891,7 @@ size_t snappy_max_compressed(size_t n) { return 32 + n + n / 6; }
 
 size_t snappy_compress_scratch(size_t n) {
   const size_t nfrag = (n + kFrag - 1) / kFrag;
-  return nfrag * kSnappyFragOut + nfrag * 4 + (nfrag + 1) * 8 + 64;
+  return nfrag * kSnappyFragOut + (nfrag + 1) * 8 + 64;
 }
 
 int snappy_compress_launch(const void* in, size_t n, void* out, void* scratch, hipStream_t st, Profiler* prof,
@@ -903,18 +899,17 @@ int snappy_compress_launch(const void* in, size_t n, void* out, void* scratch, h
   if (n == 0 || n > 0xffffffffull) return kErrArg;
   const uint32_t nfrag = (uint32_t)((n + kFrag - 1) / kFrag);
   uint8_t* s = static_cast<uint8_t*>(scratch);
-  uint32_t* lens = reinterpret_cast<uint32_t*>(s + (size_t)nfrag * kSnappyFragOut);
-  uint64_t* offs = reinterpret_cast<uint64_t*>(
-      (reinterpret_cast<uintptr_t>(lens + nfrag) + 7) & ~(uintptr_t)7);
+  // look-back state (one word per fragment) and the fragment ticket counter,
+  // zeroed before the launch
+  uint64_t* state = reinterpret_cast<uint64_t*>(s + (size_t)nfrag * kSnappyFragOut);
+  uint32_t* ctr = reinterpret_cast<uint32_t*>(state + nfrag);
+  hipError_t e = hipMemsetAsync(state, 0, (size_t)nfrag * 8 + 8, st);
+  if (e != hipSuccess) return kErrHip;
   uint32_t hdr = 1;
   for (uint64_t v = n; v >= 128; v >>= 7) ++hdr;
-  {
-    ProfScope ps(prof, kKSnappyCompress, st, (double)n);
-    hipLaunchKernelGGL(snappy_compress_frags, dim3(nfrag), dim3(256), 0, st,
-                       static_cast<const uint8_t*>(in), n, s, lens);
-  }
-  hipLaunchKernelGGL(snappy_scan, dim3(1), dim3(1024), 0, st, lens, nfrag, hdr, offs, pub, ticket);
-  hipLaunchKernelGGL(snappy_pack, dim3(nfrag), dim3(256), 0, st, s, lens, offs, n, static_cast<uint8_t*>(out));
+  ProfScope ps(prof, kKSnappyCompress, st, (double)n);
+  hipLaunchKernelGGL(snappy_compress_frags, dim3(nfrag), dim3(256), 0, st, static_cast<const uint8_t*>(in), n, s,
+                     static_cast<uint8_t*>(out), hdr, state, ctr, nfrag, pub, ticket);
   return launch_status();
 }
 
