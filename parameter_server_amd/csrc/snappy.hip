@@ -9,9 +9,12 @@
 // runs the exact 1.1.8 parse with lane-parallel helpers -- 64 speculative
 // probes of the skip heuristic per step (the probe positions do not depend on
 // the data, only on where the skip loop started), match extension 64 bytes per
-// step, literal bytes copied 64 per step -- and writes its fragment into a
-// fixed-stride scratch slot.  A scan over the fragment lengths and a pack pass
-// build the stream.
+// step, literal bytes copied 64 per step.  Tags go to a fixed-stride scratch
+// slot; at the end of the parse the fragment's length is known, a decoupled
+// look-back over the fragments before it (taken in workgroup start order
+// through an atomic ticket) gives its offset in the stream, and the tags and
+// the final literal (all of an incompressible fragment, straight from LDS) are
+// written to their place.
 //
 // Uncompress accepts any valid snappy stream (a reference sender's included)
 // and reproduces RawUncompress's verdict.  Tag boundaries are found in
