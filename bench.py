@@ -2,31 +2,44 @@
 """bench.py -- BASELINE.json metric: GiB/s of key-value payload through the
 filter encode+decode chain, device-resident, on MI355X.
 
-Default workload (BASELINE.json configs[1]): one message
-per step carrying n = 2^27 dense float32 values (512 MiB, N(0,1), seed 1) and
-the chain [FIXING_FLOAT num_bytes=1] with min/max computed; a step encodes it on
-the worker's RemoteNode, delivers it and decodes it on the server's
-(libpsf psf_node_roundtrip: no Python per message).  Payload = 4n bytes/step.
+Default workload (BASELINE.json north_star target; SURVEY.md §8(d) C2 at the
+north-star size): one message per step carrying n = 2^28 dense float32 values
+(1 GiB, N(0,1), seed 1) and the chain [FIXING_FLOAT num_bytes=1] with min/max
+computed; a step encodes it on the worker's RemoteNode, delivers it and
+decodes it on the server's (libpsf psf_node_roundtrip: no Python per message).
+Payload = 4n bytes/step.  The same run also measures BASELINE configs[1]'s
+128M values (2^27) and reports it under "config_128M".
 
-N GPUs (torchrun, one rank per GPU): rank g is server g of EvenDivide(N, g)
-and codes its own pre-placed shard (no data-path collective; weak scaling).
-Timed region: barrier + synchronize, K steps, barrier + synchronize; the max
-elapsed over ranks is the job time.  value = N * K * payload / time.
+N GPUs: rank g is server g of EvenDivide(N, g) and codes its own pre-placed
+shard (no data-path collective; weak scaling).  `python bench.py --gpus N`
+starts the N rank processes itself (from a parent that makes no GPU call)
+unless WORLD_SIZE is already set (torchrun).  Timed region: barrier +
+synchronize, K steps, barrier + synchronize; the max elapsed over ranks is the
+job time.  value = N * K * payload / time.
+
+Other configs (--config): c1 (ctr push streams, batched), c3 / c3miss (10M
+keys @1% + values, KEY_CACHING hit / miss), c4 (64 push streams over 8 server
+key ranges, cross-range spill in one all-to-all-v per step), c5 (embedding
+rows dim 128 sliced over 8 servers, [KEY_CACHING, FIXING_FLOAT(, COMPRESSING)]).
 
 roofline: per-kernel durations from HIP events recorded on the launch stream
-around every kernel inside the timed region (libpsf profiler); the dominant
-kernel's algorithmic bytes / average duration vs 8 TB/s.  traffic: PMC-derived
-HBM bytes per launch from profiles/pmc_traffic.json when it matches (see
-tools/pmc_traffic.py), else null.
-cpu_baseline: the reference's own filter code (oracle/_ref, unmodified
-headers) -- or the C restatement if that is absent -- on one host core, rank 0
-at N=1 only, over a bounded sample (2^24 values, repeated ~10 s).
+around the dominant kernel inside the timed region (libpsf profiler); its
+algorithmic bytes / average duration vs 8 TB/s.  traffic: PMC-derived HBM bytes
+per launch from profiles/pmc_traffic.json when it matches this kernel and
+size (tools/pmc_traffic.py), else null.
+cpu_baseline: the C restatement of the reference's filter code (oracle/,
+"port") on the host cores of the same box, rank 0 at N=1 only, over a bounded
+sample of the same workload: one core where the reference's filters run
+serialised (C1-C3), one thread per stream / slice up to 16 for C4 / C5
+(SURVEY.md §8(d)).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -35,11 +48,12 @@ sys.path.insert(0, ROOT)
 
 GIB = float(1 << 30)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, MI355X_MICROARCH.md
+CPU_THREADS_MAX = 16   # the GPU box's CPU share per GPU
 
 
 WORKLOADS = {
-    "c2": "C2 (BASELINE configs[1]): dense f32 values, chain [FIXING_FLOAT num_bytes={nb}], "
-          "min/max computed, encode+decode round trip per step",
+    "c2": "C2 (BASELINE configs[1] chain at the north-star size): dense f32 values, chain "
+          "[FIXING_FLOAT num_bytes={nb}], min/max computed, encode+decode round trip per step",
     "c3": "C3 (BASELINE configs[2]): 10M uint64 keys @1% of [0,1e9) + f32 values, chain "
           "[KEY_CACHING, FIXING_FLOAT num_bytes={nb}], repeat send (key cache hit: keys elided)",
     "c3miss": "C3 (BASELINE configs[2]) first-send path: 10M uint64 keys @1% of [0,1e9) + f32 "
@@ -47,15 +61,18 @@ WORKLOADS = {
               "every send a key cache miss",
     "c4": "C4 (BASELINE configs[3]): {streams} push streams in total (stream s on rank s % N), each "
           "{m} sorted unique uint64 keys spread over 2^64 (splitmix64) + f32 values, sliced at the "
-          "EvenDivide(N) server ranges, per-(stream, server) [KEY_CACHING, FIXING_FLOAT num_bytes={nb}], "
-          "cross-range slices spilled in one all-to-all-v per step (RCCL), repeat sends (key cache hit)",
-    "c1": "C1 (BASELINE configs[0]) on the device: the ctr example's push stream "
-          "(example/linear/ctr/online_l1lr.conf: [KEY_CACHING(clear_cache_if_done), FIXING_FLOAT "
-          "num_bytes={nb}]), {streams} concurrent minibatch streams of {m} sorted unique keys + f32 "
-          "gradients, all streams' messages of a step encoded / decoded in one batched call (repeat sends)",
-    "c5": "C5 (BASELINE configs[4]) per GPU: 2^20 uint64 keys spread over 2^64 (splitmix64) + "
-          "embedding rows dim=128 f32 (512 MiB, one min/max per array), chain [KEY_CACHING, "
-          "FIXING_FLOAT num_bytes={nb}{cmp}], repeat send (key cache hit)",
+          "EvenDivide({servers}) server ranges (servers in contiguous blocks per rank), "
+          "per-(stream, server) [KEY_CACHING, FIXING_FLOAT num_bytes={nb}], cross-range slices spilled in "
+          "one all-to-all-v per step (RCCL), repeat sends (key cache hit)",
+    "c1": "C1 (BASELINE configs[0]) on the device: the ctr example's minibatch "
+          "(example/linear/ctr/online_l1lr.conf:36-53) for {streams} concurrent streams of {m} sorted unique "
+          "keys: pull request (keys, [KEY_CACHING, FIXING_FLOAT num_bytes={nb}]), pull response (keys elided "
+          "+ f32 weights), push (keys elided + f32 gradients, [KEY_CACHING(clear_cache_if_done), "
+          "FIXING_FLOAT num_bytes={nb}]), each batched over the streams",
+    "c5": "C5 (BASELINE configs[4]) per GPU: one stream of {m} uint64 keys spread over 2^64 "
+          "(splitmix64) + embedding rows dim=128 f32, sliced at the EvenDivide({servers}) server ranges "
+          "(k = 128 values per key), per-(stream, server) [KEY_CACHING, FIXING_FLOAT num_bytes={nb}{cmp}], "
+          "cross-range slices spilled in one all-to-all-v per step, repeat sends (key cache hit)",
 }
 
 
@@ -70,92 +87,52 @@ def splitmix64_keys(m: int, seed: int):
     return np.unique(z)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--n", type=int, default=1 << 27, help="values per message (per GPU)")
+    ap.add_argument("--n", type=int, default=1 << 28, help="c2: values per message (per GPU)")
     ap.add_argument("--nb", type=int, default=1, help="FIXING_FLOAT num_bytes")
     ap.add_argument("--bufs", type=int, default=3, help="distinct messages cycled through")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
-    ap.add_argument("--streams", type=int, default=64, help="c4: push streams in total")
-    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c3miss", "c4", "c5"],
-                    help="c2: dense f32 values (default, the headline); c3: 10M sorted uint64 "
-                         "keys from [0,1e9) + f32 values, [KEY_CACHING, FIXING_FLOAT] repeat "
-                         "sends (cache hits); c3miss: same with clear_cache_if_done (every send "
-                         "a miss)")
-    ap.add_argument("--m", type=int, default=None, help="keys per message (c3: 10M, c5: 2^20)")
+    ap.add_argument("--no-128m", action="store_true", help="c2: skip the configs[1] 2^27 measurement")
+    ap.add_argument("--streams", type=int, default=64, help="c1/c4: push streams in total")
+    ap.add_argument("--servers", type=int, default=8, help="c4/c5: server key ranges (>= N)")
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c3miss", "c4", "c5"])
+    ap.add_argument("--m", type=int, default=None, help="keys per message (c1 1e5, c3 10M, c4 2^21, c5 2^20)")
     ap.add_argument("--compress", action="store_true", help="append COMPRESSING to the chain (c5)")
-    return ap.parse_args()
+    ap.add_argument("--launch-check", action="store_true",
+                    help="start the ranks and the process group only (no GPU work); for CPU tests")
+    return ap.parse_args(argv)
 
 
-def cpu_baseline(n_sample: int, nb: int, seconds: float, config: str = "c2"):
-    import ctypes as C
-
-    import numpy as np
-
-    import oracle
-    x = np.random.default_rng(1).standard_normal(n_sample).astype(np.float32)
-    keys = None
-    if config != "c2":  # C3 sample: sorted unique keys from [0, 1e9), KEY_CACHING first
-        keys = np.unique(np.random.default_rng(3).integers(0, 10**9, n_sample + n_sample // 8,
-                                                            dtype=np.uint64))[:n_sample]
-        keys = np.ascontiguousarray(keys[:x.size])
-        x = x[:keys.size]
-    kind = "port"
-    try:
-        R = oracle.Ref()
-        kind = "reference"
-    except Exception:
-        R = None
-    reps, t = 0, 0.0
-    if R is not None:
-        L = R.lib
-        R.set_time(12345)
-        snd, rcv = L.psref_node_new(), L.psref_node_new()
-        while t < seconds or reps == 0:
-            m = R.msg_new(request=True, push=True, key_range=(0, 10**9))
-            if keys is not None:
-                L.psref_msg_set_key(m, keys.ctypes.data_as(C.c_void_p), keys.nbytes, 8)
-                kf = L.psref_msg_add_filter(m, 1)
-                L.psref_fc_set_clear_cache(m, kf, int(config == "c3miss"))
-            L.psref_msg_add_value(m, x.ctypes.data_as(C.c_void_p), x.nbytes, 9)
-            fi = L.psref_msg_add_filter(m, 3)
-            L.psref_fc_set_num_bytes(m, fi, nb)
-            t0 = time.perf_counter()
-            assert L.psref_node_encode(snd, m) == 0
-            w = L.psref_msg_clone(m)
-            assert L.psref_node_decode(rcv, w) == 0
-            t += time.perf_counter() - t0
-            L.psref_msg_free(w)
-            L.psref_msg_free(m)
-            reps += 1
-    else:
-        P = oracle.Port()
-        while t < seconds or reps == 0:
-            t0 = time.perf_counter()
-            st, codes, mn, mx = P.ff_encode(x, nb, 12345)
-            P.ff_decode(codes, nb, mn, mx)
-            t += time.perf_counter() - t0
-            reps += 1
-    payload = x.nbytes + (keys.nbytes if keys is not None else 0)
-    chain = "FIXING_FLOAT" if keys is None else "KEY_CACHING+FIXING_FLOAT"
-    return {
-        "value": round(reps * payload / t / GIB, 4),
-        "unit": "GiB/s",
-        "cores": 1,
-        "kind": kind,
-        "sample": f"{reps} x {chain}(nb={nb}) encode+decode of 2^{n_sample.bit_length() - 1} f32 "
-                  f"({payload >> 20} MiB payload), single-threaded as the reference's filters run, "
-                  f"{t:.1f} s CPU",
-        "cpu_model": _cpu_model(),
-        "nproc": os.cpu_count(),
-    }
+# --------------------------------------------------------------- launcher --
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
 
 
+def launch(args) -> int:
+    """Start args.gpus rank processes (one per GPU), the way torchrun would;
+    this parent never touches the GPU.  Returns the worst exit code."""
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
+# ----------------------------------------------------------- CPU baseline --
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -166,6 +143,114 @@ def _cpu_model():
     return "unknown"
 
 
+def _run_tasks(tasks, threads: int, seconds: float):
+    """Run the list of task callables (one step of the sample) repeatedly on
+    `threads` host threads until `seconds` of wall time; returns (reps, t)."""
+    from concurrent.futures import ThreadPoolExecutor
+    reps, t = 0, 0.0
+    with ThreadPoolExecutor(max_workers=threads) as ex:
+        while t < seconds or reps == 0:
+            t0 = time.perf_counter()
+            list(ex.map(lambda f: f(), tasks))
+            t += time.perf_counter() - t0
+            reps += 1
+    return reps, t
+
+
+def cpu_baseline(args, nb: int):
+    """The C restatement of the reference's filters (oracle/psf_port.c) on
+    host cores, over a bounded sample of the configured workload."""
+    import numpy as np
+
+    import oracle
+    P = oracle.Port()
+    rng = np.random.default_rng(1)
+    cfg, seed = args.config, 12345
+    tasks, payload, threads, what = [], 0, 1, ""
+
+    def ff_rt(x):
+        def f():
+            st, codes, mn, mx = P.ff_encode(x, nb, seed)
+            if args.compress:
+                c = P.snappy_compress(codes)
+                P.snappy_uncompress(c, cap=codes.size + 64)
+            P.ff_decode(codes, nb, mn, mx)
+        return f
+
+    def kc_ff(keys, x, decode_crc):
+        rt = ff_rt(x)
+
+        def f():
+            P.key_signature(keys)   # KEY_CACHING encode: CRC of the first <= 2 KiB
+            if decode_crc:
+                P.key_signature(keys)  # decode checks the CRC when keys travel
+            rt()
+        return f
+
+    if cfg == "c2":
+        x = rng.standard_normal(1 << 24).astype(np.float32)
+        tasks, payload = [ff_rt(x)], x.nbytes
+        what = f"FIXING_FLOAT(nb={nb}) encode+decode of 2^24 f32 (64 MiB)"
+    elif cfg in ("c3", "c3miss"):
+        m = 1 << 22
+        keys = np.unique(np.random.default_rng(3).integers(0, 10**9, m + m // 8, dtype=np.uint64))[:m]
+        x = rng.standard_normal(keys.size).astype(np.float32)
+        tasks, payload = [kc_ff(keys, x, cfg == "c3miss")], keys.nbytes + x.nbytes
+        what = f"KEY_CACHING+FIXING_FLOAT(nb={nb}) of 2^22 keys from [0,1e9) + f32"
+    elif cfg == "c1":
+        m = args.m or 100_000
+        ns = args.streams
+        for s in range(ns):
+            keys = np.unique(np.random.default_rng(100 + s).integers(0, 10**9, m + m // 8, dtype=np.uint64))[:m]
+            w = rng.standard_normal(keys.size).astype(np.float32)
+            x = rng.standard_normal(keys.size).astype(np.float32)
+            sig = lambda k=keys: P.key_signature(k)  # noqa: E731
+            # pull request: CRC on encode and on decode (keys travel); pull
+            # response and push: CRC on encode (hit, keys elided) + FF round trip
+            tasks += [sig, sig, kc_ff(keys, w, False), kc_ff(keys, x, False)]
+            payload += 8 * keys.size + 2 * (keys.nbytes + x.nbytes)
+        what = (f"{ns} ctr minibatches (pull request, pull response, push; [KEY_CACHING, "
+                f"FIXING_FLOAT(nb={nb})]) of {m} keys + f32, one core (the reference's filters run "
+                f"serialised per Customer)")
+    else:  # c4 / c5: the per-(stream, server) slices, one thread per slice up to 16
+        from parameter_server_amd import shard
+        ranges = shard.server_ranges(args.servers)
+        bounds = np.array([r[0] for r in ranges] + [ranges[-1][1]], dtype=np.uint64)
+        if cfg == "c4":
+            m, dim = args.m or (1 << 21), 1
+            nstreams = min(args.streams, CPU_THREADS_MAX)
+        else:
+            m, dim = min(args.m or (1 << 20), 1 << 18), 128
+            nstreams = 1
+        for s in range(nstreams):
+            keys = splitmix64_keys(m, 4 + s)
+            x = rng.standard_normal(keys.size * dim).astype(np.float32)
+            pos = np.searchsorted(keys, bounds)
+            for d in range(args.servers):
+                lo, hi = int(pos[d]), int(pos[d + 1])
+                if hi > lo:
+                    tasks.append(kc_ff(keys[lo:hi], x[lo * dim:hi * dim], False))
+            payload += keys.nbytes + x.nbytes
+        what = (f"{nstreams} stream(s) of {m} keys (dim {dim}) sliced over {args.servers} servers, "
+                f"[KEY_CACHING, FIXING_FLOAT(nb={nb}){', COMPRESSING' if args.compress else ''}] per slice")
+    if cfg in ("c4", "c5"):
+        try:
+            avail = len(os.sched_getaffinity(0))
+        except AttributeError:
+            avail = os.cpu_count() or 1
+        threads = max(1, min(len(tasks), CPU_THREADS_MAX, avail))
+    reps, t = _run_tasks(tasks, threads, args.cpu_seconds)
+    return {
+        "value": round(reps * payload / t / GIB, 4),
+        "unit": "GiB/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{reps} x {what}, {threads} thread(s), {t:.1f} s",
+        "cpu_model": _cpu_model(),
+        "nproc": os.cpu_count(),
+    }
+
+
 def pmc_traffic(kernel: str, n: int, nb: int, config: str):
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
@@ -173,17 +258,141 @@ def pmc_traffic(kernel: str, n: int, nb: int, config: str):
     except (OSError, ValueError):
         return None
     e = d.get(kernel)
-    # profiles/pmc_traffic.json holds the C2 passes (tools/gpu_profile.sh)
-    if config != "c2" or not e or e.get("n") != n or e.get("nb") != nb:
+    if not e or e.get("config", "c2") != config or e.get("n") != n or e.get("nb") != nb:
         return None
     return e.get("hbm_bytes_per_launch")
 
 
+# ------------------------------------------------------------- workloads --
+def build_workload(args, F, ctx, rank, world, dev, g, n):
+    """Returns (run(k), payload bytes per step on this rank, n values, extra)."""
+    import torch
+
+    from parameter_server_amd import COMPRESSING, FIXING_FLOAT, KEY_CACHING
+    nb = args.nb
+    if args.config == "c1":
+        # the ctr example's async SGD minibatch (async_sgd.h:229-296, CS-1/CS-2
+        # of SURVEY.md): per stream and step a pull request (keys,
+        # pull_filter [KEY_CACHING, FIXING_FLOAT nb=1]), the server's pull
+        # response (keys elided on the cache hit + weights) and the push
+        # (keys elided + gradients, push_filter [KEY_CACHING(clear_cache_if_done),
+        # FIXING_FLOAT nb=1]); each of the three runs batched over all streams
+        m = args.m or 100_000
+        S = args.streams
+        wk = [F.RemoteNode(ctx) for _ in range(S)]  # worker's node for its server
+        sv = [F.RemoteNode(ctx) for _ in range(S)]  # server's node for the worker
+        req, resp, push = [], [], []
+        for sid in range(S):
+            keys = torch.sort(torch.unique(torch.randint(0, 10**9, (m + m // 8,), device=dev, generator=g))[:m])[0]
+            for lst, request, is_push, vals, clear in ((req, True, False, False, None),
+                                                       (resp, False, False, True, None),
+                                                       (push, True, True, True, True)):
+                t = F.Message(request=request, push=is_push, key_channel=sid, key_range=(0, 10**9))
+                t.set_key(keys)
+                if vals:
+                    t.add_value(torch.randn(m, device=dev, generator=g, dtype=torch.float32))
+                t.add_filter(KEY_CACHING, clear_cache_if_done=clear)
+                t.add_filter(FIXING_FLOAT, num_bytes=nb)
+                lst.append(t)
+        tmpls, snd, rcv = req + resp + push, wk + sv + wk, sv + wk + sv
+
+        def run(k):
+            F.RemoteNode.roundtrip_many(snd, rcv, tmpls, k, phase_end=[S, 2 * S, 3 * S])
+        return run, 32 * m * S, 2 * m * S, {}
+    if args.config in ("c4", "c5"):
+        # SURVEY.md §8(d) C4 / C5: streams sliced at the server ranges, encoded
+        # per destination server, spilled (one all-to-all-v) and decoded
+        from parameter_server_amd import shard
+        if args.servers < world:
+            raise SystemExit(f"--servers {args.servers} < {world} ranks")
+        ex = shard.SpillExchange(ctx, device=dev) if world > 1 else None
+        router = shard.PushRouter(ctx, shard.server_ranges(args.servers), rank, world, ex)
+        streams, nloc, payload = {}, 0, 0
+        if args.config == "c4":
+            m, dim, sids = args.m or (1 << 21), 1, range(rank, args.streams, world)
+        else:
+            m, dim, sids = args.m or (1 << 20), 128, [rank]
+        for sid in sids:
+            keys = torch.from_numpy(splitmix64_keys(m, 4 + sid).view("int64")).to(dev)
+            t = F.Message(request=True, push=True, key_channel=sid, key_range=shard.KEY_ALL)
+            t.set_key(keys)
+            t.add_value(torch.randn(keys.numel() * dim, device=dev, generator=g, dtype=torch.float32))
+            t.add_filter(KEY_CACHING)
+            t.add_filter(FIXING_FLOAT, num_bytes=nb)
+            if args.compress:
+                t.add_filter(COMPRESSING)
+            streams[sid] = t
+            nloc += keys.numel() * dim
+            payload += keys.numel() * (8 + 4 * dim)
+
+        def run(k):
+            for _ in range(k):
+                router.step(streams)
+        return run, payload, nloc, {"router": router}
+    worker, server = F.RemoteNode(ctx), F.RemoteNode(ctx)
+    tmpls = []
+    if args.config == "c2":
+        # this rank's shard of the key range (range.h:100-107 EvenDivide),
+        # pre-placed.  Consecutive steps use different messages (args.bufs
+        # distinct arrays whose total exceeds the 256 MiB Infinity Cache), so no
+        # step reads data a previous step left on chip.
+        for _ in range(args.bufs):
+            t = F.Message(request=True, push=True, key_channel=0)
+            t.add_value(torch.randn(n, device=dev, generator=g, dtype=torch.float32))
+            t.add_filter(FIXING_FLOAT, num_bytes=nb)
+            tmpls.append(t)
+        payload = 4 * n  # key bytes 0 (dense values), value bytes 4n
+    else:
+        # C3: m sorted unique keys sampled without replacement from [0, 1e9)
+        # (SURVEY.md §8(d)), one f32 value per key; the worker's push stream
+        # repeats the key set (KEY_CACHING hit) or clears it after every
+        # send (c3miss: clear_cache_if_done on push, key_caching.h:30-33)
+        m = args.m or 10_000_000
+        keys = torch.unique(torch.randint(0, 10**9, (m + m // 8,), device=dev, generator=g))
+        keys = torch.sort(keys[torch.randperm(keys.numel(), device=dev, generator=g)[:m]])[0]
+        n = m
+        for _ in range(args.bufs):
+            t = F.Message(request=True, push=True, key_channel=0, key_range=(0, 10**9))
+            t.set_key(keys)
+            t.add_value(torch.randn(m, device=dev, generator=g, dtype=torch.float32))
+            t.add_filter(KEY_CACHING, clear_cache_if_done=(args.config == "c3miss"))
+            t.add_filter(FIXING_FLOAT, num_bytes=nb)
+            tmpls.append(t)
+        payload = 12 * m
+
+    def run(k):
+        worker.roundtrip(server, tmpls, k)
+    return run, payload, n, {}
+
+
+def timed(run, steps, world, dist, ctx, prof_kernel=None, stride=1):
+    import torch
+    if prof_kernel:
+        ctx.profile(True, kernels=[prof_kernel], stride=stride)
+    ctx.profile_reset()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(steps)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    prof = ctx.profile_read()
+    ctx.profile(False)
+    return elapsed, prof
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch(args))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
 
     import torch
     import torch.distributed as dist
@@ -193,14 +402,30 @@ def main():
     backend = os.environ.get("PSF_DIST_BACKEND", "nccl")
     if os.environ.get("PSF_SAME_GPU") == "1":
         local = 0
-    torch.cuda.set_device(local)
+    if not args.launch_check:
+        torch.cuda.set_device(local)
     if world > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
         else:
             dist.init_process_group(backend)
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"bench.py: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
+    world_pg = dist.get_world_size() if world > 1 else 1
+    backend_pg = dist.get_backend() if world > 1 else "none"
 
-    from parameter_server_amd import COMPRESSING, FIXING_FLOAT, KEY_CACHING
+    if args.launch_check:  # plumbing only: process group, barrier, max-reduce, one JSON line
+        if world > 1:
+            t = torch.tensor([float(rank)], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dist.barrier()
+        if rank == 0:
+            print(json.dumps({"launch_check": True, "n_gpus": world_pg, "world_size": world_pg,
+                              "backend": backend_pg, "config": {"workload": args.config}}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
     from parameter_server_amd import filter as F
 
     n, nb = args.n, args.nb
@@ -208,104 +433,8 @@ def main():
     g = torch.Generator(device=dev)
     g.manual_seed(1 + rank)
     ctx = F.Context(local)
-    worker, server = F.RemoteNode(ctx), F.RemoteNode(ctx)
     F.set_clock(12345)  # FIXING_FLOAT seed (time(NULL) in the reference)
-    tmpls = []
-    router = None
-    streams_batch = None
-    if args.config == "c1":
-        # async SGD pushes (async_sgd.h:264-296): every minibatch stream pushes
-        # its ~10^5 keys with gradients, [KEY_CACHING, FIXING_FLOAT nb=1]
-        m = args.m or 100_000
-        nstreams = args.streams
-        for sid in range(nstreams):
-            keys = torch.unique(torch.randint(0, 10**9, (m + m // 8,), device=dev, generator=g))[:m]
-            t = F.Message(request=True, push=True, key_channel=sid, key_range=(0, 10**9))
-            t.set_key(torch.sort(keys)[0])
-            t.add_value(torch.randn(m, device=dev, generator=g, dtype=torch.float32))
-            t.add_filter(KEY_CACHING)
-            t.add_filter(FIXING_FLOAT, num_bytes=nb)
-            tmpls.append(t)
-        streams_batch = ([F.RemoteNode(ctx) for _ in tmpls], [F.RemoteNode(ctx) for _ in tmpls])
-        n = m * nstreams
-        payload = 12 * n
-    elif args.config == "c4":
-        # stream s lives on rank s % N; every step slices,
-        # encodes per destination server, spills and decodes (shard.PushRouter)
-        from parameter_server_amd import shard
-        m = args.m or (1 << 21)
-        ex = shard.SpillExchange(device=dev) if world > 1 else None
-        router = shard.PushRouter(ctx, shard.server_ranges(world), rank, world, ex)
-        streams = {}
-        nloc = 0
-        for sid in range(rank, args.streams, world):
-            keys = torch.from_numpy(splitmix64_keys(m, 4 + sid).view("int64")).to(dev)
-            t = F.Message(request=True, push=True, key_channel=sid, key_range=shard.KEY_ALL)
-            t.set_key(keys)
-            t.add_value(torch.randn(keys.numel(), device=dev, generator=g, dtype=torch.float32))
-            t.add_filter(KEY_CACHING)
-            t.add_filter(FIXING_FLOAT, num_bytes=nb)
-            streams[sid] = t
-            nloc += keys.numel()
-        n = nloc
-        payload = 12 * nloc  # this rank's streams: 8 key + 4 value bytes per key
-    elif args.config == "c2":
-        # this rank's shard of the key range (range.h:100-107 EvenDivide),
-        # pre-placed.  Consecutive steps use different messages (args.bufs
-        # distinct arrays whose total exceeds the 256 MiB Infinity Cache), so no
-        # step reads data a previous step left on chip.
-        xs = [torch.randn(n, device=dev, generator=g, dtype=torch.float32) for _ in range(args.bufs)]
-        for x in xs:
-            t = F.Message(request=True, push=True, key_channel=0)
-            t.add_value(x)
-            t.add_filter(FIXING_FLOAT, num_bytes=nb)
-            tmpls.append(t)
-        payload = 4 * n  # key bytes 0 (dense values), value bytes 4n
-    elif args.config == "c5":
-        m = args.m or (1 << 20)
-        keys = torch.from_numpy(splitmix64_keys(m, 4 + rank).view("int64")).to(dev)
-        m = keys.numel()
-        n = m * 128
-        xs = [torch.randn(n, device=dev, generator=g, dtype=torch.float32) for _ in range(args.bufs)]
-        for x in xs:
-            t = F.Message(request=True, push=True, key_channel=0)
-            t.set_key(keys)
-            t.add_value(x)
-            t.add_filter(KEY_CACHING)
-            t.add_filter(FIXING_FLOAT, num_bytes=nb)
-            if args.compress:
-                t.add_filter(COMPRESSING)
-            tmpls.append(t)
-        payload = 8 * m + 4 * n
-    else:
-        # C3: m sorted unique keys sampled without replacement from [0, 1e9)
-        # (SURVEY.md §8(d)), one f32 value per key; the worker's push stream
-        # repeats the key set (KEY_CACHING hit) or clears it after every
-        # send (c3miss: clear_cache_if_done on push, key_caching.h:30-33)
-        m = args.m or 10_000_000
-        keys = torch.unique(torch.randint(0, 10**9, (m + m // 8,), device=dev, generator=g))
-        keys = torch.sort(keys[torch.randperm(keys.numel(), device=dev, generator=g)[:m]])[0]
-        assert keys.numel() == m
-        n = m
-        xs = [torch.randn(m, device=dev, generator=g, dtype=torch.float32) for _ in range(args.bufs)]
-        for x in xs:
-            t = F.Message(request=True, push=True, key_channel=0, key_range=(0, 10**9))
-            t.set_key(keys)
-            t.add_value(x)
-            t.add_filter(KEY_CACHING, clear_cache_if_done=(args.config == "c3miss"))
-            t.add_filter(FIXING_FLOAT, num_bytes=nb)
-            tmpls.append(t)
-        payload = 12 * m  # 8m key bytes + 4m value bytes
-    tmpl = tmpls
-
-    def run(k):
-        if router is not None:
-            for _ in range(k):
-                router.step(streams)
-        elif streams_batch is not None:
-            F.RemoteNode.roundtrip_many(streams_batch[0], streams_batch[1], tmpl, k)
-        else:
-            worker.roundtrip(server, tmpl, k)
+    run, payload, n, extra = build_workload(args, F, ctx, rank, world, dev, g, n)
 
     run(args.warmup)
     torch.cuda.synchronize()
@@ -316,7 +445,7 @@ def main():
     if not args.no_profile:
         ctx.profile(True)
         ctx.profile_reset()
-        run(min(args.steps, 20))
+        run(min(args.steps, 10))
         torch.cuda.synchronize()
         diag = ctx.profile_read()
         ctx.profile(False)
@@ -326,27 +455,26 @@ def main():
     # in the many-small-message configs only every 8th launch of it, so the
     # event pairs do not dominate a step of short kernels
     stride = 8 if args.config in ("c1", "c4") else 1
-    if dom:
-        ctx.profile(True, kernels=[dom], stride=stride)
-    ctx.profile_reset()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    run(args.steps)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    prof = ctx.profile_read()
-    ctx.profile(False)
+    router = extra.get("router")
+    if router is not None and router.exchange is not None:
+        router.exchange.bytes_sent = 0
+    elapsed, prof = timed(run, args.steps, world, dist, ctx, dom, stride)
+    spill = router.exchange.bytes_sent if router is not None and router.exchange is not None else 0
 
-    if world > 1:
-        t = torch.tensor([elapsed], device=f"cuda:{local}" if backend == "nccl" else "cpu", dtype=torch.float64)
+    def max_over_ranks(v):
+        if world == 1:
+            return v
+        t = torch.tensor([v], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        return float(t.item())
 
-    value = world * args.steps * payload / elapsed / GIB
+    elapsed = max_over_ranks(elapsed)
+    total_payload = payload
+    if world > 1:
+        t = torch.tensor([float(payload)], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
+        dist.all_reduce(t)
+        total_payload = float(t.item())
+    value = args.steps * total_payload / elapsed / GIB
 
     roofline = None
     if dom and dom in prof:
@@ -354,11 +482,10 @@ def main():
         per_launch_bytes = alg / launches
         avg_s = ms / launches / 1e3
         achieved = per_launch_bytes / avg_s / 1e9
-        traffic = pmc_traffic(dom, n, nb, args.config)
         roofline = {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": traffic,
+            "traffic": pmc_traffic(dom, n, nb, args.config),
             "kernel": dom,
             "avg_us": round(avg_s * 1e6, 2),
             "alg_bytes_per_launch": int(per_launch_bytes),
@@ -371,16 +498,30 @@ def main():
                         for k, v in diag.items()},
         }
 
+    # BASELINE configs[1] (128M values) measured in the same run
+    also = None
+    if args.config == "c2" and not args.no_128m and n != (1 << 27):
+        a2 = argparse.Namespace(**vars(args))
+        a2.n = 1 << 27
+        del run
+        run2, payload2, _, _ = build_workload(a2, F, ctx, rank, world, dev, g, 1 << 27)
+        run2(args.warmup)
+        el2, _ = timed(run2, args.steps, world, dist, ctx)
+        el2 = max_over_ranks(el2)
+        also = {"n_values_per_gpu": 1 << 27, "value": round(world * args.steps * payload2 / el2 / GIB, 2),
+                "ms_per_step": round(el2 / args.steps * 1e3, 4)}
+
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config not in ("c1", "c4", "c5"):
-        cpu = cpu_baseline(1 << 24 if args.config == "c2" else 1 << 22, nb, args.cpu_seconds, args.config)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, nb)
 
     if rank == 0:
+        m_default = {"c1": 100_000, "c4": 1 << 21, "c5": 1 << 20}.get(args.config, 1 << 21)
         line = {
             "metric": "GiB/s key-value payload through filter encode+decode, device-resident",
             "value": round(value, 2),
             "unit": "GiB/s",
-            "n_gpus": world,
+            "n_gpus": world_pg,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
@@ -395,19 +536,25 @@ def main():
                         args.config, "; sorted unique uint64 keys from [0,1e9)"),
             "config": {
                 "workload": WORKLOADS[args.config].format(nb=nb, cmp=", COMPRESSING" if args.compress else "",
-                                                          streams=args.streams,
-                                                          m=args.m or (100_000 if args.config == "c1" else 1 << 21)),
+                                                          streams=args.streams, servers=args.servers,
+                                                          m=args.m or m_default),
                 "n_values_per_gpu": n,
                 "payload_bytes_per_step_per_gpu": payload,
                 "value_type": "float32",
                 "num_bytes": nb,
+                "world_size": world_pg,
+                "backend": backend_pg,
                 "parallelism": f"server key-range shards x{world} (EvenDivide), " + (
-                    "cross-range spill: one all-to-all-v per step" if args.config == "c4" and world > 1
-                    else "no data-path collective"),
+                    f"{args.servers} servers, cross-range spill: one all-to-all-v per step"
+                    if args.config in ("c4", "c5") and world > 1 else "no data-path collective"),
             },
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
+        if spill:
+            line["config"]["spill_bytes_per_step_rank0"] = spill // max(args.steps, 1)
+        if also:
+            line["config_128M"] = also
         print(json.dumps(line), flush=True)
 
     if world > 1:

@@ -223,6 +223,10 @@ int psf_msgs_slice(psf_context* ctx, const psf_message* const* msgs, int nmsgs, 
  * *out (may be NULL).  Used by bench.py so no Python runs per message. */
 int psf_node_roundtrip(psf_node* snd, psf_node* rcv, const psf_message* const* tmpls, int ntmpl,
                        int iters, psf_message** out);
+/* The same, also returning the last encoded message as it went on the wire
+ * (*enc_out) next to the decoded one (*dec_out); either may be NULL. */
+int psf_node_roundtrip_ex(psf_node* snd, psf_node* rcv, const psf_message* const* tmpls, int ntmpl,
+                          int iters, psf_message** enc_out, psf_message** dec_out);
 
 /* ---- server-side consumers ------------------------
  * What the receiving server does with a decoded message, fused with the
@@ -310,6 +314,44 @@ int psf_nodes_decode(psf_node* const* nodes, psf_message* const* msgs, int n);
  * copies of tmpls[0..n) on snd[0..n), deliver, decode on rcv[0..n). */
 int psf_nodes_roundtrip(psf_node* const* snd, psf_node* const* rcv, const psf_message* const* tmpls, int n,
                         int iters);
+/* ... in phases: messages [phase_end[p-1], phase_end[p]) are encoded, delivered
+ * and decoded before phase p+1 starts (phase_end ascending, last = n; NULL =
+ * one phase), so a request / response / push sequence runs in the
+ * reference's order (the ctr example's pull request, pull response and push
+ * of a minibatch, async_sgd.h:229-296); returning the last iteration's
+ * encoded and decoded messages, message i in enc_out[i] / dec_out[i] (arrays
+ * of n, or NULL). */
+int psf_nodes_roundtrip_ex(psf_node* const* snd, psf_node* const* rcv, const psf_message* const* tmpls, int n,
+                           const int* phase_end, int nphases, int iters, psf_message** enc_out,
+                           psf_message** dec_out);
+
+/* ---- cross-range spill (multi-GPU split, one all-to-all-v per step) -----
+ * Replaces the reference's per-server send loop (src/system/executor.cc:
+ * 135-146), each slice one ZeroMQ multipart message [Task][key][value...]
+ * (Van::Send src/system/van.cc:122-191, Van::Recv :193-269): every slice a rank
+ * sends in a step is laid out in ONE send buffer, one segment per destination
+ * rank, for a single all-to-all-v (RCCL over xGMI).  Segment = [meta][payload],
+ * both multiples of 256 bytes: meta holds one record per message (server id,
+ * the Task frame, frame lengths), payload the key / value frames at 256-byte
+ * aligned offsets.
+ *
+ * psf_spill_pack: message i goes to rank dest[i], addressed to server
+ * server[i]; sizes[2r] / sizes[2r+1] = meta / payload bytes of rank r's
+ * segment (serialises the Tasks: resolves side-info a batched encode left on
+ * the device).  psf_spill_fill writes the send buffer (sum of sizes bytes; HBM
+ * on a device context) with one gather launch on the context's stream.
+ * psf_spill_unpack rebuilds the received messages (segments of sources
+ * 0..world-1 back to back, sizes_in as their senders reported them) over
+ * recvbuf without copying the frames (keep recvbuf alive); servers[i] is the
+ * server message i is addressed to; *n = message count (PSF_ERR_ARG when it
+ * exceeds cap). */
+typedef struct psf_spill psf_spill;
+int psf_spill_pack(psf_context* ctx, psf_message* const* msgs, const int* dest, const int* server, int n,
+                   int world, int64_t* sizes, psf_spill** out);
+int psf_spill_fill(psf_spill* plan, void* sendbuf);
+int psf_spill_destroy(psf_spill* plan);
+int psf_spill_unpack(psf_context* ctx, const void* recvbuf, int world, const int64_t* sizes_in,
+                     psf_message** outs, int* servers, int cap, int* n);
 
 /* ---- launch profiler (HIP events on the launch stream) ----------------- */
 #define PSF_K_MINMAX 0

@@ -90,6 +90,9 @@ SIGNATURES = {
     "psf_fc_uncompressed": ([vp, C.c_int, C.c_int, C.POINTER(u64)], C.c_int),
     "psf_fc_add_uncompressed": ([vp, C.c_int, u64], C.c_int),
     "psf_node_roundtrip": ([vp, vp, C.POINTER(vp), C.c_int, C.c_int, C.POINTER(vp)], C.c_int),
+    "psf_node_roundtrip_ex": ([vp, vp, C.POINTER(vp), C.c_int, C.c_int, C.POINTER(vp), C.POINTER(vp)], C.c_int),
+    "psf_nodes_roundtrip_ex": ([C.POINTER(vp), C.POINTER(vp), C.POINTER(vp), C.c_int, PI, C.c_int, C.c_int,
+                                C.POINTER(vp), C.POINTER(vp)], C.c_int),
     "psf_range_even_divide": ([u64, u64, u64, u64, C.POINTER(u64), C.POINTER(u64)], C.c_int),
     "psf_msg_slice": ([vp, vp, C.POINTER(u64), C.c_int, C.c_int, C.POINTER(vp), PI], C.c_int),
     "psf_msgs_slice": ([vp, C.POINTER(vp), C.c_int, C.POINTER(u64), C.c_int, C.c_int, C.POINTER(vp), PI],
@@ -114,6 +117,11 @@ SIGNATURES = {
     "psf_nodes_encode": ([C.POINTER(vp), C.POINTER(vp), C.c_int], C.c_int),
     "psf_nodes_decode": ([C.POINTER(vp), C.POINTER(vp), C.c_int], C.c_int),
     "psf_nodes_roundtrip": ([C.POINTER(vp), C.POINTER(vp), C.POINTER(vp), C.c_int, C.c_int], C.c_int),
+    "psf_spill_pack": ([vp, C.POINTER(vp), PI, PI, C.c_int, C.c_int, C.POINTER(C.c_int64), C.POINTER(vp)],
+                       C.c_int),
+    "psf_spill_fill": ([vp, vp], C.c_int),
+    "psf_spill_destroy": ([vp], C.c_int),
+    "psf_spill_unpack": ([vp, vp, C.c_int, C.POINTER(C.c_int64), C.POINTER(vp), PI, C.c_int, PI], C.c_int),
     "psf_profile_enable": ([vp, C.c_int], C.c_int),
     "psf_profile_stride": ([vp, C.c_int], C.c_int),
     "psf_profile_reset": ([vp], C.c_int),

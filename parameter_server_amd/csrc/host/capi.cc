@@ -10,6 +10,7 @@
 #include "kvstore.h"
 #include "slice.h"
 #include "snappy_host.h"
+#include "spill.h"
 #include "wire.h"
 
 struct psf_context { psf::Context* impl; };
@@ -181,6 +182,9 @@ int psf_snappy_compress(psf_context* ctx, const void* d_in, size_t n, void* d_ou
     if (st != PSF_OK) return st;
     c.wait_ticket(0, ticket);
     *out_len = c.pub_host(0)->size;
+    // the size is published before every fragment has placed its bytes:
+    // "synchronous" means the stream in d_out is complete on return
+    c.sync();
     return PSF_OK;
   });
 }
@@ -505,11 +509,12 @@ int psf_msgs_slice(psf_context* ctx, const psf_message* const* msgs, int nmsgs, 
   });
 }
 
-int psf_node_roundtrip(psf_node* snd, psf_node* rcv, const psf_message* const* tmpls, int ntmpl,
-                       int iters, psf_message** out) {
+int psf_node_roundtrip_ex(psf_node* snd, psf_node* rcv, const psf_message* const* tmpls, int ntmpl,
+                          int iters, psf_message** enc_out, psf_message** dec_out) {
   return guarded([&] {
     if (!snd || !rcv || !tmpls || ntmpl <= 0 || iters < 0) return PSF_ERR_ARG;
-    psf_message* last = nullptr;
+    psf_message* last_enc = nullptr;
+    psf_message* last_dec = nullptr;
     psf::RemoteNode* s = snd->impl;
     psf::RemoteNode* r = rcv->impl;
     for (int i = 0; i < iters; ++i) {
@@ -519,12 +524,20 @@ int psf_node_roundtrip(psf_node* snd, psf_node* rcv, const psf_message* const* t
       psf::Message w = m;             // delivered copy (van: Task frame + data frames)
       psf::Message* wp = &w;
       psf::decode_batch(&r, &wp, 1);  // = DecodeMessage
-      if (out && i == iters - 1) last = new psf_message{w};
+      if (i == iters - 1) {
+        if (enc_out) last_enc = new psf_message{m};
+        if (dec_out) last_dec = new psf_message{w};
+      }
     }
     s->ctx()->check_ranges();  // CHECK_GT(bin, 0) of the computed ranges
-    if (out) *out = last;
+    if (enc_out) *enc_out = last_enc;
+    if (dec_out) *dec_out = last_dec;
     return PSF_OK;
   });
+}
+int psf_node_roundtrip(psf_node* snd, psf_node* rcv, const psf_message* const* tmpls, int ntmpl,
+                       int iters, psf_message** out) {
+  return psf_node_roundtrip_ex(snd, rcv, tmpls, ntmpl, iters, nullptr, out);
 }
 
 int psf_nodes_encode(psf_node* const* nodes, psf_message* const* msgs, int n) {
@@ -555,32 +568,105 @@ int psf_nodes_decode(psf_node* const* nodes, psf_message* const* msgs, int n) {
     return PSF_OK;
   });
 }
-int psf_nodes_roundtrip(psf_node* const* snd, psf_node* const* rcv, const psf_message* const* tmpls, int n,
-                        int iters) {
+int psf_nodes_roundtrip_ex(psf_node* const* snd, psf_node* const* rcv, const psf_message* const* tmpls, int n,
+                           const int* phase_end, int nphases, int iters, psf_message** enc_out,
+                           psf_message** dec_out) {
   return guarded([&] {
     if (n <= 0 || iters < 0 || !snd || !rcv || !tmpls) return PSF_ERR_ARG;
+    std::vector<int> ends;
+    if (phase_end && nphases > 0) {
+      for (int p = 0; p < nphases; ++p) {
+        if (phase_end[p] <= (p ? phase_end[p - 1] : 0) || phase_end[p] > n) return PSF_ERR_ARG;
+        ends.push_back(phase_end[p]);
+      }
+      if (ends.back() != n) return PSF_ERR_ARG;
+    } else {
+      ends.push_back(n);
+    }
     std::vector<psf::RemoteNode*> s(n), r(n);
     for (int i = 0; i < n; ++i) {
+      if (!snd[i] || !rcv[i] || !tmpls[i]) return PSF_ERR_ARG;
       s[i] = snd[i]->impl;
       r[i] = rcv[i]->impl;
     }
     std::vector<psf::Message> m(n), w(n);
     std::vector<psf::Message*> mp(n), wp(n);
     for (int it = 0; it < iters; ++it) {
-      for (int i = 0; i < n; ++i) {
-        m[i] = tmpls[i]->m;  // fresh Task + zero-copy buffers
-        mp[i] = &m[i];
+      int b = 0;
+      for (int e : ends) {  // phase [b, e): encode all, deliver, decode all
+        for (int i = b; i < e; ++i) {
+          m[i] = tmpls[i]->m;  // fresh Task + zero-copy buffers
+          mp[i] = &m[i];
+        }
+        psf::encode_batch(s.data() + b, mp.data() + b, e - b);
+        for (int i = b; i < e; ++i) {
+          w[i] = m[i];  // delivered copy
+          wp[i] = &w[i];
+        }
+        psf::decode_batch(r.data() + b, wp.data() + b, e - b);
+        b = e;
       }
-      psf::encode_batch(s.data(), mp.data(), n);
-      for (int i = 0; i < n; ++i) {
-        w[i] = m[i];  // delivered copy
-        wp[i] = &w[i];
-      }
-      psf::decode_batch(r.data(), wp.data(), n);
     }
     std::set<psf::Context*> ctxs;  // CHECK_GT(bin, 0) of the lazily encoded ranges
     for (int i = 0; i < n; ++i) ctxs.insert(s[i]->ctx());
     for (psf::Context* c : ctxs) c->check_ranges();
+    for (int i = 0; i < n; ++i) {
+      if (enc_out) enc_out[i] = iters ? new psf_message{m[i]} : nullptr;
+      if (dec_out) dec_out[i] = iters ? new psf_message{w[i]} : nullptr;
+    }
+    return PSF_OK;
+  });
+}
+int psf_nodes_roundtrip(psf_node* const* snd, psf_node* const* rcv, const psf_message* const* tmpls, int n,
+                        int iters) {
+  return psf_nodes_roundtrip_ex(snd, rcv, tmpls, n, nullptr, 0, iters, nullptr, nullptr);
+}
+
+int psf_spill_pack(psf_context* ctx, psf_message* const* msgs, const int* dest, const int* server, int n,
+                   int world, int64_t* sizes, psf_spill** out) {
+  return guarded([&] {
+    if (!ctx || !sizes || !out || n < 0 || world <= 0 || (n && (!msgs || !dest || !server))) return PSF_ERR_ARG;
+    std::vector<psf::Message*> ms(n);
+    for (int i = 0; i < n; ++i) {
+      if (!msgs[i]) return PSF_ERR_ARG;
+      ms[i] = &msgs[i]->m;
+    }
+    auto* p = new psf::SpillPlan(ctx->impl, ms.data(), dest, server, n, world);
+    for (int r = 0; r < 2 * world; ++r) sizes[r] = p->sizes()[r];
+    *out = reinterpret_cast<psf_spill*>(p);
+    return PSF_OK;
+  });
+}
+int psf_spill_fill(psf_spill* plan, void* sendbuf) {
+  return guarded([&] {
+    if (!plan) return PSF_ERR_ARG;
+    reinterpret_cast<psf::SpillPlan*>(plan)->fill(sendbuf);
+    return PSF_OK;
+  });
+}
+int psf_spill_destroy(psf_spill* plan) {
+  delete reinterpret_cast<psf::SpillPlan*>(plan);
+  return PSF_OK;
+}
+int psf_spill_unpack(psf_context* ctx, const void* recvbuf, int world, const int64_t* sizes, psf_message** outs,
+                     int* servers, int cap, int* n) {
+  return guarded([&] {
+    if (!ctx || !sizes || !n || world <= 0 || cap < 0 || (cap && (!outs || !servers))) return PSF_ERR_ARG;
+    int64_t total = 0;
+    for (int r = 0; r < 2 * world; ++r) total += sizes[r];
+    if (total && !recvbuf) return PSF_ERR_ARG;
+    std::vector<psf::Message> ms;
+    std::vector<int> sv;
+    psf::spill_unpack(ctx->impl, static_cast<const uint8_t*>(recvbuf), world, sizes, &ms, &sv);
+    *n = (int)ms.size();
+    if ((int)ms.size() > cap) {
+      g_last_error = "psf_spill_unpack: more messages than cap";
+      return PSF_ERR_ARG;
+    }
+    for (size_t i = 0; i < ms.size(); ++i) {
+      outs[i] = new psf_message{std::move(ms[i])};
+      servers[i] = sv[i];
+    }
     return PSF_OK;
   });
 }

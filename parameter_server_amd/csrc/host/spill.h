@@ -1,0 +1,43 @@
+// Cross-range spill: pack a rank's outgoing slices into one send buffer and
+// rebuild received messages over the receive buffer (see spill.cc).
+#pragma once
+#include <vector>
+
+#include "context.h"
+#include "message.h"
+
+namespace psf {
+
+class SpillPlan {
+ public:
+  // message i goes to rank dest[i], addressed to server server[i]
+  SpillPlan(Context* ctx, Message* const* msgs, const int* dest, const int* server, int n, int world);
+  // per rank r: sizes()[2r] = meta bytes, sizes()[2r+1] = payload bytes
+  const std::vector<int64_t>& sizes() const { return sizes_; }
+  uint64_t total() const { return total_; }
+  // write the send buffer (device buffer of total() bytes; host memory on a
+  // host-only context), ordered on the context's stream
+  void fill(void* sendbuf);
+
+ private:
+  struct Copy {
+    const uint8_t* src;  // device frame, or null: blob_ + blob_off
+    uint64_t blob_off;
+    uint64_t dst_off;
+    uint64_t len;
+  };
+  Context* ctx_;
+  std::vector<int64_t> sizes_;
+  std::vector<uint8_t> blob_;
+  std::vector<Copy> copies_;
+  std::vector<Buffer> keep_;
+  uint64_t total_ = 0;
+};
+
+// Rebuild the messages of a receive buffer laid out by SpillPlan (segments of
+// sources 0..world-1 back to back, sizes as the senders reported them).  The
+// messages' frames point into `recv` (the caller keeps it alive).
+int spill_unpack(Context* ctx, const uint8_t* recv, int world, const int64_t* sizes, std::vector<Message>* out,
+                 std::vector<int>* servers);
+
+}  // namespace psf

@@ -175,6 +175,18 @@ int snappy_uncompress_launch(const void* in, size_t c, uint32_t hdr, size_t dsiz
                              void* scratch, hipStream_t st, Profiler* prof, PubSlot* pub,
                              uint32_t ticket);
 
+// spill.hip: gather `n` copies (sorted by chunk0) into one send buffer; copy i
+// moves len bytes from src to dst + dst_off and owns chunks
+// [chunk0, chunk0 + ceil(len / kSpillChunk)) of the grid
+constexpr uint64_t kSpillChunk = 32768;
+struct SpillCopy {
+  const uint8_t* src;
+  uint64_t dst_off;
+  uint64_t len;
+  uint64_t chunk0;
+};
+int spill_gather_launch(const SpillCopy* d_copies, int n, uint64_t nchunks, void* dst, hipStream_t st);
+
 // kv_store.hip: server-side consumers.  `code` != null
 // makes the source a FIXING_FLOAT code array (nb bytes, range [mn, mx]) that
 // is dequantised in-register exactly as ff_decode would.

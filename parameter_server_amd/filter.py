@@ -290,17 +290,6 @@ class Message:
         check(lib().psf_msg_recv_frame(self.h, C.c_void_p(t.data_ptr()), t.numel() * t.element_size(),
                                        self._loc(t)))
 
-    def device_frames(self, device) -> list:
-        """[Task][key][value...] as uint8 tensors on `device` (the Task frame
-        copied up from the host, key / value frames copied on the device)."""
-        tb = self.task_bytes()
-        out = [torch.frombuffer(bytearray(tb), dtype=torch.uint8).to(device)]
-        p, n, loc = self.key_ptr()
-        arrays = ([(p, n, loc)] if n else []) + [self.value_ptr(i) for i in range(self.num_values())]
-        for p, n, loc in arrays:
-            out.append(copy_out(p, n, loc, device))
-        return out
-
     @staticmethod
     def _loc(t: torch.Tensor) -> int:
         return LOC_DEVICE if t.is_cuda else LOC_HOST
@@ -441,16 +430,21 @@ class RemoteNode:
             self._keepalive[id(t)] = t
 
     def roundtrip(self, rcv: "RemoteNode", tmpls, iters: int, keep_last: bool = False):
-        """Native loop: encode a copy of tmpls[i % len] here, deliver, decode on rcv."""
+        """Native loop: encode a copy of tmpls[i % len] here, deliver, decode on
+        rcv.  keep_last: return the last (encoded, decoded) message pair."""
         tmpls = tmpls if isinstance(tmpls, (list, tuple)) else [tmpls]
         for t in tmpls:
             self._hold(t)
             rcv._hold(t)
         arr = (C.c_void_p * len(tmpls))(*[t.h.value for t in tmpls])
-        out = C.c_void_p()
-        check(lib().psf_node_roundtrip(self.h, rcv.h, arr, len(tmpls), iters,
-                                       C.byref(out) if keep_last else None))
-        return Message(_handle=out, _refs=tmpls[-1]._refs) if keep_last else None
+        enc, dec = C.c_void_p(), C.c_void_p()
+        check(lib().psf_node_roundtrip_ex(self.h, rcv.h, arr, len(tmpls), iters,
+                                          C.byref(enc) if keep_last else None,
+                                          C.byref(dec) if keep_last else None))
+        if not keep_last:
+            return None
+        refs = tmpls[(iters - 1) % len(tmpls)]._refs
+        return Message(_handle=enc, _refs=refs), Message(_handle=dec, _refs=refs)
 
     def set_defer_dequant(self, on: bool = True) -> None:
         """Server side: FIXING_FLOAT decode leaves codes for the consumer."""
@@ -474,14 +468,25 @@ class RemoteNode:
                                      (C.c_void_p * n)(*[m.h.value for m in msgs]), n))
 
     @staticmethod
-    def roundtrip_many(snd, rcv, tmpls, iters: int) -> None:
+    def roundtrip_many(snd, rcv, tmpls, iters: int, keep_last: bool = False, phase_end=None):
+        """psf_nodes_roundtrip_ex: message i encoded on snd[i], decoded on
+        rcv[i]; phase_end splits the messages into batches run in order.
+        keep_last: return the last iteration's [(encoded, decoded)] per message."""
         n = len(tmpls)
-        for a, b, t in zip(snd, rcv, tmpls):  # node i only ever sees tmpls[i]
+        for a, b, t in zip(snd, rcv, tmpls):
             a._hold(t)
             b._hold(t)
-        check(lib().psf_nodes_roundtrip((C.c_void_p * n)(*[nd.h.value for nd in snd]),
-                                        (C.c_void_p * n)(*[nd.h.value for nd in rcv]),
-                                        (C.c_void_p * n)(*[t.h.value for t in tmpls]), n, iters))
+        enc, dec = (C.c_void_p * n)(), (C.c_void_p * n)()
+        pe = None if not phase_end else (C.c_int * len(phase_end))(*phase_end)
+        check(lib().psf_nodes_roundtrip_ex((C.c_void_p * n)(*[nd.h.value for nd in snd]),
+                                           (C.c_void_p * n)(*[nd.h.value for nd in rcv]),
+                                           (C.c_void_p * n)(*[t.h.value for t in tmpls]), n, pe,
+                                           len(phase_end or ()), iters,
+                                           enc if keep_last else None, dec if keep_last else None))
+        if not keep_last:
+            return None
+        return [(Message(_handle=C.c_void_p(enc[i]), _refs=tmpls[i]._refs),
+                 Message(_handle=C.c_void_p(dec[i]), _refs=tmpls[i]._refs)) for i in range(n)]
 
     def encode(self, msg: Message) -> None:
         self._hold(msg)

@@ -1,16 +1,22 @@
 """The multi-GPU split of the filter path.
 
-GPU g is server g and owns Range<Key>(key_start, key_end).EvenDivide(N, g)
-(src/system/assigner.h:17-28, src/util/range.h:100-107).  A push/pull message
-is sliced at those ranges (SliceKOFVMessage, src/system/message.h:107-147),
-each slice is encoded by the sender's per-peer RemoteNode (executor.cc:131-146)
-and delivered to its owner, where the owner's RemoteNode decodes it.
+Server s owns Range<Key>(key_start, key_end).EvenDivide(S, s)
+(src/system/assigner.h:17-28, src/util/range.h:100-107); servers live on ranks
+in contiguous blocks (rank r hosts servers [r*S/W, (r+1)*S/W), one server per
+GPU when S == W).  A push/pull message is sliced at the server ranges
+(SliceKOFVMessage, src/system/message.h:107-147), each slice is encoded by the
+sender's per-(stream, server) RemoteNode (executor.cc:131-146) and delivered to
+its server, whose per-(server, stream) RemoteNode decodes it.
 
-The only data-path collective is the cross-range spill: slices whose owner is
-another GPU travel in one all-to-all-v per step (RCCL over xGMI with the
-"nccl" backend; gloo for the CPU tests).  What travels is the ENCODED slice --
-the reference's wire frames [Task][key][value...] (van.cc:122-191) -- so
-KEY_CACHING hits and FIXING_FLOAT's 4x shrink cut the xGMI bytes too.
+The only data-path collective is the cross-range spill: slices whose server
+lives on another rank travel in one all-to-all-v per step (RCCL over xGMI with
+the "nccl" backend; gloo for the CPU tests).  What travels is the ENCODED
+slice -- the reference's wire frames [Task][key][value...] (van.cc:122-191),
+laid out by libpsf (psf_spill_pack / psf_spill_fill, one gather launch) and
+rebuilt zero-copy on the receiver (psf_spill_unpack) -- so KEY_CACHING hits
+and FIXING_FLOAT's 4x shrink cut the xGMI bytes too.  Per step the host does
+one small all-to-all of segment sizes (one device->host read) and one
+all-to-all-v of bytes; no per-frame or per-peer host work.
 """
 from __future__ import annotations
 
@@ -36,24 +42,16 @@ def server_ranges(nservers: int, key_range=KEY_ALL):
     return [even_divide(key_range, nservers, g) for g in range(nservers)]
 
 
+def server_rank(server: int, nservers: int, world: int) -> int:
+    """The rank hosting `server`: contiguous blocks of servers per rank."""
+    return server * world // nservers
+
+
 def slice_message(ctx, msg, ranges: Sequence, key_bytes: int = 8):
     """SliceKOFVMessage: returns one Message per range, or None where the range
     misses the message's key range (the reference marks those invalid and
     does not send them)."""
-    from .filter import Message
-    n = len(ranges)
-    for i in range(1, n):
-        if ranges[i - 1][1] != ranges[i][0]:
-            raise ValueError("ranges must be contiguous (message.h:120)")
-    bounds = (C.c_uint64 * (n + 1))(*([r[0] for r in ranges[:1]] + [r[1] for r in ranges]))
-    outs = (C.c_void_p * n)()
-    valid = (C.c_int * n)()
-    check(lib().psf_msg_slice(ctx.h, msg.h, bounds, n, key_bytes, outs, valid))
-    res: List[Optional[Message]] = []
-    for i in range(n):
-        m = Message(_handle=C.c_void_p(outs[i]), _refs=msg._refs)
-        res.append(m if valid[i] else None)
-    return res
+    return slice_messages(ctx, [msg], ranges, key_bytes)[0]
 
 
 def slice_messages(ctx, msgs, ranges: Sequence, key_bytes: int = 8):
@@ -79,65 +77,120 @@ def slice_messages(ctx, msgs, ranges: Sequence, key_bytes: int = 8):
     return res
 
 
-def parse_frames(frames: List[torch.Tensor]):
-    """Split a flat list of received frames into messages: each is a Task frame
-    followed by its key frame (when the Task has has_key) and one frame per
-    value_type entry (van.cc:193-255)."""
-    from .filter import Message
-    out, i = [], 0
-    while i < len(frames):
-        m = Message.from_task_bytes(frames[i].cpu().numpy().tobytes())
-        i += 1
-        has_key, _ = m.key_info()
-        nval = task_value_count(m)
-        for _ in range(int(has_key) + nval):
-            m.recv_frame(frames[i])
-            i += 1
-        out.append(m)
-    return out
+def w_channel(m) -> int:
+    ch = C.c_int32()
+    check(lib().psf_msg_key_channel(m.h, C.byref(ch)))
+    return ch.value
 
 
-def task_value_count(m) -> int:
-    """number of value_type entries of a parsed Task (its value frames)."""
-    n = C.c_int()
-    check(lib().psf_task_value_count(m.h, C.byref(n)))
-    return n.value
+class SpillExchange:
+    """The cross-range spill of one step: encoded messages -> their ranks, in
+    one all-to-all-v (plus one all-to-all of the 2 x world segment sizes).
+
+    `device` is where the buffers live ("cuda:k" with RCCL; with gloo, device
+    buffers are staged through host memory, which is what the CPU tests and
+    the single-GPU gloo rehearsals use)."""
+
+    def __init__(self, ctx, group=None, device=None):
+        import torch.distributed as dist
+        self.dist = dist
+        self.ctx = ctx
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.device = device if device is not None else (
+            f"cuda:{ctx.device}" if ctx.device >= 0 else "cpu")
+        self.staged = dist.get_backend(group) == "gloo" and str(self.device).startswith("cuda")
+        self.bytes_sent = 0
+
+    def exchange(self, msgs, dest: List[int], server: List[int]):
+        """Send msgs[i] to rank dest[i] (addressed to server server[i]);
+        returns (received messages, their servers)."""
+        from .filter import Message
+        dist, W, L = self.dist, self.world, lib()
+        n = len(msgs)
+        sizes = (C.c_int64 * (2 * W))()
+        plan = C.c_void_p()
+        check(L.psf_spill_pack(self.ctx.h, (C.c_void_p * n)(*[m.h.value for m in msgs]),
+                               (C.c_int * n)(*dest), (C.c_int * n)(*server), n, W, sizes, C.byref(plan)))
+        try:
+            wire_dev = "cpu" if self.staged else self.device
+            size_t = torch.tensor(list(sizes), dtype=torch.int64)
+            size_in = torch.empty_like(size_t)
+            if wire_dev != "cpu":
+                size_t, size_in = size_t.to(wire_dev, non_blocking=True), size_in.to(wire_dev)
+            dist.all_to_all_single(size_in, size_t, group=self.group)
+            sizes_in = size_in.cpu().tolist()  # the one device->host read of the step
+            in_splits = [sizes[2 * r] + sizes[2 * r + 1] for r in range(W)]
+            out_splits = [sizes_in[2 * s] + sizes_in[2 * s + 1] for s in range(W)]
+            sendbuf = torch.empty(max(sum(in_splits), 1), dtype=torch.uint8, device=self.device)
+            check(L.psf_spill_fill(plan, C.c_void_p(sendbuf.data_ptr())))
+        finally:
+            L.psf_spill_destroy(plan)
+        self.bytes_sent += sum(in_splits) - in_splits[dist.get_rank(self.group)]
+        recvbuf = torch.empty(max(sum(out_splits), 1), dtype=torch.uint8, device=wire_dev)
+        if self.staged:
+            self.ctx.sync()
+            sendbuf = sendbuf.cpu()
+        dist.all_to_all_single(recvbuf[:sum(out_splits)], sendbuf[:sum(in_splits)], out_splits, in_splits,
+                               group=self.group)
+        if self.staged:
+            recvbuf = recvbuf.to(self.device)
+        cap = max(1, sum(sizes_in[0::2]) // 24)  # a record is >= 24 bytes
+        outs = (C.c_void_p * cap)()
+        servers = (C.c_int * cap)()
+        got = C.c_int()
+        sin = (C.c_int64 * (2 * W))(*sizes_in)
+        check(L.psf_spill_unpack(self.ctx.h, C.c_void_p(recvbuf.data_ptr()), W, sin, outs, servers, cap,
+                                 C.byref(got)))
+        res = [Message(_handle=C.c_void_p(outs[i]), _refs=[recvbuf]) for i in range(got.value)]
+        return res, [servers[i] for i in range(got.value)]
 
 
 class PushRouter:
-    """The multi-server push path of one rank (SURVEY.md §8(d) C4): every
-    local stream's message is sliced at the server key ranges
+    """The multi-server push path of one rank (SURVEY.md §8(d) C4/C5): every
+    local stream's message is sliced at the `ranges` of S servers
     (SliceKOFVMessage), each slice is encoded by the sender's per-(stream,
-    server) RemoteNode (executor.cc:131-146); slices owned by this rank are
-    decoded here, the others travel as wire frames in ONE all-to-all-v per step
-    (the cross-range spill) and are decoded by their owner's per-stream node.
-    The stream id travels as the Task's key_channel."""
+    server) RemoteNode (executor.cc:131-146); slices whose server lives on
+    this rank are decoded here, the others travel in ONE all-to-all-v per step
+    (the cross-range spill) and are decoded by their server's per-stream node.
+    The stream id travels as the Task's key_channel.  `loopback` sends the
+    local slices through the exchange too (a world-1 run of the RCCL path)."""
 
-    def __init__(self, ctx, ranges, rank: int, world: int, exchange=None):
+    def __init__(self, ctx, ranges, rank: int, world: int, exchange: Optional[SpillExchange] = None,
+                 loopback: bool = False):
         from .filter import RemoteNode
         self.ctx, self.ranges, self.rank, self.world = ctx, ranges, rank, world
+        self.nservers = len(ranges)
+        if self.nservers < world:
+            raise ValueError("need at least one server per rank")
         self.exchange = exchange
+        if (world > 1 or loopback) and exchange is None:
+            raise ValueError("a spill exchange is needed")
+        self.loopback = loopback
         self._RemoteNode = RemoteNode
         self.senders, self.receivers = {}, {}
-        self.device = f"cuda:{ctx.device}" if ctx.device >= 0 else "cpu"
+        self.last_encoded = []  # (stream, server, encoded slice) of the last step
+
+    def owner(self, server: int) -> int:
+        return server_rank(server, self.nservers, self.world)
 
     def _sender(self, s, d):
         if (s, d) not in self.senders:
             self.senders[(s, d)] = self._RemoteNode(self.ctx)
         return self.senders[(s, d)]
 
-    def _receiver(self, s):
-        if s not in self.receivers:
-            self.receivers[s] = self._RemoteNode(self.ctx)
-        return self.receivers[s]
+    def _receiver(self, d, s):
+        if (d, s) not in self.receivers:
+            self.receivers[(d, s)] = self._RemoteNode(self.ctx)
+        return self.receivers[(d, s)]
 
-    def step(self, streams) -> list:
+    def step(self, streams, keep_encoded: bool = False) -> list:
         """streams: {stream id: template Message (key_channel = stream id)} of
-        this rank.  Returns the decoded messages this rank received.  All
-        slices of the step are encoded in one batched call (psf_nodes_encode)
-        and all received ones decoded in one (psf_nodes_decode)."""
+        this rank.  Returns [(server, decoded message)] of what this rank's
+        servers received.  All slices of the step are encoded in one batched
+        call (psf_nodes_encode) and all received ones decoded in one
+        (psf_nodes_decode)."""
         from .filter import RemoteNode
-        send = [[] for _ in range(self.world)]
         enc_nodes, enc_msgs, dest = [], [], []
         sids = list(streams)
         clones = [streams[sid].clone() for sid in sids]
@@ -150,84 +203,26 @@ class PushRouter:
                 dest.append((sid, d))
         if enc_msgs:
             RemoteNode.encode_many(enc_nodes, enc_msgs)
-        dec_nodes, dec_msgs = [], []
+        self.last_encoded = list(zip(dest, enc_msgs)) if keep_encoded else []
+        dec_nodes, dec_msgs, got = [], [], []
+        out_m, out_r, out_s = [], [], []
         for (sid, d), part in zip(dest, enc_msgs):
-            if d == self.rank:
-                dec_nodes.append(self._receiver(sid))
-                dec_msgs.append(part.clone())
+            r = self.owner(d)
+            if r == self.rank and not self.loopback:
+                w = part.clone()  # delivered copy (Task + zero-copy buffers)
+                dec_nodes.append(self._receiver(d, sid))
+                dec_msgs.append(w)
+                got.append((d, w))
             else:
-                send[d].extend(part.device_frames(self.device))
-        if self.world > 1:
-            recv = self.exchange.exchange(send)
-            for src in range(self.world):
-                for w in parse_frames(recv[src]):
-                    dec_nodes.append(self._receiver(w_channel(w)))
-                    dec_msgs.append(w)
+                out_m.append(part)
+                out_r.append(r)
+                out_s.append(d)
+        if self.world > 1 or self.loopback:
+            recv, servers = self.exchange.exchange(out_m, out_r, out_s)
+            for w, d in zip(recv, servers):
+                dec_nodes.append(self._receiver(d, w_channel(w)))
+                dec_msgs.append(w)
+                got.append((d, w))
         if dec_msgs:
             RemoteNode.decode_many(dec_nodes, dec_msgs)
-        return dec_msgs
-
-
-def w_channel(m) -> int:
-    ch = C.c_int32()
-    check(lib().psf_msg_key_channel(m.h, C.byref(ch)))
-    return ch.value
-
-
-class SpillExchange:
-    """All-to-all-v of byte frames between ranks (one collective per step).
-
-    send[dst] is a list of uint8 tensors (frames) for rank dst; the result
-    recv[src] is the list of frames rank src sent here, in order.  Frame
-    lengths travel first (one small all-to-all), then all bytes in one
-    all_to_all_single with per-peer split sizes."""
-
-    def __init__(self, group=None, device=None):
-        import torch.distributed as dist
-        self.dist = dist
-        self.group = group
-        self.world = dist.get_world_size(group)
-        self.device = device
-
-    def exchange(self, send: List[List[torch.Tensor]]) -> List[List[torch.Tensor]]:
-        dist, W = self.dist, self.world
-        dev = self.device if self.device is not None else "cpu"
-        if dist.get_backend(self.group) == "gloo" and str(dev).startswith("cuda"):
-            # gloo moves host memory only: stage through the host (CPU tests /
-            # single-GPU rehearsals; RCCL moves HBM directly)
-            self.device = "cpu"
-            try:
-                recv = self.exchange([[f.cpu() for f in frames] for frames in send])
-            finally:
-                self.device = dev
-            return [[f.to(dev) for f in frames] for frames in recv]
-        counts = torch.tensor([len(f) for f in send], dtype=torch.int64, device=dev)
-        counts_in = torch.empty_like(counts)
-        dist.all_to_all_single(counts_in, counts, group=self.group)
-        # every rank must use the same row width for the lens all-to-all
-        maxf_t = torch.tensor([max(1, int(counts.max()))], dtype=torch.int64, device=dev)
-        dist.all_reduce(maxf_t, op=dist.ReduceOp.MAX, group=self.group)
-        maxf = int(maxf_t.item())
-        lens = torch.zeros(W, maxf, dtype=torch.int64, device=dev)
-        for d, frames in enumerate(send):
-            for j, f in enumerate(frames):
-                lens[d, j] = f.numel()
-        lens_in = torch.empty_like(lens)
-        dist.all_to_all_single(lens_in.view(-1), lens.view(-1), group=self.group)
-        in_splits = [int(lens[d].sum()) for d in range(W)]
-        out_splits = [int(lens_in[s].sum()) for s in range(W)]
-        flat = [f.reshape(-1) for frames in send for f in frames]
-        sendbuf = torch.cat(flat) if flat else torch.empty(0, dtype=torch.uint8, device=dev)
-        recvbuf = torch.empty(sum(out_splits), dtype=torch.uint8, device=dev)
-        dist.all_to_all_single(recvbuf, sendbuf, out_splits, in_splits, group=self.group)
-        recv, off = [], 0
-        counts_l = counts_in.tolist()
-        lens_l = lens_in.tolist()
-        for s in range(W):
-            frames = []
-            for j in range(counts_l[s]):
-                ln = lens_l[s][j]
-                frames.append(recvbuf[off:off + ln])
-                off += ln
-            recv.append(frames)
-        return recv
+        return got

@@ -126,6 +126,62 @@ def test_batch_roundtrip_driver(ctx):
     ctx.sync()
 
 
+def test_batch_roundtrip_driver_c1_vs_port(ctx, port):
+    """The timed C1 driver (psf_nodes_roundtrip_ex in three phases, what
+    `bench.py --config c1` runs): 64 ctr minibatch streams of 10^5 sorted keys,
+    per step a pull request (keys), pull response (weights) and push
+    (gradients) with the ctr filters (online_l1lr.conf:36-53), three steps.
+    The last step's encoded messages (KEY_CACHING signature and elision,
+    codes, side-info) and decoded messages (keys restored, values) of every
+    stream against the C restatement."""
+    from parameter_server_amd import FIXING_FLOAT, KEY_CACHING
+    from parameter_server_amd import filter as F
+    m, S, seed = 100_000, 64, 31337
+    g = torch.Generator(device=DEV)
+    g.manual_seed(7)
+    wk = [F.RemoteNode(ctx) for _ in range(S)]
+    sv = [F.RemoteNode(ctx) for _ in range(S)]
+    req, resp, push, data = [], [], [], []
+    for sid in range(S):
+        keys = torch.sort(torch.unique(torch.randint(0, 10**9, (m + m // 8,), device=DEV, generator=g))[:m])[0]
+        vals = []
+        for lst, request, is_push, has_v, clear in ((req, True, False, False, None),
+                                                    (resp, False, False, True, None),
+                                                    (push, True, True, True, True)):
+            t = F.Message(request=request, push=is_push, key_channel=sid, key_range=(0, 10**9))
+            t.set_key(keys)
+            if has_v:
+                v = torch.randn(m, device=DEV, generator=g)
+                t.add_value(v)
+                vals.append(v.cpu().numpy())
+            t.add_filter(KEY_CACHING, clear_cache_if_done=clear)
+            t.add_filter(FIXING_FLOAT, num_bytes=1)
+            lst.append(t)
+        data.append((keys.cpu().numpy().view(np.uint64), vals))
+    F.set_clock(seed)
+    try:
+        last = F.RemoteNode.roundtrip_many(wk + sv + wk, sv + wk + sv, req + resp + push, 3, keep_last=True,
+                                           phase_end=[S, 2 * S, 3 * S])
+    finally:
+        F.set_clock(None)
+    node = lambda msg: wk[0]  # noqa: E731  (any node of the context copies out)
+    for sid, (keys, (w, x)) in enumerate(data):
+        sig = port.key_signature(keys)
+        (qe, qd), (re_, rd), (pe, pd_) = last[sid], last[S + sid], last[2 * S + sid]
+        # pull request: the push of the previous step erased the cache -> miss
+        assert qe.signature(0) == (True, sig) and qe.key_info()[0], sid
+        assert node(qd).key(qd).cpu().numpy().view(np.uint64).tobytes() == keys.tobytes()
+        for enc, dec, v in ((re_, rd, w), (pe, pd_, x)):  # response / push: hit, keys elided
+            assert enc.signature(0) == (True, sig) and not enc.key_info()[0], sid
+            st, pc, pmn, pmx = port.ff_encode(v, 1, seed)
+            (hm, mn, hx, mx), = enc.fixed_points(1)
+            assert hm and hx and (mn, mx) == (pmn, pmx), sid
+            assert np.array_equal(node(enc).value(enc, 0).cpu().numpy(), pc), sid
+            st, pdec = port.ff_decode(pc, 1, pmn, pmx, np.float32)
+            assert node(dec).value(dec, 0).cpu().numpy().tobytes() == pdec.tobytes(), sid
+            assert node(dec).key(dec).cpu().numpy().view(np.uint64).tobytes() == keys.tobytes(), sid
+
+
 def test_batch_key_caching_order(ctx, port):
     """Two messages with the same keys and channel on ONE node in one batch:
     the first misses and caches, the second hits and drops its keys -- as

@@ -127,10 +127,56 @@ def test_ff_full_size_properties(ctx):
     step = (np.float64(mx) - np.float64(mn)) / 254.0
     err = (dec.double() - x.double()).abs().max().item()
     assert err <= step * (1 + 1e-6) + 1e-6  # fixing_float.h: |out - x| <= bin/ratio (+ f32 rounding)
-    # codes never exceed ratio + 1 = 255 and the LCG bit is ~fair
-    hist = torch.bincount(codes.long(), minlength=256)
-    assert hist.sum().item() == n
-    del x, dec
+    # code range: floor(tmp) + bit <= ratio + 1 = 255, and the extremes are hit
+    # (x == min -> 0 + bit; x == max - 1e-6 -> 253 or 254 + bit)
+    c = codes.long()
+    hist = torch.bincount(c, minlength=256)
+    assert hist.numel() == 256
+    assert int(c.min()) <= 1 and int(c.max()) >= 253
+    # the stochastic-rounding bit: code - floor(tmp) is the LCG bit of element
+    # i, the inverted bit 16 of the MSVC LCG state s_{i+1}; over a full period
+    # of the low 17 bits it is exactly balanced, so over 2^28 elements (2^11
+    # periods) it is balanced to the element
+    mn64, mx64 = np.float64(mn), np.float64(mx)
+    tmp = torch.floor((x.double().clamp(mn64, mx64) - mn64) / (mx64 - mn64) * 254.0).long()
+    bit = c - tmp
+    assert int(bit.min()) >= 0 and int(bit.max()) <= 1
+    assert int(bit.sum()) == n // 2
+    del x, dec, c, tmp, bit
+
+
+def test_roundtrip_driver_c2_vs_port(ctx, port):
+    """The timed driver (psf_node_roundtrip, what bench.py runs) on the bench
+    template at BASELINE configs[1]'s size (2^27 f32, [FIXING_FLOAT nb=1],
+    min/max computed): the encoded message as it went on the wire (codes +
+    side-info) and the decoded message, byte for byte against the C
+    restatement."""
+    from parameter_server_amd import FIXING_FLOAT
+    from parameter_server_amd import filter as F
+    n = 1 << 27
+    g = torch.Generator(device=DEV)
+    g.manual_seed(1)
+    xs = [torch.randn(n, device=DEV, generator=g) for _ in range(2)]
+    tm = []
+    for x in xs:
+        m = F.Message(request=True, push=True, key_channel=0)
+        m.add_value(x)
+        m.add_filter(FIXING_FLOAT, num_bytes=1)
+        tm.append(m)
+    worker, server = F.RemoteNode(ctx), F.RemoteNode(ctx)
+    F.set_clock(12345)
+    try:
+        enc, dec = worker.roundtrip(server, tm, 5, keep_last=True)  # last = tm[0]
+    finally:
+        F.set_clock(None)
+    (has_mn, mn, has_mx, mx), = enc.fixed_points(0)
+    st, pc, pmn, pmx = port.ff_encode(xs[0].cpu().numpy(), 1, 12345)
+    assert st == 0 and has_mn and has_mx
+    assert _bits(mn) == _bits(pmn) and _bits(mx) == _bits(pmx)
+    assert np.array_equal(worker.value(enc, 0).cpu().numpy(), pc)
+    st, pd = port.ff_decode(pc, 1, pmn, pmx, np.float32)
+    assert server.value(dec, 0).cpu().numpy().tobytes() == pd.tobytes()
+    assert dec.fixed_points(0) == enc.fixed_points(0)
 
 
 def test_crc32c_vectors(ctx):

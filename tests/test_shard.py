@@ -83,33 +83,67 @@ def _free_port():
     return p
 
 
+def _spill_msgs(rank, world):
+    """the messages rank `rank` sends: (dest, server, key bytes or None, values)"""
+    out = []
+    for d in range(world):
+        if rank == 0 and d == 1:
+            continue  # a peer with nothing to send
+        for j in range(d + 1 + rank):
+            keys = (np.arange(10 * rank + 3 * d + j + 1, dtype=np.uint64) * 7 + j) if j % 2 == 0 else None
+            vals = [np.full(5 + j, rank + d + 0.5, np.float32), np.zeros(0, np.float32),
+                    np.arange(j + 1, dtype=np.float64)]
+            out.append((d, 10 + d, 100 * rank + 10 * d + j, keys, vals))
+    return out
+
+
 def _exchange_worker(rank, world, port, q):
     import torch.distributed as dist
 
-    from parameter_server_amd.shard import SpillExchange
+    from parameter_server_amd import KEY_CACHING
+    from parameter_server_amd import filter as F
+    from parameter_server_amd.shard import SpillExchange, w_channel
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        ex = SpillExchange()
-        send = []
-        for d in range(world):
-            frames = [torch.full((10 * rank + d + j,), 16 * rank + d, dtype=torch.uint8) for j in range(d + 1)]
-            if rank == 0 and d == 1:
-                frames = []  # a peer with nothing to send
-            send.append(frames)
-        recv = ex.exchange(send)
-        ok = True
-        for s in range(world):
-            exp = 0 if (s == 0 and rank == 1) else rank + 1
-            ok &= len(recv[s]) == exp
-            for j, f in enumerate(recv[s]):
-                ok &= f.numel() == 10 * s + rank + j and bool((f == 16 * s + rank).all())
-        q.put((rank, ok))
+        ctx = F.HostContext()
+        ex = SpillExchange(ctx)
+        msgs, dest, server = [], [], []
+        for d, srv, ch, keys, vals in _spill_msgs(rank, world):
+            m = F.Message(request=True, push=True, key_channel=ch, key_range=(5, 1 << 40))
+            if keys is not None:
+                m.set_key(torch.from_numpy(keys.view(np.int64).copy()))
+            for v in vals:
+                m.add_value(torch.from_numpy(v.copy()))
+            m.add_filter(KEY_CACHING)
+            msgs.append(m)
+            dest.append(d)
+            server.append(srv)
+        got, servers = ex.exchange(msgs, dest, server)
+        want = [w for s in range(world) for w in _spill_msgs(s, world) if w[0] == rank]
+        ok = len(got) == len(want)
+        for m, srv, (d, wsrv, ch, keys, vals) in zip(got, servers, want):
+            ok &= srv == wsrv and w_channel(m) == ch
+            has_key, _ = m.key_info()
+            ptr, nb, _ = m.key_ptr()
+            kb = bytes((np.ctypeslib.ctypes.c_uint8 * nb).from_address(ptr)) if nb else b""
+            ok &= has_key == (keys is not None) and kb == (b"" if keys is None else keys.tobytes())
+            ok &= m.num_values() == len(vals)
+            for i, v in enumerate(vals):
+                vp, vb, _ = m.value_ptr(i)
+                gb = bytes((np.ctypeslib.ctypes.c_uint8 * vb).from_address(vp)) if vb else b""
+                ok &= gb == v.tobytes()
+        q.put((rank, bool(ok)))
+    except Exception as e:  # report instead of hanging the parent
+        q.put((rank, repr(e)))
     finally:
         dist.destroy_process_group()
 
 
 def test_spill_exchange_gloo_world2():
+    """psf_spill_pack / fill / unpack through one gloo all-to-all-v: every
+    message (Task, key frame, value frames incl. empty ones, server id) arrives
+    intact, in order, at its rank."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -121,6 +155,24 @@ def test_spill_exchange_gloo_world2():
     for p in procs:
         p.join(timeout=60)
     assert res == {0: True, 1: True}
+
+
+def test_bench_launcher_gloo_world2():
+    """`bench.py --gpus 2` starts its two ranks itself (no torchrun) and the
+    process group really has two members (launch plumbing only, on CPU)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PSF_DIST_BACKEND="gloo")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--config", "c4",
+                          "--launch-check"], env=env, capture_output=True, text=True, timeout=180)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [json.loads(x) for x in out.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    assert lines[0]["n_gpus"] == 2 and lines[0]["world_size"] == 2 and lines[0]["backend"] == "gloo"
 
 
 def test_slice_many_host_keys_matches_restatement():
