@@ -326,8 +326,7 @@ def build_workload(args, F, ctx, rank, world, dev, g, n):
             payload += keys.numel() * (8 + 4 * dim)
 
         def run(k):
-            for _ in range(k):
-                router.step(streams)
+            router.run(streams, k)
         return run, payload, nloc, {"router": router}
     worker, server = F.RemoteNode(ctx), F.RemoteNode(ctx)
     tmpls = []

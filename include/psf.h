@@ -353,6 +353,42 @@ int psf_spill_destroy(psf_spill* plan);
 int psf_spill_unpack(psf_context* ctx, const void* recvbuf, int world, const int64_t* sizes_in,
                      psf_message** outs, int* servers, int cap, int* n);
 
+/* ---- the multi-server push path of one rank -----------------------------
+ * What Executor::Submit does for a push to the server group
+ * (src/system/executor.cc:127-146: SliceKOFVMessage at the server key ranges,
+ * src/system/message.h:107-147, then EncodeMessage on the per-peer
+ * RemoteNode) and what each server's executor does with what arrives
+ * (DecodeMessage, executor.cc:178-219), for many push streams at once:
+ * S servers with the contiguous key ranges [bounds[s], bounds[s+1]), server s
+ * hosted by rank s * world / S; one sender node per (stream key_channel,
+ * server), one receiver node per (server, stream).  loopback = 1 sends the
+ * local slices through the exchange as well.
+ *
+ * A step: psf_router_encode (slice + encode every stream's template, copied
+ * as the executor copies the Task; pack the slices for other ranks: sizes as
+ * psf_spill_pack), psf_router_fill (the send buffer), the caller's
+ * all-to-all-v, psf_router_decode_local / psf_router_decode_received (the
+ * receive buffer is copied into library-owned memory: KEY_CACHING keeps
+ * received keys by reference).  psf_router_step runs `iters` whole steps of a
+ * world-1 router (no exchange).  Results of the last step: the decoded
+ * messages with their server (psf_router_result), and with
+ * psf_router_keep_encoded(1) the encoded slices (psf_router_encoded); both
+ * return new message handles. */
+typedef struct psf_router psf_router;
+int psf_router_create(psf_context* ctx, const uint64_t* bounds, int nservers, int rank, int world, int loopback,
+                      psf_router** out);
+int psf_router_destroy(psf_router* r);
+int psf_router_keep_encoded(psf_router* r, int enable);
+int psf_router_encode(psf_router* r, psf_message* const* streams, int n, int64_t* sizes);
+int psf_router_fill(psf_router* r, void* sendbuf);
+int psf_router_decode_local(psf_router* r);
+int psf_router_decode_received(psf_router* r, const void* recvbuf, const int64_t* sizes_in);
+int psf_router_step(psf_router* r, psf_message* const* streams, int n, int iters);
+int psf_router_num_results(psf_router* r);
+int psf_router_result(psf_router* r, int i, int* server, psf_message** out);
+int psf_router_num_encoded(psf_router* r);
+int psf_router_encoded(psf_router* r, int i, int32_t* stream, int* server, psf_message** out);
+
 /* ---- launch profiler (HIP events on the launch stream) ----------------- */
 #define PSF_K_MINMAX 0
 #define PSF_K_ENCODE 1

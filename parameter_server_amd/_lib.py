@@ -122,6 +122,18 @@ SIGNATURES = {
     "psf_spill_fill": ([vp, vp], C.c_int),
     "psf_spill_destroy": ([vp], C.c_int),
     "psf_spill_unpack": ([vp, vp, C.c_int, C.POINTER(C.c_int64), C.POINTER(vp), PI, C.c_int, PI], C.c_int),
+    "psf_router_create": ([vp, C.POINTER(u64), C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(vp)], C.c_int),
+    "psf_router_destroy": ([vp], C.c_int),
+    "psf_router_keep_encoded": ([vp, C.c_int], C.c_int),
+    "psf_router_encode": ([vp, C.POINTER(vp), C.c_int, C.POINTER(C.c_int64)], C.c_int),
+    "psf_router_fill": ([vp, vp], C.c_int),
+    "psf_router_decode_local": ([vp], C.c_int),
+    "psf_router_decode_received": ([vp, vp, C.POINTER(C.c_int64)], C.c_int),
+    "psf_router_step": ([vp, C.POINTER(vp), C.c_int, C.c_int], C.c_int),
+    "psf_router_num_results": ([vp], C.c_int),
+    "psf_router_result": ([vp, C.c_int, PI, C.POINTER(vp)], C.c_int),
+    "psf_router_num_encoded": ([vp], C.c_int),
+    "psf_router_encoded": ([vp, C.c_int, C.POINTER(i32), PI, C.POINTER(vp)], C.c_int),
     "psf_profile_enable": ([vp, C.c_int], C.c_int),
     "psf_profile_stride": ([vp, C.c_int], C.c_int),
     "psf_profile_reset": ([vp], C.c_int),

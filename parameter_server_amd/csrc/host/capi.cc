@@ -8,6 +8,7 @@
 
 #include "filter.h"
 #include "kvstore.h"
+#include "router.h"
 #include "slice.h"
 #include "snappy_host.h"
 #include "spill.h"
@@ -657,7 +658,7 @@ int psf_spill_unpack(psf_context* ctx, const void* recvbuf, int world, const int
     if (total && !recvbuf) return PSF_ERR_ARG;
     std::vector<psf::Message> ms;
     std::vector<int> sv;
-    psf::spill_unpack(ctx->impl, static_cast<const uint8_t*>(recvbuf), world, sizes, &ms, &sv);
+    psf::spill_unpack(ctx->impl, psf::own_copy(ctx->impl, recvbuf, (size_t)total), world, sizes, &ms, &sv);
     *n = (int)ms.size();
     if ((int)ms.size() > cap) {
       g_last_error = "psf_spill_unpack: more messages than cap";
@@ -667,6 +668,98 @@ int psf_spill_unpack(psf_context* ctx, const void* recvbuf, int world, const int
       outs[i] = new psf_message{std::move(ms[i])};
       servers[i] = sv[i];
     }
+    return PSF_OK;
+  });
+}
+
+int psf_router_create(psf_context* ctx, const uint64_t* bounds, int nservers, int rank, int world, int loopback,
+                      psf_router** out) {
+  return guarded([&] {
+    if (!ctx || !bounds || !out || nservers <= 0) return PSF_ERR_ARG;
+    std::vector<psf::KeyRange> krs(nservers);
+    for (int i = 0; i < nservers; ++i) krs[i] = psf::KeyRange{bounds[i], bounds[i + 1]};
+    *out = reinterpret_cast<psf_router*>(new psf::PushRouter(ctx->impl, krs, rank, world, loopback != 0));
+    return PSF_OK;
+  });
+}
+int psf_router_destroy(psf_router* r) {
+  delete reinterpret_cast<psf::PushRouter*>(r);
+  return PSF_OK;
+}
+static psf::PushRouter* R(psf_router* r) {
+  if (!r) throw psf::CheckError(PSF_ERR_ARG, "null router");
+  return reinterpret_cast<psf::PushRouter*>(r);
+}
+int psf_router_keep_encoded(psf_router* r, int on) {
+  return guarded([&] { R(r)->keep_encoded(on != 0); return PSF_OK; });
+}
+int psf_router_encode(psf_router* r, psf_message* const* streams, int n, int64_t* sizes) {
+  return guarded([&] {
+    if (n < 0 || (n && !streams) || !sizes) return PSF_ERR_ARG;
+    std::vector<const psf::Message*> ms(n);
+    for (int i = 0; i < n; ++i) {
+      if (!streams[i]) return PSF_ERR_ARG;
+      ms[i] = &streams[i]->m;
+    }
+    R(r)->encode(ms.data(), n, sizes);
+    return PSF_OK;
+  });
+}
+int psf_router_fill(psf_router* r, void* sendbuf) {
+  return guarded([&] { R(r)->fill(sendbuf); return PSF_OK; });
+}
+int psf_router_decode_local(psf_router* r) {
+  return guarded([&] { R(r)->decode_local(); return PSF_OK; });
+}
+int psf_router_decode_received(psf_router* r, const void* recvbuf, const int64_t* sizes_in) {
+  return guarded([&] {
+    if (!sizes_in) return PSF_ERR_ARG;
+    R(r)->decode_received(static_cast<const uint8_t*>(recvbuf), sizes_in);
+    return PSF_OK;
+  });
+}
+int psf_router_step(psf_router* r, psf_message* const* streams, int n, int iters) {
+  return guarded([&] {
+    if (n < 0 || (n && !streams) || iters < 0) return PSF_ERR_ARG;
+    psf::PushRouter* pr = R(r);
+    std::vector<const psf::Message*> ms(n);
+    for (int i = 0; i < n; ++i) {
+      if (!streams[i]) return PSF_ERR_ARG;
+      ms[i] = &streams[i]->m;
+    }
+    std::vector<int64_t> sizes(2 * (size_t)pr->world());
+    for (int it = 0; it < iters; ++it) {
+      pr->encode(ms.data(), n, sizes.data());
+      for (int64_t s : sizes)
+        if (s) throw psf::CheckError(PSF_ERR_ARG, "psf_router_step: slices for other ranks need an exchange");
+      pr->fill(nullptr);
+      pr->decode_local();
+    }
+    return PSF_OK;
+  });
+}
+int psf_router_num_results(psf_router* r) {
+  return guarded([&] { return (int)R(r)->results().size(); });
+}
+int psf_router_result(psf_router* r, int i, int* server, psf_message** out) {
+  return guarded([&] {
+    const auto& res = R(r)->results();
+    if (i < 0 || i >= (int)res.size() || !out) return PSF_ERR_ARG;
+    if (server) *server = res[i].first;
+    *out = new psf_message{res[i].second};
+    return PSF_OK;
+  });
+}
+int psf_router_num_encoded(psf_router* r) {
+  return guarded([&] { return (int)R(r)->encoded().size(); });
+}
+int psf_router_encoded(psf_router* r, int i, int32_t* stream, int* server, psf_message** out) {
+  return guarded([&] {
+    const auto& e = R(r)->encoded();
+    if (i < 0 || i >= (int)e.size() || !out) return PSF_ERR_ARG;
+    if (stream) *stream = e[i].stream;
+    if (server) *server = e[i].server;
+    *out = new psf_message{e[i].msg};
     return PSF_OK;
   });
 }

@@ -1,0 +1,111 @@
+#include "router.h"
+
+#include "slice.h"
+
+namespace psf {
+
+PushRouter::PushRouter(Context* ctx, const std::vector<KeyRange>& ranges, int rank, int world, bool loopback)
+    : ctx_(ctx), ranges_(ranges), rank_(rank), world_(world), loopback_(loopback) {
+  if (world <= 0 || rank < 0 || rank >= world) throw CheckError(kErrArg, "bad rank / world");
+  if ((int)ranges.size() < world) throw CheckError(kErrArg, "need at least one server per rank");
+  for (size_t i = 1; i < ranges.size(); ++i)
+    if (ranges[i - 1].end != ranges[i].begin) throw CheckError(kErrArg, "server ranges must be contiguous");
+}
+
+PushRouter::~PushRouter() = default;
+
+RemoteNode* PushRouter::sender(int32_t stream, int server) {
+  auto& p = senders_[{stream, server}];
+  if (!p) p.reset(new RemoteNode(ctx_));
+  return p.get();
+}
+
+RemoteNode* PushRouter::receiver(int server, int32_t stream) {
+  auto& p = receivers_[{(int32_t)server, (int)stream}];
+  if (!p) p.reset(new RemoteNode(ctx_));
+  return p.get();
+}
+
+// Executor::Submit for a push to kServerGroup (executor.cc:127-146): slice
+// (message.h:107-147), encode each valid slice on its per-peer node.
+void PushRouter::encode(const Message* const* streams, int n, int64_t* sizes) {
+  results_.clear();
+  enc_.clear();
+  local_.clear();
+  local_server_.clear();
+  plan_.reset();
+  std::vector<Message> clones(n);  // `new Message(msg->task)` + zero-copy data
+  for (int i = 0; i < n; ++i) clones[i] = *streams[i];
+  std::vector<const Message*> cp(n);
+  for (int i = 0; i < n; ++i) cp[i] = &clones[i];
+  std::vector<std::vector<Message>> parts;
+  std::vector<std::vector<bool>> ok;
+  slice_messages(ctx_, cp, ranges_, 8, &parts, &ok);
+  const int S = (int)ranges_.size();
+  std::vector<Message> slices;
+  slices.reserve((size_t)n * S);
+  std::vector<RemoteNode*> nodes;
+  std::vector<int> srv;
+  for (int i = 0; i < n; ++i)
+    for (int d = 0; d < S; ++d) {
+      if (!ok[i][d]) continue;  // the range misses the message's key range: not sent
+      slices.push_back(std::move(parts[i][d]));
+      nodes.push_back(sender(clones[i].task.key_channel, d));
+      srv.push_back(d);
+    }
+  std::vector<Message*> mp(slices.size());
+  for (size_t k = 0; k < slices.size(); ++k) mp[k] = &slices[k];
+  encode_batch(nodes.data(), mp.data(), (int)slices.size());
+  std::vector<Message*> remote;
+  std::vector<int> dest, rsrv;
+  for (size_t k = 0; k < slices.size(); ++k) {
+    if (keep_enc_) enc_.push_back(Encoded{slices[k].task.key_channel, srv[k], slices[k]});
+    const int r = owner(srv[k]);
+    if (r == rank_ && !loopback_) {
+      local_.push_back(slices[k]);  // delivered copy (Task + zero-copy buffers)
+      local_server_.push_back(srv[k]);
+    } else {
+      remote.push_back(&slices[k]);
+      dest.push_back(r);
+      rsrv.push_back(srv[k]);
+    }
+  }
+  plan_.reset(new SpillPlan(ctx_, remote.data(), dest.data(), rsrv.data(), (int)remote.size(), world_));
+  for (int r = 0; r < 2 * world_; ++r) sizes[r] = plan_->sizes()[r];
+}
+
+void PushRouter::fill(void* sendbuf) {
+  if (!plan_) throw CheckError(kErrArg, "fill() before encode()");
+  plan_->fill(sendbuf);
+  plan_.reset();
+}
+
+// PickActiveMsg on each server (executor.cc:178-219): decode on the server's
+// node for that stream, all of them in one batch.
+void PushRouter::decode_into_results(std::vector<Message>& ms, const std::vector<int>& servers) {
+  std::vector<RemoteNode*> nodes(ms.size());
+  std::vector<Message*> mp(ms.size());
+  for (size_t k = 0; k < ms.size(); ++k) {
+    nodes[k] = receiver(servers[k], ms[k].task.key_channel);
+    mp[k] = &ms[k];
+  }
+  decode_batch(nodes.data(), mp.data(), (int)ms.size());
+  for (size_t k = 0; k < ms.size(); ++k) results_.emplace_back(servers[k], std::move(ms[k]));
+}
+
+void PushRouter::decode_local() {
+  decode_into_results(local_, local_server_);
+  local_.clear();
+  local_server_.clear();
+}
+
+void PushRouter::decode_received(const uint8_t* recvbuf, const int64_t* sizes_in) {
+  uint64_t total = 0;
+  for (int r = 0; r < 2 * world_; ++r) total += (uint64_t)sizes_in[r];
+  std::vector<Message> ms;
+  std::vector<int> sv;
+  spill_unpack(ctx_, own_copy(ctx_, recvbuf, total), world_, sizes_in, &ms, &sv);
+  decode_into_results(ms, sv);
+}
+
+}  // namespace psf

@@ -1,0 +1,64 @@
+// The multi-server push path of one rank,
+// native: what the reference's Executor::Submit does for a kServerGroup push
+// -- slice the message at the server key ranges (SliceKOFVMessage,
+// message.h:107-147), encode each slice on the sender's per-peer RemoteNode
+// (executor.cc:127-146) -- and what each server's PickActiveMsg does with
+// what arrives (decode on its per-peer node, executor.cc:178-219), for many
+// push streams at once, with no per-slice host work outside this library.
+#pragma once
+#include <map>
+#include <memory>
+#include <utility>
+#include <vector>
+
+#include "filter.h"
+#include "spill.h"
+
+namespace psf {
+
+class PushRouter {
+ public:
+  // ranges: the S server key ranges (contiguous); server s lives on rank
+  // s * world / S.  loopback: local slices go through the exchange too.
+  PushRouter(Context* ctx, const std::vector<KeyRange>& ranges, int rank, int world, bool loopback);
+  ~PushRouter();
+
+  // Slice + encode every stream's message (templates are copied, as the
+  // executor copies the Task), pack the slices for other ranks; sizes[2r],
+  // sizes[2r+1] = meta / payload bytes for rank r (see SpillPlan).
+  void encode(const Message* const* streams, int n, int64_t* sizes);
+  // write the send buffer of the last encode()
+  void fill(void* sendbuf);
+  // decode the slices whose server is on this rank
+  void decode_local();
+  // unpack a receive buffer (segments of ranks 0..world-1) and decode it
+  void decode_received(const uint8_t* recvbuf, const int64_t* sizes_in);
+
+  // decoded messages of the last step: (server, message)
+  const std::vector<std::pair<int, Message>>& results() const { return results_; }
+  // encoded slices of the last step: (stream key_channel, server, message)
+  struct Encoded { int32_t stream; int server; Message msg; };
+  const std::vector<Encoded>& encoded() const { return enc_; }
+  void keep_encoded(bool v) { keep_enc_ = v; }
+  int owner(int server) const { return (int)((int64_t)server * world_ / (int64_t)ranges_.size()); }
+  int world() const { return world_; }
+
+ private:
+  RemoteNode* sender(int32_t stream, int server);
+  RemoteNode* receiver(int server, int32_t stream);
+  void decode_into_results(std::vector<Message>& ms, const std::vector<int>& servers);
+
+  Context* ctx_;
+  std::vector<KeyRange> ranges_;
+  int rank_, world_;
+  bool loopback_;
+  bool keep_enc_ = false;
+  std::map<std::pair<int32_t, int>, std::unique_ptr<RemoteNode>> senders_, receivers_;
+  std::vector<Message> local_;
+  std::vector<int> local_server_;
+  std::unique_ptr<SpillPlan> plan_;
+  std::vector<std::pair<int, Message>> results_;
+  std::vector<Encoded> enc_;
+};
+
+}  // namespace psf

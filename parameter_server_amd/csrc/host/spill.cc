@@ -131,10 +131,28 @@ void SpillPlan::fill(void* sendbuf) {
   keep_.clear();
 }
 
-int spill_unpack(Context* ctx, const uint8_t* recv, int world, const int64_t* sizes, std::vector<Message>* out,
+Buffer own_copy(Context* ctx, const void* p, size_t bytes) {
+  if (ctx->device() >= 0) {
+    Buffer b = ctx->alloc(bytes);
+    if (bytes) PSF_HIP_CHECK(hipMemcpyAsync(b.ptr, p, bytes, hipMemcpyDeviceToDevice, ctx->stream()));
+    return b;
+  }
+  Buffer b;
+  b.loc = Loc::kHost;
+  b.bytes = bytes;
+  if (!bytes) return b;
+  uint8_t* q = new uint8_t[bytes];
+  memcpy(q, p, bytes);
+  b.owner = std::shared_ptr<void>(q, [](void* v) { delete[] static_cast<uint8_t*>(v); });
+  b.ptr = q;
+  return b;
+}
+
+int spill_unpack(Context* ctx, const Buffer& rbuf, int world, const int64_t* sizes, std::vector<Message>* out,
                  std::vector<int>* servers) {
   out->clear();
   servers->clear();
+  const uint8_t* recv = rbuf.ptr;
   uint64_t at = 0;
   std::vector<uint8_t> meta;
   for (int s = 0; s < world; ++s) {
@@ -172,8 +190,10 @@ int spill_unpack(Context* ctx, const uint8_t* recv, int world, const int64_t* si
       size_t f = 0;
       auto frame = [&]() {
         Buffer b;
+        b.owner = rbuf.owner;
         b.bytes = fl[f];
         b.ptr = b.bytes ? const_cast<uint8_t*>(pay + poff) : nullptr;
+        if (!b.bytes) b.owner.reset();
         b.loc = ctx->device() < 0 ? Loc::kHost : Loc::kDevice;
         poff += up(fl[f], 256);
         if (poff > plen) throw CheckError(kErrCheck, "spill frames overrun the payload");

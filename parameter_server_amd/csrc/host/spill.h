@@ -36,8 +36,13 @@ class SpillPlan {
 
 // Rebuild the messages of a receive buffer laid out by SpillPlan (segments of
 // sources 0..world-1 back to back, sizes as the senders reported them).  The
-// messages' frames point into `recv` (the caller keeps it alive).
-int spill_unpack(Context* ctx, const uint8_t* recv, int world, const int64_t* sizes, std::vector<Message>* out,
+// messages' frames point into `recv` and share its owner (recv.owner null:
+// the caller keeps the memory alive).
+int spill_unpack(Context* ctx, const Buffer& recv, int world, const int64_t* sizes, std::vector<Message>* out,
                  std::vector<int>* servers);
+// A copy of `bytes` at p that the library owns (HBM on a device context, heap
+// memory on a host-only one), so received frames can outlive the caller's
+// buffer (KEY_CACHING keeps received keys by reference, key_caching.h:45-47).
+Buffer own_copy(Context* ctx, const void* p, size_t bytes);
 
 }  // namespace psf

@@ -3,25 +3,25 @@
 Server s owns Range<Key>(key_start, key_end).EvenDivide(S, s)
 (src/system/assigner.h:17-28, src/util/range.h:100-107); servers live on ranks
 in contiguous blocks (rank r hosts servers [r*S/W, (r+1)*S/W), one server per
-GPU when S == W).  A push/pull message is sliced at the server ranges
+GPU when S == W).  A push message is sliced at the server ranges
 (SliceKOFVMessage, src/system/message.h:107-147), each slice is encoded by the
 sender's per-(stream, server) RemoteNode (executor.cc:131-146) and delivered to
-its server, whose per-(server, stream) RemoteNode decodes it.
+its server, whose per-(server, stream) RemoteNode decodes it -- all inside
+libpsf (psf_router_*), one native call per phase of a step.
 
 The only data-path collective is the cross-range spill: slices whose server
 lives on another rank travel in one all-to-all-v per step (RCCL over xGMI with
 the "nccl" backend; gloo for the CPU tests).  What travels is the ENCODED
 slice -- the reference's wire frames [Task][key][value...] (van.cc:122-191),
-laid out by libpsf (psf_spill_pack / psf_spill_fill, one gather launch) and
-rebuilt zero-copy on the receiver (psf_spill_unpack) -- so KEY_CACHING hits
-and FIXING_FLOAT's 4x shrink cut the xGMI bytes too.  Per step the host does
-one small all-to-all of segment sizes (one device->host read) and one
-all-to-all-v of bytes; no per-frame or per-peer host work.
+laid out by libpsf in one gather launch and rebuilt on the receiver -- so
+KEY_CACHING hits and FIXING_FLOAT's 4x shrink cut the xGMI bytes too.  Per
+step the host does one small all-to-all of segment sizes (one device->host
+read) and one all-to-all-v of bytes; no per-slice or per-frame host work.
 """
 from __future__ import annotations
 
 import ctypes as C
-from typing import List, Optional, Sequence
+from typing import List, Sequence
 
 import torch
 
@@ -47,6 +47,14 @@ def server_rank(server: int, nservers: int, world: int) -> int:
     return server * world // nservers
 
 
+def _bounds(ranges: Sequence):
+    n = len(ranges)
+    for i in range(1, n):
+        if ranges[i - 1][1] != ranges[i][0]:
+            raise ValueError("ranges must be contiguous (message.h:120)")
+    return (C.c_uint64 * (n + 1))(*([r[0] for r in ranges[:1]] + [r[1] for r in ranges]))
+
+
 def slice_message(ctx, msg, ranges: Sequence, key_bytes: int = 8):
     """SliceKOFVMessage: returns one Message per range, or None where the range
     misses the message's key range (the reference marks those invalid and
@@ -59,10 +67,7 @@ def slice_messages(ctx, msgs, ranges: Sequence, key_bytes: int = 8):
     returns one list per message."""
     from .filter import Message
     n, M = len(ranges), len(msgs)
-    for i in range(1, n):
-        if ranges[i - 1][1] != ranges[i][0]:
-            raise ValueError("ranges must be contiguous (message.h:120)")
-    bounds = (C.c_uint64 * (n + 1))(*([r[0] for r in ranges[:1]] + [r[1] for r in ranges]))
+    bounds = _bounds(ranges)
     outs = (C.c_void_p * (n * M))()
     valid = (C.c_int * (n * M))()
     hs = (C.c_void_p * M)(*[m.h.value for m in msgs])
@@ -84,8 +89,9 @@ def w_channel(m) -> int:
 
 
 class SpillExchange:
-    """The cross-range spill of one step: encoded messages -> their ranks, in
-    one all-to-all-v (plus one all-to-all of the 2 x world segment sizes).
+    """The collective side of the cross-range spill: one all-to-all of the
+    2 x world segment sizes (meta, payload) and one all-to-all-v of the
+    bytes, over `group`.
 
     `device` is where the buffers live ("cuda:k" with RCCL; with gloo, device
     buffers are staged through host memory, which is what the CPU tests and
@@ -97,132 +103,170 @@ class SpillExchange:
         self.ctx = ctx
         self.group = group
         self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
         self.device = device if device is not None else (
             f"cuda:{ctx.device}" if ctx.device >= 0 else "cpu")
         self.staged = dist.get_backend(group) == "gloo" and str(self.device).startswith("cuda")
+        self.wire = "cpu" if self.staged else self.device
         self.bytes_sent = 0
+        self._send = torch.empty(0, dtype=torch.uint8, device=self.device)
+        self._recv = torch.empty(0, dtype=torch.uint8, device=self.wire)
+
+    def sizes(self, sizes) -> List[int]:
+        """all-to-all of this rank's 2 x world segment sizes; returns what
+        every source reports for this rank (the step's one device->host read)."""
+        t = torch.tensor(list(sizes), dtype=torch.int64)
+        out = torch.empty_like(t)
+        if self.wire != "cpu":
+            t, out = t.to(self.wire, non_blocking=True), out.to(self.wire)
+        self.dist.all_to_all_single(out, t, group=self.group)
+        return out.cpu().tolist()
+
+    def send_buffer(self, nbytes: int) -> torch.Tensor:
+        if self._send.numel() < nbytes:
+            self._send = torch.empty(max(nbytes, 2 * self._send.numel()), dtype=torch.uint8, device=self.device)
+        return self._send
+
+    def move(self, sizes, sizes_in, after_send=None) -> torch.Tensor:
+        """The all-to-all-v of the filled send buffer; `after_send` (device
+        work that does not touch the buffers) is queued while it runs.
+        Returns the receive buffer on the context's device."""
+        W = self.world
+        in_splits = [sizes[2 * r] + sizes[2 * r + 1] for r in range(W)]
+        out_splits = [sizes_in[2 * s] + sizes_in[2 * s + 1] for s in range(W)]
+        self.bytes_sent += sum(in_splits) - in_splits[self.rank]
+        nout = sum(out_splits)
+        if self._recv.numel() < nout:
+            self._recv = torch.empty(max(nout, 2 * self._recv.numel()), dtype=torch.uint8, device=self.wire)
+        send = self._send[:sum(in_splits)]
+        recv = self._recv[:nout]
+        if self.staged:
+            self.ctx.sync()
+            send = send.cpu()
+        work = self.dist.all_to_all_single(recv, send, out_splits, in_splits, group=self.group, async_op=True)
+        if after_send is not None:
+            after_send()
+        work.wait()
+        return recv.to(self.device) if self.staged else recv
 
     def exchange(self, msgs, dest: List[int], server: List[int]):
-        """Send msgs[i] to rank dest[i] (addressed to server server[i]);
-        returns (received messages, their servers)."""
+        """Message-level spill (psf_spill_pack / fill / unpack): send msgs[i]
+        to rank dest[i] addressed to server server[i]; returns (received
+        messages, their servers)."""
         from .filter import Message
-        dist, W, L = self.dist, self.world, lib()
-        n = len(msgs)
+        L, W, n = lib(), self.world, len(msgs)
         sizes = (C.c_int64 * (2 * W))()
         plan = C.c_void_p()
         check(L.psf_spill_pack(self.ctx.h, (C.c_void_p * n)(*[m.h.value for m in msgs]),
                                (C.c_int * n)(*dest), (C.c_int * n)(*server), n, W, sizes, C.byref(plan)))
         try:
-            wire_dev = "cpu" if self.staged else self.device
-            size_t = torch.tensor(list(sizes), dtype=torch.int64)
-            size_in = torch.empty_like(size_t)
-            if wire_dev != "cpu":
-                size_t, size_in = size_t.to(wire_dev, non_blocking=True), size_in.to(wire_dev)
-            dist.all_to_all_single(size_in, size_t, group=self.group)
-            sizes_in = size_in.cpu().tolist()  # the one device->host read of the step
-            in_splits = [sizes[2 * r] + sizes[2 * r + 1] for r in range(W)]
-            out_splits = [sizes_in[2 * s] + sizes_in[2 * s + 1] for s in range(W)]
-            sendbuf = torch.empty(max(sum(in_splits), 1), dtype=torch.uint8, device=self.device)
-            check(L.psf_spill_fill(plan, C.c_void_p(sendbuf.data_ptr())))
+            sizes_in = self.sizes(sizes)
+            buf = self.send_buffer(sum(sizes))
+            check(L.psf_spill_fill(plan, C.c_void_p(buf.data_ptr())))
         finally:
             L.psf_spill_destroy(plan)
-        self.bytes_sent += sum(in_splits) - in_splits[dist.get_rank(self.group)]
-        recvbuf = torch.empty(max(sum(out_splits), 1), dtype=torch.uint8, device=wire_dev)
-        if self.staged:
-            self.ctx.sync()
-            sendbuf = sendbuf.cpu()
-        dist.all_to_all_single(recvbuf[:sum(out_splits)], sendbuf[:sum(in_splits)], out_splits, in_splits,
-                               group=self.group)
-        if self.staged:
-            recvbuf = recvbuf.to(self.device)
+        recv = self.move(list(sizes), sizes_in)
         cap = max(1, sum(sizes_in[0::2]) // 24)  # a record is >= 24 bytes
         outs = (C.c_void_p * cap)()
         servers = (C.c_int * cap)()
         got = C.c_int()
-        sin = (C.c_int64 * (2 * W))(*sizes_in)
-        check(L.psf_spill_unpack(self.ctx.h, C.c_void_p(recvbuf.data_ptr()), W, sin, outs, servers, cap,
-                                 C.byref(got)))
-        res = [Message(_handle=C.c_void_p(outs[i]), _refs=[recvbuf]) for i in range(got.value)]
+        check(L.psf_spill_unpack(self.ctx.h, C.c_void_p(recv.data_ptr()), W, (C.c_int64 * (2 * W))(*sizes_in),
+                                 outs, servers, cap, C.byref(got)))
+        res = [Message(_handle=C.c_void_p(outs[i])) for i in range(got.value)]
         return res, [servers[i] for i in range(got.value)]
 
 
 class PushRouter:
-    """The multi-server push path of one rank: every
-    local stream's message is sliced at the `ranges` of S servers
-    (SliceKOFVMessage), each slice is encoded by the sender's per-(stream,
-    server) RemoteNode (executor.cc:131-146); slices whose server lives on
-    this rank are decoded here, the others travel in ONE all-to-all-v per step
-    (the cross-range spill) and are decoded by their server's per-stream node.
-    The stream id travels as the Task's key_channel.  `loopback` sends the
-    local slices through the exchange too (a world-1 run of the RCCL path)."""
+    """The multi-server push path of one rank (libpsf
+    psf_router_*): every local stream's message is sliced at the `ranges` of S
+    servers, each slice encoded by the sender's per-(stream, server) node;
+    slices whose server lives on this rank are decoded here, the others travel
+    in ONE all-to-all-v per step (the cross-range spill) and are decoded by
+    their server's per-stream node.  The stream id travels as the Task's
+    key_channel.  `loopback` sends the local slices through the exchange too
+    (a world-1 run of the RCCL path)."""
 
-    def __init__(self, ctx, ranges, rank: int, world: int, exchange: Optional[SpillExchange] = None,
+    def __init__(self, ctx, ranges, rank: int, world: int, exchange: SpillExchange = None,
                  loopback: bool = False):
-        from .filter import RemoteNode
         self.ctx, self.ranges, self.rank, self.world = ctx, ranges, rank, world
         self.nservers = len(ranges)
         if self.nservers < world:
             raise ValueError("need at least one server per rank")
-        self.exchange = exchange
         if (world > 1 or loopback) and exchange is None:
             raise ValueError("a spill exchange is needed")
-        self.loopback = loopback
-        self._RemoteNode = RemoteNode
-        self.senders, self.receivers = {}, {}
-        self.last_encoded = []  # (stream, server, encoded slice) of the last step
+        self.exchange, self.loopback = exchange, loopback
+        h = C.c_void_p()
+        check(lib().psf_router_create(ctx.h, _bounds(ranges), self.nservers, rank, world, int(loopback),
+                                      C.byref(h)))
+        self.h = h
+        self._held = {}
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().psf_router_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
 
     def owner(self, server: int) -> int:
         return server_rank(server, self.nservers, self.world)
 
-    def _sender(self, s, d):
-        if (s, d) not in self.senders:
-            self.senders[(s, d)] = self._RemoteNode(self.ctx)
-        return self.senders[(s, d)]
+    def _handles(self, streams):
+        for sid, m in streams.items():
+            if self._held.get(sid) is not m:  # nodes and caches refer to template buffers
+                self._held[sid] = m
+        msgs = list(streams.values())
+        return (C.c_void_p * len(msgs))(*[m.h.value for m in msgs]), len(msgs)
 
-    def _receiver(self, d, s):
-        if (d, s) not in self.receivers:
-            self.receivers[(d, s)] = self._RemoteNode(self.ctx)
-        return self.receivers[(d, s)]
+    def run(self, streams, steps: int) -> None:
+        """`steps` whole steps; world 1 without loopback: one native call."""
+        if self.world == 1 and not self.loopback:
+            hs, n = self._handles(streams)
+            check(lib().psf_router_step(self.h, hs, n, steps))
+            return
+        for _ in range(steps):
+            self.step(streams)
 
-    def step(self, streams, keep_encoded: bool = False) -> list:
+    def step(self, streams, keep_encoded: bool = False) -> None:
         """streams: {stream id: template Message (key_channel = stream id)} of
-        this rank.  Returns [(server, decoded message)] of what this rank's
-        servers received.  All slices of the step are encoded in one batched
-        call (psf_nodes_encode) and all received ones decoded in one
-        (psf_nodes_decode)."""
-        from .filter import RemoteNode
-        enc_nodes, enc_msgs, dest = [], [], []
-        sids = list(streams)
-        clones = [streams[sid].clone() for sid in sids]
-        for sid, parts in zip(sids, slice_messages(self.ctx, clones, self.ranges)):
-            for d, part in enumerate(parts):
-                if part is None:
-                    continue
-                enc_nodes.append(self._sender(sid, d))
-                enc_msgs.append(part)
-                dest.append((sid, d))
-        if enc_msgs:
-            RemoteNode.encode_many(enc_nodes, enc_msgs)
-        self.last_encoded = list(zip(dest, enc_msgs)) if keep_encoded else []
-        dec_nodes, dec_msgs, got = [], [], []
-        out_m, out_r, out_s = [], [], []
-        for (sid, d), part in zip(dest, enc_msgs):
-            r = self.owner(d)
-            if r == self.rank and not self.loopback:
-                w = part.clone()  # delivered copy (Task + zero-copy buffers)
-                dec_nodes.append(self._receiver(d, sid))
-                dec_msgs.append(w)
-                got.append((d, w))
-            else:
-                out_m.append(part)
-                out_r.append(r)
-                out_s.append(d)
-        if self.world > 1 or self.loopback:
-            recv, servers = self.exchange.exchange(out_m, out_r, out_s)
-            for w, d in zip(recv, servers):
-                dec_nodes.append(self._receiver(d, w_channel(w)))
-                dec_msgs.append(w)
-                got.append((d, w))
-        if dec_msgs:
-            RemoteNode.decode_many(dec_nodes, dec_msgs)
-        return got
+        this rank.  The decoded messages this rank's servers received are in
+        results(); with keep_encoded, the encoded slices in encoded()."""
+        L = lib()
+        check(L.psf_router_keep_encoded(self.h, int(keep_encoded)))
+        hs, n = self._handles(streams)
+        if self.world == 1 and not self.loopback:
+            check(L.psf_router_step(self.h, hs, n, 1))
+            return
+        W = self.world
+        sizes = (C.c_int64 * (2 * W))()
+        check(L.psf_router_encode(self.h, hs, n, sizes))
+        ex = self.exchange
+        sizes_in = ex.sizes(sizes)
+        buf = ex.send_buffer(sum(sizes))
+        check(L.psf_router_fill(self.h, C.c_void_p(buf.data_ptr())))
+        recv = ex.move(list(sizes), sizes_in, after_send=lambda: check(L.psf_router_decode_local(self.h)))
+        check(L.psf_router_decode_received(self.h, C.c_void_p(recv.data_ptr()),
+                                           (C.c_int64 * (2 * W))(*sizes_in)))
+
+    def results(self):
+        """[(server, decoded Message)] of the last step."""
+        from .filter import Message
+        L = lib()
+        out = []
+        for i in range(check(L.psf_router_num_results(self.h))):
+            s, h = C.c_int(), C.c_void_p()
+            check(L.psf_router_result(self.h, i, C.byref(s), C.byref(h)))
+            out.append((s.value, Message(_handle=h)))
+        return out
+
+    def encoded(self):
+        """[((stream, server), encoded Message)] of the last step (keep_encoded)."""
+        from .filter import Message
+        L = lib()
+        out = []
+        for i in range(check(L.psf_router_num_encoded(self.h))):
+            st, s, h = C.c_int32(), C.c_int(), C.c_void_p()
+            check(L.psf_router_encoded(self.h, i, C.byref(st), C.byref(s), C.byref(h)))
+            out.append(((st.value, s.value), Message(_handle=h)))
+        return out

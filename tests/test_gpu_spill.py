@@ -103,11 +103,9 @@ def test_push_router_64_streams_8_servers():
     port = oracle.Port()
     expect = {(d, s) for d in range(S) for s in range(STREAMS)}
     for step in range(2):
-        got = router.step(streams)
+        router.step(streams)
         torch.cuda.synchronize()
-        _check_step(F, got, ranges, M, 1, port, expect)
-    # the second step was a KEY_CACHING hit on every (stream, server) node
-    assert len(router.senders) == STREAMS * S and len(router.receivers) == STREAMS * S
+        _check_step(F, router.results(), ranges, M, 1, port, expect)
 
 
 def test_c5_rows_dim128_full_chain_8_servers():
@@ -127,10 +125,12 @@ def test_c5_rows_dim128_full_chain_8_servers():
     port = oracle.Port()
     keys, vals = _stream_data(0, M, DIM)
     for step in range(2):
-        got = router.step(streams, keep_encoded=True)
+        router.step(streams, keep_encoded=True)
         torch.cuda.synchronize()
-        _check_step(F, got, ranges, M, DIM, port, {(d, 0) for d in range(S)})
-        for (sid, d), enc in router.last_encoded:
+        _check_step(F, router.results(), ranges, M, DIM, port, {(d, 0) for d in range(S)})
+        encoded = router.encoded()
+        assert sorted(k for k, _ in encoded) == [(0, d) for d in range(S)]
+        for (sid, d), enc in encoded:
             lo, hi = ranges[d]
             sel = (keys >= np.uint64(lo)) & (keys < np.uint64(hi))
             st, codes, mn, mx = port.ff_encode(vals.reshape(-1, DIM)[sel].reshape(-1), 1, SEED)
@@ -172,9 +172,9 @@ def _spill_worker(rank, world, port, backend, loopback, q):
         expect = {(d, s) for d in mine for s in range(STREAMS)}
         sent = []
         for step in range(2):
-            got = router.step(streams)
+            router.step(streams)
             torch.cuda.synchronize()
-            _check_step(F, got, ranges, M, 1, port_, expect)
+            _check_step(F, router.results(), ranges, M, 1, port_, expect)
             sent.append(ex.bytes_sent)
         q.put((rank, True, sent))
     except Exception as e:  # report instead of hanging the parent

@@ -157,6 +157,76 @@ def test_spill_exchange_gloo_world2():
     assert res == {0: True, 1: True}
 
 
+def _router_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    from bench import splitmix64_keys
+    from parameter_server_amd import KEY_CACHING
+    from parameter_server_amd import filter as F
+    from parameter_server_amd import shard
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ctx = F.HostContext()
+        ranges = shard.server_ranges(5)  # 5 servers over 2 ranks: blocks of 2 and 3
+        router = shard.PushRouter(ctx, ranges, rank, world, shard.SpillExchange(ctx))
+        sids = [10 * r + j for r in range(world) for j in range(3)]
+        data = {s: (splitmix64_keys(700 + s, 4 + s),) for s in sids}
+        data = {s: (k[0], np.random.default_rng(s).standard_normal(2 * k[0].size).astype(np.float32))
+                for s, k in data.items()}
+        streams = {}
+        for s in sids:
+            if s // 10 != rank:
+                continue
+            keys, vals = data[s]
+            m = F.Message(request=True, push=True, key_channel=s, key_range=shard.KEY_ALL)
+            m.set_key(torch.from_numpy(keys.view(np.int64).copy()))
+            m.add_value(torch.from_numpy(vals.copy()))
+            m.add_filter(KEY_CACHING)
+            streams[s] = m
+        mine = [d for d in range(5) if shard.server_rank(d, 5, world) == rank]
+        ok = True
+        for step in range(2):  # miss (keys travel), then hit (keys elided, restored)
+            router.step(streams)
+            seen = set()
+            for d, w in router.results():
+                s = shard.w_channel(w)
+                seen.add((d, s))
+                keys, vals = data[s]
+                lo, hi = ranges[d]
+                sel = (keys >= np.uint64(lo)) & (keys < np.uint64(hi))
+                p, nb, _ = w.key_ptr()
+                kb = bytes((np.ctypeslib.ctypes.c_uint8 * nb).from_address(p)) if nb else b""
+                vp, vb, _ = w.value_ptr(0)
+                vbytes = bytes((np.ctypeslib.ctypes.c_uint8 * vb).from_address(vp)) if vb else b""
+                ok &= kb == keys[sel].tobytes() and vbytes == vals.reshape(-1, 2)[sel].tobytes()
+            ok &= seen == {(d, s) for d in mine for s in sids}
+        q.put((rank, bool(ok)))
+    except Exception as e:  # report instead of hanging the parent
+        import traceback
+        q.put((rank, repr(e) + traceback.format_exc()[-1500:]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_push_router_gloo_world2_host():
+    """The native router (psf_router_*) across two ranks on CPU: 6 streams, 5
+    servers (2 on rank 0, 3 on rank 1), host keys, [KEY_CACHING]; every
+    server's decoded slices equal the restated slicing, on the miss and the
+    hit step."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_router_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: True, 1: True}, res
+
+
 def test_bench_launcher_gloo_world2():
     """`bench.py --gpus 2` starts its two ranks itself (no torchrun) and the
     process group really has two members (launch plumbing only, on CPU)."""
