@@ -136,6 +136,11 @@ template <> struct Vec4<float> {
 #endif
     v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
   }
+  // only element-aligned (a slice of a value array, message.h:141-143)
+  __device__ static void loadu(const float* p, float v[4]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = __builtin_nontemporal_load(p + j);
+  }
   __device__ static void store(float* p, const float v[4]) {
     f32x4 t = {v[0], v[1], v[2], v[3]};
     __builtin_nontemporal_store(t, reinterpret_cast<f32x4*>(p));
@@ -146,6 +151,10 @@ template <> struct Vec4<double> {
     f64x2 a = __builtin_nontemporal_load(reinterpret_cast<const f64x2*>(p));
     f64x2 b = __builtin_nontemporal_load(reinterpret_cast<const f64x2*>(p) + 1);
     v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
+  }
+  __device__ static void loadu(const double* p, double v[4]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = __builtin_nontemporal_load(p + j);
   }
   __device__ static void store(double* p, const double v[4]) {
     f64x2 a = {v[0], v[1]}, b = {v[2], v[3]};
@@ -853,6 +862,7 @@ __global__ __launch_bounds__(kBlock) void ff_minmax_batch(FfBatch B) {
   const V* __restrict__ x = static_cast<const V*>(J.x);
   const size_t n = J.n;
   const uint32_t wg = blockIdx.x - B.mm_first[jb];
+  const bool al = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
   K lo = KeyOf<V>::kLoId, hi = KeyOf<V>::kHiId;
   const size_t ngroups = n >> 2;
   const size_t ntiles = (ngroups + kTileGroups - 1) / kTileGroups;
@@ -863,8 +873,13 @@ __global__ __launch_bounds__(kBlock) void ff_minmax_batch(FfBatch B) {
   for (size_t t = t0; t < tf; ++t) {  // full tiles: all four loads in flight before the folds
     const size_t gb = t * kTileGroups + threadIdx.x;
     V v[4][4];
+    if (al) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) Vec4<V>::load(x + 4 * (gb + u * kBlock), v[u]);
+      for (int u = 0; u < 4; ++u) Vec4<V>::load(x + 4 * (gb + u * kBlock), v[u]);
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) Vec4<V>::loadu(x + 4 * (gb + u * kBlock), v[u]);
+    }
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
@@ -877,7 +892,8 @@ __global__ __launch_bounds__(kBlock) void ff_minmax_batch(FfBatch B) {
       const size_t g = gb + u * kBlock;
       if (g < ngroups) {
         V v[4];
-        Vec4<V>::load(x + 4 * g, v);
+        if (al) Vec4<V>::load(x + 4 * g, v);
+        else Vec4<V>::loadu(x + 4 * g, v);
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc_minmax<V, K>(v[j], lo, hi);
       }
@@ -973,11 +989,17 @@ __global__ __launch_bounds__(kBlock) void ff_encode_batch(FfBatch B) {
   size_t t0, t1;
   tile_range_of(ntiles, wg, nwg, t0, t1);
   const size_t tf = t1 < nfull ? t1 : nfull;
+  const bool al = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
   for (size_t t = t0; t < tf; ++t) {
     const size_t gb = t * kTileGroups + threadIdx.x;
     V v[4][4];
+    if (al) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) Vec4<V>::load(x + 4 * (gb + u * kBlock), v[u]);
+      for (int u = 0; u < 4; ++u) Vec4<V>::load(x + 4 * (gb + u * kBlock), v[u]);
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) Vec4<V>::loadu(x + 4 * (gb + u * kBlock), v[u]);
+    }
     encode_full_tile<V, NB>(v, q, p, out, gb);
   }
   for (size_t t = (t0 > tf ? t0 : tf); t < t1; ++t) {
@@ -988,7 +1010,8 @@ __global__ __launch_bounds__(kBlock) void ff_encode_batch(FfBatch B) {
       const size_t g = gb + u * kBlock;
       if (g < ngroups) {
         V v[4];
-        Vec4<V>::load(x + 4 * g, v);
+        if (al) Vec4<V>::load(x + 4 * g, v);
+        else Vec4<V>::loadu(x + 4 * g, v);
         uint64_t r[4];
         quant_group<V, NB>(v, q, su, p.k17, r);
         store_codes<NB>(out, g, r);
@@ -1253,11 +1276,16 @@ int ff_decode_launch(const void* code, size_t n, int value_type, int nb, const f
 
 
 // ------------------------------------------------------ batched launchers ---
-bool ff_batchable(const void* x, const void* out, size_t n, int nb, bool encode) {
+bool ff_batchable(const void* x, const void* out, size_t n, int nb, int value_type, bool encode) {
   if (nb < 1 || nb > 3 || n == 0 || n >= (1ull << 32)) return false;
   const uintptr_t xa = reinterpret_cast<uintptr_t>(x), oa = reinterpret_cast<uintptr_t>(out);
   const uintptr_t code_align = nb == 2 ? 7 : 3;
-  return encode ? ((xa & 15) == 0 && (oa & code_align) == 0) : ((oa & 15) == 0 && (xa & code_align) == 0);
+  // encode: values element-aligned (slices of a value array, message.h:141-143,
+  // start at any element; the batched kernels load unaligned groups element
+  // by element), codes aligned for the packed stores
+  const uintptr_t elem_align = value_type == kDouble ? 7 : 3;
+  return encode ? ((xa & elem_align) == 0 && (oa & code_align) == 0)
+                : ((oa & 15) == 0 && (xa & code_align) == 0);
 }
 
 template <typename V, int NB>

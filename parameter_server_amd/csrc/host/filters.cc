@@ -181,7 +181,7 @@ void for_each_batch(std::vector<FfJob>& jobs, size_t b, size_t e, bool encode, F
   std::map<std::pair<int, int>, std::vector<size_t>> groups;
   for (size_t q = b; q < e; ++q) {
     FfJob& j = jobs[q];
-    if (e - b > 1 && ff_batchable(j.in.ptr, j.out.ptr, j.elems, j.nb, encode))
+    if (e - b > 1 && ff_batchable(j.in.ptr, j.out.ptr, j.elems, j.nb, j.type, encode))
       groups[{j.type, j.nb}].push_back(q);
     else
       launch_one(q);

@@ -19,13 +19,14 @@
 //
 // Exactness: the engine, the uniforms, x, y, r2 and the acceptance test are
 // exact IEEE operations, identical to libstdc++'s.  mult = sqrt(-2 log(r2)/r2)
-// uses correctly rounded sqrt/division and, for f32, glibc's own logf algorithm
-// (glibc_logf.h) -> f32 NOISE is bit-exact.  For f64 the device's double log is
-// used; glibc's log may differ from it in the last bit in rare cases (the
-// tolerance is written in tests/test_gpu_noise.py).
+// uses correctly rounded sqrt/division and glibc's own log algorithms --
+// logf for f32 (glibc_logf.h), log for f64 (glibc_log.h, including the fused
+// multiply-adds of the FMA build the reference's host runs) -> NOISE is
+// bit-exact for both types.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "glibc_log.h"
 #include "glibc_logf.h"
 #include "psf_internal.h"
 
@@ -112,7 +113,8 @@ template <> struct Polar<double> {
     const double b = __dadd_rn(__dmul_rn(2.0, uniform(x)), -1.0);
     const double r2 = __dadd_rn(__dmul_rn(a, a), __dmul_rn(b, b));
     if (r2 > 1.0 || r2 == 0.0) return false;
-    const double mult = __dsqrt_rn(__ddiv_rn(__dmul_rn(-2.0, log(r2)), r2));
+    const double lg = glibc_log(r2);  // the reference's libm log, bit for bit
+    const double mult = __dsqrt_rn(__ddiv_rn(__dmul_rn(-2.0, lg), r2));
     z0 = __dmul_rn(b, mult);
     z1 = __dmul_rn(a, mult);
     return true;

@@ -134,7 +134,7 @@ struct FfDecArray {
   float mn, mx;
   const float* range;  // device {min, max} written by the encode, or null (use mn, mx)
 };
-bool ff_batchable(const void* x, const void* out, size_t n, int nb, bool encode);
+bool ff_batchable(const void* x, const void* out, size_t n, int nb, int value_type, bool encode);
 size_t ff_batch_partials_bytes(const FfArray* arrs, int count);
 int ff_encode_batch_launch(int value_type, int nb, const FfArray* arrs, int count, void* partials,
                            PubSlot* pub_base, hipStream_t st, Profiler* prof);

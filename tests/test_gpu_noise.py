@@ -1,11 +1,10 @@
 """GPU parity for NOISE (add_noise.h:11-39) through the message path.
 
 The engine draws, uniforms, polar coordinates and acceptance decisions are
-exact IEEE operations reproduced bit for bit, and f32 uses glibc's own logf
-algorithm, so f32 NOISE must be bit-identical to the reference.  f64 uses the
-device's double log, which may differ from glibc's log in the last bit: the
-tolerance written here is >= 95 % bit-identical (measured ~98.8 %) and every
-value within 4 ulp of the z * std term."""
+exact IEEE operations reproduced bit for bit, and the logs are glibc's own
+algorithms (logf for f32, glibc_logf.h; log for f64 with the FMA build's fused
+operations, glibc_log.h), so NOISE must be bit-identical to the reference for
+both value types."""
 import os
 
 import numpy as np
@@ -39,24 +38,9 @@ def _noise_via_node(ctx, x, mean, sd):
 
 
 def _check(got, want, x, mean=0.0):
-    """f32: bit-identical (the kernel uses glibc's own logf algorithm).
-    f64: >= 95 % bit-identical, the rest within 4 ulp of z*std (a 1-ulp log
-    difference moves mult by <= 1 ulp and z = y*mult by <= 2)."""
+    """bit-identical, f32 and f64"""
     d = _ulp_diff(got, want)
-    exact = float((d == 0).mean())
-    if want.dtype == np.float32:
-        assert exact == 1.0, exact
-        return
-    # device log(double) differs from glibc's log in the last bit on ~2.7 % of
-    # inputs (tools/debug_ops64.hip); each accepted attempt yields 2 values
-    assert exact >= 0.95, exact
-    noise = want.astype(np.float64) - x.astype(np.float64)
-    zsd = np.abs(noise - mean)  # |z * std|: where a last-bit difference in z lands
-    tol = 4 * (np.spacing(zsd.astype(want.dtype)).astype(np.float64) +
-               np.spacing(np.abs(noise).astype(want.dtype)).astype(np.float64) +
-               np.spacing(np.abs(want)).astype(np.float64))
-    err = np.abs(got.astype(np.float64) - want.astype(np.float64))
-    assert (err <= tol).all(), float((err / np.maximum(tol, 1e-300)).max())
+    assert int((d != 0).sum()) == 0, (want.dtype, int((d != 0).sum()), int(d.max()))
 
 
 def test_noise_golden(ctx):

@@ -169,6 +169,21 @@ def test_noise_logf_matches_libm():
     assert out.returncode == 0, out.stdout
 
 
+def test_noise_log_matches_libm():
+    """The NOISE kernel's double log (csrc/glibc_log.h) equals this libm's log
+    (the reference's std::log(double)) bit for bit: 4 x 2M random doubles of
+    each kind (bit patterns in (0, 1], near 1, polar r2, above 1) and every
+    exponent's extreme mantissas (~3.8e8 doubles with argument 1e8: 0 found)."""
+    import subprocess
+
+    import oracle
+    exe = os.path.join(oracle.HERE, "_port", "log_check")
+    if not os.path.exists(exe):
+        oracle.build(ref=False)
+    out = subprocess.run([exe, "2000000"], capture_output=True, text=True)
+    assert out.returncode == 0 and " 0 mismatches" in out.stdout, out.stdout
+
+
 def _ref():
     import oracle
     if not os.path.exists(oracle.REF_SO):
