@@ -14,19 +14,27 @@
 // src/system/van.cc:244-255), so this adapter is the host edge: each array is
 // staged into HBM, coded by libpsf's kernels, and the result comes back as a
 // new SArray<char> -- exactly where the reference's filter would put its output
-// (fixing_float.h:37-44).  Side-info (fixed_point min/max) is written into the
-// message's own FilterConfig as the reference does.  libpsf status codes map to
-// the reference's fatal CHECK.
+// (fixing_float.h:37-44) -- or, for NOISE, into the value array itself, in
+// place, as add_noise.h:33-37 does.  Side-info (fixed_point min/max,
+// uncompressed sizes) is written into the message's own FilterConfig as the
+// reference does.  libpsf status codes map to the reference's fatal CHECK.
+//
+// Concurrency: RemoteNode creates one filter instance per type per peer
+// (remote_node.cc:7-15), the calls of one instance are serialised by its
+// Customer's Executor::node_mu_ (executor.cc:110,143,170), and different
+// Customers' executor threads run their instances concurrently (SURVEY.md
+// §8(b)).  So every adapter instance owns its libpsf context -- a private HIP
+// stream, workspace and allocator -- and no lock is shared between instances.
 //
 // Filters adapted: FIXING_FLOAT, COMPRESSING (snappy 1.1.8-identical streams)
 // and NOISE.  KEY_CACHING on host-resident keys is 2 KiB of CRC plus a hash
-// map -- libpsf runs it on the host too -- so CreateFilter returns nullptr for
-// it and the reference's own class is used.
+// map whose entries reference the caller's key SArrays (key_caching.h:27-28):
+// CreateFilter returns nullptr for it and the reference's own class is used
+// (device-resident keys go through psf_node_* directly).
 #pragma once
 #include <stdint.h>
 #include <string.h>
 
-#include <mutex>
 #include <string>
 
 #include "psf.h"
@@ -34,34 +42,54 @@
 namespace PS {
 namespace psf_hip {
 
-// one libpsf context (device 0, private stream) per process, created lazily
-inline psf_context* Context() {
-  static psf_context* ctx = [] {
-    psf_context* c = nullptr;
-    int st = psf_context_create(0, nullptr, 1, &c);
-    CHECK_EQ(st, PSF_OK) << "libpsf: " << psf_last_error();
-    return c;
-  }();
-  return ctx;
-}
-
-// The context's stream, publish slots and caching allocator are not
-// thread-safe, and filters of different Customers run on different executor
-// threads: every adapter call holds this one lock.
-inline std::mutex& ContextMutex() {
-  static std::mutex mu;
-  return mu;
-}
-
 inline void Check(int st) { CHECK_EQ(st, PSF_OK) << "libpsf: " << psf_last_error(); }
 
-// FixingFloatFilter (src/filter/fixing_float.h:6-103) on MI355X.
-class FixingFloatFilter : public Filter {
- public:
-  FixingFloatFilter() {
-    Check(psf_node_create(Context(), &node_));
+// One filter instance's libpsf state: a context on device 0 with its own
+// non-blocking stream, and a RemoteNode holding the libpsf filter instances.
+class Bound {
+ protected:
+  Bound() {
+    Check(psf_context_create(0, nullptr, 1, &ctx_));
+    Check(psf_node_create(ctx_, &node_));
   }
-  ~FixingFloatFilter() { psf_node_destroy(node_); }
+  ~Bound() {
+    psf_node_destroy(node_);
+    psf_context_destroy(ctx_);
+  }
+  // the Task fields the filters read (task.proto:28-39)
+  psf_message* NewMessage(const Task& t) {
+    psf_message* m = nullptr;
+    Check(psf_msg_create(t.request(), t.has_param(), t.has_param() && t.param().push(), t.key_channel(),
+                         t.has_key_range(), t.key_range().begin(), t.key_range().end(), &m));
+    return m;
+  }
+  void Run(psf_message* m, bool encode, const char* what) {
+    const int st = encode ? psf_node_encode(node_, m) : psf_node_decode(node_, m);
+    if (st != PSF_OK) {
+      std::string err = psf_last_error();
+      psf_msg_destroy(m);
+      CHECK(false) << "libpsf " << what << ": " << err;
+    }
+  }
+  // array i (-1 = key) of the libpsf message as an SArray<char>; the input
+  // array itself when libpsf left it in place
+  SArray<char> Take(psf_message* m, int i, const SArray<char>& in) {
+    void* p = nullptr;
+    size_t bytes = 0;
+    int loc = 0;
+    Check(i < 0 ? psf_msg_key(m, &p, &bytes, &loc) : psf_msg_value(m, i, &p, &bytes, &loc));
+    if (p == in.data() && bytes == in.size()) return in;
+    SArray<char> out(bytes);
+    if (bytes) Check(psf_copy_to_host(ctx_, out.data(), p, bytes));
+    return out;
+  }
+  psf_context* ctx_ = nullptr;
+  psf_node* node_ = nullptr;
+};
+
+// FixingFloatFilter (src/filter/fixing_float.h:6-103) on MI355X.
+class FixingFloatFilter : public Filter, Bound {
+ public:
   void encode(Message* msg) { convert(msg, true); }
   void decode(Message* msg) { convert(msg, false); }
 
@@ -69,17 +97,12 @@ class FixingFloatFilter : public Filter {
   void convert(Message* msg, bool encode) {
     FilterConfig* conf = CHECK_NOTNULL(find(FilterConfig::FIXING_FLOAT, msg));
     if (conf->num_bytes() == 0) return;
-    std::lock_guard<std::mutex> l(ContextMutex());
-    // Task + values as libpsf messages (host buffers, not copied)
-    psf_message* m = nullptr;
     const Task& t = msg->task;
-    Check(psf_msg_create(t.request(), t.has_param(), t.has_param() && t.param().push(),
-                         t.key_channel(), t.has_key_range(), t.key_range().begin(),
-                         t.key_range().end(), &m));
-    for (size_t i = 0; i < msg->value.size(); ++i) {
-      int vt = i < (size_t)t.value_type_size() ? (int)t.value_type(i) : 0;
-      Check(psf_msg_add_value(m, msg->value[i].data(), msg->value[i].size(), vt, PSF_LOC_HOST));
-    }
+    CHECK_EQ(msg->value.size(), (size_t)t.value_type_size());  // fixing_float.h:28
+    // Task + values as a libpsf message (host buffers, not copied)
+    psf_message* m = NewMessage(t);
+    for (size_t i = 0; i < msg->value.size(); ++i)
+      Check(psf_msg_add_value(m, msg->value[i].data(), msg->value[i].size(), (int)t.value_type(i), PSF_LOC_HOST));
     int fi = psf_msg_add_filter(m, PSF_FIXING_FLOAT);
     Check(fi < 0 ? fi : PSF_OK);
     Check(psf_fc_set_num_bytes(m, fi, conf->num_bytes()));
@@ -88,24 +111,10 @@ class FixingFloatFilter : public Filter {
       psf_fixed_point p = {f.has_min_value(), f.has_max_value(), f.min_value(), f.max_value()};
       Check(psf_fc_add_fixed_point(m, fi, &p));
     }
-    const int st = encode ? psf_node_encode(node_, m) : psf_node_decode(node_, m);
-    if (st != PSF_OK) {
-      std::string err = psf_last_error();
-      psf_msg_destroy(m);
-      CHECK(false) << "libpsf FIXING_FLOAT: " << err;
-    }
+    Run(m, encode, "FIXING_FLOAT");
     // outputs back into the reference's message (new SArray<char>, as
     // fixing_float.h:37-44 replaces msg->value[i])
-    for (size_t i = 0; i < msg->value.size(); ++i) {
-      void* p = nullptr;
-      size_t bytes = 0;
-      int loc = 0;
-      Check(psf_msg_value(m, (int)i, &p, &bytes, &loc));
-      if (p == msg->value[i].data() && bytes == msg->value[i].size()) continue;  // untouched
-      SArray<char> out(bytes);
-      Check(psf_copy_to_host(Context(), out.data(), p, bytes));
-      msg->value[i] = out;
-    }
+    for (size_t i = 0; i < msg->value.size(); ++i) msg->value[i] = Take(m, (int)i, msg->value[i]);
     // side-info: the fixed_point list as libpsf left it
     const int nfp = psf_fc_num_fixed_point(m, fi);
     for (int k = 0; k < nfp; ++k) {
@@ -117,84 +126,73 @@ class FixingFloatFilter : public Filter {
     }
     psf_msg_destroy(m);
   }
-
-  psf_node* node_ = nullptr;
 };
 
-// One libpsf filter of `type` over the whole message: key (when present) and
-// values travel as host buffers, the FilterConfig fields that type reads are
-// copied in, outputs and side-info come back.
-//   COMPRESSING  <- src/filter/compressing.h:8-37 (uncompressed_size side-info)
-//   NOISE        <- src/filter/add_noise.h:11-39 (in place on the value arrays)
-class MessageFilter : public Filter {
+// CompressingFilter (src/filter/compressing.h:8-37): key (when present) and
+// values compressed / uncompressed, uncompressed_size side-info.
+class CompressingFilter : public Filter, Bound {
  public:
-  explicit MessageFilter(FilterConfig::Type type) : type_(type) {
-    Check(psf_node_create(Context(), &node_));
-  }
-  ~MessageFilter() { psf_node_destroy(node_); }
   void encode(Message* msg) { run(msg, true); }
   void decode(Message* msg) { run(msg, false); }
 
  private:
   void run(Message* msg, bool encode) {
-    FilterConfig* conf = find(type_, msg);
-    if (!conf) {
-      if (type_ == FilterConfig::NOISE && encode) CHECK_NOTNULL(conf);  // add_noise.h:13
-      return;
-    }
-    std::lock_guard<std::mutex> l(ContextMutex());
+    FilterConfig* conf = find(FilterConfig::COMPRESSING, msg);
+    if (!conf) return;
     const Task& t = msg->task;
-    psf_message* m = nullptr;
-    Check(psf_msg_create(t.request(), t.has_param(), t.has_param() && t.param().push(),
-                         t.key_channel(), t.has_key_range(), t.key_range().begin(),
-                         t.key_range().end(), &m));
+    psf_message* m = NewMessage(t);
     const bool had_key = msg->has_key();
     if (had_key) Check(psf_msg_set_key(m, msg->key.data(), msg->key.size(), PSF_DT_CHAR, PSF_LOC_HOST));
     for (size_t i = 0; i < msg->value.size(); ++i) {
-      int vt = i < (size_t)t.value_type_size() ? (int)t.value_type(i) : 0;
+      const int vt = i < (size_t)t.value_type_size() ? (int)t.value_type(i) : 0;  // compressing.h reads no types
       Check(psf_msg_add_value(m, msg->value[i].data(), msg->value[i].size(), vt, PSF_LOC_HOST));
     }
-    int fi = psf_msg_add_filter(m, type_);
+    int fi = psf_msg_add_filter(m, PSF_COMPRESSING);
     Check(fi < 0 ? fi : PSF_OK);
-    if (type_ == FilterConfig::NOISE) Check(psf_fc_set_noise(m, fi, conf->mean(), conf->std()));
-    if (type_ == FilterConfig::COMPRESSING)
-      for (int i = 0; i < conf->uncompressed_size_size(); ++i)
-        Check(psf_fc_add_uncompressed(m, fi, conf->uncompressed_size(i)));
-    const int st = encode ? psf_node_encode(node_, m) : psf_node_decode(node_, m);
-    if (st != PSF_OK) {
-      std::string err = psf_last_error();
-      psf_msg_destroy(m);
-      CHECK(false) << "libpsf filter " << (int)type_ << ": " << err;
+    for (int i = 0; i < conf->uncompressed_size_size(); ++i)
+      Check(psf_fc_add_uncompressed(m, fi, conf->uncompressed_size(i)));
+    Run(m, encode, "COMPRESSING");
+    if (had_key) msg->key = Take(m, -1, msg->key);
+    for (size_t i = 0; i < msg->value.size(); ++i) msg->value[i] = Take(m, (int)i, msg->value[i]);
+    conf->clear_uncompressed_size();
+    const int nu = psf_fc_num_uncompressed(m, fi);
+    for (int i = 0; i < nu; ++i) {
+      uint64_t v = 0;
+      Check(psf_fc_uncompressed(m, fi, i, &v));
+      conf->add_uncompressed_size(v);
     }
-    if (had_key) msg->key = take(m, -1, msg->key);
-    for (size_t i = 0; i < msg->value.size(); ++i) msg->value[i] = take(m, (int)i, msg->value[i]);
-    if (type_ == FilterConfig::COMPRESSING) {
-      conf->clear_uncompressed_size();
-      const int nu = psf_fc_num_uncompressed(m, fi);
-      for (int i = 0; i < nu; ++i) {
-        uint64_t v = 0;
-        Check(psf_fc_uncompressed(m, fi, i, &v));
-        conf->add_uncompressed_size(v);
+    psf_msg_destroy(m);
+  }
+};
+
+// AddNoiseFilter (src/filter/add_noise.h:9-41): the noise is added in place,
+// on the value arrays themselves, so every SArray sharing them sees it (as
+// add_noise.h:33-37 writes through its SArray<V> view).
+class AddNoiseFilter : public Filter, Bound {
+ public:
+  void encode(Message* msg) {
+    FilterConfig* conf = CHECK_NOTNULL(find(FilterConfig::NOISE, msg));  // add_noise.h:13
+    const Task& t = msg->task;
+    CHECK_EQ(msg->value.size(), (size_t)t.value_type_size());  // add_noise.h:14
+    psf_message* m = NewMessage(t);
+    for (size_t i = 0; i < msg->value.size(); ++i)
+      Check(psf_msg_add_value(m, msg->value[i].data(), msg->value[i].size(), (int)t.value_type(i), PSF_LOC_HOST));
+    int fi = psf_msg_add_filter(m, PSF_NOISE);
+    Check(fi < 0 ? fi : PSF_OK);
+    Check(psf_fc_set_noise(m, fi, conf->mean(), conf->std()));
+    Run(m, true, "NOISE");
+    for (size_t i = 0; i < msg->value.size(); ++i) {
+      void* p = nullptr;
+      size_t bytes = 0;
+      int loc = 0;
+      Check(psf_msg_value(m, (int)i, &p, &bytes, &loc));
+      if (p != msg->value[i].data() && bytes) {
+        CHECK_EQ(bytes, msg->value[i].size());
+        Check(psf_copy_to_host(ctx_, msg->value[i].data(), p, bytes));
       }
     }
     psf_msg_destroy(m);
   }
-
-  // array i (-1 = key) of the libpsf message as an SArray<char>; the input
-  // array itself when libpsf left it in place
-  static SArray<char> take(psf_message* m, int i, const SArray<char>& in) {
-    void* p = nullptr;
-    size_t bytes = 0;
-    int loc = 0;
-    Check(i < 0 ? psf_msg_key(m, &p, &bytes, &loc) : psf_msg_value(m, i, &p, &bytes, &loc));
-    if (p == in.data() && bytes == in.size()) return in;
-    SArray<char> out(bytes);
-    if (bytes) Check(psf_copy_to_host(Context(), out.data(), p, bytes));
-    return out;
-  }
-
-  FilterConfig::Type type_;
-  psf_node* node_ = nullptr;
 };
 
 // Registration hook for Filter::create (filter.cc:9-23): a libpsf filter, or
@@ -202,8 +200,8 @@ class MessageFilter : public Filter {
 inline Filter* CreateFilter(const FilterConfig& conf) {
   switch (conf.type()) {
     case FilterConfig::FIXING_FLOAT: return new FixingFloatFilter();
-    case FilterConfig::COMPRESSING: return new MessageFilter(FilterConfig::COMPRESSING);
-    case FilterConfig::NOISE: return new MessageFilter(FilterConfig::NOISE);
+    case FilterConfig::COMPRESSING: return new CompressingFilter();
+    case FilterConfig::NOISE: return new AddNoiseFilter();
     default: return nullptr;
   }
 }

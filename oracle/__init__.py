@@ -1,18 +1,28 @@
 """ORACLE TEST INFRASTRUCTURE -- the parity checker, never the product.
 
 Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
-this package.  Two CPU implementations live here:
+this package.
 
-* ``Port`` -- ``oracle/psf_port.c``: a plain-C restatement of the reference's
-  codec arithmetic (FIXING_FLOAT fixing_float.h:18-101, CRC32C crc32c.cc:292-335,
-  NOISE add_noise.h:29-39).  Builds from this repo alone; travels to the GPU box.
-* ``Ref`` -- ``oracle/_ref/libpsref.so``: the reference's UNMODIFIED filter
-  headers + filter.cc + crc32c.cc compiled from /root/reference against
-  ``oracle/ref_stub``.  Used to generate and re-check the
-  golden fixtures in tests/golden/ and to pin ``Port``.
+Parity status: the reference's filter path cannot be built in this image (it
+needs glog, gflags, Eigen, the protobuf runtime and protoc-generated code;
+SURVEY.md §8(c)), and its own tests hold no vectors for this path
+(src/test/fixing_float_test.cc is stale and asserts nothing).  So apart from
+CRC32C the oracle is a restatement, and parity is UNPINNED by the reference
+for FIXING_FLOAT, KEY_CACHING's state machine, COMPRESSING's glue and NOISE
+(DESIGN.md §3).  What is here:
 
-``keycache.KeyCacheModel`` restates the KEY_CACHING state machine
-(key_caching.h:9-75) in Python for small message sequences.
+* ``Port`` -- ``oracle/psf_port.c`` + ``snappy_port.c``: a plain-C restatement
+  of the reference's codec arithmetic (FIXING_FLOAT fixing_float.h:18-101,
+  CRC32C crc32c.cc:292-335, NOISE add_noise.h:29-39 over libstdc++'s
+  normal_distribution and this libm) and of snappy 1.1.8 (the third-party
+  library the reference links for COMPRESSING).  Builds from this repo alone;
+  travels to the GPU box.
+* ``chain`` -- the message path (Message / RemoteNode / the four filters)
+  restated in Python over ``Port``; tests/golden/scenarios.json is its record.
+* ``RefCrc32c`` -- ``oracle/_ref/libcrc32c_ref.so``: the reference's own
+  src/util/crc32c.cc compiled from /root/reference (it needs nothing else):
+  pins CRC32C, KEY_CACHING's signature, against the reference itself.
+* ``slicing`` -- SliceKOFVMessage / EvenDivide restated in numpy.
 """
 from __future__ import annotations
 
@@ -24,7 +34,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PORT_SO = os.path.join(HERE, "_port", "libpsf_port.so")
-REF_SO = os.path.join(HERE, "_ref", "libpsref.so")
+CRC_REF_SO = os.path.join(HERE, "_ref", "libcrc32c_ref.so")
 
 DT_FLOAT, DT_DOUBLE = 9, 10
 KEY_CACHING, COMPRESSING, FIXING_FLOAT, NOISE = 1, 2, 3, 4
@@ -33,15 +43,16 @@ PORT_OK, PORT_ERR_ARG, PORT_ERR_NBYTES, PORT_ERR_BIN = 0, -1, -2, -3
 
 
 def build(ref: bool | None = None) -> None:
-    """Compile the C restatement (always) and the reference harness (when
-    /root/reference is present)."""
+    """Compile the C restatement (always), the reference's crc32c.cc (when
+    /root/reference is present) and the adapter harness (when libpsf is
+    built)."""
     subprocess.check_call(["make", "-s", "-C", HERE, "port"])
     if ref is None:
-        ref = os.path.isdir("/root/reference/src/filter")
+        ref = os.path.isfile("/root/reference/src/util/crc32c.cc")
     if ref:
         subprocess.check_call(["make", "-s", "-C", HERE, "ref"])
-        if os.path.exists(os.path.join(os.path.dirname(HERE), "parameter_server_amd", "libpsf.so")):
-            subprocess.check_call(["make", "-s", "-C", HERE, "adapter"])
+    if os.path.exists(os.path.join(os.path.dirname(HERE), "parameter_server_amd", "libpsf.so")):
+        subprocess.check_call(["make", "-s", "-C", HERE, "adapter"])
 
 
 def _np_dtype(dt: int):
@@ -224,144 +235,67 @@ class FtrlModel:
         return out
 
 
-class Ref:
-    """ctypes view of oracle/_ref/libpsref.so (reference headers, unmodified).
+class RefCrc32c:
+    """ctypes view of oracle/_ref/libcrc32c_ref.so: the reference's own
+    crc32c::Value (src/util/crc32c.cc:292-335, compiled in place)."""
 
-    Message-level API mirroring Message/Task/FilterConfig plus a RemoteNode-like
-    chain driver; see oracle/ref_harness.cc."""
-
-    def __init__(self, path: str = REF_SO):
+    def __init__(self, path: str = CRC_REF_SO):
         if not os.path.exists(path):
             raise FileNotFoundError(f"{path} (build with `make -C oracle ref`)")
+        self.lib = C.CDLL(path)
+        self.lib.ref_crc32c.argtypes = [C.c_void_p, C.c_size_t]
+        self.lib.ref_crc32c.restype = C.c_uint32
+
+    def crc32c(self, b) -> int:
+        a = np.frombuffer(bytes(b), dtype=np.uint8) if not isinstance(b, np.ndarray) else \
+            np.ascontiguousarray(b).view(np.uint8)
+        return int(self.lib.ref_crc32c(_ptr(a) if a.size else None, a.size))
+
+    def key_signature(self, keys: np.ndarray) -> int:
+        """KEY_CACHING's signature: the first min(bytes, 2048) key bytes (key_caching.h:18)."""
+        b = np.ascontiguousarray(keys).view(np.uint8)
+        return self.crc32c(b[:2048])
+
+
+SNAPPY_SO = "/opt/conda/lib/libsnappy.so.1"
+
+
+class Snappy118:
+    """snappy 1.1.8 itself (the third-party library the reference's
+    COMPRESSING calls through SArray::CompressTo / UncompressFrom,
+    shared_array_inl.h:232-255), through its C API, where the image has it:
+    it generated tests/golden/snappy*.npz and pins snappy_port.c."""
+
+    def __init__(self, path: str = SNAPPY_SO):
+        if not os.path.exists(path):
+            raise FileNotFoundError(path)
         L = self.lib = C.CDLL(path)
-        vp, sz, u64 = C.c_void_p, C.c_size_t, C.c_uint64
-        sig = {
-            "psref_last_error": ([], C.c_char_p),
-            "psref_set_time": ([C.c_int64], None),
-            "psref_crc32c": ([vp, sz], C.c_uint32),
-            "psref_node_new": ([], vp),
-            "psref_node_free": ([vp], None),
-            "psref_msg_new": ([C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, u64, u64], vp),
-            "psref_msg_free": ([vp], None),
-            "psref_msg_clone": ([vp], vp),
-            "psref_msg_set_key": ([vp, vp, sz, C.c_int], None),
-            "psref_msg_add_value": ([vp, vp, sz, C.c_int], None),
-            "psref_msg_key_bytes": ([vp], sz),
-            "psref_msg_has_key_flag": ([vp], C.c_int),
-            "psref_msg_key_type": ([vp], C.c_int),
-            "psref_msg_copy_key": ([vp, vp], None),
-            "psref_msg_num_values": ([vp], C.c_int),
-            "psref_msg_value_bytes": ([vp, C.c_int], sz),
-            "psref_msg_copy_value": ([vp, C.c_int, vp], None),
-            "psref_msg_add_filter": ([vp, C.c_int], C.c_int),
-            "psref_fc_set_num_bytes": ([vp, C.c_int, C.c_int], None),
-            "psref_fc_set_clear_cache": ([vp, C.c_int, C.c_int], None),
-            "psref_fc_set_noise": ([vp, C.c_int, C.c_float, C.c_float], None),
-            "psref_fc_add_fixed_point": ([vp, C.c_int, C.c_int, C.c_float, C.c_int, C.c_float], None),
-            "psref_fc_num_fixed_point": ([vp, C.c_int], C.c_int),
-            "psref_fc_get_fixed_point": ([vp, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_float),
-                                          C.POINTER(C.c_int), C.POINTER(C.c_float)], None),
-            "psref_fc_get_signature": ([vp, C.c_int, C.POINTER(C.c_uint32)], C.c_int),
-            "psref_fc_num_uncompressed": ([vp, C.c_int], C.c_int),
-            "psref_fc_uncompressed": ([vp, C.c_int, C.c_int], u64),
-            "psref_node_encode": ([vp, vp], C.c_int),
-            "psref_node_decode": ([vp, vp], C.c_int),
-            "psref_snappy_max": ([sz], sz),
-            "psref_snappy_compress": ([vp, sz, vp], sz),
-            "psref_snappy_uncompress": ([vp, sz, vp, sz, C.POINTER(sz)], C.c_int),
-        }
-        for name, (a, r) in sig.items():
-            f = getattr(L, name)
-            f.argtypes = a
-            f.restype = r
+        sz = C.c_size_t
+        L.snappy_compress.argtypes = [C.c_void_p, sz, C.c_void_p, C.POINTER(sz)]
+        L.snappy_max_compressed_length.argtypes = [sz]
+        L.snappy_max_compressed_length.restype = sz
+        L.snappy_uncompressed_length.argtypes = [C.c_void_p, sz, C.POINTER(sz)]
+        L.snappy_uncompress.argtypes = [C.c_void_p, sz, C.c_void_p, C.POINTER(sz)]
 
-    # -- thin helpers -------------------------------------------------------
-    def set_time(self, t: int) -> None:
-        self.lib.psref_set_time(t)
+    def compress(self, b: bytes) -> bytes:
+        a = np.frombuffer(bytes(b) + b"\0", dtype=np.uint8)
+        cap = C.c_size_t(self.lib.snappy_max_compressed_length(len(b)))
+        out = np.empty(cap.value, np.uint8)
+        assert self.lib.snappy_compress(_ptr(a), len(b), _ptr(out), C.byref(cap)) == 0
+        return out[:cap.value].tobytes()
 
-    def crc32c(self, b: bytes) -> int:
-        a = np.frombuffer(bytes(b), dtype=np.uint8)
-        return int(self.lib.psref_crc32c(_ptr(a) if a.size else None, a.size))
+    def uncompress(self, b: bytes, cap: int = 1 << 26):
+        """(0, bytes) or (status != 0, b"") as RawUncompress accepts / rejects"""
+        a = np.frombuffer(bytes(b) + b"\0", dtype=np.uint8)
+        n = C.c_size_t()
+        if self.lib.snappy_uncompressed_length(_ptr(a), len(b), C.byref(n)) != 0:
+            return -1, b""
+        if n.value > cap:
+            return -2, b""
+        out = np.empty(max(n.value, 1), np.uint8)
+        if self.lib.snappy_uncompress(_ptr(a), len(b), _ptr(out), C.byref(n)) != 0:
+            return -3, b""
+        return 0, out[:n.value].tobytes()
 
-    def snappy_compress(self, b: bytes) -> bytes:
-        a = np.frombuffer(bytes(b), dtype=np.uint8)
-        out = np.empty(self.lib.psref_snappy_max(a.size), dtype=np.uint8)
-        n = self.lib.psref_snappy_compress(_ptr(a) if a.size else None, a.size, _ptr(out))
-        return out[:n].tobytes()
-
-    def snappy_uncompress(self, b, cap: int = 1 << 26):
-        return _uncompress(self.lib.psref_snappy_uncompress, b, cap)
-
-    def last_error(self) -> str:
-        return self.lib.psref_last_error().decode()
-
-    def msg_new(self, request=True, push=False, has_param=True, key_channel=0, key_range=None):
-        kr = key_range
-        return self.lib.psref_msg_new(int(request), int(has_param), int(push), key_channel,
-                                      int(kr is not None), 0 if kr is None else kr[0],
-                                      0 if kr is None else kr[1])
-
-    def msg_values(self, m):
-        out = []
-        for i in range(self.lib.psref_msg_num_values(m)):
-            b = np.empty(self.lib.psref_msg_value_bytes(m, i), dtype=np.uint8)
-            if b.size:
-                self.lib.psref_msg_copy_value(m, i, _ptr(b))
-            out.append(b)
-        return out
-
-    def msg_key(self, m):
-        b = np.empty(self.lib.psref_msg_key_bytes(m), dtype=np.uint8)
-        if b.size:
-            self.lib.psref_msg_copy_key(m, _ptr(b))
-        return b
-
-    def fixed_points(self, m, idx):
-        res = []
-        for k in range(self.lib.psref_fc_num_fixed_point(m, idx)):
-            hm, mn, hx, mx = C.c_int(), C.c_float(), C.c_int(), C.c_float()
-            self.lib.psref_fc_get_fixed_point(m, idx, k, C.byref(hm), C.byref(mn), C.byref(hx), C.byref(mx))
-            res.append((bool(hm.value), mn.value, bool(hx.value), mx.value))
-        return res
-
-    def signature(self, m, idx):
-        s = C.c_uint32()
-        has = self.lib.psref_fc_get_signature(m, idx, C.byref(s))
-        return (bool(has), int(s.value))
-
-    def ff_roundtrip(self, x: np.ndarray, nb: int, seed: int, fixed=None):
-        """Run one FIXING_FLOAT-only message through encode then decode on a
-        fresh node pair.  Returns dict(status, codes, min, max, decoded)."""
-        L = self.lib
-        self.set_time(seed)
-        snd, rcv = L.psref_node_new(), L.psref_node_new()
-        m = self.msg_new()
-        dt = DT_FLOAT if x.dtype == np.float32 else DT_DOUBLE
-        L.psref_msg_add_value(m, _ptr(x) if x.size else None, x.nbytes, dt)
-        fi = L.psref_msg_add_filter(m, FIXING_FLOAT)
-        L.psref_fc_set_num_bytes(m, fi, nb)
-        if fixed is not None:
-            mn, mx = fixed
-            L.psref_fc_add_fixed_point(m, fi, mn is not None, 0.0 if mn is None else mn,
-                                       mx is not None, 0.0 if mx is None else mx)
-        res = {"status": 0}
-        try:
-            if L.psref_node_encode(snd, m) != 0:
-                res.update(status=-1, error=self.last_error())
-                return res
-            res["codes"] = self.msg_values(m)[0]
-            fp = self.fixed_points(m, fi)
-            res["min"], res["max"] = fp[0][1], fp[0][3]
-            w = L.psref_msg_clone(m)
-            try:
-                if L.psref_node_decode(rcv, w) != 0:
-                    res.update(status=-2, error=self.last_error())
-                    return res
-                res["decoded"] = self.msg_values(w)[0].view(x.dtype)
-            finally:
-                L.psref_msg_free(w)
-            return res
-        finally:
-            L.psref_msg_free(m)
-            L.psref_node_free(snd)
-            L.psref_node_free(rcv)
+    snappy_compress = compress      # Port's names
+    snappy_uncompress = uncompress

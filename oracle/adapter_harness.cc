@@ -1,29 +1,20 @@
-// ORACLE TEST INFRASTRUCTURE -- drop-in check for include/psf_ps_filter.h.
-//
-// Compiles the adapter against the PS types of oracle/ref_stub (the same
-// accessor names as the reference's generated protobuf classes) next to the
-// reference's UNMODIFIED src/filter/fixing_float.h, and runs both on the same
-// PS::Message: the reference filter and the libpsf-backed filter must produce
-// identical codes, identical FilterConfig side-info and identical decoded
-// values, and each must decode the other's wire output identically.
-// Built by `make -C oracle adapter` into oracle/_ref/libpsadapter.so.
+// ORACLE TEST INFRASTRUCTURE -- exercises include/psf_ps_filter.h, the
+// reference-side drop-in, compiled against oracle/ps_mock (a test double of
+// the PS types it calls; no reference source is compiled here).  Each entry
+// point runs one PS::Message through an adapter filter and hands back what
+// the reference's message would hold afterwards (wire bytes, FilterConfig
+// side-info, decoded arrays); tests/test_gpu_adapter.py compares them with
+// the C restatement (oracle/psf_port.c, snappy_port.c).
+// Built by `make -C oracle adapter` into oracle/_port/libpsadapter.so.
 #include "filter/filter.h"
-#include "filter/fixing_float.h"
-#include "filter/compressing.h"
-#include "filter/add_noise.h"
 #include "psf_ps_filter.h"
-#include "snappy_glue.h"
 
+#include <chrono>
 #include <string>
+#include <thread>
 #include <vector>
 
 using namespace PS;
-
-static time_t g_time = 0;
-extern "C" time_t __wrap_time(time_t* t) {
-  if (t) *t = g_time;
-  return g_time;
-}
 
 namespace PS {
 FilterConfig* Filter::find(FilterConfig::Type type, Task* task) {  // filter.cc:26-31
@@ -36,8 +27,7 @@ FilterConfig* Filter::find(FilterConfig::Type type, Task* task) {  // filter.cc:
 namespace {
 thread_local std::string g_err;
 
-Message* make_msg(const void* x, size_t bytes, int vt, int nb, int has_min, float mn, int has_max,
-                  float mx) {
+Message* ff_msg(const void* x, size_t bytes, int vt, int nb, int has_min, float mn, int has_max, float mx) {
   auto* m = new Message();
   SArray<char> v(bytes);
   memcpy(v.data(), x, bytes);
@@ -54,17 +44,34 @@ Message* make_msg(const void* x, size_t bytes, int vt, int nb, int has_min, floa
   return m;
 }
 
-bool same_bytes(const SArray<char>& a, const SArray<char>& b) {
-  return a.size() == b.size() && (a.size() == 0 || memcmp(a.data(), b.data(), a.size()) == 0);
-}
-bool same_fp(const FilterConfig& a, const FilterConfig& b) {
-  if (a.fixed_point_size() != b.fixed_point_size()) return false;
-  for (int k = 0; k < a.fixed_point_size(); ++k) {
-    const auto &p = a.fixed_point(k), &q = b.fixed_point(k);
-    if (p.has_min_value() != q.has_min_value() || p.has_max_value() != q.has_max_value()) return false;
-    if (memcmp(&p.min_, &q.min_, 4) || memcmp(&p.max_, &q.max_, 4)) return false;
+// encode + decode of one FIXING_FLOAT array through the adapter; 0 ok,
+// -1 encode CHECK, -2 decode CHECK
+int ff_roundtrip(psf_hip::FixingFloatFilter& f, const void* x, size_t bytes, int vt, int nb, int has_min, float mn,
+                 int has_max, float mx, void* codes, float* range, void* dec) {
+  Message* a = ff_msg(x, bytes, vt, nb, has_min, mn, has_max, mx);
+  int rc = 0;
+  try {
+    f.encode(a);
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    rc = -1;
   }
-  return true;
+  if (rc == 0) {
+    memcpy(codes, a->value[0].data(), a->value[0].size());
+    const auto& fp = a->task.filter(0).fixed_point(0);
+    range[0] = fp.min_value();
+    range[1] = fp.max_value();
+    Message w = *a;  // what the receiver's executor decodes
+    try {
+      f.decode(&w);
+      memcpy(dec, w.value[0].data(), w.value[0].size());
+    } catch (const std::exception& e) {
+      g_err = e.what();
+      rc = -2;
+    }
+  }
+  delete a;
+  return rc;
 }
 }  // namespace
 
@@ -72,118 +79,103 @@ extern "C" {
 
 const char* psadapter_last_error() { return g_err.c_str(); }
 
-// 0 = identical; >0 = which comparison failed; <0 = both rejected identically
-int psadapter_compare_ff(const void* x, size_t bytes, int value_type, int nb, int64_t seed,
-                         int has_min, float mn, int has_max, float mx) {
-  g_time = (time_t)seed;
+int psadapter_ff(const void* x, size_t bytes, int vt, int nb, int64_t seed, int has_min, float mn, int has_max,
+                 float mx, void* codes, float* range, void* dec) {
   psf_set_clock(1, seed);
-  Message* a = make_msg(x, bytes, value_type, nb, has_min, mn, has_max, mx);
-  Message* b = make_msg(x, bytes, value_type, nb, has_min, mn, has_max, mx);
-  PS::FixingFloatFilter ref;
-  psf_hip::FixingFloatFilter hip;
-  int rc = 0;
-  bool ra = true, rb = true;
-  try { ref.encode(a); } catch (const std::exception& e) { ra = false; g_err = e.what(); }
-  try { hip.encode(b); } catch (const std::exception& e) { rb = false; g_err += std::string(" | ") + e.what(); }
-  if (!ra || !rb) {
-    rc = (ra == rb) ? -1 : 1;
-  } else if (!same_bytes(a->value[0], b->value[0])) {
-    rc = 2;
-  } else if (!same_fp(a->task.filter(0), b->task.filter(0))) {
-    rc = 3;
-  } else {
-    // cross decode: reference decodes the adapter's wire output and vice versa
-    Message a2 = *b, b2 = *a;
-    try {
-      ref.decode(&a2);
-      hip.decode(&b2);
-      if (!same_bytes(a2.value[0], b2.value[0])) rc = 4;
-    } catch (const std::exception& e) {
-      g_err = e.what();
-      rc = 5;
-    }
-  }
-  delete a;
-  delete b;
-  return rc;
+  psf_hip::FixingFloatFilter f;
+  return ff_roundtrip(f, x, bytes, vt, nb, has_min, mn, has_max, mx, codes, range, dec);
 }
 
-// COMPRESSING: reference CompressingFilter vs the adapter on one message with
-// keys (if kbytes) and one value array.  0 = identical wire bytes, identical
-// uncompressed_size and both cross decodes restore the input.
-int psadapter_compare_compress(const void* key, size_t kbytes, const void* val, size_t vbytes, int vt) {
-  auto mk = [&] {
-    auto* m = new Message();
-    if (kbytes) {
-      SArray<char> k(kbytes);
-      memcpy(k.data(), key, kbytes);
-      m->set_key(k);
-    }
-    SArray<char> v(vbytes);
-    if (vbytes) memcpy(v.data(), val, vbytes);
-    m->task.value_type_.push_back((DataType)vt);
-    m->value.push_back(v);
-    m->task.add_filter()->set_type(FilterConfig::COMPRESSING);
-    return m;
-  };
-  Message *a = mk(), *b = mk(), *orig = mk();
-  PS::CompressingFilter ref;
-  psf_hip::MessageFilter hip(FilterConfig::COMPRESSING);
+// `nthreads` adapter instances (one per executor thread, as RemoteNode creates
+// one per peer) each encoding + decoding the same array `reps` times
+// concurrently; outputs of thread t land at codes + t * n * nb etc.  Returns
+// the wall time in seconds (negative: a CHECK failed).
+double psadapter_ff_threads(int nthreads, int reps, const void* x, size_t bytes, int vt, int nb, int64_t seed,
+                            void* codes, float* range, void* dec) {
+  psf_set_clock(1, seed);
+  const size_t vsz = vt == 9 ? 4 : 8, n = bytes / vsz;
+  std::vector<int> rc(nthreads, 0);
+  std::vector<std::thread> th;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int t = 0; t < nthreads; ++t)
+    th.emplace_back([&, t] {
+      psf_hip::FixingFloatFilter f;
+      for (int r = 0; r < reps && rc[t] == 0; ++r)
+        rc[t] = ff_roundtrip(f, x, bytes, vt, nb, 0, 0.f, 0, 0.f, static_cast<uint8_t*>(codes) + t * n * nb,
+                             range + 2 * t, static_cast<uint8_t*>(dec) + t * bytes);
+    });
+  for (auto& t : th) t.join();
+  const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  for (int r : rc)
+    if (r) return -1.0;
+  return s;
+}
+
+// COMPRESSING: one message with keys (if kbytes) and one value array.
+// Wire bytes -> key_out / val_out (lengths *klen / *vlen), uncompressed_size
+// side-info -> sizes (*nsizes), decoded key / value -> key_dec / val_dec.
+int psadapter_compress(const void* key, size_t kbytes, const void* val, size_t vbytes, int vt, void* key_out,
+                       size_t* klen, void* val_out, size_t* vlen, uint64_t* sizes, int* nsizes, void* key_dec,
+                       void* val_dec) {
+  auto* m = new Message();
+  if (kbytes) {
+    SArray<char> k(kbytes);
+    memcpy(k.data(), key, kbytes);
+    m->set_key(k);
+  }
+  SArray<char> v(vbytes);
+  if (vbytes) memcpy(v.data(), val, vbytes);
+  m->task.value_type_.push_back((DataType)vt);
+  m->value.push_back(v);
+  m->task.add_filter()->set_type(FilterConfig::COMPRESSING);
+  psf_hip::CompressingFilter f;
   int rc = 0;
   try {
-    ref.encode(a);
-    hip.encode(b);
-    const auto &fa = a->task.filter(0), &fb = b->task.filter(0);
-    if (!same_bytes(a->key, b->key) || !same_bytes(a->value[0], b->value[0])) rc = 2;
-    else if (fa.uncompressed_size_size() != fb.uncompressed_size_size()) rc = 3;
-    for (int i = 0; rc == 0 && i < fa.uncompressed_size_size(); ++i)
-      if (fa.uncompressed_size(i) != fb.uncompressed_size(i)) rc = 3;
-    if (rc == 0) {
-      Message a2 = *b, b2 = *a;
-      ref.decode(&a2);
-      hip.decode(&b2);
-      if (!same_bytes(a2.key, orig->key) || !same_bytes(b2.key, orig->key) ||
-          !same_bytes(a2.value[0], orig->value[0]) || !same_bytes(b2.value[0], orig->value[0]))
-        rc = 4;
-    }
+    f.encode(m);
+    *klen = m->key.size();
+    *vlen = m->value[0].size();
+    if (*klen) memcpy(key_out, m->key.data(), *klen);
+    if (*vlen) memcpy(val_out, m->value[0].data(), *vlen);
+    const auto& fc = m->task.filter(0);
+    *nsizes = fc.uncompressed_size_size();
+    for (int i = 0; i < *nsizes && i < 2; ++i) sizes[i] = fc.uncompressed_size(i);
+    Message w = *m;
+    f.decode(&w);
+    if (w.key.size()) memcpy(key_dec, w.key.data(), w.key.size());
+    if (w.value[0].size()) memcpy(val_dec, w.value[0].data(), w.value[0].size());
+    if (w.key.size() != kbytes || w.value[0].size() != vbytes) rc = 4;
   } catch (const std::exception& e) {
     g_err = e.what();
     rc = 5;
   }
-  delete a;
-  delete b;
-  delete orig;
+  delete m;
   return rc;
 }
 
-// NOISE: reference AddNoiseFilter vs the adapter (in place); 0 = identical bytes
-int psadapter_compare_noise(const void* val, size_t vbytes, int vt, float mean, float sd) {
-  auto mk = [&] {
-    auto* m = new Message();
-    SArray<char> v(vbytes);
-    memcpy(v.data(), val, vbytes);
-    m->task.value_type_.push_back((DataType)vt);
-    m->value.push_back(v);
-    auto* f = m->task.add_filter();
-    f->set_type(FilterConfig::NOISE);
-    f->mean_ = mean;
-    f->std_ = sd;
-    return m;
-  };
-  Message *a = mk(), *b = mk();
-  PS::AddNoiseFilter ref;
-  psf_hip::MessageFilter hip(FilterConfig::NOISE);
+// NOISE on one value array, in place; `alias` receives the array's bytes as
+// seen through a second SArray sharing the buffer (the sender's own copy).
+int psadapter_noise(const void* val, size_t vbytes, int vt, float mean, float sd, void* out, void* alias) {
+  auto* m = new Message();
+  SArray<char> v(vbytes);
+  memcpy(v.data(), val, vbytes);
+  SArray<char> keep = v;  // another reference to the same buffer
+  m->task.value_type_.push_back((DataType)vt);
+  m->value.push_back(v);
+  auto* f = m->task.add_filter();
+  f->set_type(FilterConfig::NOISE);
+  f->mean_ = mean;
+  f->std_ = sd;
+  psf_hip::AddNoiseFilter a;
   int rc = 0;
   try {
-    ref.encode(a);
-    hip.encode(b);
-    if (!same_bytes(a->value[0], b->value[0])) rc = 2;
+    a.encode(m);
+    memcpy(out, m->value[0].data(), vbytes);
+    memcpy(alias, keep.data(), vbytes);
   } catch (const std::exception& e) {
     g_err = e.what();
     rc = 5;
   }
-  delete a;
-  delete b;
+  delete m;
   return rc;
 }
 

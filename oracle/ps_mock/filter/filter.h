@@ -1,18 +1,15 @@
 // ORACLE TEST INFRASTRUCTURE -- not product code.
 //
-// A minimal stand-in for the parts of the reference's `system/message.h`,
-// `util/shared_array.h`, `util/range.h` and the generated `filter.pb.h` /
-// `task.pb.h` that the reference's four codec headers touch, so that those
-// headers compile UNMODIFIED from /root/reference/src/filter/ and can be run as
-// the parity oracle.  This file is written from the
-// reference's interface (field names / proto field semantics), not copied:
-//   filter.h:9-24            Filter interface (declared identically so the
-//                            reference's own filter.cc links against it)
+// A test double of the PS types that include/psf_ps_filter.h (the
+// reference-side drop-in adapter) is written against, so that the adapter can
+// be compiled and exercised here (oracle/adapter_harness.cc).  No reference
+// source is compiled against this file: it mirrors the reference's interface
+// (names and proto field semantics), written from
+//   filter.h:9-24            Filter interface
 //   filter.proto:3-35        FilterConfig / FixedFloatConfig fields + has-bits
 //   task.proto:28-39,78-91   Task fields used by the filters, DataType enum
 //   message.h:10-76          Message key/value, has_key/clear_key/set_key
-//   range.h:11-131           Range<Key> equality + hash for the KC cache key
-//   shared_array_inl.h:232-255  CompressTo / UncompressFrom snappy glue
+//   range.h:11-131           Range<Key> equality + hash
 //
 // CHECK failures throw PsCheckError so the ctypes harness can report them
 // instead of aborting the test process (the reference aborts via glog).

@@ -1,21 +1,29 @@
-"""Generate the golden fixtures in tests/golden/ from the REFERENCE itself.
+"""Generate (or --check) the golden fixtures in tests/golden/.
 
-Run in the build container (needs /root/reference and oracle/_ref):
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py           # write the fixtures
+    python tests/golden/make_golden.py --check   # regenerate in memory, compare
 
-Every fixture is produced by oracle/_ref/libpsref.so -- the reference's
-unmodified src/filter headers + filter.cc + util/crc32c.cc -- and, before it is
-written, re-computed by the plain-C restatement oracle/psf_port.c; any
-disagreement aborts.  The fixtures are data only (inputs + expected outputs):
+The reference's filter path cannot be built in this image (it needs glog,
+gflags, Eigen and the protobuf runtime), so the fixtures come
+from the restatements, cross-checked where the real thing exists here:
   ff_cases.npz / ff_cases.json   FIXING_FLOAT codes, side-info, decoded values
-  crc32c.npz                     CRC32C vectors
-  noise.npz                      NOISE outputs (f32, f64)
-  snappy.npz                     snappy 1.1.8 RawCompress outputs (COMPRESSING)
-  snappy_dec.npz                 snappy 1.1.8 RawUncompress verdicts + outputs on
-                                 valid and mutated streams
-  scenarios.json                 message-sequence records (KEY_CACHING, chain,
-                                 FIXING_FLOAT message rules) from tests/scenarios.py
-  even_divide.json               Range<Key>::EvenDivide server ranges (range.h)
+                                 (oracle/psf_port.c; parity unpinned)
+  crc32c.npz                     CRC32C vectors from the reference's own
+                                 src/util/crc32c.cc (oracle/_ref), = the port
+  noise.npz                      NOISE outputs (psf_port.c over libstdc++'s
+                                 polar method and this libm; parity unpinned)
+  snappy.npz                     snappy 1.1.8 RawCompress outputs from the
+                                 library itself (/opt/conda), = snappy_port.c
+  snappy_dec.npz                 snappy 1.1.8 RawUncompress verdicts + outputs
+                                 on valid and mutated streams, same source
+  scenarios.json                 message-sequence records (KEY_CACHING, the
+                                 ctr chain, FIXING_FLOAT message rules,
+                                 COMPRESSING) of oracle/chain.py
+  even_divide.json               Range<Key>::EvenDivide (oracle/slicing.py)
+The committed files were first written in round 1 by a harness that compiled
+the reference's filter headers against hand-written stand-ins for the types
+they need; that harness pins nothing and is gone, and --check shows the
+restatements regenerate every file unchanged.
 """
 from __future__ import annotations
 
@@ -70,40 +78,30 @@ def ff_case_list():
     return cases
 
 
-def gen_ff(R, P):
+def gen_ff(P):
     arrays, meta = {}, []
     for i, c in enumerate(ff_case_list()):
         x = c["x"]
-        fixed = None if (c["mn"] is None and c["mx"] is None) else (c["mn"], c["mx"])
-        r = R.ff_roundtrip(x, c["nb"], c["seed"], fixed=fixed)
         st, codes, mn, mx = P.ff_encode(x, c["nb"], c["seed"], c["mn"], c["mx"])
         m = dict(name=c["name"], nb=c["nb"], seed=c["seed"], preset_min=c["mn"], preset_max=c["mx"],
                  dtype="f32" if x.dtype == np.float32 else "f64", n=int(x.size))
         arrays[f"x{i}"] = x
-        if r["status"] != 0:
-            assert st != 0, (c["name"], "port accepted what the reference rejected", r)
+        if st != 0:
             m["status"] = "error"
-            m["error"] = r.get("error", "")
         else:
-            assert st == 0, (c["name"], st)
-            assert np.array_equal(r["codes"], codes), c["name"]
-            assert np.float32(r["min"]).tobytes() == np.float32(mn).tobytes(), c["name"]
-            assert np.float32(r["max"]).tobytes() == np.float32(mx).tobytes(), c["name"]
             st2, dec = P.ff_decode(codes, c["nb"], mn, mx, x.dtype)
-            assert st2 == 0 and dec.tobytes() == r["decoded"].tobytes(), c["name"]
+            assert st2 == 0, c["name"]
             m["status"] = "ok"
-            m["min_bits"] = int(np.float32(r["min"]).view(np.uint32))
-            m["max_bits"] = int(np.float32(r["max"]).view(np.uint32))
-            arrays[f"codes{i}"] = r["codes"]
-            arrays[f"dec{i}"] = r["decoded"]
+            m["min_bits"] = int(np.float32(mn).view(np.uint32))
+            m["max_bits"] = int(np.float32(mx).view(np.uint32))
+            arrays[f"codes{i}"] = codes
+            arrays[f"dec{i}"] = dec
         meta.append(m)
-    np.savez_compressed(os.path.join(HERE, "ff_cases.npz"), **arrays)
-    with open(os.path.join(HERE, "ff_cases.json"), "w") as f:
-        json.dump(meta, f, indent=1)
-    print(f"ff_cases: {len(meta)} cases")
+    return {"ff_cases.npz": arrays, "ff_cases.json": meta}
 
 
-def gen_crc(R, P):
+def gen_crc(P):
+    R = oracle.RefCrc32c()  # the reference's crc32c.cc
     rng = np.random.default_rng(7)
     lens = [0, 1, 2, 3, 4, 5, 7, 8, 9, 15, 16, 17, 31, 32, 33, 63, 64, 100, 255, 256, 1000,
             2047, 2048, 2049, 4096, 10000, 65537]
@@ -115,38 +113,23 @@ def gen_crc(R, P):
         blobs.append(b)
         crcs.append(c)
         offs.append(offs[-1] + n)
-    check = R.crc32c(b"123456789")
-    assert check == 0xE3069283
-    np.savez_compressed(os.path.join(HERE, "crc32c.npz"), data=np.concatenate(blobs),
-                        offsets=np.array(offs, np.int64), crc=np.array(crcs, np.uint32))
-    print(f"crc32c: {len(lens)} vectors")
+    assert R.crc32c(b"123456789") == 0xE3069283
+    return {"crc32c.npz": dict(data=np.concatenate(blobs), offsets=np.array(offs, np.int64),
+                               crc=np.array(crcs, np.uint32))}
 
 
-def gen_noise(R, P):
-    import ctypes as C
-    L = R.lib
+def gen_noise(P):
     arrays = {}
-    for tag, dt, code in (("f32", np.float32, 9), ("f64", np.float64, 10)):
+    for tag, dt in (("f32", np.float32), ("f64", np.float64)):
         for j, (n, mean, sd) in enumerate(((1001, 0.25, 2.0), (64, 0.0, 1.0), (7, -3.0, 0.01))):
             v = np.linspace(-1, 1, n).astype(dt)
-            node = L.psref_node_new()
-            m = R.msg_new()
-            L.psref_msg_add_value(m, v.ctypes.data_as(C.c_void_p), v.nbytes, code)
-            fi = L.psref_msg_add_filter(m, 4)
-            L.psref_fc_set_noise(m, fi, mean, sd)
-            assert L.psref_node_encode(node, m) == 0
-            out = R.msg_values(m)[0].view(dt)
-            assert out.tobytes() == P.add_noise(v, mean, sd).tobytes()
             arrays[f"{tag}_{j}_in"] = v
-            arrays[f"{tag}_{j}_out"] = out
+            arrays[f"{tag}_{j}_out"] = P.add_noise(v, np.float32(mean), np.float32(sd))
             arrays[f"{tag}_{j}_param"] = np.array([mean, sd], np.float32)
-            L.psref_msg_free(m)
-            L.psref_node_free(node)
-    np.savez_compressed(os.path.join(HERE, "noise.npz"), **arrays)
-    print("noise: ok")
+    return {"noise.npz": arrays}
 
 
-def gen_snappy(R):
+def gen_snappy(P, S):
     rng = np.random.default_rng(5)
     inputs = {
         "random": rng.integers(0, 256, 1000, dtype=np.uint8).tobytes(),
@@ -164,20 +147,17 @@ def gen_snappy(R):
         if n in (15, 16, 4096, 65537):
             inputs[f"random_{n}"] = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
     inputs["runs"] = np.repeat(rng.integers(0, 256, 3000, dtype=np.uint8), rng.integers(1, 200, 3000)).tobytes()
-    P = oracle.Port()
     arrays = {}
     for k, v in inputs.items():
-        out = R.snappy_compress(v)
+        out = S.compress(v)
         assert P.snappy_compress(v) == out, k
         arrays[f"{k}_in"] = np.frombuffer(v, np.uint8)
         arrays[f"{k}_out"] = np.frombuffer(out, np.uint8)
-    np.savez_compressed(os.path.join(HERE, "snappy.npz"), **arrays)
-    print(f"snappy: {len(inputs)} vectors (snappy 1.1.8)")
-    gen_snappy_malformed(R, P)
+    return {"snappy.npz": arrays}
 
 
-def gen_snappy_malformed(R, P):
-    """RawUncompress verdicts of the reference's snappy on mutated streams
+def gen_snappy_malformed(P, S):
+    """RawUncompress verdicts of snappy 1.1.8 on valid and mutated streams
     (the decoder's CHECK paths: shared_array_inl.h:236,240)."""
     rng = np.random.default_rng(11)
     streams, status, outs = [], [], []
@@ -192,7 +172,7 @@ def gen_snappy_malformed(R, P):
         streams.append(h)
     for t in range(400):
         b = srcs[t % 3](int(rng.integers(0, 2500)))
-        r = bytearray(R.snappy_compress(b))
+        r = bytearray(S.compress(b))
         for _ in range(int(rng.integers(0, 3))):
             if not r:
                 break
@@ -207,27 +187,21 @@ def gen_snappy_malformed(R, P):
                 del r[i:]
         streams.append(bytes(r))
     for s in streams:
-        st, out = R.snappy_uncompress(s, cap=1 << 20)
+        st, out = S.uncompress(s, cap=1 << 20)
         assert (st, out) == P.snappy_uncompress(s, cap=1 << 20), s[:16]
         status.append(st)
         outs.append(out)
     off = np.cumsum([0] + [len(s) for s in streams])
     ooff = np.cumsum([0] + [len(o) for o in outs])
-    np.savez_compressed(os.path.join(HERE, "snappy_dec.npz"),
-                        data=np.frombuffer(b"".join(streams), np.uint8), offsets=off.astype(np.int64),
-                        status=np.array(status, np.int32),
-                        out=np.frombuffer(b"".join(outs), np.uint8), out_offsets=ooff.astype(np.int64))
-    print(f"snappy_dec: {len(streams)} streams, {sum(1 for s in status if s == 0)} valid")
+    return {"snappy_dec.npz": dict(data=np.frombuffer(b"".join(streams), np.uint8), offsets=off.astype(np.int64),
+                                   status=np.array(status, np.int32),
+                                   out=np.frombuffer(b"".join(outs), np.uint8),
+                                   out_offsets=ooff.astype(np.int64))}
 
 
 def gen_even_divide():
-    """Range<Key>::EvenDivide from the reference's own range.h
-    (oracle/_ref/libpsrange.so), checked against oracle/slicing.py."""
-    import ctypes as C
-
+    """Range<Key>::EvenDivide (range.h:100-107) restated in oracle/slicing.py."""
     from oracle import slicing
-    L = C.CDLL(os.path.join(ROOT, "oracle", "_ref", "libpsrange.so"))
-    L.psref_even_divide.argtypes = [C.c_uint64] * 4 + [C.POINTER(C.c_uint64)] * 2
     rng = np.random.default_rng(9)
     spaces = [(0, (1 << 64) - 1), (0, 10**9), (5, 5 + 7), (123456789, 1 << 63), ((1 << 64) - 1000, (1 << 64) - 1)]
     for _ in range(20):
@@ -237,37 +211,66 @@ def gen_even_divide():
     for (b, e) in spaces:
         for n in (1, 2, 3, 4, 5, 7, 8, 16, 64):
             for i in range(n):
-                ob, oe = C.c_uint64(), C.c_uint64()
-                assert L.psref_even_divide(b, e, n, i, C.byref(ob), C.byref(oe)) == 0
-                assert slicing.even_divide(b, e, n, i) == (ob.value, oe.value), (b, e, n, i)
-                rows.append([str(b), str(e), n, i, str(ob.value), str(oe.value)])
-    with open(os.path.join(HERE, "even_divide.json"), "w") as f:
-        json.dump(rows, f)
-    print(f"even_divide: {len(rows)} rows")
+                ob, oe = slicing.even_divide(b, e, n, i)
+                rows.append([str(b), str(e), n, i, str(ob), str(oe)])
+    return {"even_divide.json": rows}
 
 
-def gen_scenarios(R):
-    impl = scenarios.RefImpl(R)
-    out = {
+def gen_scenarios(P):
+    from oracle.chain import PortImpl
+    impl = PortImpl(P)
+    return {"scenarios.json": {
         "key_caching": scenarios.run(impl, scenarios.kc_scenario()),
         "chain_ctr": scenarios.run(impl, scenarios.chain_scenario()),
         "ff_message": scenarios.run(impl, scenarios.ff_message_scenario()),
         "compressing": scenarios.run(impl, scenarios.compress_scenario()),
-    }
-    with open(os.path.join(HERE, "scenarios.json"), "w") as f:
-        json.dump(out, f, indent=1)
-    print("scenarios:", {k: len(v) for k, v in out.items()})
+    }}
+
+
+def generate(snappy=True):
+    P = oracle.Port()
+    out = {}
+    out.update(gen_ff(P))
+    out.update(gen_crc(P))
+    out.update(gen_noise(P))
+    if snappy:
+        S = oracle.Snappy118()
+        out.update(gen_snappy(P, S))
+        out.update(gen_snappy_malformed(P, S))
+    out.update(gen_scenarios(P))
+    out.update(gen_even_divide())
+    return out
+
+
+def _same(name, data):
+    path = os.path.join(HERE, name)
+    if name.endswith(".json"):
+        return json.load(open(path)) == json.loads(json.dumps(data))
+    old = np.load(path, allow_pickle=False)
+    return sorted(old.files) == sorted(data) and all(
+        old[k].dtype == np.asarray(data[k]).dtype and old[k].tobytes() == np.asarray(data[k]).tobytes()
+        for k in data)
+
+
+def check(snappy=True):
+    """names of the committed fixtures the generators do NOT reproduce"""
+    return [name for name, data in generate(snappy).items() if not _same(name, data)]
 
 
 def main():
-    oracle.build(ref=True)
-    R, P = oracle.Ref(), oracle.Port()
-    gen_ff(R, P)
-    gen_crc(R, P)
-    gen_noise(R, P)
-    gen_snappy(R)
-    gen_scenarios(R)
-    gen_even_divide()
+    if "--check" in sys.argv:
+        bad = check()
+        print("all fixtures reproduced" if not bad else f"differ: {bad}")
+        sys.exit(1 if bad else 0)
+    oracle.build()
+    for name, data in generate().items():
+        path = os.path.join(HERE, name)
+        if name.endswith(".json"):
+            with open(path, "w") as f:
+                json.dump(data, f, indent=None if name == "even_divide.json" else 1)
+        else:
+            np.savez_compressed(path, **data)
+        print("wrote", name)
 
 
 if __name__ == "__main__":

@@ -1,12 +1,12 @@
-"""Message-sequence scenarios run identically against the reference harness
-(oracle/_ref, reference headers unmodified) and against libpsf.
+"""Message-sequence scenarios run identically against the restated message
+path (oracle/chain.py: PortImpl) and against libpsf (PsfImpl).
 
 A scenario is a list of steps; each step builds one message, encodes it on the
 sender's RemoteNode, "sends" it (Task copy + zero-copy buffers, as the van
 delivers it) and decodes it on the receiver's node.  ``run`` returns a
 JSON-serialisable record of everything observable: side-info written into the
 FilterConfigs, which buffers survived encode, the decoded keys/values, and
-error statuses.  tests/golden/make_golden.py stores the reference's record;
+error statuses.  tests/golden/make_golden.py stores the restatement's record;
 the tests compare libpsf's record with it.
 """
 from __future__ import annotations
@@ -214,81 +214,6 @@ def _side(impl, m, fidx):
 
 
 # --------------------------------------------------------------- adapters ---
-class RefImpl:
-    """oracle/_ref (reference headers) behind the runner interface."""
-
-    def __init__(self, ref):
-        self.R = ref
-        self.L = ref.lib
-
-    def set_clock(self, t):
-        self.R.set_time(t)
-
-    def new_node(self):
-        return self.L.psref_node_new()
-
-    def free_node(self, n):
-        self.L.psref_node_free(n)
-
-    def new_msg(self, request, push, channel, kr):
-        return self.R.msg_new(request=request, push=push, has_param=True, key_channel=channel,
-                              key_range=kr)
-
-    def free_msg(self, m):
-        self.L.psref_msg_free(m)
-
-    def clone(self, m):
-        return self.L.psref_msg_clone(m)
-
-    def set_key(self, m, keys):
-        keys = np.ascontiguousarray(keys)
-        self.L.psref_msg_set_key(m, keys.ctypes.data if keys.size else None, keys.nbytes, DT_UINT64)
-
-    def add_value(self, m, v):
-        v = np.ascontiguousarray(v)
-        dt = {np.dtype(np.float32): DT_FLOAT, np.dtype(np.float64): DT_DOUBLE,
-              np.dtype(np.uint64): DT_UINT64}[v.dtype]
-        self.L.psref_msg_add_value(m, v.ctypes.data if v.size else None, v.nbytes, dt)
-
-    def add_filter(self, m, ftype, num_bytes=None, clear_cache_if_done=None, fixed_point=None,
-                   noise=None):
-        i = self.L.psref_msg_add_filter(m, ftype)
-        if num_bytes is not None:
-            self.L.psref_fc_set_num_bytes(m, i, num_bytes)
-        if clear_cache_if_done is not None:
-            self.L.psref_fc_set_clear_cache(m, i, int(clear_cache_if_done))
-        if noise is not None:
-            self.L.psref_fc_set_noise(m, i, noise[0], noise[1])
-        for mn, mx in fixed_point or []:
-            self.L.psref_fc_add_fixed_point(m, i, mn is not None, 0.0 if mn is None else mn,
-                                            mx is not None, 0.0 if mx is None else mx)
-        return i
-
-    def encode(self, n, m):
-        return 0 if self.L.psref_node_encode(n, m) == 0 else -1
-
-    def decode(self, n, m):
-        return 0 if self.L.psref_node_decode(n, m) == 0 else -1
-
-    def key(self, m):
-        return self.R.msg_key(m)
-
-    def key_info(self, m):
-        return bool(self.L.psref_msg_has_key_flag(m)), int(self.L.psref_msg_key_type(m))
-
-    def values(self, m):
-        return self.R.msg_values(m)
-
-    def signature(self, m, i):
-        return self.R.signature(m, i)
-
-    def fixed_points(self, m, i):
-        return self.R.fixed_points(m, i)
-
-    def uncompressed(self, m, i):
-        return [int(self.L.psref_fc_uncompressed(m, i, j)) for j in range(self.L.psref_fc_num_uncompressed(m, i))]
-
-
 class PsfImpl:
     """libpsf behind the runner interface.  device=None -> host-resident
     buffers on a host-only context (KEY_CACHING logic without a GPU)."""

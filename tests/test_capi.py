@@ -63,7 +63,7 @@ def test_message_model_host_only():
     assert c.num_values() == 0
 
 
-def test_key_caching_host_keys_matches_reference(scenario_golden):
+def test_key_caching_host_keys_matches_restatement(scenario_golden):
     """KEY_CACHING on host-resident keys (host-only context, no GPU)."""
     import scenarios
     got = scenarios.run(scenarios.PsfImpl(device=None), scenarios.kc_scenario())

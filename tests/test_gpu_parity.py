@@ -198,7 +198,10 @@ def test_key_signature_prefix(ctx, port):
 
 
 @pytest.mark.parametrize("which", ["key_caching", "chain_ctr", "ff_message", "compressing"])
-def test_scenarios_match_reference(scenario_golden, which):
+def test_scenarios_match_restatement(scenario_golden, which):
+    """The message path (RemoteNode + filters, HBM buffers) reproduces the
+    committed scenario records of oracle/chain.py (parity unpinned by the
+    reference: DESIGN.md §3)."""
     import scenarios
     steps = {"key_caching": scenarios.kc_scenario, "chain_ctr": scenarios.chain_scenario,
              "ff_message": scenarios.ff_message_scenario,

@@ -72,7 +72,7 @@ def test_compress_unaligned_input(ctx, port):
         assert got == port.snappy_compress(x), off
 
 
-def test_decoder_verdicts_match_reference(ctx):
+def test_decoder_verdicts_match_snappy_1_1_8(ctx):
     from parameter_server_amd._lib import PSF_ERR_CHECK, PsfError
     a = np.load(os.path.join(GOLDEN, "snappy_dec.npz"), allow_pickle=False)
     d, off, st, out, ooff = a["data"], a["offsets"], a["status"], a["out"], a["out_offsets"]

@@ -1,6 +1,6 @@
 """CPU: the multi-server / multi-GPU split.
 
-* Range<Key>::EvenDivide in libpsf == the reference's own range.h (fixture)
+* Range<Key>::EvenDivide in libpsf == the restatement of range.h:100-107 (fixture)
 * SliceKOFVMessage in libpsf (host keys) == the numpy restatement
 * the all-to-all-v spill exchange over world_size 2 with gloo
 """
@@ -15,7 +15,7 @@ import torch
 from conftest import GOLDEN
 
 
-def test_even_divide_matches_reference_fixture():
+def test_even_divide_matches_fixture():
     from oracle import slicing
     from parameter_server_amd import shard
     rows = json.load(open(os.path.join(GOLDEN, "even_divide.json")))

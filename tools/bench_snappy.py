@@ -3,7 +3,7 @@
 
 For each synthetic payload: device compress / uncompress wall time (synchronous
 C-ABI calls, HBM-resident), the compressor kernel time from the libpsf event
-profiler, and the reference's snappy 1.1.8 on one host core (oracle/_ref when
+profiler, and the reference's snappy 1.1.8 on one host core (the library, when
 present) on a bounded sample.  Prints one JSON line per payload.
 """
 import argparse
@@ -40,7 +40,7 @@ def main():
     ref = None
     try:
         import oracle
-        ref = oracle.Ref()
+        ref = oracle.Snappy118()  # the library the reference links, where the image has it
     except Exception:
         pass
     for name, x in payloads(a.mib).items():
