@@ -169,10 +169,62 @@ __device__ void place_bytes(uint8_t* __restrict__ dst, uint64_t o, const uint8_t
   for (uint32_t i = tail0 + tid; i < len; i += 256) dst[o + i] = s[i];
 }
 
-// One workgroup of 4 waves per 64 KiB fragment (the LDS footprint allows one
-// workgroup per CU): all 256 lanes stage the fragment, wave 0 runs the serial
-// 1.1.8 parse, and the final literal (all of an incompressible fragment) is
-// copied out by all 256 lanes again.
+// dst[0, len) = src[0, len) for any alignment of either side (global to
+// global): destination dwords are composed from the two aligned source dwords
+// they straddle, bytes at the edges
+__device__ void copy_unaligned(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint32_t len,
+                               uint32_t tid) {
+  const uintptr_t da = reinterpret_cast<uintptr_t>(dst);
+  const uint32_t head = (uint32_t)(((da + 3) & ~(uintptr_t)3) - da);
+  if (head >= len) {
+    if (tid < len) dst[tid] = src[tid];
+    return;
+  }
+  if (tid < head) dst[tid] = src[tid];
+  const uint32_t nw = (len - head) >> 2;
+  const uintptr_t sa = reinterpret_cast<uintptr_t>(src + head);
+  const uint32_t sh = (uint32_t)(sa & 3);
+  const uint32_t* s32 = reinterpret_cast<const uint32_t*>(sa & ~(uintptr_t)3);
+  uint32_t* d32 = reinterpret_cast<uint32_t*>(dst + head);
+  for (uint32_t j = tid; j < nw; j += 256) {
+    const uint32_t lo = s32[j];
+    d32[j] = sh ? __builtin_amdgcn_alignbyte(s32[j + 1], lo, sh) : lo;  // s32[j+1] lies inside src when sh != 0
+  }
+  const uint32_t t0 = head + 4 * nw;
+  if (tid < len - t0) dst[t0 + tid] = src[t0 + tid];
+}
+
+constexpr int kPre = (int)(kFrag / 16 / 256);  // uint4 per lane that cover one fragment
+// one fragment's share of a lane as one vector value (an array of uint4 would
+// be placed in scratch memory)
+typedef uint32_t FragRegs __attribute__((ext_vector_type(4 * kPre)));
+
+// issue the loads of fragment f (16-byte aligned input) into registers
+__device__ __forceinline__ void prefetch_frag(const uint8_t* __restrict__ in, size_t n, uint32_t f, FragRegs& pre,
+                                              uint32_t tid) {
+  const size_t start = (size_t)f * kFrag;
+  const uint32_t nv = (uint32_t)(min((size_t)kFrag, n - start) >> 4);
+  const uint4* g4 = reinterpret_cast<const uint4*>(in + start);
+#pragma unroll
+  for (int u = 0; u < kPre; ++u) {
+    const uint32_t i = u * 256 + tid;
+    if (i < nv) {
+      const uint4 v = g4[i];
+      pre[4 * u] = v.x;
+      pre[4 * u + 1] = v.y;
+      pre[4 * u + 2] = v.z;
+      pre[4 * u + 3] = v.w;
+    }
+  }
+}
+
+// Persistent workgroups of 4 waves (the LDS footprint allows one per CU), each
+// taking 64 KiB fragments by an atomic ticket: the fragment is staged in LDS
+// from registers, wave 0 runs the serial 1.1.8 parse, and while the
+// placement of that fragment runs (look-back, tags, the final literal copied
+// global to global straight from the input -- all of an incompressible
+// fragment) the next fragment's 64 KiB are already in flight into the
+// registers of all 256 lanes.
 __global__ __launch_bounds__(256) void snappy_compress_frags(const uint8_t* __restrict__ in, size_t n,
                                                              uint8_t* __restrict__ scratch,
                                                              uint8_t* __restrict__ dst, uint32_t hdr,
@@ -184,33 +236,31 @@ __global__ __launch_bounds__(256) void snappy_compress_frags(const uint8_t* __re
   __shared__ uint64_t s_off;
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid;  // wave 0's lanes in the parse (tid < 64 there)
-  // fragments are taken in the order workgroups start, so every fragment a
-  // workgroup's look-back waits on belongs to a workgroup already running
+  // fragments are taken in the order workgroups take tickets, and a
+  // workgroup's next ticket is taken after its current fragment's aggregate is
+  // published: every fragment a look-back waits on is parsed by a workgroup
+  // that is running and whose own waits are on smaller fragments only
   if (tid == 0) s_f = atomicAdd(ctr, 1u);
   __syncthreads();
-  const uint32_t f = s_f;
+  uint32_t f = s_f;
+  if (f >= nfrag) return;
+  const bool al = (reinterpret_cast<uintptr_t>(in) & 15) == 0;
+  FragRegs pre = {};
+  if (al) prefetch_frag(in, n, f, pre, tid);
+  uint8_t* srcb = reinterpret_cast<uint8_t*>(L.src);
+  for (;;) {
   const size_t start = (size_t)f * kFrag;
   const uint32_t len = (uint32_t)min((size_t)kFrag, n - start);
   const uint8_t* g = in + start;
   uint8_t* out = scratch + (size_t)f * kSnappyFragOut;
-  uint8_t* srcb = reinterpret_cast<uint8_t*>(L.src);
 
-  if ((reinterpret_cast<uintptr_t>(g) & 15) == 0) {
+  if (al) {
     const uint32_t nv = len >> 4;
-    const uint4* g4 = reinterpret_cast<const uint4*>(g);
     uint4* s4 = reinterpret_cast<uint4*>(L.src);
-    for (uint32_t i0 = 0; i0 < nv; i0 += 4 * 256) {  // 4 loads in flight per lane
-      uint4 t[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const uint32_t i = i0 + u * 256 + tid;
-        if (i < nv) t[u] = g4[i];
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const uint32_t i = i0 + u * 256 + tid;
-        if (i < nv) s4[i] = t[u];
-      }
+    for (int u = 0; u < kPre; ++u) {
+      const uint32_t i = u * 256 + tid;
+      if (i < nv) s4[i] = make_uint4(pre[4 * u], pre[4 * u + 1], pre[4 * u + 2], pre[4 * u + 3]);
     }
     for (uint32_t i = (nv << 4) + tid; i < len; i += 256) srcb[i] = g[i];
   } else {
@@ -311,10 +361,11 @@ remainder:
   op = s_op;
   next_emit = s_next;
   // this fragment's length: the tags emitted so far plus the final literal
-  uint32_t flen = op;
+  uint32_t flen = op, lit_hl = 0;
   if (next_emit < len) {
     const uint32_t m = len - next_emit - 1;
-    flen += 1 + m + 1 + (m < 60 ? 0 : ((31 - __builtin_clz(m)) >> 3) + 1);
+    lit_hl = 1 + (m < 60 ? 0 : ((31 - __builtin_clz(m)) >> 3) + 1);
+    flen += lit_hl + m + 1;
   }
   // its offset in the stream: decoupled look-back over the fragments before
   // it (state word = flag << 62 | bytes; flag 1: this fragment's length, 2:
@@ -339,14 +390,24 @@ remainder:
       pub->status = kOk;
       publish_ticket(pub, ticket);
     }
+    s_f = atomicAdd(ctr, 1u);  // the next fragment, taken once this one's aggregate is out
   }
   __syncthreads();
   const uint64_t off = s_off;
+  const uint32_t fn = s_f;
+  if (al && fn < nfrag) prefetch_frag(in, n, fn, pre, tid);  // in flight during the placement below
   if (f == 0 && tid < hdr) dst[tid] = (uint8_t)(((uint32_t)n >> (7 * tid)) | (tid + 1 < hdr ? 128u : 0u));
   if (op) place_bytes(dst, off, out, op, tid);  // the tags written to the scratch slot
-  if (next_emit < len) {  // emit_literal composes dwords relative to a 4-aligned base
+  if (next_emit < len) {  // the final literal: its tag, then its bytes straight from the input
     const uint64_t at = off + op;
-    emit_literal<256>(dst + (at & ~3ull), (uint32_t)(at & 3), srcb, next_emit, len - next_emit, tid);
+    const uint32_t ll = len - next_emit, m = ll - 1;
+    if (tid == 0) dst[at] = (uint8_t)(m < 60 ? m << 2 : (59 + (lit_hl - 1)) << 2);
+    if (tid >= 1 && tid < lit_hl) dst[at + tid] = (uint8_t)(m >> (8 * (tid - 1)));
+    copy_unaligned(dst + at + lit_hl, g + next_emit, ll, tid);
+  }
+  if (fn >= nfrag) break;
+  f = fn;
+  __syncthreads();  // LDS (source, table, lane marks) is rebuilt for fragment fn
   }
 }
 
@@ -910,8 +971,14 @@ int snappy_compress_launch(const void* in, size_t n, void* out, void* scratch, h
   if (e != hipSuccess) return kErrHip;
   uint32_t hdr = 1;
   for (uint64_t v = n; v >= 128; v >>= 7) ++hdr;
+  // persistent workgroups, one per CU (the LDS footprint allows no more)
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return kErrHip;
+  const uint32_t grid = nfrag < (uint32_t)cus ? nfrag : (uint32_t)cus;
   ProfScope ps(prof, kKSnappyCompress, st, (double)n);
-  hipLaunchKernelGGL(snappy_compress_frags, dim3(nfrag), dim3(256), 0, st, static_cast<const uint8_t*>(in), n, s,
+  hipLaunchKernelGGL(snappy_compress_frags, dim3(grid), dim3(256), 0, st, static_cast<const uint8_t*>(in), n, s,
                      static_cast<uint8_t*>(out), hdr, state, ctr, nfrag, pub, ticket);
   return launch_status();
 }

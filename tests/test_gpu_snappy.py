@@ -72,6 +72,30 @@ def test_compress_unaligned_input(ctx, port):
         assert got == port.snappy_compress(x), off
 
 
+def test_compress_many_fragments_mixed_vs_port(ctx, port):
+    """64 MiB = 1024 fragments (several per persistent workgroup, more than can
+    be resident at once) alternating incompressible and compressible blocks of
+    odd lengths, so fragment offsets in the stream land on every residue mod 4,
+    into output buffers at byte offsets 0..3: byte-identical to 1.1.8."""
+    rng = np.random.default_rng(77)
+    parts, n = [], 0
+    kinds = ("random", "codes", "keys", "runs", "text")
+    while n < (64 << 20):
+        b = _inputs(rng, int(rng.integers(30000, 300000)), kinds[len(parts) % len(kinds)])
+        parts.append(b)
+        n += len(b)
+    x = b"".join(parts)[:64 << 20]
+    want = port.snappy_compress(x)
+    xd = _dev(x)
+    cap = len(x) + len(x) // 6 + 32
+    for off in (0, 1, 2, 3):
+        buf = torch.zeros(cap + 4, dtype=torch.uint8, device="cuda")
+        got = ctx.snappy_compress(xd, out=buf[off:]).cpu().numpy().tobytes()
+        assert got == want, off
+    back = ctx.snappy_uncompress(_dev(want)).cpu().numpy().tobytes()
+    assert back == x
+
+
 def test_decoder_verdicts_match_snappy_1_1_8(ctx):
     from parameter_server_amd._lib import PSF_ERR_CHECK, PsfError
     a = np.load(os.path.join(GOLDEN, "snappy_dec.npz"), allow_pickle=False)
