@@ -192,6 +192,9 @@ int psf_fc_add_fixed_point(psf_message* msg, int idx, const psf_fixed_point* fp)
 int psf_fc_num_fixed_point(const psf_message* msg, int idx);
 int psf_fc_fixed_point(const psf_message* msg, int idx, int k, psf_fixed_point* fp);
 int psf_fc_signature(const psf_message* msg, int idx, int* has_signature, uint32_t* sig);
+/* the signature a received FilterConfig carries (filter.proto:33), for a
+ * decode fed from another wire format than psf_task_deserialize */
+int psf_fc_set_signature(psf_message* msg, int idx, int has_signature, uint32_t sig);
 int psf_fc_num_uncompressed(const psf_message* msg, int idx);
 int psf_fc_uncompressed(const psf_message* msg, int idx, int i, uint64_t* size);
 int psf_fc_add_uncompressed(psf_message* msg, int idx, uint64_t size);

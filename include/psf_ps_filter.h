@@ -26,16 +26,17 @@
 // §8(b)).  So every adapter instance owns its libpsf context -- a private HIP
 // stream, workspace and allocator -- and no lock is shared between instances.
 //
-// Filters adapted: FIXING_FLOAT, COMPRESSING (snappy 1.1.8-identical streams)
-// and NOISE.  KEY_CACHING on host-resident keys is 2 KiB of CRC plus a hash
-// map whose entries reference the caller's key SArrays (key_caching.h:27-28):
-// CreateFilter returns nullptr for it and the reference's own class is used
-// (device-resident keys go through psf_node_* directly).
+// Filters adapted: all four -- KEY_CACHING, FIXING_FLOAT, COMPRESSING
+// (snappy 1.1.8-identical streams) and NOISE.  (Device-resident messages go
+// through psf_node_* directly, without this host edge.)
 #pragma once
 #include <stdint.h>
 #include <string.h>
 
+#include <map>
+#include <mutex>
 #include <string>
+#include <tuple>
 
 #include "psf.h"
 
@@ -195,10 +196,70 @@ class AddNoiseFilter : public Filter, Bound {
   }
 };
 
+// KeyCachingFilter (src/filter/key_caching.h:7-67) through libpsf: the
+// signature (CRC32C of the first 2 KiB of the key, :18,43) and the cache per
+// (key_channel, key_range) are this instance's libpsf KEY_CACHING filter.
+// libpsf's cache entry refers to the key bytes of the message that filled it
+// (host memory here), so the adapter keeps that message's SArray beside it:
+// the cached key shares ownership as the reference's cache does (:27-28,55).
+class KeyCachingFilter : public Filter, Bound {
+ public:
+  void encode(Message* msg) { run(msg, true); }
+  void decode(Message* msg) { run(msg, false); }
+
+ private:
+  typedef std::tuple<int, uint64_t, uint64_t> CacheKey;
+  static bool Done(const Task& t) { return !t.request() || (t.has_param() && t.param().push()); }  // :63-67
+
+  void run(Message* msg, bool encode) {
+    FilterConfig* conf = find(FilterConfig::KEY_CACHING, msg);
+    if (!conf || (!encode && !conf->has_signature())) return;
+    const Task& t = msg->task;
+    psf_message* m = NewMessage(t);
+    const bool had_key = msg->has_key();
+    if (had_key) Check(psf_msg_set_key(m, msg->key.data(), msg->key.size(), PSF_DT_CHAR, PSF_LOC_HOST));
+    const int fi = psf_msg_add_filter(m, PSF_KEY_CACHING);
+    Check(fi < 0 ? fi : PSF_OK);
+    if (conf->clear_cache_if_done()) Check(psf_fc_set_clear_cache(m, fi, 1));
+    if (!encode) Check(psf_fc_set_signature(m, fi, 1, conf->signature()));
+    const CacheKey ck(t.key_channel(), t.key_range().begin(), t.key_range().end());
+    std::lock_guard<std::mutex> l(mu_);  // "thread safe" (:8), as the reference's mu_
+    Run(m, encode, "KEY_CACHING");
+    int has = 0;
+    uint32_t sig = 0;
+    Check(psf_fc_signature(m, fi, &has, &sig));
+    if (has)
+      conf->set_signature(sig);
+    else
+      conf->clear_signature();
+    void* kp = nullptr;
+    size_t kb = 0;
+    int loc = 0;
+    Check(psf_msg_key(m, &kp, &kb, &loc));
+    if (had_key) {
+      if (encode && kb == 0)
+        msg->clear_key();  // a hit: the receiver restores the key from its cache
+      else
+        keep_[ck] = msg->key;
+    } else if (!encode) {  // restored from the cache (:53-55)
+      auto it = keep_.find(ck);
+      SArray<char> k = it == keep_.end() ? SArray<char>() : it->second;
+      CHECK(k.size() == kb && (kb == 0 || k.data() == kp)) << "KEY_CACHING: adapter cache out of step";
+      msg->set_key(k);
+    }
+    if (conf->clear_cache_if_done() && Done(t)) keep_.erase(ck);
+    psf_msg_destroy(m);
+  }
+
+  std::map<CacheKey, SArray<char>> keep_;
+  std::mutex mu_;
+};
+
 // Registration hook for Filter::create (filter.cc:9-23): a libpsf filter, or
 // nullptr to fall through to the reference's own switch.
 inline Filter* CreateFilter(const FilterConfig& conf) {
   switch (conf.type()) {
+    case FilterConfig::KEY_CACHING: return new KeyCachingFilter();
     case FilterConfig::FIXING_FLOAT: return new FixingFloatFilter();
     case FilterConfig::COMPRESSING: return new CompressingFilter();
     case FilterConfig::NOISE: return new AddNoiseFilter();

@@ -152,6 +152,62 @@ int psadapter_compress(const void* key, size_t kbytes, const void* val, size_t v
   return rc;
 }
 
+// KEY_CACHING over a sequence of n messages between one sender and one
+// receiver instance.  Message i: key bytes kbuf[koff[i], koff[i+1]) (none when
+// empty), key_channel ch[i], key_range [rb[i], re[i]); flags fl[i]: 1 request,
+// 2 has_param + push, 4 clear_cache_if_done, 8 the receiver restarts (a fresh
+// instance) before it.  The receiver decodes a copy of what the sender's
+// encode left (Task by value, SArrays shared).  Per message: sent[i] = key
+// bytes left on the wire, has_sig/sig = the FilterConfig side-info, got[i] =
+// 1 when the decoded key equals the input's, rc[i] = 0, 1 (encode CHECK) or
+// 2 (decode CHECK; the sequence stops there).
+void psadapter_kc(int n, const uint8_t* kbuf, const uint64_t* koff, const int* ch, const uint64_t* rb,
+                  const uint64_t* re, const int* fl, uint64_t* sent, int* has_sig, uint32_t* sig, int* got,
+                  int* rc) {
+  psf_hip::KeyCachingFilter snd;
+  std::unique_ptr<psf_hip::KeyCachingFilter> rcv(new psf_hip::KeyCachingFilter());
+  for (int i = 0; i < n; ++i) rc[i] = -1;
+  for (int i = 0; i < n; ++i) {
+    if (fl[i] & 8) rcv.reset(new psf_hip::KeyCachingFilter());
+    Message a;
+    a.task.request_ = fl[i] & 1;
+    a.task.has_param_ = (fl[i] & 2) != 0;
+    a.task.param_.push_ = (fl[i] & 2) != 0;
+    a.task.key_channel_ = ch[i];
+    a.task.mutable_key_range()->set_begin(rb[i]);
+    a.task.mutable_key_range()->set_end(re[i]);
+    const size_t kb = koff[i + 1] - koff[i];
+    if (kb) {
+      SArray<char> k(kb);
+      memcpy(k.data(), kbuf + koff[i], kb);
+      a.set_key(k);
+    }
+    auto* f = a.task.add_filter();
+    f->set_type(FilterConfig::KEY_CACHING);
+    f->clear_cache_if_done_ = (fl[i] & 4) != 0;
+    try {
+      snd.encode(&a);
+    } catch (const std::exception& e) {
+      g_err = e.what();
+      rc[i] = 1;
+      return;
+    }
+    sent[i] = a.key.size();
+    has_sig[i] = a.task.filter(0).has_signature();
+    sig[i] = a.task.filter(0).signature();
+    Message w = a;
+    try {
+      rcv->decode(&w);
+    } catch (const std::exception& e) {
+      g_err = e.what();
+      rc[i] = 2;
+      return;
+    }
+    got[i] = w.key.size() == kb && (kb == 0 || memcmp(w.key.data(), kbuf + koff[i], kb) == 0);
+    rc[i] = 0;
+  }
+}
+
 // NOISE on one value array, in place; `alias` receives the array's bytes as
 // seen through a second SArray sharing the buffer (the sender's own copy).
 int psadapter_noise(const void* val, size_t vbytes, int vt, float mean, float sd, void* out, void* alias) {

@@ -86,6 +86,7 @@ SIGNATURES = {
     "psf_fc_num_fixed_point": ([vp, C.c_int], C.c_int),
     "psf_fc_fixed_point": ([vp, C.c_int, C.c_int, C.POINTER(FixedPoint)], C.c_int),
     "psf_fc_signature": ([vp, C.c_int, PI, C.POINTER(u32)], C.c_int),
+    "psf_fc_set_signature": ([vp, C.c_int, C.c_int, u32], C.c_int),
     "psf_fc_num_uncompressed": ([vp, C.c_int], C.c_int),
     "psf_fc_uncompressed": ([vp, C.c_int, C.c_int, C.POINTER(u64)], C.c_int),
     "psf_fc_add_uncompressed": ([vp, C.c_int, u64], C.c_int),

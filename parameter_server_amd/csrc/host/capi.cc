@@ -456,6 +456,14 @@ int psf_fc_signature(const psf_message* msg, int idx, int* has_signature, uint32
     return PSF_OK;
   });
 }
+int psf_fc_set_signature(psf_message* msg, int idx, int has_signature, uint32_t sig) {
+  return guarded([&] {
+    auto* f = fc_at(msg, idx);
+    f->has_signature = has_signature != 0;
+    f->signature = has_signature ? sig : 0u;
+    return PSF_OK;
+  });
+}
 int psf_fc_num_uncompressed(const psf_message* msg, int idx) {
   return guarded([&] { return (int)fc_at(msg, idx)->uncompressed_size.size(); });
 }

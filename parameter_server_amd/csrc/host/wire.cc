@@ -14,12 +14,20 @@
 // number order, repeated scalars unpacked (proto2).  Parsing follows protobuf:
 // any field order, packed or unpacked repeated scalars, unknown fields and
 // unknown enum values skipped, proto defaults for absent fields (ParamCall.push
-// defaults to true), required fields (FilterConfig.type, PbRange.begin/end)
-// enforced.  Fields outside the filter path (time, wait_time, msg, ctrl, ...)
-// belong to the executor / van and are skipped.
+// defaults to true).  Fields outside the filter path (time, wait_time, msg,
+// ctrl, sgd, ...) belong to the executor / van and are skipped -- after the
+// whole frame has been checked the way protobuf's C++ ParseFromArray checks
+// it: against the schema of Task and every message it reaches
+// (wire_schema.h, generated from the reference's .proto files), nested
+// messages parsed, packed repeats well formed, required fields present.
 #include "wire.h"
 
 #include <string.h>
+
+#include <utility>
+#include <vector>
+
+#include "wire_schema.h"
 
 namespace psf {
 namespace {
@@ -205,6 +213,86 @@ void parse_filter(Reader r, FilterConfig* f) {
   if (!has_type) Reader::fail("FilterConfig.type missing");
 }
 
+// ---------------------------------------- ParseFromArray's verdict ----
+namespace ws = wire_schema;
+
+const ws::Field* schema_field(const ws::Message& m, uint32_t number) {
+  for (int i = 0; i < m.nfields; ++i)
+    if (m.fields[i].number == number) return &m.fields[i];
+  return nullptr;
+}
+
+bool enum_value_known(int e, uint64_t v) {
+  const ws::Enum& E = ws::kEnums[e];
+  const int64_t x = (int64_t)v;  // enums are int32 on the wire, sign-extended
+  for (int i = 0; i < E.n; ++i)
+    if (E.values[i] == x) return true;
+  return false;
+}
+
+// a known field in the wire type protobuf parses it from (a repeated scalar
+// also packed); any other wire type makes it an unknown field
+bool wire_type_matches(const ws::Field& f, int wt) {
+  const bool packed = f.label == ws::kRepeated && wt == 2;
+  switch (f.kind) {
+    case ws::kVarint:
+    case ws::kEnum: return wt == 0 || packed;
+    case ws::kFixed32: return wt == 5 || packed;
+    case ws::kFixed64: return wt == 1 || packed;
+    default: return wt == 2;
+  }
+}
+
+typedef std::vector<std::pair<const uint8_t*, const uint8_t*>> Parts;
+
+// One message given as the byte ranges of its occurrences (a singular
+// sub-message that occurs several times is merged, i.e. parsed as the
+// concatenation); throws where parse + IsInitialized fails.
+void check_message(const Parts& parts, int mi, int depth) {
+  if (depth > 100) Reader::fail("nesting deeper than protobuf's recursion limit");
+  const ws::Message& M = ws::kMessages[mi];
+  std::vector<char> seen(M.nfields, 0);
+  std::vector<Parts> singular(M.nfields);
+  for (const auto& part : parts) {
+    Reader r{part.first, part.second};
+    while (!r.done()) {
+      int field, wt;
+      r.tag(&field, &wt);
+      const ws::Field* f = schema_field(M, (uint32_t)field);
+      if (!f || !wire_type_matches(*f, wt)) {
+        r.skip(wt, field);
+        continue;
+      }
+      const int idx = (int)(f - M.fields);
+      if (f->kind == ws::kMessage) {
+        Reader s = r.sub();
+        if (f->label == ws::kRepeated)
+          check_message(Parts{{s.p, s.end}}, f->sub, depth + 1);
+        else
+          singular[idx].push_back({s.p, s.end});
+        seen[idx] = 1;
+      } else if (wt == 2 && f->kind != ws::kBytes) {  // packed repeated scalars
+        Reader s = r.sub();
+        const size_t len = (size_t)(s.end - s.p);
+        if (f->kind == ws::kFixed32 ? len % 4 : f->kind == ws::kFixed64 ? len % 8 : 0)
+          Reader::fail("packed fixed-width field of ragged length");
+        if (f->kind == ws::kVarint || f->kind == ws::kEnum)
+          while (!s.done()) s.varint();
+        seen[idx] = 1;
+      } else if (f->kind == ws::kEnum) {
+        if (enum_value_known(f->sub, r.varint())) seen[idx] = 1;  // else an unknown field
+      } else {
+        r.skip(wt, field);
+        seen[idx] = 1;
+      }
+    }
+  }
+  for (int i = 0; i < M.nfields; ++i) {
+    if (!singular[i].empty()) check_message(singular[i], M.fields[i].sub, depth + 1);
+    if (M.fields[i].label == ws::kRequired && !seen[i]) Reader::fail("required field missing");
+  }
+}
+
 }  // namespace
 
 std::string serialize_task(const Task& t) {
@@ -231,6 +319,7 @@ std::string serialize_task(const Task& t) {
 
 void parse_task(const uint8_t* p, size_t n, Task* t) {
   *t = Task();
+  check_message(Parts{{p, p + n}}, ws::kTask, 0);
   Reader r{p, p + n};
   bool hb = false, he = false;  // PbRange required fields (merged over repeats)
   while (!r.done()) {

@@ -2,8 +2,8 @@
 a test double of the PS types (oracle/ps_mock, oracle/adapter_harness.cc) and
 run on PS::Messages in host memory, as a patched reference would run it:
 wire bytes, FilterConfig side-info and decoded arrays against the C
-restatement (oracle/psf_port.c, snappy_port.c); each adapter instance on its
-own stream, several of them concurrently on their own threads."""
+restatement (oracle/psf_port.c, snappy_port.c, oracle/chain.py); each adapter
+instance on its own stream, several of them concurrently on their own threads."""
 import ctypes as C
 import os
 
@@ -33,6 +33,8 @@ def harness():
     L.psadapter_compress.restype = C.c_int
     L.psadapter_noise.argtypes = [vp, sz, C.c_int, C.c_float, C.c_float, vp, vp]
     L.psadapter_noise.restype = C.c_int
+    L.psadapter_kc.argtypes = [C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.psadapter_kc.restype = None
     L.psadapter_last_error.restype = C.c_char_p
     return L
 
@@ -129,3 +131,62 @@ def test_adapter_noise_in_place_vs_port(harness, port, dtype):
     assert rc == 0, (rc, harness.psadapter_last_error())
     want = port.add_noise(x, 0.5, 2.0)
     assert out.tobytes() == want.tobytes() and alias.tobytes() == want.tobytes()
+
+
+def test_adapter_key_caching_vs_restatement(harness, port):
+    """KeyCachingFilter (key_caching.h:9-60) through libpsf, sender and
+    receiver instances over a message sequence: hits clear the key on the wire
+    and the receiver restores it, per (channel, key_range); a key changed only
+    past its first 2 KiB is a (reference) false hit; clear_cache_if_done on a
+    push request or a response drops the entry; a restarted receiver fails
+    the decode CHECK.  Every wire length, signature and restored key equals
+    the restatement's (oracle/chain.py)."""
+    from oracle import chain
+    rng = np.random.default_rng(11)
+    A = np.sort(rng.choice(10**9, 5000, replace=False)).astype(np.uint64).view(np.uint8)
+    B = np.sort(rng.choice(10**9, 7000, replace=False)).astype(np.uint64).view(np.uint8)
+    B2 = B.copy()
+    B2[3000] ^= 0x5A  # past the signature's 2 KiB
+    Cs = rng.integers(0, 256, 100, dtype=np.uint8)
+    E = np.zeros(0, np.uint8)
+    R0, R1 = (0, 1 << 40), (1 << 40, 1 << 41)
+    seq = [(A, 0, R0, 1), (A, 0, R0, 1), (A, 1, R0, 1), (A, 0, R1, 1), (B, 0, R0, 1), (B2, 0, R0, 1),
+           (E, 0, R0, 1), (B, 0, R0, 1 | 2 | 4), (B, 0, R0, 1), (B, 0, R0, 1), (A, 1, R0, 4),
+           (A, 1, R0, 1), (Cs, 2, R1, 1), (Cs, 2, R1, 1 | 8)]
+    n = len(seq)
+    kbuf = np.concatenate([k for k, *_ in seq])
+    koff = np.concatenate([[0], np.cumsum([k.size for k, *_ in seq])]).astype(np.uint64)
+    ch = np.array([c for _, c, _, _ in seq], np.int32)
+    rb = np.array([r[0] for _, _, r, _ in seq], np.uint64)
+    re_ = np.array([r[1] for _, _, r, _ in seq], np.uint64)
+    fl = np.array([f for *_, f in seq], np.int32)
+    sent, has, sig = np.zeros(n, np.uint64), np.zeros(n, np.int32), np.zeros(n, np.uint32)
+    got, rc = np.zeros(n, np.int32), np.zeros(n, np.int32)
+    harness.psadapter_kc(n, kbuf.ctypes.data, koff.ctypes.data, ch.ctypes.data, rb.ctypes.data, re_.ctypes.data,
+                         fl.ctypes.data, sent.ctypes.data, has.ctypes.data, sig.ctypes.data, got.ctypes.data,
+                         rc.ctypes.data)
+    snd, rcv = chain.KeyCaching(port), chain.KeyCaching(port)
+    for i, (k, c, r, f) in enumerate(seq):
+        if f & 8:
+            rcv = chain.KeyCaching(port)
+        t = chain.Task(bool(f & 1), bool(f & 2), bool(f & 2), c, r)
+        m = chain.Message(t)
+        if k.size:
+            m.set_key_char(k)
+        conf = chain.FilterConfig(chain.KEY_CACHING)
+        conf.clear_cache_if_done = bool(f & 4)
+        t.filter.append(conf)
+        snd.encode(m)
+        assert rc[i] != 1, (i, harness.psadapter_last_error())
+        assert (int(sent[i]), bool(has[i]), int(sig[i])) == (m.key.size, conf.has_signature, conf.signature), i
+        w = m.clone()
+        try:
+            rcv.decode(w)
+        except chain.CheckFailed:
+            assert rc[i] == 2, i  # both fail the CHECK here
+            assert i == n - 1
+            break
+        assert rc[i] == 0, (i, harness.psadapter_last_error())
+        want = w.key.size == k.size and w.key.tobytes() == k.tobytes()
+        assert bool(got[i]) == want, i
+    assert rc[-1] == 2 and not got[5] and sent[1] == 0 and sent[5] == 0

@@ -1,10 +1,13 @@
 """CPU: the Task frame of the wire (van.cc:122-191) against protobuf itself.
 
-The reference serialises Task with protobuf-generated C++.  protobuf's Python
-runtime is importable here, so the message types are rebuilt from their field
-numbers and types (task.proto:10-57 for the fields the filter path uses,
-filter.proto:3-35, range.proto, param.proto) as descriptors, plus some Task
-fields outside the filter path to exercise skipping.  Checks:
+The reference serialises Task with protobuf-generated C++.  The message types
+come from the reference's own .proto files (system/proto/task.proto and its
+imports: filter.proto, range.proto, param.proto, ...), compiled here by the
+image's protoc (torch/bin/protoc) into a descriptor set and loaded into
+protobuf's Python runtime.  Where /root/reference is absent the tests fall
+back to descriptors typed from the same field numbers and types, and
+test_fallback_descriptors_match_reference_proto pins that fallback to the
+compiled ones.  Checks:
 
 * libpsf's frame == protobuf's serialisation of the same fields, byte for byte;
 * protobuf frames (any field order, packed repeats, unknown fields) parse to
@@ -12,13 +15,49 @@ fields outside the filter path to exercise skipping.  Checks:
 * truncated / corrupted frames are rejected exactly where protobuf's C++
   ParseFromArray (parse + required fields) rejects them.
 """
+import os
+import subprocess
+import tempfile
+
 import numpy as np
 import pytest
 
 pb = pytest.importorskip("google.protobuf")
 
+REF_SRC = "/root/reference/src"
+
+
+def _protoc():
+    import torch
+    p = os.path.join(os.path.dirname(torch.__file__), "bin", "protoc")
+    return p if os.access(p, os.X_OK) else None
+
+
+def _reference_types():
+    """PS.Task / PS.FilterConfig compiled from the reference's task.proto (and
+    everything it imports), or None where the reference or protoc is absent."""
+    protoc = _protoc()
+    if protoc is None or not os.path.exists(os.path.join(REF_SRC, "system/proto/task.proto")):
+        return None
+    from google.protobuf import descriptor_pb2, descriptor_pool, message_factory
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "ps.desc")
+        subprocess.run([protoc, f"-I{REF_SRC}", "--include_imports", f"--descriptor_set_out={out}",
+                        "system/proto/task.proto"], check=True, capture_output=True)
+        with open(out, "rb") as f:
+            fds = descriptor_pb2.FileDescriptorSet.FromString(f.read())
+    pool = descriptor_pool.DescriptorPool()
+    for fd in fds.file:  # dependencies first (--include_imports order)
+        pool.Add(fd)
+    get = message_factory.GetMessageClass
+    return get(pool.FindMessageTypeByName("PS.Task")), get(pool.FindMessageTypeByName("PS.FilterConfig"))
+
 
 def _types():
+    return _reference_types() or _fallback_types()
+
+
+def _fallback_types():
     from google.protobuf import descriptor_pb2, descriptor_pool, message_factory
     F = descriptor_pb2.FieldDescriptorProto
     fd = descriptor_pb2.FileDescriptorProto(name="psf_wire_test.proto", package="PS", syntax="proto2")
@@ -59,14 +98,14 @@ def _types():
         ("uncompressed_size", 3, F.TYPE_UINT64, REP, {}),
     ], nested=[ffc], enums=[ty])
     msg("Task", [
-        ("control", 1, F.TYPE_BOOL, OPT, {}),           # outside the filter path
-        ("request", 2, F.TYPE_BOOL, OPT, {}),
+        ("control", 1, F.TYPE_BOOL, OPT, {"default_value": "false"}),  # outside the filter path
+        ("request", 2, F.TYPE_BOOL, OPT, {"default_value": "false"}),
         ("customer_id", 3, F.TYPE_INT32, OPT, {}),      # outside
         ("time", 5, F.TYPE_INT32, OPT, {}),             # outside
         ("wait_time", 6, F.TYPE_INT32, REP, {}),        # outside
         ("key_range", 7, F.TYPE_MESSAGE, OPT, {"type_name": ".PS.PbRange"}),
         ("key_channel", 8, F.TYPE_INT32, OPT, {}),
-        ("has_key", 9, F.TYPE_BOOL, OPT, {}),
+        ("has_key", 9, F.TYPE_BOOL, OPT, {"default_value": "false"}),
         ("filter", 12, F.TYPE_MESSAGE, REP, {"type_name": ".PS.FilterConfig"}),
         ("key_type", 13, F.TYPE_ENUM, OPT, {"type_name": ".PS.DataType"}),
         ("value_type", 14, F.TYPE_ENUM, REP, {"type_name": ".PS.DataType"}),
@@ -82,6 +121,34 @@ def _types():
 @pytest.fixture(scope="module")
 def Task():
     return _types()[0]
+
+
+def _fields(desc, seen=None):
+    """(message, field) -> (number, type, label, default) over desc and the
+    message types it reaches"""
+    from google.protobuf import descriptor_pb2
+    seen = {} if seen is None else seen
+    if desc.full_name in seen:
+        return seen
+    p = descriptor_pb2.DescriptorProto()
+    desc.CopyToProto(p)
+    seen[desc.full_name] = {f.name: (f.number, f.type, f.label, f.type_name.split(".")[-1], f.default_value)
+                            for f in p.field}
+    for f in desc.fields:
+        if f.message_type is not None:
+            _fields(f.message_type, seen)
+    return seen
+
+
+def test_fallback_descriptors_match_reference_proto():
+    ref = _reference_types()
+    if ref is None:
+        pytest.skip("reference .proto files or protoc absent")
+    want, got = _fields(ref[0].DESCRIPTOR), _fields(_fallback_types()[0].DESCRIPTOR)
+    assert set(got) <= set(want)
+    for msg, fields in got.items():
+        for name, spec in fields.items():
+            assert want[msg][name] == spec, (msg, name)
 
 
 def _random_psf_message(rng):
@@ -198,10 +265,26 @@ def _random_pb(Task, rng):
         t.param.SetInParent()
         if rng.integers(2):
             t.param.push = bool(rng.integers(2))
+    fields = Task.DESCRIPTOR.fields_by_name
+    if "more" in fields and rng.integers(4) == 0:  # reference-only fields: skipped by libpsf
+        t.more = bool(rng.integers(2))
+    if "task" in fields and rng.integers(4) == 0:
+        sub = t.task.add()
+        sub.request = True
+        sub.key_channel = int(rng.integers(0, 100))
+        if rng.integers(2):
+            sub.key_range.begin, sub.key_range.end = 1, 2
+    if "ctrl" in fields and rng.integers(4) == 0:  # required Control.cmd / Node.role nested
+        t.ctrl.cmd = int(rng.choice([1, 2, 10, 14]))
+        for _ in range(int(rng.integers(0, 3))):
+            nd = t.ctrl.node.add()
+            nd.role = int(rng.choice([0, 1, 3]))
+            if rng.integers(2):
+                nd.hostname = "h%d" % rng.integers(100)
     return t
 
 
-_OUTSIDE = ("control", "time", "wait_time", "msg", "customer_id")
+_OUTSIDE = ("control", "time", "wait_time", "msg", "customer_id", "more", "task", "ctrl")
 
 
 def _filter_path_view(Task, t):
@@ -210,7 +293,8 @@ def _filter_path_view(Task, t):
     u = Task()
     u.CopyFrom(t)
     for f in _OUTSIDE:
-        u.ClearField(f)
+        if f in Task.DESCRIPTOR.fields_by_name:
+            u.ClearField(f)
     u.DiscardUnknownFields()  # e.g. unknown enum values: protobuf keeps them aside
     u.request = t.request
     u.key_channel = t.key_channel
@@ -263,7 +347,7 @@ def test_malformed_frames_rejected_like_protobuf(Task):
     from parameter_server_amd._lib import PsfError
     rng = np.random.default_rng(2)
     agree = rejected = 0
-    for i in range(1500):
+    for i in range(4000):
         b = bytearray(_random_pb(Task, rng).SerializeToString())
         op = i % 3
         if b and op == 0:
@@ -305,3 +389,46 @@ def test_frames_follow_van_send(Task):
     m2.add_value(torch.ones(2))
     fr = m2.frames()
     assert len(fr) == 2 and not Task.FromString(fr[0]).HasField("has_key")
+
+
+def test_nested_fields_outside_filter_path_checked_like_protobuf(Task):
+    """Fields libpsf skips are still parsed as protobuf parses them: a nested
+    Control without its required cmd, a nested Task whose key_range lacks end,
+    an unknown enum value in a required field, a packed repeat cut inside a
+    varint -- all rejected, and their well-formed twins accepted."""
+    from google.protobuf.message import DecodeError
+
+    from parameter_server_amd import filter as F
+    from parameter_server_amd._lib import PsfError
+    fields = Task.DESCRIPTOR.fields_by_name
+    if "ctrl" not in fields:
+        pytest.skip("reference .proto files absent: the fallback Task has no ctrl / task fields")
+    cases = []
+    t = Task()
+    t.ctrl.SetInParent()
+    cases.append(t.SerializePartialToString())
+    t.ctrl.cmd = 2
+    cases.append(t.SerializePartialToString())
+    t = Task()
+    t.task.add().key_range.begin = 5
+    cases.append(t.SerializePartialToString())
+    t.task[0].key_range.end = 9
+    cases.append(t.SerializePartialToString())
+    cases.append(bytes([0x92, 0x01, 2, 8, 7]))  # ctrl { cmd: 7 } -- not a Control.Command
+    cases.append(bytes([0x92, 0x01, 2, 8, 4]))  # ctrl { cmd: READY_TO_EXIT }
+    cases.append(bytes([6 << 3 | 2, 2, 1, 0x81]))  # packed wait_time cut inside a varint
+    cases.append(bytes([6 << 3 | 2, 2, 1, 0x01]))
+    verdicts = []
+    for b in cases:
+        try:
+            ok_pb = Task.FromString(b).IsInitialized()
+        except DecodeError:
+            ok_pb = False
+        try:
+            F.Message.from_task_bytes(b)
+            ok = True
+        except PsfError:
+            ok = False
+        assert ok == ok_pb, b
+        verdicts.append(ok)
+    assert verdicts == [False, True] * 4
