@@ -4,17 +4,19 @@
 //
 // Compress.  A snappy stream is varint32(n) followed by the greedy LZ77 parse
 // of each 64 KiB input fragment, and every fragment is parsed on its own (fresh
-// hash table, no references across fragments).  So one workgroup (one wave)
-// takes one fragment: the fragment and its hash table live in LDS, the wave
+// hash table, no references across fragments).  So one wave parses one
+// fragment at a time: the fragment and its hash table live in LDS, the wave
 // runs the exact 1.1.8 parse with lane-parallel helpers -- 64 speculative
 // probes of the skip heuristic per step (the probe positions do not depend on
 // the data, only on where the skip loop started), match extension 64 bytes per
 // step, literal bytes copied 64 per step.  Tags go to a fixed-stride scratch
 // slot; at the end of the parse the fragment's length is known, a decoupled
-// look-back over the fragments before it (taken in workgroup start order
-// through an atomic ticket) gives its offset in the stream, and the tags and
-// the final literal (all of an incompressible fragment, straight from LDS) are
-// written to their place.
+// look-back over the fragments before it (taken in order through an atomic
+// ticket) gives its offset in the stream, and the tags and the final literal
+// (all of an incompressible fragment, read from the input) are copied to their
+// place.  Persistent workgroups pipeline this over rounds: while wave 0 parses
+// one fragment, three waves place the one parsed before and four hold the next
+// in registers (snappy_compress_frags).
 //
 // Uncompress accepts any valid snappy stream (a reference sender's included)
 // and reproduces RawUncompress's verdict.  Tag boundaries are found in
@@ -144,70 +146,117 @@ __device__ __forceinline__ uint32_t match_len(const uint8_t* b, uint32_t s1, uin
   }
 }
 
-// dst[o, o+len) = s[0, len) for a 256-aligned source with 8 readable bytes
-// past len (a scratch slot): destination dwords wholly inside the range are
-// composed from the two aligned source dwords they straddle, byte stores at
-// the edges
-__device__ void place_bytes(uint8_t* __restrict__ dst, uint64_t o, const uint8_t* __restrict__ s, uint32_t len,
-                            uint32_t tid) {
-  const uintptr_t ob = reinterpret_cast<uintptr_t>(dst);
-  const uint64_t a0 = ((ob + o + 3) & ~(uintptr_t)3) - ob, a1 = ((ob + o + len) & ~(uintptr_t)3) - ob;
-  if (a0 >= a1) {
-    for (uint32_t i = tid; i < len; i += 256) dst[o + i] = s[i];
-    return;
+// the 16 bytes that start sh bytes into lo:hi (sh is the same in every lane)
+__device__ __forceinline__ uint4 funnel16(const uint4& lo, const uint4& hi, uint32_t sh) {
+  const uint32_t b = sh & 3;
+#define AB(x, y) __builtin_amdgcn_alignbyte(x, y, b)
+  switch (sh >> 2) {
+    case 0: return make_uint4(AB(lo.y, lo.x), AB(lo.z, lo.y), AB(lo.w, lo.z), AB(hi.x, lo.w));
+    case 1: return make_uint4(AB(lo.z, lo.y), AB(lo.w, lo.z), AB(hi.x, lo.w), AB(hi.y, hi.x));
+    case 2: return make_uint4(AB(lo.w, lo.z), AB(hi.x, lo.w), AB(hi.y, hi.x), AB(hi.z, hi.y));
+    default: return make_uint4(AB(hi.x, lo.w), AB(hi.y, hi.x), AB(hi.z, hi.y), AB(hi.w, hi.z));
   }
-  const uint32_t head = (uint32_t)(a0 - o);
-  if (tid < head) dst[o + tid] = s[tid];
-  const uint32_t* s32 = reinterpret_cast<const uint32_t*>(s);
-  uint32_t* d32 = reinterpret_cast<uint32_t*>(dst + a0);
-  const uint32_t nw = (uint32_t)((a1 - a0) >> 2);
-  for (uint32_t j = tid; j < nw; j += 256) {  // destination bytes a0+4j.. are source bytes head+4j..
-    const uint32_t lo = s32[j], hi = s32[j + 1];
-    d32[j] = head ? __builtin_amdgcn_alignbyte(hi, lo, head) : lo;
-  }
-  const uint32_t tail0 = (uint32_t)(a1 - o);
-  for (uint32_t i = tail0 + tid; i < len; i += 256) dst[o + i] = s[i];
+#undef AB
 }
 
-// dst[0, len) = src[0, len) for any alignment of either side (global to
-// global): destination dwords are composed from the two aligned source dwords
-// they straddle, bytes at the edges
-__device__ void copy_unaligned(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint32_t len,
-                               uint32_t tid) {
-  const uintptr_t da = reinterpret_cast<uintptr_t>(dst);
-  const uint32_t head = (uint32_t)(((da + 3) & ~(uintptr_t)3) - da);
+__device__ __forceinline__ uint4 shfl_down1(const uint4& v) {
+  return make_uint4(__shfl_down(v.x, 1, 64), __shfl_down(v.y, 1, 64), __shfl_down(v.z, 1, 64),
+                    __shfl_down(v.w, 1, 64));
+}
+
+constexpr int kPlaceU = 16;  // rows of 63 chunks per placing wave per round: 47 KiB per round (256 VGPRs)
+
+// dst[0, len) = s[0, len), any alignment of either, by the 192 lanes of waves
+// 1-3 (pt = 0..191).  A wave takes rows of 63 destination chunks (16 bytes
+// each): lane l loads the aligned source block under chunk l of the row, and
+// a chunk's second block is the next lane's (lane 63 only loads).  Each round
+// issues all of its loads before its stores: a wave's memory counter retires
+// in order, so loads queued behind stores would wait for them.  Reads stay
+// inside 16-byte blocks that hold source bytes.
+__device__ void place_copy(uint8_t* __restrict__ dst, const uint8_t* __restrict__ s, uint32_t len, uint32_t pt,
+                           uint32_t lane) {
+  const uint32_t head = (uint32_t)(-reinterpret_cast<uintptr_t>(dst) & 15);
   if (head >= len) {
-    if (tid < len) dst[tid] = src[tid];
+    if (pt < len) dst[pt] = s[pt];
     return;
   }
-  if (tid < head) dst[tid] = src[tid];
-  const uint32_t nw = (len - head) >> 2;
-  const uintptr_t sa = reinterpret_cast<uintptr_t>(src + head);
-  const uint32_t sh = (uint32_t)(sa & 3);
-  const uint32_t* s32 = reinterpret_cast<const uint32_t*>(sa & ~(uintptr_t)3);
-  uint32_t* d32 = reinterpret_cast<uint32_t*>(dst + head);
-  for (uint32_t j = tid; j < nw; j += 256) {
-    const uint32_t lo = s32[j];
-    d32[j] = sh ? __builtin_amdgcn_alignbyte(s32[j + 1], lo, sh) : lo;  // s32[j+1] lies inside src when sh != 0
+  if (pt < head) dst[pt] = s[pt];
+  const uint32_t nc = (len - head) >> 4;
+  const uintptr_t sp = reinterpret_cast<uintptr_t>(s + head);
+  const uint4* s16 = reinterpret_cast<const uint4*>(sp & ~(uintptr_t)15);
+  const uint32_t sh = (uint32_t)(sp & 15);
+  const uint32_t lim = nc + (sh ? 1u : 0u);  // blocks that hold source bytes
+  uint4* d16 = reinterpret_cast<uint4*>(dst + head);
+  const uint32_t wv = pt >> 6;
+  for (uint32_t c0 = 0; c0 < nc; c0 += kPlaceU * 3 * 63) {
+    uint4 lo[kPlaceU];
+#pragma unroll
+    for (int u = 0; u < kPlaceU; ++u) {
+      const uint32_t c = c0 + (u * 3 + wv) * 63 + lane;
+      lo[u] = c < lim ? s16[c] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < kPlaceU; ++u) {
+      const uint32_t c = c0 + (u * 3 + wv) * 63 + lane;
+      const uint4 hi = shfl_down1(lo[u]);
+      if (lane < 63 && c < nc) d16[c] = funnel16(lo[u], hi, sh);
+    }
   }
-  const uint32_t t0 = head + 4 * nw;
-  if (tid < len - t0) dst[t0 + tid] = src[t0 + tid];
+  const uint32_t t0 = head + 16 * nc;
+  if (pt < len - t0) dst[t0 + pt] = s[t0 + pt];
 }
 
-constexpr int kPre = (int)(kFrag / 16 / 256);  // uint4 per lane that cover one fragment
+// snappy's literal tag for a literal of len bytes at p (lanes pt 0..4)
+__device__ __forceinline__ uint32_t literal_tag(uint8_t* p, uint32_t len, uint32_t pt) {
+  const uint32_t m = len - 1;
+  if (m < 60) {
+    if (pt == 0) p[0] = (uint8_t)(m << 2);
+    return 1;
+  }
+  const uint32_t count = ((31 - __builtin_clz(m)) >> 3) + 1;
+  if (pt == 0) p[0] = (uint8_t)((59 + count) << 2);
+  if (pt >= 1 && pt <= count) p[pt] = (uint8_t)(m >> (8 * (pt - 1)));
+  return 1 + count;
+}
+
+// Phase timestamps of the compress kernel (diagnostic builds only,
+// -DPSF_SNAPPY_TRACE, tools/snappy_trace.py): per fragment the 100 MHz clock at
+// the start of staging (0), after staging (4), after the parse (1), after the
+// look-back (2) and after the placement (3), plus the workgroup (5).
+#ifdef PSF_SNAPPY_TRACE
+constexpr uint32_t kTraceFrags = 1u << 14;
+__device__ uint64_t g_snappy_trace[kTraceFrags * 6];
+#define PSF_TRACE_T(f, k, t)                                                                \
+  do {                                                                                      \
+    if (threadIdx.x == (t) && (f) < kTraceFrags) {                                          \
+      g_snappy_trace[(f) * 6 + (k)] = __builtin_amdgcn_s_memrealtime();                     \
+      if ((k) == 0) g_snappy_trace[(f) * 6 + 5] = blockIdx.x;                               \
+    }                                                                                       \
+  } while (0)
+#else
+#define PSF_TRACE_T(f, k, t) \
+  do {                       \
+  } while (0)
+#endif
+#define PSF_TRACE(f, k) PSF_TRACE_T(f, k, 0)
+
+constexpr uint32_t kCThreads = 512;  // 8 waves: parse (0), place (1-3), stage (4-7)
+constexpr uint32_t kStageT = 256;    // lanes of the staging waves
+constexpr int kPre = (int)(kFrag / 16 / kStageT);  // uint4 per staging lane that cover one fragment
+constexpr uint32_t kNoFrag = 0xffffffffu;
 // one fragment's share of a lane as one vector value (an array of uint4 would
 // be placed in scratch memory)
 typedef uint32_t FragRegs __attribute__((ext_vector_type(4 * kPre)));
 
 // issue the loads of fragment f (16-byte aligned input) into registers
 __device__ __forceinline__ void prefetch_frag(const uint8_t* __restrict__ in, size_t n, uint32_t f, FragRegs& pre,
-                                              uint32_t tid) {
+                                              uint32_t st) {
   const size_t start = (size_t)f * kFrag;
   const uint32_t nv = (uint32_t)(min((size_t)kFrag, n - start) >> 4);
   const uint4* g4 = reinterpret_cast<const uint4*>(in + start);
 #pragma unroll
   for (int u = 0; u < kPre; ++u) {
-    const uint32_t i = u * 256 + tid;
+    const uint32_t i = u * kStageT + st;
     if (i < nv) {
       const uint4 v = g4[i];
       pre[4 * u] = v.x;
@@ -218,196 +267,256 @@ __device__ __forceinline__ void prefetch_frag(const uint8_t* __restrict__ in, si
   }
 }
 
-// Persistent workgroups of 4 waves (the LDS footprint allows one per CU), each
-// taking 64 KiB fragments by an atomic ticket: the fragment is staged in LDS
-// from registers, wave 0 runs the serial 1.1.8 parse, and while the
-// placement of that fragment runs (look-back, tags, the final literal copied
-// global to global straight from the input -- all of an incompressible
-// fragment) the next fragment's 64 KiB are already in flight into the
-// registers of all 256 lanes.
-__global__ __launch_bounds__(256) void snappy_compress_frags(const uint8_t* __restrict__ in, size_t n,
-                                                             uint8_t* __restrict__ scratch,
-                                                             uint8_t* __restrict__ dst, uint32_t hdr,
-                                                             uint64_t* __restrict__ state,
-                                                             uint32_t* __restrict__ ctr, uint32_t nfrag,
-                                                             PubSlot* pub, uint32_t ticket) {
+// Persistent workgroups of 8 waves (the LDS footprint allows one per CU) over
+// a pipeline of 64 KiB fragments taken by atomic ticket.  In each round, after
+// the staged fragment f is in LDS:
+//   wave 0      runs the serial 1.1.8 parse of f (tags to f's scratch slot)
+//               and publishes f's length for the look-back;
+//   waves 1-3   look back for the stream offset of the fragment parsed in the
+//               round before (fp) and copy its tags and final literal (read
+//               from the input) into place;
+//   waves 4-7   hold the next fragment's 64 KiB in registers, in flight while
+//               the others work, and stage it in LDS at the start of the next
+//               round.
+// Every wave's memory counter holds one kind of traffic -- the stagers' only
+// their prefetch loads, the parser's only stores -- so no wait at staging or
+// in the parse is behind another role's stores.
+//
+// Deadlock freedom: a workgroup holds at most three tickets (fp, f and the one
+// in flight; it takes the next while parsing), taken in increasing order by
+// running workgroups, and it waits only in the look-back of fp, on fragments
+// before fp.  The smallest fragment m whose length is unpublished belongs to a
+// workgroup that is parsing it, or will parse it after a round whose
+// look-back concerns fragments below m -- all published -- so every look-back
+// ends.
+__global__ __launch_bounds__(kCThreads) void snappy_compress_frags(const uint8_t* __restrict__ in, size_t n,
+                                                                   uint8_t* __restrict__ scratch,
+                                                                   uint8_t* __restrict__ dst, uint32_t hdr,
+                                                                   uint64_t* __restrict__ state,
+                                                                   uint32_t* __restrict__ ctr, uint32_t nfrag,
+                                                                   PubSlot* pub, uint32_t ticket) {
   __shared__ CompressLds L;
-  __shared__ uint32_t s_op, s_next, s_f;
-  __shared__ uint64_t s_off;
+  __shared__ uint32_t s_t0, s_t1, s_op, s_next, s_tn;
   const uint32_t tid = threadIdx.x;
-  const uint32_t lane = tid;  // wave 0's lanes in the parse (tid < 64 there)
-  // fragments are taken in the order workgroups take tickets, and a
-  // workgroup's next ticket is taken after its current fragment's aggregate is
-  // published: every fragment a look-back waits on is parsed by a workgroup
-  // that is running and whose own waits are on smaller fragments only
-  if (tid == 0) s_f = atomicAdd(ctr, 1u);
+  const uint32_t wave = tid >> 6, lane = tid & 63;
+  if (tid == 0) {
+    s_t0 = atomicAdd(ctr, 1u);
+    s_t1 = atomicAdd(ctr, 1u);
+  }
+  for (uint32_t i = tid; i < (uint32_t)kSkipN; i += kCThreads) L.skip[i] = kSkip.v[i];
+  for (uint32_t i = tid; i < kMinSlots; i += kCThreads) L.minlane[i] = 0xffffffffu;  // each parse step cleans up after itself
   __syncthreads();
-  uint32_t f = s_f;
+  uint32_t f = s_t0, fn = s_t1;
   if (f >= nfrag) return;
   const bool al = (reinterpret_cast<uintptr_t>(in) & 15) == 0;
+  const uint32_t st = tid - (kCThreads - kStageT);  // staging lane (waves 4-7)
   FragRegs pre = {};
-  if (al) prefetch_frag(in, n, f, pre, tid);
+  if (al && wave >= 4) prefetch_frag(in, n, f, pre, st);
   uint8_t* srcb = reinterpret_cast<uint8_t*>(L.src);
+  uint32_t fp = kNoFrag, fp_op = 0, fp_next = 0;  // the fragment parsed in the round before
   for (;;) {
-  const size_t start = (size_t)f * kFrag;
-  const uint32_t len = (uint32_t)min((size_t)kFrag, n - start);
-  const uint8_t* g = in + start;
-  uint8_t* out = scratch + (size_t)f * kSnappyFragOut;
-
-  if (al) {
-    const uint32_t nv = len >> 4;
-    uint4* s4 = reinterpret_cast<uint4*>(L.src);
+    // ---- stage f in LDS, clear its hash table
+    uint32_t len = 0, shift = 0;
+    if (f < nfrag) {
+      PSF_TRACE(f, 0);
+      const size_t start = (size_t)f * kFrag;
+      len = (uint32_t)min((size_t)kFrag, n - start);
+      const uint8_t* g = in + start;
+      if (al) {
+        const uint32_t nv = len >> 4;
+        if (wave >= 4) {
+          uint4* s4 = reinterpret_cast<uint4*>(L.src);
 #pragma unroll
-    for (int u = 0; u < kPre; ++u) {
-      const uint32_t i = u * 256 + tid;
-      if (i < nv) s4[i] = make_uint4(pre[4 * u], pre[4 * u + 1], pre[4 * u + 2], pre[4 * u + 3]);
-    }
-    for (uint32_t i = (nv << 4) + tid; i < len; i += 256) srcb[i] = g[i];
-  } else {
-    for (uint32_t i = tid; i < len; i += 256) srcb[i] = g[i];
-  }
-  if (tid < 16) srcb[len + tid] = 0;
-  for (uint32_t i = tid; i < (uint32_t)kSkipN; i += 256) L.skip[i] = kSkip.v[i];
-  for (uint32_t i = tid; i < kMinSlots; i += 256) L.minlane[i] = 0xffffffffu;
-  uint32_t tsize = 256;
-  while (tsize < kMaxTable && tsize < len) tsize <<= 1;
-  const int shift = __builtin_clz(tsize) + 1;  // 32 - log2(tsize)
-  uint32_t* t32 = reinterpret_cast<uint32_t*>(L.table);
-  for (uint32_t i = tid; i < tsize / 2; i += 256) t32[i] = 0;
-  __syncthreads();
-
-  uint32_t op = 0, next_emit = 0;
-  if (tid < 64 && len >= 15) {
-    const uint32_t ip_limit = len - 15;
-    uint32_t ip = 1;
-    for (;;) {
-      // ---- skip loop: up to 64 probes per step, first match wins.  Probes are
-      // exact up to the first lane jc whose hash slot an earlier lane of the
-      // step also probed: lanes < jc see the table as it was, and lane jc either
-      // sees that lane's write (same hash; it is the only earlier one, a second
-      // would itself have been jc) or the table (slot alias).  Later lanes are
-      // dropped and the next step starts after jc.
-      uint32_t cand = 0, kbase = 0;
-      for (;;) {
-        const uint32_t k = kbase + lane;
-        const uint32_t pos = ip + L.skip[k];
-        const bool valid = ip + L.skip[k + 1] <= ip_limit;  // else "goto emit_remainder"
-        uint32_t v = 0, h = 0, slot = 0;
-        if (valid) {
-          v = ld32(L.src, pos);
-          h = hash(v, shift);
-          slot = h & (kMinSlots - 1);
-          atomicMin(&L.minlane[slot], lane);
+          for (int u = 0; u < kPre; ++u) {
+            const uint32_t i = u * kStageT + st;
+            if (i < nv) s4[i] = make_uint4(pre[4 * u], pre[4 * u + 1], pre[4 * u + 2], pre[4 * u + 3]);
+          }
+        } else if (tid < len - (nv << 4)) {
+          srcb[(nv << 4) + tid] = g[(nv << 4) + tid];
         }
-        asm volatile("" ::: "memory");
-        uint32_t first = valid ? L.minlane[slot] : lane;
-        asm volatile("" ::: "memory");
-        if (valid) L.minlane[slot] = 0xffffffffu;  // clean for the next step
-        const uint64_t vm = __ballot(valid);
-        const uint64_t em = __ballot(valid && first < lane);
-        int limit = 63;  // last exact lane
-        int jc = 64, jm = 0;
-        bool exact_pair = false;
-        if (em) {
-          jc = __builtin_ctzll(em);
-          jm = (int)__builtin_amdgcn_readlane(first, jc);
-          exact_pair = __builtin_amdgcn_readlane(h, jm) == __builtin_amdgcn_readlane(h, jc);
-          limit = jc;
+      } else {
+        for (uint32_t i = tid; i < len; i += kCThreads) srcb[i] = g[i];
+      }
+      if (tid < 16) srcb[len + tid] = 0;
+      uint32_t tsize = 256;
+      while (tsize < kMaxTable && tsize < len) tsize <<= 1;
+      shift = __builtin_clz(tsize) + 1;  // 32 - log2(tsize)
+      uint32_t* t32 = reinterpret_cast<uint32_t*>(L.table);
+      for (uint32_t i = tid; i < tsize / 2; i += kCThreads) t32[i] = 0;
+    }
+    __syncthreads();
+    PSF_TRACE(f < nfrag ? f : kTraceFrags, 4);
+    if (wave == 0) {
+      // ---- parse f
+      if (f < nfrag) {
+        uint8_t* out = scratch + (size_t)f * kSnappyFragOut;
+        uint32_t op = 0, next_emit = 0;
+        if (len >= 15) {
+          const uint32_t ip_limit = len - 15;
+          uint32_t ip = 1;
+          for (;;) {
+            // ---- skip loop: up to 64 probes per step, first match wins.  Probes are
+            // exact up to the first lane jc whose hash slot an earlier lane of the
+            // step also probed: lanes < jc see the table as it was, and lane jc either
+            // sees that lane's write (same hash; it is the only earlier one, a second
+            // would itself have been jc) or the table (slot alias).  Later lanes are
+            // dropped and the next step starts after jc.
+            uint32_t cand = 0, kbase = 0;
+            for (;;) {
+              const uint32_t k = kbase + lane;
+              const uint32_t pos = ip + L.skip[k];
+              const bool valid = ip + L.skip[k + 1] <= ip_limit;  // else "goto emit_remainder"
+              uint32_t v = 0, h = 0, slot = 0;
+              if (valid) {
+                v = ld32(L.src, pos);
+                h = hash(v, shift);
+                slot = h & (kMinSlots - 1);
+                atomicMin(&L.minlane[slot], lane);
+              }
+              asm volatile("" ::: "memory");
+              uint32_t first = valid ? L.minlane[slot] : lane;
+              asm volatile("" ::: "memory");
+              if (valid) L.minlane[slot] = 0xffffffffu;  // clean for the next step
+              const uint64_t vm = __ballot(valid);
+              const uint64_t em = __ballot(valid && first < lane);
+              int limit = 63;  // last exact lane
+              int jc = 64, jm = 0;
+              bool exact_pair = false;
+              if (em) {
+                jc = __builtin_ctzll(em);
+                jm = (int)__builtin_amdgcn_readlane(first, jc);
+                exact_pair = __builtin_amdgcn_readlane(h, jm) == __builtin_amdgcn_readlane(h, jc);
+                limit = jc;
+              }
+              uint32_t c = valid ? L.table[h] : 0;
+              if (exact_pair && (int)lane == jc) c = __builtin_amdgcn_readlane(pos, jm);
+              const bool m = valid && (int)lane <= limit && v == ld32(L.src, c);
+              const uint64_t mm = __ballot(m);
+              const uint64_t lim_mask = limit >= 63 ? ~0ull : ((1ull << (limit + 1)) - 1);
+              const int last = mm ? __builtin_ctzll(mm) : limit;
+              const bool overwritten = exact_pair && (int)lane == jm && jc <= last;
+              if (valid && (int)lane <= last && !overwritten) L.table[h] = (uint16_t)pos;
+              if (mm) {
+                const int ks = __builtin_ctzll(mm);
+                ip = __builtin_amdgcn_readlane(pos, ks);
+                cand = __builtin_amdgcn_readlane(c, ks);
+                break;
+              }
+              if ((vm & lim_mask) != lim_mask) goto remainder;
+              kbase += (uint32_t)limit + 1;
+            }
+            op = emit_literal(out, op, srcb, next_emit, ip - next_emit, lane);
+            // ---- emit copies while the next position matches immediately
+            for (;;) {
+              const uint32_t base = ip;
+              const uint32_t matched = 4 + uni(match_len(srcb, cand + 4, ip + 4, len, lane));
+              ip += matched;
+              op = emit_copy(out, op, base - cand, matched, lane);
+              next_emit = ip;
+              if (ip >= ip_limit) goto remainder;
+              const uint32_t prev = ld32(L.src, ip - 1);
+              const uint32_t cur = uni(ld32(L.src, ip));
+              if (lane == 0) L.table[hash(prev, shift)] = (uint16_t)(ip - 1);
+              const uint32_t ch = hash(cur, shift);
+              cand = uni(L.table[ch]);
+              const uint32_t cb = uni(ld32(L.src, cand));
+              if (lane == 0) L.table[ch] = (uint16_t)ip;
+              if (cur != cb) break;
+            }
+            ip += 1;
+          }
         }
-        uint32_t c = valid ? L.table[h] : 0;
-        if (exact_pair && (int)lane == jc) c = __builtin_amdgcn_readlane(pos, jm);
-        const bool m = valid && (int)lane <= limit && v == ld32(L.src, c);
-        const uint64_t mm = __ballot(m);
-        const uint64_t lim_mask = limit >= 63 ? ~0ull : ((1ull << (limit + 1)) - 1);
-        const int last = mm ? __builtin_ctzll(mm) : limit;
-        const bool overwritten = exact_pair && (int)lane == jm && jc <= last;
-        if (valid && (int)lane <= last && !overwritten) L.table[h] = (uint16_t)pos;
-        if (mm) {
-          const int ks = __builtin_ctzll(mm);
-          ip = __builtin_amdgcn_readlane(pos, ks);
-          cand = __builtin_amdgcn_readlane(c, ks);
-          break;
+      remainder:
+        // f's length: the tags so far plus the final literal; published for
+        // the look-back (state word = flag << 62 | bytes; flag 1: the length,
+        // 2: the inclusive prefix with the varint header -- fragment 0's at once)
+        uint32_t flen = op;
+        if (next_emit < len) {
+          const uint32_t m = len - next_emit - 1;
+          flen += 1 + m + 1 + (m < 60 ? 0 : ((31 - __builtin_clz(m)) >> 3) + 1);
         }
-        if ((vm & lim_mask) != lim_mask) goto remainder;
-        kbase += (uint32_t)limit + 1;
+        if (lane == 0) {
+          if (f == 0)
+            __hip_atomic_store(&state[0], (2ull << 62) | (hdr + flen), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          else
+            atomicAdd(&state[f], (1ull << 62) | flen);
+          s_op = op;
+          s_next = next_emit;
+          s_tn = atomicAdd(ctr, 1u);  // the fragment after fn
+        }
+        PSF_TRACE(f, 1);
       }
-      op = emit_literal(out, op, srcb, next_emit, ip - next_emit, lane);
-      // ---- emit copies while the next position matches immediately
-      for (;;) {
-        const uint32_t base = ip;
-        const uint32_t matched = 4 + uni(match_len(srcb, cand + 4, ip + 4, len, lane));
-        ip += matched;
-        op = emit_copy(out, op, base - cand, matched, lane);
-        next_emit = ip;
-        if (ip >= ip_limit) goto remainder;
-        const uint32_t prev = ld32(L.src, ip - 1);
-        const uint32_t cur = uni(ld32(L.src, ip));
-        if (lane == 0) L.table[hash(prev, shift)] = (uint16_t)(ip - 1);
-        const uint32_t ch = hash(cur, shift);
-        cand = uni(L.table[ch]);
-        const uint32_t cb = uni(ld32(L.src, cand));
-        if (lane == 0) L.table[ch] = (uint16_t)ip;
-        if (cur != cb) break;
+    } else if (wave < 4) {
+      // ---- look back for fp's offset, then copy fp into place
+      if (fp < nfrag) {
+        const uint32_t pt = tid - 64;
+        const size_t pstart = (size_t)fp * kFrag;
+        const uint32_t plen = (uint32_t)min((size_t)kFrag, n - pstart);
+        uint32_t flen = fp_op;
+        if (fp_next < plen) {
+          const uint32_t m = plen - fp_next - 1;
+          flen += 1 + m + 1 + (m < 60 ? 0 : ((31 - __builtin_clz(m)) >> 3) + 1);
+        }
+        // each of the three waves walks back on its own, 64 predecessors per
+        // step: the nearest inclusive prefix ends the walk, the lengths in
+        // front of it are summed across the wave
+        uint64_t excl = hdr;
+        if (fp > 0) {
+          uint64_t sum = 0;
+          int64_t base = (int64_t)fp - 1;  // lane l reads fragment base - l
+          for (;;) {
+            const int64_t j = base - (int64_t)lane;
+            const uint64_t w = j >= 0 ? __hip_atomic_load(&state[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+            const bool ready = j < 0 || (w >> 62) != 0;  // fragment 0 publishes inclusive only: the walk ends there
+            const uint64_t im = __ballot(j >= 0 && (w >> 62) == 2);
+            const int stop = im ? __builtin_ctzll(im) : 63;
+            const uint64_t need = stop >= 63 ? ~0ull : ((2ull << stop) - 1);
+            if (__ballot(!ready) & need) {  // a predecessor in front of the stop has not published yet
+              __builtin_amdgcn_s_sleep(1);
+              continue;
+            }
+            uint64_t v = ((int)lane <= stop && j >= 0) ? (w & ((1ull << 62) - 1)) : 0;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+            sum += v;
+            if (im) break;
+            base -= 64;
+          }
+          excl = sum;
+        }
+        if (pt == 0) {
+          if (fp > 0)
+            __hip_atomic_store(&state[fp], (2ull << 62) | (excl + flen), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (fp + 1 == nfrag && pub) {
+            pub->size = excl + flen;
+            pub->status = kOk;
+            publish_ticket(pub, ticket);
+          }
+        }
+        PSF_TRACE_T(fp, 2, 64);
+        if (fp == 0 && pt < hdr) dst[pt] = (uint8_t)(((uint32_t)n >> (7 * pt)) | (pt + 1 < hdr ? 128u : 0u));
+        uint8_t* d = dst + excl;
+        if (fp_op) place_copy(d, scratch + (size_t)fp * kSnappyFragOut, fp_op, pt, lane);
+        if (fp_next < plen) {
+          d += fp_op;
+          d += literal_tag(d, plen - fp_next, pt);
+          place_copy(d, in + pstart + fp_next, plen - fp_next, pt, lane);
+        }
+        PSF_TRACE_T(fp, 3, 64);
       }
-      ip += 1;
+    } else if (al && fn < nfrag) {
+      prefetch_frag(in, n, fn, pre, st);  // the registers were staged: the next fragment goes out now
     }
-  }
-remainder:
-  if (tid == 0) {
-    s_op = op;
-    s_next = next_emit;
-  }
-  __syncthreads();
-  op = s_op;
-  next_emit = s_next;
-  // this fragment's length: the tags emitted so far plus the final literal
-  uint32_t flen = op, lit_hl = 0;
-  if (next_emit < len) {
-    const uint32_t m = len - next_emit - 1;
-    lit_hl = 1 + (m < 60 ? 0 : ((31 - __builtin_clz(m)) >> 3) + 1);
-    flen += lit_hl + m + 1;
-  }
-  // its offset in the stream: decoupled look-back over the fragments before
-  // it (state word = flag << 62 | bytes; flag 1: this fragment's length, 2:
-  // the inclusive prefix with the varint header); device-scope atomics only
-  if (tid == 0) {
-    uint64_t excl = hdr;
-    if (f > 0) {
-      atomicAdd(&state[f], (1ull << 62) | flen);
-      uint64_t sum = 0;
-      for (uint32_t j = f - 1;; --j) {
-        uint64_t w;
-        while (((w = atomicAdd(&state[j], 0ull)) >> 62) == 0) __builtin_amdgcn_s_sleep(1);
-        sum += w & ((1ull << 62) - 1);
-        if ((w >> 62) == 2) break;
-      }
-      excl = sum;
-    }
-    atomicExch(reinterpret_cast<unsigned long long*>(&state[f]), (2ull << 62) | (excl + flen));
-    s_off = excl;
-    if (f + 1 == nfrag && pub) {
-      pub->size = excl + flen;
-      pub->status = kOk;
-      publish_ticket(pub, ticket);
-    }
-    s_f = atomicAdd(ctr, 1u);  // the next fragment, taken once this one's aggregate is out
-  }
-  __syncthreads();
-  const uint64_t off = s_off;
-  const uint32_t fn = s_f;
-  if (al && fn < nfrag) prefetch_frag(in, n, fn, pre, tid);  // in flight during the placement below
-  if (f == 0 && tid < hdr) dst[tid] = (uint8_t)(((uint32_t)n >> (7 * tid)) | (tid + 1 < hdr ? 128u : 0u));
-  if (op) place_bytes(dst, off, out, op, tid);  // the tags written to the scratch slot
-  if (next_emit < len) {  // the final literal: its tag, then its bytes straight from the input
-    const uint64_t at = off + op;
-    const uint32_t ll = len - next_emit, m = ll - 1;
-    if (tid == 0) dst[at] = (uint8_t)(m < 60 ? m << 2 : (59 + (lit_hl - 1)) << 2);
-    if (tid >= 1 && tid < lit_hl) dst[at + tid] = (uint8_t)(m >> (8 * (tid - 1)));
-    copy_unaligned(dst + at + lit_hl, g + next_emit, ll, tid);
-  }
-  if (fn >= nfrag) break;
-  f = fn;
-  __syncthreads();  // LDS (source, table, lane marks) is rebuilt for fragment fn
+    __syncthreads();
+    // fragments move down the pipeline
+    const bool parsed = f < nfrag;
+    fp = parsed ? f : kNoFrag;
+    fp_op = s_op;
+    fp_next = s_next;
+    f = fn;
+    fn = parsed ? s_tn : kNoFrag;
+    if (fp == kNoFrag) break;  // nothing left to place (and so nothing to parse)
+    // (s_op, s_next and s_tn are rewritten only after the next staging barrier)
   }
 }
 
@@ -978,7 +1087,7 @@ int snappy_compress_launch(const void* in, size_t n, void* out, void* scratch, h
     return kErrHip;
   const uint32_t grid = nfrag < (uint32_t)cus ? nfrag : (uint32_t)cus;
   ProfScope ps(prof, kKSnappyCompress, st, (double)n);
-  hipLaunchKernelGGL(snappy_compress_frags, dim3(grid), dim3(256), 0, st, static_cast<const uint8_t*>(in), n, s,
+  hipLaunchKernelGGL(snappy_compress_frags, dim3(grid), dim3(kCThreads), 0, st, static_cast<const uint8_t*>(in), n, s,
                      static_cast<uint8_t*>(out), hdr, state, ctr, nfrag, pub, ticket);
   return launch_status();
 }
@@ -1031,3 +1140,12 @@ int snappy_uncompress_launch(const void* in, size_t C, uint32_t hdr, size_t dsiz
 }
 
 }  // namespace psf
+
+#ifdef PSF_SNAPPY_TRACE
+// diagnostic builds: copy the compress kernel's phase timestamps out
+extern "C" int psf_debug_snappy_trace(void* out, size_t bytes) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(psf::g_snappy_trace), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess
+             ? 0
+             : -4;
+}
+#endif

@@ -1,0 +1,90 @@
+#!/usr/bin/env python3
+"""Phase timeline of the snappy compress kernel (diagnostic).
+
+Builds a libpsf variant with -DPSF_SNAPPY_TRACE (tools/variants/trace/) and
+loads it: python tools/snappy_trace.py --build (here, on CPU), then on the GPU
+box python tools/snappy_trace.py --run [--mib 128] [--kind codes|keys|random].
+Prints per-phase statistics over fragments: staging+parse (0->1), look-back
+(1->2), placement (2->3), and the gap between a workgroup's fragments.
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+VAR = os.path.join(ROOT, "tools", "variants", "trace")
+
+
+def build():
+    sys.path.insert(0, ROOT)
+    from parameter_server_amd import build as b
+    b.build()
+    os.makedirs(VAR, exist_ok=True)
+    objs = [os.path.join(b.OBJ, f) for f in sorted(os.listdir(b.OBJ)) if f.endswith(".o") and f != "snappy.hip.o"]
+    obj = os.path.join(VAR, "snappy.o")
+    subprocess.check_call([b._hipcc(), "-x", "hip", f"--offload-arch={b.ARCH}", *b.COMMON, "-DPSF_SNAPPY_TRACE",
+                           "-c", os.path.join(b.CSRC, "snappy.hip"), "-o", obj])
+    subprocess.check_call([b._hipcc(), f"--offload-arch={b.ARCH}", "-shared", "-fPIC", "-o",
+                           os.path.join(VAR, "libpsf.so"), *objs, obj])
+    print(os.path.join(VAR, "libpsf.so"))
+
+
+def run(mib, kind):
+    os.environ["PSF_LIBRARY_VARIANT"] = os.path.join(VAR, "libpsf.so")
+    sys.path.insert(0, ROOT)
+    import numpy as np
+    import torch
+
+    from parameter_server_amd import filter as F
+    from parameter_server_amd._lib import lib
+    n = mib << 20
+    g = torch.Generator(device="cuda").manual_seed(3)
+    if kind == "codes":
+        x = (torch.randn(n, device="cuda", generator=g) * 30 + 128).clamp(0, 255).to(torch.uint8)
+    elif kind == "keys":
+        x = torch.sort(torch.randint(0, 10**9, (n // 8,), device="cuda", generator=g))[0].view(torch.uint8)
+    else:
+        x = torch.randint(0, 256, (n,), device="cuda", dtype=torch.uint8, generator=g)
+    ctx = F.Context(0)
+    for _ in range(3):
+        ctx.snappy_compress(x)
+    torch.cuda.synchronize()
+    nfrag = (n + 65535) // 65536
+    buf = np.zeros(nfrag * 6, np.uint64)
+    L = lib()
+    L.psf_debug_snappy_trace.argtypes = [C.c_void_p, C.c_size_t]
+    assert L.psf_debug_snappy_trace(buf.ctypes.data, buf.nbytes) == 0
+    t = buf.reshape(nfrag, 6).astype(np.int64)
+    t0 = t[:, 0].min()
+    ns = lambda a: a * 10.0  # noqa: E731  (100 MHz clock)
+    stage, parse = ns(t[:, 4] - t[:, 0]), ns(t[:, 1] - t[:, 4])
+    look, place = ns(t[:, 2] - t[:, 1]), ns(t[:, 3] - t[:, 2])
+    hw = t[:, 5]
+    gaps = []
+    order = np.argsort(t[:, 0])
+    last = {}
+    for f in order:
+        if hw[f] in last:
+            gaps.append(ns(t[f, 0] - t[last[hw[f]], 3]))
+        last[hw[f]] = f
+    q = lambda a: {p: round(float(np.percentile(a, p)) / 1000, 2) for p in (10, 50, 90, 99)}  # noqa: E731
+    print(json.dumps({"kind": kind, "mib": mib, "frags": nfrag, "total_us": round(ns(t[:, 3].max() - t0) / 1000, 1),
+                      "stage_us": q(stage), "parse_us": q(parse), "lookback_us": q(look), "place_us": q(place),
+                      "gap_us": q(np.array(gaps)) if gaps else None,
+                      "first_start_spread_us": round(ns(np.sort(t[:, 0])[min(255, nfrag - 1)] - t0) / 1000, 2)}))
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--build", action="store_true")
+    ap.add_argument("--run", action="store_true")
+    ap.add_argument("--mib", type=int, default=128)
+    ap.add_argument("--kind", default="codes")
+    a = ap.parse_args()
+    if a.build:
+        build()
+    if a.run:
+        run(a.mib, a.kind)
