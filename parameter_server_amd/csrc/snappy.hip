@@ -19,17 +19,20 @@
 // in registers (snappy_compress_frags).
 //
 // Uncompress accepts any valid snappy stream (a reference sender's included)
-// and reproduces RawUncompress's verdict.  Tag boundaries are found in
-// parallel: every 64 KiB window of the compressed bytes is parsed
-// speculatively from its first byte (K1); one lane then links the windows (K2)
-// -- the true chain enters each window at a position that is, almost always,
-// on that window's speculative chain, and the speculative bookkeeping gives the
-// exit and the output count from there.  K3 re-walks each window from its true
-// entry, validates every copy (1 <= offset <= produced) and indexes the tag that
+// and reproduces RawUncompress's verdict.  First every output fragment is
+// assumed stored as one literal where a 1.1.8 encoder of incompressible data
+// puts it, checked and copied (K-spec; such a stream is done there).
+// Otherwise tag boundaries are found in parallel: a one-wave linker hops over
+// stored fragments (K0); if it meets too many small tags, every 16 KiB window
+// of the compressed bytes is parsed speculatively from each of its first 64
+// offsets (K1) and one lane links the windows (K2) -- the true chain enters a
+// window on one of those chains almost always, and their bookkeeping gives the
+// exit and the output count.  K3 re-walks each window from its true entry,
+// validates every copy (1 <= offset <= produced) and indexes the tag that
 // starts each 64 KiB output fragment.  K4 decodes the output fragments in
-// parallel, one wave each, in LDS.  A stream whose tags straddle output
-// fragments or whose copies reach into an earlier fragment (never produced by a
-// 1.1.8 encoder, but valid) is decoded by one lane instead (K5).
+// parallel in LDS.  A stream whose tags straddle output fragments or whose
+// copies reach into an earlier fragment (never produced by a 1.1.8 encoder,
+// but valid) is decoded by one lane instead (K5).
 #include "psf_internal.h"
 
 namespace psf {
@@ -164,7 +167,7 @@ __device__ __forceinline__ uint4 shfl_down1(const uint4& v) {
                     __shfl_down(v.w, 1, 64));
 }
 
-constexpr int kPlaceU = 16;  // rows of 63 chunks per placing wave per round: 47 KiB per round (256 VGPRs)
+constexpr int kPlaceU = 15;  // rows of 63 chunks per placing wave per round: 44 KiB per round (256 VGPRs)
 
 // dst[0, len) = s[0, len), any alignment of either, by the 192 lanes of waves
 // 1-3 (pt = 0..191).  A wave takes rows of 63 destination chunks (16 bytes
@@ -239,6 +242,18 @@ __device__ uint64_t g_snappy_trace[kTraceFrags * 6];
   } while (0)
 #endif
 #define PSF_TRACE(f, k) PSF_TRACE_T(f, k, 0)
+#ifdef PSF_SNAPPY_TRACE
+__device__ uint64_t g_dfrag_trace[kTraceFrags * 4];
+#define PSF_DTRACE(f, k)                                                          \
+  do {                                                                            \
+    if (threadIdx.x == 0 && (f) < kTraceFrags)                                    \
+      g_dfrag_trace[(f) * 4 + (k)] = __builtin_amdgcn_s_memrealtime();            \
+  } while (0)
+#else
+#define PSF_DTRACE(f, k) \
+  do {                   \
+  } while (0)
+#endif
 
 constexpr uint32_t kCThreads = 512;  // 8 waves: parse (0), place (1-3), stage (4-7)
 constexpr uint32_t kStageT = 256;    // lanes of the staging waves
@@ -362,6 +377,31 @@ __global__ __launch_bounds__(kCThreads) void snappy_compress_frags(const uint8_t
             // would itself have been jc) or the table (slot alias).  Later lanes are
             // dropped and the next step starts after jc.
             uint32_t cand = 0, kbase = 0;
+            // probes 0 and 1 (at ip, ip + 1) first, as uniform values: data
+            // dense in short matches finds most of them there.  Probe 1 sees
+            // probe 0's table write when both hash alike.
+            if (ip + 1 > ip_limit) goto remainder;
+            {
+              const uint32_t v0 = uni(ld32(L.src, ip)), v1 = uni(ld32(L.src, ip + 1));
+              const uint32_t h0 = hash(v0, shift), h1 = hash(v1, shift);
+              const uint32_t c0 = uni(L.table[h0]);
+              const uint32_t c1 = h1 == h0 ? ip : uni(L.table[h1]);
+              const bool m0 = v0 == uni(ld32(L.src, c0));
+              const bool m1 = v1 == uni(ld32(L.src, c1));
+              if (lane == 0) L.table[h0] = (uint16_t)ip;
+              if (m0) {
+                cand = c0;
+                goto matched;
+              }
+              if (ip + 2 > ip_limit) goto remainder;  // probe 1 is past the limit
+              if (lane == 0) L.table[h1] = (uint16_t)(ip + 1);
+              if (m1) {
+                ip += 1;
+                cand = c1;
+                goto matched;
+              }
+              kbase = 2;
+            }
             for (;;) {
               const uint32_t k = kbase + lane;
               const uint32_t pos = ip + L.skip[k];
@@ -405,6 +445,7 @@ __global__ __launch_bounds__(kCThreads) void snappy_compress_frags(const uint8_t
               if ((vm & lim_mask) != lim_mask) goto remainder;
               kbase += (uint32_t)limit + 1;
             }
+          matched:
             op = emit_literal(out, op, srcb, next_emit, ip - next_emit, lane);
             // ---- emit copies while the next position matches immediately
             for (;;) {
@@ -536,46 +577,6 @@ struct Tag {
   bool lit;
 };
 
-// tag at b[0..]; up to 5 bytes are read
-__device__ __forceinline__ Tag parse_tag(const uint8_t* b, uint64_t p) {
-  Tag t;
-  const uint32_t c = b[0];
-  if ((c & 3) == 0) {
-    uint64_t L = (c >> 2) + 1;
-    uint32_t hl = 1;
-    if (L > 60) {
-      const uint32_t k = (uint32_t)L - 60;
-      uint32_t v = 0;
-      for (uint32_t i = 0; i < k; ++i) v |= (uint32_t)b[1 + i] << (8 * i);
-      L = (uint64_t)v + 1;
-      hl += k;
-    }
-    t.lit = true;
-    t.len = L;
-    t.off = 0;
-    t.hl = hl;
-    t.next = p + hl + L;
-  } else {
-    const uint32_t ty = c & 3;
-    t.lit = false;
-    if (ty == 1) {
-      t.len = 4 + ((c >> 2) & 7);
-      t.off = ((c >> 5) << 8) | b[1];
-      t.hl = 2;
-    } else if (ty == 2) {
-      t.len = (c >> 2) + 1;
-      t.off = b[1] | ((uint32_t)b[2] << 8);
-      t.hl = 3;
-    } else {
-      t.len = (c >> 2) + 1;
-      t.off = b[1] | ((uint32_t)b[2] << 8) | ((uint32_t)b[3] << 16) | ((uint32_t)b[4] << 24);
-      t.hl = 5;
-    }
-    t.next = p + t.hl;
-  }
-  return t;
-}
-
 // Branch-free decode of the tag whose first 5 bytes are x (little endian).
 __device__ __forceinline__ Tag decode_tag(uint64_t x, uint64_t p) {
   Tag t;
@@ -658,6 +659,83 @@ __device__ __forceinline__ uint64_t tag_bytes(const uint8_t* in, uint64_t C, uin
   return sh ? (lo >> sh) | ((uint64_t)d[2] << (64 - sh)) : lo;
 }
 
+// The host sized the launch from a hint (the FilterConfig's uncompressed
+// size): the stream's own varint header must say the same, else the host
+// redoes the call from the header (Varint::Parse32WithLimit).
+__device__ __forceinline__ bool header_matches(const uint8_t* __restrict__ in, uint64_t C, uint32_t hdr,
+                                               uint64_t dsize) {
+  const uint64_t h = tag_bytes(in, C, 0);
+  uint64_t v = 0;
+  uint32_t len = 0;
+  for (uint32_t i = 0; i < 5 && i < C; ++i) {
+    const uint32_t b = (uint32_t)(h >> (8 * i)) & 0xff;
+    if (i == 4 && b >= 16) break;
+    v |= (uint64_t)(b & 127u) << (7 * i);
+    if (b < 128) {
+      len = i + 1;
+      break;
+    }
+  }
+  return len == hdr && v == dsize;
+}
+
+// d[0, len) = s[0, len) for any alignment of either, by 256 lanes: byte
+// stores up to the first 16-aligned destination chunk, then chunks composed
+// from the 5 aligned source dwords that cover them (funnel shifts), 4 chunks
+// per lane per step with all loads issued before the stores (a wave's memory
+// counter retires in order: a load behind a store waits for it).  The loads
+// are unconditional (clamped), the stores predicated, so the compiler keeps
+// exact wait counts.
+__device__ __forceinline__ void copy_g2g(uint8_t* __restrict__ d, const uint8_t* __restrict__ s, uint32_t len,
+                                         uint32_t tid) {
+  uint32_t head = (uint32_t)(-reinterpret_cast<uintptr_t>(d) & 15);
+  if (head > len) head = len;
+  if (tid < head) d[tid] = s[tid];
+  d += head;
+  s += head;
+  len -= head;
+  const uintptr_t sa = reinterpret_cast<uintptr_t>(s);
+  const uint32_t sh = (uint32_t)(sa & 3) * 8;
+  const uint32_t* a = reinterpret_cast<const uint32_t*>(sa & ~(uintptr_t)3);
+  const uint32_t nv = len >> 4;
+  constexpr int U = 4;
+  for (uint32_t i0 = 0; i0 < nv; i0 += U * 256) {
+    uint32_t w[U][5];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = min(i0 + u * 256 + tid, nv - 1);
+      const uint32_t* q = a + 4 * i;
+      w[u][0] = q[0];
+      w[u][1] = q[1];
+      w[u][2] = q[2];
+      w[u][3] = q[3];
+      w[u][4] = q[sh ? 4 : 3];  // the fifth dword lies inside the source only when it is needed
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = i0 + u * 256 + tid;
+      uint4 v;
+      v.x = sh ? __builtin_amdgcn_alignbit(w[u][1], w[u][0], sh) : w[u][0];
+      v.y = sh ? __builtin_amdgcn_alignbit(w[u][2], w[u][1], sh) : w[u][1];
+      v.z = sh ? __builtin_amdgcn_alignbit(w[u][3], w[u][2], sh) : w[u][2];
+      v.w = sh ? __builtin_amdgcn_alignbit(w[u][4], w[u][3], sh) : w[u][3];
+      if (i < nv) reinterpret_cast<uint4*>(d)[i] = v;
+    }
+  }
+  for (uint32_t i = (nv << 4) + tid; i < len; i += 256) d[i] = s[i];
+}
+
+// Last-workgroup election by one device-scope counter.  No fence: what the
+// last workgroup goes on to do reads nothing the others wrote in this launch
+// (an agent-scope fence on MI355X writes back the XCD's whole L2, which
+// every workgroup of a streaming kernel would pay for).
+__device__ __forceinline__ bool last_block(uint32_t* ctr, uint32_t* s_last) {
+  __syncthreads();
+  if (threadIdx.x == 0) *s_last = atomicAdd(ctr, 1u) == gridDim.x - 1;
+  __syncthreads();
+  return *s_last;
+}
+
 // K0: link the chain directly when the stream is mostly 64 KiB fragments
 // stored as single literals (what a snappy 1.1.8 encoder emits for
 // incompressible fragments, e.g. FIXING_FLOAT codes): lane k decodes the tags
@@ -665,44 +743,26 @@ __device__ __forceinline__ uint64_t tag_bytes(const uint8_t* in, uint64_t C, uin
 // positions that hold a full literal is consumed in one step (512 fragments
 // per memory latency); other tags take a single step.  After kLitBudget
 // single steps the stream is handed to the window scan (K1) and its linker
-// (K2) through kFlagScan.  While every tag so far is a literal starting on a
-// 64 KiB output boundary and ending on the next one (or at the end of the
-// output), K0 also records each output fragment's first tag; if that holds to
-// the end, flags[1] = 1 tells K3 the stream is indexed and has no copies to
-// validate.
+// (K2) through kFlagScan.  K0 also records each output fragment's first tag
+// and checks the tags it steps over one at a time as K3 would (the full
+// literals have no copies); if it walks the whole stream, flags[1] = 1 tells
+// K3 there is nothing left to index or validate.
+// (One wave; its stores to a word are issued in program order, so the
+// initialisation needs no barrier.)
 constexpr int kLitRows = 8;
-__global__ __launch_bounds__(64) void snappy_dlit(const uint8_t* __restrict__ in, uint64_t C, uint32_t hdr,
-                                                  uint64_t dsize, uint32_t nwin, uint64_t* __restrict__ wentry,
-                                                  uint64_t* __restrict__ woff, uint64_t* __restrict__ fragpos,
-                                                  uint32_t* __restrict__ flags) {
-  const uint32_t lane = threadIdx.x;
+__device__ void dlit_body(const uint8_t* __restrict__ in, uint64_t C, uint32_t hdr, uint64_t dsize, uint32_t nwin,
+                          uint64_t* __restrict__ wentry, uint64_t* __restrict__ woff, uint64_t* __restrict__ fragpos,
+                          uint32_t* __restrict__ flags, uint32_t lane) {
   for (uint32_t i = lane; i < nwin; i += 64) wentry[i] = kNone;
   if (lane == 0) flags[1] = 0;
-  __syncthreads();
-  {  // the host sized the launch from a hint (the FilterConfig's uncompressed
-     // size): the stream's own varint header must say the same, else the host
-     // redoes the call from the header (Varint::Parse32WithLimit)
-    const uint64_t h = tag_bytes(in, C, 0);
-    uint64_t v = 0;
-    uint32_t len = 0;
-    for (uint32_t i = 0; i < 5 && i < C; ++i) {
-      const uint32_t b = (uint32_t)(h >> (8 * i)) & 0xff;
-      if (i == 4 && b >= 16) break;
-      v |= (uint64_t)(b & 127u) << (7 * i);
-      if (b < 128) {
-        len = i + 1;
-        break;
-      }
-    }
-    if (len != hdr || v != dsize) {
-      if (lane == 0) *flags = kFlagHeader;
-      return;
-    }
+  if (!header_matches(in, C, hdr, dsize)) {
+    if (lane == 0) *flags = kFlagHeader;
+    return;
   }
   uint64_t p = hdr, o = 0;
   int64_t last_w = -1;
   uint32_t singles = 0;
-  bool bad = false, pure = true, wide = true;
+  bool bad = false, serial = false, wide = true;
   while (p < C) {
     bool full[kLitRows];
     uint64_t pk[kLitRows];
@@ -730,7 +790,7 @@ __global__ __launch_bounds__(64) void snappy_dlit(const uint8_t* __restrict__ in
     }
     if (c > 0) {
       const bool aligned = (o & (kFrag - 1)) == 0;
-      pure = pure && aligned;
+      serial = serial || !aligned;  // full literals across output fragments
 #pragma unroll
       for (int j = 0; j < kLitRows; ++j) {
         const uint32_t idx = lane + 64 * j;
@@ -751,17 +811,23 @@ __global__ __launch_bounds__(64) void snappy_dlit(const uint8_t* __restrict__ in
       wide = false;
       const uint64_t t0next = __shfl(t0.next, 0, 64), t0len = __shfl(t0.len, 0, 64);
       const bool t0lit = __shfl((int)t0.lit, 0, 64) != 0;
+      const uint32_t t0off = __shfl(t0.off, 0, 64);
       const int64_t w0 = (int64_t)((p - hdr) / kWin);
-      // still indexed: a literal from a fragment boundary to the next one or to the end
-      const bool keep = t0lit && (o & (kFrag - 1)) == 0 && t0len <= kFrag && (t0len == kFrag || o + t0len == dsize);
       if (lane == 0) {
         if (w0 > last_w) {
           wentry[w0] = p;
           woff[w0] = o;
         }
-        if (pure && keep) fragpos[o / kFrag] = p;
+        if ((o & (kFrag - 1)) == 0) fragpos[o / kFrag] = p;  // the tag that starts an output fragment
       }
-      pure = pure && keep;
+      // what K3 checks, for the tags seen one at a time (the full literals
+      // of the wide steps have no copies): a copy within the output so far,
+      // and no tag or copy across output fragments (else the one-lane decoder)
+      if (!t0lit) {
+        if (t0off == 0 || t0off > o) bad = true;
+        else if (o - t0off < (o & ~(uint64_t)(kFrag - 1))) serial = true;
+      }
+      if (o / kFrag != (o + t0len - 1) / kFrag) serial = true;
       if (w0 > last_w) last_w = w0;
       p = t0next;
       o += t0len;
@@ -777,62 +843,102 @@ __global__ __launch_bounds__(64) void snappy_dlit(const uint8_t* __restrict__ in
   }
   const bool ok = !(bad || p != C || o != dsize);
   if (lane == 0) {
-    *flags = ok ? 0u : kFlagInvalid;
-    flags[1] = ok && pure ? 1u : 0u;
+    *flags = !ok ? kFlagInvalid : serial ? kFlagSerial : 0u;
+    flags[1] = ok ? 1u : 0u;  // every tag seen: K3 has nothing to add
   }
 }
 
-constexpr uint32_t kStarts = 64;  // K1 parses from each of the first 64 offsets of a window
-
-// K1: speculative parse of each window from each of its first 64 byte offsets
-// (lane l from offset l).  A window's true entry is one of them unless a literal
-// carried the chain further in; for those K2 walks until it meets lane 0's chain.
-__global__ __launch_bounds__(64) void snappy_dscan(const uint8_t* __restrict__ in, uint64_t C, uint32_t hdr,
-                                                   uint32_t* __restrict__ bitmap, uint32_t* __restrict__ cum,
-                                                   uint64_t* __restrict__ wexit, uint64_t* __restrict__ wtotal,
-                                                   const uint32_t* __restrict__ flags) {
-  __shared__ uint32_t b32[(kWin + 32) / 4];
-  __shared__ uint32_t bm[kWin / 32];
-  if (!(*flags & kFlagScan)) return;  // K0 linked the stream already
-  const uint32_t lane = threadIdx.x, w = blockIdx.x;
-  const uint64_t base = hdr + (uint64_t)w * kWin;
-  const uint32_t wl = (uint32_t)min((uint64_t)kWin, C - base);
-  const uint32_t s = stage(b32, in, C, base, wl + 16, lane);
-  for (uint32_t i = lane; i < kWin / 32; i += 64) bm[i] = 0;
+// K-spec: every output fragment k is first taken to be stored as one literal
+// at hdr + k * (65536 + 3) -- what a 1.1.8 encoder writes for a stream of
+// incompressible fragments (FIXING_FLOAT codes).  A workgroup checks its
+// fragment's tag there and, if it is the literal that fills the fragment,
+// copies it at once.  If every fragment checks out and the last literal ends
+// the stream, the stream is exactly that chain (fragment 0's tag follows the
+// header, and each checked literal ends where the next is checked): decoded
+// and valid, as the last workgroup to finish records.  One more workgroup
+// runs K0 alongside (its verdict and index agree with that on such a stream);
+// otherwise the kernels after this one redo every fragment whose true
+// position differs from the one assumed here (specpos).
+__global__ __launch_bounds__(256) void snappy_dspec(const uint8_t* __restrict__ in, uint64_t C, uint32_t hdr,
+                                                    uint64_t dsize, uint32_t nfo, uint32_t nwin,
+                                                    uint64_t* __restrict__ wentry, uint64_t* __restrict__ woff,
+                                                    uint64_t* __restrict__ fragpos, uint64_t* __restrict__ specpos,
+                                                    uint32_t* __restrict__ flags, uint32_t* __restrict__ ctr,
+                                                    uint8_t* __restrict__ out, PubSlot* pub, uint32_t ticket) {
+  __shared__ uint32_t s_last, s_checked;
+  const uint32_t tid = threadIdx.x, k = blockIdx.x, nspec = gridDim.x - 1;
+  if (k == nspec) {  // the extra workgroup links the stream meanwhile (K0), needed or not
+    if (tid < 64) dlit_body(in, C, hdr, dsize, nwin, wentry, woff, fragpos, flags, tid);
+    return;
+  }
+  const uint64_t o0 = (uint64_t)k * kFrag;
+  const uint32_t end = (uint32_t)min((uint64_t)kFrag, dsize - o0);  // 0 only for an empty output
+  const uint64_t p = hdr + (uint64_t)k * kFullLit;
+  bool ok = k > 0 || header_matches(in, C, hdr, dsize);
+  uint32_t hl = 0;
+  if (end == 0) {
+    ok = ok && C == hdr;
+  } else {
+    hl = end - 1 < 60 ? 1 : ((31 - __builtin_clz(end - 1)) >> 3) + 2;
+    const Tag t = decode_tag(tag_bytes(in, C, p), p);
+    ok = ok && p < C && t.lit && t.len == end && t.hl == hl && t.next <= C && (k + 1 < nfo || t.next == C);
+  }
+  // A fragment after one that is not stored (a 1.1.8 encoder found a match in
+  // it) sits a few bytes off its assumed place: look for its literal within
+  // +-128 bytes and copy it from there too.  That is a guess only (it does not
+  // count as checked); K4 redoes the fragment unless K0/K3 find it there.
+  uint64_t at = ok ? p : kNone;
+  if (!ok && end && k > 0) {
+    __shared__ uint32_t s_best;
+    if (tid == 0) s_best = 0xffffffffu;
+    __syncthreads();
+    const int32_t dl = (int32_t)tid - 128;
+    const uint64_t q = p + dl;
+    if (dl != 0 && q < C) {
+      const Tag t = decode_tag(tag_bytes(in, C, q), q);
+      if (t.lit && t.len == end && t.hl == hl && t.next <= C && (k + 1 < nfo || t.next == C))
+        atomicMin(&s_best, ((uint32_t)abs(dl) << 9) | tid);
+    }
+    __syncthreads();
+    if (s_best != 0xffffffffu) at = p + (int32_t)(s_best & 511) - 128;
+  }
+  if (at != kNone) copy_g2g(out + o0, in + at + hl, end, tid);
+  if (tid == 0) specpos[k] = at;
+  // one counter for both: workgroups done (high word) and fragments checked
   __syncthreads();
-  uint64_t p = lane, o = 0;
-  bool alive = p < wl;
-  while (__ballot(alive)) {
-    if (alive) {
-      if (lane == 0) {
-        atomicOr(&bm[p >> 5], 1u << (p & 31));
-        cum[base + p] = (uint32_t)o;
+  if (tid == 0) {
+    const unsigned long long old =
+        atomicAdd(reinterpret_cast<unsigned long long*>(ctr), (1ull << 32) | (ok ? 1ull : 0ull));
+    s_last = (uint32_t)(old >> 32) == nspec - 1;
+    s_checked = (uint32_t)old + (ok ? 1u : 0u);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  if (s_checked == nspec) {
+    if (tid == 0) {
+      flags[0] = 0;
+      flags[1] = 1;
+      flags[2] = 1;  // decoded: the kernels after this one have nothing to do
+      if (pub) {
+        pub->status = kOk;
+        pub->size = dsize;
+        publish_ticket(pub, ticket);
       }
-      const Tag t = lds_tag(b32, s + p, p);
-      o += t.len;
-      p = t.next;
-      alive = p < wl;
     }
   }
-  wexit[(size_t)w * kStarts + lane] = base + p;
-  wtotal[(size_t)w * kStarts + lane] = o;
-  __syncthreads();
-  uint32_t* gb = bitmap + (size_t)w * (kWin / 32);
-  for (uint32_t i = lane; i < kWin / 32; i += 64) gb[i] = bm[i];
 }
+
+
+constexpr uint32_t kStarts = 64;  // K1 parses from each of the first 64 offsets of a window
 
 // K2: link the windows along the true chain (one lane).  Every step costs
 // one memory latency: windows are entered in increasing order, so the
 // first-entry bookkeeping stays in registers, and the bitmap word and the
 // next tag's bytes (two aligned dwords) are loaded together.
-__global__ __launch_bounds__(64) void snappy_dlink(const uint8_t* __restrict__ in, uint64_t C, uint32_t hdr,
-                                                   uint64_t dsize, const uint32_t* __restrict__ bitmap,
-                                                   const uint32_t* __restrict__ cum,
-                                                   const uint64_t* __restrict__ wexit,
-                                                   const uint64_t* __restrict__ wtotal, uint32_t nwin,
-                                                   uint64_t* __restrict__ wentry, uint64_t* __restrict__ woff,
-                                                   uint32_t* __restrict__ flags) {
-  if (!(*flags & kFlagScan)) return;  // K0 linked the stream already
+__device__ void dlink_body(const uint8_t* __restrict__ in, uint64_t C, uint32_t hdr, uint64_t dsize,
+                           const uint32_t* __restrict__ bitmap, const uint32_t* __restrict__ cum,
+                           const uint64_t* __restrict__ wexit, const uint64_t* __restrict__ wtotal, uint32_t nwin,
+                           uint64_t* __restrict__ wentry, uint64_t* __restrict__ woff, uint32_t* __restrict__ flags) {
   for (uint32_t i = threadIdx.x; i < nwin; i += 64) wentry[i] = kNone;
   __syncthreads();
   if (threadIdx.x != 0) return;
@@ -891,6 +997,55 @@ __global__ __launch_bounds__(64) void snappy_dlink(const uint8_t* __restrict__ i
   else *flags = 0;
 }
 
+// K1: speculative parse of each window from each of its first 64 byte offsets
+// (lane l from offset l).  A window's true entry is one of them unless a literal
+// carried the chain further in; for those K2 walks until it meets lane 0's chain.
+__global__ __launch_bounds__(64) void snappy_dscan(const uint8_t* __restrict__ in, uint64_t C, uint32_t hdr,
+                                                   uint32_t* __restrict__ bitmap, uint32_t* __restrict__ cum,
+                                                   uint64_t* __restrict__ wexit, uint64_t* __restrict__ wtotal,
+                                                   const uint32_t* __restrict__ flags) {
+  __shared__ uint32_t b32[(kWin + 32) / 4];
+  __shared__ uint32_t bm[kWin / 32];
+  if (!(*flags & kFlagScan)) return;  // K0 linked the stream already
+  const uint32_t lane = threadIdx.x, w = blockIdx.x;
+  const uint64_t base = hdr + (uint64_t)w * kWin;
+  const uint32_t wl = (uint32_t)min((uint64_t)kWin, C - base);
+  const uint32_t s = stage(b32, in, C, base, wl + 16, lane);
+  for (uint32_t i = lane; i < kWin / 32; i += 64) bm[i] = 0;
+  __syncthreads();
+  uint64_t p = lane, o = 0;
+  bool alive = p < wl;
+  while (__ballot(alive)) {
+    if (alive) {
+      if (lane == 0) {
+        atomicOr(&bm[p >> 5], 1u << (p & 31));
+        cum[base + p] = (uint32_t)o;
+      }
+      const Tag t = lds_tag(b32, s + p, p);
+      o += t.len;
+      p = t.next;
+      alive = p < wl;
+    }
+  }
+  wexit[(size_t)w * kStarts + lane] = base + p;
+  wtotal[(size_t)w * kStarts + lane] = o;
+  __syncthreads();
+  uint32_t* gb = bitmap + (size_t)w * (kWin / 32);
+  for (uint32_t i = lane; i < kWin / 32; i += 64) gb[i] = bm[i];
+}
+
+// K2 as its own launch: it reads what every K1 workgroup wrote
+__global__ __launch_bounds__(64) void snappy_dlink(const uint8_t* __restrict__ in, uint64_t C, uint32_t hdr,
+                                                   uint64_t dsize, const uint32_t* __restrict__ bitmap,
+                                                   const uint32_t* __restrict__ cum,
+                                                   const uint64_t* __restrict__ wexit,
+                                                   const uint64_t* __restrict__ wtotal, uint32_t nwin,
+                                                   uint64_t* __restrict__ wentry, uint64_t* __restrict__ woff,
+                                                   uint32_t* __restrict__ flags) {
+  if (!(*flags & kFlagScan)) return;  // K0 linked the stream already
+  dlink_body(in, C, hdr, dsize, bitmap, cum, wexit, wtotal, nwin, wentry, woff, flags);
+}
+
 // K3: validate copies and index the tag that starts each output fragment
 __global__ __launch_bounds__(64) void snappy_dindex(const uint8_t* __restrict__ in, uint64_t C, uint32_t hdr,
                                                     const uint64_t* __restrict__ wentry,
@@ -935,113 +1090,49 @@ __global__ __launch_bounds__(64) void snappy_dindex(const uint8_t* __restrict__ 
   if (fl) atomicOr(flags, fl);
 }
 
-// K4: one wave per 64 KiB output fragment, decoded in LDS; tags and short
-// literals are read from a staged window of the compressed bytes
-__global__ __launch_bounds__(64) void snappy_dfrag(const uint8_t* __restrict__ in, uint64_t C, uint64_t dsize,
-                                                   const uint64_t* __restrict__ fragpos,
-                                                   const uint32_t* __restrict__ flags, uint8_t* __restrict__ out) {
-  __shared__ uint32_t ob32[kFrag / 4];
-  __shared__ uint32_t ib32[(kInWin + 32) / 4];
-  if (*flags) return;
-  uint8_t* ob = reinterpret_cast<uint8_t*>(ob32);
-  const uint32_t lane = threadIdx.x, k = blockIdx.x;
-  const uint64_t o0 = (uint64_t)k * kFrag;
-  const uint32_t end = (uint32_t)min((uint64_t)kFrag, dsize - o0);
-  constexpr uint32_t kSpan = kInWin + 16;  // staged bytes [wb, wb + kSpan)
-  uint64_t p = fragpos[k];
-  {  // a fragment stored as one literal was copied by snappy_dstored
-    const Tag t0 = decode_tag(tag_bytes(in, C, p), p);
-    if (t0.lit && t0.len == end) return;
+// A literal too long for the staging window, read straight into the LDS
+// fragment: 16-byte LDS stores to the aligned chunks, each composed from the
+// two aligned 16-byte source blocks it straddles; 8 chunks per lane in
+// flight (8 KiB per memory latency for the wave), bytes at the edges.
+__device__ void literal_to_lds(uint8_t* ob, uint32_t o, const uint8_t* __restrict__ in, uint64_t src, uint32_t L,
+                               uint32_t lane) {
+  const uint32_t head = (16 - (o & 15)) & 15;
+  if (head >= L) {
+    for (uint32_t i = lane; i < L; i += 64) ob[o + i] = in[src + i];
+    return;
   }
-  uint64_t wb = p;
-  uint32_t s = stage(ib32, in, C, wb, kSpan, lane);
-  uint32_t o = 0;
-  while (o < end) {
-    if (p + 8 > wb + kSpan) {
-      wb = p;
-      s = stage(ib32, in, C, wb, kSpan, lane);
+  if (lane < head) ob[o + lane] = in[src + lane];
+  const uint32_t nc = (L - head) >> 4;
+  const uintptr_t sp = reinterpret_cast<uintptr_t>(in + src + head);
+  const uint4* s16 = reinterpret_cast<const uint4*>(sp & ~(uintptr_t)15);
+  const uint32_t sh = (uint32_t)(sp & 15);
+  uint4* d16 = reinterpret_cast<uint4*>(ob + o + head);
+  constexpr int U = 8;
+  for (uint32_t c0 = 0; c0 < nc; c0 += U * 64) {
+    uint4 lo[U], hi[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t c = c0 + u * 64 + lane;
+      lo[u] = c < nc ? s16[c] : make_uint4(0, 0, 0, 0);
+      hi[u] = (c < nc && sh) ? s16[c + 1] : lo[u];
     }
-    const Tag t = lds_tag(ib32, s + (p - wb), p);
-    const uint32_t L = (uint32_t)t.len;
-    if (t.lit) {
-      const uint64_t src = p + t.hl;
-      if (src + L > wb + kSpan && L <= kInWin) {
-        wb = src;
-        s = stage(ib32, in, C, wb, kSpan, lane);
-      }
-      if (src + L <= wb + kSpan) {
-        const uint8_t* q = reinterpret_cast<const uint8_t*>(ib32) + s + (src - wb);
-        for (uint32_t i = lane; i < L; i += 64) ob[o + i] = q[i];
-      } else {
-        for (uint32_t i = lane; i < L; i += 64) ob[o + i] = in[src + i];
-      }
-    } else if (t.off >= L) {
-      for (uint32_t i = lane; i < L; i += 64) ob[o + i] = ob[o - t.off + i];
-    } else {
-      for (uint32_t i = lane; i < L; i += 64) ob[o + i] = ob[o - t.off + i % t.off];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t c = c0 + u * 64 + lane;
+      if (c < nc) d16[c] = funnel16(lo[u], hi[u], sh);
     }
-    o += L;
-    p = t.next;
   }
-  __syncthreads();
-  uint8_t* d = out + o0;
-  if ((reinterpret_cast<uintptr_t>(d) & 15) == 0) {
-    const uint32_t nv = end >> 4;
-    for (uint32_t i = lane; i < nv; i += 64)
-      reinterpret_cast<uint4*>(d)[i] = reinterpret_cast<const uint4*>(ob32)[i];
-    for (uint32_t i = (nv << 4) + lane; i < end; i += 64) d[i] = ob[i];
-  } else {
-    for (uint32_t i = lane; i < end; i += 64) d[i] = ob[i];
-  }
+  const uint32_t t0 = head + 16 * nc;
+  if (lane < L - t0) ob[o + t0 + lane] = in[src + t0 + lane];
 }
 
-// K4a: fragments stored as one literal: a straight copy from the compressed
-// stream, 256 lanes x 16 B per step, unaligned source realigned with funnel
-// shifts (aligned dword loads only)
-__global__ __launch_bounds__(256) void snappy_dstored(const uint8_t* __restrict__ in, uint64_t C, uint64_t dsize,
-                                                      const uint64_t* __restrict__ fragpos,
-                                                      const uint32_t* __restrict__ flags, uint8_t* __restrict__ out) {
-  if (*flags) return;
-  const uint32_t k = blockIdx.x;
-  const uint64_t o0 = (uint64_t)k * kFrag;
-  const uint32_t end = (uint32_t)min((uint64_t)kFrag, dsize - o0);
-  const uint64_t p = fragpos[k];
-  const Tag t = decode_tag(tag_bytes(in, C, p), p);
-  if (!(t.lit && t.len == end)) return;
-  const uint64_t src = p + t.hl;
-  uint8_t* d = out + o0;
-  const uintptr_t ia = reinterpret_cast<uintptr_t>(in);
-  const uint32_t sh = (uint32_t)((ia + src) & 3) * 8;
-  const uint32_t* a = reinterpret_cast<const uint32_t*>((ia + src) & ~(uintptr_t)3);
-  const uint32_t nv = ((reinterpret_cast<uintptr_t>(d) & 15) == 0) ? end >> 4 : 0;
-  for (uint32_t i = threadIdx.x; i < nv; i += 256) {
-    // 16 output bytes from the 5 aligned dwords that cover them; the fifth is
-    // only read when the source is misaligned (then it lies inside the stream)
-    const uint32_t* q = a + 4 * i;
-    const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3];
-    const uint32_t w4 = sh ? q[4] : 0u;
-    uint4 v;
-    v.x = sh ? __builtin_amdgcn_alignbit(w1, w0, sh) : w0;
-    v.y = sh ? __builtin_amdgcn_alignbit(w2, w1, sh) : w1;
-    v.z = sh ? __builtin_amdgcn_alignbit(w3, w2, sh) : w2;
-    v.w = sh ? __builtin_amdgcn_alignbit(w4, w3, sh) : w3;
-    reinterpret_cast<uint4*>(d)[i] = v;
-  }
-  for (uint32_t i = (nv << 4) + threadIdx.x; i < end; i += 256) d[i] = in[src + i];
-}
-
-// K5: the verdict; one-lane decode of valid streams K4 could not split
-__global__ __launch_bounds__(64) void snappy_dfinish(const uint8_t* __restrict__ in, uint64_t C, uint32_t hdr,
-                                                     uint64_t dsize, const uint32_t* __restrict__ flags,
-                                                     uint8_t* __restrict__ out, PubSlot* pub, uint32_t ticket) {
-  if (threadIdx.x != 0) return;
-  const uint32_t f = *flags;
+// K5 body: the verdict; one-lane decode of valid streams K4 could not split
+__device__ void dfinish_body(const uint8_t* __restrict__ in, uint64_t C, uint32_t hdr, uint64_t dsize, uint32_t f,
+                             uint8_t* __restrict__ out, PubSlot* pub, uint32_t ticket) {
   if (f == kFlagSerial) {
     uint64_t p = hdr, o = 0;
-    uint8_t tb[5];
     while (p < C) {
-      for (int i = 0; i < 5; ++i) tb[i] = p + i < C ? in[p + i] : 0;
-      const Tag t = parse_tag(tb, p);
+      const Tag t = decode_tag(tag_bytes(in, C, p), p);
       if (t.lit) {
         for (uint64_t i = 0; i < t.len; ++i) out[o + i] = in[p + t.hl + i];
       } else {
@@ -1056,6 +1147,117 @@ __global__ __launch_bounds__(64) void snappy_dfinish(const uint8_t* __restrict__
     pub->size = dsize;
     publish_ticket(pub, ticket);
   }
+}
+
+constexpr uint32_t kFewTags = 8;  // K4 decodes a fragment of at most this many tags without LDS
+
+// K4: one workgroup per 64 KiB output fragment whose true position differs
+// from the one K-spec assumed.  A fragment stored as one literal is copied by
+// all 256 lanes; any other is decoded by wave 0 in LDS (tags and short
+// literals read from a staged window of the compressed bytes) and written
+// out by all.  The last workgroup to finish gives the verdict (K5).
+__global__ __launch_bounds__(256) void snappy_dfrag(const uint8_t* __restrict__ in, uint64_t C, uint32_t hdr,
+                                                    uint64_t dsize, const uint64_t* __restrict__ fragpos,
+                                                    const uint64_t* __restrict__ specpos,
+                                                    const uint32_t* __restrict__ flags, uint32_t* __restrict__ ctr,
+                                                    uint8_t* __restrict__ out, PubSlot* pub, uint32_t ticket) {
+  __shared__ uint32_t ob32[kFrag / 4];
+  __shared__ uint32_t ib32[(kInWin + 32) / 4];
+  __shared__ uint32_t s_last, s_n, s_o[kFewTags], s_len[kFewTags], s_off[kFewTags];
+  __shared__ uint64_t s_src[kFewTags];
+  if (flags[2]) return;  // K-spec decoded the whole stream and gave the verdict
+  const uint32_t f = flags[0];
+  uint8_t* ob = reinterpret_cast<uint8_t*>(ob32);
+  const uint32_t tid = threadIdx.x, k = blockIdx.x;
+  const uint64_t o0 = (uint64_t)k * kFrag;
+  const uint32_t end = (uint32_t)min((uint64_t)kFrag, dsize - o0);
+  PSF_DTRACE(k, 0);
+  const uint64_t p0 = end ? fragpos[k] : kNone;
+  if (f == 0 && end && p0 != specpos[k]) {
+    PSF_DTRACE(k, 1);
+    const Tag t0 = decode_tag(tag_bytes(in, C, p0), p0);
+    // a fragment of a few tags (stored data with a match or two): its tags
+    // walked by one lane, literals copied global to global by all, then the
+    // copies in order
+    if (tid == 0) {
+      uint64_t p = p0;
+      uint32_t o = 0, n = 0;
+      while (o < end && n < kFewTags) {
+        const Tag t = decode_tag(tag_bytes(in, C, p), p);
+        s_o[n] = o;
+        s_len[n] = (uint32_t)t.len;
+        s_off[n] = t.off;
+        s_src[n] = t.lit ? p + t.hl : kNone;
+        o += (uint32_t)t.len;
+        p = t.next;
+        ++n;
+      }
+      s_n = o >= end ? n : kFewTags + 1;
+    }
+    __syncthreads();
+    const uint32_t nt = s_n;
+    if (nt <= kFewTags) {
+      uint8_t* d = out + o0;
+      for (uint32_t i = 0; i < nt; ++i)
+        if (s_src[i] != kNone) copy_g2g(d + s_o[i], in + s_src[i], s_len[i], tid);
+      __syncthreads();
+      for (uint32_t i = 0; i < nt; ++i) {
+        if (s_src[i] != kNone) continue;
+        const uint32_t o = s_o[i], L = s_len[i], off = s_off[i];
+        for (uint32_t j = tid; j < L; j += 256) d[o + j] = d[o - off + (off >= L ? j : j % off)];
+        __syncthreads();
+      }
+    } else if (t0.lit && t0.len == end) {
+      copy_g2g(out + o0, in + p0 + t0.hl, end, tid);
+    } else {
+      if (tid < 64) {
+        const uint32_t lane = tid;
+        constexpr uint32_t kSpan = kInWin + 16;  // staged bytes [wb, wb + kSpan)
+        uint64_t p = p0, wb = p0;
+        uint32_t s = stage(ib32, in, C, wb, kSpan, lane);
+        uint32_t o = 0;
+        while (o < end) {
+          if (p + 8 > wb + kSpan) {
+            wb = p;
+            s = stage(ib32, in, C, wb, kSpan, lane);
+          }
+          const Tag t = lds_tag(ib32, s + (p - wb), p);
+          const uint32_t L = (uint32_t)t.len;
+          if (t.lit) {
+            const uint64_t src = p + t.hl;
+            if (src + L > wb + kSpan && L <= kInWin) {
+              wb = src;
+              s = stage(ib32, in, C, wb, kSpan, lane);
+            }
+            if (src + L <= wb + kSpan) {
+              const uint8_t* q = reinterpret_cast<const uint8_t*>(ib32) + s + (src - wb);
+              for (uint32_t i = lane; i < L; i += 64) ob[o + i] = q[i];
+            } else {
+              literal_to_lds(ob, o, in, src, L, lane);
+            }
+          } else if (t.off >= L) {
+            for (uint32_t i = lane; i < L; i += 64) ob[o + i] = ob[o - t.off + i];
+          } else {
+            for (uint32_t i = lane; i < L; i += 64) ob[o + i] = ob[o - t.off + i % t.off];
+          }
+          o += L;
+          p = t.next;
+        }
+      }
+      __syncthreads();
+      uint8_t* d = out + o0;
+      if ((reinterpret_cast<uintptr_t>(d) & 15) == 0) {
+        const uint32_t nv = end >> 4;
+        for (uint32_t i = tid; i < nv; i += 256)
+          reinterpret_cast<uint4*>(d)[i] = reinterpret_cast<const uint4*>(ob32)[i];
+        for (uint32_t i = (nv << 4) + tid; i < end; i += 256) d[i] = ob[i];
+      } else {
+        for (uint32_t i = tid; i < end; i += 256) d[i] = ob[i];
+      }
+    }
+  }
+  PSF_DTRACE(k, 2);
+  if (last_block(ctr, &s_last) && tid == 0) dfinish_body(in, C, hdr, dsize, f, out, pub, ticket);
 }
 
 }  // namespace
@@ -1095,47 +1297,46 @@ int snappy_compress_launch(const void* in, size_t n, void* out, void* scratch, h
 size_t snappy_uncompress_scratch(size_t C, size_t dsize) {
   const size_t nwin = (C + kWin - 1) / kWin + 1;
   const size_t nfo = (dsize + kFrag - 1) / kFrag + 1;
-  return nwin * (kWin / 8) + C * 4 + nwin * 8 * (2 * kStarts + 2) + nfo * 8 + 256;
+  return nwin * (kWin / 8) + C * 4 + nwin * 8 * (2 * kStarts + 2) + 2 * nfo * 8 + 256;
 }
 
+// Five launches: K-spec (+ K0 in one more workgroup), K1, K2, K3, K4 (+ K5
+// in its last workgroup).  On a stream of stored fragments K-spec decodes
+// everything and the others return at once.
 int snappy_uncompress_launch(const void* in, size_t C, uint32_t hdr, size_t dsize, void* out, void* scratch,
                              hipStream_t st, Profiler* prof, PubSlot* pub, uint32_t ticket) {
   if (hdr == 0 || hdr > C || hdr > 5) return kErrArg;
   const uint64_t body = C - hdr;
   const uint32_t nwin = (uint32_t)((body + kWin - 1) / kWin);
   const uint32_t nfo = (uint32_t)((dsize + kFrag - 1) / kFrag);
+  const uint32_t nfo1 = nfo ? nfo : 1;  // an empty output still takes one workgroup (header check, verdict)
   uint8_t* s = static_cast<uint8_t*>(scratch);
-  uint32_t* flags = reinterpret_cast<uint32_t*>(s);
+  uint32_t* flags = reinterpret_cast<uint32_t*>(s);  // [0] verdict, [1] indexed, [2] decoded by K-spec
+  uint32_t* ctr = flags + 4;  // last-workgroup counters: K-spec (64 bits: done | checked), K4
   uint64_t* wexit = reinterpret_cast<uint64_t*>(s + 64);
   uint64_t* wtotal = wexit + (size_t)(nwin + 1) * kStarts;
   uint64_t* wentry = wtotal + (size_t)(nwin + 1) * kStarts;
   uint64_t* woff = wentry + (nwin + 1);
   uint64_t* fragpos = woff + (nwin + 1);
-  uint32_t* bitmap = reinterpret_cast<uint32_t*>(fragpos + (nfo + 1));
+  uint64_t* specpos = fragpos + (nfo + 1);
+  uint32_t* bitmap = reinterpret_cast<uint32_t*>(specpos + (nfo + 1));
   uint32_t* cum = bitmap + (size_t)(nwin + 1) * (kWin / 32);
   const uint8_t* src = static_cast<const uint8_t*>(in);
   uint8_t* dst = static_cast<uint8_t*>(out);
+  if (hipMemsetAsync(s, 0, 32, st) != hipSuccess) return kErrHip;
   ProfScope ps(prof, kKSnappyDecompress, st, (double)C + (double)dsize);
-  hipLaunchKernelGGL(snappy_dlit, dim3(1), dim3(64), 0, st, src, (uint64_t)C, hdr, (uint64_t)dsize, nwin, wentry,
-                     woff, fragpos, flags);
+  hipLaunchKernelGGL(snappy_dspec, dim3(nfo1 + 1), dim3(256), 0, st, src, (uint64_t)C, hdr, (uint64_t)dsize, nfo, nwin,
+                     wentry, woff, fragpos, specpos, flags, ctr, dst, pub, ticket);
   if (nwin) {
     hipLaunchKernelGGL(snappy_dscan, dim3(nwin), dim3(64), 0, st, src, (uint64_t)C, hdr, bitmap, cum, wexit,
                        wtotal, flags);
-  }
-  hipLaunchKernelGGL(snappy_dlink, dim3(1), dim3(64), 0, st, src, (uint64_t)C, hdr, (uint64_t)dsize, bitmap, cum,
-                     wexit, wtotal, nwin, wentry, woff, flags);
-  if (nwin) {
+    hipLaunchKernelGGL(snappy_dlink, dim3(1), dim3(64), 0, st, src, (uint64_t)C, hdr, (uint64_t)dsize, bitmap, cum,
+                       wexit, wtotal, nwin, wentry, woff, flags);
     hipLaunchKernelGGL(snappy_dindex, dim3(nwin), dim3(64), 0, st, src, (uint64_t)C, hdr, wentry, woff, fragpos,
                        flags);
   }
-  if (nfo) {
-    hipLaunchKernelGGL(snappy_dstored, dim3(nfo), dim3(256), 0, st, src, (uint64_t)C, (uint64_t)dsize, fragpos,
-                       flags, dst);
-    hipLaunchKernelGGL(snappy_dfrag, dim3(nfo), dim3(64), 0, st, src, (uint64_t)C, (uint64_t)dsize, fragpos, flags,
-                       dst);
-  }
-  hipLaunchKernelGGL(snappy_dfinish, dim3(1), dim3(64), 0, st, src, (uint64_t)C, hdr, (uint64_t)dsize, flags, dst,
-                     pub, ticket);
+  hipLaunchKernelGGL(snappy_dfrag, dim3(nfo1), dim3(256), 0, st, src, (uint64_t)C, hdr, (uint64_t)dsize, fragpos,
+                     specpos, flags, ctr + 2, dst, pub, ticket);
   return launch_status();
 }
 
@@ -1143,6 +1344,11 @@ int snappy_uncompress_launch(const void* in, size_t C, uint32_t hdr, size_t dsiz
 
 #ifdef PSF_SNAPPY_TRACE
 // diagnostic builds: copy the compress kernel's phase timestamps out
+extern "C" int psf_debug_dfrag_trace(void* out, size_t bytes) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(psf::g_dfrag_trace), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess
+             ? 0
+             : -4;
+}
 extern "C" int psf_debug_snappy_trace(void* out, size_t bytes) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(psf::g_snappy_trace), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess
              ? 0

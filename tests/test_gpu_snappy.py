@@ -231,3 +231,20 @@ def test_decode_size_hint_vs_header(ctx, port):
     lib().psf_fc_add_uncompressed(m.h, idx, data.size)
     with pytest.raises(PsfError):
         F.RemoteNode(ctx).decode(m)
+
+
+@pytest.mark.parametrize("where", [0, 5, 37])
+def test_decode_stored_stream_with_shifted_tail(ctx, port, where):
+    """Incompressible fragments (each one stored literal) with one fragment
+    that has a match: every later fragment sits a few bytes off the place the
+    stored-stream fast path (K-spec) assumes, and the ones it guesses right
+    must agree with the linked positions; the decode is exact."""
+    rng = np.random.default_rng(where)
+    n = 40 * 65536 + 12345
+    x = rng.integers(0, 256, n, dtype=np.uint8)
+    base = where * 65536 + 3000
+    x[base + 100:base + 140] = x[base:base + 40]  # one 40-byte match
+    s = port.snappy_compress(x.tobytes())
+    for off in (0, 1, 3):
+        got = ctx.snappy_uncompress(_dev(s, off)).cpu().numpy()
+        assert got.tobytes() == x.tobytes(), off

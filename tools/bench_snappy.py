@@ -34,16 +34,22 @@ def main():
     ap.add_argument("--mib", type=int, default=64)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--cpu-mib", type=int, default=8)
+    ap.add_argument("--only", default=None, help="comma-separated payload names")
+    ap.add_argument("--no-cpu", action="store_true")
     a = ap.parse_args()
     from parameter_server_amd import filter as F
     ctx = F.Context(0)
     ref = None
     try:
+        if a.no_cpu:
+            raise ImportError
         import oracle
         ref = oracle.Snappy118()  # the library the reference links, where the image has it
     except Exception:
         pass
     for name, x in payloads(a.mib).items():
+        if a.only and name not in a.only.split(","):
+            continue
         nbytes = x.numel()
         s = ctx.snappy_compress(x)  # warm
         back = ctx.snappy_uncompress(s)

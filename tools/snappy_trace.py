@@ -32,7 +32,7 @@ def build():
     print(os.path.join(VAR, "libpsf.so"))
 
 
-def run(mib, kind):
+def run(mib, kind, dfrag=False):
     os.environ["PSF_LIBRARY_VARIANT"] = os.path.join(VAR, "libpsf.so")
     sys.path.insert(0, ROOT)
     import numpy as np
@@ -57,6 +57,23 @@ def run(mib, kind):
     L = lib()
     L.psf_debug_snappy_trace.argtypes = [C.c_void_p, C.c_size_t]
     assert L.psf_debug_snappy_trace(buf.ctypes.data, buf.nbytes) == 0
+    if dfrag:
+        s = ctx.snappy_compress(x)
+        for _ in range(2):
+            ctx.snappy_uncompress(s)
+        torch.cuda.synchronize()
+        L.psf_debug_dfrag_trace.argtypes = [C.c_void_p, C.c_size_t]
+        db = np.zeros(nfrag * 4, np.uint64)
+        assert L.psf_debug_dfrag_trace(db.ctypes.data, db.nbytes) == 0
+        d = db.reshape(nfrag, 4).astype(np.int64)
+        t0 = d[:, 0].min()
+        work = np.nonzero(d[:, 1] >= t0)[0]
+        dur = (d[:, 2] - d[:, 0]) * 10.0 / 1000
+        print(json.dumps({"dfrag_span_us": round(float((d[:, 2].max() - t0) * 10 / 1000), 1),
+                          "working": int(work.size), "first_working": int(work.min()) if work.size else None,
+                          "slowest": [(int(i), round(float(dur[i]), 1)) for i in np.argsort(-dur)[:5]],
+                          "start_spread_us": round(float((np.sort(d[:, 0])[-1] - t0) * 10 / 1000), 1)}))
+        return
     t = buf.reshape(nfrag, 6).astype(np.int64)
     t0 = t[:, 0].min()
     ns = lambda a: a * 10.0  # noqa: E731  (100 MHz clock)
@@ -83,8 +100,9 @@ if __name__ == "__main__":
     ap.add_argument("--run", action="store_true")
     ap.add_argument("--mib", type=int, default=128)
     ap.add_argument("--kind", default="codes")
+    ap.add_argument("--dfrag", action="store_true", help="per-fragment times of the decoder's K4")
     a = ap.parse_args()
     if a.build:
         build()
     if a.run:
-        run(a.mib, a.kind)
+        run(a.mib, a.kind, a.dfrag)
