@@ -101,6 +101,10 @@ class CompressingFilter : public Filter {
   using Filter::Filter;
   void encode(Message* msg) override;
   void decode(Message* msg) override;
+  // the arrays of several messages on one context in batched launch chains
+  // (same result as encode / decode on each message in turn)
+  static void encode_messages(Context* ctx, const std::vector<Message*>& msgs);
+  static void decode_messages(Context* ctx, const std::vector<Message*>& msgs);
 };
 
 // NOISE, add_noise.h:9-41

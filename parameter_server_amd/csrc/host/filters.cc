@@ -395,34 +395,42 @@ void FixingFloatFilter::decode_messages(Context* ctx, std::vector<FfMessage>& ms
 }
 
 // --------------------------------------------------------- COMPRESSING ----
-void CompressingFilter::encode(Message* msg) {  // compressing.h:8-19
-  FilterConfig* conf = find(FilterConfig::COMPRESSING, msg);
-  if (!conf) return;
-  conf->uncompressed_size.clear();
-  SnappyBatch batch(*ctx_);
-  if (msg->has_key()) {
-    conf->uncompressed_size.push_back(msg->key.bytes);
-    batch.compress(msg->key, &msg->key);
-  }
-  for (auto& v : msg->value) {
-    conf->uncompressed_size.push_back(v.bytes);
-    batch.compress(v, &v);
+void CompressingFilter::encode(Message* msg) { encode_messages(ctx_, {msg}); }
+
+void CompressingFilter::decode(Message* msg) { decode_messages(ctx_, {msg}); }
+
+void CompressingFilter::encode_messages(Context* ctx, const std::vector<Message*>& msgs) {  // compressing.h:8-19
+  SnappyBatch batch(*ctx);
+  for (Message* msg : msgs) {
+    FilterConfig* conf = find(FilterConfig::COMPRESSING, msg);
+    if (!conf) continue;
+    conf->uncompressed_size.clear();
+    if (msg->has_key()) {
+      conf->uncompressed_size.push_back(msg->key.bytes);
+      batch.compress(msg->key, &msg->key);
+    }
+    for (auto& v : msg->value) {
+      conf->uncompressed_size.push_back(v.bytes);
+      batch.compress(v, &v);
+    }
   }
   batch.flush();
 }
 
-void CompressingFilter::decode(Message* msg) {  // compressing.h:20-37
-  FilterConfig* conf = find(FilterConfig::COMPRESSING, msg);
-  if (!conf) return;
-  const int has_key = msg->has_key() ? 1 : 0;
-  if (conf->uncompressed_size.size() != msg->value.size() + has_key)
-    throw CheckError(kErrCheck, "CHECK_EQ(conf->uncompressed_size_size(), msg->value.size() + has_key)");
-  // the recorded sizes size the launches (the device checks them against each
-  // stream's header; snappy_host.cc)
-  SnappyBatch batch(*ctx_);
-  size_t k = 0;
-  if (has_key) batch.uncompress(msg->key, &msg->key, &conf->uncompressed_size[k++]);
-  for (auto& v : msg->value) batch.uncompress(v, &v, &conf->uncompressed_size[k++]);
+void CompressingFilter::decode_messages(Context* ctx, const std::vector<Message*>& msgs) {  // compressing.h:20-37
+  SnappyBatch batch(*ctx);
+  for (Message* msg : msgs) {
+    FilterConfig* conf = find(FilterConfig::COMPRESSING, msg);
+    if (!conf) continue;
+    const int has_key = msg->has_key() ? 1 : 0;
+    if (conf->uncompressed_size.size() != msg->value.size() + has_key)
+      throw CheckError(kErrCheck, "CHECK_EQ(conf->uncompressed_size_size(), msg->value.size() + has_key)");
+    // the recorded sizes size the launches (the device checks them against
+    // each stream's header; snappy_host.cc)
+    size_t k = 0;
+    if (has_key) batch.uncompress(msg->key, &msg->key, &conf->uncompressed_size[k++]);
+    for (auto& v : msg->value) batch.uncompress(v, &v, &conf->uncompressed_size[k++]);
+  }
   batch.flush();
 }
 
@@ -575,6 +583,7 @@ void encode_batch(RemoteNode* const* nodes, Message* const* msgs, int n) {
         only_ff = false;
     if (!only_ff) finish_kc();
     std::map<Context*, std::vector<FfMessage>> ff;
+    std::map<Context*, std::vector<Message*>> cz;
     std::vector<int> kc, kc_sig;
     for (int i = 0; i < n; ++i) {
       if (pos >= msgs[i]->task.filter.size()) continue;
@@ -585,10 +594,13 @@ void encode_batch(RemoteNode* const* nodes, Message* const* msgs, int n) {
       } else if (conf.type == FilterConfig::KEY_CACHING) {
         kc.push_back(i);
         if (KeyCachingFilter::needs_signature(msgs[i], true)) kc_sig.push_back(i);
+      } else if (conf.type == FilterConfig::COMPRESSING) {
+        cz[nodes[i]->ctx()].push_back(msgs[i]);
       } else {
         f->encode(msgs[i]);
       }
     }
+    for (auto& kv : cz) CompressingFilter::encode_messages(kv.first, kv.second);
     if (!kc.empty()) {  // signatures launched now, the caches after the next position's launches
       pend.pos = pos;
       pend.kc = std::move(kc);
@@ -606,6 +618,7 @@ void decode_batch(RemoteNode* const* nodes, Message* const* msgs, int n) {
   for (int i = 0; i < n; ++i) maxlen = std::max(maxlen, msgs[i]->task.filter.size());
   for (size_t r = 0; r < maxlen; ++r) {  // r-th filter from the end of every chain
     std::map<Context*, std::vector<FfMessage>> ff;
+    std::map<Context*, std::vector<Message*>> cz;
     std::vector<int> kc, kc_sig;
     for (int i = 0; i < n; ++i) {
       const size_t len = msgs[i]->task.filter.size();
@@ -617,10 +630,13 @@ void decode_batch(RemoteNode* const* nodes, Message* const* msgs, int n) {
       } else if (conf.type == FilterConfig::KEY_CACHING) {
         kc.push_back(i);
         if (KeyCachingFilter::needs_signature(msgs[i], false)) kc_sig.push_back(i);
+      } else if (conf.type == FilterConfig::COMPRESSING) {
+        cz[nodes[i]->ctx()].push_back(msgs[i]);
       } else {
         f->decode(msgs[i]);
       }
     }
+    for (auto& kv : cz) CompressingFilter::decode_messages(kv.first, kv.second);
     if (!kc.empty()) {
       SigBatch sb;
       launch_signatures(nodes, msgs, kc_sig, false, &sb);

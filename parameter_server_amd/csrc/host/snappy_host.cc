@@ -44,15 +44,12 @@ void SnappyBatch::compress(const Buffer& src, Buffer* dst) {
   if (src.bytes > 0xffffffffull) throw CheckError(kErrArg, "snappy: input longer than 4 GiB");
   if (jobs_.size() == (size_t)Context::kSyncSlots) flush();
   Job j;
+  j.compress = true;
   j.in = c_.to_device(src);
   j.dst = dst;
   j.out = c_.alloc(snappy_max_compressed(src.bytes));
-  Buffer scratch = c_.alloc(snappy_compress_scratch(src.bytes));
   j.slot = (int)jobs_.size();
   j.ticket = c_.next_ticket();
-  int st = snappy_compress_launch(j.in.ptr, j.in.bytes, j.out.ptr, scratch.ptr, c_.stream(), c_.prof(),
-                                  c_.pub_dev(j.slot), j.ticket);
-  if (st != kOk) throw CheckError(st, "snappy compress launch failed");
   jobs_.push_back(std::move(j));
 }
 
@@ -62,15 +59,12 @@ static uint32_t varint_len(uint64_t v) {
   return n;
 }
 
-void SnappyBatch::launch_uncompress(Job& j, const Buffer& src, uint32_t hdr, uint64_t dsize) {
+void SnappyBatch::prepare_uncompress(Job& j, const Buffer& src, uint32_t hdr, uint64_t dsize) {
   j.in = c_.to_device(src);
   j.out = dsize ? c_.alloc(dsize) : Buffer{};
   j.out.bytes = dsize;
-  Buffer scratch = c_.alloc(snappy_uncompress_scratch(src.bytes, dsize));
+  j.hdr = hdr;
   j.ticket = c_.next_ticket();
-  int st = snappy_uncompress_launch(j.in.ptr, j.in.bytes, hdr, dsize, j.out.ptr, scratch.ptr, c_.stream(),
-                                    c_.prof(), c_.pub_dev(j.slot), j.ticket);
-  if (st != kOk) throw CheckError(st, "snappy uncompress launch failed");
 }
 
 void SnappyBatch::uncompress(const Buffer& src, Buffer* dst, const uint64_t* size_hint) {
@@ -95,11 +89,45 @@ void SnappyBatch::uncompress(const Buffer& src, Buffer* dst, const uint64_t* siz
   j.slot = (int)jobs_.size();
   j.hinted = hinted;
   if (hinted) j.src = src;
-  launch_uncompress(j, src, hdr, dsize);
+  prepare_uncompress(j, src, hdr, dsize);
   jobs_.push_back(std::move(j));
 }
 
+// every pending stream in as few launch chains as possible: compress and
+// uncompress jobs each in groups of up to kSnappyBatchMax
+void SnappyBatch::launch(size_t b, size_t e) {
+  for (int pass = 0; pass < 2; ++pass) {
+    const bool comp = pass == 0;
+    std::vector<SnappyCJob> cj;
+    std::vector<SnappyDJob> dj;
+    auto go = [&] {
+      int st = kOk;
+      if (comp && !cj.empty()) {
+        Buffer scratch = c_.alloc(snappy_compress_batch_scratch(cj.data(), (int)cj.size()));
+        st = snappy_compress_batch_launch(cj.data(), (int)cj.size(), scratch.ptr, c_.stream(), c_.prof(),
+                                          c_.pub_dev(0));
+        cj.clear();
+      } else if (!comp && !dj.empty()) {
+        Buffer scratch = c_.alloc(snappy_uncompress_batch_scratch(dj.data(), (int)dj.size()));
+        st = snappy_uncompress_batch_launch(dj.data(), (int)dj.size(), scratch.ptr, c_.stream(), c_.prof(),
+                                            c_.pub_dev(0));
+        dj.clear();
+      }
+      if (st != kOk) throw CheckError(st, comp ? "snappy compress launch failed" : "snappy uncompress launch failed");
+    };
+    for (size_t i = b; i < e; ++i) {
+      Job& j = jobs_[i];
+      if (j.compress != comp) continue;
+      if (comp) cj.push_back(SnappyCJob{j.in.ptr, j.in.bytes, j.out.ptr, j.slot, j.ticket});
+      else dj.push_back(SnappyDJob{j.in.ptr, j.in.bytes, j.hdr, j.out.bytes, j.out.ptr, j.slot, j.ticket});
+      if (cj.size() == (size_t)kSnappyBatchMax || dj.size() == (size_t)kSnappyBatchMax) go();
+    }
+    go();
+  }
+}
+
 void SnappyBatch::flush() {
+  launch(0, jobs_.size());
   int bad = kOk;
   for (auto& j : jobs_) {
     c_.wait_ticket(j.slot, j.ticket);
@@ -112,7 +140,11 @@ void SnappyBatch::flush() {
         bad = kErrCheck;
         continue;
       }
-      launch_uncompress(j, j.src, hdr, dsize);
+      prepare_uncompress(j, j.src, hdr, dsize);
+      const SnappyDJob d{j.in.ptr, j.in.bytes, j.hdr, j.out.bytes, j.out.ptr, 0, j.ticket};
+      Buffer scratch = c_.alloc(snappy_uncompress_batch_scratch(&d, 1));
+      const int st = snappy_uncompress_batch_launch(&d, 1, scratch.ptr, c_.stream(), c_.prof(), c_.pub_dev(j.slot));
+      if (st != kOk) throw CheckError(st, "snappy uncompress launch failed");
       c_.wait_ticket(j.slot, j.ticket);
     }
     const Slot& h = *c_.pub_host(j.slot);

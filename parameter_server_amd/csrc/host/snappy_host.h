@@ -1,6 +1,6 @@
-// COMPRESSING buffers: compress / uncompress several arrays of a message with
-// one wait at the end (each kernel chain publishes its stream length / verdict
-// to its own host-mapped slot).
+// COMPRESSING buffers: compress / uncompress the arrays of one message or of
+// a batch of messages in batched launch chains with one wait at the end (each
+// stream publishes its length / verdict to its own host-mapped slot).
 #pragma once
 #include <vector>
 
@@ -22,20 +22,24 @@ class SnappyBatch {
   // header to the host, the device checks the header against it, and a
   // mismatch is redone from the header at flush()
   void uncompress(const Buffer& src, Buffer* dst, const uint64_t* size_hint = nullptr);
+  // one launch chain per kSnappyBatchMax streams of a kind, then one wait
   void flush();
 
  private:
   struct Job {
+    bool compress = false;
     Buffer in, out;
     Buffer* dst = nullptr;
     Buffer src;      // uncompress with a size hint: redone from the header on mismatch
     bool hinted = false;
+    uint32_t hdr = 0;
     int slot = 0;
     uint32_t ticket = 0;
   };
   Context& c_;
   std::vector<Job> jobs_;
-  void launch_uncompress(Job& j, const Buffer& src, uint32_t hdr, uint64_t dsize);
+  void prepare_uncompress(Job& j, const Buffer& src, uint32_t hdr, uint64_t dsize);
+  void launch(size_t b, size_t e);
 };
 
 }  // namespace psf

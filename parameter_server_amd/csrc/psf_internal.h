@@ -174,6 +174,31 @@ size_t snappy_uncompress_scratch(size_t c, size_t dsize);
 int snappy_uncompress_launch(const void* in, size_t c, uint32_t hdr, size_t dsize, void* out,
                              void* scratch, hipStream_t st, Profiler* prof, PubSlot* pub,
                              uint32_t ticket);
+// Up to kSnappyBatchMax streams in one launch chain (the COMPRESSING arrays of
+// a batch of messages); stream i publishes to pub_base[slot_i] with ticket_i.
+constexpr int kSnappyBatchMax = 32;
+struct SnappyCJob {
+  const void* in;
+  size_t n;
+  void* out;  // snappy_max_compressed(n) bytes
+  int slot;
+  uint32_t ticket;
+};
+size_t snappy_compress_batch_scratch(const SnappyCJob* jobs, int njobs);
+int snappy_compress_batch_launch(const SnappyCJob* jobs, int njobs, void* scratch, hipStream_t st,
+                                 Profiler* prof, PubSlot* pub_base);
+struct SnappyDJob {
+  const void* in;
+  size_t c;
+  uint32_t hdr;
+  size_t dsize;
+  void* out;
+  int slot;
+  uint32_t ticket;
+};
+size_t snappy_uncompress_batch_scratch(const SnappyDJob* jobs, int njobs);
+int snappy_uncompress_batch_launch(const SnappyDJob* jobs, int njobs, void* scratch, hipStream_t st,
+                                   Profiler* prof, PubSlot* pub_base);
 
 // spill.hip: gather `n` copies (sorted by chunk0) into one send buffer; copy i
 // moves len bytes from src to dst + dst_off and owns chunks

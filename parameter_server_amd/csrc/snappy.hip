@@ -304,12 +304,31 @@ __device__ __forceinline__ void prefetch_frag(const uint8_t* __restrict__ in, si
 // workgroup that is parsing it, or will parse it after a round whose
 // look-back concerns fragments below m -- all published -- so every look-back
 // ends.
-__global__ __launch_bounds__(kCThreads) void snappy_compress_frags(const uint8_t* __restrict__ in, size_t n,
-                                                                   uint8_t* __restrict__ scratch,
-                                                                   uint8_t* __restrict__ dst, uint32_t hdr,
+// Several streams compress in one launch (the COMPRESSING arrays of a batch of
+// messages): fragments are numbered across the streams, the tickets hand them
+// out in that order, and a stream's first fragment publishes its inclusive
+// prefix at once, which ends every look-back inside the stream.
+struct CJob {
+  const uint8_t* in;
+  uint8_t* dst;
+  uint64_t n;
+  uint32_t frag0, nfrag, hdr, slot, ticket, pad;
+};
+struct SnappyCJobs {
+  CJob j[kSnappyBatchMax];
+  PubSlot* pub;
+  uint32_t njobs, nfrag;
+};
+__device__ __forceinline__ const CJob& cjob_of(const SnappyCJobs& J, uint32_t g) {
+  uint32_t i = 0;
+  while (i + 1 < J.njobs && g >= J.j[i + 1].frag0) ++i;
+  return J.j[i];
+}
+__device__ __forceinline__ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+__global__ __launch_bounds__(kCThreads) void snappy_compress_frags(const SnappyCJobs J, uint8_t* __restrict__ scratch,
                                                                    uint64_t* __restrict__ state,
-                                                                   uint32_t* __restrict__ ctr, uint32_t nfrag,
-                                                                   PubSlot* pub, uint32_t ticket) {
+                                                                   uint32_t* __restrict__ ctr) {
   __shared__ CompressLds L;
   __shared__ uint32_t s_t0, s_t1, s_op, s_next, s_tn;
   const uint32_t tid = threadIdx.x;
@@ -321,23 +340,29 @@ __global__ __launch_bounds__(kCThreads) void snappy_compress_frags(const uint8_t
   for (uint32_t i = tid; i < (uint32_t)kSkipN; i += kCThreads) L.skip[i] = kSkip.v[i];
   for (uint32_t i = tid; i < kMinSlots; i += kCThreads) L.minlane[i] = 0xffffffffu;  // each parse step cleans up after itself
   __syncthreads();
+  const uint32_t nfrag = J.nfrag;
   uint32_t f = s_t0, fn = s_t1;
   if (f >= nfrag) return;
-  const bool al = (reinterpret_cast<uintptr_t>(in) & 15) == 0;
   const uint32_t st = tid - (kCThreads - kStageT);  // staging lane (waves 4-7)
   FragRegs pre = {};
-  if (al && wave >= 4) prefetch_frag(in, n, f, pre, st);
+  if (wave >= 4) {
+    const CJob& c = cjob_of(J, f);
+    if (aligned16(c.in)) prefetch_frag(c.in, c.n, f - c.frag0, pre, st);
+  }
   uint8_t* srcb = reinterpret_cast<uint8_t*>(L.src);
   uint32_t fp = kNoFrag, fp_op = 0, fp_next = 0;  // the fragment parsed in the round before
   for (;;) {
     // ---- stage f in LDS, clear its hash table
-    uint32_t len = 0, shift = 0;
+    uint32_t len = 0, shift = 0, f_local = 0, f_hdr = 0;
     if (f < nfrag) {
       PSF_TRACE(f, 0);
-      const size_t start = (size_t)f * kFrag;
-      len = (uint32_t)min((size_t)kFrag, n - start);
-      const uint8_t* g = in + start;
-      if (al) {
+      const CJob& c = cjob_of(J, f);
+      f_local = f - c.frag0;
+      f_hdr = c.hdr;
+      const size_t start = (size_t)f_local * kFrag;
+      len = (uint32_t)min((size_t)kFrag, c.n - start);
+      const uint8_t* g = c.in + start;
+      if (aligned16(c.in)) {
         const uint32_t nv = len >> 4;
         if (wave >= 4) {
           uint4* s4 = reinterpret_cast<uint4*>(L.src);
@@ -477,8 +502,8 @@ __global__ __launch_bounds__(kCThreads) void snappy_compress_frags(const uint8_t
           flen += 1 + m + 1 + (m < 60 ? 0 : ((31 - __builtin_clz(m)) >> 3) + 1);
         }
         if (lane == 0) {
-          if (f == 0)
-            __hip_atomic_store(&state[0], (2ull << 62) | (hdr + flen), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (f_local == 0)  // a stream's first fragment: its inclusive prefix at once
+            __hip_atomic_store(&state[f], (2ull << 62) | (f_hdr + flen), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           else
             atomicAdd(&state[f], (1ull << 62) | flen);
           s_op = op;
@@ -491,8 +516,10 @@ __global__ __launch_bounds__(kCThreads) void snappy_compress_frags(const uint8_t
       // ---- look back for fp's offset, then copy fp into place
       if (fp < nfrag) {
         const uint32_t pt = tid - 64;
-        const size_t pstart = (size_t)fp * kFrag;
-        const uint32_t plen = (uint32_t)min((size_t)kFrag, n - pstart);
+        const CJob& cp = cjob_of(J, fp);
+        const uint32_t lp = fp - cp.frag0;
+        const size_t pstart = (size_t)lp * kFrag;
+        const uint32_t plen = (uint32_t)min((size_t)kFrag, cp.n - pstart);
         uint32_t flen = fp_op;
         if (fp_next < plen) {
           const uint32_t m = plen - fp_next - 1;
@@ -501,8 +528,8 @@ __global__ __launch_bounds__(kCThreads) void snappy_compress_frags(const uint8_t
         // each of the three waves walks back on its own, 64 predecessors per
         // step: the nearest inclusive prefix ends the walk, the lengths in
         // front of it are summed across the wave
-        uint64_t excl = hdr;
-        if (fp > 0) {
+        uint64_t excl = cp.hdr;
+        if (lp > 0) {  // (the stream's first fragment is inclusive: the walk ends there at the latest)
           uint64_t sum = 0;
           int64_t base = (int64_t)fp - 1;  // lane l reads fragment base - l
           for (;;) {
@@ -526,27 +553,30 @@ __global__ __launch_bounds__(kCThreads) void snappy_compress_frags(const uint8_t
           excl = sum;
         }
         if (pt == 0) {
-          if (fp > 0)
+          if (lp > 0)
             __hip_atomic_store(&state[fp], (2ull << 62) | (excl + flen), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (fp + 1 == nfrag && pub) {
+          if (lp + 1 == cp.nfrag && J.pub) {
+            PubSlot* pub = J.pub + cp.slot;
             pub->size = excl + flen;
             pub->status = kOk;
-            publish_ticket(pub, ticket);
+            publish_ticket(pub, cp.ticket);
           }
         }
         PSF_TRACE_T(fp, 2, 64);
-        if (fp == 0 && pt < hdr) dst[pt] = (uint8_t)(((uint32_t)n >> (7 * pt)) | (pt + 1 < hdr ? 128u : 0u));
-        uint8_t* d = dst + excl;
+        if (lp == 0 && pt < cp.hdr)
+          cp.dst[pt] = (uint8_t)(((uint32_t)cp.n >> (7 * pt)) | (pt + 1 < cp.hdr ? 128u : 0u));
+        uint8_t* d = cp.dst + excl;
         if (fp_op) place_copy(d, scratch + (size_t)fp * kSnappyFragOut, fp_op, pt, lane);
         if (fp_next < plen) {
           d += fp_op;
           d += literal_tag(d, plen - fp_next, pt);
-          place_copy(d, in + pstart + fp_next, plen - fp_next, pt, lane);
+          place_copy(d, cp.in + pstart + fp_next, plen - fp_next, pt, lane);
         }
         PSF_TRACE_T(fp, 3, 64);
       }
-    } else if (al && fn < nfrag) {
-      prefetch_frag(in, n, fn, pre, st);  // the registers were staged: the next fragment goes out now
+    } else if (fn < nfrag) {  // the registers were staged: the next fragment goes out now
+      const CJob& c = cjob_of(J, fn);
+      if (aligned16(c.in)) prefetch_frag(c.in, c.n, fn - c.frag0, pre, st);
     }
     __syncthreads();
     // fragments move down the pipeline
@@ -567,6 +597,7 @@ constexpr uint32_t kInWin = 8192;  // staged compressed bytes in the fragment de
 constexpr uint64_t kNone = ~0ull;
 constexpr uint32_t kFlagInvalid = 1, kFlagSerial = 2, kFlagScan = 4, kFlagHeader = 8;
 constexpr uint64_t kFullLit = 65536 + 3;  // a 64 KiB fragment stored as one literal (tag 0xF4 + 2 length bytes)
+constexpr uint32_t kStarts = 64;          // K1 parses from each of the first 64 offsets of a window
 constexpr uint32_t kLitBudget = 512;      // K0's single steps before it hands the stream to K1/K2
 
 struct Tag {
@@ -729,11 +760,62 @@ __device__ __forceinline__ void copy_g2g(uint8_t* __restrict__ d, const uint8_t*
 // last workgroup goes on to do reads nothing the others wrote in this launch
 // (an agent-scope fence on MI355X writes back the XCD's whole L2, which
 // every workgroup of a streaming kernel would pay for).
-__device__ __forceinline__ bool last_block(uint32_t* ctr, uint32_t* s_last) {
+__device__ __forceinline__ bool last_block(uint32_t* ctr, uint32_t total, uint32_t* s_last) {
   __syncthreads();
-  if (threadIdx.x == 0) *s_last = atomicAdd(ctr, 1u) == gridDim.x - 1;
+  if (threadIdx.x == 0) *s_last = atomicAdd(ctr, 1u) == total - 1;
   __syncthreads();
   return *s_last;
+}
+
+// Several streams decode in one launch chain (the COMPRESSING arrays of a
+// batch of messages): every kernel's grid is the union of the streams' output
+// fragments (or windows, or streams), and a workgroup first finds its stream
+// in the job table, which rides in the kernel arguments.
+struct DJob {
+  const uint8_t* in;
+  uint8_t* out;
+  uint8_t* scratch;  // this stream's index arrays
+  uint64_t C, dsize;
+  uint32_t hdr, nfo, nwin;
+  uint32_t fo0, win0;  // first output fragment / window of this stream in the grids
+  uint32_t slot, ticket;
+};
+struct SnappyDJobs {
+  DJob j[kSnappyBatchMax];
+  uint32_t* ctrl;  // 8 words per stream: flags[0..3] (verdict, indexed, decoded by K-spec), counters[4..7]
+  PubSlot* pub;
+  uint32_t njobs, nfo1, nwin;  // streams; output fragments (at least one per stream); windows
+};
+struct DScr {
+  uint32_t *flags, *ctr;
+  uint64_t *wexit, *wtotal, *wentry, *woff, *fragpos, *specpos, *specend;
+  uint32_t *bitmap, *cum;
+};
+__device__ __forceinline__ DScr dscr(const SnappyDJobs& J, const DJob& D, uint32_t i) {
+  DScr S;
+  S.flags = J.ctrl + 8 * i;
+  S.ctr = S.flags + 4;
+  S.wexit = reinterpret_cast<uint64_t*>(D.scratch);
+  S.wtotal = S.wexit + (size_t)(D.nwin + 1) * kStarts;
+  S.wentry = S.wtotal + (size_t)(D.nwin + 1) * kStarts;
+  S.woff = S.wentry + (D.nwin + 1);
+  S.fragpos = S.woff + (D.nwin + 1);
+  S.specpos = S.fragpos + (D.nfo + 1);
+  S.specend = S.specpos + (D.nfo + 1);
+  S.bitmap = reinterpret_cast<uint32_t*>(S.specend + (D.nfo + 1));
+  S.cum = S.bitmap + (size_t)(D.nwin + 1) * (kWin / 32);
+  return S;
+}
+// the stream of output fragment b / window b of the union grids
+__device__ __forceinline__ uint32_t djob_frag(const SnappyDJobs& J, uint32_t b) {
+  uint32_t i = 0;
+  while (i + 1 < J.njobs && b >= J.j[i + 1].fo0) ++i;
+  return i;
+}
+__device__ __forceinline__ uint32_t djob_win(const SnappyDJobs& J, uint32_t b) {
+  uint32_t i = 0;
+  while (i + 1 < J.njobs && b >= J.j[i + 1].win0) ++i;
+  return i;
 }
 
 // K0: link the chain directly when the stream is mostly 64 KiB fragments
@@ -848,29 +930,89 @@ __device__ void dlit_body(const uint8_t* __restrict__ in, uint64_t C, uint32_t h
   }
 }
 
+constexpr uint32_t kFewTags = 8;  // fragments of at most this many tags are decoded without LDS
+
+struct FewLds {
+  uint32_t n, o[kFewTags], len[kFewTags], off[kFewTags];
+  uint64_t src[kFewTags], next;
+};
+
+// Output fragment d[0, end) from the tags at p, when they are at most
+// kFewTags, end exactly at the fragment's end and copy only from inside it
+// (stored data with a match or two): one lane walks the tags (checking each as
+// RawUncompress would), all 256 lanes copy the literals global to global, then
+// the copies run in order.  Returns the position after the fragment's last
+// tag, or kNone (nothing written) when the fragment is not of that kind.
+// Called by the whole workgroup.
+__device__ uint64_t decode_few(const uint8_t* __restrict__ in, uint64_t C, uint64_t p, uint32_t end,
+                               uint8_t* __restrict__ d, uint32_t tid, FewLds& F) {
+  if (tid == 0) {
+    uint32_t o = 0, n = 0;
+    bool good = p < C;
+    while (good && o < end && n < kFewTags) {
+      const Tag t = decode_tag(tag_bytes(in, C, p), p);
+      if (t.lit ? t.next > C : (t.off == 0 || t.off > o)) good = false;
+      F.o[n] = o;
+      F.len[n] = (uint32_t)t.len;
+      F.off[n] = t.off;
+      F.src[n] = t.lit ? p + t.hl : kNone;
+      o += (uint32_t)min(t.len, (uint64_t)kFrag + 1);
+      p = t.next;
+      ++n;
+    }
+    F.n = good && o == end ? n : 0;
+    F.next = p;
+  }
+  __syncthreads();
+  const uint32_t nt = F.n;
+  if (nt == 0) return kNone;
+  for (uint32_t i = 0; i < nt; ++i)
+    if (F.src[i] != kNone) copy_g2g(d + F.o[i], in + F.src[i], F.len[i], tid);
+  __syncthreads();
+  for (uint32_t i = 0; i < nt; ++i) {
+    if (F.src[i] != kNone) continue;
+    const uint32_t o = F.o[i], L = F.len[i], off = F.off[i];
+    for (uint32_t j = tid; j < L; j += 256) d[o + j] = d[o - off + (off >= L ? j : j % off)];
+    __syncthreads();
+  }
+  return F.next;
+}
+
 // K-spec: every output fragment k is first taken to be stored as one literal
 // at hdr + k * (65536 + 3) -- what a 1.1.8 encoder writes for a stream of
 // incompressible fragments (FIXING_FLOAT codes).  A workgroup checks its
 // fragment's tag there and, if it is the literal that fills the fragment,
-// copies it at once.  If every fragment checks out and the last literal ends
-// the stream, the stream is exactly that chain (fragment 0's tag follows the
-// header, and each checked literal ends where the next is checked): decoded
-// and valid, as the last workgroup to finish records.  One more workgroup
+// copies it at once; a fragment found a few bytes off that place (after one
+// with a match) is copied from there, and the first fragment with a few tags
+// is decoded where assumed.  If every fragment was placed and each ends where
+// the next begins (the first after the header, the last at the end of the
+// stream), the stream is exactly that chain: decoded and valid, as the last
+// workgroup to finish records.  One more workgroup
 // runs K0 alongside (its verdict and index agree with that on such a stream);
 // otherwise the kernels after this one redo every fragment whose true
 // position differs from the one assumed here (specpos).
-__global__ __launch_bounds__(256) void snappy_dspec(const uint8_t* __restrict__ in, uint64_t C, uint32_t hdr,
-                                                    uint64_t dsize, uint32_t nfo, uint32_t nwin,
-                                                    uint64_t* __restrict__ wentry, uint64_t* __restrict__ woff,
-                                                    uint64_t* __restrict__ fragpos, uint64_t* __restrict__ specpos,
-                                                    uint32_t* __restrict__ flags, uint32_t* __restrict__ ctr,
-                                                    uint8_t* __restrict__ out, PubSlot* pub, uint32_t ticket) {
+__global__ __launch_bounds__(256) void snappy_dspec(const SnappyDJobs J) {
   __shared__ uint32_t s_last, s_checked;
-  const uint32_t tid = threadIdx.x, k = blockIdx.x, nspec = gridDim.x - 1;
-  if (k == nspec) {  // the extra workgroup links the stream meanwhile (K0), needed or not
-    if (tid < 64) dlit_body(in, C, hdr, dsize, nwin, wentry, woff, fragpos, flags, tid);
+  const uint32_t tid = threadIdx.x;
+  if (blockIdx.x >= J.nfo1) {  // one more workgroup per stream links it meanwhile (K0), needed or not
+    const uint32_t i = blockIdx.x - J.nfo1;
+    const DJob& D = J.j[i];
+    const DScr S = dscr(J, D, i);
+    if (tid < 64) dlit_body(D.in, D.C, D.hdr, D.dsize, D.nwin, S.wentry, S.woff, S.fragpos, S.flags, tid);
     return;
   }
+  const uint32_t ji = djob_frag(J, blockIdx.x);
+  const DJob& D = J.j[ji];
+  const DScr S = dscr(J, D, ji);
+  const uint8_t* __restrict__ in = D.in;
+  uint8_t* __restrict__ out = D.out;
+  const uint64_t C = D.C, dsize = D.dsize;
+  const uint32_t hdr = D.hdr, nfo = D.nfo, ticket = D.ticket;
+  uint64_t* __restrict__ specpos = S.specpos;
+  uint32_t* __restrict__ flags = S.flags;
+  uint32_t* __restrict__ ctr = S.ctr;
+  PubSlot* pub = J.pub ? J.pub + D.slot : nullptr;
+  const uint32_t k = blockIdx.x - D.fo0, nspec = nfo ? nfo : 1;
   const uint64_t o0 = (uint64_t)k * kFrag;
   const uint32_t end = (uint32_t)min((uint64_t)kFrag, dsize - o0);  // 0 only for an empty output
   const uint64_t p = hdr + (uint64_t)k * kFullLit;
@@ -902,19 +1044,55 @@ __global__ __launch_bounds__(256) void snappy_dspec(const uint8_t* __restrict__ 
     __syncthreads();
     if (s_best != 0xffffffffu) at = p + (int32_t)(s_best & 511) - 128;
   }
-  if (at != kNone) copy_g2g(out + o0, in + at + hl, end, tid);
-  if (tid == 0) specpos[k] = at;
-  // one counter for both: workgroups done (high word) and fragments checked
+  uint64_t e = kNone;  // where this fragment's tags end
+  if (at != kNone) {
+    copy_g2g(out + o0, in + at + hl, end, tid);
+    e = at + hl + end;
+  } else if (end && (k > 0 || header_matches(in, C, hdr, dsize))) {
+    // not stored: a fragment with a few tags, right after stored ones that
+    // all sit where assumed (the first such fragment of the stream), is
+    // decoded here too
+    __shared__ FewLds F;
+    e = decode_few(in, C, p, end, out + o0, tid, F);
+    if (e != kNone) at = p;
+  } else if (ok) {
+    e = C;  // the empty output: the header is the stream
+  }
+  // device-scope stores: the last workgroup reads them from another XCD
+  if (tid == 0) {
+    __hip_atomic_store(&specpos[k], at, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&S.specend[k], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // one counter for both: workgroups done (high word) and fragments placed
+  const bool placed = e != kNone;
   __syncthreads();
   if (tid == 0) {
     const unsigned long long old =
-        atomicAdd(reinterpret_cast<unsigned long long*>(ctr), (1ull << 32) | (ok ? 1ull : 0ull));
+        atomicAdd(reinterpret_cast<unsigned long long*>(ctr), (1ull << 32) | (placed ? 1ull : 0ull));
     s_last = (uint32_t)(old >> 32) == nspec - 1;
-    s_checked = (uint32_t)old + (ok ? 1u : 0u);
+    s_checked = (uint32_t)old + (placed ? 1u : 0u);
   }
   __syncthreads();
   if (!s_last) return;
-  if (s_checked == nspec) {
+  // every fragment placed somewhere: the stream is that chain if each one
+  // ends where the next begins, the first begins after the header and the
+  // last ends the stream
+  __shared__ uint32_t s_chain;
+  if (tid == 0) s_chain = s_checked == nspec ? 1u : 0u;
+  __syncthreads();
+  if (s_chain) {
+    for (uint32_t i = tid; i < nspec; i += 256) {
+      const uint64_t pos = __hip_atomic_load(&specpos[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t prev = i ? __hip_atomic_load(&S.specend[i - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                              : (uint64_t)hdr;
+      bool good = pos == prev;
+      if (i + 1 == nspec)
+        good = good && __hip_atomic_load(&S.specend[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == C;
+      if (!good) s_chain = 0;  // any lane may clear it
+    }
+  }
+  __syncthreads();
+  if (s_chain) {
     if (tid == 0) {
       flags[0] = 0;
       flags[1] = 1;
@@ -928,8 +1106,6 @@ __global__ __launch_bounds__(256) void snappy_dspec(const uint8_t* __restrict__ 
   }
 }
 
-
-constexpr uint32_t kStarts = 64;  // K1 parses from each of the first 64 offsets of a window
 
 // K2: link the windows along the true chain (one lane).  Every step costs
 // one memory latency: windows are entered in increasing order, so the
@@ -1000,14 +1176,21 @@ __device__ void dlink_body(const uint8_t* __restrict__ in, uint64_t C, uint32_t 
 // K1: speculative parse of each window from each of its first 64 byte offsets
 // (lane l from offset l).  A window's true entry is one of them unless a literal
 // carried the chain further in; for those K2 walks until it meets lane 0's chain.
-__global__ __launch_bounds__(64) void snappy_dscan(const uint8_t* __restrict__ in, uint64_t C, uint32_t hdr,
-                                                   uint32_t* __restrict__ bitmap, uint32_t* __restrict__ cum,
-                                                   uint64_t* __restrict__ wexit, uint64_t* __restrict__ wtotal,
-                                                   const uint32_t* __restrict__ flags) {
+__global__ __launch_bounds__(64) void snappy_dscan(const SnappyDJobs J) {
   __shared__ uint32_t b32[(kWin + 32) / 4];
   __shared__ uint32_t bm[kWin / 32];
-  if (!(*flags & kFlagScan)) return;  // K0 linked the stream already
-  const uint32_t lane = threadIdx.x, w = blockIdx.x;
+  const uint32_t ji = djob_win(J, blockIdx.x);
+  const DJob& D = J.j[ji];
+  const DScr S = dscr(J, D, ji);
+  if (!(*S.flags & kFlagScan)) return;  // K0 linked the stream already
+  const uint8_t* __restrict__ in = D.in;
+  const uint64_t C = D.C;
+  const uint32_t hdr = D.hdr;
+  uint32_t* __restrict__ bitmap = S.bitmap;
+  uint32_t* __restrict__ cum = S.cum;
+  uint64_t* __restrict__ wexit = S.wexit;
+  uint64_t* __restrict__ wtotal = S.wtotal;
+  const uint32_t lane = threadIdx.x, w = blockIdx.x - D.win0;
   const uint64_t base = hdr + (uint64_t)w * kWin;
   const uint32_t wl = (uint32_t)min((uint64_t)kWin, C - base);
   const uint32_t s = stage(b32, in, C, base, wl + 16, lane);
@@ -1035,25 +1218,29 @@ __global__ __launch_bounds__(64) void snappy_dscan(const uint8_t* __restrict__ i
 }
 
 // K2 as its own launch: it reads what every K1 workgroup wrote
-__global__ __launch_bounds__(64) void snappy_dlink(const uint8_t* __restrict__ in, uint64_t C, uint32_t hdr,
-                                                   uint64_t dsize, const uint32_t* __restrict__ bitmap,
-                                                   const uint32_t* __restrict__ cum,
-                                                   const uint64_t* __restrict__ wexit,
-                                                   const uint64_t* __restrict__ wtotal, uint32_t nwin,
-                                                   uint64_t* __restrict__ wentry, uint64_t* __restrict__ woff,
-                                                   uint32_t* __restrict__ flags) {
-  if (!(*flags & kFlagScan)) return;  // K0 linked the stream already
-  dlink_body(in, C, hdr, dsize, bitmap, cum, wexit, wtotal, nwin, wentry, woff, flags);
+__global__ __launch_bounds__(64) void snappy_dlink(const SnappyDJobs J) {
+  const uint32_t ji = blockIdx.x;  // one workgroup per stream
+  const DJob& D = J.j[ji];
+  const DScr S = dscr(J, D, ji);
+  if (!(*S.flags & kFlagScan)) return;  // K0 linked the stream already
+  dlink_body(D.in, D.C, D.hdr, D.dsize, S.bitmap, S.cum, S.wexit, S.wtotal, D.nwin, S.wentry, S.woff, S.flags);
 }
 
 // K3: validate copies and index the tag that starts each output fragment
-__global__ __launch_bounds__(64) void snappy_dindex(const uint8_t* __restrict__ in, uint64_t C, uint32_t hdr,
-                                                    const uint64_t* __restrict__ wentry,
-                                                    const uint64_t* __restrict__ woff,
-                                                    uint64_t* __restrict__ fragpos, uint32_t* __restrict__ flags) {
+__global__ __launch_bounds__(64) void snappy_dindex(const SnappyDJobs J) {
   __shared__ uint32_t b32[(kWin + 32) / 4];
-  const uint32_t lane = threadIdx.x, w = blockIdx.x;
-  if (flags[1]) return;  // K0 indexed a stream of whole-fragment literals
+  const uint32_t ji = djob_win(J, blockIdx.x);
+  const DJob& D = J.j[ji];
+  const DScr S = dscr(J, D, ji);
+  uint32_t* __restrict__ flags = S.flags;
+  if (flags[1]) return;  // K0 walked and indexed the whole stream
+  const uint8_t* __restrict__ in = D.in;
+  const uint64_t C = D.C;
+  const uint32_t hdr = D.hdr;
+  const uint64_t* __restrict__ wentry = S.wentry;
+  const uint64_t* __restrict__ woff = S.woff;
+  uint64_t* __restrict__ fragpos = S.fragpos;
+  const uint32_t lane = threadIdx.x, w = blockIdx.x - D.win0;
   const uint64_t e = wentry[w];
   if (e == kNone || (*flags & kFlagInvalid)) return;
   const uint64_t base = hdr + (uint64_t)w * kWin;
@@ -1149,26 +1336,31 @@ __device__ void dfinish_body(const uint8_t* __restrict__ in, uint64_t C, uint32_
   }
 }
 
-constexpr uint32_t kFewTags = 8;  // K4 decodes a fragment of at most this many tags without LDS
-
 // K4: one workgroup per 64 KiB output fragment whose true position differs
 // from the one K-spec assumed.  A fragment stored as one literal is copied by
 // all 256 lanes; any other is decoded by wave 0 in LDS (tags and short
 // literals read from a staged window of the compressed bytes) and written
 // out by all.  The last workgroup to finish gives the verdict (K5).
-__global__ __launch_bounds__(256) void snappy_dfrag(const uint8_t* __restrict__ in, uint64_t C, uint32_t hdr,
-                                                    uint64_t dsize, const uint64_t* __restrict__ fragpos,
-                                                    const uint64_t* __restrict__ specpos,
-                                                    const uint32_t* __restrict__ flags, uint32_t* __restrict__ ctr,
-                                                    uint8_t* __restrict__ out, PubSlot* pub, uint32_t ticket) {
+__global__ __launch_bounds__(256) void snappy_dfrag(const SnappyDJobs J) {
   __shared__ uint32_t ob32[kFrag / 4];
   __shared__ uint32_t ib32[(kInWin + 32) / 4];
-  __shared__ uint32_t s_last, s_n, s_o[kFewTags], s_len[kFewTags], s_off[kFewTags];
-  __shared__ uint64_t s_src[kFewTags];
+  __shared__ uint32_t s_last;
+  __shared__ FewLds F;
+  const uint32_t ji = djob_frag(J, blockIdx.x);
+  const DJob& D = J.j[ji];
+  const DScr S = dscr(J, D, ji);
+  const uint32_t* __restrict__ flags = S.flags;
   if (flags[2]) return;  // K-spec decoded the whole stream and gave the verdict
+  const uint8_t* __restrict__ in = D.in;
+  uint8_t* __restrict__ out = D.out;
+  const uint64_t C = D.C, dsize = D.dsize;
+  const uint32_t hdr = D.hdr, ticket = D.ticket;
+  const uint64_t* __restrict__ fragpos = S.fragpos;
+  const uint64_t* __restrict__ specpos = S.specpos;
+  PubSlot* pub = J.pub ? J.pub + D.slot : nullptr;
   const uint32_t f = flags[0];
   uint8_t* ob = reinterpret_cast<uint8_t*>(ob32);
-  const uint32_t tid = threadIdx.x, k = blockIdx.x;
+  const uint32_t tid = threadIdx.x, k = blockIdx.x - D.fo0;
   const uint64_t o0 = (uint64_t)k * kFrag;
   const uint32_t end = (uint32_t)min((uint64_t)kFrag, dsize - o0);
   PSF_DTRACE(k, 0);
@@ -1176,37 +1368,8 @@ __global__ __launch_bounds__(256) void snappy_dfrag(const uint8_t* __restrict__ 
   if (f == 0 && end && p0 != specpos[k]) {
     PSF_DTRACE(k, 1);
     const Tag t0 = decode_tag(tag_bytes(in, C, p0), p0);
-    // a fragment of a few tags (stored data with a match or two): its tags
-    // walked by one lane, literals copied global to global by all, then the
-    // copies in order
-    if (tid == 0) {
-      uint64_t p = p0;
-      uint32_t o = 0, n = 0;
-      while (o < end && n < kFewTags) {
-        const Tag t = decode_tag(tag_bytes(in, C, p), p);
-        s_o[n] = o;
-        s_len[n] = (uint32_t)t.len;
-        s_off[n] = t.off;
-        s_src[n] = t.lit ? p + t.hl : kNone;
-        o += (uint32_t)t.len;
-        p = t.next;
-        ++n;
-      }
-      s_n = o >= end ? n : kFewTags + 1;
-    }
-    __syncthreads();
-    const uint32_t nt = s_n;
-    if (nt <= kFewTags) {
-      uint8_t* d = out + o0;
-      for (uint32_t i = 0; i < nt; ++i)
-        if (s_src[i] != kNone) copy_g2g(d + s_o[i], in + s_src[i], s_len[i], tid);
-      __syncthreads();
-      for (uint32_t i = 0; i < nt; ++i) {
-        if (s_src[i] != kNone) continue;
-        const uint32_t o = s_o[i], L = s_len[i], off = s_off[i];
-        for (uint32_t j = tid; j < L; j += 256) d[o + j] = d[o - off + (off >= L ? j : j % off)];
-        __syncthreads();
-      }
+    if (decode_few(in, C, p0, end, out + o0, tid, F) != kNone) {
+      // (a fragment of a few tags: done)
     } else if (t0.lit && t0.len == end) {
       copy_g2g(out + o0, in + p0 + t0.hl, end, tid);
     } else {
@@ -1257,87 +1420,137 @@ __global__ __launch_bounds__(256) void snappy_dfrag(const uint8_t* __restrict__ 
     }
   }
   PSF_DTRACE(k, 2);
-  if (last_block(ctr, &s_last) && tid == 0) dfinish_body(in, C, hdr, dsize, f, out, pub, ticket);
+  if (last_block(S.ctr + 2, D.nfo ? D.nfo : 1, &s_last) && tid == 0) dfinish_body(in, C, hdr, dsize, f, out, pub, ticket);
 }
 
 }  // namespace
 
 size_t snappy_max_compressed(size_t n) { return 32 + n + n / 6; }
 
-size_t snappy_compress_scratch(size_t n) {
-  const size_t nfrag = (n + kFrag - 1) / kFrag;
+size_t snappy_compress_batch_scratch(const SnappyCJob* jobs, int njobs) {
+  size_t nfrag = 0;
+  for (int i = 0; i < njobs; ++i) nfrag += (jobs[i].n + kFrag - 1) / kFrag;
   return nfrag * kSnappyFragOut + (nfrag + 1) * 8 + 64;
 }
 
-int snappy_compress_launch(const void* in, size_t n, void* out, void* scratch, hipStream_t st, Profiler* prof,
-                           PubSlot* pub, uint32_t ticket) {
-  if (n == 0 || n > 0xffffffffull) return kErrArg;
-  const uint32_t nfrag = (uint32_t)((n + kFrag - 1) / kFrag);
+size_t snappy_compress_scratch(size_t n) {
+  const SnappyCJob j{nullptr, n, nullptr, 0, 0};
+  return snappy_compress_batch_scratch(&j, 1);
+}
+
+int snappy_compress_batch_launch(const SnappyCJob* jobs, int njobs, void* scratch, hipStream_t st, Profiler* prof,
+                                 PubSlot* pub_base) {
+  if (njobs <= 0 || njobs > kSnappyBatchMax) return kErrArg;
+  SnappyCJobs K{};
+  K.pub = pub_base;
+  K.njobs = (uint32_t)njobs;
+  double bytes = 0;
+  for (int i = 0; i < njobs; ++i) {
+    const SnappyCJob& q = jobs[i];
+    if (q.n == 0 || q.n > 0xffffffffull) return kErrArg;
+    CJob& c = K.j[i];
+    c.in = static_cast<const uint8_t*>(q.in);
+    c.dst = static_cast<uint8_t*>(q.out);
+    c.n = q.n;
+    c.frag0 = K.nfrag;
+    c.nfrag = (uint32_t)((q.n + kFrag - 1) / kFrag);
+    c.hdr = 1;
+    for (uint64_t v = q.n; v >= 128; v >>= 7) ++c.hdr;
+    c.slot = (uint32_t)q.slot;
+    c.ticket = q.ticket;
+    K.nfrag += c.nfrag;
+    bytes += (double)q.n;
+  }
   uint8_t* s = static_cast<uint8_t*>(scratch);
   // look-back state (one word per fragment) and the fragment ticket counter,
   // zeroed before the launch
-  uint64_t* state = reinterpret_cast<uint64_t*>(s + (size_t)nfrag * kSnappyFragOut);
-  uint32_t* ctr = reinterpret_cast<uint32_t*>(state + nfrag);
-  hipError_t e = hipMemsetAsync(state, 0, (size_t)nfrag * 8 + 8, st);
-  if (e != hipSuccess) return kErrHip;
-  uint32_t hdr = 1;
-  for (uint64_t v = n; v >= 128; v >>= 7) ++hdr;
+  uint64_t* state = reinterpret_cast<uint64_t*>(s + (size_t)K.nfrag * kSnappyFragOut);
+  uint32_t* ctr = reinterpret_cast<uint32_t*>(state + K.nfrag);
+  if (hipMemsetAsync(state, 0, (size_t)K.nfrag * 8 + 8, st) != hipSuccess) return kErrHip;
   // persistent workgroups, one per CU (the LDS footprint allows no more)
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return kErrHip;
-  const uint32_t grid = nfrag < (uint32_t)cus ? nfrag : (uint32_t)cus;
-  ProfScope ps(prof, kKSnappyCompress, st, (double)n);
-  hipLaunchKernelGGL(snappy_compress_frags, dim3(grid), dim3(kCThreads), 0, st, static_cast<const uint8_t*>(in), n, s,
-                     static_cast<uint8_t*>(out), hdr, state, ctr, nfrag, pub, ticket);
+  const uint32_t grid = K.nfrag < (uint32_t)cus ? K.nfrag : (uint32_t)cus;
+  ProfScope ps(prof, kKSnappyCompress, st, bytes);
+  hipLaunchKernelGGL(snappy_compress_frags, dim3(grid), dim3(kCThreads), 0, st, K, s, state, ctr);
   return launch_status();
 }
 
-size_t snappy_uncompress_scratch(size_t C, size_t dsize) {
+int snappy_compress_launch(const void* in, size_t n, void* out, void* scratch, hipStream_t st, Profiler* prof,
+                           PubSlot* pub, uint32_t ticket) {
+  const SnappyCJob j{in, n, out, 0, ticket};
+  return snappy_compress_batch_launch(&j, 1, scratch, st, prof, pub);
+}
+
+static size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
+
+// one stream's index arrays (DScr)
+static size_t djob_bytes(size_t C, size_t dsize) {
   const size_t nwin = (C + kWin - 1) / kWin + 1;
   const size_t nfo = (dsize + kFrag - 1) / kFrag + 1;
-  return nwin * (kWin / 8) + C * 4 + nwin * 8 * (2 * kStarts + 2) + 2 * nfo * 8 + 256;
+  return align256(nwin * (kWin / 8) + C * 4 + nwin * 8 * (2 * kStarts + 2) + 3 * nfo * 8 + 64);
 }
 
-// Five launches: K-spec (+ K0 in one more workgroup), K1, K2, K3, K4 (+ K5
-// in its last workgroup).  On a stream of stored fragments K-spec decodes
-// everything and the others return at once.
+size_t snappy_uncompress_batch_scratch(const SnappyDJob* jobs, int njobs) {
+  size_t b = align256((size_t)njobs * 32);
+  for (int i = 0; i < njobs; ++i) b += djob_bytes(jobs[i].c, jobs[i].dsize);
+  return b;
+}
+
+size_t snappy_uncompress_scratch(size_t C, size_t dsize) { return align256(32) + djob_bytes(C, dsize); }
+
+// Five launches for the whole batch: K-spec (+ K0 in one more workgroup per
+// stream), K1, K2, K3, K4 (+ K5 in each stream's last workgroup).  On streams
+// of stored fragments K-spec decodes everything and the others return at once.
+int snappy_uncompress_batch_launch(const SnappyDJob* jobs, int njobs, void* scratch, hipStream_t st,
+                                   Profiler* prof, PubSlot* pub_base) {
+  if (njobs <= 0 || njobs > kSnappyBatchMax) return kErrArg;
+  SnappyDJobs K{};
+  uint8_t* s = static_cast<uint8_t*>(scratch);
+  K.ctrl = reinterpret_cast<uint32_t*>(s);
+  K.pub = pub_base;
+  K.njobs = (uint32_t)njobs;
+  uint8_t* data = s + align256((size_t)njobs * 32);
+  double bytes = 0;
+  for (int i = 0; i < njobs; ++i) {
+    const SnappyDJob& q = jobs[i];
+    if (q.hdr == 0 || q.hdr > q.c || q.hdr > 5) return kErrArg;
+    DJob& D = K.j[i];
+    D.in = static_cast<const uint8_t*>(q.in);
+    D.out = static_cast<uint8_t*>(q.out);
+    D.scratch = data;
+    D.C = q.c;
+    D.dsize = q.dsize;
+    D.hdr = q.hdr;
+    D.nwin = (uint32_t)((q.c - q.hdr + kWin - 1) / kWin);
+    D.nfo = (uint32_t)((q.dsize + kFrag - 1) / kFrag);
+    D.fo0 = K.nfo1;
+    D.win0 = K.nwin;
+    D.slot = (uint32_t)q.slot;
+    D.ticket = q.ticket;
+    K.nfo1 += D.nfo ? D.nfo : 1;  // an empty output still takes one workgroup (header check, verdict)
+    K.nwin += D.nwin;
+    data += djob_bytes(q.c, q.dsize);
+    bytes += (double)q.c + (double)q.dsize;
+  }
+  if (hipMemsetAsync(K.ctrl, 0, (size_t)njobs * 32, st) != hipSuccess) return kErrHip;
+  ProfScope ps(prof, kKSnappyDecompress, st, bytes);
+  hipLaunchKernelGGL(snappy_dspec, dim3(K.nfo1 + K.njobs), dim3(256), 0, st, K);
+  if (K.nwin) {
+    hipLaunchKernelGGL(snappy_dscan, dim3(K.nwin), dim3(64), 0, st, K);
+    hipLaunchKernelGGL(snappy_dlink, dim3(K.njobs), dim3(64), 0, st, K);
+    hipLaunchKernelGGL(snappy_dindex, dim3(K.nwin), dim3(64), 0, st, K);
+  }
+  hipLaunchKernelGGL(snappy_dfrag, dim3(K.nfo1), dim3(256), 0, st, K);
+  return launch_status();
+}
+
 int snappy_uncompress_launch(const void* in, size_t C, uint32_t hdr, size_t dsize, void* out, void* scratch,
                              hipStream_t st, Profiler* prof, PubSlot* pub, uint32_t ticket) {
-  if (hdr == 0 || hdr > C || hdr > 5) return kErrArg;
-  const uint64_t body = C - hdr;
-  const uint32_t nwin = (uint32_t)((body + kWin - 1) / kWin);
-  const uint32_t nfo = (uint32_t)((dsize + kFrag - 1) / kFrag);
-  const uint32_t nfo1 = nfo ? nfo : 1;  // an empty output still takes one workgroup (header check, verdict)
-  uint8_t* s = static_cast<uint8_t*>(scratch);
-  uint32_t* flags = reinterpret_cast<uint32_t*>(s);  // [0] verdict, [1] indexed, [2] decoded by K-spec
-  uint32_t* ctr = flags + 4;  // last-workgroup counters: K-spec (64 bits: done | checked), K4
-  uint64_t* wexit = reinterpret_cast<uint64_t*>(s + 64);
-  uint64_t* wtotal = wexit + (size_t)(nwin + 1) * kStarts;
-  uint64_t* wentry = wtotal + (size_t)(nwin + 1) * kStarts;
-  uint64_t* woff = wentry + (nwin + 1);
-  uint64_t* fragpos = woff + (nwin + 1);
-  uint64_t* specpos = fragpos + (nfo + 1);
-  uint32_t* bitmap = reinterpret_cast<uint32_t*>(specpos + (nfo + 1));
-  uint32_t* cum = bitmap + (size_t)(nwin + 1) * (kWin / 32);
-  const uint8_t* src = static_cast<const uint8_t*>(in);
-  uint8_t* dst = static_cast<uint8_t*>(out);
-  if (hipMemsetAsync(s, 0, 32, st) != hipSuccess) return kErrHip;
-  ProfScope ps(prof, kKSnappyDecompress, st, (double)C + (double)dsize);
-  hipLaunchKernelGGL(snappy_dspec, dim3(nfo1 + 1), dim3(256), 0, st, src, (uint64_t)C, hdr, (uint64_t)dsize, nfo, nwin,
-                     wentry, woff, fragpos, specpos, flags, ctr, dst, pub, ticket);
-  if (nwin) {
-    hipLaunchKernelGGL(snappy_dscan, dim3(nwin), dim3(64), 0, st, src, (uint64_t)C, hdr, bitmap, cum, wexit,
-                       wtotal, flags);
-    hipLaunchKernelGGL(snappy_dlink, dim3(1), dim3(64), 0, st, src, (uint64_t)C, hdr, (uint64_t)dsize, bitmap, cum,
-                       wexit, wtotal, nwin, wentry, woff, flags);
-    hipLaunchKernelGGL(snappy_dindex, dim3(nwin), dim3(64), 0, st, src, (uint64_t)C, hdr, wentry, woff, fragpos,
-                       flags);
-  }
-  hipLaunchKernelGGL(snappy_dfrag, dim3(nfo1), dim3(256), 0, st, src, (uint64_t)C, hdr, (uint64_t)dsize, fragpos,
-                     specpos, flags, ctr + 2, dst, pub, ticket);
-  return launch_status();
+  const SnappyDJob j{in, C, hdr, dsize, out, 0, ticket};
+  return snappy_uncompress_batch_launch(&j, 1, scratch, st, prof, pub);
 }
 
 }  // namespace psf
