@@ -167,10 +167,11 @@ __device__ __forceinline__ uint4 shfl_down1(const uint4& v) {
                     __shfl_down(v.w, 1, 64));
 }
 
-constexpr int kPlaceU = 15;  // rows of 63 chunks per placing wave per round: 44 KiB per round (256 VGPRs)
+constexpr int kPlaceW = 7;   // placing waves (1-7)
+constexpr int kPlaceU = 10;  // rows of 63 chunks per placing wave per round: 69 KiB per round
 
-// dst[0, len) = s[0, len), any alignment of either, by the 192 lanes of waves
-// 1-3 (pt = 0..191).  A wave takes rows of 63 destination chunks (16 bytes
+// dst[0, len) = s[0, len), any alignment of either, by the 448 lanes of waves
+// 1-7 (pt = 0..447).  A wave takes rows of 63 destination chunks (16 bytes
 // each): lane l loads the aligned source block under chunk l of the row, and
 // a chunk's second block is the next lane's (lane 63 only loads).  Each round
 // issues all of its loads before its stores: a wave's memory counter retires
@@ -191,16 +192,16 @@ __device__ void place_copy(uint8_t* __restrict__ dst, const uint8_t* __restrict_
   const uint32_t lim = nc + (sh ? 1u : 0u);  // blocks that hold source bytes
   uint4* d16 = reinterpret_cast<uint4*>(dst + head);
   const uint32_t wv = pt >> 6;
-  for (uint32_t c0 = 0; c0 < nc; c0 += kPlaceU * 3 * 63) {
+  for (uint32_t c0 = 0; c0 < nc; c0 += kPlaceU * kPlaceW * 63) {
     uint4 lo[kPlaceU];
 #pragma unroll
     for (int u = 0; u < kPlaceU; ++u) {
-      const uint32_t c = c0 + (u * 3 + wv) * 63 + lane;
+      const uint32_t c = c0 + (u * kPlaceW + wv) * 63 + lane;
       lo[u] = c < lim ? s16[c] : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int u = 0; u < kPlaceU; ++u) {
-      const uint32_t c = c0 + (u * 3 + wv) * 63 + lane;
+      const uint32_t c = c0 + (u * kPlaceW + wv) * 63 + lane;
       const uint4 hi = shfl_down1(lo[u]);
       if (lane < 63 && c < nc) d16[c] = funnel16(lo[u], hi, sh);
     }
@@ -330,12 +331,14 @@ __global__ __launch_bounds__(kCThreads) void snappy_compress_frags(const SnappyC
                                                                    uint64_t* __restrict__ state,
                                                                    uint32_t* __restrict__ ctr) {
   __shared__ CompressLds L;
-  __shared__ uint32_t s_t0, s_t1, s_op, s_next, s_tn;
+  __shared__ uint32_t s_t0, s_t1, s_op, s_next, s_tn, s_round;
+  __shared__ uint64_t s_excl;
   const uint32_t tid = threadIdx.x;
   const uint32_t wave = tid >> 6, lane = tid & 63;
   if (tid == 0) {
     s_t0 = atomicAdd(ctr, 1u);
     s_t1 = atomicAdd(ctr, 1u);
+    s_round = 0;
   }
   for (uint32_t i = tid; i < (uint32_t)kSkipN; i += kCThreads) L.skip[i] = kSkip.v[i];
   for (uint32_t i = tid; i < kMinSlots; i += kCThreads) L.minlane[i] = 0xffffffffu;  // each parse step cleans up after itself
@@ -351,6 +354,7 @@ __global__ __launch_bounds__(kCThreads) void snappy_compress_frags(const SnappyC
   }
   uint8_t* srcb = reinterpret_cast<uint8_t*>(L.src);
   uint32_t fp = kNoFrag, fp_op = 0, fp_next = 0;  // the fragment parsed in the round before
+  uint32_t round = 1;  // the placing waves' handshake with wave 1
   for (;;) {
     // ---- stage f in LDS, clear its hash table
     uint32_t len = 0, shift = 0, f_local = 0, f_hdr = 0;
@@ -512,8 +516,12 @@ __global__ __launch_bounds__(kCThreads) void snappy_compress_frags(const SnappyC
         }
         PSF_TRACE(f, 1);
       }
-    } else if (wave < 4) {
-      // ---- look back for fp's offset, then copy fp into place
+    } else {
+      if (wave >= 4 && fn < nfrag) {  // the registers were staged: the next fragment goes out now
+        const CJob& c = cjob_of(J, fn);
+        if (aligned16(c.in)) prefetch_frag(c.in, c.n, fn - c.frag0, pre, st);
+      }
+      // ---- look back for fp's offset (wave 1), then copy fp into place (waves 1-7)
       if (fp < nfrag) {
         const uint32_t pt = tid - 64;
         const CJob& cp = cjob_of(J, fp);
@@ -525,11 +533,11 @@ __global__ __launch_bounds__(kCThreads) void snappy_compress_frags(const SnappyC
           const uint32_t m = plen - fp_next - 1;
           flen += 1 + m + 1 + (m < 60 ? 0 : ((31 - __builtin_clz(m)) >> 3) + 1);
         }
-        // each of the three waves walks back on its own, 64 predecessors per
-        // step: the nearest inclusive prefix ends the walk, the lengths in
-        // front of it are summed across the wave
+        // wave 1 walks back, 64 predecessors per step: the nearest inclusive
+        // prefix ends the walk, the lengths in front of it are summed across
+        // the wave; the other placing waves wait for its result in LDS
         uint64_t excl = cp.hdr;
-        if (lp > 0) {  // (the stream's first fragment is inclusive: the walk ends there at the latest)
+        if (wave == 1 && lp > 0) {  // (the stream's first fragment is inclusive: the walk ends there at the latest)
           uint64_t sum = 0;
           int64_t base = (int64_t)fp - 1;  // lane l reads fragment base - l
           for (;;) {
@@ -552,15 +560,23 @@ __global__ __launch_bounds__(kCThreads) void snappy_compress_frags(const SnappyC
           }
           excl = sum;
         }
-        if (pt == 0) {
-          if (lp > 0)
-            __hip_atomic_store(&state[fp], (2ull << 62) | (excl + flen), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (lp + 1 == cp.nfrag && J.pub) {
-            PubSlot* pub = J.pub + cp.slot;
-            pub->size = excl + flen;
-            pub->status = kOk;
-            publish_ticket(pub, cp.ticket);
+        if (wave == 1) {
+          if (lane == 0) {
+            s_excl = excl;
+            __hip_atomic_store(&s_round, round, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (lp > 0)
+              __hip_atomic_store(&state[fp], (2ull << 62) | (excl + flen), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (lp + 1 == cp.nfrag && J.pub) {
+              PubSlot* pub = J.pub + cp.slot;
+              pub->size = excl + flen;
+              pub->status = kOk;
+              publish_ticket(pub, cp.ticket);
+            }
           }
+        } else {
+          while (__hip_atomic_load(&s_round, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != round)
+            __builtin_amdgcn_s_sleep(1);
+          excl = s_excl;
         }
         PSF_TRACE_T(fp, 2, 64);
         if (lp == 0 && pt < cp.hdr)
@@ -574,11 +590,9 @@ __global__ __launch_bounds__(kCThreads) void snappy_compress_frags(const SnappyC
         }
         PSF_TRACE_T(fp, 3, 64);
       }
-    } else if (fn < nfrag) {  // the registers were staged: the next fragment goes out now
-      const CJob& c = cjob_of(J, fn);
-      if (aligned16(c.in)) prefetch_frag(c.in, c.n, fn - c.frag0, pre, st);
     }
     __syncthreads();
+    ++round;
     // fragments move down the pipeline
     const bool parsed = f < nfrag;
     fp = parsed ? f : kNoFrag;
