@@ -395,6 +395,8 @@ __global__ __launch_bounds__(kCThreads) void snappy_compress_frags(const SnappyC
       if (f < nfrag) {
         uint8_t* out = scratch + (size_t)f * kSnappyFragOut;
         uint32_t op = 0, next_emit = 0;
+        // the fragment after fn: the ticket is drawn now and lands during the parse
+        const uint32_t tn = lane == 0 ? atomicAdd(ctr, 1u) : 0u;
         if (len >= 15) {
           const uint32_t ip_limit = len - 15;
           uint32_t ip = 1;
@@ -512,7 +514,7 @@ __global__ __launch_bounds__(kCThreads) void snappy_compress_frags(const SnappyC
             atomicAdd(&state[f], (1ull << 62) | flen);
           s_op = op;
           s_next = next_emit;
-          s_tn = atomicAdd(ctr, 1u);  // the fragment after fn
+          s_tn = tn;
         }
         PSF_TRACE(f, 1);
       }
@@ -1190,10 +1192,7 @@ __device__ void dlink_body(const uint8_t* __restrict__ in, uint64_t C, uint32_t 
 // K1: speculative parse of each window from each of its first 64 byte offsets
 // (lane l from offset l).  A window's true entry is one of them unless a literal
 // carried the chain further in; for those K2 walks until it meets lane 0's chain.
-__global__ __launch_bounds__(64) void snappy_dscan(const SnappyDJobs J) {
-  __shared__ uint32_t b32[(kWin + 32) / 4];
-  __shared__ uint32_t bm[kWin / 32];
-  const uint32_t ji = djob_win(J, blockIdx.x);
+__device__ void dscan_body(const SnappyDJobs& J, uint32_t ji, uint32_t w, uint32_t* b32, uint32_t* bm) {
   const DJob& D = J.j[ji];
   const DScr S = dscr(J, D, ji);
   if (!(*S.flags & kFlagScan)) return;  // K0 linked the stream already
@@ -1204,7 +1203,7 @@ __global__ __launch_bounds__(64) void snappy_dscan(const SnappyDJobs J) {
   uint32_t* __restrict__ cum = S.cum;
   uint64_t* __restrict__ wexit = S.wexit;
   uint64_t* __restrict__ wtotal = S.wtotal;
-  const uint32_t lane = threadIdx.x, w = blockIdx.x - D.win0;
+  const uint32_t lane = threadIdx.x;
   const uint64_t base = hdr + (uint64_t)w * kWin;
   const uint32_t wl = (uint32_t)min((uint64_t)kWin, C - base);
   const uint32_t s = stage(b32, in, C, base, wl + 16, lane);
@@ -1231,19 +1230,9 @@ __global__ __launch_bounds__(64) void snappy_dscan(const SnappyDJobs J) {
   for (uint32_t i = lane; i < kWin / 32; i += 64) gb[i] = bm[i];
 }
 
-// K2 as its own launch: it reads what every K1 workgroup wrote
-__global__ __launch_bounds__(64) void snappy_dlink(const SnappyDJobs J) {
-  const uint32_t ji = blockIdx.x;  // one workgroup per stream
-  const DJob& D = J.j[ji];
-  const DScr S = dscr(J, D, ji);
-  if (!(*S.flags & kFlagScan)) return;  // K0 linked the stream already
-  dlink_body(D.in, D.C, D.hdr, D.dsize, S.bitmap, S.cum, S.wexit, S.wtotal, D.nwin, S.wentry, S.woff, S.flags);
-}
 
 // K3: validate copies and index the tag that starts each output fragment
-__global__ __launch_bounds__(64) void snappy_dindex(const SnappyDJobs J) {
-  __shared__ uint32_t b32[(kWin + 32) / 4];
-  const uint32_t ji = djob_win(J, blockIdx.x);
+__device__ void dindex_body(const SnappyDJobs& J, uint32_t ji, uint32_t w, uint32_t* b32) {
   const DJob& D = J.j[ji];
   const DScr S = dscr(J, D, ji);
   uint32_t* __restrict__ flags = S.flags;
@@ -1254,7 +1243,7 @@ __global__ __launch_bounds__(64) void snappy_dindex(const SnappyDJobs J) {
   const uint64_t* __restrict__ wentry = S.wentry;
   const uint64_t* __restrict__ woff = S.woff;
   uint64_t* __restrict__ fragpos = S.fragpos;
-  const uint32_t lane = threadIdx.x, w = blockIdx.x - D.win0;
+  const uint32_t lane = threadIdx.x;
   const uint64_t e = wentry[w];
   if (e == kNone || (*flags & kFlagInvalid)) return;
   const uint64_t base = hdr + (uint64_t)w * kWin;
@@ -1289,6 +1278,56 @@ __global__ __launch_bounds__(64) void snappy_dindex(const SnappyDJobs J) {
     p = t.next;
   }
   if (fl) atomicOr(flags, fl);
+}
+
+// Grid-wide barrier of a persistent launch (every workgroup resident): the
+// agent-scope fences write this XCD's L2 back and read the others' writes
+// (the scan path only, where K1's tables feed K2 and K2's entries feed K3).
+__device__ void grid_barrier(uint32_t* bar, uint32_t target) {
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    atomicAdd(bar, 1u);
+    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) __builtin_amdgcn_s_sleep(2);
+  }
+  __syncthreads();
+  __threadfence();
+}
+
+// K1 + K2 + K3 in one persistent launch: windows scanned (streams K0 handed
+// over), a grid barrier, each such stream linked by one workgroup, a grid
+// barrier, windows indexed (streams K0 did not walk to the end).  When no
+// stream of the batch needs them, every workgroup returns at once.
+__global__ __launch_bounds__(64) void snappy_dslow(const SnappyDJobs J) {
+  __shared__ uint32_t b32[(kWin + 32) / 4];
+  __shared__ uint32_t bm[kWin / 32];
+  bool scan = false, index = false;
+  for (uint32_t i = 0; i < J.njobs; ++i) {
+    const uint32_t f0 = J.ctrl[8 * i], f1 = J.ctrl[8 * i + 1];
+    scan = scan || (f0 & kFlagScan);
+    index = index || (!f1 && !(f0 & (kFlagInvalid | kFlagHeader)));
+  }
+  if (!scan && !index) return;
+  uint32_t* bar = J.ctrl + 8 * J.njobs;
+  if (scan) {
+    for (uint32_t w = blockIdx.x; w < J.nwin; w += gridDim.x) {
+      const uint32_t ji = djob_win(J, w);
+      dscan_body(J, ji, w - J.j[ji].win0, b32, bm);
+    }
+    grid_barrier(bar, gridDim.x);
+    for (uint32_t ji = blockIdx.x; ji < J.njobs; ji += gridDim.x) {
+      const DScr S = dscr(J, J.j[ji], ji);
+      if (*S.flags & kFlagScan) {
+        const DJob& D = J.j[ji];
+        dlink_body(D.in, D.C, D.hdr, D.dsize, S.bitmap, S.cum, S.wexit, S.wtotal, D.nwin, S.wentry, S.woff, S.flags);
+      }
+    }
+    grid_barrier(bar, 2 * gridDim.x);
+  }
+  for (uint32_t w = blockIdx.x; w < J.nwin; w += gridDim.x) {
+    const uint32_t ji = djob_win(J, w);
+    dindex_body(J, ji, w - J.j[ji].win0, b32);
+  }
 }
 
 // A literal too long for the staging window, read straight into the LDS
@@ -1508,25 +1547,26 @@ static size_t djob_bytes(size_t C, size_t dsize) {
 }
 
 size_t snappy_uncompress_batch_scratch(const SnappyDJob* jobs, int njobs) {
-  size_t b = align256((size_t)njobs * 32);
+  size_t b = align256((size_t)njobs * 32 + 4);
   for (int i = 0; i < njobs; ++i) b += djob_bytes(jobs[i].c, jobs[i].dsize);
   return b;
 }
 
-size_t snappy_uncompress_scratch(size_t C, size_t dsize) { return align256(32) + djob_bytes(C, dsize); }
+size_t snappy_uncompress_scratch(size_t C, size_t dsize) { return align256(32 + 4) + djob_bytes(C, dsize); }
 
-// Five launches for the whole batch: K-spec (+ K0 in one more workgroup per
-// stream), K1, K2, K3, K4 (+ K5 in each stream's last workgroup).  On streams
+// Three launches for the whole batch: K-spec (+ K0 in one more workgroup per
+// stream), K1-K3 (one persistent launch), K4 (+ K5 in each stream's last
+// workgroup).  On streams
 // of stored fragments K-spec decodes everything and the others return at once.
 int snappy_uncompress_batch_launch(const SnappyDJob* jobs, int njobs, void* scratch, hipStream_t st,
                                    Profiler* prof, PubSlot* pub_base) {
   if (njobs <= 0 || njobs > kSnappyBatchMax) return kErrArg;
   SnappyDJobs K{};
   uint8_t* s = static_cast<uint8_t*>(scratch);
-  K.ctrl = reinterpret_cast<uint32_t*>(s);
+  K.ctrl = reinterpret_cast<uint32_t*>(s);  // 8 words per stream, then the grid barrier counter
   K.pub = pub_base;
   K.njobs = (uint32_t)njobs;
-  uint8_t* data = s + align256((size_t)njobs * 32);
+  uint8_t* data = s + align256((size_t)njobs * 32 + 4);
   double bytes = 0;
   for (int i = 0; i < njobs; ++i) {
     const SnappyDJob& q = jobs[i];
@@ -1549,13 +1589,18 @@ int snappy_uncompress_batch_launch(const SnappyDJob* jobs, int njobs, void* scra
     data += djob_bytes(q.c, q.dsize);
     bytes += (double)q.c + (double)q.dsize;
   }
-  if (hipMemsetAsync(K.ctrl, 0, (size_t)njobs * 32, st) != hipSuccess) return kErrHip;
+  if (hipMemsetAsync(K.ctrl, 0, (size_t)njobs * 32 + 4, st) != hipSuccess) return kErrHip;
   ProfScope ps(prof, kKSnappyDecompress, st, bytes);
   hipLaunchKernelGGL(snappy_dspec, dim3(K.nfo1 + K.njobs), dim3(256), 0, st, K);
   if (K.nwin) {
-    hipLaunchKernelGGL(snappy_dscan, dim3(K.nwin), dim3(64), 0, st, K);
-    hipLaunchKernelGGL(snappy_dlink, dim3(K.njobs), dim3(64), 0, st, K);
-    hipLaunchKernelGGL(snappy_dindex, dim3(K.nwin), dim3(64), 0, st, K);
+    // every workgroup of the persistent launch resident at once: 8 per CU
+    // (18 KiB of LDS and one wave each: a CU's LDS holds 8)
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return kErrHip;
+    const uint32_t cap = (uint32_t)(8 * cus);
+    hipLaunchKernelGGL(snappy_dslow, dim3(K.nwin < cap ? K.nwin : cap), dim3(64), 0, st, K);
   }
   hipLaunchKernelGGL(snappy_dfrag, dim3(K.nfo1), dim3(256), 0, st, K);
   return launch_status();
