@@ -248,3 +248,22 @@ def test_decode_stored_stream_with_shifted_tail(ctx, port, where):
     for off in (0, 1, 3):
         got = ctx.snappy_uncompress(_dev(s, off)).cpu().numpy()
         assert got.tobytes() == x.tobytes(), off
+
+
+def test_compress_on_private_stream_is_complete_on_return(port):
+    """psf_snappy_compress is synchronous: on a context with its own stream,
+    the stream bytes are all in place when the call returns, so a reader on
+    another stream (here torch's default one, no sync) sees the whole of it."""
+    from parameter_server_amd import filter as F
+    side = torch.cuda.Stream()
+    ctx = F.Context(0, stream=side)
+    rng = np.random.default_rng(21)
+    x = rng.integers(0, 256, 48 << 20, dtype=np.uint8)
+    x[::7] = 3  # some matches in every fragment
+    with torch.cuda.stream(side):
+        xd = torch.from_numpy(x).to("cuda", non_blocking=False)
+    side.synchronize()
+    with torch.cuda.stream(side):
+        s = ctx.snappy_compress(xd)
+    got = s.to("cpu").numpy().tobytes()  # copied on the default stream
+    assert got == port.snappy_compress(x.tobytes())
