@@ -85,10 +85,7 @@ __global__ __launch_bounds__(kBlock) void crc32c_chunks(const uint8_t* __restric
     for (int w = 0; w < kBlock / 64; ++w) acc ^= wave_acc[w];
     if (gridDim.x == 1) {  // whole message in this workgroup: final value
       *out = acc;
-      if (pub) {
-        pub->crc = acc;
-        publish_ticket(pub, ticket);
-      }
+      if (pub) publish_crc(pub, acc, ticket);
     } else {
       atomicXor(out, acc);
     }
@@ -189,10 +186,7 @@ __global__ __launch_bounds__(kBlock) void crc32c_small(const uint8_t* __restrict
   const uint32_t acc = crc_small_block(d, n);
   if (threadIdx.x == 0) {
     *out = acc;
-    if (pub) {
-      pub->crc = acc;
-      publish_ticket(pub, ticket);
-    }
+    if (pub) publish_crc(pub, acc, ticket);
   }
 }
 
@@ -208,9 +202,7 @@ __global__ __launch_bounds__(kBlock) void crc32c_small_batch(CrcBatch B, PubSlot
   const uint32_t b = blockIdx.x;
   const uint32_t acc = crc_small_block(B.d[b], B.n[b]);
   if (threadIdx.x == 0) {
-    PubSlot* ps = pub + B.slot[b];
-    ps->crc = acc;
-    publish_ticket(ps, B.ticket[b]);
+    publish_crc(pub + B.slot[b], acc, B.ticket[b]);
   }
 }
 

@@ -131,6 +131,26 @@ void Context::wait_ticket(int i, uint32_t ticket) {
   }
 }
 
+uint32_t Context::wait_crc(int i, uint32_t ticket) {
+  if (device_ < 0) throw CheckError(kErrArg, "host-only context has no device workspace");
+  const Slot* s = h_slots_ + i;
+  for (uint64_t spin = 0;; ++spin) {
+    uint64_t w = __atomic_load_n(&s->crc_ticket, __ATOMIC_ACQUIRE);
+    if ((uint32_t)(w >> 32) == ticket) return (uint32_t)w;
+    if ((spin & 255) == 255) {
+      hipError_t q = hipStreamQuery(stream_);
+      if (q == hipSuccess) {  // stream drained: the publish must be visible now
+        w = __atomic_load_n(&s->crc_ticket, __ATOMIC_ACQUIRE);
+        if ((uint32_t)(w >> 32) == ticket) return (uint32_t)w;
+        throw CheckError(kErrHip, "kernel finished without publishing its CRC");
+      }
+      if (q != hipErrorNotReady)
+        throw CheckError(kErrHip, std::string("stream failed: ") + hipGetErrorString(q));
+      if (spin > (1u << 16)) sched_yield();
+    }
+  }
+}
+
 void Context::sync() {
   if (device_ >= 0) PSF_HIP_CHECK(hipStreamSynchronize(stream_));
 }

@@ -71,6 +71,8 @@ class Context {
   // Wait until slot i carries `ticket` (spins on host memory; falls back to
   // the stream state so a kernel that never publishes cannot hang the host).
   void wait_ticket(int i, uint32_t ticket);
+  // the same for a CRC published with its ticket in one word; returns the CRC
+  uint32_t wait_crc(int i, uint32_t ticket);
   void sync();
   // stage a host buffer into HBM (used at the host edge)
   Buffer to_device(const Buffer& b);

@@ -40,8 +40,7 @@ uint32_t KeyCachingFilter::signature(const Buffer& key) {
   int st = crc32c_launch(key.ptr, len, &ctx_->d_slots()[0].crc, ctx_->stream(), ctx_->prof(),
                          ctx_->pub_dev(0), ticket);
   if (st != kOk) throw CheckError(st, "crc32c launch failed");
-  ctx_->wait_ticket(0, ticket);
-  return ctx_->pub_host(0)->crc;
+  return ctx_->wait_crc(0, ticket);
 }
 
 void KeyCachingFilter::encode(Message* msg) {  // key_caching.h:9-34
@@ -501,8 +500,7 @@ struct SigBatch {
   std::vector<Chunk> chunks;
   void finish_chunk(const Chunk& c) {
     for (size_t q = 0; q < c.ks.size(); ++q) {
-      c.ctx->wait_ticket(c.slot0 + (int)q, c.tk[q]);
-      sigs[c.ks[q]] = c.ctx->pub_host(c.slot0 + (int)q)->crc;
+      sigs[c.ks[q]] = c.ctx->wait_crc(c.slot0 + (int)q, c.tk[q]);
     }
   }
   void finish() {

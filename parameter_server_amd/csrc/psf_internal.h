@@ -47,12 +47,20 @@ struct PubSlot {
   uint32_t crc;
   uint32_t ticket;
   uint32_t pad;
-  uint64_t size;  // COMPRESSING: stream / output length
+  uint64_t size;         // COMPRESSING: stream / output length
+  uint64_t crc_ticket;   // KEY_CACHING: ticket << 32 | crc, one store
 };
 
 __device__ __forceinline__ void publish_ticket(PubSlot* s, uint32_t ticket) {
   __threadfence_system();
   __hip_atomic_store(&s->ticket, ticket, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// a CRC and its ticket in one 8-byte system-scope store: nothing else needs
+// ordering before it, so no fence (a system-scope release writes the whole L2
+// back, which 64 signature workgroups would each pay for)
+__device__ __forceinline__ void publish_crc(PubSlot* s, uint32_t crc, uint32_t ticket) {
+  __hip_atomic_store(&s->crc_ticket, ((uint64_t)ticket << 32) | crc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Kernel launch profiler: HIP events recorded on the launch stream around
