@@ -372,6 +372,7 @@ def timed(run, steps, world, dist, ctx, prof_kernel=None, stride=1):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    ctx.host_waits(reset=True)
     t0 = time.perf_counter()
     run(steps)
     torch.cuda.synchronize()
@@ -457,8 +458,28 @@ def main():
     router = extra.get("router")
     if router is not None and router.exchange is not None:
         router.exchange.bytes_sent = 0
+    if router is not None:
+        router.host_stats(reset=True)
     elapsed, prof = timed(run, args.steps, world, dist, ctx, dom, stride)
+    waits = ctx.host_waits()
     spill = router.exchange.bytes_sent if router is not None and router.exchange is not None else 0
+    # host accounting of the timed steps (this rank): wall time, the part the
+    # host spent blocked on the device, the rest (host work), and the kernel
+    # time per step from the diagnostic pass
+    host = None
+    if diag:
+        blocked = sum(v[0] for v in waits.values())
+        kern_ms = sum(v[1] for v in diag.values()) / min(args.steps, 10)
+        host = {"wall_ms_per_step": round(elapsed / args.steps * 1e3, 4),
+                "blocked_ms_per_step": round(blocked / args.steps * 1e3, 4),
+                "active_ms_per_step": round((elapsed - blocked) / args.steps * 1e3, 4),
+                "kernel_ms_per_step": round(kern_ms, 4),
+                "waits": {k: {"ms_per_step": round(v[0] / args.steps * 1e3, 4), "per_step": v[1] / args.steps}
+                          for k, v in waits.items()}}
+        if router is not None:
+            rs = router.host_stats()
+            host["router_encode_ms_per_step"] = round(rs["encode_s"] / args.steps * 1e3, 4)
+            host["router_decode_ms_per_step"] = round(rs["decode_s"] / args.steps * 1e3, 4)
 
     def max_over_ranks(v):
         if world == 1:
@@ -550,6 +571,8 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
+        if host:
+            line["host"] = host
         if spill:
             line["config"]["spill_bytes_per_step_rank0"] = spill // max(args.steps, 1)
         if also:

@@ -392,6 +392,22 @@ int psf_router_result(psf_router* r, int i, int* server, psf_message** out);
 int psf_router_num_encoded(psf_router* r);
 int psf_router_encoded(psf_router* r, int i, int32_t* stream, int* server, psf_message** out);
 
+/* ---- host-side accounting ----------------------------------------------
+ * Host time blocked on the device, by cause: PSF_WAIT_SYNC stream
+ * synchronisations, PSF_WAIT_PUBLISH waits on side-info a kernel publishes
+ * (KEY_CACHING CRCs, FIXING_FLOAT ranges, snappy sizes), PSF_WAIT_SLICE waits
+ * on the slicing pass.  wait_ns and waits hold PSF_WAIT_NUM entries. */
+#define PSF_WAIT_SYNC 0
+#define PSF_WAIT_PUBLISH 1
+#define PSF_WAIT_SLICE 2
+#define PSF_WAIT_NUM 3
+int psf_context_host_stats(psf_context* ctx, int64_t* wait_ns, int64_t* waits);
+int psf_context_host_stats_reset(psf_context* ctx);
+/* router phase timers: out[0] steps (encodes), out[1] host ns inside encode,
+ * out[2] host ns inside the decodes (both include the waits above) */
+int psf_router_host_stats(psf_router* r, int64_t* out);
+int psf_router_host_stats_reset(psf_router* r);
+
 /* ---- launch profiler (HIP events on the launch stream) ----------------- */
 #define PSF_K_MINMAX 0
 #define PSF_K_ENCODE 1

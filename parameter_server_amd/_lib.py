@@ -131,6 +131,10 @@ SIGNATURES = {
     "psf_router_decode_local": ([vp], C.c_int),
     "psf_router_decode_received": ([vp, vp, C.POINTER(C.c_int64)], C.c_int),
     "psf_router_step": ([vp, C.POINTER(vp), C.c_int, C.c_int], C.c_int),
+    "psf_router_host_stats": ([vp, C.POINTER(C.c_int64)], C.c_int),
+    "psf_router_host_stats_reset": ([vp], C.c_int),
+    "psf_context_host_stats": ([vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64)], C.c_int),
+    "psf_context_host_stats_reset": ([vp], C.c_int),
     "psf_router_num_results": ([vp], C.c_int),
     "psf_router_result": ([vp, C.c_int, PI, C.POINTER(vp)], C.c_int),
     "psf_router_num_encoded": ([vp], C.c_int),

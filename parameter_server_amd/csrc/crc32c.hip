@@ -206,6 +206,61 @@ __global__ __launch_bounds__(kBlock) void crc32c_small_batch(CrcBatch B, PubSlot
   }
 }
 
+// SliceKOFVMessage's split positions (message.h:107-147) fused with the
+// KEY_CACHING signature of every slice (key_caching.h:18), for many messages
+// in one launch: workgroup (m, i) finds pos[i] and pos[i + 1] of message m
+// (two lanes, one binary search each over the sorted keys), then CRCs the
+// first min(2048, slice bytes) key bytes of slice i.  Inputs and results live
+// in host-mapped memory: the host reads them once the launch's event has
+// completed, with no copy and no stream synchronisation.
+template <typename K>
+__global__ __launch_bounds__(kBlock) void slice_sig_kernel(SliceSigParams P) {
+  __shared__ uint64_t s_pos[2];
+  const int ns = P.nslices, nb = ns + 1;
+  const int m = blockIdx.x / ns, i = blockIdx.x % ns;
+  const K* keys = reinterpret_cast<const K*>(P.desc[2 * m]);
+  if (threadIdx.x < 2) {
+    const size_t n = (size_t)P.desc[2 * m + 1];
+    const K v = (K)P.bounds[(size_t)m * nb + i + threadIdx.x];
+    size_t lo = 0, len = n;
+    while (len > 0) {  // first index with keys[idx] >= v
+      const size_t half = len >> 1;
+      if (keys[lo + half] < v) {
+        lo += half + 1;
+        len -= half + 1;
+      } else {
+        len = half;
+      }
+    }
+    s_pos[threadIdx.x] = lo;
+  }
+  __syncthreads();
+  const uint64_t lo = s_pos[0], hi = s_pos[1] > lo ? s_pos[1] : lo;
+  const uint64_t bytes = (hi - lo) * sizeof(K);
+  const uint32_t len = bytes < kCrcSingleBlock ? (uint32_t)bytes : (uint32_t)kCrcSingleBlock;
+  uint32_t crc = 0;
+  if (len) crc = crc_small_block(reinterpret_cast<const uint8_t*>(keys + lo), len);
+  if (threadIdx.x == 0) {
+    uint64_t* pos = P.pos + (size_t)m * nb;
+    if (i == 0) pos[0] = s_pos[0];
+    pos[i + 1] = s_pos[1];
+    P.sig[(size_t)m * ns + i] = crc;
+  }
+}
+
+int slice_sig_launch(const SliceSigParams& p, int key_bytes, hipStream_t st) {
+  if (p.nslices <= 0 || p.nmsg <= 0) return kOk;
+  const size_t grid = (size_t)p.nslices * (size_t)p.nmsg;
+  if (grid > 0x7fffffffu) return kErrArg;
+  if (key_bytes == 8)
+    hipLaunchKernelGGL(slice_sig_kernel<uint64_t>, dim3((unsigned)grid), dim3(kBlock), 0, st, p);
+  else if (key_bytes == 4)
+    hipLaunchKernelGGL(slice_sig_kernel<uint32_t>, dim3((unsigned)grid), dim3(kBlock), 0, st, p);
+  else
+    return kErrArg;
+  return launch_status();
+}
+
 int crc32c_batch_launch(const void* const* d, const uint32_t* n, const int* slot, const uint32_t* ticket,
                         int count, PubSlot* pub, hipStream_t st, Profiler* prof) {
   if (count <= 0) return kOk;

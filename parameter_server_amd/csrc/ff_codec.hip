@@ -28,6 +28,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string.h>
+
+#include <algorithm>
 #include <map>
 #include <mutex>
 #include <vector>
@@ -128,6 +131,15 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 template <typename V> struct Vec4;
 template <> struct Vec4<float> {
+  // a temporal load (the batched min/max pass: its encode re-reads the values)
+  __device__ static void load_keep(const float* p, float v[4]) {
+    f32x4 t = *reinterpret_cast<const f32x4*>(p);
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+  }
+  __device__ static void loadu_keep(const float* p, float v[4]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = p[j];
+  }
   __device__ static void load(const float* p, float v[4]) {
 #ifdef PSF_PLAIN_LOADS
     f32x4 t = *reinterpret_cast<const f32x4*>(p);
@@ -147,6 +159,8 @@ template <> struct Vec4<float> {
   }
 };
 template <> struct Vec4<double> {
+  __device__ static void load_keep(const double* p, double v[4]) { load(p, v); }
+  __device__ static void loadu_keep(const double* p, double v[4]) { loadu(p, v); }
   __device__ static void load(const double* p, double v[4]) {
     f64x2 a = __builtin_nontemporal_load(reinterpret_cast<const f64x2*>(p));
     f64x2 b = __builtin_nontemporal_load(reinterpret_cast<const f64x2*>(p) + 1);
@@ -162,6 +176,38 @@ template <> struct Vec4<double> {
     __builtin_nontemporal_store(b, reinterpret_cast<f64x2*>(p) + 1);
   }
 };
+
+// Full-tile loads of a value array that starts off a 16-byte boundary (a
+// slice of a value array, message.h:141-143, starts at any element).  f32: the
+// array begins r = 1..3 elements past the aligned address xa; lane l loads the
+// aligned block under its group and takes the rest of the group from lane
+// l+1's block (DPP wave_shl:1), the wave's last lane loading its second block
+// itself -- one 16-byte load per group instead of four 4-byte ones.  Every
+// block read holds at least one element of the array, so no read leaves the
+// array's pages.  f64 keeps the element loads.  All 64 lanes must be active.
+__device__ __forceinline__ float next_lane(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, false));
+}
+template <typename V> struct Shifted {
+  __device__ static void load(const V* x, const V*, int, size_t g, V v[4]) { Vec4<V>::loadu(x + 4 * g, v); }
+};
+#ifdef PSF_SHIFTED_LOADS
+template <> struct Shifted<float> {
+  __device__ static void load(const float*, const float* xa, int r, size_t g, float v[4]) {
+    const f32x4* a4 = reinterpret_cast<const f32x4*>(xa) + g;
+    const f32x4 a = __builtin_nontemporal_load(a4);
+#ifdef PSF_SHIFT_DPP
+    f32x4 b = {next_lane(a.x), next_lane(a.y), next_lane(a.z), next_lane(a.w)};
+    if ((threadIdx.x & 63) == 63) b = __builtin_nontemporal_load(a4 + 1);
+#else
+    const f32x4 b = __builtin_nontemporal_load(a4 + 1);
+#endif
+    if (r == 1) { v[0] = a.y; v[1] = a.z; v[2] = a.w; v[3] = b.x; }
+    else if (r == 2) { v[0] = a.z; v[1] = a.w; v[2] = b.x; v[3] = b.y; }
+    else { v[0] = a.w; v[1] = b.x; v[2] = b.y; v[3] = b.z; }
+  }
+};
+#endif
 
 // tiles [t0, t1) owned by this workgroup
 __device__ __forceinline__ void tile_range(size_t ntiles, size_t& t0, size_t& t1) {
@@ -786,7 +832,7 @@ __global__ __launch_bounds__(kBlock) void ff_decode(const uint8_t* __restrict__ 
 // ------------------------------------------------- batched (many arrays) ---
 // Many small messages (the async-SGD minibatches, the C4 slices) make the
 // per-array launches latency-bound.  The batched kernels take a table of up
-// to kBatchJobs arrays in their kernel arguments; a workgroup finds its array
+// to kFfBatchMax arrays in their kernel arguments; a workgroup finds its array
 // by its index in the batch grid and runs the same tile code as the
 // single-array kernels on its share of that array's tiles.  Aligned f32/f64
 // arrays with num_bytes 1..3 only (the launcher routes the rest to the
@@ -807,14 +853,19 @@ struct FfJob {
 };
 static_assert(sizeof(FfJob) == 48, "FfJob layout");
 constexpr uint16_t kNoLazy = 0xFFFFu;
-constexpr int kBatchJobs = kFfBatchMax;
-struct FfBatch {
+// Two table sizes: up to 64 arrays (4 KiB of kernel arguments, the C1-sized
+// batches whose launches are latency-bound) and up to kFfBatchMax = 512 (a
+// whole C4 step's slices in one launch per kernel; HIP on ROCm 7 takes
+// kernel arguments up to 32 KiB, tools/kernarg_probe.hip).
+constexpr int kBatchSmall = 64;
+template <int CAP>
+struct FfBatchT {
   // a job's workgroups are [first[i], first[i + 1]) (the last ends at the
   // grid); mm_first likewise for the min/max kernel, where a job without a
   // min/max pass has an empty range.  Unused entries ~0u.
-  uint32_t first[kBatchJobs];
-  uint32_t mm_first[kBatchJobs];
-  FfJob job[kBatchJobs];
+  uint32_t first[CAP];
+  uint32_t mm_first[CAP];
+  FfJob job[CAP];
   int njobs;
   uint32_t total;           // workgroups of the encode / decode grid
   uint32_t mm_total;        // workgroups of the min/max kernel (partials count)
@@ -827,23 +878,37 @@ struct FfBatch {
   uint32_t a_lane, c_lane;
   double ratio;
 };
-static_assert(sizeof(FfBatch) <= 4096, "FfBatch must fit the 4 KiB kernel-argument segment");
+static_assert(sizeof(FfBatchT<kBatchSmall>) <= 4096, "the small batch fits 4 KiB of kernel arguments");
+static_assert(sizeof(FfBatchT<kFfBatchMax>) <= 32000, "the large batch fits the kernel-argument segment");
 static_assert(kMinmaxGrid <= 0xFFFF, "FfJob::mm_nwg is 16 bits");
 
 
 // the job whose [first, first + count) workgroup range holds b: a fully
 // unrolled count over the contiguous first-workgroup table (wide scalar loads
-// issued together, no dependent loop)
-__device__ __forceinline__ int batch_job(const FfBatch& B, uint32_t b, bool mm) {
+// issued together, no dependent loop); the large table in two levels (every
+// 16th entry, then the 16 entries of that group)
+template <int CAP>
+__device__ __forceinline__ int batch_job(const FfBatchT<CAP>& B, uint32_t b, bool mm) {
   const uint32_t* f = mm ? B.mm_first : B.first;
-  int j = -1;
+  if (CAP <= kBatchSmall) {
+    int j = -1;
 #pragma unroll
-  for (int i = 0; i < kBatchJobs; ++i) j += f[i] <= b ? 1 : 0;
+    for (int i = 0; i < CAP; ++i) j += f[i] <= b ? 1 : 0;
+    return j;
+  }
+  int c = -1;
+#pragma unroll
+  for (int i = 0; i < CAP / 16; ++i) c += f[16 * i] <= b ? 1 : 0;
+  const uint32_t* g = f + 16 * c;
+  int j = 16 * c - 1;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) j += g[i] <= b ? 1 : 0;
   return j;
 }
 
 // workgroups of job j in the encode / decode grid
-__device__ __forceinline__ uint32_t batch_nwg(const FfBatch& B, int j) {
+template <int CAP>
+__device__ __forceinline__ uint32_t batch_nwg(const FfBatchT<CAP>& B, int j) {
   return (j + 1 < B.njobs ? B.first[j + 1] : B.total) - B.first[j];
 }
 
@@ -854,8 +919,8 @@ __device__ __forceinline__ void tile_range_of(size_t ntiles, uint32_t wg, uint32
   t1 = t0 + per < ntiles ? t0 + per : ntiles;
 }
 
-template <typename V>
-__global__ __launch_bounds__(kBlock) void ff_minmax_batch(FfBatch B) {
+template <typename V, int CAP>
+__global__ __launch_bounds__(kBlock) void ff_minmax_batch(FfBatchT<CAP> B) {
   typedef typename KeyOf<V>::K K;
   const int jb = batch_job(B, blockIdx.x, true);
   const FfJob& J = B.job[jb];
@@ -863,6 +928,8 @@ __global__ __launch_bounds__(kBlock) void ff_minmax_batch(FfBatch B) {
   const size_t n = J.n;
   const uint32_t wg = blockIdx.x - B.mm_first[jb];
   const bool al = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+  const int r = (int)((reinterpret_cast<uintptr_t>(x) & 15) / sizeof(V));
+  const V* xa = x - r;
   K lo = KeyOf<V>::kLoId, hi = KeyOf<V>::kHiId;
   const size_t ngroups = n >> 2;
   const size_t ntiles = (ngroups + kTileGroups - 1) / kTileGroups;
@@ -875,10 +942,22 @@ __global__ __launch_bounds__(kBlock) void ff_minmax_batch(FfBatch B) {
     V v[4][4];
     if (al) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) Vec4<V>::load(x + 4 * (gb + u * kBlock), v[u]);
+      for (int u = 0; u < 4; ++u) {
+#ifdef PSF_MM_KEEP
+        Vec4<V>::load_keep(x + 4 * (gb + u * kBlock), v[u]);
+#else
+        Vec4<V>::load(x + 4 * (gb + u * kBlock), v[u]);
+#endif
+      }
     } else {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) Vec4<V>::loadu(x + 4 * (gb + u * kBlock), v[u]);
+      for (int u = 0; u < 4; ++u) {
+#ifdef PSF_MM_KEEP
+        Vec4<V>::loadu_keep(x + 4 * (gb + u * kBlock), v[u]);
+#else
+        Shifted<V>::load(x, xa, r, gb + u * kBlock, v[u]);
+#endif
+      }
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u)
@@ -909,8 +988,8 @@ __global__ __launch_bounds__(kBlock) void ff_minmax_batch(FfBatch B) {
   }
 }
 
-template <typename V, int NB>
-__global__ __launch_bounds__(kBlock) void ff_encode_batch(FfBatch B) {
+template <typename V, int NB, int CAP>
+__global__ __launch_bounds__(kBlock) void ff_encode_batch(FfBatchT<CAP> B) {
   const int jb = batch_job(B, blockIdx.x, false);
   const FfJob& J = B.job[jb];
   const V* __restrict__ x = static_cast<const V*>(J.x);
@@ -919,6 +998,29 @@ __global__ __launch_bounds__(kBlock) void ff_encode_batch(FfBatch B) {
   const uint32_t wg = blockIdx.x - B.first[jb];
   const uint32_t nwg = batch_nwg(B, jb);
   const uint32_t mm_wg0 = B.mm_first[jb];
+  const size_t ngroups = n >> 2;
+  const size_t ntiles = (ngroups + kTileGroups - 1) / kTileGroups;
+  const size_t nfull = ngroups / kTileGroups;
+  size_t t0, t1;
+  tile_range_of(ntiles, wg, nwg, t0, t1);
+  const size_t tf = t1 < nfull ? t1 : nfull;
+  const bool al = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+  const int r = (int)((reinterpret_cast<uintptr_t>(x) & 15) / sizeof(V));
+  const V* xa = x - r;
+  // the first full tile's loads go out before the partials fold, which they
+  // do not depend on
+  V v[4][4];
+  auto load_tile = [&](size_t t) {
+    const size_t gb = t * kTileGroups + threadIdx.x;
+    if (al) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) Vec4<V>::load(x + 4 * (gb + u * kBlock), v[u]);
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) Shifted<V>::load(x, xa, r, gb + u * kBlock, v[u]);
+    }
+  };
+  if (t0 < tf) load_tile(t0);
   float mn_f = J.mn, mx_f = J.mx;
   if (J.mm_nwg) {
     typedef typename KeyOf<V>::K K;
@@ -983,24 +1085,9 @@ __global__ __launch_bounds__(kBlock) void ff_encode_batch(FfBatch B) {
   p.k17 = B.k17;
   p.a_lane = B.a_lane;
   p.c_lane = B.c_lane;
-  const size_t ngroups = n >> 2;
-  const size_t ntiles = (ngroups + kTileGroups - 1) / kTileGroups;
-  const size_t nfull = ngroups / kTileGroups;
-  size_t t0, t1;
-  tile_range_of(ntiles, wg, nwg, t0, t1);
-  const size_t tf = t1 < nfull ? t1 : nfull;
-  const bool al = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
   for (size_t t = t0; t < tf; ++t) {
-    const size_t gb = t * kTileGroups + threadIdx.x;
-    V v[4][4];
-    if (al) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) Vec4<V>::load(x + 4 * (gb + u * kBlock), v[u]);
-    } else {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) Vec4<V>::loadu(x + 4 * (gb + u * kBlock), v[u]);
-    }
-    encode_full_tile<V, NB>(v, q, p, out, gb);
+    if (t != t0) load_tile(t);
+    encode_full_tile<V, NB>(v, q, p, out, t * kTileGroups + threadIdx.x);
   }
   for (size_t t = (t0 > tf ? t0 : tf); t < t1; ++t) {
     const size_t gb = t * kTileGroups + threadIdx.x;
@@ -1029,8 +1116,8 @@ __global__ __launch_bounds__(kBlock) void ff_encode_batch(FfBatch B) {
   }
 }
 
-template <typename V, int NB>
-__global__ __launch_bounds__(kBlock) void ff_decode_batch(FfBatch B) {
+template <typename V, int NB, int CAP>
+__global__ __launch_bounds__(kBlock) void ff_decode_batch(FfBatchT<CAP> B) {
   const int jb = batch_job(B, blockIdx.x, false);
   const FfJob& J = B.job[jb];
   const uint8_t* __restrict__ code = static_cast<const uint8_t*>(J.x);
@@ -1288,18 +1375,30 @@ bool ff_batchable(const void* x, const void* out, size_t n, int nb, int value_ty
                 : ((oa & 15) == 0 && (xa & code_align) == 0);
 }
 
-template <typename V, int NB>
-static void launch_encode_batch(FfBatch& B, uint32_t enc_total, hipStream_t st, Profiler* prof, double bytes_mm,
-                                double bytes_enc) {
+template <typename V, int NB, int CAP>
+static void launch_encode_batch(FfBatchT<CAP>& B, uint32_t enc_total, hipStream_t st, Profiler* prof,
+                                double bytes_mm, double bytes_enc) {
   if (B.mm_total) {
     ProfScope ps(prof, kKMinmax, st, bytes_mm);
-    hipLaunchKernelGGL((ff_minmax_batch<V>), dim3(B.mm_total), dim3(kBlock), 0, st, B);
+    hipLaunchKernelGGL((ff_minmax_batch<V, CAP>), dim3(B.mm_total), dim3(kBlock), 0, st, B);
   }
   ProfScope pe(prof, kKEncode, st, bytes_enc);
-  hipLaunchKernelGGL((ff_encode_batch<V, NB>), dim3(enc_total), dim3(kBlock), 0, st, B);
+  hipLaunchKernelGGL((ff_encode_batch<V, NB, CAP>), dim3(enc_total), dim3(kBlock), 0, st, B);
 }
 
 static size_t tiles_of(size_t n) { return ((n >> 2) + kTileGroups - 1) / kTileGroups; }
+
+// fewest tiles per workgroup in the batched min/max and encode grids
+#ifndef PSF_BATCH_MM_TPW
+#define PSF_BATCH_MM_TPW 1
+#endif
+#ifndef PSF_BATCH_ENC_TPW
+#define PSF_BATCH_ENC_TPW 2  // 2 measured 10 % faster than 1 on 64 x 1 MiB batches (r02)
+#endif
+#ifndef PSF_BATCH_DEC_TPW
+#define PSF_BATCH_DEC_TPW 1  // one tile per workgroup measured best for decode
+#endif
+constexpr size_t kBatchMmTpw = PSF_BATCH_MM_TPW, kBatchEncTpw = PSF_BATCH_ENC_TPW, kBatchDecTpw = PSF_BATCH_DEC_TPW;
 
 // Workgroups of one array in a batched launch: its share (by tiles) of the
 // grid the single-array kernel would use, at least one.  A batch of large
@@ -1322,13 +1421,14 @@ size_t ff_batch_partials_bytes(const FfArray* arrs, int count) {
   return 2 * sizeof(uint64_t) * (wgs + 1);
 }
 
-int ff_encode_batch_launch(int value_type, int nb, const FfArray* arrs, int count, void* partials,
-                           PubSlot* pub_base, hipStream_t st, Profiler* prof) {
-  if (count <= 0) return kOk;
-  if (count > kBatchJobs) return kErrArg;
-  if (value_type != kFloat && value_type != kDouble) return kErrArg;
-  FfBatch B{};
-  for (int i = 0; i < kBatchJobs; ++i) B.first[i] = B.mm_first[i] = ~0u;
+template <int CAP>
+static int encode_batch_cap(int value_type, int nb, const FfArray* arrs, int count, void* partials,
+                            PubSlot* pub_base, hipStream_t st, Profiler* prof) {
+  static FfBatchT<CAP> B;  // host staging of the kernel arguments (launches are serialised per thread)
+  static std::mutex mu;
+  std::lock_guard<std::mutex> lock(mu);
+  memset(&B, 0, sizeof(B));
+  for (int i = 0; i < CAP; ++i) B.first[i] = B.mm_first[i] = ~0u;
   B.njobs = count;
   B.partials = partials;
   B.pub = pub_base;
@@ -1383,13 +1483,15 @@ int ff_encode_batch_launch(int value_type, int nb, const FfArray* arrs, int coun
     } else if (a.range_host) {
       return kErrArg;
     }
-    const uint32_t mm_nwg =
+    uint32_t mm_nwg =
         (a.preset.has_min && a.preset.has_max) ? 0u : (uint32_t)share_grid(a.n, tiles_mm, kMinmaxGrid);
+    if (mm_nwg > 1) mm_nwg = std::min<uint32_t>(mm_nwg, (uint32_t)((tiles_of(a.n) + kBatchMmTpw - 1) / kBatchMmTpw));
     J.mm_nwg = (uint16_t)mm_nwg;
     B.mm_first[i] = mm;
     mm += mm_nwg;
     B.first[i] = enc;
-    enc += (uint32_t)share_grid(a.n, tiles_all, kStreamGrid);
+    enc += std::min<uint32_t>((uint32_t)share_grid(a.n, tiles_all, kStreamGrid),
+                              (uint32_t)std::max<size_t>(1, (tiles_of(a.n) + kBatchEncTpw - 1) / kBatchEncTpw));
     if (mm_nwg) bytes_mm += (double)a.n * vsz;
     bytes_enc += (double)a.n * (vsz + nb);
   }
@@ -1397,26 +1499,37 @@ int ff_encode_batch_launch(int value_type, int nb, const FfArray* arrs, int coun
   B.mm_total = mm;
   if (value_type == kFloat) {
     switch (nb) {
-      case 1: launch_encode_batch<float, 1>(B, enc, st, prof, bytes_mm, bytes_enc); break;
-      case 2: launch_encode_batch<float, 2>(B, enc, st, prof, bytes_mm, bytes_enc); break;
-      default: launch_encode_batch<float, 3>(B, enc, st, prof, bytes_mm, bytes_enc); break;
+      case 1: launch_encode_batch<float, 1, CAP>(B, enc, st, prof, bytes_mm, bytes_enc); break;
+      case 2: launch_encode_batch<float, 2, CAP>(B, enc, st, prof, bytes_mm, bytes_enc); break;
+      default: launch_encode_batch<float, 3, CAP>(B, enc, st, prof, bytes_mm, bytes_enc); break;
     }
   } else {
     switch (nb) {
-      case 1: launch_encode_batch<double, 1>(B, enc, st, prof, bytes_mm, bytes_enc); break;
-      case 2: launch_encode_batch<double, 2>(B, enc, st, prof, bytes_mm, bytes_enc); break;
-      default: launch_encode_batch<double, 3>(B, enc, st, prof, bytes_mm, bytes_enc); break;
+      case 1: launch_encode_batch<double, 1, CAP>(B, enc, st, prof, bytes_mm, bytes_enc); break;
+      case 2: launch_encode_batch<double, 2, CAP>(B, enc, st, prof, bytes_mm, bytes_enc); break;
+      default: launch_encode_batch<double, 3, CAP>(B, enc, st, prof, bytes_mm, bytes_enc); break;
     }
   }
   return launch_status();
 }
 
-int ff_decode_batch_launch(int value_type, int nb, const FfDecArray* arrs, int count, hipStream_t st,
-                           Profiler* prof) {
+int ff_encode_batch_launch(int value_type, int nb, const FfArray* arrs, int count, void* partials,
+                           PubSlot* pub_base, hipStream_t st, Profiler* prof) {
   if (count <= 0) return kOk;
-  if (count > kBatchJobs) return kErrArg;
-  FfBatch B{};
-  for (int i = 0; i < kBatchJobs; ++i) B.first[i] = B.mm_first[i] = ~0u;
+  if (count > kFfBatchMax) return kErrArg;
+  if (value_type != kFloat && value_type != kDouble) return kErrArg;
+  return count <= kBatchSmall ? encode_batch_cap<kBatchSmall>(value_type, nb, arrs, count, partials, pub_base, st, prof)
+                              : encode_batch_cap<kFfBatchMax>(value_type, nb, arrs, count, partials, pub_base, st, prof);
+}
+
+template <int CAP>
+static int decode_batch_cap(int value_type, int nb, const FfDecArray* arrs, int count, hipStream_t st,
+                            Profiler* prof) {
+  static FfBatchT<CAP> B;
+  static std::mutex mu;
+  std::lock_guard<std::mutex> lock(mu);
+  memset(&B, 0, sizeof(B));
+  for (int i = 0; i < CAP; ++i) B.first[i] = B.mm_first[i] = ~0u;
   B.njobs = count;
   B.ratio = ff_ratio(nb);
   uint32_t wg = 0;
@@ -1432,25 +1545,34 @@ int ff_decode_batch_launch(int value_type, int nb, const FfDecArray* arrs, int c
     J.mx = arrs[i].mx;
     J.u.range = arrs[i].range;
     B.first[i] = wg;
-    wg += (uint32_t)tile_grid(arrs[i].n, kStreamGrid);  // one tile per workgroup measured best here
+    wg += std::min<uint32_t>((uint32_t)tile_grid(arrs[i].n, kStreamGrid),
+                             (uint32_t)std::max<size_t>(1, (tiles_of(arrs[i].n) + kBatchDecTpw - 1) / kBatchDecTpw));
     bytes += (double)arrs[i].n * (vsz + nb);
   }
   B.total = wg;
   ProfScope ps(prof, kKDecode, st, bytes);
   if (value_type == kFloat) {
     switch (nb) {
-      case 1: hipLaunchKernelGGL((ff_decode_batch<float, 1>), dim3(wg), dim3(kBlock), 0, st, B); break;
-      case 2: hipLaunchKernelGGL((ff_decode_batch<float, 2>), dim3(wg), dim3(kBlock), 0, st, B); break;
-      default: hipLaunchKernelGGL((ff_decode_batch<float, 3>), dim3(wg), dim3(kBlock), 0, st, B); break;
+      case 1: hipLaunchKernelGGL((ff_decode_batch<float, 1, CAP>), dim3(wg), dim3(kBlock), 0, st, B); break;
+      case 2: hipLaunchKernelGGL((ff_decode_batch<float, 2, CAP>), dim3(wg), dim3(kBlock), 0, st, B); break;
+      default: hipLaunchKernelGGL((ff_decode_batch<float, 3, CAP>), dim3(wg), dim3(kBlock), 0, st, B); break;
     }
   } else {
     switch (nb) {
-      case 1: hipLaunchKernelGGL((ff_decode_batch<double, 1>), dim3(wg), dim3(kBlock), 0, st, B); break;
-      case 2: hipLaunchKernelGGL((ff_decode_batch<double, 2>), dim3(wg), dim3(kBlock), 0, st, B); break;
-      default: hipLaunchKernelGGL((ff_decode_batch<double, 3>), dim3(wg), dim3(kBlock), 0, st, B); break;
+      case 1: hipLaunchKernelGGL((ff_decode_batch<double, 1, CAP>), dim3(wg), dim3(kBlock), 0, st, B); break;
+      case 2: hipLaunchKernelGGL((ff_decode_batch<double, 2, CAP>), dim3(wg), dim3(kBlock), 0, st, B); break;
+      default: hipLaunchKernelGGL((ff_decode_batch<double, 3, CAP>), dim3(wg), dim3(kBlock), 0, st, B); break;
     }
   }
   return launch_status();
+}
+
+int ff_decode_batch_launch(int value_type, int nb, const FfDecArray* arrs, int count, hipStream_t st,
+                           Profiler* prof) {
+  if (count <= 0) return kOk;
+  if (count > kFfBatchMax) return kErrArg;
+  return count <= kBatchSmall ? decode_batch_cap<kBatchSmall>(value_type, nb, arrs, count, st, prof)
+                              : decode_batch_cap<kFfBatchMax>(value_type, nb, arrs, count, st, prof);
 }
 
 }  // namespace psf

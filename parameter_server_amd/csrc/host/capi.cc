@@ -741,8 +741,27 @@ int psf_router_step(psf_router* r, psf_message* const* streams, int n, int iters
       for (int64_t s : sizes)
         if (s) throw psf::CheckError(PSF_ERR_ARG, "psf_router_step: slices for other ranks need an exchange");
       pr->fill(nullptr);
+      // the next step's slicing pass goes ahead of this step's decodes
+      if (it + 1 < iters) pr->prefetch(ms.data(), n);
       pr->decode_local();
     }
+    return PSF_OK;
+  });
+}
+int psf_router_host_stats(psf_router* r, int64_t* out) {
+  return guarded([&] {
+    if (!out) return PSF_ERR_ARG;
+    psf::PushRouter* pr = R(r);
+    out[0] = pr->stat_steps;
+    out[1] = pr->stat_encode_ns;
+    out[2] = pr->stat_decode_ns;
+    return PSF_OK;
+  });
+}
+int psf_router_host_stats_reset(psf_router* r) {
+  return guarded([&] {
+    psf::PushRouter* pr = R(r);
+    pr->stat_steps = pr->stat_encode_ns = pr->stat_decode_ns = 0;
     return PSF_OK;
   });
 }
@@ -772,6 +791,19 @@ int psf_router_encoded(psf_router* r, int i, int32_t* stream, int* server, psf_m
   });
 }
 
+int psf_context_host_stats(psf_context* ctx, int64_t* wait_ns, int64_t* waits) {
+  if (!ctx || !wait_ns || !waits) return PSF_ERR_ARG;
+  for (int w = 0; w < psf::Context::kWaitNum; ++w) {
+    wait_ns[w] = ctx->impl->wait_ns(w);
+    waits[w] = ctx->impl->wait_count(w);
+  }
+  return PSF_OK;
+}
+int psf_context_host_stats_reset(psf_context* ctx) {
+  if (!ctx) return PSF_ERR_ARG;
+  ctx->impl->reset_waits();
+  return PSF_OK;
+}
 int psf_profile_enable(psf_context* ctx, int kernel_mask) {
   if (!ctx) return PSF_ERR_ARG;
   ctx->impl->prof()->enable((uint32_t)kernel_mask);

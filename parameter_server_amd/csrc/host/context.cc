@@ -22,6 +22,7 @@ struct Context::StreamHolder {
   bool own;
   std::mutex mu;
   std::unordered_map<size_t, std::vector<void*>> free_lists;
+  std::unordered_map<size_t, std::vector<void*>> pinned_free;
 
   StreamHolder(int d, hipStream_t s, bool o) : device(d), stream(s), own(o) {}
   ~StreamHolder() {
@@ -29,6 +30,8 @@ struct Context::StreamHolder {
     (void)hipStreamSynchronize(stream);
     for (auto& kv : free_lists)
       for (void* p : kv.second) (void)hipFree(p);
+    for (auto& kv : pinned_free)
+      for (void* p : kv.second) (void)hipHostFree(p);
     if (own) (void)hipStreamDestroy(stream);
   }
   static size_t size_class(size_t bytes) {
@@ -57,6 +60,24 @@ struct Context::StreamHolder {
   void put(size_t cls, void* p) {
     std::lock_guard<std::mutex> l(mu);
     free_lists[cls].push_back(p);
+  }
+  void* get_pinned(size_t cls) {
+    {
+      std::lock_guard<std::mutex> l(mu);
+      auto it = pinned_free.find(cls);
+      if (it != pinned_free.end() && !it->second.empty()) {
+        void* p = it->second.back();
+        it->second.pop_back();
+        return p;
+      }
+    }
+    void* p = nullptr;
+    PSF_HIP_CHECK(hipHostMalloc(&p, cls, hipHostMallocMapped | hipHostMallocCoherent));
+    return p;
+  }
+  void put_pinned(size_t cls, void* p) {
+    std::lock_guard<std::mutex> l(mu);
+    pinned_free[cls].push_back(p);
   }
 };
 
@@ -93,6 +114,7 @@ Context::~Context() {
   }
   ring_uses_.clear();
   tracked_.clear();
+  for (hipEvent_t e : events_) (void)hipEventDestroy(e);
   (void)hipHostFree(lazy_h_);
   (void)hipFree(d_partials_);
   (void)hipFree(d_slots_);
@@ -113,9 +135,59 @@ Buffer Context::alloc(size_t bytes) {
   return b;
 }
 
+int64_t now_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (int64_t)ts.tv_sec * 1000000000 + ts.tv_nsec;
+}
+
+Context::Pinned Context::pinned(size_t bytes) {
+  Pinned p;
+  if (bytes == 0) return p;
+  if (device_ < 0) throw CheckError(kErrArg, "host-only context has no mapped memory");
+  const size_t cls = StreamHolder::size_class(bytes);
+  void* h = holder_->get_pinned(cls);
+  auto holder = holder_;
+  p.owner = std::shared_ptr<void>(h, [holder, cls](void* q) { holder->put_pinned(cls, q); });
+  p.host = static_cast<uint8_t*>(h);
+  void* d = nullptr;
+  PSF_HIP_CHECK(hipHostGetDevicePointer(&d, h, 0));
+  p.dev = static_cast<uint8_t*>(d);
+  p.bytes = bytes;
+  return p;
+}
+
+hipEvent_t Context::take_event() {
+  if (!events_.empty()) {
+    hipEvent_t e = events_.back();
+    events_.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  PSF_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  return e;
+}
+
+void Context::give_event(hipEvent_t e) {
+  if (e) events_.push_back(e);
+}
+
+void Context::wait_event(hipEvent_t e, int w) {
+  hipError_t q = hipEventQuery(e);
+  if (q == hipSuccess) return;
+  WaitTimer wt(this, static_cast<HostWait>(w));
+  for (uint64_t spin = 0; q == hipErrorNotReady; ++spin) {
+    if (spin > 4096) sched_yield();
+    q = hipEventQuery(e);
+  }
+  if (q != hipSuccess) throw CheckError(kErrHip, std::string("event wait failed: ") + hipGetErrorString(q));
+}
+
 void Context::wait_ticket(int i, uint32_t ticket) {
   if (device_ < 0) throw CheckError(kErrArg, "host-only context has no device workspace");
   const Slot* s = h_slots_ + i;
+  if (__atomic_load_n(&s->ticket, __ATOMIC_ACQUIRE) == ticket) return;
+  WaitTimer wt(this, kWaitPublish);
   for (uint64_t spin = 0;; ++spin) {
     if (__atomic_load_n(&s->ticket, __ATOMIC_ACQUIRE) == ticket) return;
     if ((spin & 255) == 255) {
@@ -134,6 +206,11 @@ void Context::wait_ticket(int i, uint32_t ticket) {
 uint32_t Context::wait_crc(int i, uint32_t ticket) {
   if (device_ < 0) throw CheckError(kErrArg, "host-only context has no device workspace");
   const Slot* s = h_slots_ + i;
+  {
+    const uint64_t w = __atomic_load_n(&s->crc_ticket, __ATOMIC_ACQUIRE);
+    if ((uint32_t)(w >> 32) == ticket) return (uint32_t)w;
+  }
+  WaitTimer wt(this, kWaitPublish);
   for (uint64_t spin = 0;; ++spin) {
     uint64_t w = __atomic_load_n(&s->crc_ticket, __ATOMIC_ACQUIRE);
     if ((uint32_t)(w >> 32) == ticket) return (uint32_t)w;
@@ -152,7 +229,9 @@ uint32_t Context::wait_crc(int i, uint32_t ticket) {
 }
 
 void Context::sync() {
-  if (device_ >= 0) PSF_HIP_CHECK(hipStreamSynchronize(stream_));
+  if (device_ < 0) return;
+  WaitTimer wt(this, kWaitSync);
+  PSF_HIP_CHECK(hipStreamSynchronize(stream_));
 }
 
 void RangeBatch::resolve(bool synced) {

@@ -60,6 +60,19 @@ class Context {
 
   // HBM buffer freed (stream-ordered) when its last reference drops.
   Buffer alloc(size_t bytes);
+  // Host-mapped coherent memory (kernel inputs the host fills, results the
+  // host reads once an event after the kernel has completed), pooled by size
+  // class; returned to the pool when the last reference drops.
+  struct Pinned {
+    uint8_t* host = nullptr;
+    uint8_t* dev = nullptr;
+    size_t bytes = 0;
+    std::shared_ptr<void> owner;
+  };
+  Pinned pinned(size_t bytes);
+  // pooled timing-free events
+  hipEvent_t take_event();
+  void give_event(hipEvent_t e);
 
   void* partials() const { return d_partials_; }
   Slot* d_slots() const { return d_slots_; }
@@ -74,6 +87,8 @@ class Context {
   // the same for a CRC published with its ticket in one word; returns the CRC
   uint32_t wait_crc(int i, uint32_t ticket);
   void sync();
+  // spin until `e` has completed; the time is counted as wait `w`
+  void wait_event(hipEvent_t e, int w);
   // stage a host buffer into HBM (used at the host edge)
   Buffer to_device(const Buffer& b);
   // NOISE: device table of the reference engine's standard normals, >= n long
@@ -94,8 +109,23 @@ class Context {
   std::mutex& mu() { return mu_; }
   Profiler* prof() { return &prof_; }
 
+  // Host time spent blocked on the device, by cause (psf_context_host_stats):
+  // stream synchronisations, waits on a kernel's published side-info, and
+  // slice-position read-backs.
+  enum HostWait { kWaitSync = 0, kWaitPublish, kWaitSlice, kWaitNum };
+  void add_wait(HostWait w, int64_t ns) {
+    wait_ns_[w] += ns;
+    ++wait_n_[w];
+  }
+  int64_t wait_ns(int w) const { return wait_ns_[w]; }
+  int64_t wait_count(int w) const { return wait_n_[w]; }
+  void reset_waits() {
+    for (int w = 0; w < kWaitNum; ++w) wait_ns_[w] = wait_n_[w] = 0;
+  }
+
  private:
   Profiler prof_;
+  int64_t wait_ns_[kWaitNum] = {0, 0, 0}, wait_n_[kWaitNum] = {0, 0, 0};
   static constexpr size_t kMaxTracked = 1024;
   std::vector<std::shared_ptr<RangeBatch>> tracked_;
   uint32_t* lazy_h_ = nullptr;  // host view of the ring
@@ -115,8 +145,20 @@ class Context {
   Slot* h_slots_ = nullptr;
   Slot* m_slots_ = nullptr;
   uint32_t ticket_ = 0;
+  std::vector<hipEvent_t> events_;
   Buffer noise_f32_, noise_f64_;
   std::mutex mu_;
+};
+
+// monotonic nanoseconds (host waits, router phase timers)
+int64_t now_ns();
+// adds the time from construction to destruction to ctx's wait counter w
+struct WaitTimer {
+  Context* ctx;
+  Context::HostWait w;
+  int64_t t0;
+  WaitTimer(Context* c, Context::HostWait which) : ctx(c), w(which), t0(now_ns()) {}
+  ~WaitTimer() { ctx->add_wait(w, now_ns() - t0); }
 };
 
 // time(NULL) as the reference's FIXING_FLOAT seed source (fixing_float.h:78),

@@ -135,11 +135,22 @@ class RemoteNode {
   std::unordered_map<int, Filter*> filters_;
 };
 
+// A KEY_CACHING signature computed before the chain ran (the slicer's fused
+// pass, slice.cc): the CRC32C of the first min(2048, bytes) bytes of the key
+// buffer at `ptr`.  Used only while the message's key is still that buffer.
+struct KeySigHint {
+  const uint8_t* ptr = nullptr;
+  size_t bytes = 0;
+  uint32_t crc = 0;
+  bool matches(const Buffer& key) const { return ptr && ptr == key.ptr && bytes == key.bytes; }
+};
+
 // RemoteNode::EncodeMessage / DecodeMessage of n messages at once, message i
 // on nodes[i] (each message still runs its own chain, in its own order, on its
 // own node's filter instances; stateful filters see their messages in array
 // order).  FIXING_FLOAT's element work is batched across the messages.
-void encode_batch(RemoteNode* const* nodes, Message* const* msgs, int n);
+// hints: null, or one per message.
+void encode_batch(RemoteNode* const* nodes, Message* const* msgs, int n, const KeySigHint* hints = nullptr);
 void decode_batch(RemoteNode* const* nodes, Message* const* msgs, int n);
 
 // Run the dequantise a deferred FIXING_FLOAT decode left pending (every

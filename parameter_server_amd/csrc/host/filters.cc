@@ -210,8 +210,10 @@ void FixingFloatFilter::encode_messages(Context* ctx, std::vector<FfMessage>& ms
   if (jobs.empty()) return;
   if (ctx->device() < 0) lazy = false;
   hipStream_t st = ctx->stream();
-  for (size_t base = 0; base < jobs.size(); base += Context::kSyncSlots) {
-    const size_t end = std::min(jobs.size(), base + (size_t)Context::kSyncSlots);
+  // publish slots serve kSyncSlots arrays at a time; lazy encodes use none
+  const size_t chunk = lazy ? std::max<size_t>(jobs.size(), 1) : (size_t)Context::kSyncSlots;
+  for (size_t base = 0; base < jobs.size(); base += chunk) {
+    const size_t end = std::min(jobs.size(), base + chunk);
     std::vector<uint32_t> tickets(end - base, 0);
     std::vector<FixedPoint> presets(end - base);
     std::vector<uint32_t> seeds(end - base);
@@ -511,14 +513,15 @@ struct SigBatch {
 }  // namespace
 
 static void launch_signatures(RemoteNode* const* nodes, Message* const* msgs, const std::vector<int>& idx,
-                              bool defer, SigBatch* sb) {
+                              bool defer, SigBatch* sb, const KeySigHint* hints = nullptr) {
   sb->sigs.assign(idx.size(), 0u);
   sb->chunks.clear();
   std::map<Context*, std::vector<size_t>> dev;
   for (size_t k = 0; k < idx.size(); ++k) {
     const Buffer& key = msgs[idx[k]]->key;
     const size_t len = std::min(key.bytes, (size_t)2048);
-    if (key.loc == Loc::kHost || nodes[idx[k]]->ctx()->device() < 0) sb->sigs[k] = crc32c_host(key.ptr, len);
+    if (hints && hints[idx[k]].matches(key)) sb->sigs[k] = hints[idx[k]].crc;
+    else if (key.loc == Loc::kHost || nodes[idx[k]]->ctx()->device() < 0) sb->sigs[k] = crc32c_host(key.ptr, len);
     else dev[nodes[idx[k]]->ctx()].push_back(k);
   }
   constexpr size_t kDeferCap = (size_t)(Context::kSlots - Context::kDeferSlot0);
@@ -554,7 +557,7 @@ static void launch_signatures(RemoteNode* const* nodes, Message* const* msgs, co
 // all-FIXING_FLOAT position launches (the two touch disjoint parts of a
 // message: keys vs values); the cache logic then runs in message order, so
 // the result equals sequential EncodeMessage calls.
-void encode_batch(RemoteNode* const* nodes, Message* const* msgs, int n) {
+void encode_batch(RemoteNode* const* nodes, Message* const* msgs, int n, const KeySigHint* hints) {
   size_t maxlen = 0;
   for (int i = 0; i < n; ++i) maxlen = std::max(maxlen, msgs[i]->task.filter.size());
   struct PendingKc {
@@ -603,7 +606,7 @@ void encode_batch(RemoteNode* const* nodes, Message* const* msgs, int n) {
       pend.pos = pos;
       pend.kc = std::move(kc);
       pend.kc_sig = std::move(kc_sig);
-      launch_signatures(nodes, msgs, pend.kc_sig, true, &pend.sb);
+      launch_signatures(nodes, msgs, pend.kc_sig, true, &pend.sb, hints);
       pend.active = true;
     }
     for (auto& kv : ff) FixingFloatFilter::encode_messages(kv.first, kv.second, /*lazy=*/true);

@@ -27,42 +27,50 @@ RemoteNode* PushRouter::receiver(int server, int32_t stream) {
 }
 
 // Executor::Submit for a push to kServerGroup (executor.cc:127-146): slice
-// (message.h:107-147), encode each valid slice on its per-peer node.
+// (message.h:107-147), encode each valid slice on its per-peer node.  The
+// slices copy the stream's Task and share its buffers, as `new
+// Message(msg->task)` plus the zero-copy SArray segments do.
 void PushRouter::encode(const Message* const* streams, int n, int64_t* sizes) {
+  const int64_t t0 = now_ns();
   results_.clear();
   enc_.clear();
   local_.clear();
   local_server_.clear();
   plan_.reset();
-  std::vector<Message> clones(n);  // `new Message(msg->task)` + zero-copy data
-  for (int i = 0; i < n; ++i) clones[i] = *streams[i];
-  std::vector<const Message*> cp(n);
-  for (int i = 0; i < n; ++i) cp[i] = &clones[i];
+  std::unique_ptr<SliceJob> job;
+  if (next_ && next_->same_inputs(streams, n)) job = std::move(next_);
+  next_.reset();
+  if (!job) job = slice_begin(ctx_, std::vector<const Message*>(streams, streams + n), ranges_, 8);
   std::vector<std::vector<Message>> parts;
   std::vector<std::vector<bool>> ok;
-  slice_messages(ctx_, cp, ranges_, 8, &parts, &ok);
+  std::vector<std::vector<KeySigHint>> hints;
+  slice_end(*job, &parts, &ok, &hints);
+  job.reset();
   const int S = (int)ranges_.size();
   std::vector<Message> slices;
   slices.reserve((size_t)n * S);
+  std::vector<KeySigHint> sh;
+  sh.reserve((size_t)n * S);
   std::vector<RemoteNode*> nodes;
   std::vector<int> srv;
   for (int i = 0; i < n; ++i)
     for (int d = 0; d < S; ++d) {
       if (!ok[i][d]) continue;  // the range misses the message's key range: not sent
       slices.push_back(std::move(parts[i][d]));
-      nodes.push_back(sender(clones[i].task.key_channel, d));
+      sh.push_back(hints[i][d]);
+      nodes.push_back(sender(streams[i]->task.key_channel, d));
       srv.push_back(d);
     }
   std::vector<Message*> mp(slices.size());
   for (size_t k = 0; k < slices.size(); ++k) mp[k] = &slices[k];
-  encode_batch(nodes.data(), mp.data(), (int)slices.size());
+  encode_batch(nodes.data(), mp.data(), (int)slices.size(), sh.data());
   std::vector<Message*> remote;
   std::vector<int> dest, rsrv;
   for (size_t k = 0; k < slices.size(); ++k) {
     if (keep_enc_) enc_.push_back(Encoded{slices[k].task.key_channel, srv[k], slices[k]});
     const int r = owner(srv[k]);
     if (r == rank_ && !loopback_) {
-      local_.push_back(slices[k]);  // delivered copy (Task + zero-copy buffers)
+      local_.push_back(std::move(slices[k]));  // delivered (the sender keeps nothing of it)
       local_server_.push_back(srv[k]);
     } else {
       remote.push_back(&slices[k]);
@@ -72,6 +80,12 @@ void PushRouter::encode(const Message* const* streams, int n, int64_t* sizes) {
   }
   plan_.reset(new SpillPlan(ctx_, remote.data(), dest.data(), rsrv.data(), (int)remote.size(), world_));
   for (int r = 0; r < 2 * world_; ++r) sizes[r] = plan_->sizes()[r];
+  ++stat_steps;
+  stat_encode_ns += now_ns() - t0;
+}
+
+void PushRouter::prefetch(const Message* const* streams, int n) {
+  next_ = slice_begin(ctx_, std::vector<const Message*>(streams, streams + n), ranges_, 8);
 }
 
 void PushRouter::fill(void* sendbuf) {
@@ -94,18 +108,22 @@ void PushRouter::decode_into_results(std::vector<Message>& ms, const std::vector
 }
 
 void PushRouter::decode_local() {
+  const int64_t t0 = now_ns();
   decode_into_results(local_, local_server_);
+  stat_decode_ns += now_ns() - t0;
   local_.clear();
   local_server_.clear();
 }
 
 void PushRouter::decode_received(const uint8_t* recvbuf, const int64_t* sizes_in) {
+  const int64_t t0 = now_ns();
   uint64_t total = 0;
   for (int r = 0; r < 2 * world_; ++r) total += (uint64_t)sizes_in[r];
   std::vector<Message> ms;
   std::vector<int> sv;
   spill_unpack(ctx_, own_copy(ctx_, recvbuf, total), world_, sizes_in, &ms, &sv);
   decode_into_results(ms, sv);
+  stat_decode_ns += now_ns() - t0;
 }
 
 }  // namespace psf

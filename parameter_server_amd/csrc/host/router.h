@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "filter.h"
+#include "slice.h"
 #include "spill.h"
 
 namespace psf {
@@ -27,6 +28,12 @@ class PushRouter {
   // executor copies the Task), pack the slices for other ranks; sizes[2r],
   // sizes[2r+1] = meta / payload bytes for rank r (see SpillPlan).
   void encode(const Message* const* streams, int n, int64_t* sizes);
+  // Launch the slicing pass of the NEXT encode() of the same streams now
+  // (called once this step's encode launches are queued, so the pass runs
+  // ahead of this step's decodes and the next encode waits for it alone).
+  // Only valid when nothing changes the streams' keys in between -- the
+  // multi-step driver (psf_router_step) -- and dropped if the inputs differ.
+  void prefetch(const Message* const* streams, int n);
   // write the send buffer of the last encode()
   void fill(void* sendbuf);
   // decode the slices whose server is on this rank
@@ -42,6 +49,8 @@ class PushRouter {
   void keep_encoded(bool v) { keep_enc_ = v; }
   int owner(int server) const { return (int)((int64_t)server * world_ / (int64_t)ranges_.size()); }
   int world() const { return world_; }
+  // host phase timers: steps, ns in encode(), ns in decode_local/received()
+  int64_t stat_steps = 0, stat_encode_ns = 0, stat_decode_ns = 0;
 
  private:
   RemoteNode* sender(int32_t stream, int server);
@@ -59,6 +68,7 @@ class PushRouter {
   std::unique_ptr<SpillPlan> plan_;
   std::vector<std::pair<int, Message>> results_;
   std::vector<Encoded> enc_;
+  std::unique_ptr<SliceJob> next_;
 };
 
 }  // namespace psf

@@ -15,10 +15,6 @@
 
 namespace psf {
 
-int lower_bound_launch(const void* keys, size_t n, int key_bytes, const uint64_t* d_bounds, int nb,
-                       uint64_t* d_pos, hipStream_t st);
-int lower_bound_batch_launch(const uint64_t* d_desc, int key_bytes, const uint64_t* d_bounds, int nb, int nmsg,
-                             uint64_t* d_pos, hipStream_t st);
 
 KeyRange even_divide(const KeyRange& r, uint64_t n, uint64_t i) {
   if (!(r.end >= r.begin)) throw CheckError(kErrCheck, "CHECK(valid())");
@@ -101,52 +97,112 @@ void slice_message(Context* ctx, const Message& msg, const std::vector<KeyRange>
   *valid = std::move(v[0]);
 }
 
-// SliceKOFVMessage for many messages at once: the device lower_bounds of all
-// of them are queued back to back and read back with one synchronisation.
+// SliceKOFVMessage for many messages at once: one launch, one event wait.
 void slice_messages(Context* ctx, const std::vector<const Message*>& msgs, const std::vector<KeyRange>& krs,
                     int key_bytes, std::vector<std::vector<Message>>* outs, std::vector<std::vector<bool>>* valid) {
+  std::unique_ptr<SliceJob> job = slice_begin(ctx, msgs, krs, key_bytes);
+  slice_end(*job, outs, valid);
+}
+
+static SliceJob::KeyId key_id(const Message& m) {
+  return SliceJob::KeyId{m.key.ptr, m.key.bytes, m.task.has_key_range, m.task.key_range};
+}
+
+bool SliceJob::same_inputs(const Message* const* ms, int n) const {
+  if ((size_t)n != msgs.size()) return false;
+  for (int i = 0; i < n; ++i) {
+    if (ms[i] != msgs[i]) return false;
+    const KeyId k = key_id(*ms[i]);
+    const KeyId& o = ids[i];
+    if (k.ptr != o.ptr || k.bytes != o.bytes || k.has_range != o.has_range || !(k.range == o.range)) return false;
+  }
+  return true;
+}
+
+SliceJob::~SliceJob() {
+  if (!ev) return;
+  if (!ended) (void)hipEventSynchronize(ev);  // the pinned records go back to the pool
+  ctx->give_event(ev);
+}
+
+std::unique_ptr<SliceJob> slice_begin(Context* ctx, const std::vector<const Message*>& msgs,
+                                      const std::vector<KeyRange>& krs, int key_bytes) {
   if (key_bytes != 8 && key_bytes != 4) throw CheckError(kErrArg, "key type must be 32 or 64 bit");
   const size_t n = krs.size();
   for (size_t i = 1; i < n; ++i)
     if (krs[i - 1].end != krs[i].begin) throw CheckError(kErrCheck, "CHECK_EQ(krs[i-1].end(), krs[i].begin())");
-  const size_t M = msgs.size();
-  outs->assign(M, {});
-  valid->assign(M, {});
-  std::vector<uint64_t> pos(M * (n + 1), 0), bounds(M * (n + 1), 0);
-  std::vector<size_t> dev;
+  std::unique_ptr<SliceJob> job(new SliceJob());
+  job->ctx = ctx;
+  job->msgs = msgs;
+  job->krs = krs;
+  job->key_bytes = key_bytes;
+  const size_t M = msgs.size(), nb = n + 1;
+  job->pos.assign(M * nb, 0);
+  job->ids.reserve(M);
+  std::vector<std::vector<uint64_t>> bounds(M);
   for (size_t m = 0; m < M; ++m) {
     const Message& msg = *msgs[m];
-    const std::vector<uint64_t> b = slice_bounds(msg, krs, key_bytes);
-    std::copy(b.begin(), b.end(), bounds.begin() + m * (n + 1));
+    job->ids.push_back(key_id(msg));
+    bounds[m] = slice_bounds(msg, krs, key_bytes);
     const size_t nkeys = msg.key.bytes / (size_t)key_bytes;
     if (nkeys == 0 || n == 0) continue;
-    if (msg.key.loc == Loc::kHost) host_lower_bounds(msg, key_bytes, b, pos.data() + m * (n + 1));
-    else dev.push_back(m);
+    if (msg.key.loc == Loc::kHost) host_lower_bounds(msg, key_bytes, bounds[m], job->pos.data() + m * nb);
+    else job->dev.push_back(m);
   }
-  if (!dev.empty()) {  // one upload, one launch, one read-back for all device-keyed messages
-    hipStream_t st = ctx->stream();
-    const size_t D = dev.size(), nb = n + 1;
-    std::vector<uint64_t> up(D * nb + 2 * D);
-    for (size_t q = 0; q < D; ++q) {
-      const Message& msg = *msgs[dev[q]];
-      std::copy(bounds.begin() + dev[q] * nb, bounds.begin() + (dev[q] + 1) * nb, up.begin() + q * nb);
-      up[D * nb + 2 * q] = reinterpret_cast<uint64_t>(msg.key.ptr);
-      up[D * nb + 2 * q + 1] = msg.key.bytes / (size_t)key_bytes;
-    }
-    Buffer d_up = ctx->alloc(up.size() * 8), d_p = ctx->alloc(D * nb * 8);
-    PSF_HIP_CHECK(hipMemcpyAsync(d_up.ptr, up.data(), up.size() * 8, hipMemcpyHostToDevice, st));
-    const uint64_t* d_b = reinterpret_cast<const uint64_t*>(d_up.ptr);
-    int s = lower_bound_batch_launch(d_b + D * nb, key_bytes, d_b, (int)nb, (int)D,
-                                     reinterpret_cast<uint64_t*>(d_p.ptr), st);
-    if (s != kOk) throw CheckError(s, "lower_bound launch failed");
-    std::vector<uint64_t> dpos(D * nb);
-    PSF_HIP_CHECK(hipMemcpyAsync(dpos.data(), d_p.ptr, D * nb * 8, hipMemcpyDeviceToHost, st));
-    ctx->sync();
-    for (size_t q = 0; q < D; ++q)
-      std::copy(dpos.begin() + q * nb, dpos.begin() + (q + 1) * nb, pos.begin() + dev[q] * nb);
+  const size_t D = job->dev.size();
+  if (D == 0) return job;
+  // host-mapped layout: desc[2D] | bounds[D nb] | pos[D nb] (u64) | sig[D n] (u32)
+  const size_t desc_b = 16 * D, bnd_b = 8 * D * nb, pos_b = 8 * D * nb, sig_b = 4 * D * n;
+  job->buf = ctx->pinned(desc_b + bnd_b + pos_b + sig_b);
+  uint64_t* h = reinterpret_cast<uint64_t*>(job->buf.host);
+  for (size_t q = 0; q < D; ++q) {
+    const Message& msg = *msgs[job->dev[q]];
+    h[2 * q] = reinterpret_cast<uint64_t>(msg.key.ptr);
+    h[2 * q + 1] = msg.key.bytes / (size_t)key_bytes;
+    std::copy(bounds[job->dev[q]].begin(), bounds[job->dev[q]].end(), h + 2 * D + q * nb);
   }
+  uint8_t* d = job->buf.dev;
+  SliceSigParams p{};
+  p.desc = reinterpret_cast<const uint64_t*>(d);
+  p.bounds = reinterpret_cast<const uint64_t*>(d + desc_b);
+  p.nslices = (int)n;
+  p.nmsg = (int)D;
+  p.pos = reinterpret_cast<uint64_t*>(d + desc_b + bnd_b);
+  p.sig = reinterpret_cast<uint32_t*>(d + desc_b + bnd_b + pos_b);
+  int s = slice_sig_launch(p, key_bytes, ctx->stream());
+  if (s != kOk) throw CheckError(s, "slice launch failed");
+  job->ev = ctx->take_event();
+  PSF_HIP_CHECK(hipEventRecord(job->ev, ctx->stream()));
+  return job;
+}
+
+void slice_end(SliceJob& job, std::vector<std::vector<Message>>* outs, std::vector<std::vector<bool>>* valid,
+               std::vector<std::vector<KeySigHint>>* hints) {
+  if (job.ended) throw CheckError(kErrArg, "slice job already ended");
+  const size_t M = job.msgs.size(), n = job.krs.size(), nb = n + 1, D = job.dev.size();
+  const uint32_t* sig = nullptr;
+  if (D) {
+    job.ctx->wait_event(job.ev, Context::kWaitSlice);
+    const uint8_t* h = job.buf.host;
+    const uint64_t* pos = reinterpret_cast<const uint64_t*>(h + 16 * D + 8 * D * nb);
+    sig = reinterpret_cast<const uint32_t*>(h + 16 * D + 16 * D * nb);
+    for (size_t q = 0; q < D; ++q) std::copy(pos + q * nb, pos + (q + 1) * nb, job.pos.begin() + job.dev[q] * nb);
+  }
+  job.ended = true;
+  outs->assign(M, {});
+  valid->assign(M, {});
   for (size_t m = 0; m < M; ++m)
-    build_slices(*msgs[m], krs, key_bytes, pos.data() + m * (n + 1), &(*outs)[m], &(*valid)[m]);
+    build_slices(*job.msgs[m], job.krs, job.key_bytes, job.pos.data() + m * nb, &(*outs)[m], &(*valid)[m]);
+  if (!hints) return;
+  hints->assign(M, std::vector<KeySigHint>(n));
+  for (size_t q = 0; q < D; ++q) {
+    const size_t m = job.dev[q];
+    for (size_t i = 0; i < n; ++i) {
+      const Message& sl = (*outs)[m][i];
+      if (!(*valid)[m][i] || sl.key.empty()) continue;
+      (*hints)[m][i] = KeySigHint{sl.key.ptr, sl.key.bytes, sig[q * n + i]};
+    }
+  }
 }
 
 }  // namespace psf

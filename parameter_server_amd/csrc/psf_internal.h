@@ -123,7 +123,7 @@ int ff_decode_launch(const void* code, size_t n, int value_type, int nb, const f
 // Batched launches over up to kFfBatchMax arrays of one value type and
 // num_bytes (aligned, nb 1..3: ff_batchable); encode publishes each array's
 // side-info to pub_base[slot] with its ticket.
-constexpr int kFfBatchMax = 64;
+constexpr int kFfBatchMax = 512;
 struct FfArray {
   const void* x;
   void* out;
@@ -160,6 +160,19 @@ int crc32c_launch(const void* d, size_t n, uint32_t* out, hipStream_t st,
 constexpr int kCrcBatchMax = 64;
 int crc32c_batch_launch(const void* const* d, const uint32_t* n, const int* slot, const uint32_t* ticket,
                         int count, PubSlot* pub, hipStream_t st, Profiler* prof);
+
+// crc32c.hip: the split positions of many sorted key arrays at the same
+// number of boundaries, with the CRC32C signature of each slice's first
+// min(2048, bytes) key bytes (slice i of message m: keys [pos[i], pos[i+1]))
+struct SliceSigParams {
+  const uint64_t* desc;    // per message {key pointer, key count}
+  const uint64_t* bounds;  // per message nslices + 1 lower_bound targets
+  int nslices;
+  int nmsg;
+  uint64_t* pos;  // per message nslices + 1 positions
+  uint32_t* sig;  // per message nslices signatures (0 for an empty slice)
+};
+int slice_sig_launch(const SliceSigParams& p, int key_bytes, hipStream_t st);
 
 // noise.hip: the standard-normal sequence of add_noise.h's default-seeded
 // engine (built once, on the device) and the per-message in-place apply.

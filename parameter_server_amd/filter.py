@@ -70,6 +70,15 @@ class Context:
                 out[name] = (n.value, ms.value, b.value)
         return out
 
+    def host_waits(self, reset: bool = False) -> dict:
+        """Host time blocked on the device since the last reset, by cause:
+        {"sync" | "publish" | "slice": (seconds, count)}."""
+        ns, cnt = (C.c_int64 * 3)(), (C.c_int64 * 3)()
+        check(lib().psf_context_host_stats(self.h, ns, cnt))
+        if reset:
+            check(lib().psf_context_host_stats_reset(self.h))
+        return {k: (ns[i] / 1e9, cnt[i]) for i, k in enumerate(("sync", "publish", "slice"))}
+
     def close(self):
         if self.h:
             lib().psf_context_destroy(self.h)

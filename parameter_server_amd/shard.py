@@ -249,6 +249,15 @@ class PushRouter:
         check(L.psf_router_decode_received(self.h, C.c_void_p(recv.data_ptr()),
                                            (C.c_int64 * (2 * W))(*sizes_in)))
 
+    def host_stats(self, reset: bool = False) -> dict:
+        """Host phase timers since the last reset: encodes, and seconds spent
+        inside the encodes and the decodes (blocked time included)."""
+        out = (C.c_int64 * 3)()
+        check(lib().psf_router_host_stats(self.h, out))
+        if reset:
+            check(lib().psf_router_host_stats_reset(self.h))
+        return {"steps": out[0], "encode_s": out[1] / 1e9, "decode_s": out[2] / 1e9}
+
     def results(self):
         """[(server, decoded Message)] of the last step."""
         from .filter import Message

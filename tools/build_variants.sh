@@ -2,16 +2,14 @@
 # Tuning experiments: build libpsf.so variants of ff_codec.hip with -D knobs
 # into tools/variants/<name>/ (git-ignored); load one with
 # PSF_LIBRARY_VARIANT=tools/variants/<name>/libpsf.so.
+#   tools/build_variants.sh <name> [flags...]      (SRC=<file> overrides the source)
 set -e
 cd "$(dirname "$0")/.."
 python -m parameter_server_amd.build > /dev/null
 OBJS=$(ls parameter_server_amd/build/*.o | grep -v ff_codec)
-build() {  # build <name> <flags...>   (SRC=<file> overrides the kernel source)
-  local name=$1; shift
-  mkdir -p tools/variants/$name
-  /opt/rocm/bin/hipcc -x hip --offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -Iinclude "$@" \
-    -c ${SRC:-parameter_server_amd/csrc/ff_codec.hip} -o tools/variants/$name/ff_codec.o
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o tools/variants/$name/libpsf.so $OBJS tools/variants/$name/ff_codec.o
-}
-build base
-SRC=tools/variants/src/ff_codec_old.hip build old
+name=$1; shift
+mkdir -p tools/variants/$name
+/opt/rocm/bin/hipcc -x hip --offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -Iinclude -Iparameter_server_amd/csrc "$@" \
+  -c ${SRC:-parameter_server_amd/csrc/ff_codec.hip} -o tools/variants/$name/ff_codec.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o tools/variants/$name/libpsf.so $OBJS tools/variants/$name/ff_codec.o
+echo tools/variants/$name/libpsf.so
