@@ -365,3 +365,58 @@ def test_batch_full_job_table(ctx, port, count):
             assert rcv_b[i].value(wb[i], 0).cpu().numpy().tobytes() == dec.tobytes(), i
     finally:
         F.set_clock(None)
+
+
+@pytest.mark.parametrize("count", [600])
+def test_batch_two_launches_of_large_table(ctx, port, count):
+    """More arrays than one job table holds (512): two launches, the first
+    with the 512-entry table; codes and decoded values equal the C
+    restatement."""
+    test_batch_full_job_table(ctx, port, count)
+
+
+def test_batch_tile_edges_and_offsets(ctx, port):
+    """One batch of arrays at tile edges (exactly 256 full tiles of 4096
+    values, 256 tiles plus a 1-value tail, 256 tiles plus one group, a
+    3-value array) and slices starting 1, 2 and 3 elements past a 16-byte
+    boundary (the C4 slices), presets mixed in: codes, side-info and decoded
+    values equal the C restatement and the one-at-a-time path."""
+    from parameter_server_amd import filter as F
+    F.set_clock(2024)
+    try:
+        rng = np.random.default_rng(3)
+        base = torch.from_numpy(rng.standard_normal(300_000).astype(np.float32)).to(DEV)
+        arrays = [torch.from_numpy(rng.standard_normal(n).astype(np.float32)).to(DEV)
+                  for n in (1 << 20, (1 << 20) + 1, (1 << 20) + 4, 3)]
+        arrays += [base[off:off + 100_000 + off] for off in (1, 2, 3)]
+        presets = [None, (-1.0, None), None, None, (None, 2.5), None, (-3.0, 3.0)]
+        snd_b = [F.RemoteNode(ctx) for _ in arrays]
+        rcv_b = [F.RemoteNode(ctx) for _ in arrays]
+        snd_s = [F.RemoteNode(ctx) for _ in arrays]
+
+        def msg(i, a):
+            from parameter_server_amd import FIXING_FLOAT
+            m = F.Message(request=True, push=True, key_channel=i)
+            m.add_value(a)
+            m.add_filter(FIXING_FLOAT, num_bytes=1, fixed_point=None if presets[i] is None else [presets[i]])
+            return m
+        mb = [msg(i, a) for i, a in enumerate(arrays)]
+        ms = [msg(i, a) for i, a in enumerate(arrays)]
+        F.RemoteNode.encode_many(snd_b, mb)
+        for nd, m in zip(snd_s, ms):
+            nd.encode(m)
+        wb = [m.clone() for m in mb]
+        F.RemoteNode.decode_many(rcv_b, wb)
+        ctx.sync()
+        for i, a in enumerate(arrays):
+            x = a.cpu().numpy()
+            assert mb[i].fixed_points(0) == ms[i].fixed_points(0), i
+            vb = snd_b[i].value(mb[i], 0).cpu().numpy().tobytes()
+            assert vb == snd_s[i].value(ms[i], 0).cpu().numpy().tobytes(), i
+            mn, mx = (None, None) if presets[i] is None else presets[i]
+            st, codes, pmn, pmx = port.ff_encode(x, 1, 2024, mn, mx)
+            assert st == 0 and vb == codes.tobytes(), i
+            st, dec = port.ff_decode(codes, 1, pmn, pmx, x.dtype)
+            assert rcv_b[i].value(wb[i], 0).cpu().numpy().tobytes() == dec.tobytes(), i
+    finally:
+        F.set_clock(None)
