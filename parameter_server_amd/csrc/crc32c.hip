@@ -219,20 +219,24 @@ __global__ __launch_bounds__(kBlock) void slice_sig_kernel(SliceSigParams P) {
   const int ns = P.nslices, nb = ns + 1;
   const int m = blockIdx.x / ns, i = blockIdx.x % ns;
   const K* keys = reinterpret_cast<const K*>(P.desc[2 * m]);
-  if (threadIdx.x < 2) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (w < 2) {  // wave w: lower_bound of bound i + w, a 64-ary search (log64 n dependent loads)
     const size_t n = (size_t)P.desc[2 * m + 1];
-    const K v = (K)P.bounds[(size_t)m * nb + i + threadIdx.x];
-    size_t lo = 0, len = n;
-    while (len > 0) {  // first index with keys[idx] >= v
-      const size_t half = len >> 1;
-      if (keys[lo + half] < v) {
-        lo += half + 1;
-        len -= half + 1;
-      } else {
-        len = half;
-      }
+    const K v = (K)P.bounds[(size_t)m * nb + i + w];
+    size_t lo = 0, len = n;  // the first index with keys[idx] >= v lies in [lo, lo + len]
+    while (len > 64) {
+      // pivots p_k = lo + (k+1) len / 65, strictly increasing; keys[p_k] < v
+      // holds for k < c and fails from c on (sorted keys)
+      const size_t pk = lo + ((size_t)(lane + 1) * len) / 65;
+      const int c = __popcll(__ballot(keys[pk] < v));
+      const size_t below = c ? lo + ((size_t)c * len) / 65 + 1 : lo;  // p_{c-1} + 1
+      const size_t above = c < 64 ? lo + ((size_t)(c + 1) * len) / 65 : lo + len;  // p_c
+      lo = below;
+      len = above - below;
     }
-    s_pos[threadIdx.x] = lo;
+    const bool lt = (size_t)lane < len && keys[lo + lane] < v;
+    const size_t pos = lo + (size_t)__popcll(__ballot(lt));  // the whole wave votes
+    if (lane == 0) s_pos[w] = pos;
   }
   __syncthreads();
   const uint64_t lo = s_pos[0], hi = s_pos[1] > lo ? s_pos[1] : lo;

@@ -81,6 +81,10 @@ struct Context::StreamHolder {
   }
 };
 
+// compress: the look-back words of up to 8191 fragments (512 MiB per launch);
+// uncompress: the control words of kSnappyBatchMax streams
+static constexpr size_t kZeroBytes[Context::kZeroKinds] = {65536, 2048};
+
 Context::Context(int device, hipStream_t stream, bool own) : device_(device), stream_(nullptr) {
   if (device < 0) return;  // host-only context: host-resident buffers, no HIP calls
   PSF_HIP_CHECK(hipSetDevice(device));
@@ -90,6 +94,8 @@ Context::Context(int device, hipStream_t stream, bool own) : device_(device), st
   // constructed in place: a temporary StreamHolder would destroy the stream
   holder_ = std::shared_ptr<StreamHolder>(new StreamHolder(device, stream, own));
   PSF_HIP_CHECK(hipMalloc(&d_partials_, 2 * sizeof(uint64_t) * kMaxGrid));
+  PSF_HIP_CHECK(hipMalloc(&zero_base_, 2 * (kZeroBytes[0] + kZeroBytes[1])));
+  PSF_HIP_CHECK(hipMemset(zero_base_, 0, 2 * (kZeroBytes[0] + kZeroBytes[1])));
   PSF_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&d_slots_), sizeof(Slot) * kSlots));
   PSF_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_slots_), sizeof(Slot) * kSlots,
                               hipHostMallocMapped | hipHostMallocCoherent));
@@ -117,6 +123,7 @@ Context::~Context() {
   for (hipEvent_t e : events_) (void)hipEventDestroy(e);
   (void)hipHostFree(lazy_h_);
   (void)hipFree(d_partials_);
+  (void)hipFree(zero_base_);
   (void)hipFree(d_slots_);
   (void)hipHostFree(h_slots_);
 }
@@ -139,6 +146,15 @@ int64_t now_ns() {
   timespec ts;
   clock_gettime(CLOCK_MONOTONIC, &ts);
   return (int64_t)ts.tv_sec * 1000000000 + ts.tv_nsec;
+}
+
+ZeroPair Context::zero_pair(int kind, size_t need) {
+  if (device_ < 0 || kind < 0 || kind >= kZeroKinds || need > kZeroBytes[kind]) return ZeroPair{};
+  uint8_t* base = static_cast<uint8_t*>(zero_base_);
+  for (int k = 0; k < kind; ++k) base += 2 * kZeroBytes[k];
+  const int p = zero_parity_[kind];
+  zero_parity_[kind] ^= 1;
+  return ZeroPair{base + p * kZeroBytes[kind], base + (p ^ 1) * kZeroBytes[kind], kZeroBytes[kind]};
 }
 
 Context::Pinned Context::pinned(size_t bytes) {

@@ -70,6 +70,11 @@ class Context {
     std::shared_ptr<void> owner;
   };
   Pinned pinned(size_t bytes);
+  // ZeroPair regions (psf_internal.h) by kind, zeroed at creation; a call
+  // whose `need` fits returns {this launch's, the next launch's} and flips the
+  // kind's parity, else {} (the launch then memsets its own scratch)
+  enum ZeroKind { kZeroCompress = 0, kZeroUncompress, kZeroKinds };
+  ZeroPair zero_pair(int kind, size_t need);
   // pooled timing-free events
   hipEvent_t take_event();
   void give_event(hipEvent_t e);
@@ -146,6 +151,8 @@ class Context {
   Slot* m_slots_ = nullptr;
   uint32_t ticket_ = 0;
   std::vector<hipEvent_t> events_;
+  void* zero_base_ = nullptr;
+  int zero_parity_[kZeroKinds] = {0, 0};
   Buffer noise_f32_, noise_f64_;
   std::mutex mu_;
 };

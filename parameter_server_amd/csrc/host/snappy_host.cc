@@ -104,13 +104,15 @@ void SnappyBatch::launch(size_t b, size_t e) {
       int st = kOk;
       if (comp && !cj.empty()) {
         Buffer scratch = c_.alloc(snappy_compress_batch_scratch(cj.data(), (int)cj.size()));
+        size_t nfrag = 0;
+        for (const SnappyCJob& q : cj) nfrag += (q.n + 65535) / 65536;
         st = snappy_compress_batch_launch(cj.data(), (int)cj.size(), scratch.ptr, c_.stream(), c_.prof(),
-                                          c_.pub_dev(0));
+                                          c_.pub_dev(0), c_.zero_pair(Context::kZeroCompress, nfrag * 8 + 8));
         cj.clear();
       } else if (!comp && !dj.empty()) {
         Buffer scratch = c_.alloc(snappy_uncompress_batch_scratch(dj.data(), (int)dj.size()));
         st = snappy_uncompress_batch_launch(dj.data(), (int)dj.size(), scratch.ptr, c_.stream(), c_.prof(),
-                                            c_.pub_dev(0));
+                                            c_.pub_dev(0), c_.zero_pair(Context::kZeroUncompress, dj.size() * 32 + 4));
         dj.clear();
       }
       if (st != kOk) throw CheckError(st, comp ? "snappy compress launch failed" : "snappy uncompress launch failed");

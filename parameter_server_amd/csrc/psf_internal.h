@@ -205,9 +205,18 @@ struct SnappyCJob {
   int slot;
   uint32_t ticket;
 };
+// A pair of device regions of `bytes` each that replaces a launch's memset of
+// its small control state: `cur` is zero when the launch starts (the previous
+// launch of the same kind cleared it), and the launch clears `next` for the
+// one after it.  {} (or a region too small): the launch memsets its scratch.
+struct ZeroPair {
+  void* cur = nullptr;
+  void* next = nullptr;
+  size_t bytes = 0;
+};
 size_t snappy_compress_batch_scratch(const SnappyCJob* jobs, int njobs);
 int snappy_compress_batch_launch(const SnappyCJob* jobs, int njobs, void* scratch, hipStream_t st,
-                                 Profiler* prof, PubSlot* pub_base);
+                                 Profiler* prof, PubSlot* pub_base, const ZeroPair& z = ZeroPair{});
 struct SnappyDJob {
   const void* in;
   size_t c;
@@ -219,7 +228,7 @@ struct SnappyDJob {
 };
 size_t snappy_uncompress_batch_scratch(const SnappyDJob* jobs, int njobs);
 int snappy_uncompress_batch_launch(const SnappyDJob* jobs, int njobs, void* scratch, hipStream_t st,
-                                   Profiler* prof, PubSlot* pub_base);
+                                   Profiler* prof, PubSlot* pub_base, const ZeroPair& z = ZeroPair{});
 
 // spill.hip: gather `n` copies (sorted by chunk0) into one send buffer; copy i
 // moves len bytes from src to dst + dst_off and owns chunks

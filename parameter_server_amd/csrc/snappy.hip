@@ -319,6 +319,8 @@ struct SnappyCJobs {
   CJob j[kSnappyBatchMax];
   PubSlot* pub;
   uint32_t njobs, nfrag;
+  uint64_t* znext;  // the next launch's zeroed state region (null: none)
+  uint32_t zwords;
 };
 __device__ __forceinline__ const CJob& cjob_of(const SnappyCJobs& J, uint32_t g) {
   uint32_t i = 0;
@@ -342,6 +344,8 @@ __global__ __launch_bounds__(kCThreads) void snappy_compress_frags(const SnappyC
   }
   for (uint32_t i = tid; i < (uint32_t)kSkipN; i += kCThreads) L.skip[i] = kSkip.v[i];
   for (uint32_t i = tid; i < kMinSlots; i += kCThreads) L.minlane[i] = 0xffffffffu;  // each parse step cleans up after itself
+  if (J.znext)  // the next launch's look-back state, zeroed here (stream order publishes it)
+    for (uint32_t i = blockIdx.x * kCThreads + tid; i < J.zwords; i += gridDim.x * kCThreads) J.znext[i] = 0;
   __syncthreads();
   const uint32_t nfrag = J.nfrag;
   uint32_t f = s_t0, fn = s_t1;
@@ -801,6 +805,8 @@ struct SnappyDJobs {
   uint32_t* ctrl;  // 8 words per stream: flags[0..3] (verdict, indexed, decoded by K-spec), counters[4..7]
   PubSlot* pub;
   uint32_t njobs, nfo1, nwin;  // streams; output fragments (at least one per stream); windows
+  uint32_t* znext;  // the next launch's zeroed ctrl region (null: none), cleared by K4
+  uint32_t zwords;
 };
 struct DScr {
   uint32_t *flags, *ctr;
@@ -1399,6 +1405,8 @@ __global__ __launch_bounds__(256) void snappy_dfrag(const SnappyDJobs J) {
   __shared__ uint32_t ib32[(kInWin + 32) / 4];
   __shared__ uint32_t s_last;
   __shared__ FewLds F;
+  if (J.znext)
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < J.zwords; i += gridDim.x * 256) J.znext[i] = 0;
   const uint32_t ji = djob_frag(J, blockIdx.x);
   const DJob& D = J.j[ji];
   const DScr S = dscr(J, D, ji);
@@ -1492,7 +1500,7 @@ size_t snappy_compress_scratch(size_t n) {
 }
 
 int snappy_compress_batch_launch(const SnappyCJob* jobs, int njobs, void* scratch, hipStream_t st, Profiler* prof,
-                                 PubSlot* pub_base) {
+                                 PubSlot* pub_base, const ZeroPair& z) {
   if (njobs <= 0 || njobs > kSnappyBatchMax) return kErrArg;
   SnappyCJobs K{};
   K.pub = pub_base;
@@ -1516,10 +1524,19 @@ int snappy_compress_batch_launch(const SnappyCJob* jobs, int njobs, void* scratc
   }
   uint8_t* s = static_cast<uint8_t*>(scratch);
   // look-back state (one word per fragment) and the fragment ticket counter,
-  // zeroed before the launch
-  uint64_t* state = reinterpret_cast<uint64_t*>(s + (size_t)K.nfrag * kSnappyFragOut);
+  // zero at the launch: the context's region the previous launch cleared, or
+  // the scratch's, cleared here
+  const size_t zneed = (size_t)K.nfrag * 8 + 8;
+  uint64_t* state;
+  if (z.cur && zneed <= z.bytes) {
+    state = static_cast<uint64_t*>(z.cur);
+    K.znext = static_cast<uint64_t*>(z.next);
+    K.zwords = (uint32_t)(z.bytes / 8);
+  } else {
+    state = reinterpret_cast<uint64_t*>(s + (size_t)K.nfrag * kSnappyFragOut);
+    if (hipMemsetAsync(state, 0, zneed, st) != hipSuccess) return kErrHip;
+  }
   uint32_t* ctr = reinterpret_cast<uint32_t*>(state + K.nfrag);
-  if (hipMemsetAsync(state, 0, (size_t)K.nfrag * 8 + 8, st) != hipSuccess) return kErrHip;
   // persistent workgroups, one per CU (the LDS footprint allows no more)
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) != hipSuccess ||
@@ -1534,7 +1551,7 @@ int snappy_compress_batch_launch(const SnappyCJob* jobs, int njobs, void* scratc
 int snappy_compress_launch(const void* in, size_t n, void* out, void* scratch, hipStream_t st, Profiler* prof,
                            PubSlot* pub, uint32_t ticket) {
   const SnappyCJob j{in, n, out, 0, ticket};
-  return snappy_compress_batch_launch(&j, 1, scratch, st, prof, pub);
+  return snappy_compress_batch_launch(&j, 1, scratch, st, prof, pub, ZeroPair{});
 }
 
 static size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
@@ -1559,7 +1576,7 @@ size_t snappy_uncompress_scratch(size_t C, size_t dsize) { return align256(32 + 
 // workgroup).  On streams
 // of stored fragments K-spec decodes everything and the others return at once.
 int snappy_uncompress_batch_launch(const SnappyDJob* jobs, int njobs, void* scratch, hipStream_t st,
-                                   Profiler* prof, PubSlot* pub_base) {
+                                   Profiler* prof, PubSlot* pub_base, const ZeroPair& z) {
   if (njobs <= 0 || njobs > kSnappyBatchMax) return kErrArg;
   SnappyDJobs K{};
   uint8_t* s = static_cast<uint8_t*>(scratch);
@@ -1589,7 +1606,14 @@ int snappy_uncompress_batch_launch(const SnappyDJob* jobs, int njobs, void* scra
     data += djob_bytes(q.c, q.dsize);
     bytes += (double)q.c + (double)q.dsize;
   }
-  if (hipMemsetAsync(K.ctrl, 0, (size_t)njobs * 32 + 4, st) != hipSuccess) return kErrHip;
+  const size_t zneed = (size_t)njobs * 32 + 4;
+  if (z.cur && zneed <= z.bytes) {  // the context's region the previous launch cleared
+    K.ctrl = static_cast<uint32_t*>(z.cur);
+    K.znext = static_cast<uint32_t*>(z.next);
+    K.zwords = (uint32_t)(z.bytes / 4);
+  } else if (hipMemsetAsync(K.ctrl, 0, zneed, st) != hipSuccess) {
+    return kErrHip;
+  }
   ProfScope ps(prof, kKSnappyDecompress, st, bytes);
   hipLaunchKernelGGL(snappy_dspec, dim3(K.nfo1 + K.njobs), dim3(256), 0, st, K);
   if (K.nwin) {
@@ -1609,7 +1633,7 @@ int snappy_uncompress_batch_launch(const SnappyDJob* jobs, int njobs, void* scra
 int snappy_uncompress_launch(const void* in, size_t C, uint32_t hdr, size_t dsize, void* out, void* scratch,
                              hipStream_t st, Profiler* prof, PubSlot* pub, uint32_t ticket) {
   const SnappyDJob j{in, C, hdr, dsize, out, 0, ticket};
-  return snappy_uncompress_batch_launch(&j, 1, scratch, st, prof, pub);
+  return snappy_uncompress_batch_launch(&j, 1, scratch, st, prof, pub, ZeroPair{});
 }
 
 }  // namespace psf
