@@ -737,12 +737,14 @@ int psf_router_step(psf_router* r, psf_message* const* streams, int n, int iters
     }
     std::vector<int64_t> sizes(2 * (size_t)pr->world());
     for (int it = 0; it < iters; ++it) {
-      pr->encode(ms.data(), n, sizes.data());
+      pr->encode_launch(ms.data(), n);
+      // the next step's slicing pass goes ahead of this step's decodes (and
+      // of the wait for its COMPRESSING lengths)
+      if (it + 1 < iters) pr->prefetch(ms.data(), n);
+      pr->encode_finish(sizes.data());
       for (int64_t s : sizes)
         if (s) throw psf::CheckError(PSF_ERR_ARG, "psf_router_step: slices for other ranks need an exchange");
       pr->fill(nullptr);
-      // the next step's slicing pass goes ahead of this step's decodes
-      if (it + 1 < iters) pr->prefetch(ms.data(), n);
       pr->decode_local();
     }
     return PSF_OK;

@@ -4,12 +4,14 @@
 // libpsf's HIP kernels on the owning node's Context stream.
 #pragma once
 #include <map>
+#include <memory>
 #include <mutex>
 #include <unordered_map>
 #include <utility>
 
 #include "context.h"
 #include "message.h"
+#include "snappy_host.h"
 
 namespace psf {
 
@@ -103,7 +105,10 @@ class CompressingFilter : public Filter {
   void decode(Message* msg) override;
   // the arrays of several messages on one context in batched launch chains
   // (same result as encode / decode on each message in turn)
-  static void encode_messages(Context* ctx, const std::vector<Message*>& msgs);
+  // defer: launch only, and hand the batch over (its finish() assigns the
+  // compressed buffers)
+  static void encode_messages(Context* ctx, const std::vector<Message*>& msgs,
+                              std::unique_ptr<SnappyBatch>* defer = nullptr);
   static void decode_messages(Context* ctx, const std::vector<Message*>& msgs);
 };
 
@@ -150,7 +155,18 @@ struct KeySigHint {
 // own node's filter instances; stateful filters see their messages in array
 // order).  FIXING_FLOAT's element work is batched across the messages.
 // hints: null, or one per message.
-void encode_batch(RemoteNode* const* nodes, Message* const* msgs, int n, const KeySigHint* hints = nullptr);
+// COMPRESSING launches of an encode_batch left in flight (pend argument):
+// the compressed buffers are assigned by finish().  Only the last filter
+// position is ever deferred, so nothing else in the batch waits on them.
+struct PendingEncode {
+  std::vector<std::unique_ptr<SnappyBatch>> snappy;
+  void finish() {
+    for (auto& b : snappy) b->finish();
+    snappy.clear();
+  }
+};
+void encode_batch(RemoteNode* const* nodes, Message* const* msgs, int n, const KeySigHint* hints = nullptr,
+                  PendingEncode* pend = nullptr);
 void decode_batch(RemoteNode* const* nodes, Message* const* msgs, int n);
 
 // Run the dequantise a deferred FIXING_FLOAT decode left pending (every

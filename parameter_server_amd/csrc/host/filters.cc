@@ -400,8 +400,10 @@ void CompressingFilter::encode(Message* msg) { encode_messages(ctx_, {msg}); }
 
 void CompressingFilter::decode(Message* msg) { decode_messages(ctx_, {msg}); }
 
-void CompressingFilter::encode_messages(Context* ctx, const std::vector<Message*>& msgs) {  // compressing.h:8-19
-  SnappyBatch batch(*ctx);
+void CompressingFilter::encode_messages(Context* ctx, const std::vector<Message*>& msgs,
+                                        std::unique_ptr<SnappyBatch>* defer) {  // compressing.h:8-19
+  std::unique_ptr<SnappyBatch> held(new SnappyBatch(*ctx));
+  SnappyBatch& batch = *held;
   for (Message* msg : msgs) {
     FilterConfig* conf = find(FilterConfig::COMPRESSING, msg);
     if (!conf) continue;
@@ -414,6 +416,11 @@ void CompressingFilter::encode_messages(Context* ctx, const std::vector<Message*
       conf->uncompressed_size.push_back(v.bytes);
       batch.compress(v, &v);
     }
+  }
+  if (defer) {
+    batch.launch_all();
+    *defer = std::move(held);
+    return;
   }
   batch.flush();
 }
@@ -557,7 +564,8 @@ static void launch_signatures(RemoteNode* const* nodes, Message* const* msgs, co
 // all-FIXING_FLOAT position launches (the two touch disjoint parts of a
 // message: keys vs values); the cache logic then runs in message order, so
 // the result equals sequential EncodeMessage calls.
-void encode_batch(RemoteNode* const* nodes, Message* const* msgs, int n, const KeySigHint* hints) {
+void encode_batch(RemoteNode* const* nodes, Message* const* msgs, int n, const KeySigHint* hints,
+                  PendingEncode* later) {
   size_t maxlen = 0;
   for (int i = 0; i < n; ++i) maxlen = std::max(maxlen, msgs[i]->task.filter.size());
   struct PendingKc {
@@ -601,7 +609,14 @@ void encode_batch(RemoteNode* const* nodes, Message* const* msgs, int n, const K
         f->encode(msgs[i]);
       }
     }
-    for (auto& kv : cz) CompressingFilter::encode_messages(kv.first, kv.second);
+    for (auto& kv : cz) {
+      if (later && pos + 1 == maxlen) {  // the last position: left in flight for the caller
+        later->snappy.emplace_back();
+        CompressingFilter::encode_messages(kv.first, kv.second, &later->snappy.back());
+      } else {
+        CompressingFilter::encode_messages(kv.first, kv.second);
+      }
+    }
     if (!kc.empty()) {  // signatures launched now, the caches after the next position's launches
       pend.pos = pos;
       pend.kc = std::move(kc);

@@ -30,13 +30,14 @@ RemoteNode* PushRouter::receiver(int server, int32_t stream) {
 // (message.h:107-147), encode each valid slice on its per-peer node.  The
 // slices copy the stream's Task and share its buffers, as `new
 // Message(msg->task)` plus the zero-copy SArray segments do.
-void PushRouter::encode(const Message* const* streams, int n, int64_t* sizes) {
-  const int64_t t0 = now_ns();
+void PushRouter::encode_launch(const Message* const* streams, int n) {
+  t_launch_ = now_ns();
   results_.clear();
   enc_.clear();
   local_.clear();
   local_server_.clear();
   plan_.reset();
+  pend_.finish();  // (a launch without its finish: complete it first)
   std::unique_ptr<SliceJob> job;
   if (next_ && next_->same_inputs(streams, n)) job = std::move(next_);
   next_.reset();
@@ -47,35 +48,41 @@ void PushRouter::encode(const Message* const* streams, int n, int64_t* sizes) {
   slice_end(*job, &parts, &ok, &hints);
   job.reset();
   const int S = (int)ranges_.size();
-  std::vector<Message> slices;
-  slices.reserve((size_t)n * S);
+  slices_.clear();
+  srv_.clear();
+  slices_.reserve((size_t)n * S);
   std::vector<KeySigHint> sh;
   sh.reserve((size_t)n * S);
   std::vector<RemoteNode*> nodes;
-  std::vector<int> srv;
   for (int i = 0; i < n; ++i)
     for (int d = 0; d < S; ++d) {
       if (!ok[i][d]) continue;  // the range misses the message's key range: not sent
-      slices.push_back(std::move(parts[i][d]));
+      slices_.push_back(std::move(parts[i][d]));
       sh.push_back(hints[i][d]);
       nodes.push_back(sender(streams[i]->task.key_channel, d));
-      srv.push_back(d);
+      srv_.push_back(d);
     }
-  std::vector<Message*> mp(slices.size());
-  for (size_t k = 0; k < slices.size(); ++k) mp[k] = &slices[k];
-  encode_batch(nodes.data(), mp.data(), (int)slices.size(), sh.data());
+  std::vector<Message*> mp(slices_.size());
+  for (size_t k = 0; k < slices_.size(); ++k) mp[k] = &slices_[k];
+  encode_batch(nodes.data(), mp.data(), (int)slices_.size(), sh.data(), &pend_);
+  stat_encode_ns += now_ns() - t_launch_;
+}
+
+void PushRouter::encode_finish(int64_t* sizes) {
+  const int64_t t0 = now_ns();
+  pend_.finish();
   std::vector<Message*> remote;
   std::vector<int> dest, rsrv;
-  for (size_t k = 0; k < slices.size(); ++k) {
-    if (keep_enc_) enc_.push_back(Encoded{slices[k].task.key_channel, srv[k], slices[k]});
-    const int r = owner(srv[k]);
+  for (size_t k = 0; k < slices_.size(); ++k) {
+    if (keep_enc_) enc_.push_back(Encoded{slices_[k].task.key_channel, srv_[k], slices_[k]});
+    const int r = owner(srv_[k]);
     if (r == rank_ && !loopback_) {
-      local_.push_back(std::move(slices[k]));  // delivered (the sender keeps nothing of it)
-      local_server_.push_back(srv[k]);
+      local_.push_back(std::move(slices_[k]));  // delivered (the sender keeps nothing of it)
+      local_server_.push_back(srv_[k]);
     } else {
-      remote.push_back(&slices[k]);
+      remote.push_back(&slices_[k]);
       dest.push_back(r);
-      rsrv.push_back(srv[k]);
+      rsrv.push_back(srv_[k]);
     }
   }
   plan_.reset(new SpillPlan(ctx_, remote.data(), dest.data(), rsrv.data(), (int)remote.size(), world_));

@@ -27,7 +27,16 @@ class PushRouter {
   // Slice + encode every stream's message (templates are copied, as the
   // executor copies the Task), pack the slices for other ranks; sizes[2r],
   // sizes[2r+1] = meta / payload bytes for rank r (see SpillPlan).
-  void encode(const Message* const* streams, int n, int64_t* sizes);
+  void encode(const Message* const* streams, int n, int64_t* sizes) {
+    encode_launch(streams, n);
+    encode_finish(sizes);
+  }
+  // encode() in two halves: everything up to the chains' last position,
+  // whose COMPRESSING launches stay in flight, and the wait for them plus the
+  // delivery split (the multi-step driver queues the next step's slicing in
+  // between)
+  void encode_launch(const Message* const* streams, int n);
+  void encode_finish(int64_t* sizes);
   // Launch the slicing pass of the NEXT encode() of the same streams now
   // (called once this step's encode launches are queued, so the pass runs
   // ahead of this step's decodes and the next encode waits for it alone).
@@ -69,6 +78,11 @@ class PushRouter {
   std::vector<std::pair<int, Message>> results_;
   std::vector<Encoded> enc_;
   std::unique_ptr<SliceJob> next_;
+  // the step between encode_launch and encode_finish
+  std::vector<Message> slices_;
+  std::vector<int> srv_;
+  PendingEncode pend_;
+  int64_t t_launch_ = 0;
 };
 
 }  // namespace psf

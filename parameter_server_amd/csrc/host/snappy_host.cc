@@ -128,8 +128,13 @@ void SnappyBatch::launch(size_t b, size_t e) {
   }
 }
 
-void SnappyBatch::flush() {
-  launch(0, jobs_.size());
+void SnappyBatch::launch_all() {
+  launch(launched_, jobs_.size());
+  launched_ = jobs_.size();
+}
+
+void SnappyBatch::finish() {
+  launch_all();
   int bad = kOk;
   for (auto& j : jobs_) {
     c_.wait_ticket(j.slot, j.ticket);
@@ -158,6 +163,7 @@ void SnappyBatch::flush() {
     *j.dst = j.out;
   }
   jobs_.clear();
+  launched_ = 0;
   if (bad != kOk) throw CheckError(kErrCheck, "CHECK(snappy::RawUncompress(src, src_size, data_))");
 }
 

@@ -23,7 +23,14 @@ class SnappyBatch {
   // mismatch is redone from the header at flush()
   void uncompress(const Buffer& src, Buffer* dst, const uint64_t* size_hint = nullptr);
   // one launch chain per kSnappyBatchMax streams of a kind, then one wait
-  void flush();
+  void flush() {
+    launch_all();
+    finish();
+  }
+  // flush() in two halves: the launches, and the wait that assigns the *dst
+  // (the publish slots stay taken in between)
+  void launch_all();
+  void finish();
 
  private:
   struct Job {
@@ -38,6 +45,7 @@ class SnappyBatch {
   };
   Context& c_;
   std::vector<Job> jobs_;
+  size_t launched_ = 0;  // jobs_[0, launched_) are in flight
   void prepare_uncompress(Job& j, const Buffer& src, uint32_t hdr, uint64_t dsize);
   void launch(size_t b, size_t e);
 };
