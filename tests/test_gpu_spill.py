@@ -146,6 +146,34 @@ def test_c5_rows_dim128_full_chain_8_servers():
                 assert not has_key and kn == 0
 
 
+@pytest.mark.parametrize("dim,compress", [(1, False), (128, True)])
+def test_router_multi_step_driver(dim, compress):
+    """psf_router_step over several steps in one call (what bench.py times):
+    each step's slicing pass is queued ahead of the previous step's decodes
+    and the COMPRESSING lengths are waited for after it; the last step's
+    decoded slices equal the restatement's, and a second call continues the
+    key cache (hits)."""
+    import torch
+
+    import oracle
+    from parameter_server_amd import filter as F
+    from parameter_server_amd import shard
+    STREAMS, M, S = (16, 1 << 12, 8) if dim == 1 else (1, 1 << 12, 8)
+    F.set_clock(SEED)
+    ctx = F.Context(0)
+    ranges = shard.server_ranges(S)
+    router = shard.PushRouter(ctx, ranges, 0, 1)
+    streams = _make_streams(F, range(STREAMS), M, dim, compress)
+    port = oracle.Port()
+    expect = {(d, s) for d in range(S) for s in range(STREAMS)}
+    for _ in range(2):
+        router.run(streams, 3)
+        torch.cuda.synchronize()
+        _check_step(F, router.results(), ranges, M, dim, port, expect)
+    hs = router.host_stats()
+    assert hs["steps"] == 6
+
+
 def _spill_worker(rank, world, port, backend, loopback, q):
     import torch
     import torch.distributed as dist
