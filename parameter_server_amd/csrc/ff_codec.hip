@@ -1395,6 +1395,10 @@ static size_t tiles_of(size_t n) { return ((n >> 2) + kTileGroups - 1) / kTileGr
 #define PSF_BATCH_MINMAX_GRID 8192
 #endif
 constexpr int kBatchMinmaxGrid = PSF_BATCH_MINMAX_GRID;
+#ifndef PSF_BATCH_STREAM_GRID
+#define PSF_BATCH_STREAM_GRID 16384  // the batched encode grid: 16384 measured 4 % faster than 8192 on C4
+#endif
+constexpr int kBatchStreamGrid = PSF_BATCH_STREAM_GRID;
 static_assert(kBatchMinmaxGrid <= 0xFFFF, "FfJob::mm_nwg is 16 bits");
 
 // fewest tiles per workgroup in the batched min/max and encode grids
@@ -1499,7 +1503,7 @@ static int encode_batch_cap(int value_type, int nb, const FfArray* arrs, int cou
     B.mm_first[i] = mm;
     mm += mm_nwg;
     B.first[i] = enc;
-    enc += std::min<uint32_t>((uint32_t)share_grid(a.n, tiles_all, kStreamGrid),
+    enc += std::min<uint32_t>((uint32_t)share_grid(a.n, tiles_all, kBatchStreamGrid),
                               (uint32_t)std::max<size_t>(1, (tiles_of(a.n) + kBatchEncTpw - 1) / kBatchEncTpw));
     if (mm_nwg) bytes_mm += (double)a.n * vsz;
     bytes_enc += (double)a.n * (vsz + nb);
