@@ -603,16 +603,28 @@ int psf_nodes_roundtrip_ex(psf_node* const* snd, psf_node* const* rcv, const psf
     for (int it = 0; it < iters; ++it) {
       int b = 0;
       for (int e : ends) {  // phase [b, e): encode all, deliver, decode all
-        for (int i = b; i < e; ++i) {
-          m[i] = tmpls[i]->m;  // fresh Task + zero-copy buffers
-          mp[i] = &m[i];
+        {
+          PSF_HPROF(0);
+          for (int i = b; i < e; ++i) {
+            m[i] = tmpls[i]->m;  // fresh Task + zero-copy buffers
+            mp[i] = &m[i];
+          }
         }
-        psf::encode_batch(s.data() + b, mp.data() + b, e - b);
-        for (int i = b; i < e; ++i) {
-          w[i] = m[i];  // delivered copy
-          wp[i] = &w[i];
+        {
+          PSF_HPROF(1);
+          psf::encode_batch(s.data() + b, mp.data() + b, e - b);
         }
-        psf::decode_batch(r.data() + b, wp.data() + b, e - b);
+        {
+          PSF_HPROF(5);
+          for (int i = b; i < e; ++i) {
+            w[i] = m[i];  // delivered copy
+            wp[i] = &w[i];
+          }
+        }
+        {
+          PSF_HPROF(6);
+          psf::decode_batch(r.data() + b, wp.data() + b, e - b);
+        }
         b = e;
       }
     }

@@ -142,6 +142,18 @@ Buffer Context::alloc(size_t bytes) {
   return b;
 }
 
+#ifdef PSF_HOST_PROF
+int64_t g_hprof_ns[kHProfSlots], g_hprof_n[kHProfSlots];
+extern "C" int psf_debug_host_prof(int64_t* ns, int64_t* n, int reset) {
+  for (int i = 0; i < kHProfSlots; ++i) {
+    ns[i] = g_hprof_ns[i];
+    n[i] = g_hprof_n[i];
+    if (reset) g_hprof_ns[i] = g_hprof_n[i] = 0;
+  }
+  return 0;
+}
+#endif
+
 int64_t now_ns() {
   timespec ts;
   clock_gettime(CLOCK_MONOTONIC, &ts);

@@ -168,6 +168,27 @@ struct WaitTimer {
   ~WaitTimer() { ctx->add_wait(w, now_ns() - t0); }
 };
 
+// Diagnostic builds (-DPSF_HOST_PROF): host time per code section, read with
+// psf_debug_host_prof.  Compiles to nothing otherwise.
+#ifdef PSF_HOST_PROF
+constexpr int kHProfSlots = 16;
+extern int64_t g_hprof_ns[kHProfSlots], g_hprof_n[kHProfSlots];
+struct HProf {
+  int id;
+  int64_t t0;
+  explicit HProf(int i) : id(i), t0(now_ns()) {}
+  ~HProf() {
+    g_hprof_ns[id] += now_ns() - t0;
+    ++g_hprof_n[id];
+  }
+};
+#define PSF_HPROF(id) ::psf::HProf _hprof_##id(id)
+#else
+#define PSF_HPROF(id) \
+  do {                \
+  } while (0)
+#endif
+
 // time(NULL) as the reference's FIXING_FLOAT seed source (fixing_float.h:78),
 // with an override hook so parity tests can pin it (psf_set_clock).
 int32_t ff_clock_seed();

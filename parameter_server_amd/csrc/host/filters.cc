@@ -277,6 +277,7 @@ void FixingFloatFilter::encode_messages(Context* ctx, std::vector<FfMessage>& ms
                                t ? (int)(q - base) : -1, t, range_of(q), ring_of(q)});
       }
       Buffer scratch = ctx->alloc(ff_batch_partials_bytes(arrs.data(), (int)arrs.size()));
+      PSF_HPROF(9);
       int s = ff_encode_batch_launch(jobs[part[0]].type, jobs[part[0]].nb, arrs.data(), (int)arrs.size(),
                                      scratch.ptr, ctx->pub_dev(0), st, ctx->prof());
       if (s != kOk) throw CheckError(s, "ff_encode batch launch failed");
@@ -387,6 +388,7 @@ void FixingFloatFilter::decode_messages(Context* ctx, std::vector<FfMessage>& ms
       const FfJob& j = jobs[q];
       arrs.push_back(FfDecArray{j.in.ptr, j.out.ptr, j.elems, j.fp->min_value, j.fp->max_value, j.range});
     }
+    PSF_HPROF(10);
     int s = ff_decode_batch_launch(jobs[part[0]].type, jobs[part[0]].nb, arrs.data(), (int)arrs.size(), st,
                                    ctx->prof());
     if (s != kOk) throw CheckError(s, "ff_decode batch launch failed");
@@ -550,6 +552,7 @@ static void launch_signatures(RemoteNode* const* nodes, Message* const* msgs, co
         c.ks.push_back(ks[q]);
         c.tk.push_back(ctx->next_ticket());
       }
+      PSF_HPROF(11);
       int s = crc32c_batch_launch(d.data(), n.data(), slot.data(), c.tk.data(), (int)d.size(),
                                   ctx->pub_dev(c.slot0), ctx->stream(), ctx->prof());
       if (s != kOk) throw CheckError(s, "crc32c batch launch failed");
@@ -576,6 +579,7 @@ void encode_batch(RemoteNode* const* nodes, Message* const* msgs, int n, const K
   } pend;
   auto finish_kc = [&] {
     if (!pend.active) return;
+    PSF_HPROF(4);
     pend.active = false;
     pend.sb.finish();
     size_t k = 0;
@@ -621,10 +625,16 @@ void encode_batch(RemoteNode* const* nodes, Message* const* msgs, int n, const K
       pend.pos = pos;
       pend.kc = std::move(kc);
       pend.kc_sig = std::move(kc_sig);
-      launch_signatures(nodes, msgs, pend.kc_sig, true, &pend.sb, hints);
+      {
+        PSF_HPROF(2);
+        launch_signatures(nodes, msgs, pend.kc_sig, true, &pend.sb, hints);
+      }
       pend.active = true;
     }
-    for (auto& kv : ff) FixingFloatFilter::encode_messages(kv.first, kv.second, /*lazy=*/true);
+    {
+      PSF_HPROF(3);
+      for (auto& kv : ff) FixingFloatFilter::encode_messages(kv.first, kv.second, /*lazy=*/true);
+    }
   }
   finish_kc();
 }
@@ -654,6 +664,7 @@ void decode_batch(RemoteNode* const* nodes, Message* const* msgs, int n) {
     }
     for (auto& kv : cz) CompressingFilter::decode_messages(kv.first, kv.second);
     if (!kc.empty()) {
+      PSF_HPROF(8);
       SigBatch sb;
       launch_signatures(nodes, msgs, kc_sig, false, &sb);
       size_t k = 0;
@@ -664,7 +675,10 @@ void decode_batch(RemoteNode* const* nodes, Message* const* msgs, int n) {
             ->decode_with(msgs[i], sig);
       }
     }
-    for (auto& kv : ff) FixingFloatFilter::decode_messages(kv.first, kv.second);
+    {
+      PSF_HPROF(7);
+      for (auto& kv : ff) FixingFloatFilter::decode_messages(kv.first, kv.second);
+    }
   }
 }
 
