@@ -97,6 +97,8 @@ class FixingFloatFilter : public Filter {
   void convert(Message* msg, bool encode);
 };
 
+class RemoteNode;
+
 // COMPRESSING, compressing.h:6-38 (snappy raw format)
 class CompressingFilter : public Filter {
  public:
@@ -109,7 +111,12 @@ class CompressingFilter : public Filter {
   // compressed buffers)
   static void encode_messages(Context* ctx, const std::vector<Message*>& msgs,
                               std::unique_ptr<SnappyBatch>* defer = nullptr);
-  static void decode_messages(Context* ctx, const std::vector<Message*>& msgs);
+  // nodes (optional, one per message): where a message's next decodes are
+  // KEY_CACHING then FIXING_FLOAT on that node, FIXING_FLOAT's decode runs
+  // fused into the uncompress for every value array it can take
+  // (Message::predecoded)
+  static void decode_messages(Context* ctx, const std::vector<Message*>& msgs,
+                              const std::vector<RemoteNode*>* nodes = nullptr);
 };
 
 // NOISE, add_noise.h:9-41
@@ -133,6 +140,7 @@ class RemoteNode {
   // Server side: let FIXING_FLOAT's decode hand its codes to the consumer
   // (KvMapFtrl / ordered match dequantise them in-register).
   void set_defer_dequant(bool v);
+  bool defer_dequant() const { return defer_dequant_; }
 
  private:
   Context* ctx_;

@@ -340,9 +340,12 @@ void FixingFloatFilter::decode_messages(Context* ctx, std::vector<FfMessage>& ms
       if (f.type != FilterConfig::KEY_CACHING) defer = false;
     }
     size_t keep = first;
+    std::vector<uint8_t> pre;
+    pre.swap(m.msg->predecoded);  // decoded by the COMPRESSING decode before (fused_ff_plan)
     for (size_t q = first; q < jobs.size(); ++q) {
       FfJob& j = jobs[q];
       FixedFloatConfig& fp = *j.fp;
+      if ((size_t)j.i < pre.size() && pre[j.i]) continue;
       if (fp.pending && fp.pending->ctx == ctx && !fp.pending->done && !(defer && j.type == kFloat)) {
         // encoded on this context's stream: the kernel reads {min, max} where
         // the encode left them (CHECK_GT(bin, 0) is reported when settled)
@@ -427,21 +430,101 @@ void CompressingFilter::encode_messages(Context* ctx, const std::vector<Message*
   batch.flush();
 }
 
-void CompressingFilter::decode_messages(Context* ctx, const std::vector<Message*>& msgs) {  // compressing.h:20-37
+// The FIXING_FLOAT decode that follows message msg's COMPRESSING decode on
+// `node`, as SnappyDequant parameters per value array (values == null: that
+// array is decoded unfused).  Only where the decodes in between are
+// KEY_CACHING (keys only) and FixingFloatFilter::decode_messages would take
+// the array with nothing left to check: num_bytes 1 or 2, a float/double
+// array whose codes fill whole values, its range known (set on the config, or
+// left on the device by an encode on this context), and no deferred
+// dequantise.  The fixed_point entry of an array is found as collect_jobs
+// finds it, from the arrays' sizes after the uncompress (the recorded sizes).
+static void fused_ff_plan(Context* ctx, RemoteNode* node, Message* msg, const FilterConfig* cz,
+                          std::vector<SnappyDequant>* plan) {
+  plan->assign(msg->value.size(), SnappyDequant{});
+  const auto& fl = msg->task.filter;
+  size_t c = fl.size();
+  for (size_t q = 0; q < fl.size(); ++q)
+    if (&fl[q] == cz) c = q;
+  if (c == fl.size()) return;
+  while (c > 0 && fl[c - 1].type == FilterConfig::KEY_CACHING) --c;
+  if (c == 0 || fl[c - 1].type != FilterConfig::FIXING_FLOAT) return;
+  FilterConfig* ff = Filter::find(FilterConfig::FIXING_FLOAT, msg);
+  if (ff != &fl[c - 1]) return;
+  const int nb = ff->num_bytes;
+  if (nb != 1 && nb != 2) return;
+  if (msg->value.size() != msg->task.value_type.size()) return;
+  const size_t has_key = msg->has_key() ? 1 : 0;
+  size_t k = 0;
+  for (size_t i = 0; i < msg->value.size(); ++i) {
+    const uint64_t dsize = msg->value[i].empty() ? 0 : cz->uncompressed_size[i + has_key];
+    if (dsize == 0) continue;  // empty after the uncompress: collect_jobs skips it
+    const int type = msg->task.value_type[i];
+    if (type != kFloat && type != kDouble) continue;
+    const size_t kk = k++;
+    if (kk >= ff->fixed_point.size()) break;
+    if (dsize % (uint64_t)nb || msg->value[i].loc != Loc::kDevice) continue;
+    if (node->defer_dequant() && type == kFloat) continue;
+    const FixedFloatConfig& fp = ff->fixed_point[kk];
+    SnappyDequant d;
+    d.nb = nb;
+    d.value_type = type;
+    if (fp.pending) {
+      if (fp.pending->ctx != ctx || fp.pending->done) continue;  // decode_messages would settle it
+      d.range = fp.device_range();
+    } else {
+      if (!fp.has_min || !fp.has_max || !((double)fp.max_value - (double)fp.min_value > 0)) continue;
+      d.mn = fp.min_value;
+      d.mx = fp.max_value;
+    }
+    d.values = reinterpret_cast<void*>(1);  // taken; the buffer is SnappyBatch's
+    (*plan)[i] = d;
+  }
+}
+
+void CompressingFilter::decode_messages(Context* ctx, const std::vector<Message*>& msgs,
+                                        const std::vector<RemoteNode*>* nodes) {  // compressing.h:20-37
   SnappyBatch batch(*ctx);
-  for (Message* msg : msgs) {
+  std::vector<SnappyDequant> plan;
+  std::vector<std::unique_ptr<bool[]>> fused;  // one flag per value array of each message in owners
+  std::vector<Message*> owners;
+  for (size_t m = 0; m < msgs.size(); ++m) {
+    Message* msg = msgs[m];
     FilterConfig* conf = find(FilterConfig::COMPRESSING, msg);
     if (!conf) continue;
     const int has_key = msg->has_key() ? 1 : 0;
     if (conf->uncompressed_size.size() != msg->value.size() + has_key)
       throw CheckError(kErrCheck, "CHECK_EQ(conf->uncompressed_size_size(), msg->value.size() + has_key)");
+    plan.clear();
+    if (nodes && ctx->device() >= 0) fused_ff_plan(ctx, (*nodes)[m], msg, conf, &plan);
+    bool* flags = nullptr;
+    for (const SnappyDequant& d : plan)
+      if (d.values && !flags) {
+        fused.emplace_back(new bool[msg->value.size()]());
+        owners.push_back(msg);
+        flags = fused.back().get();
+      }
     // the recorded sizes size the launches (the device checks them against
     // each stream's header; snappy_host.cc)
     size_t k = 0;
     if (has_key) batch.uncompress(msg->key, &msg->key, &conf->uncompressed_size[k++]);
-    for (auto& v : msg->value) batch.uncompress(v, &v, &conf->uncompressed_size[k++]);
+    for (size_t i = 0; i < msg->value.size(); ++i, ++k) {
+      Buffer& v = msg->value[i];
+      if (flags && plan[i].values) batch.uncompress_dequant(v, &v, conf->uncompressed_size[k], plan[i], &flags[i], (int)m);
+      else batch.uncompress(v, &v, &conf->uncompressed_size[k]);
+    }
   }
   batch.flush();
+  for (size_t f = 0; f < owners.size(); ++f) {  // the flags flush() set
+    Message* msg = owners[f];
+    msg->predecoded.assign(msg->value.size(), 0);
+    bool any = false;
+    for (size_t i = 0; i < msg->value.size(); ++i) {
+      msg->predecoded[i] = fused[f][i] ? 1 : 0;
+      any = any || fused[f][i];
+    }
+    if (!any) msg->predecoded.clear();
+  }
 }
 
 // --------------------------------------------------------------- NOISE ----
@@ -488,6 +571,7 @@ void RemoteNode::EncodeMessage(Message* msg) {  // remote_node.cc:17-22
 }
 
 void RemoteNode::DecodeMessage(Message* msg) {  // remote_node.cc:23-29, reverse order
+  msg->predecoded.clear();
   for (int i = (int)msg->task.filter.size() - 1; i >= 0; --i)
     FindFilterOrCreate(msg->task.filter[i])->decode(msg);
 }
@@ -641,10 +725,14 @@ void encode_batch(RemoteNode* const* nodes, Message* const* msgs, int n, const K
 
 void decode_batch(RemoteNode* const* nodes, Message* const* msgs, int n) {
   size_t maxlen = 0;
-  for (int i = 0; i < n; ++i) maxlen = std::max(maxlen, msgs[i]->task.filter.size());
+  for (int i = 0; i < n; ++i) {
+    maxlen = std::max(maxlen, msgs[i]->task.filter.size());
+    msgs[i]->predecoded.clear();
+  }
   for (size_t r = 0; r < maxlen; ++r) {  // r-th filter from the end of every chain
     std::map<Context*, std::vector<FfMessage>> ff;
     std::map<Context*, std::vector<Message*>> cz;
+    std::map<Context*, std::vector<RemoteNode*>> cz_nodes;
     std::vector<int> kc, kc_sig;
     for (int i = 0; i < n; ++i) {
       const size_t len = msgs[i]->task.filter.size();
@@ -658,11 +746,12 @@ void decode_batch(RemoteNode* const* nodes, Message* const* msgs, int n) {
         if (KeyCachingFilter::needs_signature(msgs[i], false)) kc_sig.push_back(i);
       } else if (conf.type == FilterConfig::COMPRESSING) {
         cz[nodes[i]->ctx()].push_back(msgs[i]);
+        cz_nodes[nodes[i]->ctx()].push_back(nodes[i]);
       } else {
         f->decode(msgs[i]);
       }
     }
-    for (auto& kv : cz) CompressingFilter::decode_messages(kv.first, kv.second);
+    for (auto& kv : cz) CompressingFilter::decode_messages(kv.first, kv.second, &cz_nodes[kv.first]);
     if (!kc.empty()) {
       PSF_HPROF(8);
       SigBatch sb;

@@ -181,6 +181,9 @@ struct Message {
   Buffer key;
   std::vector<Buffer> value;
   std::vector<PendingDequant> pending;  // empty, or one entry per value array
+  // value arrays whose FIXING_FLOAT decode already ran, fused into the
+  // COMPRESSING decode before it (decode_batch); empty, or one per value array
+  std::vector<uint8_t> predecoded;
   bool key_frame_seen = false;          // Van::Recv bookkeeping (psf_msg_recv_frame)
 
   bool is_pending(size_t i) const { return i < pending.size() && pending[i].nb != 0; }

@@ -93,6 +93,26 @@ void SnappyBatch::uncompress(const Buffer& src, Buffer* dst, const uint64_t* siz
   jobs_.push_back(std::move(j));
 }
 
+void SnappyBatch::uncompress_dequant(const Buffer& src, Buffer* dst, uint64_t size_hint, const SnappyDequant& dq,
+                                     bool* fused, int group) {
+  const size_t before = jobs_.size();
+  uncompress(src, dst, &size_hint);
+  if (jobs_.size() != before + 1 || jobs_.back().dst != dst) return;  // empty source: nothing launched
+  Job& j = jobs_.back();
+  if (!j.hinted) return;  // the header was read: decoded unfused
+  const size_t vsz = dq.value_type == kDouble ? 8 : 4;
+  j.values = c_.alloc(j.out.bytes / (size_t)dq.nb * vsz);
+  j.dq = dq;
+  j.dq.values = j.values.ptr;
+  if (!snappy_dequant_ok(j.dq, j.out.bytes)) {
+    j.dq = SnappyDequant{};
+    j.values = Buffer{};
+    return;
+  }
+  j.fused = fused;
+  j.group = group;
+}
+
 // every pending stream in as few launch chains as possible: compress and
 // uncompress jobs each in groups of up to kSnappyBatchMax
 void SnappyBatch::launch(size_t b, size_t e) {
@@ -121,7 +141,7 @@ void SnappyBatch::launch(size_t b, size_t e) {
       Job& j = jobs_[i];
       if (j.compress != comp) continue;
       if (comp) cj.push_back(SnappyCJob{j.in.ptr, j.in.bytes, j.out.ptr, j.slot, j.ticket});
-      else dj.push_back(SnappyDJob{j.in.ptr, j.in.bytes, j.hdr, j.out.bytes, j.out.ptr, j.slot, j.ticket});
+      else dj.push_back(SnappyDJob{j.in.ptr, j.in.bytes, j.hdr, j.out.bytes, j.out.ptr, j.slot, j.ticket, j.dq});
       if (cj.size() == (size_t)kSnappyBatchMax || dj.size() == (size_t)kSnappyBatchMax) go();
     }
     go();
@@ -136,9 +156,32 @@ void SnappyBatch::launch_all() {
 void SnappyBatch::finish() {
   launch_all();
   int bad = kOk;
+  // a fused stream whose header disagrees with its hint: every fused stream of
+  // its group (one message's arrays) is decoded again unfused, so the
+  // FIXING_FLOAT decode that follows sees the arrays the unfused chain gives
+  std::vector<int> redo_groups;
   for (auto& j : jobs_) {
     c_.wait_ticket(j.slot, j.ticket);
-    if (j.hinted && c_.pub_host(j.slot)->status == kErrHeaderHint) {
+    if (j.dq.values && c_.pub_host(j.slot)->status == kErrHeaderHint) redo_groups.push_back(j.group);
+  }
+  for (auto& j : jobs_) {
+    const bool regroup = j.dq.values && std::find(redo_groups.begin(), redo_groups.end(), j.group) != redo_groups.end();
+    if (regroup) {  // the codes, by the header (the slot is this job's own)
+      j.dq = SnappyDequant{};
+      j.values = Buffer{};
+      uint64_t dsize = 0;
+      const uint32_t hdr = snappy_read_header(c_, j.src, &dsize);
+      if (!hdr) {
+        bad = kErrCheck;
+        continue;
+      }
+      prepare_uncompress(j, j.src, hdr, dsize);
+      const SnappyDJob d{j.in.ptr, j.in.bytes, j.hdr, j.out.bytes, j.out.ptr, 0, j.ticket};
+      Buffer scratch = c_.alloc(snappy_uncompress_batch_scratch(&d, 1));
+      const int st = snappy_uncompress_batch_launch(&d, 1, scratch.ptr, c_.stream(), c_.prof(), c_.pub_dev(j.slot));
+      if (st != kOk) throw CheckError(st, "snappy uncompress launch failed");
+      c_.wait_ticket(j.slot, j.ticket);
+    } else if (j.hinted && c_.pub_host(j.slot)->status == kErrHeaderHint) {
       // the stream's header disagrees with the size hint: decode by the
       // header, as UncompressFrom does (the slot is this job's own)
       uint64_t dsize = 0;
@@ -160,7 +203,12 @@ void SnappyBatch::finish() {
       continue;
     }
     j.out.bytes = h.size;
-    *j.dst = j.out;
+    if (j.dq.values) {
+      *j.dst = j.values;
+      *j.fused = true;
+    } else {
+      *j.dst = j.out;
+    }
   }
   jobs_.clear();
   launched_ = 0;

@@ -22,6 +22,13 @@ class SnappyBatch {
   // header to the host, the device checks the header against it, and a
   // mismatch is redone from the header at flush()
   void uncompress(const Buffer& src, Buffer* dst, const uint64_t* size_hint = nullptr);
+  // The same, with FIXING_FLOAT's decode fused (SnappyDequant; dq.values is
+  // allocated here): at flush() *dst receives the values and *fused is set,
+  // or -- when the stream's header disagrees with the hint, which the fused
+  // launch cannot follow -- every stream of `group` is decoded again unfused
+  // and *dst receives codes as uncompress() would give.
+  void uncompress_dequant(const Buffer& src, Buffer* dst, uint64_t size_hint, const SnappyDequant& dq,
+                          bool* fused, int group);
   // one launch chain per kSnappyBatchMax streams of a kind, then one wait
   void flush() {
     launch_all();
@@ -42,6 +49,10 @@ class SnappyBatch {
     uint32_t hdr = 0;
     int slot = 0;
     uint32_t ticket = 0;
+    SnappyDequant dq;     // fused decode (dq.values: the values buffer's pointer)
+    Buffer values;
+    bool* fused = nullptr;
+    int group = -1;       // streams decoded again together when one falls back
   };
   Context& c_;
   std::vector<Job> jobs_;

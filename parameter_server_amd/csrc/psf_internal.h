@@ -217,6 +217,19 @@ struct ZeroPair {
 size_t snappy_compress_batch_scratch(const SnappyCJob* jobs, int njobs);
 int snappy_compress_batch_launch(const SnappyCJob* jobs, int njobs, void* scratch, hipStream_t st,
                                  Profiler* prof, PubSlot* pub_base, const ZeroPair& z = ZeroPair{});
+// FIXING_FLOAT's decode fused into the uncompress (decode_batch, when a
+// COMPRESSING array's next decode is FIXING_FLOAT): the stream holds codes of
+// nb bytes (1 or 2), and `values` receives dsize / nb dequantised values
+// (fixing_float.h:89-101) with the bits ff_decode would give.  `out` still
+// receives the codes of any fragment the fast path does not place, so the
+// fallback kernels dequantise from there.
+struct SnappyDequant {
+  void* values = nullptr;        // null: no fused decode
+  int nb = 0;
+  int value_type = 0;            // kFloat / kDouble
+  const float* range = nullptr;  // device {min, max} left by the encode, or null: (mn, mx)
+  float mn = 0.f, mx = 0.f;
+};
 struct SnappyDJob {
   const void* in;
   size_t c;
@@ -225,7 +238,10 @@ struct SnappyDJob {
   void* out;
   int slot;
   uint32_t ticket;
+  SnappyDequant dq = {};
 };
+// whether an uncompress of dsize code bytes into `values` can take the fused decode
+bool snappy_dequant_ok(const SnappyDequant& dq, size_t dsize);
 size_t snappy_uncompress_batch_scratch(const SnappyDJob* jobs, int njobs);
 int snappy_uncompress_batch_launch(const SnappyDJob* jobs, int njobs, void* scratch, hipStream_t st,
                                    Profiler* prof, PubSlot* pub_base, const ZeroPair& z = ZeroPair{});

@@ -34,6 +34,7 @@
 // copies reach into an earlier fragment (never produced by a 1.1.8 encoder,
 // but valid) is decoded by one lane instead (K5).
 #include "psf_internal.h"
+#include "ff_dequant.h"
 
 namespace psf {
 namespace {
@@ -799,6 +800,12 @@ struct DJob {
   uint32_t hdr, nfo, nwin;
   uint32_t fo0, win0;  // first output fragment / window of this stream in the grids
   uint32_t slot, ticket;
+  // fused FIXING_FLOAT decode (SnappyDequant): values of the codes, or null
+  void* fv;
+  const float* frange;
+  double fratio;
+  float fmn, fmx;
+  uint32_t fnb, fdbl;
 };
 struct SnappyDJobs {
   DJob j[kSnappyBatchMax];
@@ -811,6 +818,7 @@ struct SnappyDJobs {
 struct DScr {
   uint32_t *flags, *ctr;
   uint64_t *wexit, *wtotal, *wentry, *woff, *fragpos, *specpos, *specend;
+  uint32_t *fdone;  // fused decode: fragment k's values written by K-spec (1) or still codes (0)
   uint32_t *bitmap, *cum;
 };
 __device__ __forceinline__ DScr dscr(const SnappyDJobs& J, const DJob& D, uint32_t i) {
@@ -824,7 +832,8 @@ __device__ __forceinline__ DScr dscr(const SnappyDJobs& J, const DJob& D, uint32
   S.fragpos = S.woff + (D.nwin + 1);
   S.specpos = S.fragpos + (D.nfo + 1);
   S.specend = S.specpos + (D.nfo + 1);
-  S.bitmap = reinterpret_cast<uint32_t*>(S.specend + (D.nfo + 1));
+  S.fdone = reinterpret_cast<uint32_t*>(S.specend + (D.nfo + 1));
+  S.bitmap = reinterpret_cast<uint32_t*>(S.specend + 2 * (D.nfo + 1));
   S.cum = S.bitmap + (size_t)(D.nwin + 1) * (kWin / 32);
   return S;
 }
@@ -838,6 +847,131 @@ __device__ __forceinline__ uint32_t djob_win(const SnappyDJobs& J, uint32_t b) {
   uint32_t i = 0;
   while (i + 1 < J.njobs && b >= J.j[i + 1].win0) ++i;
   return i;
+}
+
+// ---- FIXING_FLOAT decode fused into the uncompress (SnappyDequant) ----
+// A stream of FIXING_FLOAT codes whose next decode is FIXING_FLOAT is decoded
+// straight to values: where the fast path copies a stored fragment, it
+// dequantises it instead (the codes never reach HBM), and fragments placed any
+// other way are dequantised from their codes afterwards.  The arithmetic is
+// ff_decode's (ff_dequant.h), so the values are bit-identical to the unfused
+// chain.
+typedef float dq_f32x4 __attribute__((ext_vector_type(4)));
+typedef float dq_f32x2 __attribute__((ext_vector_type(2)));
+typedef double dq_f64x2 __attribute__((ext_vector_type(2)));
+
+struct DqParams {
+  double ratio, inv, bin, min_v;
+};
+// ff_decode's parameters for stream D (the encode's device range when it left one)
+__device__ __forceinline__ DqParams dq_params(const DJob& D) {
+  float mn = D.fmn, mx = D.fmx;
+  if (D.frange) {
+    mn = D.frange[0];
+    mx = D.frange[1];
+  }
+  DqParams P;
+  P.min_v = (double)mn;
+  P.bin = (double)mx - P.min_v;
+  P.ratio = D.fratio;
+  P.inv = 1.0 / P.ratio;
+  return P;
+}
+
+// nb = 1: the 256-entry table ff_decode builds (same formula, same bits)
+template <typename V>
+__device__ __forceinline__ void dq_lut(V* lut, const DqParams& P, uint32_t tid) {
+  lut[tid] = dequant<V>((uint64_t)tid, P.ratio, P.bin, P.min_v);
+}
+
+// the values of one dword of codes (4 / NB of them) to o, non-temporal
+template <typename V, int NB>
+__device__ __forceinline__ void dq_store(V* o, uint32_t w, const V* lut, const DqParams& P) {
+  if (NB == 1) {
+    const V x0 = lut[w & 255], x1 = lut[(w >> 8) & 255], x2 = lut[(w >> 16) & 255], x3 = lut[w >> 24];
+    if constexpr (sizeof(V) == 4) {
+      const dq_f32x4 t = {(float)x0, (float)x1, (float)x2, (float)x3};
+      __builtin_nontemporal_store(t, reinterpret_cast<dq_f32x4*>(o));
+    } else {
+      const dq_f64x2 a = {(double)x0, (double)x1}, b = {(double)x2, (double)x3};
+      __builtin_nontemporal_store(a, reinterpret_cast<dq_f64x2*>(o));
+      __builtin_nontemporal_store(b, reinterpret_cast<dq_f64x2*>(o) + 1);
+    }
+  } else {
+    const V x0 = dequant_q<V>(w & 0xFFFF, P.ratio, P.inv, P.bin, P.min_v);
+    const V x1 = dequant_q<V>(w >> 16, P.ratio, P.inv, P.bin, P.min_v);
+    if constexpr (sizeof(V) == 4) {
+      const dq_f32x2 t = {(float)x0, (float)x1};
+      __builtin_nontemporal_store(t, reinterpret_cast<dq_f32x2*>(o));
+    } else {
+      const dq_f64x2 t = {(double)x0, (double)x1};
+      __builtin_nontemporal_store(t, reinterpret_cast<dq_f64x2*>(o));
+    }
+  }
+}
+
+// v[0, len / NB) = the values of the codes s[0, len) (s at any alignment, v
+// 16-byte aligned, len a multiple of NB), by 256 lanes: lane l takes the
+// dwords of codes l, l + 256, ..., each funnel-shifted from the two aligned
+// dwords that cover it (the second lies inside the source whenever it is
+// needed), 8 in flight before any store.
+template <typename V, int NB>
+__device__ void dq_bytes(const uint8_t* __restrict__ s, V* __restrict__ v, uint32_t len, const V* lut,
+                         const DqParams& P, uint32_t tid) {
+  const uintptr_t sa = reinterpret_cast<uintptr_t>(s);
+  const uint32_t sh = (uint32_t)(sa & 3) * 8;
+  const uint32_t* a = reinterpret_cast<const uint32_t*>(sa & ~(uintptr_t)3);
+  const uint32_t ng = len >> 2;
+  constexpr int U = 8;
+  for (uint32_t g0 = 0; g0 < ng; g0 += U * 256) {
+    uint32_t w0[U], w1[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t g = min(g0 + u * 256 + tid, ng - 1);
+      w0[u] = a[g];
+      w1[u] = a[sh ? g + 1 : g];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t g = g0 + u * 256 + tid;
+      const uint32_t w = sh ? __builtin_amdgcn_alignbit(w1[u], w0[u], sh) : w0[u];
+      if (g < ng) dq_store<V, NB>(v + (size_t)g * (4 / NB), w, lut, P);
+    }
+  }
+  for (uint32_t i = (ng << 2) / NB + tid; i < len / NB; i += 256) {  // the array's last len % 4 bytes
+    uint32_t r = 0;
+    for (int j = 0; j < NB; ++j) r |= (uint32_t)s[i * NB + j] << (8 * j);
+    v[i] = NB == 1 ? lut[r] : dequant_q<V>(r, P.ratio, P.inv, P.bin, P.min_v);
+  }
+}
+
+// The workgroup's LDS table (nb = 1) for stream D; called by all 256 lanes,
+// ends with a barrier.
+__device__ __forceinline__ void dq_prepare(const DJob& D, double* lut64, uint32_t tid) {
+  const DqParams P = dq_params(D);
+  if (D.fnb == 1) {
+    if (D.fdbl) dq_lut<double>(lut64, P, tid);
+    else dq_lut<float>(reinterpret_cast<float*>(lut64), P, tid);
+  }
+  __syncthreads();
+}
+
+// Output fragment bytes [o0, o0 + len) of stream D, whose codes are at s, to
+// their values (after dq_prepare).
+__device__ __forceinline__ void dq_frag(const DJob& D, const uint8_t* s, uint64_t o0, uint32_t len,
+                                        const double* lut64, uint32_t tid) {
+  const DqParams P = dq_params(D);
+  const uint64_t first = o0 / D.fnb;  // 65536 is a multiple of nb
+  if (D.fdbl) {
+    double* v = static_cast<double*>(D.fv) + first;
+    if (D.fnb == 1) dq_bytes<double, 1>(s, v, len, lut64, P, tid);
+    else dq_bytes<double, 2>(s, v, len, lut64, P, tid);
+  } else {
+    float* v = static_cast<float*>(D.fv) + first;
+    const float* lut = reinterpret_cast<const float*>(lut64);
+    if (D.fnb == 1) dq_bytes<float, 1>(s, v, len, lut, P, tid);
+    else dq_bytes<float, 2>(s, v, len, lut, P, tid);
+  }
 }
 
 // K0: link the chain directly when the stream is mostly 64 KiB fragments
@@ -1015,6 +1149,7 @@ __device__ uint64_t decode_few(const uint8_t* __restrict__ in, uint64_t C, uint6
 // position differs from the one assumed here (specpos).
 __global__ __launch_bounds__(256) void snappy_dspec(const SnappyDJobs J) {
   __shared__ uint32_t s_last, s_checked;
+  __shared__ double s_lut[256];  // fused decode, nb = 1
   const uint32_t tid = threadIdx.x;
   if (blockIdx.x >= J.nfo1) {  // one more workgroup per stream links it meanwhile (K0), needed or not
     const uint32_t i = blockIdx.x - J.nfo1;
@@ -1067,8 +1202,15 @@ __global__ __launch_bounds__(256) void snappy_dspec(const SnappyDJobs J) {
     if (s_best != 0xffffffffu) at = p + (int32_t)(s_best & 511) - 128;
   }
   uint64_t e = kNone;  // where this fragment's tags end
+  uint32_t vdone = 0;   // fused decode: this fragment's values written here
   if (at != kNone) {
-    copy_g2g(out + o0, in + at + hl, end, tid);
+    if (D.fv) {
+      dq_prepare(D, s_lut, tid);
+      dq_frag(D, in + at + hl, o0, end, s_lut, tid);
+      vdone = 1;
+    } else {
+      copy_g2g(out + o0, in + at + hl, end, tid);
+    }
     e = at + hl + end;
   } else if (end && (k > 0 || header_matches(in, C, hdr, dsize))) {
     // not stored: a fragment with a few tags, right after stored ones that
@@ -1076,7 +1218,14 @@ __global__ __launch_bounds__(256) void snappy_dspec(const SnappyDJobs J) {
     // decoded here too
     __shared__ FewLds F;
     e = decode_few(in, C, p, end, out + o0, tid, F);
-    if (e != kNone) at = p;
+    if (e != kNone) {
+      at = p;
+      if (D.fv) {  // the codes just written (L2-hot) to their values (decode_few ends with a barrier)
+        dq_prepare(D, s_lut, tid);
+        dq_frag(D, out + o0, o0, end, s_lut, tid);
+        vdone = 1;
+      }
+    }
   } else if (ok) {
     e = C;  // the empty output: the header is the stream
   }
@@ -1084,6 +1233,7 @@ __global__ __launch_bounds__(256) void snappy_dspec(const SnappyDJobs J) {
   if (tid == 0) {
     __hip_atomic_store(&specpos[k], at, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(&S.specend[k], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    S.fdone[k] = vdone;  // read by K4 (a later launch)
   }
   // one counter for both: workgroups done (high word) and fragments placed
   const bool placed = e != kNone;
@@ -1373,21 +1523,20 @@ __device__ void literal_to_lds(uint8_t* ob, uint32_t o, const uint8_t* __restric
 }
 
 // K5 body: the verdict; one-lane decode of valid streams K4 could not split
-__device__ void dfinish_body(const uint8_t* __restrict__ in, uint64_t C, uint32_t hdr, uint64_t dsize, uint32_t f,
-                             uint8_t* __restrict__ out, PubSlot* pub, uint32_t ticket) {
-  if (f == kFlagSerial) {
-    uint64_t p = hdr, o = 0;
-    while (p < C) {
-      const Tag t = decode_tag(tag_bytes(in, C, p), p);
-      if (t.lit) {
-        for (uint64_t i = 0; i < t.len; ++i) out[o + i] = in[p + t.hl + i];
-      } else {
-        for (uint64_t i = 0; i < t.len; ++i) out[o + i] = out[o - t.off + i];
-      }
-      o += t.len;
-      p = t.next;
+__device__ void dserial_body(const uint8_t* __restrict__ in, uint64_t C, uint32_t hdr, uint8_t* __restrict__ out) {
+  uint64_t p = hdr, o = 0;
+  while (p < C) {
+    const Tag t = decode_tag(tag_bytes(in, C, p), p);
+    if (t.lit) {
+      for (uint64_t i = 0; i < t.len; ++i) out[o + i] = in[p + t.hl + i];
+    } else {
+      for (uint64_t i = 0; i < t.len; ++i) out[o + i] = out[o - t.off + i];
     }
+    o += t.len;
+    p = t.next;
   }
+}
+__device__ void dverdict(uint32_t f, uint64_t dsize, PubSlot* pub, uint32_t ticket) {
   if (pub) {
     pub->status = (f & kFlagHeader) ? kErrHeaderHint : (f & kFlagInvalid) ? kErrCheck : kOk;
     pub->size = dsize;
@@ -1405,28 +1554,36 @@ __global__ __launch_bounds__(256) void snappy_dfrag(const SnappyDJobs J) {
   __shared__ uint32_t ib32[(kInWin + 32) / 4];
   __shared__ uint32_t s_last;
   __shared__ FewLds F;
+  __shared__ double s_lut[256];  // fused decode, nb = 1
   if (J.znext)
     for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < J.zwords; i += gridDim.x * 256) J.znext[i] = 0;
   const uint32_t ji = djob_frag(J, blockIdx.x);
   const DJob& D = J.j[ji];
   const DScr S = dscr(J, D, ji);
   const uint32_t* __restrict__ flags = S.flags;
-  if (flags[2]) return;  // K-spec decoded the whole stream and gave the verdict
   const uint8_t* __restrict__ in = D.in;
   uint8_t* __restrict__ out = D.out;
   const uint64_t C = D.C, dsize = D.dsize;
   const uint32_t hdr = D.hdr, ticket = D.ticket;
+  const uint32_t tid = threadIdx.x, k = blockIdx.x - D.fo0;
+  const uint64_t o0 = (uint64_t)k * kFrag;
+  const uint32_t end = (uint32_t)min((uint64_t)kFrag, dsize - o0);
+  if (flags[2]) {  // K-spec decoded the whole stream and gave the verdict
+    if (D.fv && end && !S.fdone[k]) {  // a fragment it placed as codes: their values
+      dq_prepare(D, s_lut, tid);
+      dq_frag(D, out + o0, o0, end, s_lut, tid);
+    }
+    return;
+  }
   const uint64_t* __restrict__ fragpos = S.fragpos;
   const uint64_t* __restrict__ specpos = S.specpos;
   PubSlot* pub = J.pub ? J.pub + D.slot : nullptr;
   const uint32_t f = flags[0];
   uint8_t* ob = reinterpret_cast<uint8_t*>(ob32);
-  const uint32_t tid = threadIdx.x, k = blockIdx.x - D.fo0;
-  const uint64_t o0 = (uint64_t)k * kFrag;
-  const uint32_t end = (uint32_t)min((uint64_t)kFrag, dsize - o0);
   PSF_DTRACE(k, 0);
   const uint64_t p0 = end ? fragpos[k] : kNone;
-  if (f == 0 && end && p0 != specpos[k]) {
+  const bool redo = f == 0 && end && p0 != specpos[k];
+  if (redo) {
     PSF_DTRACE(k, 1);
     const Tag t0 = decode_tag(tag_bytes(in, C, p0), p0);
     if (decode_few(in, C, p0, end, out + o0, tid, F) != kNone) {
@@ -1480,8 +1637,23 @@ __global__ __launch_bounds__(256) void snappy_dfrag(const SnappyDJobs J) {
       }
     }
   }
+  if (D.fv && f == 0 && end && (redo || !S.fdone[k])) {  // values of the codes placed here or by K-spec
+    __syncthreads();
+    dq_prepare(D, s_lut, tid);
+    dq_frag(D, out + o0, o0, end, s_lut, tid);
+  }
   PSF_DTRACE(k, 2);
-  if (last_block(S.ctr + 2, D.nfo ? D.nfo : 1, &s_last) && tid == 0) dfinish_body(in, C, hdr, dsize, f, out, pub, ticket);
+  if (!last_block(S.ctr + 2, D.nfo ? D.nfo : 1, &s_last)) return;
+  if (f == kFlagSerial) {
+    if (tid == 0) dserial_body(in, C, hdr, out);
+    if (D.fv) {
+      __syncthreads();
+      dq_prepare(D, s_lut, tid);
+      for (uint64_t o = 0; o < dsize; o += kFrag) dq_frag(D, out + o, o, (uint32_t)min((uint64_t)kFrag, dsize - o), s_lut, tid);
+    }
+    __syncthreads();
+  }
+  if (tid == 0) dverdict(f, dsize, pub, ticket);
 }
 
 }  // namespace
@@ -1560,13 +1732,18 @@ static size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 static size_t djob_bytes(size_t C, size_t dsize) {
   const size_t nwin = (C + kWin - 1) / kWin + 1;
   const size_t nfo = (dsize + kFrag - 1) / kFrag + 1;
-  return align256(nwin * (kWin / 8) + C * 4 + nwin * 8 * (2 * kStarts + 2) + 3 * nfo * 8 + 64);
+  return align256(nwin * (kWin / 8) + C * 4 + nwin * 8 * (2 * kStarts + 2) + 4 * nfo * 8 + 64);
 }
 
 size_t snappy_uncompress_batch_scratch(const SnappyDJob* jobs, int njobs) {
   size_t b = align256((size_t)njobs * 32 + 4);
   for (int i = 0; i < njobs; ++i) b += djob_bytes(jobs[i].c, jobs[i].dsize);
   return b;
+}
+
+bool snappy_dequant_ok(const SnappyDequant& dq, size_t dsize) {
+  return dq.values && (dq.nb == 1 || dq.nb == 2) && (dq.value_type == kFloat || dq.value_type == kDouble) &&
+         dsize > 0 && dsize % (size_t)dq.nb == 0 && (reinterpret_cast<uintptr_t>(dq.values) & 15) == 0;
 }
 
 size_t snappy_uncompress_scratch(size_t C, size_t dsize) { return align256(32 + 4) + djob_bytes(C, dsize); }
@@ -1601,10 +1778,21 @@ int snappy_uncompress_batch_launch(const SnappyDJob* jobs, int njobs, void* scra
     D.win0 = K.nwin;
     D.slot = (uint32_t)q.slot;
     D.ticket = q.ticket;
+    if (q.dq.values) {
+      if (!snappy_dequant_ok(q.dq, q.dsize)) return kErrArg;
+      D.fv = q.dq.values;
+      D.frange = q.dq.range;
+      D.fratio = ff_ratio(q.dq.nb);
+      D.fmn = q.dq.mn;
+      D.fmx = q.dq.mx;
+      D.fnb = (uint32_t)q.dq.nb;
+      D.fdbl = q.dq.value_type == kDouble ? 1u : 0u;
+    }
     K.nfo1 += D.nfo ? D.nfo : 1;  // an empty output still takes one workgroup (header check, verdict)
     K.nwin += D.nwin;
     data += djob_bytes(q.c, q.dsize);
-    bytes += (double)q.c + (double)q.dsize;
+    bytes += (double)q.c +
+             (q.dq.values ? (double)(q.dsize / q.dq.nb) * (q.dq.value_type == kDouble ? 8 : 4) : (double)q.dsize);
   }
   const size_t zneed = (size_t)njobs * 32 + 4;
   if (z.cur && zneed <= z.bytes) {  // the context's region the previous launch cleared
