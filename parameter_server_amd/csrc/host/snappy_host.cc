@@ -3,7 +3,10 @@
 // (reference src/util/shared_array_inl.h:232-255).
 #include "snappy_host.h"
 
+#include <sched.h>
+
 #include <algorithm>
+#include <string>
 
 namespace psf {
 
@@ -120,6 +123,7 @@ void SnappyBatch::launch(size_t b, size_t e) {
     const bool comp = pass == 0;
     std::vector<SnappyCJob> cj;
     std::vector<SnappyDJob> dj;
+    std::vector<size_t> di;  // dj's jobs_ indices
     auto go = [&] {
       int st = kOk;
       if (comp && !cj.empty()) {
@@ -130,10 +134,22 @@ void SnappyBatch::launch(size_t b, size_t e) {
                                           c_.pub_dev(0), c_.zero_pair(Context::kZeroCompress, nfrag * 8 + 8));
         cj.clear();
       } else if (!comp && !dj.empty()) {
-        Buffer scratch = c_.alloc(snappy_uncompress_batch_scratch(dj.data(), (int)dj.size()));
-        st = snappy_uncompress_batch_launch(dj.data(), (int)dj.size(), scratch.ptr, c_.stream(), c_.prof(),
-                                            c_.pub_dev(0), c_.zero_pair(Context::kZeroUncompress, dj.size() * 32 + 4));
+        Tail t;
+        t.scratch = c_.alloc(snappy_uncompress_batch_scratch(dj.data(), (int)dj.size()));
+        // the context's pre-zeroed control region serves the first batch
+        // only: a later batch's fast path would clear it for the next launch
+        // while this batch's tail may still need it
+        const ZeroPair z = tails_.empty() ? c_.zero_pair(Context::kZeroUncompress, dj.size() * 32 + 4) : ZeroPair{};
+        st = snappy_uncompress_batch_launch(dj.data(), (int)dj.size(), t.scratch.ptr, c_.stream(), c_.prof(),
+                                            c_.pub_dev(0), z, &t.t);
+        if (st == kOk) {
+          t.done = c_.take_event();
+          PSF_HIP_CHECK(hipEventRecord(t.done, c_.stream()));
+          t.jobs = di;
+          tails_.push_back(std::move(t));
+        }
         dj.clear();
+        di.clear();
       }
       if (st != kOk) throw CheckError(st, comp ? "snappy compress launch failed" : "snappy uncompress launch failed");
     };
@@ -141,7 +157,10 @@ void SnappyBatch::launch(size_t b, size_t e) {
       Job& j = jobs_[i];
       if (j.compress != comp) continue;
       if (comp) cj.push_back(SnappyCJob{j.in.ptr, j.in.bytes, j.out.ptr, j.slot, j.ticket});
-      else dj.push_back(SnappyDJob{j.in.ptr, j.in.bytes, j.hdr, j.out.bytes, j.out.ptr, j.slot, j.ticket, j.dq});
+      else {
+        dj.push_back(SnappyDJob{j.in.ptr, j.in.bytes, j.hdr, j.out.bytes, j.out.ptr, j.slot, j.ticket, j.dq});
+        di.push_back(i);
+      }
       if (cj.size() == (size_t)kSnappyBatchMax || dj.size() == (size_t)kSnappyBatchMax) go();
     }
     go();
@@ -155,6 +174,40 @@ void SnappyBatch::launch_all() {
 
 void SnappyBatch::finish() {
   launch_all();
+  // uncompress batches: once the fast path has completed, the tail kernels
+  // run only if a stream has not published its verdict (on FIXING_FLOAT
+  // codes and other stored streams the fast path decodes everything)
+  for (Tail& t : tails_) {
+    // every verdict published (the fast path's last workgroups publish while
+    // the rest of its grid drains), or the fast path complete without them
+    auto published = [&] {
+      for (size_t i : t.jobs) {
+        const Job& j = jobs_[i];
+        if (__atomic_load_n(&c_.pub_host(j.slot)->ticket, __ATOMIC_ACQUIRE) != j.ticket) return false;
+      }
+      return true;
+    };
+    bool all = published();
+    if (!all) {
+      WaitTimer wt(&c_, Context::kWaitPublish);
+      for (uint64_t spin = 0;; ++spin) {
+        if ((all = published())) break;
+        const hipError_t q = hipEventQuery(t.done);
+        if (q == hipSuccess) {
+          all = published();
+          break;
+        }
+        if (q != hipErrorNotReady) throw CheckError(kErrHip, std::string("stream failed: ") + hipGetErrorString(q));
+        if (spin > 4096) sched_yield();
+      }
+    }
+    c_.give_event(t.done);
+    if (!all) {
+      const int st = snappy_uncompress_tail_launch(&t.t, c_.stream());
+      if (st != kOk) throw CheckError(st, "snappy uncompress launch failed");
+    }
+  }
+  tails_.clear();  // (scratch freed stream-ordered, after the tails)
   int bad = kOk;
   // a fused stream whose header disagrees with its hint: every fused stream of
   // its group (one message's arrays) is decoded again unfused, so the

@@ -54,8 +54,17 @@ class SnappyBatch {
     bool* fused = nullptr;
     int group = -1;       // streams decoded again together when one falls back
   };
+  // an uncompress batch launched with its fast path only (SnappyTail): the
+  // rest is launched at finish() unless every stream published its verdict
+  struct Tail {
+    SnappyTail t;
+    hipEvent_t done = nullptr;  // recorded after the fast path
+    std::vector<size_t> jobs;
+    Buffer scratch;             // alive until the tail has been launched
+  };
   Context& c_;
   std::vector<Job> jobs_;
+  std::vector<Tail> tails_;
   size_t launched_ = 0;  // jobs_[0, launched_) are in flight
   void prepare_uncompress(Job& j, const Buffer& src, uint32_t hdr, uint64_t dsize);
   void launch(size_t b, size_t e);

@@ -5,6 +5,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <memory>
+
 namespace psf {
 
 constexpr int kBlock = 256;     // 4 waves of 64
@@ -243,8 +245,21 @@ struct SnappyDJob {
 // whether an uncompress of dsize code bytes into `values` can take the fused decode
 bool snappy_dequant_ok(const SnappyDequant& dq, size_t dsize);
 size_t snappy_uncompress_batch_scratch(const SnappyDJob* jobs, int njobs);
+// The kernels after the fast path (window scan / link / index, fragment
+// decode, verdict) of one launched batch; they find nothing to do on streams
+// the fast path decoded whole, which then published their verdict already.
+struct SnappyTail {
+  std::shared_ptr<void> jobs;  // the batch's job table (kernel arguments)
+  bool pending = false;        // launched fast path, tail not launched yet
+};
+// tail != null: launch the fast path only and leave the rest in *tail for
+// snappy_uncompress_tail_launch -- to be called (before any other uncompress
+// launch with a ZeroPair on this stream) unless every stream of the batch has
+// published its ticket once the fast path has completed
 int snappy_uncompress_batch_launch(const SnappyDJob* jobs, int njobs, void* scratch, hipStream_t st,
-                                   Profiler* prof, PubSlot* pub_base, const ZeroPair& z = ZeroPair{});
+                                   Profiler* prof, PubSlot* pub_base, const ZeroPair& z = ZeroPair{},
+                                   SnappyTail* tail = nullptr);
+int snappy_uncompress_tail_launch(SnappyTail* tail, hipStream_t st);
 
 // spill.hip: gather `n` copies (sorted by chunk0) into one send buffer; copy i
 // moves len bytes from src to dst + dst_off and owns chunks

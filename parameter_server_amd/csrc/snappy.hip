@@ -812,7 +812,7 @@ struct SnappyDJobs {
   uint32_t* ctrl;  // 8 words per stream: flags[0..3] (verdict, indexed, decoded by K-spec), counters[4..7]
   PubSlot* pub;
   uint32_t njobs, nfo1, nwin;  // streams; output fragments (at least one per stream); windows
-  uint32_t* znext;  // the next launch's zeroed ctrl region (null: none), cleared by K4
+  uint32_t* znext;  // the next launch's zeroed ctrl region (null: none), cleared by K-spec
   uint32_t zwords;
 };
 struct DScr {
@@ -1151,14 +1151,17 @@ __global__ __launch_bounds__(256) void snappy_dspec(const SnappyDJobs J) {
   __shared__ uint32_t s_last, s_checked;
   __shared__ double s_lut[256];  // fused decode, nb = 1
   const uint32_t tid = threadIdx.x;
-  if (blockIdx.x >= J.nfo1) {  // one more workgroup per stream links it meanwhile (K0), needed or not
-    const uint32_t i = blockIdx.x - J.nfo1;
+  if (J.znext)  // the next launch's control words (this launch's were cleared by the one before)
+    for (uint32_t i = blockIdx.x * 256 + tid; i < J.zwords; i += gridDim.x * 256) J.znext[i] = 0;
+  if (blockIdx.x < J.njobs) {  // one more workgroup per stream links it meanwhile (K0), needed or not
+    const uint32_t i = blockIdx.x;  // dispatched first: its walk overlaps the copies
     const DJob& D = J.j[i];
     const DScr S = dscr(J, D, i);
     if (tid < 64) dlit_body(D.in, D.C, D.hdr, D.dsize, D.nwin, S.wentry, S.woff, S.fragpos, S.flags, tid);
     return;
   }
-  const uint32_t ji = djob_frag(J, blockIdx.x);
+  const uint32_t b = blockIdx.x - J.njobs;
+  const uint32_t ji = djob_frag(J, b);
   const DJob& D = J.j[ji];
   const DScr S = dscr(J, D, ji);
   const uint8_t* __restrict__ in = D.in;
@@ -1169,7 +1172,7 @@ __global__ __launch_bounds__(256) void snappy_dspec(const SnappyDJobs J) {
   uint32_t* __restrict__ flags = S.flags;
   uint32_t* __restrict__ ctr = S.ctr;
   PubSlot* pub = J.pub ? J.pub + D.slot : nullptr;
-  const uint32_t k = blockIdx.x - D.fo0, nspec = nfo ? nfo : 1;
+  const uint32_t k = b - D.fo0, nspec = nfo ? nfo : 1;
   const uint64_t o0 = (uint64_t)k * kFrag;
   const uint32_t end = (uint32_t)min((uint64_t)kFrag, dsize - o0);  // 0 only for an empty output
   const uint64_t p = hdr + (uint64_t)k * kFullLit;
@@ -1182,6 +1185,7 @@ __global__ __launch_bounds__(256) void snappy_dspec(const SnappyDJobs J) {
     const Tag t = decode_tag(tag_bytes(in, C, p), p);
     ok = ok && p < C && t.lit && t.len == end && t.hl == hl && t.next <= C && (k + 1 < nfo || t.next == C);
   }
+  if (D.fv) dq_prepare(D, s_lut, tid);  // the range load overlaps the tag's
   // A fragment after one that is not stored (a 1.1.8 encoder found a match in
   // it) sits a few bytes off its assumed place: look for its literal within
   // +-128 bytes and copy it from there too.  That is a guess only (it does not
@@ -1205,7 +1209,6 @@ __global__ __launch_bounds__(256) void snappy_dspec(const SnappyDJobs J) {
   uint32_t vdone = 0;   // fused decode: this fragment's values written here
   if (at != kNone) {
     if (D.fv) {
-      dq_prepare(D, s_lut, tid);
       dq_frag(D, in + at + hl, o0, end, s_lut, tid);
       vdone = 1;
     } else {
@@ -1221,7 +1224,6 @@ __global__ __launch_bounds__(256) void snappy_dspec(const SnappyDJobs J) {
     if (e != kNone) {
       at = p;
       if (D.fv) {  // the codes just written (L2-hot) to their values (decode_few ends with a barrier)
-        dq_prepare(D, s_lut, tid);
         dq_frag(D, out + o0, o0, end, s_lut, tid);
         vdone = 1;
       }
@@ -1555,8 +1557,6 @@ __global__ __launch_bounds__(256) void snappy_dfrag(const SnappyDJobs J) {
   __shared__ uint32_t s_last;
   __shared__ FewLds F;
   __shared__ double s_lut[256];  // fused decode, nb = 1
-  if (J.znext)
-    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < J.zwords; i += gridDim.x * 256) J.znext[i] = 0;
   const uint32_t ji = djob_frag(J, blockIdx.x);
   const DJob& D = J.j[ji];
   const DScr S = dscr(J, D, ji);
@@ -1752,8 +1752,10 @@ size_t snappy_uncompress_scratch(size_t C, size_t dsize) { return align256(32 + 
 // stream), K1-K3 (one persistent launch), K4 (+ K5 in each stream's last
 // workgroup).  On streams
 // of stored fragments K-spec decodes everything and the others return at once.
+static int launch_tail(const SnappyDJobs& K, hipStream_t st);
+
 int snappy_uncompress_batch_launch(const SnappyDJob* jobs, int njobs, void* scratch, hipStream_t st,
-                                   Profiler* prof, PubSlot* pub_base, const ZeroPair& z) {
+                                   Profiler* prof, PubSlot* pub_base, const ZeroPair& z, SnappyTail* tail) {
   if (njobs <= 0 || njobs > kSnappyBatchMax) return kErrArg;
   SnappyDJobs K{};
   uint8_t* s = static_cast<uint8_t*>(scratch);
@@ -1802,8 +1804,23 @@ int snappy_uncompress_batch_launch(const SnappyDJob* jobs, int njobs, void* scra
   } else if (hipMemsetAsync(K.ctrl, 0, zneed, st) != hipSuccess) {
     return kErrHip;
   }
+  if (tail) {
+    std::shared_ptr<SnappyDJobs> keep = std::make_shared<SnappyDJobs>(K);
+    {
+      ProfScope ps(prof, kKSnappyDecompress, st, bytes);
+      hipLaunchKernelGGL(snappy_dspec, dim3(K.nfo1 + K.njobs), dim3(256), 0, st, K);
+    }
+    tail->jobs = keep;
+    tail->pending = true;
+    return launch_status();
+  }
   ProfScope ps(prof, kKSnappyDecompress, st, bytes);
   hipLaunchKernelGGL(snappy_dspec, dim3(K.nfo1 + K.njobs), dim3(256), 0, st, K);
+  return launch_tail(K, st);
+}
+
+// K1-K3 and K4 (+ K5) of a batch whose fast path has run
+static int launch_tail(const SnappyDJobs& K, hipStream_t st) {
   if (K.nwin) {
     // every workgroup of the persistent launch resident at once: 8 per CU
     // (18 KiB of LDS and one wave each: a CU's LDS holds 8)
@@ -1816,6 +1833,15 @@ int snappy_uncompress_batch_launch(const SnappyDJob* jobs, int njobs, void* scra
   }
   hipLaunchKernelGGL(snappy_dfrag, dim3(K.nfo1), dim3(256), 0, st, K);
   return launch_status();
+}
+
+// (not bracketed by the profiler: the batch's bytes were counted with its fast
+// path, whose launch the bench times)
+int snappy_uncompress_tail_launch(SnappyTail* tail, hipStream_t st) {
+  if (!tail || !tail->pending || !tail->jobs) return kErrArg;
+  tail->pending = false;
+  const SnappyDJobs& K = *static_cast<const SnappyDJobs*>(tail->jobs.get());
+  return launch_tail(K, st);
 }
 
 int snappy_uncompress_launch(const void* in, size_t C, uint32_t hdr, size_t dsize, void* out, void* scratch,
