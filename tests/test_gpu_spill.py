@@ -108,15 +108,17 @@ def test_push_router_64_streams_8_servers():
         _check_step(F, router.results(), ranges, M, 1, port, expect)
 
 
-def test_c5_rows_dim128_full_chain_8_servers():
-    """C5's shape: 2^14 keys x 128 f32, EvenDivide(8) slices (k = 128),
-    [KEY_CACHING, FIXING_FLOAT nb=1, COMPRESSING]."""
+@pytest.mark.parametrize("M", [1 << 14, (1 << 16) + 4099])
+def test_c5_rows_dim128_full_chain_8_servers(M):
+    """C5's shape: M keys x 128 f32, EvenDivide(8) slices (k = 128),
+    [KEY_CACHING, FIXING_FLOAT nb=1, COMPRESSING]; the larger M gives slices of
+    several fragments with a ragged last one."""
     import torch
 
     import oracle
     from parameter_server_amd import filter as F
     from parameter_server_amd import shard
-    M, DIM, S = 1 << 14, 128, 8
+    DIM, S = 128, 8
     F.set_clock(SEED)
     ctx = F.Context(0)
     ranges = shard.server_ranges(S)
@@ -146,8 +148,8 @@ def test_c5_rows_dim128_full_chain_8_servers():
                 assert not has_key and kn == 0
 
 
-@pytest.mark.parametrize("dim,compress", [(1, False), (128, True)])
-def test_router_multi_step_driver(dim, compress):
+@pytest.mark.parametrize("dim,compress,m", [(1, False, 1 << 12), (128, True, 1 << 12), (128, True, (1 << 16) + 77)])
+def test_router_multi_step_driver(dim, compress, m):
     """psf_router_step over several steps in one call (what bench.py times):
     each step's slicing pass is queued ahead of the previous step's decodes
     and the COMPRESSING lengths are waited for after it; the last step's
@@ -158,7 +160,7 @@ def test_router_multi_step_driver(dim, compress):
     import oracle
     from parameter_server_amd import filter as F
     from parameter_server_amd import shard
-    STREAMS, M, S = (16, 1 << 12, 8) if dim == 1 else (1, 1 << 12, 8)
+    STREAMS, M, S = (16, m, 8) if dim == 1 else (1, m, 8)
     F.set_clock(SEED)
     ctx = F.Context(0)
     ranges = shard.server_ranges(S)
