@@ -6,10 +6,11 @@
 set -e
 cd "$(dirname "$0")/.."
 python -m parameter_server_amd.build > /dev/null
-OBJS=$(ls parameter_server_amd/build/*.o | grep -v ff_codec)
+SRCF=${SRC:-parameter_server_amd/csrc/ff_codec.hip}
+OBJS=$(ls parameter_server_amd/build/*.o | grep -v "/$(basename $SRCF).o$")
 name=$1; shift
 mkdir -p tools/variants/$name
 /opt/rocm/bin/hipcc -x hip --offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -Iinclude -Iparameter_server_amd/csrc "$@" \
-  -c ${SRC:-parameter_server_amd/csrc/ff_codec.hip} -o tools/variants/$name/ff_codec.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o tools/variants/$name/libpsf.so $OBJS tools/variants/$name/ff_codec.o
+  -c $SRCF -o tools/variants/$name/variant.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o tools/variants/$name/libpsf.so $OBJS tools/variants/$name/variant.o
 echo tools/variants/$name/libpsf.so
