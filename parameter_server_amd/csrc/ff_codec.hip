@@ -1395,6 +1395,17 @@ static_assert(kBatchMinmaxGrid <= 0xFFFF, "FfJob::mm_nwg is 16 bits");
 #define PSF_BATCH_DEC_TPW 1  // one tile per workgroup measured best for decode
 #endif
 constexpr size_t kBatchMmTpw = PSF_BATCH_MM_TPW, kBatchEncTpw = PSF_BATCH_ENC_TPW, kBatchDecTpw = PSF_BATCH_DEC_TPW;
+// at most this many min/max workgroups per array: every encode workgroup of
+// the array folds all of its partials before it quantises, so a few large
+// arrays (C5: 8 x 2^24 values, 1024 partials each from the 8192 grid) pay for
+// the fold in every one of their ~2048 encode workgroups (C5, tools/ab_ff.sh:
+// 128 per array gives encode 116 us against 131 at 1024, min/max 84 -- the
+// 1024-workgroup total the single-array kernel uses for one 1 GiB array; C4's
+// 512 small arrays get 16 each and are unaffected)
+#ifndef PSF_BATCH_MM_PER_ARRAY
+#define PSF_BATCH_MM_PER_ARRAY 128
+#endif
+constexpr uint32_t kBatchMmPerArray = PSF_BATCH_MM_PER_ARRAY;
 
 // Workgroups of one array in a batched launch: its share (by tiles) of the
 // grid the single-array kernel would use, at least one.  A batch of large
@@ -1482,6 +1493,7 @@ static int encode_batch_cap(int value_type, int nb, const FfArray* arrs, int cou
     uint32_t mm_nwg =
         (a.preset.has_min && a.preset.has_max) ? 0u : (uint32_t)share_grid(a.n, tiles_mm, kBatchMinmaxGrid);
     if (mm_nwg > 1) mm_nwg = std::min<uint32_t>(mm_nwg, (uint32_t)((tiles_of(a.n) + kBatchMmTpw - 1) / kBatchMmTpw));
+    mm_nwg = std::min(mm_nwg, kBatchMmPerArray);
     J.mm_nwg = (uint16_t)mm_nwg;
     B.mm_first[i] = mm;
     mm += mm_nwg;
