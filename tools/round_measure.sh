@@ -20,6 +20,13 @@ timeout -k 10 300 python bench.py --config c5 --compress > $O/bench_c5_compress.
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/prof_c2 -o run -- python3 $R/bench.py --no-cpu-baseline --steps 20 --warmup 3 > $R/$O/prof_c2.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/prof_c4 -o run -- python3 $R/bench.py --config c4 --no-cpu-baseline --steps 20 --warmup 3 > $R/$O/prof_c4.log 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/prof_c5z -o run -- python3 $R/bench.py --config c5 --compress --no-cpu-baseline --steps 20 --warmup 3 > $R/$O/prof_c5z.log 2>&1 || exit $?
 timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/$O/pmc_c4_fetch -o run -- python3 $R/bench.py --config c4 --no-cpu-baseline --no-profile --steps 5 --warmup 1 > $R/$O/pmc_c4_fetch.log 2>&1 || exit $?
 timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/$O/pmc_c4_write -o run -- python3 $R/bench.py --config c4 --no-cpu-baseline --no-profile --steps 5 --warmup 1 > $R/$O/pmc_c4_write.log 2>&1 || exit $?
+timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/$O/pmc_c5z_fetch -o run -- python3 $R/bench.py --config c5 --compress --no-cpu-baseline --no-profile --steps 5 --warmup 1 > $R/$O/pmc_c5z_fetch.log 2>&1 || exit $?
+timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/$O/pmc_c5z_write -o run -- python3 $R/bench.py --config c5 --compress --no-cpu-baseline --no-profile --steps 5 --warmup 1 > $R/$O/pmc_c5z_write.log 2>&1 || exit $?
+cd $R
+if [ -f tools/variants/hprof/libpsf.so ]; then
+  timeout -k 10 150 python tools/host_prof.py > $O/hprof_c1.txt 2>&1 || exit $?
+fi
 echo done
