@@ -6,10 +6,12 @@ this package.
 Parity status: the reference's filter path cannot be built in this image (it
 needs glog, gflags, Eigen, the protobuf runtime and protoc-generated code;
 SURVEY.md §8(c)), and its own tests hold no vectors for this path
-(src/test/fixing_float_test.cc is stale and asserts nothing).  So apart from
-CRC32C the oracle is a restatement, and parity is UNPINNED by the reference
-for FIXING_FLOAT, KEY_CACHING's state machine, COMPRESSING's glue and NOISE
-(DESIGN.md §3).  What is here:
+(src/test/fixing_float_test.cc is stale and asserts nothing).  CRC32C is pinned
+to the reference's own crc32c.cc, COMPRESSING's codec to snappy 1.1.8 and
+NOISE's draws to libstdc++ (the libraries the reference calls); the rest is a
+restatement, and parity is UNPINNED by the reference for FIXING_FLOAT,
+KEY_CACHING's state machine and COMPRESSING's glue.  What is
+here:
 
 * ``Port`` -- ``oracle/psf_port.c`` + ``snappy_port.c``: a plain-C restatement
   of the reference's codec arithmetic (FIXING_FLOAT fixing_float.h:18-101,
@@ -22,6 +24,9 @@ for FIXING_FLOAT, KEY_CACHING's state machine, COMPRESSING's glue and NOISE
 * ``RefCrc32c`` -- ``oracle/_ref/libcrc32c_ref.so``: the reference's own
   src/util/crc32c.cc compiled from /root/reference (it needs nothing else):
   pins CRC32C, KEY_CACHING's signature, against the reference itself.
+* ``NoiseStd`` -- ``oracle/_port/libnoise_std.so`` (noise_std.cc): NOISE's
+  two libstdc++ calls (std::default_random_engine, std::normal_distribution)
+  made as add_noise.h:29-39 makes them, with the reference's flags.
 * ``slicing`` -- SliceKOFVMessage / EvenDivide restated in numpy.
 """
 from __future__ import annotations
@@ -35,6 +40,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 PORT_SO = os.path.join(HERE, "_port", "libpsf_port.so")
 CRC_REF_SO = os.path.join(HERE, "_ref", "libcrc32c_ref.so")
+NOISE_STD_SO = os.path.join(HERE, "_port", "libnoise_std.so")
 
 DT_FLOAT, DT_DOUBLE = 9, 10
 KEY_CACHING, COMPRESSING, FIXING_FLOAT, NOISE = 1, 2, 3, 4
@@ -299,3 +305,21 @@ class Snappy118:
 
     snappy_compress = compress      # Port's names
     snappy_uncompress = uncompress
+
+
+class NoiseStd:
+    """ctypes view of oracle/_port/libnoise_std.so: AddNoise through libstdc++'s
+    own engine and distribution (add_noise.h:29-39)."""
+
+    def __init__(self, path: str = NOISE_STD_SO):
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"{path} (build with `make -C oracle port`)")
+        self.lib = C.CDLL(path)
+        self.lib.noise_std.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.c_float, C.c_float]
+        self.lib.noise_std.restype = C.c_int
+
+    def add_noise(self, x: np.ndarray, mean: float, sd: float) -> np.ndarray:
+        y = np.array(x, copy=True)
+        dt = DT_FLOAT if y.dtype == np.float32 else DT_DOUBLE
+        assert self.lib.noise_std(_ptr(y), y.size, dt, mean, sd) == 0
+        return y

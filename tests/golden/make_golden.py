@@ -10,8 +10,10 @@ from the restatements, cross-checked where the real thing exists here:
                                  (oracle/psf_port.c; parity unpinned)
   crc32c.npz                     CRC32C vectors from the reference's own
                                  src/util/crc32c.cc (oracle/_ref), = the port
-  noise.npz                      NOISE outputs (psf_port.c over libstdc++'s
-                                 polar method and this libm; parity unpinned)
+  noise.npz                      NOISE outputs from libstdc++'s own
+                                 std::default_random_engine +
+                                 std::normal_distribution (oracle/noise_std.cc,
+                                 the calls add_noise.h makes), = psf_port.c
   snappy.npz                     snappy 1.1.8 RawCompress outputs from the
                                  library itself (/opt/conda), = snappy_port.c
   snappy_dec.npz                 snappy 1.1.8 RawUncompress verdicts + outputs
@@ -119,12 +121,16 @@ def gen_crc(P):
 
 
 def gen_noise(P):
+    import oracle
+    S = oracle.NoiseStd()
     arrays = {}
     for tag, dt in (("f32", np.float32), ("f64", np.float64)):
         for j, (n, mean, sd) in enumerate(((1001, 0.25, 2.0), (64, 0.0, 1.0), (7, -3.0, 0.01))):
             v = np.linspace(-1, 1, n).astype(dt)
             arrays[f"{tag}_{j}_in"] = v
-            arrays[f"{tag}_{j}_out"] = P.add_noise(v, np.float32(mean), np.float32(sd))
+            out = S.add_noise(v, np.float32(mean), np.float32(sd))
+            assert out.tobytes() == P.add_noise(v, np.float32(mean), np.float32(sd)).tobytes()
+            arrays[f"{tag}_{j}_out"] = out
             arrays[f"{tag}_{j}_param"] = np.array([mean, sd], np.float32)
     return {"noise.npz": arrays}
 

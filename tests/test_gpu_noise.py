@@ -4,7 +4,9 @@ The engine draws, uniforms, polar coordinates and acceptance decisions are
 exact IEEE operations reproduced bit for bit, and the logs are glibc's own
 algorithms (logf for f32, glibc_logf.h; log for f64 with the FMA build's fused
 operations, glibc_log.h), so NOISE must be bit-identical to the reference for
-both value types."""
+both value types -- checked against the C restatement and against libstdc++'s
+std::default_random_engine + std::normal_distribution themselves
+(oracle/noise_std.cc)."""
 import os
 
 import numpy as np
@@ -55,11 +57,14 @@ def test_noise_golden(ctx):
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 def test_noise_large_vs_port(ctx, port, dtype):
+    import oracle
     n = (1 << 21) + 7
     x = np.random.default_rng(5).standard_normal(n).astype(dtype)
     got = _noise_via_node(ctx, x, 0.5, 3.0)
     want = port.add_noise(x, 0.5, 3.0)
     _check(got, want, x, 0.5)
+    # and libstdc++'s own engine + normal_distribution, the calls add_noise.h makes
+    _check(got, oracle.NoiseStd().add_noise(x, 0.5, 3.0), x, 0.5)
     # a second, shorter array reuses the cached sequence prefix
     got2 = _noise_via_node(ctx, x[:1000], -1.0, 0.25)
     _check(got2, port.add_noise(x[:1000], -1.0, 0.25), x[:1000], -1.0)

@@ -61,6 +61,23 @@ def test_noise_port_matches_reference(port):
             assert out.tobytes() == d[f"{tag}_{j}_out"].tobytes()
 
 
+def test_noise_port_matches_libstdcxx(port):
+    """NOISE's restatement (psf_port.c) against libstdc++ itself: a default
+    std::default_random_engine feeding std::normal_distribution<V>(mean, std),
+    fresh per array, as add_noise.h:29-39 calls them (oracle/noise_std.cc,
+    built with the reference's flags)."""
+    import oracle
+    S = oracle.NoiseStd()
+    rng = np.random.default_rng(0)
+    for dt in (np.float32, np.float64):
+        for n in (1, 2, 3, 7, 64, 1001, 4099, 1 << 18):
+            for mean, sd in ((0.0, 1.0), (0.25, 2.0), (-3.0, 0.01), (1e3, 1e-3)):
+                x = rng.standard_normal(n).astype(dt)
+                a = port.add_noise(x, np.float32(mean), np.float32(sd))
+                b = S.add_noise(x, np.float32(mean), np.float32(sd))
+                assert a.tobytes() == b.tobytes(), (dt, n, mean, sd)
+
+
 def test_lcg_jump_ahead(port):
     # fixing_float.h:18-21; the HIP encoder jumps the LCG per lane
     s = np.uint32(12345)
