@@ -45,11 +45,13 @@ constexpr int kTileGroups = 4 * kBlock;  // groups of 4 values per tile
 #define PSF_MINMAX_GRID 1024
 #endif
 constexpr int kMinmaxGrid = PSF_MINMAX_GRID;  // partials the encode kernel folds
-// workgroups for the store-heavy passes: 8192 (4 tiles each at 2^27 values)
-// measured 1.5-5 % faster than 4096 for encode, equal for decode; larger grids
-// lose to per-workgroup setup (tools/build_variants.sh, r01)
+// workgroups for the store-heavy passes: 16384 (2 tiles each at 2^27 values,
+// 4 at 2^28) measured 3 % faster than 8192 for the C2 step at both sizes
+// (encode 227 -> 220 us, decode 202 -> 194 us at 2^28; 12288, which splits
+// the tiles unevenly, no faster than 8192; tools/ab_c2.sh, r02); 8192 was
+// 1.5-5 % faster than 4096 for encode (r01)
 #ifndef PSF_STREAM_GRID
-#define PSF_STREAM_GRID 8192
+#define PSF_STREAM_GRID 16384
 #endif
 constexpr int kStreamGrid = PSF_STREAM_GRID;
 constexpr uint32_t kMask17 = 0x1FFFFu;   // LCG state kept mod 2^17 (see quant_group)

@@ -10,5 +10,5 @@ for v in base "$@" base; do
   python3 -c "
 import json
 d=json.loads(open('$O/b_$v.json').read().strip().splitlines()[-1])
-print('$v', d['value'], d['ms_per_step'], {k:v['avg_us'] for k,v in d['roofline']['kernels'].items()})"
+print('$v', d['value'], d['ms_per_step'], (d.get('config_128M') or {}).get('value'), {k:v['avg_us'] for k,v in d['roofline']['kernels'].items()})"
 done
