@@ -137,9 +137,19 @@ def test_ff_full_size_properties(ctx):
     # i, the inverted bit 16 of the MSVC LCG state s_{i+1}; over a full period
     # of the low 17 bits it is exactly balanced, so over 2^28 elements (2^11
     # periods) it is balanced to the element
+    # tmp as fixing_float.h:80 forms it, (proj - min_v) / bin * ratio with an
+    # IEEE division: the divisor is a device tensor, because torch divides by a
+    # host scalar as a multiply by its reciprocal, which moves floor(tmp) by one
+    # for values within an ulp of a code boundary
     mn64, mx64 = np.float64(mn), np.float64(mx)
-    tmp = torch.floor((x.double().clamp(mn64, mx64) - mn64) / (mx64 - mn64) * 254.0).long()
+    bin_d = torch.tensor(mx64 - mn64, dtype=torch.float64, device=DEV)
+    tmp = torch.floor((x.double().clamp(mn64, mx64) - mn64) / bin_d * 254.0).long()
     bit = c - tmp
+    if int(bit.min()) < 0 or int(bit.max()) > 1:  # diagnostics for a failure
+        bad = ((bit < 0) | (bit > 1)).nonzero().flatten()[:8]
+        recip = torch.floor((x.double().clamp(mn64, mx64) - mn64) / (mx64 - mn64) * 254.0).long()
+        print("bad", bad.tolist(), "x", x[bad].tolist(), "code", c[bad].tolist(), "floor", tmp[bad].tolist(),
+              "floor via reciprocal", recip[bad].tolist(), "min/max", mn, mx)
     assert int(bit.min()) >= 0 and int(bit.max()) <= 1
     assert int(bit.sum()) == n // 2
     del x, dec, c, tmp, bit
