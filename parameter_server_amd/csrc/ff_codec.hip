@@ -48,8 +48,10 @@ constexpr int kMinmaxGrid = PSF_MINMAX_GRID;  // partials the encode kernel fold
 // workgroups for the store-heavy passes: 16384 (2 tiles each at 2^27 values,
 // 4 at 2^28) measured 3 % faster than 8192 for the C2 step at both sizes
 // (encode 227 -> 220 us, decode 202 -> 194 us at 2^28; 12288, which splits
-// the tiles unevenly, no faster than 8192; tools/ab_c2.sh, r02); 8192 was
-// 1.5-5 % faster than 4096 for encode (r01)
+// the tiles unevenly, no faster than 8192; 32768 +0.6 % at 2^28 but -2.5 % at
+// 2^27, one tile per workgroup; tools/ab_c2.sh, r02); 8192 was 1.5-5 % faster
+// than 4096 for encode (r01).  The min/max grid at 2048 lost 3 % (its
+// partials fold in every encode workgroup), at 256-512 up to 23 %.
 #ifndef PSF_STREAM_GRID
 #define PSF_STREAM_GRID 16384
 #endif
