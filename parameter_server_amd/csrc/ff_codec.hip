@@ -56,6 +56,7 @@ constexpr int kMinmaxGrid = PSF_MINMAX_GRID;  // partials the encode kernel fold
 #define PSF_STREAM_GRID 16384
 #endif
 constexpr int kStreamGrid = PSF_STREAM_GRID;
+constexpr int kDecodeGridBig = 2 * PSF_STREAM_GRID;
 constexpr uint32_t kMask17 = 0x1FFFFu;   // LCG state kept mod 2^17 (see quant_group)
 struct Lcg17 { uint32_t a[4], c[4]; };   // affine maps for 1..4 LCG steps, mod 2^17
 
@@ -1304,7 +1305,13 @@ int ff_encode_launch(const void* x, size_t n, int value_type, int nb, const Fixe
 template <typename V, int NB, bool kVec>
 static void launch_decode(const uint8_t* code, size_t n, V* out, const DecodeParams& p,
                           hipStream_t st) {
-  const int grid = (kVec && NB <= 3) ? tile_grid(n, kStreamGrid) : ff_grid(n);
+  // arrays of >= 2 x kDecodeGridBig tiles (2^28 values) decode on twice the
+  // stream grid, 2 tiles per workgroup: decode 193-194 -> 189 us at 2^28
+  // (tools/ab_c2.sh, r02); the encode and smaller arrays measured no gain
+  // from it (2^27 on one tile per workgroup: -2.5 %)
+  const size_t tiles = ((n >> 2) + kTileGroups - 1) / kTileGroups;
+  const int cap = tiles >= 2 * (size_t)kDecodeGridBig ? kDecodeGridBig : kStreamGrid;
+  const int grid = (kVec && NB <= 3) ? tile_grid(n, cap) : ff_grid(n);
   hipLaunchKernelGGL((ff_decode<V, NB, kVec>), dim3(grid), dim3(kBlock), 0, st, code, n, out, p);
 }
 
