@@ -51,6 +51,7 @@ extern "C" {
 #define PSF_ERR_HIP (-4)         /* HIP runtime failure                           */
 #define PSF_ERR_CHECK (-5)       /* other reference CHECK (signature mismatch ...) */
 #define PSF_ERR_UNSUPPORTED (-6)
+#define PSF_ERR_TIMEOUT (-7)     /* a device-side wait hit its cap; the launch gave up */
 
 /* ---- task.proto DataType / filter.proto Type values -------------------- */
 #define PSF_DT_UINT64 8
@@ -72,6 +73,13 @@ const char* psf_version(void);
 /* time(NULL) is FIXING_FLOAT's LCG seed in the reference (fixing_float.h:78);
  * enable=1 pins it to `t` process-wide (parity testing), enable=0 restores it. */
 void psf_set_clock(int enable, int64_t t);
+
+/* Debug knob (testing the bounded device waits): snappy compress launches
+ * that follow never publish fragment `fragment` of their look-back chain
+ * (< 0: none, the default) and give up after `spin_cap` polls of a wait
+ * (0: the default cap), so the call returns PSF_ERR_TIMEOUT instead of
+ * waiting.  Process-wide. */
+void psf_debug_snappy_stall(int64_t fragment, uint32_t spin_cap);
 
 /* ---- execution context (device + stream + workspace) ------------------- */
 /* A context (and the nodes and messages that use it) is not thread-safe:

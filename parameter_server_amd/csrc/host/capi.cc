@@ -56,6 +56,7 @@ extern "C" {
 const char* psf_last_error(void) { return g_last_error.c_str(); }
 const char* psf_version(void) { return "psf 0.1 gfx950"; }
 void psf_set_clock(int enable, int64_t t) { psf::set_clock_override(enable != 0, t); }
+void psf_debug_snappy_stall(int64_t fragment, uint32_t spin_cap) { psf::snappy_debug_stall(fragment, spin_cap); }
 
 int psf_context_create(int device, void* stream, int own_stream, psf_context** out) {
   return guarded([&] {
@@ -182,6 +183,10 @@ int psf_snappy_compress(psf_context* ctx, const void* d_in, size_t n, void* d_ou
     int st = psf::snappy_compress_launch(d_in, n, d_out, scratch.ptr, c.stream(), c.prof(), c.pub_dev(0), ticket);
     if (st != PSF_OK) return st;
     c.wait_ticket(0, ticket);
+    if (c.pub_host(0)->status != PSF_OK) {
+      c.sync();
+      return (int)c.pub_host(0)->status;
+    }
     *out_len = c.pub_host(0)->size;
     // the size is published before every fragment has placed its bytes:
     // "synchronous" means the stream in d_out is complete on return

@@ -75,6 +75,11 @@ class Context {
   // kind's parity, else {} (the launch then memsets its own scratch)
   enum ZeroKind { kZeroCompress = 0, kZeroUncompress, kZeroKinds };
   ZeroPair zero_pair(int kind, size_t need);
+  // the launch that took `z` failed before its kernel ran: nothing dirtied
+  // z.cur or cleared z.next, so the next launch of the kind takes z.cur again
+  void zero_pair_unused(int kind, const ZeroPair& z) {
+    if (z.cur) zero_parity_[kind] ^= 1;
+  }
   // pooled timing-free events
   hipEvent_t take_event();
   void give_event(hipEvent_t e);

@@ -14,6 +14,26 @@ PushRouter::PushRouter(Context* ctx, const std::vector<KeyRange>& ranges, int ra
 
 PushRouter::~PushRouter() = default;
 
+// The key width SliceKOFVMessage<K> slices with (message.h:107-147): the
+// application's K, which the stream's task.key_type records (EncodeType<K>,
+// message.h:70-76).  Streams without keys do not vote; the streams of one
+// step must agree, and a key buffer must hold whole keys (SArray<K>'s CHECK).
+static int step_key_bytes(const Message* const* streams, int n) {
+  int kb = 0;
+  for (int i = 0; i < n; ++i) {
+    const Message& m = *streams[i];
+    if (m.key.empty()) continue;
+    int w = 0;
+    if (m.task.has_key_type && m.task.key_type == 8) w = 8;       // UINT64
+    else if (m.task.has_key_type && m.task.key_type == 7) w = 4;  // UINT32
+    else throw CheckError(kErrArg, "router: stream keys must be UINT32 or UINT64 (task.key_type)");
+    if (m.key.bytes % (size_t)w) throw CheckError(kErrCheck, "CHECK_EQ(key.size() % sizeof(K), 0): ragged key buffer");
+    if (kb && kb != w) throw CheckError(kErrArg, "router: streams of one step must share a key type");
+    kb = w;
+  }
+  return kb ? kb : 8;
+}
+
 RemoteNode* PushRouter::sender(int32_t stream, int server) {
   auto& p = senders_[{stream, server}];
   if (!p) p.reset(new RemoteNode(ctx_));
@@ -41,7 +61,9 @@ void PushRouter::encode_launch(const Message* const* streams, int n) {
   std::unique_ptr<SliceJob> job;
   if (next_ && next_->same_inputs(streams, n)) job = std::move(next_);
   next_.reset();
-  if (!job) job = slice_begin(ctx_, std::vector<const Message*>(streams, streams + n), ranges_, 8);
+  const int kb = step_key_bytes(streams, n);
+  if (job && job->key_bytes != kb) job.reset();
+  if (!job) job = slice_begin(ctx_, std::vector<const Message*>(streams, streams + n), ranges_, kb);
   std::vector<std::vector<Message>> parts;
   std::vector<std::vector<bool>> ok;
   std::vector<std::vector<KeySigHint>> hints;
@@ -92,7 +114,7 @@ void PushRouter::encode_finish(int64_t* sizes) {
 }
 
 void PushRouter::prefetch(const Message* const* streams, int n) {
-  next_ = slice_begin(ctx_, std::vector<const Message*>(streams, streams + n), ranges_, 8);
+  next_ = slice_begin(ctx_, std::vector<const Message*>(streams, streams + n), ranges_, step_key_bytes(streams, n));
 }
 
 void PushRouter::fill(void* sendbuf) {
@@ -129,6 +151,11 @@ void PushRouter::decode_received(const uint8_t* recvbuf, const int64_t* sizes_in
   std::vector<Message> ms;
   std::vector<int> sv;
   spill_unpack(ctx_, own_copy(ctx_, recvbuf, total), world_, sizes_in, &ms, &sv);
+  // a record names its server: it must be one of this rank's (the sender
+  // routed it by owner(server)); anything else is a corrupt or misrouted buffer
+  const int S = (int)ranges_.size();
+  for (int s : sv)
+    if (s < 0 || s >= S || owner(s) != rank_) throw CheckError(kErrCheck, "spill record for a server this rank does not own");
   decode_into_results(ms, sv);
   stat_decode_ns += now_ns() - t0;
 }

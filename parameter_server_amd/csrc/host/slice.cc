@@ -75,6 +75,9 @@ void build_slices(const Message& msg, const std::vector<KeyRange>& krs, int key_
     (*valid)[i] = true;
     if (nkeys == 0) continue;  // "to void be divided by 0"
     const size_t lo = pos[i], hi = pos[i + 1];
+    // SArray::Segment (shared_array_inl.h:135): a range end that does not fit
+    // K wraps in the (K) cast and lands before the range's begin
+    if (lo > hi) throw CheckError(kErrCheck, "CHECK(range.valid())");
     ret.set_key(segment(msg.key, lo * key_bytes, (hi - lo) * key_bytes));
     ret.task.key_type = key_bytes == 8 ? 8 : 7;  // EncodeType<K>: UINT64 / UINT32
     ret.task.has_key_type = true;

@@ -130,8 +130,10 @@ void SnappyBatch::launch(size_t b, size_t e) {
         Buffer scratch = c_.alloc(snappy_compress_batch_scratch(cj.data(), (int)cj.size()));
         size_t nfrag = 0;
         for (const SnappyCJob& q : cj) nfrag += (q.n + 65535) / 65536;
+        const ZeroPair z = c_.zero_pair(Context::kZeroCompress, nfrag * 8 + 8);
         st = snappy_compress_batch_launch(cj.data(), (int)cj.size(), scratch.ptr, c_.stream(), c_.prof(),
-                                          c_.pub_dev(0), c_.zero_pair(Context::kZeroCompress, nfrag * 8 + 8));
+                                          c_.pub_dev(0), z);
+        if (st != kOk) c_.zero_pair_unused(Context::kZeroCompress, z);
         cj.clear();
       } else if (!comp && !dj.empty()) {
         Tail t;
@@ -142,6 +144,7 @@ void SnappyBatch::launch(size_t b, size_t e) {
         const ZeroPair z = tails_.empty() ? c_.zero_pair(Context::kZeroUncompress, dj.size() * 32 + 4) : ZeroPair{};
         st = snappy_uncompress_batch_launch(dj.data(), (int)dj.size(), t.scratch.ptr, c_.stream(), c_.prof(),
                                             c_.pub_dev(0), z, &t.t);
+        if (st != kOk) c_.zero_pair_unused(Context::kZeroUncompress, z);
         if (st == kOk) {
           t.done = c_.take_event();
           PSF_HIP_CHECK(hipEventRecord(t.done, c_.stream()));
@@ -252,7 +255,7 @@ void SnappyBatch::finish() {
     }
     const Slot& h = *c_.pub_host(j.slot);
     if (h.status != kOk) {
-      bad = h.status;
+      if (bad == kOk || h.status == kErrTimeout) bad = h.status;
       continue;
     }
     j.out.bytes = h.size;
@@ -265,6 +268,7 @@ void SnappyBatch::finish() {
   }
   jobs_.clear();
   launched_ = 0;
+  if (bad == kErrTimeout) throw CheckError(kErrTimeout, "snappy: a device-side wait hit its cap");
   if (bad != kOk) throw CheckError(kErrCheck, "CHECK(snappy::RawUncompress(src, src_size, data_))");
 }
 

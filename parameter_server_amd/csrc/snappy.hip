@@ -34,6 +34,8 @@
 // copies reach into an earlier fragment (never produced by a 1.1.8 encoder,
 // but valid) is decoded by one lane instead (K5).
 #include "psf_internal.h"
+
+#include <atomic>
 #include "ff_dequant.h"
 
 namespace psf {
@@ -316,13 +318,25 @@ struct CJob {
   uint64_t n;
   uint32_t frag0, nfrag, hdr, slot, ticket, pad;
 };
+// Every wait is bounded: a look-back (or the placing waves' wait on it) that
+// spins `spin_cap` times without progress sets the launch's abort word and
+// gives up; every later wait sees the word and gives up at once, and each
+// stream's last fragment publishes kErrTimeout instead of its length.  (The
+// ticket argument above says no wait of a correct launch comes near the cap;
+// the cap turns a broken assumption into a status code, not a device hang.)
+// `stall` (a debug knob, psf_debug_snappy_stall) names a fragment whose length
+// is never published, to test that path.
 struct SnappyCJobs {
   CJob j[kSnappyBatchMax];
   PubSlot* pub;
   uint32_t njobs, nfrag;
   uint64_t* znext;  // the next launch's zeroed state region (null: none)
   uint32_t zwords;
+  uint32_t spin_cap;  // look-back iterations before the launch aborts
+  uint32_t stall;     // debug: fragment that never publishes (kNoStall: none)
 };
+constexpr uint32_t kNoStall = 0xffffffffu;
+constexpr uint64_t kAborted = ~0ull;  // s_excl when the look-back gave up
 __device__ __forceinline__ const CJob& cjob_of(const SnappyCJobs& J, uint32_t g) {
   uint32_t i = 0;
   while (i + 1 < J.njobs && g >= J.j[i + 1].frag0) ++i;
@@ -338,6 +352,7 @@ __global__ __launch_bounds__(kCThreads) void snappy_compress_frags(const SnappyC
   __shared__ uint64_t s_excl;
   const uint32_t tid = threadIdx.x;
   const uint32_t wave = tid >> 6, lane = tid & 63;
+  uint32_t* const abortw = ctr + 1;  // set when a wait gave up (zero at the launch, as ctr)
   if (tid == 0) {
     s_t0 = atomicAdd(ctr, 1u);
     s_t1 = atomicAdd(ctr, 1u);
@@ -513,7 +528,9 @@ __global__ __launch_bounds__(kCThreads) void snappy_compress_frags(const SnappyC
           flen += 1 + m + 1 + (m < 60 ? 0 : ((31 - __builtin_clz(m)) >> 3) + 1);
         }
         if (lane == 0) {
-          if (f_local == 0)  // a stream's first fragment: its inclusive prefix at once
+          if (f == J.stall) {
+            // debug: never published
+          } else if (f_local == 0)  // a stream's first fragment: its inclusive prefix at once
             __hip_atomic_store(&state[f], (2ull << 62) | (f_hdr + flen), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           else
             atomicAdd(&state[f], (1ull << 62) | flen);
@@ -547,7 +564,7 @@ __global__ __launch_bounds__(kCThreads) void snappy_compress_frags(const SnappyC
         if (wave == 1 && lp > 0) {  // (the stream's first fragment is inclusive: the walk ends there at the latest)
           uint64_t sum = 0;
           int64_t base = (int64_t)fp - 1;  // lane l reads fragment base - l
-          for (;;) {
+          for (uint32_t spins = 0;;) {
             const int64_t j = base - (int64_t)lane;
             const uint64_t w = j >= 0 ? __hip_atomic_load(&state[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
             const bool ready = j < 0 || (w >> 62) != 0;  // fragment 0 publishes inclusive only: the walk ends there
@@ -555,6 +572,10 @@ __global__ __launch_bounds__(kCThreads) void snappy_compress_frags(const SnappyC
             const int stop = im ? __builtin_ctzll(im) : 63;
             const uint64_t need = stop >= 63 ? ~0ull : ((2ull << stop) - 1);
             if (__ballot(!ready) & need) {  // a predecessor in front of the stop has not published yet
+              if (++spins >= J.spin_cap || __hip_atomic_load(abortw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                sum = kAborted;
+                break;
+              }
               __builtin_amdgcn_s_sleep(1);
               continue;
             }
@@ -569,31 +590,43 @@ __global__ __launch_bounds__(kCThreads) void snappy_compress_frags(const SnappyC
         }
         if (wave == 1) {
           if (lane == 0) {
+            const bool ok = excl != kAborted;
+            if (!ok) __hip_atomic_store(abortw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             s_excl = excl;
             __hip_atomic_store(&s_round, round, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (lp > 0)
+            if (lp > 0 && ok && fp != J.stall)
               __hip_atomic_store(&state[fp], (2ull << 62) | (excl + flen), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (lp + 1 == cp.nfrag && J.pub) {
               PubSlot* pub = J.pub + cp.slot;
-              pub->size = excl + flen;
-              pub->status = kOk;
+              pub->size = ok ? excl + flen : 0;
+              pub->status = ok ? kOk : kErrTimeout;
               publish_ticket(pub, cp.ticket);
             }
           }
         } else {
-          while (__hip_atomic_load(&s_round, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != round)
+          // wave 1 stores s_round within its (bounded) look-back; the cap here
+          // is a backstop far above it
+          for (uint32_t spins = 0;
+               __hip_atomic_load(&s_round, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != round; ++spins) {
+            if (spins >= J.spin_cap * 64u) {
+              if (tid == 128) __hip_atomic_store(abortw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              break;
+            }
             __builtin_amdgcn_s_sleep(1);
-          excl = s_excl;
+          }
+          excl = __hip_atomic_load(&s_round, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == round ? s_excl : kAborted;
         }
         PSF_TRACE_T(fp, 2, 64);
         if (lp == 0 && pt < cp.hdr)
           cp.dst[pt] = (uint8_t)(((uint32_t)cp.n >> (7 * pt)) | (pt + 1 < cp.hdr ? 128u : 0u));
-        uint8_t* d = cp.dst + excl;
-        if (fp_op) place_copy(d, scratch + (size_t)fp * kSnappyFragOut, fp_op, pt, lane);
-        if (fp_next < plen) {
-          d += fp_op;
-          d += literal_tag(d, plen - fp_next, pt);
-          place_copy(d, cp.in + pstart + fp_next, plen - fp_next, pt, lane);
+        if (excl != kAborted) {  // an aborted fragment places nothing (its stream reports kErrTimeout)
+          uint8_t* d = cp.dst + excl;
+          if (fp_op) place_copy(d, scratch + (size_t)fp * kSnappyFragOut, fp_op, pt, lane);
+          if (fp_next < plen) {
+            d += fp_op;
+            d += literal_tag(d, plen - fp_next, pt);
+            place_copy(d, cp.in + pstart + fp_next, plen - fp_next, pt, lane);
+          }
         }
         PSF_TRACE_T(fp, 3, 64);
       }
@@ -1441,50 +1474,46 @@ __device__ void dindex_body(const SnappyDJobs& J, uint32_t ji, uint32_t w, uint3
   if (fl) atomicOr(flags, fl);
 }
 
-// Grid-wide barrier of a persistent launch (every workgroup resident): the
-// agent-scope fences write this XCD's L2 back and read the others' writes
-// (the scan path only, where K1's tables feed K2 and K2's entries feed K3).
-__device__ void grid_barrier(uint32_t* bar, uint32_t target) {
-  __threadfence();
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    atomicAdd(bar, 1u);
-    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) __builtin_amdgcn_s_sleep(2);
-  }
-  __syncthreads();
-  __threadfence();
-}
-
-// K1 + K2 + K3 in one persistent launch: windows scanned (streams K0 handed
-// over), a grid barrier, each such stream linked by one workgroup, a grid
-// barrier, windows indexed (streams K0 did not walk to the end).  When no
-// stream of the batch needs them, every workgroup returns at once.
-__global__ __launch_bounds__(64) void snappy_dslow(const SnappyDJobs J) {
-  __shared__ uint32_t b32[(kWin + 32) / 4];
-  __shared__ uint32_t bm[kWin / 32];
-  bool scan = false, index = false;
+// K1, K2 and K3 as three ordinary launches: stream order is the barrier
+// between them (K1's tables feed K2, K2's window entries feed K3), so no
+// workgroup ever waits for another and no co-residency is assumed.  Each
+// returns at once when no stream of the batch needs it.
+__device__ __forceinline__ void dslow_needs(const SnappyDJobs& J, bool& scan, bool& index) {
+  scan = index = false;
   for (uint32_t i = 0; i < J.njobs; ++i) {
     const uint32_t f0 = J.ctrl[8 * i], f1 = J.ctrl[8 * i + 1];
     scan = scan || (f0 & kFlagScan);
     index = index || (!f1 && !(f0 & (kFlagInvalid | kFlagHeader)));
   }
-  if (!scan && !index) return;
-  uint32_t* bar = J.ctrl + 8 * J.njobs;
-  if (scan) {
-    for (uint32_t w = blockIdx.x; w < J.nwin; w += gridDim.x) {
-      const uint32_t ji = djob_win(J, w);
-      dscan_body(J, ji, w - J.j[ji].win0, b32, bm);
-    }
-    grid_barrier(bar, gridDim.x);
-    for (uint32_t ji = blockIdx.x; ji < J.njobs; ji += gridDim.x) {
-      const DScr S = dscr(J, J.j[ji], ji);
-      if (*S.flags & kFlagScan) {
-        const DJob& D = J.j[ji];
-        dlink_body(D.in, D.C, D.hdr, D.dsize, S.bitmap, S.cum, S.wexit, S.wtotal, D.nwin, S.wentry, S.woff, S.flags);
-      }
-    }
-    grid_barrier(bar, 2 * gridDim.x);
+}
+// K1: windows of the streams K0 handed over
+__global__ __launch_bounds__(64) void snappy_dscan(const SnappyDJobs J) {
+  __shared__ uint32_t b32[(kWin + 32) / 4];
+  __shared__ uint32_t bm[kWin / 32];
+  bool scan, index;
+  dslow_needs(J, scan, index);
+  if (!scan) return;
+  for (uint32_t w = blockIdx.x; w < J.nwin; w += gridDim.x) {
+    const uint32_t ji = djob_win(J, w);
+    dscan_body(J, ji, w - J.j[ji].win0, b32, bm);
   }
+}
+// K2: one workgroup per stream links its windows
+__global__ __launch_bounds__(64) void snappy_dlink(const SnappyDJobs J) {
+  for (uint32_t ji = blockIdx.x; ji < J.njobs; ji += gridDim.x) {
+    const DScr S = dscr(J, J.j[ji], ji);
+    if (*S.flags & kFlagScan) {
+      const DJob& D = J.j[ji];
+      dlink_body(D.in, D.C, D.hdr, D.dsize, S.bitmap, S.cum, S.wexit, S.wtotal, D.nwin, S.wentry, S.woff, S.flags);
+    }
+  }
+}
+// K3: windows indexed (streams K0 did not walk to the end)
+__global__ __launch_bounds__(64) void snappy_dindex(const SnappyDJobs J) {
+  __shared__ uint32_t b32[(kWin + 32) / 4];
+  bool scan, index;
+  dslow_needs(J, scan, index);
+  if (!scan && !index) return;
   for (uint32_t w = blockIdx.x; w < J.nwin; w += gridDim.x) {
     const uint32_t ji = djob_win(J, w);
     dindex_body(J, ji, w - J.j[ji].win0, b32);
@@ -1663,6 +1692,11 @@ __global__ __launch_bounds__(256) void snappy_dfrag(const SnappyDJobs J) {
 
 size_t snappy_max_compressed(size_t n) { return 32 + n + n / 6; }
 
+// the compress kernel's wait bounds (SnappyCJobs::spin_cap, ::stall)
+constexpr uint32_t kDefaultSpinCap = 1u << 22;  // >= ~1 s of look-back polling, >100x a tag-dense parse
+static std::atomic<uint32_t> g_spin_cap{kDefaultSpinCap};
+static std::atomic<uint32_t> g_stall{kNoStall};
+
 size_t snappy_compress_batch_scratch(const SnappyCJob* jobs, int njobs) {
   size_t nfrag = 0;
   for (int i = 0; i < njobs; ++i) nfrag += (jobs[i].n + kFrag - 1) / kFrag;
@@ -1680,6 +1714,8 @@ int snappy_compress_batch_launch(const SnappyCJob* jobs, int njobs, void* scratc
   SnappyCJobs K{};
   K.pub = pub_base;
   K.njobs = (uint32_t)njobs;
+  K.spin_cap = g_spin_cap.load(std::memory_order_relaxed);
+  K.stall = g_stall.load(std::memory_order_relaxed);
   double bytes = 0;
   for (int i = 0; i < njobs; ++i) {
     const SnappyCJob& q = jobs[i];
@@ -1723,6 +1759,11 @@ int snappy_compress_batch_launch(const SnappyCJob* jobs, int njobs, void* scratc
   return launch_status();
 }
 
+void snappy_debug_stall(int64_t frag, uint32_t spin_cap) {
+  g_stall.store(frag < 0 || frag >= (int64_t)kNoStall ? kNoStall : (uint32_t)frag);
+  g_spin_cap.store(spin_cap ? spin_cap : kDefaultSpinCap);
+}
+
 int snappy_compress_launch(const void* in, size_t n, void* out, void* scratch, hipStream_t st, Profiler* prof,
                            PubSlot* pub, uint32_t ticket) {
   const SnappyCJob j{in, n, out, 0, ticket};
@@ -1751,8 +1792,8 @@ bool snappy_dequant_ok(const SnappyDequant& dq, size_t dsize) {
 
 size_t snappy_uncompress_scratch(size_t C, size_t dsize) { return align256(32 + 4) + djob_bytes(C, dsize); }
 
-// Three launches for the whole batch: K-spec (+ K0 in one more workgroup per
-// stream), K1-K3 (one persistent launch), K4 (+ K5 in each stream's last
+// Launches for the whole batch: K-spec (+ K0 in one more workgroup per
+// stream), K1, K2, K3 (one launch each), K4 (+ K5 in each stream's last
 // workgroup).  On streams
 // of stored fragments K-spec decodes everything and the others return at once.
 static int launch_tail(const SnappyDJobs& K, hipStream_t st);
@@ -1762,7 +1803,7 @@ int snappy_uncompress_batch_launch(const SnappyDJob* jobs, int njobs, void* scra
   if (njobs <= 0 || njobs > kSnappyBatchMax) return kErrArg;
   SnappyDJobs K{};
   uint8_t* s = static_cast<uint8_t*>(scratch);
-  K.ctrl = reinterpret_cast<uint32_t*>(s);  // 8 words per stream, then the grid barrier counter
+  K.ctrl = reinterpret_cast<uint32_t*>(s);  // 8 words per stream, then one spare word
   K.pub = pub_base;
   K.njobs = (uint32_t)njobs;
   uint8_t* data = s + align256((size_t)njobs * 32 + 4);
@@ -1825,14 +1866,9 @@ int snappy_uncompress_batch_launch(const SnappyDJob* jobs, int njobs, void* scra
 // K1-K3 and K4 (+ K5) of a batch whose fast path has run
 static int launch_tail(const SnappyDJobs& K, hipStream_t st) {
   if (K.nwin) {
-    // every workgroup of the persistent launch resident at once: 8 per CU
-    // (18 KiB of LDS and one wave each: a CU's LDS holds 8)
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      return kErrHip;
-    const uint32_t cap = (uint32_t)(8 * cus);
-    hipLaunchKernelGGL(snappy_dslow, dim3(K.nwin < cap ? K.nwin : cap), dim3(64), 0, st, K);
+    hipLaunchKernelGGL(snappy_dscan, dim3(K.nwin), dim3(64), 0, st, K);
+    hipLaunchKernelGGL(snappy_dlink, dim3(K.njobs), dim3(64), 0, st, K);
+    hipLaunchKernelGGL(snappy_dindex, dim3(K.nwin), dim3(64), 0, st, K);
   }
   hipLaunchKernelGGL(snappy_dfrag, dim3(K.nfo1), dim3(256), 0, st, K);
   return launch_status();

@@ -155,15 +155,17 @@ def test_ff_full_size_properties(ctx):
     del x, dec, c, tmp, bit
 
 
-def test_roundtrip_driver_c2_vs_port(ctx, port):
+@pytest.mark.parametrize("log2n", [27, 28])
+def test_roundtrip_driver_c2_vs_port(ctx, port, log2n):
     """The timed driver (psf_node_roundtrip, what bench.py runs) on the bench
-    template at BASELINE configs[1]'s size (2^27 f32, [FIXING_FLOAT nb=1],
-    min/max computed): the encoded message as it went on the wire (codes +
-    side-info) and the decoded message, byte for byte against the C
+    template at BASELINE configs[1]'s size (2^27 f32) and at the bench default
+    (2^28 f32, 1 GiB: the decode's 32768-workgroup grid), chain [FIXING_FLOAT
+    nb=1], min/max computed: the encoded message as it went on the wire (codes
+    + side-info) and the decoded message, byte for byte against the C
     restatement."""
     from parameter_server_amd import FIXING_FLOAT
     from parameter_server_amd import filter as F
-    n = 1 << 27
+    n = 1 << log2n
     g = torch.Generator(device=DEV)
     g.manual_seed(1)
     xs = [torch.randn(n, device=DEV, generator=g) for _ in range(2)]
@@ -187,6 +189,30 @@ def test_roundtrip_driver_c2_vs_port(ctx, port):
     st, pd = port.ff_decode(pc, 1, pmn, pmx, np.float32)
     assert server.value(dec, 0).cpu().numpy().tobytes() == pd.tobytes()
     assert dec.fixed_points(0) == enc.fixed_points(0)
+
+
+@pytest.mark.parametrize("nb", [2, 3])
+def test_ff_single_array_2_28_vs_port(ctx, port, nb):
+    """The single-array encode and decode at the bench size (2^28 f32: the
+    16384-workgroup encode and 32768-workgroup decode grids) with nb = 2 and 3,
+    codes, side-info and decoded values byte for byte against the C
+    restatement (fixing_float.h:73-101)."""
+    n = 1 << 28
+    g = torch.Generator(device=DEV)
+    g.manual_seed(nb)
+    x = torch.randn(n, device=DEV, generator=g)
+    codes, mn, mx = ctx.ff_encode(x, nb, 2024)
+    xh = x.cpu().numpy()
+    st, pc, pmn, pmx = port.ff_encode(xh, nb, 2024)
+    assert st == 0
+    assert _bits(mn) == _bits(pmn) and _bits(mx) == _bits(pmx)
+    assert np.array_equal(codes.cpu().numpy(), pc)
+    del xh
+    dec = ctx.ff_decode(codes, nb, mn, mx)
+    st, pd = port.ff_decode(pc, nb, pmn, pmx, np.float32)
+    assert st == 0
+    assert dec.cpu().numpy().tobytes() == pd.tobytes()
+    del x, codes, dec
 
 
 def test_crc32c_vectors(ctx):

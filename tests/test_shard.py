@@ -270,3 +270,60 @@ def test_slice_many_host_keys_matches_restatement():
             ptr, nb, loc = p.key_ptr()
             got = np.ctypeslib.as_array((np.ctypeslib.ctypes.c_uint8 * nb).from_address(ptr)) if nb else np.zeros(0, np.uint8)
             assert got.tobytes() == w[0].tobytes()
+
+
+def test_push_router_u32_keys_host():
+    """SliceKOFVMessage<K> slices with the application's key type: a stream
+    whose task.key_type is UINT32 is cut at 32-bit keys (message.h:107-147),
+    every server gets its keys and value rows; unsupported key types and ragged
+    key buffers are rejected (SArray<K>'s size CHECK), as is a step mixing
+    32- and 64-bit streams."""
+    from parameter_server_amd import KEY_CACHING, PsfError
+    from parameter_server_amd import filter as F
+    from parameter_server_amd import shard
+    from parameter_server_amd._lib import DT_UINT64
+    DT_UINT32 = 7
+    ctx = F.HostContext()
+    key_range = (0, (1 << 32) - 1)  # K = uint32: range ends must fit K
+    ranges = [shard.even_divide(key_range, 3, i) for i in range(3)]
+    router = shard.PushRouter(ctx, ranges, 0, 1)
+    rng = np.random.default_rng(5)
+    keys = np.unique(rng.integers(0, (1 << 32) - 1, 5000, dtype=np.uint64)).astype(np.uint32)
+    vals = rng.standard_normal(3 * keys.size).astype(np.float32)
+    m = F.Message(request=True, push=True, key_channel=3, key_range=key_range)
+    m.set_key(torch.from_numpy(keys.view(np.int32).copy()), key_type=DT_UINT32)
+    m.add_value(torch.from_numpy(vals.copy()))
+    m.add_filter(KEY_CACHING)
+    for step in range(2):  # miss, then hit
+        router.step({3: m})
+        got = {d: w for d, w in router.results()}
+        assert sorted(got) == [0, 1, 2]
+        for d, w in got.items():
+            lo, hi = ranges[d]
+            sel = (keys.astype(np.uint64) >= np.uint64(lo)) & (keys.astype(np.uint64) < np.uint64(hi))
+            assert sel.sum() > 0
+            p, nb, _ = w.key_ptr()
+            kb = bytes((np.ctypeslib.ctypes.c_uint8 * nb).from_address(p)) if nb else b""
+            assert kb == keys[sel].tobytes(), (step, d)
+            vp, vb, _ = w.value_ptr(0)
+            vbytes = bytes((np.ctypeslib.ctypes.c_uint8 * vb).from_address(vp))
+            assert vbytes == vals.reshape(-1, 3)[sel].tobytes(), (step, d)
+    bad = F.Message(request=True, push=True, key_channel=4, key_range=key_range)
+    bad.set_key(torch.from_numpy(np.arange(10, dtype=np.int16)), key_type=2)  # INT16
+    with pytest.raises(PsfError):
+        router.step({4: bad})
+    ragged = F.Message(request=True, push=True, key_channel=5, key_range=key_range)
+    ragged.set_key(torch.from_numpy(np.arange(7, dtype=np.uint8)), key_type=DT_UINT32)
+    with pytest.raises(PsfError):
+        router.step({5: ragged})
+    # a range end of 2^32 wraps to 0 in the (K) cast: the reference's
+    # Segment CHECK (shared_array_inl.h:135) fails, so does the router
+    r32 = [shard.even_divide((0, 1 << 32), 3, i) for i in range(3)]
+    m32 = F.Message(request=True, push=True, key_channel=7, key_range=(0, 1 << 32))
+    m32.set_key(torch.from_numpy(keys.view(np.int32).copy()), key_type=DT_UINT32)
+    with pytest.raises(PsfError):
+        shard.PushRouter(ctx, r32, 0, 1).step({7: m32})
+    wide = F.Message(request=True, push=True, key_channel=6, key_range=key_range)
+    wide.set_key(torch.from_numpy(np.arange(4, dtype=np.int64)), key_type=DT_UINT64)
+    with pytest.raises(PsfError):
+        router.step({3: m, 6: wide})
