@@ -81,6 +81,15 @@ void psf_set_clock(int enable, int64_t t);
  * waiting.  Process-wide. */
 void psf_debug_snappy_stall(int64_t fragment, uint32_t spin_cap);
 
+/* The device the reference-side adapter (include/psf_ps_filter.h) creates
+ * its contexts on: the last psf_set_default_device(d), else the PSF_DEVICE
+ * environment variable (a device ordinal), else 0.  One server process per
+ * GPU (src/system/assigner.h:17-28 gives each server its key range) sets
+ * PSF_DEVICE=<gpu> at launch.  psf_set_default_device returns PSF_ERR_ARG for
+ * a negative device; psf_default_device reads the environment once. */
+int psf_set_default_device(int device);
+int psf_default_device(void);
+
 /* ---- execution context (device + stream + workspace) ------------------- */
 /* A context (and the nodes and messages that use it) is not thread-safe:
  * callers serialise its use, as the reference serialises one Customer's

@@ -45,12 +45,13 @@ namespace psf_hip {
 
 inline void Check(int st) { CHECK_EQ(st, PSF_OK) << "libpsf: " << psf_last_error(); }
 
-// One filter instance's libpsf state: a context on device 0 with its own
-// non-blocking stream, and a RemoteNode holding the libpsf filter instances.
+// One filter instance's libpsf state: a context on the process's device
+// (psf_default_device: PSF_DEVICE, else 0) with its own non-blocking stream,
+// and a RemoteNode holding the libpsf filter instances.
 class Bound {
  protected:
   Bound() {
-    Check(psf_context_create(0, nullptr, 1, &ctx_));
+    Check(psf_context_create(psf_default_device(), nullptr, 1, &ctx_));
     Check(psf_node_create(ctx_, &node_));
   }
   ~Bound() {
@@ -251,6 +252,176 @@ class KeyCachingFilter : public Filter, Bound {
     psf_msg_destroy(m);
   }
 
+  std::map<CacheKey, SArray<char>> keep_;
+  std::mutex mu_;
+};
+
+// The whole chain of one RemoteNode on one libpsf node: what
+// RemoteNode::EncodeMessage / DecodeMessage (remote_node.cc:17-29) do with the
+// per-type instances FindFilterOrCreate keeps (remote_node.cc:7-15), in one
+// call.  One Chain per RemoteNode (a member the RemoteNode patch adds,
+// INTEGRATION.md), so one libpsf context -- device psf_default_device(), a
+// private stream, workspace and allocator -- serves all of that peer's
+// filters, and the arrays stay in HBM from the first filter to the last:
+// encode stages each host array in once (the first filter that touches it)
+// and only the chain's result comes back as new SArray<char>s; decode stages
+// the received frames in once and brings the decoded arrays back.  The
+// batched entry points run it (psf_nodes_encode / _decode with one message),
+// so a [.., FIXING_FLOAT, COMPRESSING] decode takes the fused uncompress +
+// dequantise.  Chains with NOISE (in place on the caller's buffer,
+// add_noise.h:33-37) or an unknown type are left to the per-filter path
+// (Encode/Decode return false); so is a message without filters.
+class Chain {
+ public:
+  Chain() {}
+  ~Chain() {
+    if (node_) psf_node_destroy(node_);
+    if (ctx_) psf_context_destroy(ctx_);
+  }
+  Chain(const Chain&) = delete;
+  Chain& operator=(const Chain&) = delete;
+  bool Encode(Message* msg) { return Run(msg, true); }
+  bool Decode(Message* msg) { return Run(msg, false); }
+
+ private:
+  typedef std::tuple<int, uint64_t, uint64_t> CacheKey;
+  static bool Done(const Task& t) { return !t.request() || (t.has_param() && t.param().push()); }  // key_caching.h:63-67
+  static bool Handles(const Task& t) {
+    if (t.filter_size() == 0) return false;
+    for (int i = 0; i < t.filter_size(); ++i) {
+      const int ty = t.filter(i).type();
+      if (ty != FilterConfig::KEY_CACHING && ty != FilterConfig::FIXING_FLOAT && ty != FilterConfig::COMPRESSING)
+        return false;
+    }
+    return true;
+  }
+  bool Run(Message* msg, bool encode) {
+    Task& t = msg->task;
+    if (!Handles(t)) return false;
+    std::lock_guard<std::mutex> l(mu_);
+    if (!ctx_) {
+      Check(psf_context_create(psf_default_device(), nullptr, 1, &ctx_));
+      Check(psf_node_create(ctx_, &node_));
+    }
+    psf_message* m = nullptr;
+    Check(psf_msg_create(t.request(), t.has_param(), t.has_param() && t.param().push(), t.key_channel(),
+                         t.has_key_range(), t.key_range().begin(), t.key_range().end(), &m));
+    const bool had_key = msg->has_key();
+    const SArray<char> key_in = msg->key;
+    if (had_key) Check(psf_msg_set_key(m, msg->key.data(), msg->key.size(), PSF_DT_CHAR, PSF_LOC_HOST));
+    for (size_t i = 0; i < msg->value.size(); ++i) {
+      const int vt = i < (size_t)t.value_type_size() ? (int)t.value_type(i) : 0;
+      Check(psf_msg_add_value(m, msg->value[i].data(), msg->value[i].size(), vt, PSF_LOC_HOST));
+    }
+    int kc = -1;
+    for (int i = 0; i < t.filter_size(); ++i) {
+      const FilterConfig& c = t.filter(i);
+      const int fi = psf_msg_add_filter(m, (int)c.type());
+      Check(fi < 0 ? fi : PSF_OK);
+      switch (c.type()) {
+        case FilterConfig::FIXING_FLOAT:
+          Check(psf_fc_set_num_bytes(m, fi, c.num_bytes()));
+          for (int k = 0; k < c.fixed_point_size(); ++k) {
+            const auto& f = c.fixed_point(k);
+            psf_fixed_point p = {f.has_min_value(), f.has_max_value(), f.min_value(), f.max_value()};
+            Check(psf_fc_add_fixed_point(m, fi, &p));
+          }
+          break;
+        case FilterConfig::KEY_CACHING:
+          if (kc < 0) kc = i;
+          if (c.clear_cache_if_done()) Check(psf_fc_set_clear_cache(m, fi, 1));
+          if (c.has_signature()) Check(psf_fc_set_signature(m, fi, 1, c.signature()));
+          break;
+        default:  // COMPRESSING
+          for (int k = 0; k < c.uncompressed_size_size(); ++k) Check(psf_fc_add_uncompressed(m, fi, c.uncompressed_size(k)));
+          break;
+      }
+    }
+    const int st = encode ? psf_nodes_encode(&node_, &m, 1) : psf_nodes_decode(&node_, &m, 1);
+    if (st != PSF_OK) {
+      std::string err = psf_last_error();
+      psf_msg_destroy(m);
+      CHECK(false) << "libpsf chain " << (encode ? "encode" : "decode") << ": " << err;
+    }
+    // side-info into the message's own FilterConfigs
+    for (int i = 0; i < t.filter_size(); ++i) {
+      FilterConfig* c = t.mutable_filter(i);
+      switch (c->type()) {
+        case FilterConfig::FIXING_FLOAT: {
+          const int nfp = psf_fc_num_fixed_point(m, i);
+          for (int k = 0; k < nfp; ++k) {
+            psf_fixed_point p;
+            Check(psf_fc_fixed_point(m, i, k, &p));
+            auto* f = k < c->fixed_point_size() ? c->mutable_fixed_point(k) : c->add_fixed_point();
+            if (p.has_min) f->set_min_value(p.min_value);
+            if (p.has_max) f->set_max_value(p.max_value);
+          }
+          break;
+        }
+        case FilterConfig::KEY_CACHING: {
+          int has = 0;
+          uint32_t sig = 0;
+          Check(psf_fc_signature(m, i, &has, &sig));
+          if (has) c->set_signature(sig);
+          else c->clear_signature();
+          break;
+        }
+        default: {
+          c->clear_uncompressed_size();
+          const int nu = psf_fc_num_uncompressed(m, i);
+          for (int k = 0; k < nu; ++k) {
+            uint64_t v = 0;
+            Check(psf_fc_uncompressed(m, i, k, &v));
+            c->add_uncompressed_size(v);
+          }
+        }
+      }
+    }
+    // the key: elided (a KEY_CACHING hit), restored (from the cache), or
+    // the chain's output
+    void* kp = nullptr;
+    size_t kb = 0;
+    int kloc = 0;
+    Check(psf_msg_key(m, &kp, &kb, &kloc));
+    CacheKey ck(t.key_channel(), t.key_range().begin(), t.key_range().end());
+    if (had_key && kb == 0) {
+      msg->clear_key();
+    } else if (kb && !(kloc == PSF_LOC_HOST && kp == key_in.data() && kb == key_in.size())) {
+      SArray<char> k;
+      auto it = keep_.find(ck);
+      if (kloc == PSF_LOC_HOST && it != keep_.end() && it->second.data() == kp && it->second.size() == kb) {
+        k = it->second;  // a host key the cache refers to: shared, as key_caching.h:55 shares it
+      } else {
+        CHECK_EQ(kloc, PSF_LOC_DEVICE) << "libpsf chain: host key of unknown owner";
+        k = SArray<char>(kb);
+        Check(psf_copy_to_host(ctx_, k.data(), kp, kb));
+      }
+      if (had_key) msg->key = k;  // a codec's output replaces the key (compressing.h:14,30)
+      else msg->set_key(k);       // restored (key_caching.h:55, set_key<char>)
+    }
+    // libpsf's KEY_CACHING cache may refer to the host key bytes it was
+    // given: keep that SArray while the entry lives (the cache is replaced
+    // on a miss and on a decode with keys, key_caching.h:27-28,47)
+    if (kc >= 0) {
+      if (had_key && !(encode && kb == 0)) keep_[ck] = key_in;
+      if (t.filter(kc).clear_cache_if_done() && Done(t)) keep_.erase(ck);
+    }
+    for (size_t i = 0; i < msg->value.size(); ++i) {
+      void* p = nullptr;
+      size_t bytes = 0;
+      int loc = 0;
+      Check(psf_msg_value(m, (int)i, &p, &bytes, &loc));
+      if (p == msg->value[i].data() && bytes == msg->value[i].size()) continue;
+      SArray<char> out(bytes);
+      if (bytes) Check(psf_copy_to_host(ctx_, out.data(), p, bytes));
+      msg->value[i] = out;
+    }
+    psf_msg_destroy(m);
+    return true;
+  }
+
+  psf_context* ctx_ = nullptr;
+  psf_node* node_ = nullptr;
   std::map<CacheKey, SArray<char>> keep_;
   std::mutex mu_;
 };

@@ -10,6 +10,8 @@
 #include "psf_ps_filter.h"
 
 #include <chrono>
+#include <map>
+#include <memory>
 #include <string>
 #include <thread>
 #include <vector>
@@ -235,4 +237,168 @@ int psadapter_noise(const void* val, size_t vbytes, int vt, float mean, float sd
   return rc;
 }
 
+// ---- the per-RemoteNode chain (psf_hip::Chain) and, for comparison, the
+// reference's own RemoteNode loop (remote_node.cc:7-29) over per-filter
+// adapter instances from the Filter::create hook
+struct RefNode {  // RemoteNode::FindFilterOrCreate / EncodeMessage / DecodeMessage
+  std::map<int, Filter*> filters;
+  ~RefNode() {
+    for (auto& f : filters) delete f.second;
+  }
+  Filter* find_or_create(const FilterConfig& c) {
+    auto it = filters.find((int)c.type());
+    if (it == filters.end()) it = filters.emplace((int)c.type(), psf_hip::CreateFilter(c)).first;
+    return it->second;
+  }
+  void encode(Message* m) {
+    for (int i = 0; i < m->task.filter_size(); ++i) find_or_create(m->task.filter(i))->encode(m);
+  }
+  void decode(Message* m) {
+    for (int i = m->task.filter_size() - 1; i >= 0; --i) find_or_create(m->task.filter(i))->decode(m);
+  }
+};
+struct Peer {  // one side's RemoteNode: the patched one (Chain) or the reference loop
+  bool chain;
+  psf_hip::Chain c;
+  RefNode r;
+  void encode(Message* m) {
+    if (!(chain && c.Encode(m))) r.encode(m);
+  }
+  void decode(Message* m) {
+    if (!(chain && c.Decode(m))) r.decode(m);
+  }
+};
+
+// flags: 1 request, 2 has_param + push; filters: type per entry, param = nb
+// (FIXING_FLOAT) or clear_cache_if_done (KEY_CACHING)
+Message* chain_msg(int flags, int ch, uint64_t rb, uint64_t re, const void* key, size_t kbytes, const void* val,
+                   size_t vbytes, int vt, int nf, const int* ftype, const int* fparam) {
+  auto* m = new Message();
+  m->task.request_ = flags & 1;
+  m->task.has_param_ = (flags & 2) != 0;
+  m->task.param_.push_ = (flags & 2) != 0;
+  m->task.key_channel_ = ch;
+  m->task.mutable_key_range()->set_begin(rb);
+  m->task.mutable_key_range()->set_end(re);
+  if (kbytes) {
+    SArray<char> k(kbytes);
+    memcpy(k.data(), key, kbytes);
+    m->set_key(k);
+  }
+  if (val) {
+    SArray<char> v(vbytes);
+    if (vbytes) memcpy(v.data(), val, vbytes);
+    m->task.value_type_.push_back((DataType)vt);
+    m->value.push_back(v);
+  }
+  for (int i = 0; i < nf; ++i) {
+    auto* f = m->task.add_filter();
+    f->set_type((FilterConfig::Type)ftype[i]);
+    if (ftype[i] == FilterConfig::FIXING_FLOAT) f->num_bytes_ = fparam[i];
+    if (ftype[i] == FilterConfig::KEY_CACHING) f->clear_cache_if_done_ = fparam[i] != 0;
+  }
+  return m;
+}
+}  // extern "C"
+
+extern "C" {
+void* psadapter_peer_new(int chain) {
+  auto* p = new Peer();
+  p->chain = chain != 0;
+  return p;
+}
+void psadapter_peer_free(void* p) { delete static_cast<Peer*>(p); }
+
+// One message: encode on snd, the receiver decodes a copy (Task by value,
+// SArrays shared).  Out: the wire key / value (wk, *wkl; wv, *wvl), per filter
+// 8 words of side-info {has_sig, sig, has_fp, min bits, max bits, n_unc,
+// unc0, unc1}, the decoded key / value (dk, *dkl; dv, *dvl).  0 ok, 1 encode
+// CHECK, 2 decode CHECK.
+int psadapter_chain_msg(void* snd, void* rcv, int flags, int ch, uint64_t rb, uint64_t re, const void* key,
+                        size_t kbytes, const void* val, size_t vbytes, int vt, int nf, const int* ftype,
+                        const int* fparam, uint8_t* wk, size_t* wkl, uint8_t* wv, size_t* wvl, int64_t* side,
+                        uint8_t* dk, size_t* dkl, uint8_t* dv, size_t* dvl) {
+  std::unique_ptr<Message> m(chain_msg(flags, ch, rb, re, key, kbytes, val, vbytes, vt, nf, ftype, fparam));
+  try {
+    static_cast<Peer*>(snd)->encode(m.get());
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return 1;
+  }
+  *wkl = m->key.size();
+  if (*wkl) memcpy(wk, m->key.data(), *wkl);
+  *wvl = m->value.empty() ? 0 : m->value[0].size();
+  if (*wvl) memcpy(wv, m->value[0].data(), *wvl);
+  for (int i = 0; i < nf; ++i) {
+    const FilterConfig& c = m->task.filter(i);
+    int64_t* o = side + 8 * i;
+    o[0] = c.has_signature();
+    o[1] = c.signature();
+    o[2] = c.fixed_point_size() > 0;
+    float mn = 0.f, mx = 0.f;
+    if (o[2]) {
+      mn = c.fixed_point(0).min_value();
+      mx = c.fixed_point(0).max_value();
+    }
+    uint32_t a, b;
+    memcpy(&a, &mn, 4);
+    memcpy(&b, &mx, 4);
+    o[3] = a;
+    o[4] = b;
+    o[5] = c.uncompressed_size_size();
+    o[6] = o[5] > 0 ? (int64_t)c.uncompressed_size(0) : 0;
+    o[7] = o[5] > 1 ? (int64_t)c.uncompressed_size(1) : 0;
+  }
+  Message w = *m;
+  try {
+    static_cast<Peer*>(rcv)->decode(&w);
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return 2;
+  }
+  *dkl = w.key.size();
+  if (*dkl) memcpy(dk, w.key.data(), *dkl);
+  *dvl = w.value.empty() ? 0 : w.value[0].size();
+  if (*dvl) memcpy(dv, w.value[0].data(), *dvl);
+  return 0;
+}
+
+// The host edge: `iters` rounds of `nmsg` messages (message j: key bytes
+// key[koff[j], koff[j+1]), value bytes val[voff[j], voff[j+1]) -- none when
+// empty --, flags fl[j]) encoded on snd and decoded (a copy) on rcv (the
+// other way round when dir[j]), messages already built in host
+// memory.  Returns seconds per round (negative: a CHECK); *enc_s / *dec_s =
+// the encode / decode share.
+double psadapter_chain_bench(void* snd, void* rcv, int iters, int nmsg, const uint8_t* key, const uint64_t* koff,
+                             const uint8_t* val, const uint64_t* voff, const int* fl, const int* dir, int ch, int vt,
+                             int nf, const int* ftype, const int* fparam, double* enc_s, double* dec_s) {
+  std::vector<std::unique_ptr<Message>> tm;
+  for (int j = 0; j < nmsg; ++j)
+    tm.emplace_back(chain_msg(fl[j], ch, 0, ~0ull, key + koff[j], koff[j + 1] - koff[j],
+                              voff[j + 1] > voff[j] ? val + voff[j] : nullptr, voff[j + 1] - voff[j], vt, nf, ftype,
+                              fparam));
+  double te = 0, td = 0;
+  try {
+    for (int it = 0; it < iters; ++it)
+      for (int j = 0; j < nmsg; ++j) {
+        Message a = *tm[j];  // the application's message (buffers shared, as KVVector::Push passes them)
+        Peer* s = static_cast<Peer*>(dir[j] ? rcv : snd);
+        Peer* r = static_cast<Peer*>(dir[j] ? snd : rcv);
+        auto t0 = std::chrono::steady_clock::now();
+        s->encode(&a);
+        auto t1 = std::chrono::steady_clock::now();
+        Message w = a;
+        r->decode(&w);
+        auto t2 = std::chrono::steady_clock::now();
+        te += std::chrono::duration<double>(t1 - t0).count();
+        td += std::chrono::duration<double>(t2 - t1).count();
+      }
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -1.0;
+  }
+  *enc_s = te / iters;
+  *dec_s = td / iters;
+  return (te + td) / iters;
+}
 }  // extern "C"

@@ -47,6 +47,8 @@ SIGNATURES = {
     "psf_version": ([], C.c_char_p),
     "psf_set_clock": ([C.c_int, C.c_int64], None),
     "psf_debug_snappy_stall": ([C.c_int64, u32], None),
+    "psf_set_default_device": ([C.c_int], C.c_int),
+    "psf_default_device": ([], C.c_int),
     "psf_context_create": ([C.c_int, vp, C.c_int, C.POINTER(vp)], C.c_int),
     "psf_context_destroy": ([vp], C.c_int),
     "psf_context_sync": ([vp], C.c_int),

@@ -1,8 +1,10 @@
 // extern "C" boundary of libpsf (include/psf.h).
 #include "../../../include/psf.h"
 
+#include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <set>
 #include <string>
 
@@ -57,6 +59,30 @@ const char* psf_last_error(void) { return g_last_error.c_str(); }
 const char* psf_version(void) { return "psf 0.1 gfx950"; }
 void psf_set_clock(int enable, int64_t t) { psf::set_clock_override(enable != 0, t); }
 void psf_debug_snappy_stall(int64_t fragment, uint32_t spin_cap) { psf::snappy_debug_stall(fragment, spin_cap); }
+
+static std::atomic<int> g_default_device{-1};
+int psf_set_default_device(int device) {
+  if (device < 0) {
+    g_last_error = "psf_set_default_device: negative device";
+    return PSF_ERR_ARG;
+  }
+  g_default_device.store(device);
+  return PSF_OK;
+}
+int psf_default_device(void) {
+  int d = g_default_device.load();
+  if (d >= 0) return d;
+  const char* e = getenv("PSF_DEVICE");
+  d = 0;
+  if (e && *e) {
+    char* end = nullptr;
+    const long v = strtol(e, &end, 10);
+    if (end && *end == 0 && v >= 0 && v < 1024) d = (int)v;
+  }
+  int expect = -1;
+  g_default_device.compare_exchange_strong(expect, d);
+  return g_default_device.load();
+}
 
 int psf_context_create(int device, void* stream, int own_stream, psf_context** out) {
   return guarded([&] {

@@ -83,3 +83,18 @@ def test_fixing_float_needs_device_context():
     m.add_filter(3, num_bytes=1)
     with pytest.raises(F.PsfError):
         node.encode(m)
+
+
+def test_default_device_knob():
+    """psf_default_device: the device the reference-side adapter's contexts
+    use (PSF_DEVICE, else 0; psf_set_default_device overrides)."""
+    import subprocess
+    import sys
+    code = ("import parameter_server_amd as p; L = p.lib(); print(L.psf_default_device()); "
+            "print(L.psf_set_default_device(-1) < 0, L.psf_set_default_device(3), L.psf_default_device())")
+    env = dict(os.environ, PSF_DEVICE="5")
+    out = subprocess.check_output([sys.executable, "-c", code], cwd=ROOT, env=env).decode().split()
+    assert out == ["5", "True", "0", "3"]
+    env["PSF_DEVICE"] = "junk"
+    out = subprocess.check_output([sys.executable, "-c", code], cwd=ROOT, env=env).decode().split()
+    assert out[0] == "0"
