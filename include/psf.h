@@ -420,6 +420,14 @@ int psf_router_encoded(psf_router* r, int i, int32_t* stream, int* server, psf_m
 #define PSF_WAIT_NUM 3
 int psf_context_host_stats(psf_context* ctx, int64_t* wait_ns, int64_t* waits);
 int psf_context_host_stats_reset(psf_context* ctx);
+/* The context's caching allocator: released codec buffers are kept for reuse
+ * on free lists bounded per context (default 8 GiB of HBM, 1 GiB of pinned
+ * host memory); a release past the cap frees the least recently released
+ * blocks first.  out[8] = {HBM cached, HBM cap, HBM allocated (live +
+ * cached), HBM evictions, pinned cached, pinned cap, pinned allocated,
+ * pinned evictions}. */
+int psf_context_set_cache_limit(psf_context* ctx, uint64_t hbm_bytes, uint64_t pinned_bytes);
+int psf_context_memory_stats(psf_context* ctx, uint64_t* out);
 /* router phase timers: out[0] steps (encodes), out[1] host ns inside encode,
  * out[2] host ns inside the decodes (both include the waits above) */
 int psf_router_host_stats(psf_router* r, int64_t* out);

@@ -139,6 +139,8 @@ SIGNATURES = {
     "psf_router_host_stats_reset": ([vp], C.c_int),
     "psf_context_host_stats": ([vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64)], C.c_int),
     "psf_context_host_stats_reset": ([vp], C.c_int),
+    "psf_context_set_cache_limit": ([vp, u64, u64], C.c_int),
+    "psf_context_memory_stats": ([vp, C.POINTER(u64)], C.c_int),
     "psf_router_num_results": ([vp], C.c_int),
     "psf_router_result": ([vp, C.c_int, PI, C.POINTER(vp)], C.c_int),
     "psf_router_num_encoded": ([vp], C.c_int),

@@ -849,6 +849,23 @@ int psf_context_host_stats_reset(psf_context* ctx) {
   ctx->impl->reset_waits();
   return PSF_OK;
 }
+int psf_context_set_cache_limit(psf_context* ctx, uint64_t hbm_bytes, uint64_t pinned_bytes) {
+  return guarded([&] {
+    if (!ctx) return PSF_ERR_ARG;
+    ctx->impl->set_cache_limit(hbm_bytes, pinned_bytes);
+    return PSF_OK;
+  });
+}
+int psf_context_memory_stats(psf_context* ctx, uint64_t* out) {
+  return guarded([&] {
+    if (!ctx || !out) return PSF_ERR_ARG;
+    const psf::Context::MemoryStats m = ctx->impl->memory_stats();
+    const uint64_t v[8] = {m.dev_cached, m.dev_cap, m.dev_allocated, m.dev_evictions,
+                           m.host_cached, m.host_cap, m.host_allocated, m.host_evictions};
+    for (int i = 0; i < 8; ++i) out[i] = v[i];
+    return PSF_OK;
+  });
+}
 int psf_profile_enable(psf_context* ctx, int kernel_mask) {
   if (!ctx) return PSF_ERR_ARG;
   ctx->impl->prof()->enable((uint32_t)kernel_mask);

@@ -5,6 +5,8 @@
 #include <time.h>
 
 #include <atomic>
+#include <iterator>
+#include <list>
 #include <unordered_map>
 #include <vector>
 
@@ -16,22 +18,68 @@ namespace psf {
 // alone protects it (no per-message hipMallocAsync/hipFreeAsync packets in the
 // queue).  Shared by every Buffer the context allocates, so it outlives the
 // Context if buffers do.
+//
+// The free lists are bounded: the bytes they hold (HBM and pinned host memory
+// alike) stay under a per-context cap (Context::kDefaultCache*, or
+// psf_context_set_cache_limit).  A release that would pass the cap first
+// frees the least recently released blocks, after the stream has drained (a
+// block on a free list may still be in use by queued kernels).  A server that
+// sees many distinct message sizes therefore keeps at most the cap cached,
+// on top of what its live messages hold.
 struct Context::StreamHolder {
   int device;
   hipStream_t stream;
   bool own;
   std::mutex mu;
-  std::unordered_map<size_t, std::vector<void*>> free_lists;
-  std::unordered_map<size_t, std::vector<void*>> pinned_free;
+  struct Pool {
+    struct Entry {
+      size_t cls;
+      void* p;
+    };
+    std::list<Entry> lru;  // released blocks, oldest first
+    std::unordered_map<size_t, std::vector<std::list<Entry>::iterator>> by_class;  // per class, oldest first
+    size_t cached = 0, allocated = 0, cap = 0;
+    uint64_t evictions = 0;
+    void* take(size_t cls) {
+      auto it = by_class.find(cls);
+      if (it == by_class.end() || it->second.empty()) return nullptr;
+      auto e = it->second.back();  // the most recently released
+      it->second.pop_back();
+      void* p = e->p;
+      lru.erase(e);
+      cached -= cls;
+      return p;
+    }
+    // the blocks to free so that `extra` more cached bytes fit the cap
+    void make_room(size_t extra, std::vector<Entry>* out) {
+      while (!lru.empty() && cached + extra > cap) {
+        Entry e = lru.front();
+        auto& v = by_class[e.cls];
+        v.erase(v.begin());  // the class's oldest is the overall oldest of its class
+        lru.pop_front();
+        cached -= e.cls;
+        allocated -= e.cls;
+        ++evictions;
+        out->push_back(e);
+      }
+    }
+    void give(size_t cls, void* p) {
+      lru.push_back(Entry{cls, p});
+      by_class[cls].push_back(std::prev(lru.end()));
+      cached += cls;
+    }
+  };
+  Pool dev, host;
 
-  StreamHolder(int d, hipStream_t s, bool o) : device(d), stream(s), own(o) {}
+  StreamHolder(int d, hipStream_t s, bool o) : device(d), stream(s), own(o) {
+    dev.cap = kDefaultCacheBytes;
+    host.cap = kDefaultPinnedCacheBytes;
+  }
   ~StreamHolder() {
     (void)hipSetDevice(device);
     (void)hipStreamSynchronize(stream);
-    for (auto& kv : free_lists)
-      for (void* p : kv.second) (void)hipFree(p);
-    for (auto& kv : pinned_free)
-      for (void* p : kv.second) (void)hipHostFree(p);
+    for (auto& e : dev.lru) (void)hipFree(e.p);
+    for (auto& e : host.lru) (void)hipHostFree(e.p);
     if (own) (void)hipStreamDestroy(stream);
   }
   static size_t size_class(size_t bytes) {
@@ -43,43 +91,114 @@ struct Context::StreamHolder {
     }
     return (bytes + (1u << 20) - 1) & ~(size_t)((1u << 20) - 1);  // 1 MiB granules
   }
+  // release `evict` (taken out of a pool under the lock) once the stream has drained
+  void free_blocks(const std::vector<Pool::Entry>& evict, bool pinned) {
+    if (evict.empty()) return;
+    (void)hipStreamSynchronize(stream);
+    for (const auto& e : evict) (void)(pinned ? hipHostFree(e.p) : hipFree(e.p));
+  }
   void* get(size_t cls) {
     {
       std::lock_guard<std::mutex> l(mu);
-      auto it = free_lists.find(cls);
-      if (it != free_lists.end() && !it->second.empty()) {
-        void* p = it->second.back();
-        it->second.pop_back();
-        return p;
-      }
+      if (void* p = dev.take(cls)) return p;
     }
     void* p = nullptr;
-    PSF_HIP_CHECK(hipMalloc(&p, cls));
+    hipError_t e = hipMalloc(&p, cls);
+    if (e != hipSuccess) {  // out of HBM: drop every cached block, then once more
+      (void)hipGetLastError();
+      std::vector<Pool::Entry> evict;
+      {
+        std::lock_guard<std::mutex> l(mu);
+        const size_t c = dev.cap;
+        dev.cap = 0;
+        dev.make_room(0, &evict);
+        dev.cap = c;
+      }
+      free_blocks(evict, false);
+      PSF_HIP_CHECK(hipMalloc(&p, cls));
+    }
+    std::lock_guard<std::mutex> l(mu);
+    dev.allocated += cls;
     return p;
   }
   void put(size_t cls, void* p) {
-    std::lock_guard<std::mutex> l(mu);
-    free_lists[cls].push_back(p);
+    std::vector<Pool::Entry> evict;
+    bool drop = false;
+    {
+      std::lock_guard<std::mutex> l(mu);
+      if (cls > dev.cap) {  // larger than the whole cache: not kept
+        drop = true;
+        dev.allocated -= cls;
+        ++dev.evictions;
+      } else {
+        dev.make_room(cls, &evict);
+        dev.give(cls, p);
+      }
+    }
+    if (drop) evict.push_back(Pool::Entry{cls, p});
+    free_blocks(evict, false);
   }
   void* get_pinned(size_t cls) {
     {
       std::lock_guard<std::mutex> l(mu);
-      auto it = pinned_free.find(cls);
-      if (it != pinned_free.end() && !it->second.empty()) {
-        void* p = it->second.back();
-        it->second.pop_back();
-        return p;
-      }
+      if (void* p = host.take(cls)) return p;
     }
     void* p = nullptr;
     PSF_HIP_CHECK(hipHostMalloc(&p, cls, hipHostMallocMapped | hipHostMallocCoherent));
+    std::lock_guard<std::mutex> l(mu);
+    host.allocated += cls;
     return p;
   }
   void put_pinned(size_t cls, void* p) {
+    std::vector<Pool::Entry> evict;
+    bool drop = false;
+    {
+      std::lock_guard<std::mutex> l(mu);
+      if (cls > host.cap) {
+        drop = true;
+        host.allocated -= cls;
+        ++host.evictions;
+      } else {
+        host.make_room(cls, &evict);
+        host.give(cls, p);
+      }
+    }
+    if (drop) evict.push_back(Pool::Entry{cls, p});
+    free_blocks(evict, true);
+  }
+  void set_caps(size_t dev_cap, size_t host_cap) {
+    std::vector<Pool::Entry> ed, eh;
+    {
+      std::lock_guard<std::mutex> l(mu);
+      dev.cap = dev_cap;
+      host.cap = host_cap;
+      dev.make_room(0, &ed);
+      host.make_room(0, &eh);
+    }
+    free_blocks(ed, false);
+    free_blocks(eh, true);
+  }
+  void stats(MemoryStats* s) {
     std::lock_guard<std::mutex> l(mu);
-    pinned_free[cls].push_back(p);
+    s->dev_cached = dev.cached;
+    s->dev_cap = dev.cap;
+    s->dev_allocated = dev.allocated;
+    s->dev_evictions = dev.evictions;
+    s->host_cached = host.cached;
+    s->host_cap = host.cap;
+    s->host_allocated = host.allocated;
+    s->host_evictions = host.evictions;
   }
 };
+
+void Context::set_cache_limit(size_t dev_bytes, size_t pinned_bytes) {
+  if (holder_) holder_->set_caps(dev_bytes, pinned_bytes);
+}
+Context::MemoryStats Context::memory_stats() const {
+  MemoryStats s;
+  if (holder_) holder_->stats(&s);
+  return s;
+}
 
 // compress: the look-back words of up to 8191 fragments (512 MiB per launch);
 // uncompress: the control words of kSnappyBatchMax streams

@@ -80,6 +80,16 @@ class Context {
   void zero_pair_unused(int kind, const ZeroPair& z) {
     if (z.cur) zero_parity_[kind] ^= 1;
   }
+  // The caching allocator's bounds (bytes kept on the free lists, per
+  // context): HBM and pinned host memory.  Defaults below; see context.cc.
+  static constexpr size_t kDefaultCacheBytes = size_t(8) << 30;
+  static constexpr size_t kDefaultPinnedCacheBytes = size_t(1) << 30;
+  void set_cache_limit(size_t dev_bytes, size_t pinned_bytes);
+  struct MemoryStats {
+    uint64_t dev_cached = 0, dev_cap = 0, dev_allocated = 0, dev_evictions = 0;
+    uint64_t host_cached = 0, host_cap = 0, host_allocated = 0, host_evictions = 0;
+  };
+  MemoryStats memory_stats() const;
   // pooled timing-free events
   hipEvent_t take_event();
   void give_event(hipEvent_t e);

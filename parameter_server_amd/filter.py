@@ -79,6 +79,18 @@ class Context:
             check(lib().psf_context_host_stats_reset(self.h))
         return {k: (ns[i] / 1e9, cnt[i]) for i, k in enumerate(("sync", "publish", "slice"))}
 
+    def set_cache_limit(self, hbm_bytes: int, pinned_bytes: int) -> None:
+        check(lib().psf_context_set_cache_limit(self.h, hbm_bytes, pinned_bytes))
+
+    def memory_stats(self) -> dict:
+        """The caching allocator: bytes cached / cap / allocated and evictions,
+        for HBM ("hbm_*") and pinned host memory ("pinned_*")."""
+        out = (C.c_uint64 * 8)()
+        check(lib().psf_context_memory_stats(self.h, out))
+        keys = ("cached", "cap", "allocated", "evictions")
+        return {**{f"hbm_{k}": out[i] for i, k in enumerate(keys)},
+                **{f"pinned_{k}": out[4 + i] for i, k in enumerate(keys)}}
+
     def close(self):
         if self.h:
             lib().psf_context_destroy(self.h)
