@@ -63,7 +63,7 @@ WORKLOADS = {
           "{m} sorted unique uint64 keys spread over 2^64 (splitmix64) + f32 values, sliced at the "
           "EvenDivide({servers}) server ranges (servers in contiguous blocks per rank), "
           "per-(stream, server) [KEY_CACHING, FIXING_FLOAT num_bytes={nb}], cross-range slices spilled in "
-          "one all-to-all-v per step (RCCL), repeat sends (key cache hit)",
+          "one all-to-all-v per step (RCCL), {sends}",
     "c1": "C1 (BASELINE configs[0]) on the device: the ctr example's minibatch "
           "(example/linear/ctr/online_l1lr.conf:36-53) for {streams} concurrent streams of {m} sorted unique "
           "keys: pull request (keys, [KEY_CACHING, FIXING_FLOAT num_bytes={nb}]), pull response (keys elided "
@@ -72,7 +72,7 @@ WORKLOADS = {
     "c5": "C5 (BASELINE configs[4]) per GPU: one stream of {m} uint64 keys spread over 2^64 "
           "(splitmix64) + embedding rows dim=128 f32, sliced at the EvenDivide({servers}) server ranges "
           "(k = 128 values per key), per-(stream, server) [KEY_CACHING, FIXING_FLOAT num_bytes={nb}{cmp}], "
-          "cross-range slices spilled in one all-to-all-v per step, repeat sends (key cache hit)",
+          "cross-range slices spilled in one all-to-all-v per step, {sends}",
 }
 
 
@@ -104,6 +104,9 @@ def parse(argv=None):
     ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c3miss", "c4", "c5"])
     ap.add_argument("--m", type=int, default=None, help="keys per message (c1 1e5, c3 10M, c4 2^21, c5 2^20)")
     ap.add_argument("--compress", action="store_true", help="append COMPRESSING to the chain (c5)")
+    ap.add_argument("--miss", action="store_true",
+                    help="c4/c5: KEY_CACHING(clear_cache_if_done): every send a key cache miss (keys travel, "
+                         "and are compressed with --compress)")
     ap.add_argument("--launch-check", action="store_true",
                     help="start the ranks and the process group only (no GPU work); for CPU tests")
     return ap.parse_args(argv)
@@ -184,6 +187,9 @@ def cpu_baseline(args, nb: int):
             P.key_signature(keys)   # KEY_CACHING encode: CRC of the first <= 2 KiB
             if decode_crc:
                 P.key_signature(keys)  # decode checks the CRC when keys travel
+                if args.compress:  # a miss: the keys travel, snappy-compressed
+                    c = P.snappy_compress(keys.view(np.uint8))
+                    P.snappy_uncompress(c, cap=keys.nbytes + 64)
             rt()
         return f
 
@@ -229,7 +235,7 @@ def cpu_baseline(args, nb: int):
             for d in range(args.servers):
                 lo, hi = int(pos[d]), int(pos[d + 1])
                 if hi > lo:
-                    tasks.append(kc_ff(keys[lo:hi], x[lo * dim:hi * dim], False))
+                    tasks.append(kc_ff(keys[lo:hi], x[lo * dim:hi * dim], args.miss))
             payload += keys.nbytes + x.nbytes
         what = (f"{nstreams} stream(s) of {m} keys (dim {dim}) sliced over {args.servers} servers, "
                 f"[KEY_CACHING, FIXING_FLOAT(nb={nb}){', COMPRESSING' if args.compress else ''}] per slice")
@@ -298,7 +304,8 @@ def build_workload(args, F, ctx, rank, world, dev, g, n):
 
         def run(k):
             F.RemoteNode.roundtrip_many(snd, rcv, tmpls, k, phase_end=[S, 2 * S, 3 * S])
-        return run, 32 * m * S, 2 * m * S, {}
+        # keys travel with the pull request only; the response and the push hit
+        return run, 32 * m * S, 2 * m * S, {"key_bytes_elided": 16 * m * S}
     if args.config in ("c4", "c5"):
         # streams sliced at the server ranges, encoded
         # per destination server, spilled (one all-to-all-v) and decoded
@@ -307,7 +314,7 @@ def build_workload(args, F, ctx, rank, world, dev, g, n):
             raise SystemExit(f"--servers {args.servers} < {world} ranks")
         ex = shard.SpillExchange(ctx, device=dev) if world > 1 else None
         router = shard.PushRouter(ctx, shard.server_ranges(args.servers), rank, world, ex)
-        streams, nloc, payload = {}, 0, 0
+        streams, nloc, payload, elided = {}, 0, 0, 0
         if args.config == "c4":
             m, dim, sids = args.m or (1 << 21), 1, range(rank, args.streams, world)
         else:
@@ -317,17 +324,18 @@ def build_workload(args, F, ctx, rank, world, dev, g, n):
             t = F.Message(request=True, push=True, key_channel=sid, key_range=shard.KEY_ALL)
             t.set_key(keys)
             t.add_value(torch.randn(keys.numel() * dim, device=dev, generator=g, dtype=torch.float32))
-            t.add_filter(KEY_CACHING)
+            t.add_filter(KEY_CACHING, clear_cache_if_done=True if args.miss else None)
             t.add_filter(FIXING_FLOAT, num_bytes=nb)
             if args.compress:
                 t.add_filter(COMPRESSING)
             streams[sid] = t
             nloc += keys.numel() * dim
             payload += keys.numel() * (8 + 4 * dim)
+            elided += 0 if args.miss else 8 * keys.numel()
 
         def run(k):
             router.run(streams, k)
-        return run, payload, nloc, {"router": router}
+        return run, payload, nloc, {"router": router, "key_bytes_elided": elided}
     worker, server = F.RemoteNode(ctx), F.RemoteNode(ctx)
     tmpls = []
     if args.config == "c2":
@@ -361,7 +369,7 @@ def build_workload(args, F, ctx, rank, world, dev, g, n):
 
     def run(k):
         worker.roundtrip(server, tmpls, k)
-    return run, payload, n, {}
+    return run, payload, n, {"key_bytes_elided": 8 * m if args.config == "c3" else 0}
 
 
 def timed(run, steps, world, dist, ctx, prof_kernel=None, stride=1):
@@ -546,7 +554,9 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "strong" if args.config == "c4" else "weak",
+            # C4's 64 streams are split over the ranks (total work fixed): strong
+            # scaling once there is more than one rank
+            "scaling": "strong" if args.config == "c4" and world_pg > 1 else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic: f32 N(0,1) values, seed 1+rank, FIXING_FLOAT LCG seed 12345"
@@ -555,9 +565,12 @@ def main():
                        "c1": "; sorted unique uint64 keys from [0,1e9) per stream"}.get(
                         args.config, "; sorted unique uint64 keys from [0,1e9)"),
             "config": {
-                "workload": WORKLOADS[args.config].format(nb=nb, cmp=", COMPRESSING" if args.compress else "",
-                                                          streams=args.streams, servers=args.servers,
-                                                          m=args.m or m_default),
+                "workload": WORKLOADS[args.config].format(
+                    nb=nb, cmp=", COMPRESSING" if args.compress else "", streams=args.streams,
+                    servers=args.servers, m=args.m or m_default,
+                    sends=("every send a key cache miss (KEY_CACHING clear_cache_if_done; keys travel"
+                           + (", snappy-compressed)" if args.compress else ")")) if args.miss
+                    else "repeat sends (key cache hit)"),
                 "n_values_per_gpu": n,
                 "payload_bytes_per_step_per_gpu": payload,
                 "value_type": "float32",
@@ -573,6 +586,10 @@ def main():
         }
         if host:
             line["host"] = host
+        if "key_bytes_elided" in extra:
+            # payload counts key bytes before encode; on a
+            # KEY_CACHING hit they are elided, so these bytes move nowhere
+            line["config"]["key_bytes_elided_per_step_per_gpu"] = extra["key_bytes_elided"]
         if spill:
             line["config"]["spill_bytes_per_step_rank0"] = spill // max(args.steps, 1)
         if also:

@@ -247,3 +247,47 @@ def test_scenarios_match_restatement(scenario_golden, which):
     for g, w in zip(got, want):
         assert g == w, (g["name"], g, w)
     assert len(got) == len(want)
+
+
+def test_c3_10m_keys_miss_then_hit_vs_port(ctx, port):
+    """BASELINE configs[2] (C3) at its stated size: 10M sorted unique uint64
+    keys sampled from [0, 1e9) (1 % density) + 10M f32, chain [KEY_CACHING,
+    FIXING_FLOAT nb=1].  The first send misses (keys travel, the receiver
+    checks the CRC and caches them), the repeat hits (keys elided on the wire,
+    restored by the receiver); signatures, codes, side-info and all 10M
+    decoded values byte for byte against the restatement
+    (key_caching.h:9-60, fixing_float.h:50-101)."""
+    from parameter_server_amd import FIXING_FLOAT, KEY_CACHING
+    from parameter_server_amd import filter as F
+    rng = np.random.default_rng(3)
+    keys = np.sort(rng.choice(10**9, 10_000_000, replace=False)).astype(np.uint64)
+    kd = torch.from_numpy(keys.view(np.int64)).to(DEV)
+    worker, server = F.RemoteNode(ctx), F.RemoteNode(ctx)
+    sig_want = port.key_signature(keys)
+    F.set_clock(777)
+    try:
+        for send in range(2):
+            x = rng.standard_normal(keys.size).astype(np.float32)
+            m = F.Message(request=True, push=True, key_channel=3, key_range=(0, 10**9))
+            m.set_key(kd)
+            m.add_value(torch.from_numpy(x).to(DEV))
+            m.add_filter(KEY_CACHING)
+            fi = m.add_filter(FIXING_FLOAT, num_bytes=1)
+            worker.encode(m)
+            assert m.signature(0) == (True, sig_want), send
+            wire_keys = m.key_ptr()[1]
+            assert wire_keys == (keys.nbytes if send == 0 else 0), send  # elided on the hit
+            st, pc, pmn, pmx = port.ff_encode(x, 1, 777)
+            assert st == 0
+            (has_mn, mn, has_mx, mx), = m.fixed_points(fi)
+            assert _bits(mn) == _bits(pmn) and _bits(mx) == _bits(pmx)
+            assert np.array_equal(worker.value(m, 0).cpu().numpy(), pc), send
+            w = m.clone()
+            server.decode(w)
+            got_keys = server.key(w).cpu().numpy().view(np.uint64)
+            assert np.array_equal(got_keys, keys), send  # restored from the cache on the hit
+            st, pd = port.ff_decode(pc, 1, pmn, pmx, np.float32)
+            assert server.value(w, 0).cpu().numpy().tobytes() == pd.tobytes(), send
+            del m, w
+    finally:
+        F.set_clock(None)
