@@ -4,6 +4,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <atomic>
 #include <set>
 #include <string>
@@ -560,10 +561,12 @@ int psf_node_roundtrip_ex(psf_node* snd, psf_node* rcv, const psf_message* const
     for (int i = 0; i < iters; ++i) {
       psf::Message m = tmpls[i % ntmpl]->m;  // fresh Task + zero-copy buffers
       psf::Message* mp = &m;
-      psf::encode_batch(&s, &mp, 1);  // = EncodeMessage, side-info left on the device
-      psf::Message w = m;             // delivered copy (van: Task frame + data frames)
+      psf::KeySigHint eh, dh;  // the iteration's KEY_CACHING CRCs, one wait
+      psf::presign_roundtrip(&s, &mp, 1, &eh, &dh);
+      psf::encode_batch(&s, &mp, 1, &eh);  // = EncodeMessage, side-info left on the device
+      psf::Message w = m;                  // delivered copy (van: Task frame + data frames)
       psf::Message* wp = &w;
-      psf::decode_batch(&r, &wp, 1);  // = DecodeMessage
+      psf::decode_batch(&r, &wp, 1, &dh);  // = DecodeMessage
       if (i == iters - 1) {
         if (enc_out) last_enc = new psf_message{m};
         if (dec_out) last_dec = new psf_message{w};
@@ -631,7 +634,16 @@ int psf_nodes_roundtrip_ex(psf_node* const* snd, psf_node* const* rcv, const psf
     }
     std::vector<psf::Message> m(n), w(n);
     std::vector<psf::Message*> mp(n), wp(n);
+    std::vector<const psf::Message*> tp(n);
+    for (int i = 0; i < n; ++i) tp[i] = &tmpls[i]->m;
+    std::vector<psf::KeySigHint> eh(n), dh(n);
     for (int it = 0; it < iters; ++it) {
+      {  // every KEY_CACHING CRC of the iteration (all phases), one wait
+        PSF_HPROF(12);
+        std::fill(eh.begin(), eh.end(), psf::KeySigHint{});
+        std::fill(dh.begin(), dh.end(), psf::KeySigHint{});
+        psf::presign_roundtrip(s.data(), tp.data(), n, eh.data(), dh.data());
+      }
       int b = 0;
       for (int e : ends) {  // phase [b, e): encode all, deliver, decode all
         {
@@ -643,7 +655,7 @@ int psf_nodes_roundtrip_ex(psf_node* const* snd, psf_node* const* rcv, const psf
         }
         {
           PSF_HPROF(1);
-          psf::encode_batch(s.data() + b, mp.data() + b, e - b);
+          psf::encode_batch(s.data() + b, mp.data() + b, e - b, eh.data() + b);
         }
         {
           PSF_HPROF(5);
@@ -654,7 +666,7 @@ int psf_nodes_roundtrip_ex(psf_node* const* snd, psf_node* const* rcv, const psf
         }
         {
           PSF_HPROF(6);
-          psf::decode_batch(r.data() + b, wp.data() + b, e - b);
+          psf::decode_batch(r.data() + b, wp.data() + b, e - b, dh.data() + b);
         }
         b = e;
       }

@@ -175,7 +175,18 @@ struct PendingEncode {
 };
 void encode_batch(RemoteNode* const* nodes, Message* const* msgs, int n, const KeySigHint* hints = nullptr,
                   PendingEncode* pend = nullptr);
-void decode_batch(RemoteNode* const* nodes, Message* const* msgs, int n);
+// hints: as encode_batch's, for the receiver's check of keys that arrive
+// (key_caching.h:43): used only while the message's key is that buffer.
+void decode_batch(RemoteNode* const* nodes, Message* const* msgs, int n, const KeySigHint* hints = nullptr);
+// The in-process round-trip drivers (psf_node(s)_roundtrip_ex) deliver the
+// sender's key buffer itself, zero-copy and unchanged, so every KEY_CACHING
+// CRC of an iteration can be queued up front: per distinct device key buffer
+// of msgs (chains with KEY_CACHING), one CRC job for the sender's signature
+// (key_caching.h:18) and one more over the same bytes for the receiver's
+// check (key_caching.h:43), all in one batch with one host wait; enc[i] /
+// dec[i] receive them (left empty for host keys and key-less messages).
+void presign_roundtrip(RemoteNode* const* nodes, const Message* const* msgs, int n, KeySigHint* enc,
+                       KeySigHint* dec);
 
 // Run the dequantise a deferred FIXING_FLOAT decode left pending (every
 // pending value array of msg becomes decoded data, as DecodeMessage would

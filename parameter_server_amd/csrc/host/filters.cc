@@ -646,6 +646,68 @@ static void launch_signatures(RemoteNode* const* nodes, Message* const* msgs, co
   }
 }
 
+void presign_roundtrip(RemoteNode* const* nodes, const Message* const* msgs, int n, KeySigHint* enc,
+                       KeySigHint* dec) {
+  struct Job {
+    const uint8_t* ptr;
+    size_t bytes;
+    std::vector<int> users;
+    uint32_t tk[2];
+  };
+  std::map<Context*, std::vector<Job>> by_ctx;
+  std::map<std::pair<const uint8_t*, size_t>, std::pair<Context*, size_t>> seen;
+  for (int i = 0; i < n; ++i) {
+    const Message& m = *msgs[i];
+    if (!m.has_key() || m.key.loc != Loc::kDevice || !Filter::find(FilterConfig::KEY_CACHING, const_cast<Message*>(&m)))
+      continue;
+    Context* ctx = nodes[i]->ctx();
+    if (ctx->device() < 0) continue;
+    const auto id = std::make_pair((const uint8_t*)m.key.ptr, m.key.bytes);
+    auto it = seen.find(id);
+    if (it == seen.end() || it->second.first != ctx) {
+      auto& v = by_ctx[ctx];
+      seen[id] = {ctx, v.size()};
+      v.push_back(Job{m.key.ptr, m.key.bytes, {i}, {0, 0}});
+    } else {
+      by_ctx[ctx][it->second.second].users.push_back(i);
+    }
+  }
+  constexpr size_t kPer = (size_t)Context::kSyncSlots / 2;  // jobs (x2 CRCs) in flight per wait
+  for (auto& kv : by_ctx) {
+    Context* ctx = kv.first;
+    std::vector<Job>& jobs = kv.second;
+    for (size_t b = 0; b < jobs.size(); b += kPer) {
+      const size_t e = std::min(jobs.size(), b + kPer);
+      // CRC 2q: the sender's signature of job q; CRC 2q + 1: the receiver's check
+      std::vector<const void*> d;
+      std::vector<uint32_t> len, tk;
+      std::vector<int> slot;
+      for (size_t q = b; q < e; ++q)
+        for (int r = 0; r < 2; ++r) {
+          jobs[q].tk[r] = ctx->next_ticket();
+          d.push_back(jobs[q].ptr);
+          len.push_back((uint32_t)std::min(jobs[q].bytes, (size_t)2048));
+          tk.push_back(jobs[q].tk[r]);
+          slot.push_back((int)(2 * (q - b) + r));
+        }
+      for (size_t c = 0; c < d.size(); c += (size_t)kCrcBatchMax) {
+        const int cnt = (int)std::min(d.size() - c, (size_t)kCrcBatchMax);
+        int st = crc32c_batch_launch(d.data() + c, len.data() + c, slot.data() + c, tk.data() + c, cnt,
+                                     ctx->pub_dev(0), ctx->stream(), ctx->prof());
+        if (st != kOk) throw CheckError(st, "crc32c batch launch failed");
+      }
+      for (size_t q = b; q < e; ++q) {
+        const uint32_t se = ctx->wait_crc((int)(2 * (q - b)), jobs[q].tk[0]);
+        const uint32_t sd = ctx->wait_crc((int)(2 * (q - b) + 1), jobs[q].tk[1]);
+        for (int i : jobs[q].users) {
+          enc[i] = KeySigHint{jobs[q].ptr, jobs[q].bytes, se};
+          if (dec) dec[i] = KeySigHint{jobs[q].ptr, jobs[q].bytes, sd};
+        }
+      }
+    }
+  }
+}
+
 // Encode in filter order, position by position over all chains.  The
 // KEY_CACHING signatures of a position stay in flight while a following
 // all-FIXING_FLOAT position launches (the two touch disjoint parts of a
@@ -723,7 +785,7 @@ void encode_batch(RemoteNode* const* nodes, Message* const* msgs, int n, const K
   finish_kc();
 }
 
-void decode_batch(RemoteNode* const* nodes, Message* const* msgs, int n) {
+void decode_batch(RemoteNode* const* nodes, Message* const* msgs, int n, const KeySigHint* hints) {
   size_t maxlen = 0;
   for (int i = 0; i < n; ++i) {
     maxlen = std::max(maxlen, msgs[i]->task.filter.size());
@@ -755,7 +817,7 @@ void decode_batch(RemoteNode* const* nodes, Message* const* msgs, int n) {
     if (!kc.empty()) {
       PSF_HPROF(8);
       SigBatch sb;
-      launch_signatures(nodes, msgs, kc_sig, false, &sb);
+      launch_signatures(nodes, msgs, kc_sig, false, &sb, hints);
       size_t k = 0;
       for (int i : kc) {
         const size_t len = msgs[i]->task.filter.size();
