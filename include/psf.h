@@ -74,12 +74,6 @@ const char* psf_version(void);
  * enable=1 pins it to `t` process-wide (parity testing), enable=0 restores it. */
 void psf_set_clock(int enable, int64_t t);
 
-/* Debug knob (testing the bounded device waits): snappy compress launches
- * that follow never publish fragment `fragment` of their look-back chain
- * (< 0: none, the default) and give up after `spin_cap` polls of a wait
- * (0: the default cap), so the call returns PSF_ERR_TIMEOUT instead of
- * waiting.  Process-wide. */
-void psf_debug_snappy_stall(int64_t fragment, uint32_t spin_cap);
 
 /* The device the reference-side adapter (include/psf_ps_filter.h) creates
  * its contexts on: the last psf_set_default_device(d), else the PSF_DEVICE
@@ -107,6 +101,15 @@ int psf_context_sync(psf_context* ctx);
 /* Ordered on the context's stream, then synchronous: copy `bytes` from a
  * buffer the library returned (device or host) into host memory. */
 int psf_copy_to_host(psf_context* ctx, void* dst, const void* src, size_t bytes);
+/* The same, left in flight on the context's stream (complete after
+ * psf_context_sync). */
+int psf_copy_to_host_async(psf_context* ctx, void* dst, const void* src, size_t bytes);
+/* A pinned host buffer of `bytes` from the context's pool (the fast target of
+ * the copies above); released with psf_host_buffer_release(*handle), which
+ * may outlive the context.  The adapter hands these out as the reference's
+ * zero-copy SArrays with a custom deleter (van.cc:244-255's pattern). */
+int psf_host_buffer_alloc(psf_context* ctx, size_t bytes, void** ptr, void** handle);
+int psf_host_buffer_release(void* handle);
 
 /* ---- layer 1: codec kernels (device pointers, async unless noted) ------ */
 typedef struct {

@@ -393,8 +393,7 @@ class Chain {
         k = it->second;  // a host key the cache refers to: shared, as key_caching.h:55 shares it
       } else {
         CHECK_EQ(kloc, PSF_LOC_DEVICE) << "libpsf chain: host key of unknown owner";
-        k = SArray<char>(kb);
-        Check(psf_copy_to_host(ctx_, k.data(), kp, kb));
+        k = HostArray(kp, kb);
       }
       if (had_key) msg->key = k;  // a codec's output replaces the key (compressing.h:14,30)
       else msg->set_key(k);       // restored (key_caching.h:55, set_key<char>)
@@ -412,12 +411,29 @@ class Chain {
       int loc = 0;
       Check(psf_msg_value(m, (int)i, &p, &bytes, &loc));
       if (p == msg->value[i].data() && bytes == msg->value[i].size()) continue;
-      SArray<char> out(bytes);
-      if (bytes) Check(psf_copy_to_host(ctx_, out.data(), p, bytes));
-      msg->value[i] = out;
+      msg->value[i] = HostArray(p, bytes);
     }
+    // one wait for every copy; the device buffers go back to the pool
+    // (stream-ordered) with the message
+    const int synced = psf_context_sync(ctx_);
     psf_msg_destroy(m);
+    Check(synced);
     return true;
+  }
+
+  // a chain output as a new SArray<char> in pinned host memory (the copy's
+  // fast target), filled by a copy left in flight until the chain's one
+  // sync; the SArray's last owner returns it to the context's pool, as the
+  // reference's zero-copy receive frees a frame (van.cc:244-255)
+  SArray<char> HostArray(const void* src, size_t bytes) {
+    if (bytes == 0) return SArray<char>();
+    void* p = nullptr;
+    void* h = nullptr;
+    Check(psf_host_buffer_alloc(ctx_, bytes, &p, &h));
+    SArray<char> out(static_cast<char*>(p), bytes, false);
+    out.pointer().reset(static_cast<char*>(p), [h](char*) { psf_host_buffer_release(h); });
+    Check(psf_copy_to_host_async(ctx_, p, src, bytes));
+    return out;
   }
 
   psf_context* ctx_ = nullptr;

@@ -79,6 +79,13 @@ template <typename V> class SArray {
  public:
   SArray() {}
   explicit SArray(size_t n) { resize(n); }
+  // zero-copy constructor (shared_array.h:57-59, reset in shared_array_inl.h:54-66)
+  SArray(V* data, size_t size, bool deletable = true) {
+    size_ = cap_ = size;
+    if (deletable) ptr_.reset(reinterpret_cast<char*>(data), std::default_delete<char[]>());
+    else ptr_.reset(reinterpret_cast<char*>(data), [](char*) {});
+  }
+  std::shared_ptr<char>& pointer() { return ptr_; }  // (the reference's is shared_ptr<void>)
   template <typename W> explicit SArray(const SArray<W>& o) {
     size_ = o.size() * sizeof(W) / sizeof(V);
     ptr_ = o.ptr();

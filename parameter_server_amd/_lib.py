@@ -20,7 +20,7 @@ PSF_ERR_BIN = -3
 PSF_ERR_HIP = -4
 PSF_ERR_CHECK = -5
 PSF_ERR_UNSUPPORTED = -6
-PSF_ERR_TIMEOUT = -7
+PSF_ERR_TIMEOUT = -7  # (no current entry point returns it)
 
 DT_UINT64, DT_FLOAT, DT_DOUBLE, DT_CHAR = 8, 9, 10, 11
 KEY_CACHING, COMPRESSING, FIXING_FLOAT, NOISE = 1, 2, 3, 4
@@ -46,13 +46,15 @@ SIGNATURES = {
     "psf_last_error": ([], C.c_char_p),
     "psf_version": ([], C.c_char_p),
     "psf_set_clock": ([C.c_int, C.c_int64], None),
-    "psf_debug_snappy_stall": ([C.c_int64, u32], None),
     "psf_set_default_device": ([C.c_int], C.c_int),
     "psf_default_device": ([], C.c_int),
     "psf_context_create": ([C.c_int, vp, C.c_int, C.POINTER(vp)], C.c_int),
     "psf_context_destroy": ([vp], C.c_int),
     "psf_context_sync": ([vp], C.c_int),
     "psf_copy_to_host": ([vp, vp, vp, sz], C.c_int),
+    "psf_copy_to_host_async": ([vp, vp, vp, sz], C.c_int),
+    "psf_host_buffer_alloc": ([vp, sz, C.POINTER(vp), C.POINTER(vp)], C.c_int),
+    "psf_host_buffer_release": ([vp], C.c_int),
     "psf_ff_encode": ([vp, vp, sz, C.c_int, C.c_int, C.POINTER(FixedPoint), i32, vp], C.c_int),
     "psf_ff_encode_async": ([vp, vp, sz, C.c_int, C.c_int, C.POINTER(FixedPoint), i32, vp, vp, vp], C.c_int),
     "psf_ff_decode": ([vp, vp, sz, C.c_int, C.c_int, C.c_float, C.c_float, vp], C.c_int),

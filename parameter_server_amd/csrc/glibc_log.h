@@ -1,4 +1,7 @@
 // log(double) exactly as the reference's libm computes it.
+// License: the algorithm and the table values are glibc's (sysdeps/ieee754/{f,dbl}-64/e_log*.c,
+// GNU LGPL v2.1 or later; originally Arm's optimized-routines, MIT), restated here; this
+// file is distributed under those terms.
 //
 // NOISE (add_noise.h:29-39) on DOUBLE values calls std::log(double) inside
 // libstdc++'s polar method; on the reference's platform that is glibc's log

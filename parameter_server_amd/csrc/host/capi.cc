@@ -59,7 +59,6 @@ extern "C" {
 const char* psf_last_error(void) { return g_last_error.c_str(); }
 const char* psf_version(void) { return "psf 0.1 gfx950"; }
 void psf_set_clock(int enable, int64_t t) { psf::set_clock_override(enable != 0, t); }
-void psf_debug_snappy_stall(int64_t fragment, uint32_t spin_cap) { psf::snappy_debug_stall(fragment, spin_cap); }
 
 static std::atomic<int> g_default_device{-1};
 int psf_set_default_device(int device) {
@@ -111,6 +110,35 @@ int psf_copy_to_host(psf_context* ctx, void* dst, const void* src, size_t bytes)
     c.sync();
     return PSF_OK;
   });
+}
+
+int psf_copy_to_host_async(psf_context* ctx, void* dst, const void* src, size_t bytes) {
+  return guarded([&] {
+    if (!ctx || (bytes && (!dst || !src))) return PSF_ERR_ARG;
+    if (bytes == 0) return PSF_OK;
+    psf::Context& c = *ctx->impl;
+    if (c.device() < 0) { memcpy(dst, src, bytes); return PSF_OK; }
+    PSF_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, c.stream()));
+    return PSF_OK;
+  });
+}
+
+// a pinned host buffer from the context's pool; the handle owns it (and keeps
+// the pool alive after the context is gone)
+int psf_host_buffer_alloc(psf_context* ctx, size_t bytes, void** ptr, void** handle) {
+  return guarded([&] {
+    if (!ctx || !ptr || !handle) return PSF_ERR_ARG;
+    psf::Context& c = *ctx->impl;
+    if (c.device() < 0) return PSF_ERR_ARG;
+    psf::Context::Pinned p = c.pinned(bytes ? bytes : 1);
+    *ptr = p.host;
+    *handle = new std::shared_ptr<void>(p.owner);
+    return PSF_OK;
+  });
+}
+int psf_host_buffer_release(void* handle) {
+  delete static_cast<std::shared_ptr<void>*>(handle);
+  return PSF_OK;
 }
 
 // ---------------------------------------------------------------- kernels

@@ -189,9 +189,6 @@ int noise_apply_launch(void* v, const void* z, size_t n, int value_type, float m
 // snappy_max_compressed(n) bytes; the stream length is published to pub->size.
 constexpr uint32_t kSnappyFragOut = 76544;  // >= MaxCompressedLength(64 KiB), 256-aligned
 size_t snappy_max_compressed(size_t n);
-// debug: the compress launches that follow never publish fragment `frag` (< 0:
-// none) and give up after `spin_cap` look-back polls (0: the default)
-void snappy_debug_stall(int64_t frag, uint32_t spin_cap);
 size_t snappy_compress_scratch(size_t n);
 int snappy_compress_launch(const void* in, size_t n, void* out, void* scratch, hipStream_t st,
                            Profiler* prof, PubSlot* pub, uint32_t ticket);

@@ -4,19 +4,16 @@
 //
 // Compress.  A snappy stream is varint32(n) followed by the greedy LZ77 parse
 // of each 64 KiB input fragment, and every fragment is parsed on its own (fresh
-// hash table, no references across fragments).  So one wave parses one
-// fragment at a time: the fragment and its hash table live in LDS, the wave
-// runs the exact 1.1.8 parse with lane-parallel helpers -- 64 speculative
-// probes of the skip heuristic per step (the probe positions do not depend on
-// the data, only on where the skip loop started), match extension 64 bytes per
-// step, literal bytes copied 64 per step.  Tags go to a fixed-stride scratch
-// slot; at the end of the parse the fragment's length is known, a decoupled
-// look-back over the fragments before it (taken in order through an atomic
-// ticket) gives its offset in the stream, and the tags and the final literal
-// (all of an incompressible fragment, read from the input) are copied to their
-// place.  Persistent workgroups pipeline this over rounds: while wave 0 parses
-// one fragment, three waves place the one parsed before and four hold the next
-// in registers (snappy_compress_frags).
+// hash table, no references across fragments).  A wave runs the exact 1.1.8
+// parse of a fragment with lane-parallel helpers -- 64 speculative probes of
+// the skip heuristic per step (the probe positions do not depend on the data,
+// only on where the skip loop started), match extension 64 bytes per step,
+// literal bytes copied 64 per step.  Fragments with no match at all (one
+// literal: incompressible data) are found first by a probe-only pass that
+// reads the input where the skip loop probes; the others are parsed in LDS.
+// Fragment offsets come from a per-stream scan of the fragment lengths, and a
+// last launch places tags and literals (snappy_parse / _scan / _place;
+// no workgroup waits for another).
 //
 // Uncompress accepts any valid snappy stream (a reference sender's included)
 // and reproduces RawUncompress's verdict.  First every output fragment is
@@ -35,6 +32,7 @@
 // but valid) is decoded by one lane instead (K5).
 #include "psf_internal.h"
 
+#include <algorithm>
 #include <atomic>
 #include "ff_dequant.h"
 
@@ -74,8 +72,9 @@ __device__ __forceinline__ uint32_t hash(uint32_t v, int shift) { return (v * kM
 
 constexpr uint32_t kMinSlots = 4096;
 
+// the parse of one fragment (kSkip is kept beside it, in LDS: no
+// vector-memory wait in the loop)
 struct CompressLds {
-  uint32_t skip[kSkipN + 3];  // kSkip, read from LDS: no vector-memory wait in the loop
   uint32_t src[kFrag / 4 + 8];
   uint16_t table[kMaxTable];
   uint32_t minlane[kMinSlots];  // per hash slot: lowest lane of the step that probed it
@@ -94,16 +93,28 @@ __device__ uint32_t emit_literal(uint8_t* out, uint32_t op, const uint8_t* srcb,
     if (lane >= 1 && lane <= count) out[op + lane] = (uint8_t)(n >> (8 * (lane - 1)));
     hl += count;
   }
-  // the literal bytes: byte stores up to the first 4-aligned output position,
-  // then whole dwords composed from LDS (ld32 reads unaligned), then the tail
+  // the literal bytes: byte stores up to the first aligned output position,
+  // then whole dwords (16-byte chunks for long literals) composed from LDS
+  // (ld32 reads unaligned), then the tail.  `out` is 16-byte aligned.
   const uint32_t d0 = op + hl, d1 = d0 + len;
+  const uint32_t* s32 = reinterpret_cast<const uint32_t*>(srcb);
+  if (len >= 256) {
+    const uint32_t a0 = (d0 + 15) & ~15u, a1 = d1 & ~15u;
+    if (lane < a0 - d0) out[d0 + lane] = srcb[lit + lane];
+    uint4* o16 = reinterpret_cast<uint4*>(out);
+    for (uint32_t j = (a0 >> 4) + lane; j < (a1 >> 4); j += kLanes) {
+      const uint32_t q = lit + (16 * j - d0);
+      o16[j] = make_uint4(ld32(s32, q), ld32(s32, q + 4), ld32(s32, q + 8), ld32(s32, q + 12));
+    }
+    if (lane < d1 - a1) out[a1 + lane] = srcb[lit + (a1 - d0) + lane];
+    return d1;
+  }
   const uint32_t a0 = (d0 + 3) & ~3u, a1 = d1 & ~3u;
   if (a0 >= a1) {
     for (uint32_t i = lane; i < len; i += kLanes) out[d0 + i] = srcb[lit + i];
     return d1;
   }
   if (lane < a0 - d0) out[d0 + lane] = srcb[lit + lane];
-  const uint32_t* s32 = reinterpret_cast<const uint32_t*>(srcb);
   uint32_t* o32 = reinterpret_cast<uint32_t*>(out);
   for (uint32_t j = (a0 >> 2) + lane; j < (a1 >> 2); j += kLanes) o32[j] = ld32(s32, lit + (4 * j - d0));
   if (lane < d1 - a1) out[a1 + lane] = srcb[lit + (a1 - d0) + lane];
@@ -170,49 +181,6 @@ __device__ __forceinline__ uint4 shfl_down1(const uint4& v) {
                     __shfl_down(v.w, 1, 64));
 }
 
-constexpr int kPlaceW = 7;   // placing waves (1-7)
-constexpr int kPlaceU = 10;  // rows of 63 chunks per placing wave per round: 69 KiB per round
-
-// dst[0, len) = s[0, len), any alignment of either, by the 448 lanes of waves
-// 1-7 (pt = 0..447).  A wave takes rows of 63 destination chunks (16 bytes
-// each): lane l loads the aligned source block under chunk l of the row, and
-// a chunk's second block is the next lane's (lane 63 only loads).  Each round
-// issues all of its loads before its stores: a wave's memory counter retires
-// in order, so loads queued behind stores would wait for them.  Reads stay
-// inside 16-byte blocks that hold source bytes.
-__device__ void place_copy(uint8_t* __restrict__ dst, const uint8_t* __restrict__ s, uint32_t len, uint32_t pt,
-                           uint32_t lane) {
-  const uint32_t head = (uint32_t)(-reinterpret_cast<uintptr_t>(dst) & 15);
-  if (head >= len) {
-    if (pt < len) dst[pt] = s[pt];
-    return;
-  }
-  if (pt < head) dst[pt] = s[pt];
-  const uint32_t nc = (len - head) >> 4;
-  const uintptr_t sp = reinterpret_cast<uintptr_t>(s + head);
-  const uint4* s16 = reinterpret_cast<const uint4*>(sp & ~(uintptr_t)15);
-  const uint32_t sh = (uint32_t)(sp & 15);
-  const uint32_t lim = nc + (sh ? 1u : 0u);  // blocks that hold source bytes
-  uint4* d16 = reinterpret_cast<uint4*>(dst + head);
-  const uint32_t wv = pt >> 6;
-  for (uint32_t c0 = 0; c0 < nc; c0 += kPlaceU * kPlaceW * 63) {
-    uint4 lo[kPlaceU];
-#pragma unroll
-    for (int u = 0; u < kPlaceU; ++u) {
-      const uint32_t c = c0 + (u * kPlaceW + wv) * 63 + lane;
-      lo[u] = c < lim ? s16[c] : make_uint4(0, 0, 0, 0);
-    }
-#pragma unroll
-    for (int u = 0; u < kPlaceU; ++u) {
-      const uint32_t c = c0 + (u * kPlaceW + wv) * 63 + lane;
-      const uint4 hi = shfl_down1(lo[u]);
-      if (lane < 63 && c < nc) d16[c] = funnel16(lo[u], hi, sh);
-    }
-  }
-  const uint32_t t0 = head + 16 * nc;
-  if (pt < len - t0) dst[t0 + pt] = s[t0 + pt];
-}
-
 // snappy's literal tag for a literal of len bytes at p (lanes pt 0..4)
 __device__ __forceinline__ uint32_t literal_tag(uint8_t* p, uint32_t len, uint32_t pt) {
   const uint32_t m = len - 1;
@@ -259,10 +227,9 @@ __device__ uint64_t g_dfrag_trace[kTraceFrags * 4];
   } while (0)
 #endif
 
-constexpr uint32_t kCThreads = 512;  // 8 waves: parse (0), place (1-3), stage (4-7)
+constexpr uint32_t kCThreads = 512;  // K-parse: 8 waves, parse (0), stage (4-7)
 constexpr uint32_t kStageT = 256;    // lanes of the staging waves
 constexpr int kPre = (int)(kFrag / 16 / kStageT);  // uint4 per staging lane that cover one fragment
-constexpr uint32_t kNoFrag = 0xffffffffu;
 // one fragment's share of a lane as one vector value (an array of uint4 would
 // be placed in scratch memory)
 typedef uint32_t FragRegs __attribute__((ext_vector_type(4 * kPre)));
@@ -286,137 +253,278 @@ __device__ __forceinline__ void prefetch_frag(const uint8_t* __restrict__ in, si
   }
 }
 
-// Persistent workgroups of 8 waves (the LDS footprint allows one per CU) over
-// a pipeline of 64 KiB fragments taken by atomic ticket.  In each round, after
-// the staged fragment f is in LDS:
-//   wave 0      runs the serial 1.1.8 parse of f (tags to f's scratch slot)
-//               and publishes f's length for the look-back;
-//   waves 1-3   look back for the stream offset of the fragment parsed in the
-//               round before (fp) and copy its tags and final literal (read
-//               from the input) into place;
-//   waves 4-7   hold the next fragment's 64 KiB in registers, in flight while
-//               the others work, and stage it in LDS at the start of the next
-//               round.
-// Every wave's memory counter holds one kind of traffic -- the stagers' only
-// their prefetch loads, the parser's only stores -- so no wait at staging or
-// in the parse is behind another role's stores.
+// ---- compress: four launches per batch of streams, no device-side waits.
 //
-// Deadlock freedom: a workgroup holds at most three tickets (fp, f and the one
-// in flight; it takes the next while parsing), taken in increasing order by
-// running workgroups, and it waits only in the look-back of fp, on fragments
-// before fp.  The smallest fragment m whose length is unpublished belongs to a
-// workgroup that is parsing it, or will parse it after a round whose
-// look-back concerns fragments below m -- all published -- so every look-back
-// ends.
-// Several streams compress in one launch (the COMPRESSING arrays of a batch of
-// messages): fragments are numbered across the streams, the tickets hand them
-// out in that order, and a stream's first fragment publishes its inclusive
-// prefix at once, which ends every look-back inside the stream.
+// The parse of a 64 KiB fragment reads the table only at the positions it
+// probes, and on data without 4-byte matches at those positions (FIXING_FLOAT
+// codes, anything incompressible) 1.1.8's skip heuristic probes some 270
+// positions and emits the whole fragment as one literal.  So:
+//   K-probe  one wave per fragment runs 1.1.8's skip loop exactly, 64 probes
+//            per step, reading the input where it probes (no staging) and
+//            keeping the inserted positions in a small map in LDS; a
+//            fragment whose loop ends without a match is stored (one
+//            literal); any other goes on the list for K-parse.
+//   K-parse  the full 1.1.8 parse of the listed fragments, in LDS (fragment
+//            + 32 KiB hash table, one persistent workgroup per CU, the next
+//            fragment prefetched into registers while wave 0 parses); tags to
+//            the fragment's scratch slot.
+//   K-scan   one workgroup per stream: the stream offset of every fragment
+//            (exclusive sum of the fragment lengths), the varint header and
+//            the stream length (published to the host).
+//   K-place  one workgroup per fragment: its tags from scratch and its final
+//            literal (all of a stored fragment) from the input to their place.
+// No workgroup ever waits for another: every dependency is a kernel boundary.
+// Several streams compress in one launch chain (the COMPRESSING arrays of a
+// batch of messages): fragments are numbered across the streams.
 struct CJob {
   const uint8_t* in;
   uint8_t* dst;
   uint64_t n;
   uint32_t frag0, nfrag, hdr, slot, ticket, pad;
 };
-// Every wait is bounded: a look-back (or the placing waves' wait on it) that
-// spins `spin_cap` times without progress sets the launch's abort word and
-// gives up; every later wait sees the word and gives up at once, and each
-// stream's last fragment publishes kErrTimeout instead of its length.  (The
-// ticket argument above says no wait of a correct launch comes near the cap;
-// the cap turns a broken assumption into a status code, not a device hang.)
-// `stall` (a debug knob, psf_debug_snappy_stall) names a fragment whose length
-// is never published, to test that path.
 struct SnappyCJobs {
   CJob j[kSnappyBatchMax];
   PubSlot* pub;
   uint32_t njobs, nfrag;
-  uint64_t* znext;  // the next launch's zeroed state region (null: none)
+  uint64_t* finfo;   // per fragment: op (tag bytes) << 32 | next_emit (start of the final literal)
+  uint64_t* offset;  // per fragment: its offset in the stream (K-scan)
+  uint32_t* znext;   // (unused: the compressor keeps no zeroed state)
   uint32_t zwords;
-  uint32_t spin_cap;  // look-back iterations before the launch aborts
-  uint32_t stall;     // debug: fragment that never publishes (kNoStall: none)
 };
-constexpr uint32_t kNoStall = 0xffffffffu;
-constexpr uint64_t kAborted = ~0ull;  // s_excl when the look-back gave up
-__device__ __forceinline__ const CJob& cjob_of(const SnappyCJobs& J, uint32_t g) {
+__device__ __forceinline__ uint32_t cjob_index(const SnappyCJobs& J, uint32_t g) {
   uint32_t i = 0;
   while (i + 1 < J.njobs && g >= J.j[i + 1].frag0) ++i;
-  return J.j[i];
+  return i;
 }
+__device__ __forceinline__ const CJob& cjob_of(const SnappyCJobs& J, uint32_t g) { return J.j[cjob_index(J, g)]; }
 __device__ __forceinline__ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+// bytes of the literal tag of a literal of m + 1 bytes, and of the fragment
+__device__ __forceinline__ uint32_t lit_tag_len(uint32_t m) { return 1 + (m < 60 ? 0 : ((31 - __builtin_clz(m)) >> 3) + 1); }
+__device__ __forceinline__ uint32_t frag_len(uint64_t info, uint32_t len) {
+  const uint32_t op = (uint32_t)(info >> 32), ne = (uint32_t)info;
+  return op + (ne < len ? lit_tag_len(len - ne - 1) + (len - ne) : 0);
+}
+__device__ __forceinline__ uint32_t hash_shift(uint32_t len) {
+  uint32_t tsize = 256;
+  while (tsize < kMaxTable && tsize < len) tsize <<= 1;
+  return __builtin_clz(tsize) + 1;  // 32 - log2(tsize)
+}
 
-__global__ __launch_bounds__(kCThreads) void snappy_compress_frags(const SnappyCJobs J, uint8_t* __restrict__ scratch,
-                                                                   uint64_t* __restrict__ state,
-                                                                   uint32_t* __restrict__ ctr) {
-  __shared__ CompressLds L;
-  __shared__ uint32_t s_t0, s_t1, s_op, s_next, s_tn, s_round;
-  __shared__ uint64_t s_excl;
+// ---- K-probe
+constexpr uint32_t kMapSlots = 1024;  // per wave: every inserted probe (<= 270) as {hash + 1, position, 4 bytes}
+constexpr uint32_t kProbeMax = 6 * 64;  // probes a skip loop from ip = 1 can make in 64 KiB (< kSkipN)
+// the 4 input bytes at p of a fragment starting at g (any alignment; the
+// dwords read lie inside the fragment's 16-byte margin or before it within the
+// same dword as g[0])
+__device__ __forceinline__ uint32_t gld32(const uint8_t* g, uint32_t p) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(g + p);
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+  return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(a & 3));
+}
+// the table entry of hash h: 0 when never inserted (the table's initial 0)
+__device__ __forceinline__ uint64_t map_get(const uint64_t* m, uint32_t h) {
+  uint32_t s = h & (kMapSlots - 1);
+  for (;;) {
+    const uint64_t e = m[s];
+    if (e == 0 || (uint32_t)(e >> 48) == h + 1) return e;
+    s = (s + 1) & (kMapSlots - 1);
+  }
+}
+// (no two lanes of a step insert the same hash)
+__device__ __forceinline__ void map_put(uint64_t* m, uint32_t h, uint32_t pos, uint32_t v) {
+  const uint64_t e = ((uint64_t)(h + 1) << 48) | ((uint64_t)pos << 32) | v;
+  uint32_t s = h & (kMapSlots - 1);
+  for (;;) {
+    uint64_t cur = m[s];
+    if (cur == 0) {
+      cur = atomicCAS(reinterpret_cast<unsigned long long*>(&m[s]), 0ull, (unsigned long long)e);
+      if (cur == 0) return;
+    }
+    if ((uint32_t)(cur >> 48) == h + 1) {
+      m[s] = e;
+      return;
+    }
+    s = (s + 1) & (kMapSlots - 1);
+  }
+}
+
+struct ProbeLds {  // the probe phase: per wave, the table as a map and every probe's bytes
+  uint64_t map[kCThreads / 64][kMapSlots];
+  uint32_t val[kCThreads / 64][kProbeMax];
+};
+union CompressPhaseLds {
+  CompressLds p;
+  ProbeLds q;
+};
+
+// dst[0, len) = s[0, len) (global to global, any alignment of either) by T
+// lanes (tid 0..T-1): lane l of a wave loads the aligned source block under
+// destination chunk l of its row of 63 and takes the chunk's second block
+// from the next lane; a row's loads are all issued before its stores.
+template <uint32_t T>
+__device__ void copy_bytes(uint8_t* __restrict__ dst, const uint8_t* __restrict__ s, uint32_t len, uint32_t tid) {
+  constexpr int U = 8, W = T / 64;
+  const uint32_t lane = tid & 63, wv = tid >> 6;
+  const uint32_t head = (uint32_t)(-reinterpret_cast<uintptr_t>(dst) & 15);
+  if (head >= len) {
+    for (uint32_t i = tid; i < len; i += T) dst[i] = s[i];
+    return;
+  }
+  if (tid < head) dst[tid] = s[tid];
+  const uint32_t nc = (len - head) >> 4;
+  const uintptr_t sp = reinterpret_cast<uintptr_t>(s + head);
+  const uint4* s16 = reinterpret_cast<const uint4*>(sp & ~(uintptr_t)15);
+  const uint32_t sh = (uint32_t)(sp & 15);
+  const uint32_t lim = nc + (sh ? 1u : 0u);  // blocks that hold source bytes
+  uint4* d16 = reinterpret_cast<uint4*>(dst + head);
+  for (uint32_t c0 = 0; c0 < nc; c0 += U * W * 63) {
+    uint4 lo[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t c = c0 + (u * W + wv) * 63 + lane;
+      lo[u] = c < lim ? s16[c] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t c = c0 + (u * W + wv) * 63 + lane;
+      const uint4 hi = shfl_down1(lo[u]);
+      if (lane < 63 && c < nc) d16[c] = funnel16(lo[u], hi, sh);
+    }
+  }
+  const uint32_t t0 = head + 16 * nc;
+  for (uint32_t i = tid; i < len - t0; i += T) dst[t0 + i] = s[t0 + i];
+}
+
+// One wave probes one fragment.  From ip = 1 the skip loop's probe positions
+// are fixed (1 + kSkip[k]) until it matches, so all of their 4-byte values are
+// loaded at once; the candidate a probe compares with is a position an
+// earlier probe inserted (its bytes are already here) or the table's initial
+// 0 (the fragment's first 4 bytes).  The loop then runs in LDS and registers,
+// 64 probes per step, with exactly the full parse's rules: lanes up to the
+// first one whose hash an earlier lane of the step also has see the table as
+// it was, that lane sees the earlier lane's insert; later lanes wait for the
+// next step.  Returns whether the loop ends without a match (one literal).
+__device__ bool probe_stored(const uint8_t* g, uint32_t len, const uint32_t* skip, uint64_t* m, uint32_t* pv,
+                             uint32_t lane) {
+  if (len < 15) return true;
+  const uint32_t shift = hash_shift(len), ip_limit = len - 15, ip = 1;
+  // every probe's bytes (probe k is made iff ip + skip[k + 1] <= ip_limit)
+  uint32_t pre[kProbeMax / 64];
+#pragma unroll
+  for (uint32_t r = 0; r < kProbeMax / 64; ++r) {
+    const uint32_t k = r * 64 + lane;
+    pre[r] = ip + skip[k + 1] <= ip_limit ? gld32(g, ip + skip[k]) : 0;
+  }
+  const uint32_t v_at0 = uni(gld32(g, 0));
+  for (uint32_t i = lane; i < kMapSlots; i += 64) m[i] = 0;
+#pragma unroll
+  for (uint32_t r = 0; r < kProbeMax / 64; ++r) pv[r * 64 + lane] = pre[r];
+  for (uint32_t kbase = 0;;) {
+    const uint32_t k = kbase + lane;
+    const uint32_t pos = ip + skip[k];
+    const bool valid = ip + skip[k + 1] <= ip_limit;  // else "goto emit_remainder"
+    const uint32_t v = valid ? pv[k] : 0;
+    const uint32_t h = valid ? hash(v, shift) : 0;
+    const uint64_t vm = __ballot(valid);
+    uint64_t eq = vm;  // the valid lanes whose hash equals this lane's (14 bits)
+#pragma unroll
+    for (int b = 0; b < 14; ++b) {
+      const bool bit = (h >> b) & 1;
+      const uint64_t bm = __ballot(bit);
+      eq &= bit ? bm : ~bm;
+    }
+    const uint32_t first = valid ? (uint32_t)__builtin_ctzll(eq) : lane;
+    const uint64_t em = __ballot(valid && first < lane);
+    int limit = 63, jc = 64, jm = 0;
+    if (em) {
+      jc = __builtin_ctzll(em);
+      jm = (int)__builtin_amdgcn_readlane(first, jc);
+      limit = jc;
+    }
+    uint32_t cv = v_at0;  // the candidate's 4 bytes
+    if (valid && (int)lane <= limit) {
+      const uint64_t e = map_get(m, h);
+      if (e) cv = (uint32_t)e;
+    }
+    const uint32_t vjm = __builtin_amdgcn_readlane(v, jm & 63);
+    if (em && (int)lane == jc) cv = vjm;  // lane jm's insert
+    if (__ballot(valid && (int)lane <= limit && v == cv)) return false;  // a match
+    // no match up to `limit`: every probe up to it inserts its position
+    // (jm's insert is overwritten by jc's, same hash)
+    if (valid && (int)lane <= limit && !(em && (int)lane == jm)) map_put(m, h, pos, v);
+    const uint64_t lim_mask = limit >= 63 ? ~0ull : ((1ull << (limit + 1)) - 1);
+    if ((vm & lim_mask) != lim_mask) return true;  // emit_remainder: one literal
+    kbase += (uint32_t)limit + 1;
+  }
+}
+
+// K-parse: persistent workgroups of 8 waves (the parse's LDS footprint allows
+// one per CU), each over its stripe of the fragments (b, b + G, b + 2G, ...)
+// in rounds of 8: every wave probes one fragment; then each fragment that
+// matched is staged in LDS and parsed by wave 0 (tags to its scratch slot).
+// No workgroup depends on another.
+__global__ __launch_bounds__(kCThreads) void snappy_parse(const SnappyCJobs J, uint8_t* __restrict__ scratch) {
+  __shared__ uint32_t skip[kSkipN + 3];
+  __shared__ CompressPhaseLds U;
+  __shared__ uint32_t s_need[kCThreads / 64];
+  CompressLds& L = U.p;
   const uint32_t tid = threadIdx.x;
   const uint32_t wave = tid >> 6, lane = tid & 63;
-  uint32_t* const abortw = ctr + 1;  // set when a wait gave up (zero at the launch, as ctr)
-  if (tid == 0) {
-    s_t0 = atomicAdd(ctr, 1u);
-    s_t1 = atomicAdd(ctr, 1u);
-    s_round = 0;
-  }
-  for (uint32_t i = tid; i < (uint32_t)kSkipN; i += kCThreads) L.skip[i] = kSkip.v[i];
-  for (uint32_t i = tid; i < kMinSlots; i += kCThreads) L.minlane[i] = 0xffffffffu;  // each parse step cleans up after itself
-  if (J.znext)  // the next launch's look-back state, zeroed here (stream order publishes it)
+  constexpr uint32_t W = kCThreads / 64;
+  for (uint32_t i = tid; i < (uint32_t)kSkipN; i += kCThreads) skip[i] = kSkip.v[i];
+  if (J.znext)  // the next launch chain's counters (stream order publishes them)
     for (uint32_t i = blockIdx.x * kCThreads + tid; i < J.zwords; i += gridDim.x * kCThreads) J.znext[i] = 0;
   __syncthreads();
-  const uint32_t nfrag = J.nfrag;
-  uint32_t f = s_t0, fn = s_t1;
-  if (f >= nfrag) return;
-  const uint32_t st = tid - (kCThreads - kStageT);  // staging lane (waves 4-7)
-  FragRegs pre = {};
-  if (wave >= 4) {
-    const CJob& c = cjob_of(J, f);
-    if (aligned16(c.in)) prefetch_frag(c.in, c.n, f - c.frag0, pre, st);
-  }
   uint8_t* srcb = reinterpret_cast<uint8_t*>(L.src);
-  uint32_t fp = kNoFrag, fp_op = 0, fp_next = 0;  // the fragment parsed in the round before
-  uint32_t round = 1;  // the placing waves' handshake with wave 1
-  for (;;) {
-    // ---- stage f in LDS, clear its hash table
-    uint32_t len = 0, shift = 0, f_local = 0, f_hdr = 0;
-    if (f < nfrag) {
-      PSF_TRACE(f, 0);
+  const uint32_t G = gridDim.x;
+  for (uint32_t r0 = 0; (size_t)r0 * G + blockIdx.x < J.nfrag; r0 += W) {
+    // ---- probe: wave w takes fragment (r0 + w) G + b
+    {
+      const uint32_t f = (r0 + wave) * G + blockIdx.x;
+      bool need = false;
+      if (f < J.nfrag) {
+        PSF_TRACE_T(f, 0, wave * 64);
+        const CJob& c = cjob_of(J, f);
+        const size_t start = (size_t)(f - c.frag0) * kFrag;
+        const uint32_t len = (uint32_t)min((size_t)kFrag, c.n - start);
+        need = !probe_stored(c.in + start, len, skip, U.q.map[wave], U.q.val[wave], lane);
+        if (!need && lane == 0) J.finfo[f] = 0;  // no tags, the final literal from byte 0
+        PSF_TRACE_T(f, 4, wave * 64);
+      }
+      if (lane == 0) s_need[wave] = need;
+    }
+    __syncthreads();
+    uint32_t need = 0;
+    for (uint32_t w = 0; w < W; ++w) need |= s_need[w] << w;
+    __syncthreads();  // (the probe maps are overwritten by the parses)
+    if (!need) continue;
+    for (uint32_t i = tid; i < kMinSlots; i += kCThreads) L.minlane[i] = 0xffffffffu;  // each parse step cleans up after itself
+    // ---- parse the fragments that matched, one after another
+    while (need) {
+      const uint32_t w = __builtin_ctz(need);
+      need &= need - 1;
+      const uint32_t f = (r0 + w) * G + blockIdx.x;
       const CJob& c = cjob_of(J, f);
-      f_local = f - c.frag0;
-      f_hdr = c.hdr;
-      const size_t start = (size_t)f_local * kFrag;
-      len = (uint32_t)min((size_t)kFrag, c.n - start);
+      const size_t start = (size_t)(f - c.frag0) * kFrag;
+      const uint32_t len = (uint32_t)min((size_t)kFrag, c.n - start);
       const uint8_t* g = c.in + start;
-      if (aligned16(c.in)) {
+      if (aligned16(g)) {
+        const uint4* g4 = reinterpret_cast<const uint4*>(g);
+        uint4* s4 = reinterpret_cast<uint4*>(L.src);
         const uint32_t nv = len >> 4;
-        if (wave >= 4) {
-          uint4* s4 = reinterpret_cast<uint4*>(L.src);
-#pragma unroll
-          for (int u = 0; u < kPre; ++u) {
-            const uint32_t i = u * kStageT + st;
-            if (i < nv) s4[i] = make_uint4(pre[4 * u], pre[4 * u + 1], pre[4 * u + 2], pre[4 * u + 3]);
-          }
-        } else if (tid < len - (nv << 4)) {
-          srcb[(nv << 4) + tid] = g[(nv << 4) + tid];
-        }
+        for (uint32_t i = tid; i < nv; i += kCThreads) s4[i] = g4[i];
+        if (tid < len - (nv << 4)) srcb[(nv << 4) + tid] = g[(nv << 4) + tid];
       } else {
         for (uint32_t i = tid; i < len; i += kCThreads) srcb[i] = g[i];
       }
       if (tid < 16) srcb[len + tid] = 0;
-      uint32_t tsize = 256;
-      while (tsize < kMaxTable && tsize < len) tsize <<= 1;
-      shift = __builtin_clz(tsize) + 1;  // 32 - log2(tsize)
+      const uint32_t shift = hash_shift(len);
       uint32_t* t32 = reinterpret_cast<uint32_t*>(L.table);
-      for (uint32_t i = tid; i < tsize / 2; i += kCThreads) t32[i] = 0;
-    }
-    __syncthreads();
-    PSF_TRACE(f < nfrag ? f : kTraceFrags, 4);
-    if (wave == 0) {
-      // ---- parse f
-      if (f < nfrag) {
+      for (uint32_t i = tid; i < (1u << (32 - shift)) / 2; i += kCThreads) t32[i] = 0;
+      __syncthreads();
+      if (wave == 0) {
         uint8_t* out = scratch + (size_t)f * kSnappyFragOut;
         uint32_t op = 0, next_emit = 0;
-        // the fragment after fn: the ticket is drawn now and lands during the parse
-        const uint32_t tn = lane == 0 ? atomicAdd(ctr, 1u) : 0u;
         if (len >= 15) {
           const uint32_t ip_limit = len - 15;
           uint32_t ip = 1;
@@ -455,8 +563,8 @@ __global__ __launch_bounds__(kCThreads) void snappy_compress_frags(const SnappyC
             }
             for (;;) {
               const uint32_t k = kbase + lane;
-              const uint32_t pos = ip + L.skip[k];
-              const bool valid = ip + L.skip[k + 1] <= ip_limit;  // else "goto emit_remainder"
+              const uint32_t pos = ip + skip[k];
+              const bool valid = ip + skip[k + 1] <= ip_limit;  // else "goto emit_remainder"
               uint32_t v = 0, h = 0, slot = 0;
               if (valid) {
                 v = ld32(L.src, pos);
@@ -519,130 +627,104 @@ __global__ __launch_bounds__(kCThreads) void snappy_compress_frags(const SnappyC
           }
         }
       remainder:
-        // f's length: the tags so far plus the final literal; published for
-        // the look-back (state word = flag << 62 | bytes; flag 1: the length,
-        // 2: the inclusive prefix with the varint header -- fragment 0's at once)
-        uint32_t flen = op;
-        if (next_emit < len) {
-          const uint32_t m = len - next_emit - 1;
-          flen += 1 + m + 1 + (m < 60 ? 0 : ((31 - __builtin_clz(m)) >> 3) + 1);
-        }
-        if (lane == 0) {
-          if (f == J.stall) {
-            // debug: never published
-          } else if (f_local == 0)  // a stream's first fragment: its inclusive prefix at once
-            __hip_atomic_store(&state[f], (2ull << 62) | (f_hdr + flen), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          else
-            atomicAdd(&state[f], (1ull << 62) | flen);
-          s_op = op;
-          s_next = next_emit;
-          s_tn = tn;
-        }
+        if (lane == 0) J.finfo[f] = ((uint64_t)op << 32) | next_emit;
         PSF_TRACE(f, 1);
       }
-    } else {
-      if (wave >= 4 && fn < nfrag) {  // the registers were staged: the next fragment goes out now
-        const CJob& c = cjob_of(J, fn);
-        if (aligned16(c.in)) prefetch_frag(c.in, c.n, fn - c.frag0, pre, st);
-      }
-      // ---- look back for fp's offset (wave 1), then copy fp into place (waves 1-7)
-      if (fp < nfrag) {
-        const uint32_t pt = tid - 64;
-        const CJob& cp = cjob_of(J, fp);
-        const uint32_t lp = fp - cp.frag0;
-        const size_t pstart = (size_t)lp * kFrag;
-        const uint32_t plen = (uint32_t)min((size_t)kFrag, cp.n - pstart);
-        uint32_t flen = fp_op;
-        if (fp_next < plen) {
-          const uint32_t m = plen - fp_next - 1;
-          flen += 1 + m + 1 + (m < 60 ? 0 : ((31 - __builtin_clz(m)) >> 3) + 1);
-        }
-        // wave 1 walks back, 64 predecessors per step: the nearest inclusive
-        // prefix ends the walk, the lengths in front of it are summed across
-        // the wave; the other placing waves wait for its result in LDS
-        uint64_t excl = cp.hdr;
-        if (wave == 1 && lp > 0) {  // (the stream's first fragment is inclusive: the walk ends there at the latest)
-          uint64_t sum = 0;
-          int64_t base = (int64_t)fp - 1;  // lane l reads fragment base - l
-          for (uint32_t spins = 0;;) {
-            const int64_t j = base - (int64_t)lane;
-            const uint64_t w = j >= 0 ? __hip_atomic_load(&state[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-            const bool ready = j < 0 || (w >> 62) != 0;  // fragment 0 publishes inclusive only: the walk ends there
-            const uint64_t im = __ballot(j >= 0 && (w >> 62) == 2);
-            const int stop = im ? __builtin_ctzll(im) : 63;
-            const uint64_t need = stop >= 63 ? ~0ull : ((2ull << stop) - 1);
-            if (__ballot(!ready) & need) {  // a predecessor in front of the stop has not published yet
-              if (++spins >= J.spin_cap || __hip_atomic_load(abortw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                sum = kAborted;
-                break;
-              }
-              __builtin_amdgcn_s_sleep(1);
-              continue;
-            }
-            uint64_t v = ((int)lane <= stop && j >= 0) ? (w & ((1ull << 62) - 1)) : 0;
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-            sum += v;
-            if (im) break;
-            base -= 64;
-          }
-          excl = sum;
-        }
-        if (wave == 1) {
-          if (lane == 0) {
-            const bool ok = excl != kAborted;
-            if (!ok) __hip_atomic_store(abortw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_excl = excl;
-            __hip_atomic_store(&s_round, round, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (lp > 0 && ok && fp != J.stall)
-              __hip_atomic_store(&state[fp], (2ull << 62) | (excl + flen), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (lp + 1 == cp.nfrag && J.pub) {
-              PubSlot* pub = J.pub + cp.slot;
-              pub->size = ok ? excl + flen : 0;
-              pub->status = ok ? kOk : kErrTimeout;
-              publish_ticket(pub, cp.ticket);
-            }
-          }
-        } else {
-          // wave 1 stores s_round within its (bounded) look-back; the cap here
-          // is a backstop far above it
-          for (uint32_t spins = 0;
-               __hip_atomic_load(&s_round, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != round; ++spins) {
-            if (spins >= J.spin_cap * 64u) {
-              if (tid == 128) __hip_atomic_store(abortw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-          }
-          excl = __hip_atomic_load(&s_round, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == round ? s_excl : kAborted;
-        }
-        PSF_TRACE_T(fp, 2, 64);
-        if (lp == 0 && pt < cp.hdr)
-          cp.dst[pt] = (uint8_t)(((uint32_t)cp.n >> (7 * pt)) | (pt + 1 < cp.hdr ? 128u : 0u));
-        if (excl != kAborted) {  // an aborted fragment places nothing (its stream reports kErrTimeout)
-          uint8_t* d = cp.dst + excl;
-          if (fp_op) place_copy(d, scratch + (size_t)fp * kSnappyFragOut, fp_op, pt, lane);
-          if (fp_next < plen) {
-            d += fp_op;
-            d += literal_tag(d, plen - fp_next, pt);
-            place_copy(d, cp.in + pstart + fp_next, plen - fp_next, pt, lane);
-          }
-        }
-        PSF_TRACE_T(fp, 3, 64);
-      }
+      __syncthreads();
     }
-    __syncthreads();
-    ++round;
-    // fragments move down the pipeline
-    const bool parsed = f < nfrag;
-    fp = parsed ? f : kNoFrag;
-    fp_op = s_op;
-    fp_next = s_next;
-    f = fn;
-    fn = parsed ? s_tn : kNoFrag;
-    if (fp == kNoFrag) break;  // nothing left to place (and so nothing to parse)
-    // (s_op, s_next and s_tn are rewritten only after the next staging barrier)
   }
+}
+
+// ---- K-scan: one workgroup per stream.  Fragment offsets = the varint
+// header + the exclusive sum of the fragment lengths; the stream length is
+// published to the host (the bytes are in place once K-place has run).
+constexpr uint32_t kScanT = 1024;
+__global__ __launch_bounds__(kScanT) void snappy_scan(const SnappyCJobs J) {
+  __shared__ uint64_t wsum[kScanT / 64];
+  __shared__ uint64_t s_base;
+  const CJob& c = J.j[blockIdx.x];
+  const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  if (tid == 0) s_base = c.hdr;
+  if (tid < c.hdr) c.dst[tid] = (uint8_t)(((uint32_t)c.n >> (7 * tid)) | (tid + 1 < c.hdr ? 128u : 0u));
+  __syncthreads();
+  for (uint32_t k0 = 0; k0 < c.nfrag; k0 += kScanT) {
+    const uint32_t k = k0 + tid;
+    uint64_t v = 0;
+    if (k < c.nfrag) {
+      const size_t start = (size_t)k * kFrag;
+      const uint64_t info = J.finfo[c.frag0 + k];
+      v = frag_len(info, (uint32_t)min((size_t)kFrag, c.n - start));
+    }
+    uint64_t x = v;  // inclusive scan in the wave
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint64_t y = __shfl_up(x, o, 64);
+      if ((int)lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    uint64_t before = s_base;
+    for (uint32_t q = 0; q < wave; ++q) before += wsum[q];
+    if (k < c.nfrag) J.offset[c.frag0 + k] = before + x - v;
+    __syncthreads();
+    if (tid == kScanT - 1) s_base = before + x;
+    __syncthreads();
+  }
+  if (tid == 0 && J.pub) {
+    PubSlot* pub = J.pub + c.slot;
+    pub->size = s_base;
+    pub->status = kOk;
+    publish_ticket(pub, c.ticket);
+  }
+}
+
+// ---- K-place: one workgroup of 256 per fragment
+constexpr uint32_t kPlaceT = 256;
+
+// Streams of up to kInlineScan fragments need no K-scan: the workgroup of
+// fragment k sums the lengths of fragments 0..k-1 (all full) itself, the
+// workgroup of fragment 0 writes the varint header and the last fragment's
+// publishes the stream length.
+constexpr uint32_t kInlineScan = 4096;
+__global__ __launch_bounds__(kPlaceT) void snappy_place(const SnappyCJobs J, const uint8_t* __restrict__ scratch) {
+  __shared__ uint64_t s_part[kPlaceT / 64];
+  const uint32_t f = blockIdx.x, tid = threadIdx.x;
+  const CJob& c = cjob_of(J, f);
+  const uint32_t k = f - c.frag0;
+  const size_t start = (size_t)k * kFrag;
+  const uint32_t len = (uint32_t)min((size_t)kFrag, c.n - start);
+  const uint64_t info = J.finfo[f];
+  const uint32_t op = (uint32_t)(info >> 32), ne = (uint32_t)info;
+  PSF_TRACE(f, 2);
+  uint64_t off;
+  if (J.offset) {
+    off = J.offset[f];
+  } else {
+    uint64_t part = 0;
+    for (uint32_t i = tid; i < k; i += kPlaceT) part += frag_len(J.finfo[c.frag0 + i], kFrag);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+    if ((tid & 63) == 0) s_part[tid >> 6] = part;
+    __syncthreads();
+    off = c.hdr;
+    for (uint32_t w = 0; w < kPlaceT / 64; ++w) off += s_part[w];
+    if (k == 0 && tid < c.hdr)
+      c.dst[tid] = (uint8_t)(((uint32_t)c.n >> (7 * tid)) | (tid + 1 < c.hdr ? 128u : 0u));
+    if (k + 1 == c.nfrag && tid == 0 && J.pub) {
+      PubSlot* pub = J.pub + c.slot;
+      pub->size = off + frag_len(info, len);
+      pub->status = kOk;
+      publish_ticket(pub, c.ticket);
+    }
+  }
+  uint8_t* d = c.dst + off;
+  if (op) copy_bytes<kPlaceT>(d, scratch + (size_t)f * kSnappyFragOut, op, tid);
+  if (ne < len) {
+    d += op;
+    d += literal_tag(d, len - ne, tid);
+    copy_bytes<kPlaceT>(d, c.in + start + ne, len - ne, tid);
+  }
+  PSF_TRACE(f, 3);
 }
 
 // ------------------------------------------------------------------ uncompress
@@ -1692,15 +1774,11 @@ __global__ __launch_bounds__(256) void snappy_dfrag(const SnappyDJobs J) {
 
 size_t snappy_max_compressed(size_t n) { return 32 + n + n / 6; }
 
-// the compress kernel's wait bounds (SnappyCJobs::spin_cap, ::stall)
-constexpr uint32_t kDefaultSpinCap = 1u << 22;  // >= ~1 s of look-back polling, >100x a tag-dense parse
-static std::atomic<uint32_t> g_spin_cap{kDefaultSpinCap};
-static std::atomic<uint32_t> g_stall{kNoStall};
-
+// scratch: tag slots | finfo | offset (one each per fragment)
 size_t snappy_compress_batch_scratch(const SnappyCJob* jobs, int njobs) {
   size_t nfrag = 0;
   for (int i = 0; i < njobs; ++i) nfrag += (jobs[i].n + kFrag - 1) / kFrag;
-  return nfrag * kSnappyFragOut + (nfrag + 1) * 8 + 64;
+  return nfrag * kSnappyFragOut + nfrag * 16 + 64;
 }
 
 size_t snappy_compress_scratch(size_t n) {
@@ -1714,8 +1792,6 @@ int snappy_compress_batch_launch(const SnappyCJob* jobs, int njobs, void* scratc
   SnappyCJobs K{};
   K.pub = pub_base;
   K.njobs = (uint32_t)njobs;
-  K.spin_cap = g_spin_cap.load(std::memory_order_relaxed);
-  K.stall = g_stall.load(std::memory_order_relaxed);
   double bytes = 0;
   for (int i = 0; i < njobs; ++i) {
     const SnappyCJob& q = jobs[i];
@@ -1734,34 +1810,24 @@ int snappy_compress_batch_launch(const SnappyCJob* jobs, int njobs, void* scratc
     bytes += (double)q.n;
   }
   uint8_t* s = static_cast<uint8_t*>(scratch);
-  // look-back state (one word per fragment) and the fragment ticket counter,
-  // zero at the launch: the context's region the previous launch cleared, or
-  // the scratch's, cleared here
-  const size_t zneed = (size_t)K.nfrag * 8 + 8;
-  uint64_t* state;
-  if (z.cur && zneed <= z.bytes) {
-    state = static_cast<uint64_t*>(z.cur);
-    K.znext = static_cast<uint64_t*>(z.next);
-    K.zwords = (uint32_t)(z.bytes / 8);
-  } else {
-    state = reinterpret_cast<uint64_t*>(s + (size_t)K.nfrag * kSnappyFragOut);
-    if (hipMemsetAsync(state, 0, zneed, st) != hipSuccess) return kErrHip;
-  }
-  uint32_t* ctr = reinterpret_cast<uint32_t*>(state + K.nfrag);
-  // persistent workgroups, one per CU (the LDS footprint allows no more)
+  uint8_t* p = s + (size_t)K.nfrag * kSnappyFragOut;
+  K.finfo = reinterpret_cast<uint64_t*>(p);
+  K.offset = K.finfo + K.nfrag;
+  (void)z;  // every word the kernels read is written first in the same chain
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return kErrHip;
+  // K-parse: persistent workgroups, one per CU (the parse's LDS footprint allows no more)
   const uint32_t grid = K.nfrag < (uint32_t)cus ? K.nfrag : (uint32_t)cus;
   ProfScope ps(prof, kKSnappyCompress, st, bytes);
-  hipLaunchKernelGGL(snappy_compress_frags, dim3(grid), dim3(kCThreads), 0, st, K, s, state, ctr);
+  uint32_t longest = 0;
+  for (int i = 0; i < njobs; ++i) longest = std::max(longest, K.j[i].nfrag);
+  if (longest <= kInlineScan) K.offset = nullptr;  // K-place sums the lengths itself
+  hipLaunchKernelGGL(snappy_parse, dim3(grid), dim3(kCThreads), 0, st, K, s);
+  if (K.offset) hipLaunchKernelGGL(snappy_scan, dim3(K.njobs), dim3(kScanT), 0, st, K);
+  hipLaunchKernelGGL(snappy_place, dim3(K.nfrag), dim3(kPlaceT), 0, st, K, s);
   return launch_status();
-}
-
-void snappy_debug_stall(int64_t frag, uint32_t spin_cap) {
-  g_stall.store(frag < 0 || frag >= (int64_t)kNoStall ? kNoStall : (uint32_t)frag);
-  g_spin_cap.store(spin_cap ? spin_cap : kDefaultSpinCap);
 }
 
 int snappy_compress_launch(const void* in, size_t n, void* out, void* scratch, hipStream_t st, Profiler* prof,

@@ -267,3 +267,21 @@ def test_compress_on_private_stream_is_complete_on_return(port):
         s = ctx.snappy_compress(xd)
     got = s.to("cpu").numpy().tobytes()  # copied on the default stream
     assert got == port.snappy_compress(x.tobytes())
+
+
+def test_compress_stream_past_inline_scan(ctx, port):
+    """A stream of more than 4096 fragments (256 MiB + 1 fragment + a tail):
+    the per-stream offset scan runs as its own launch (shorter streams sum
+    their fragment lengths in the placement); byte-identical to 1.1.8 and
+    round-trips, with compressible fragments scattered among stored ones."""
+    rng = np.random.default_rng(4097)
+    n = 4097 * 65536 + 12345
+    x = rng.integers(0, 256, n, dtype=np.uint8)
+    for k in (0, 5, 4095, 4096):
+        x[k * 65536:k * 65536 + 30000] = 7  # a few compressible fragments, one past 4096
+    xb = x.tobytes()
+    want = port.snappy_compress(xb)
+    got = ctx.snappy_compress(_dev(xb)).cpu().numpy().tobytes()
+    assert got == want
+    back = ctx.snappy_uncompress(_dev(want)).cpu().numpy().tobytes()
+    assert back == xb

@@ -4,8 +4,8 @@
 Builds a libpsf variant with -DPSF_SNAPPY_TRACE (tools/variants/trace/) and
 loads it: python tools/snappy_trace.py --build (here, on CPU), then on the GPU
 box python tools/snappy_trace.py --run [--mib 128] [--kind codes|keys|random].
-Prints per-phase statistics over fragments: staging+parse (0->1), look-back
-(1->2), placement (2->3), and the gap between a workgroup's fragments.
+Prints per-fragment statistics of the compress pipeline: the probe (0->4),
+the placement (2->3), and the spans of both launches.
 """
 import argparse
 import ctypes as C
@@ -18,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 VAR = os.path.join(ROOT, "tools", "variants", "trace")
 
 
-def build():
+def build(src=None):
     sys.path.insert(0, ROOT)
     from parameter_server_amd import build as b
     b.build()
@@ -26,7 +26,7 @@ def build():
     objs = [os.path.join(b.OBJ, f) for f in sorted(os.listdir(b.OBJ)) if f.endswith(".o") and f != "snappy.hip.o"]
     obj = os.path.join(VAR, "snappy.o")
     subprocess.check_call([b._hipcc(), "-x", "hip", f"--offload-arch={b.ARCH}", *b.COMMON, "-DPSF_SNAPPY_TRACE",
-                           "-c", os.path.join(b.CSRC, "snappy.hip"), "-o", obj])
+                           "-I", b.CSRC, "-c", src or os.path.join(b.CSRC, "snappy.hip"), "-o", obj])
     subprocess.check_call([b._hipcc(), f"--offload-arch={b.ARCH}", "-shared", "-fPIC", "-o",
                            os.path.join(VAR, "libpsf.so"), *objs, obj])
     print(os.path.join(VAR, "libpsf.so"))
@@ -75,23 +75,19 @@ def run(mib, kind, dfrag=False):
                           "start_spread_us": round(float((np.sort(d[:, 0])[-1] - t0) * 10 / 1000), 1)}))
         return
     t = buf.reshape(nfrag, 6).astype(np.int64)
-    t0 = t[:, 0].min()
     ns = lambda a: a * 10.0  # noqa: E731  (100 MHz clock)
-    stage, parse = ns(t[:, 4] - t[:, 0]), ns(t[:, 1] - t[:, 4])
-    look, place = ns(t[:, 2] - t[:, 1]), ns(t[:, 3] - t[:, 2])
-    hw = t[:, 5]
-    gaps = []
-    order = np.argsort(t[:, 0])
-    last = {}
-    for f in order:
-        if hw[f] in last:
-            gaps.append(ns(t[f, 0] - t[last[hw[f]], 3]))
-        last[hw[f]] = f
     q = lambda a: {p: round(float(np.percentile(a, p)) / 1000, 2) for p in (10, 50, 90, 99)}  # noqa: E731
-    print(json.dumps({"kind": kind, "mib": mib, "frags": nfrag, "total_us": round(ns(t[:, 3].max() - t0) / 1000, 1),
-                      "stage_us": q(stage), "parse_us": q(parse), "lookback_us": q(look), "place_us": q(place),
-                      "gap_us": q(np.array(gaps)) if gaps else None,
-                      "first_start_spread_us": round(ns(np.sort(t[:, 0])[min(255, nfrag - 1)] - t0) / 1000, 2)}))
+    t0 = t[:, 0].min()
+    probe = ns(t[:, 4] - t[:, 0])
+    place = ns(t[:, 3] - t[:, 2])
+    print(json.dumps({"kind": kind, "mib": mib, "frags": nfrag,
+                      "probe_span_us": round(ns(t[:, 4].max() - t0) / 1000, 1),
+                      "probe_start_spread_us": round(ns(t[:, 0].max() - t0) / 1000, 1),
+                      "probe_us": q(probe),
+                      "probe_to_place_us": round(ns(t[:, 2].min() - t[:, 4].max()) / 1000, 1),
+                      "place_span_us": round(ns(t[:, 3].max() - t[:, 2].min()) / 1000, 1),
+                      "place_us": q(place),
+                      "place_start_spread_us": round(ns(t[:, 2].max() - t[:, 2].min()) / 1000, 1)}))
 
 
 if __name__ == "__main__":
@@ -101,8 +97,11 @@ if __name__ == "__main__":
     ap.add_argument("--mib", type=int, default=128)
     ap.add_argument("--kind", default="codes")
     ap.add_argument("--dfrag", action="store_true", help="per-fragment times of the decoder's K4")
+    ap.add_argument("--name", default="trace", help="variant directory under tools/variants")
+    ap.add_argument("--src", default=None, help="build: snappy.hip to trace (default: csrc/snappy.hip)")
     a = ap.parse_args()
+    VAR = os.path.join(ROOT, "tools", "variants", a.name)
     if a.build:
-        build()
+        build(a.src)
     if a.run:
         run(a.mib, a.kind, a.dfrag)
