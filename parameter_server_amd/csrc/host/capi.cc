@@ -586,12 +586,20 @@ int psf_node_roundtrip_ex(psf_node* snd, psf_node* rcv, const psf_message* const
     psf_message* last_dec = nullptr;
     psf::RemoteNode* s = snd->impl;
     psf::RemoteNode* r = rcv->impl;
+    // each iteration's KEY_CACHING CRCs are queued behind the previous
+    // iteration's encode and collected when the iteration starts
+    const psf::Message* t0 = iters ? &tmpls[0]->m : nullptr;
+    psf::PresignJob next = psf::presign_launch(&s, &t0, iters ? 1 : 0, true);
     for (int i = 0; i < iters; ++i) {
       psf::Message m = tmpls[i % ntmpl]->m;  // fresh Task + zero-copy buffers
       psf::Message* mp = &m;
-      psf::KeySigHint eh, dh;  // the iteration's KEY_CACHING CRCs, one wait
-      psf::presign_roundtrip(&s, &mp, 1, &eh, &dh);
+      psf::KeySigHint eh, dh;
+      psf::presign_finish(next, &eh, &dh);
       psf::encode_batch(&s, &mp, 1, &eh);  // = EncodeMessage, side-info left on the device
+      if (i + 1 < iters) {
+        const psf::Message* tn = &tmpls[(i + 1) % ntmpl]->m;
+        next = psf::presign_launch(&s, &tn, 1, true);
+      }
       psf::Message w = m;                  // delivered copy (van: Task frame + data frames)
       psf::Message* wp = &w;
       psf::decode_batch(&r, &wp, 1, &dh);  // = DecodeMessage
@@ -665,12 +673,15 @@ int psf_nodes_roundtrip_ex(psf_node* const* snd, psf_node* const* rcv, const psf
     std::vector<const psf::Message*> tp(n);
     for (int i = 0; i < n; ++i) tp[i] = &tmpls[i]->m;
     std::vector<psf::KeySigHint> eh(n), dh(n);
+    // every KEY_CACHING CRC of an iteration (all phases): queued behind the
+    // previous iteration's last encode, collected when the iteration starts
+    psf::PresignJob next = psf::presign_launch(s.data(), tp.data(), iters ? n : 0, true);
     for (int it = 0; it < iters; ++it) {
-      {  // every KEY_CACHING CRC of the iteration (all phases), one wait
+      {
         PSF_HPROF(12);
         std::fill(eh.begin(), eh.end(), psf::KeySigHint{});
         std::fill(dh.begin(), dh.end(), psf::KeySigHint{});
-        psf::presign_roundtrip(s.data(), tp.data(), n, eh.data(), dh.data());
+        psf::presign_finish(next, eh.data(), dh.data());
       }
       int b = 0;
       for (int e : ends) {  // phase [b, e): encode all, deliver, decode all
@@ -685,6 +696,7 @@ int psf_nodes_roundtrip_ex(psf_node* const* snd, psf_node* const* rcv, const psf
           PSF_HPROF(1);
           psf::encode_batch(s.data() + b, mp.data() + b, e - b, eh.data() + b);
         }
+        if (e == n && it + 1 < iters) next = psf::presign_launch(s.data(), tp.data(), n, true);
         {
           PSF_HPROF(5);
           for (int i = b; i < e; ++i) {

@@ -42,12 +42,15 @@ struct RangeBatch {
 
 class Context {
  public:
-  static constexpr int kSlots = 512;
+  static constexpr int kSlots = 768;
   // slots [0, kSyncSlots) serve launches whose results the host waits for
-  // before returning; [kSyncSlots, kSlots) the KEY_CACHING signatures that a
-  // batched encode leaves in flight while later filters launch
+  // before returning; [kSyncSlots, kPresignSlot0) the KEY_CACHING signatures
+  // that a batched encode leaves in flight while later filters launch;
+  // [kPresignSlot0, kSlots) the round-trip drivers' signatures of the next
+  // iteration (presign_launch)
   static constexpr int kSyncSlots = 256;
   static constexpr int kDeferSlot0 = kSyncSlots;
+  static constexpr int kPresignSlot0 = 512;
 
   // own_stream -> a private non-blocking stream owned by the context; else
   // `stream` as given (nullptr = the legacy default stream).

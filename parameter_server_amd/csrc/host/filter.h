@@ -187,6 +187,25 @@ void decode_batch(RemoteNode* const* nodes, Message* const* msgs, int n, const K
 // dec[i] receive them (left empty for host keys and key-less messages).
 void presign_roundtrip(RemoteNode* const* nodes, const Message* const* msgs, int n, KeySigHint* enc,
                        KeySigHint* dec);
+// The same in two halves: presign_launch queues the CRCs (ahead: into the
+// context's presign slots, so the caller can queue them one iteration early,
+// behind that iteration's encodes, and collect them at the start of the next
+// one with no wait; falls back to waiting in presign_finish when they do not
+// fit), presign_finish collects them.
+struct PresignJob {
+  struct Buf {
+    Context* ctx;
+    const uint8_t* ptr;
+    size_t bytes;
+    std::vector<int> users;
+    uint32_t tk[2];
+    int slot0;
+  };
+  std::vector<Buf> bufs;
+  bool ahead = false;
+};
+PresignJob presign_launch(RemoteNode* const* nodes, const Message* const* msgs, int n, bool ahead);
+void presign_finish(PresignJob& J, KeySigHint* enc, KeySigHint* dec);
 
 // Run the dequantise a deferred FIXING_FLOAT decode left pending (every
 // pending value array of msg becomes decoded data, as DecodeMessage would

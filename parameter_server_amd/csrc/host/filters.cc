@@ -617,7 +617,7 @@ static void launch_signatures(RemoteNode* const* nodes, Message* const* msgs, co
     else if (key.loc == Loc::kHost || nodes[idx[k]]->ctx()->device() < 0) sb->sigs[k] = crc32c_host(key.ptr, len);
     else dev[nodes[idx[k]]->ctx()].push_back(k);
   }
-  constexpr size_t kDeferCap = (size_t)(Context::kSlots - Context::kDeferSlot0);
+  constexpr size_t kDeferCap = (size_t)(Context::kPresignSlot0 - Context::kDeferSlot0);
   for (auto& kv : dev) {
     Context* ctx = kv.first;
     const std::vector<size_t>& ks = kv.second;
@@ -646,16 +646,9 @@ static void launch_signatures(RemoteNode* const* nodes, Message* const* msgs, co
   }
 }
 
-void presign_roundtrip(RemoteNode* const* nodes, const Message* const* msgs, int n, KeySigHint* enc,
-                       KeySigHint* dec) {
-  struct Job {
-    const uint8_t* ptr;
-    size_t bytes;
-    std::vector<int> users;
-    uint32_t tk[2];
-  };
-  std::map<Context*, std::vector<Job>> by_ctx;
-  std::map<std::pair<const uint8_t*, size_t>, std::pair<Context*, size_t>> seen;
+PresignJob presign_launch(RemoteNode* const* nodes, const Message* const* msgs, int n, bool ahead) {
+  PresignJob J;
+  std::map<std::pair<const uint8_t*, size_t>, size_t> seen;  // key buffer -> buffer index
   for (int i = 0; i < n; ++i) {
     const Message& m = *msgs[i];
     if (!m.has_key() || m.key.loc != Loc::kDevice || !Filter::find(FilterConfig::KEY_CACHING, const_cast<Message*>(&m)))
@@ -664,48 +657,106 @@ void presign_roundtrip(RemoteNode* const* nodes, const Message* const* msgs, int
     if (ctx->device() < 0) continue;
     const auto id = std::make_pair((const uint8_t*)m.key.ptr, m.key.bytes);
     auto it = seen.find(id);
-    if (it == seen.end() || it->second.first != ctx) {
-      auto& v = by_ctx[ctx];
-      seen[id] = {ctx, v.size()};
-      v.push_back(Job{m.key.ptr, m.key.bytes, {i}, {0, 0}});
-    } else {
-      by_ctx[ctx][it->second.second].users.push_back(i);
+    if (it != seen.end() && J.bufs[it->second].ctx == ctx) {
+      J.bufs[it->second].users.push_back(i);
+      continue;
+    }
+    seen[id] = J.bufs.size();
+    J.bufs.push_back(PresignJob::Buf{ctx, m.key.ptr, m.key.bytes, {i}, {0, 0}, -1});
+  }
+  // ahead (the next iteration's, waited for later): the presign slot range,
+  // when all of it fits; else the synchronous slots, waited for chunk by chunk
+  std::map<Context*, size_t> per;
+  for (const auto& b : J.bufs) ++per[b.ctx];
+  size_t most = 0;
+  for (const auto& kv : per) most = std::max(most, kv.second);
+  J.ahead = ahead && 2 * most <= (size_t)(Context::kSlots - Context::kPresignSlot0);
+  if (!J.ahead) return J;  // launched and waited for in presign_finish
+  std::map<Context*, int> next_slot;
+  std::map<Context*, std::vector<size_t>> order;
+  for (size_t q = 0; q < J.bufs.size(); ++q) order[J.bufs[q].ctx].push_back(q);
+  for (auto& kv : order) {
+    Context* ctx = kv.first;
+    std::vector<const void*> d;
+    std::vector<uint32_t> len, tk;
+    std::vector<int> slot;
+    int s = Context::kPresignSlot0;
+    for (size_t q : kv.second) {
+      PresignJob::Buf& b = J.bufs[q];
+      b.slot0 = s;
+      for (int r = 0; r < 2; ++r) {
+        b.tk[r] = ctx->next_ticket();
+        d.push_back(b.ptr);
+        len.push_back((uint32_t)std::min(b.bytes, (size_t)2048));
+        tk.push_back(b.tk[r]);
+        slot.push_back(s - Context::kPresignSlot0 + r);
+      }
+      s += 2;
+    }
+    for (size_t c = 0; c < d.size(); c += (size_t)kCrcBatchMax) {
+      const int cnt = (int)std::min(d.size() - c, (size_t)kCrcBatchMax);
+      int st = crc32c_batch_launch(d.data() + c, len.data() + c, slot.data() + c, tk.data() + c, cnt,
+                                   ctx->pub_dev(Context::kPresignSlot0), ctx->stream(), ctx->prof());
+      if (st != kOk) throw CheckError(st, "crc32c batch launch failed");
     }
   }
-  constexpr size_t kPer = (size_t)Context::kSyncSlots / 2;  // jobs (x2 CRCs) in flight per wait
-  for (auto& kv : by_ctx) {
+  return J;
+}
+
+void presign_finish(PresignJob& J, KeySigHint* enc, KeySigHint* dec) {
+  auto fill = [&](const PresignJob::Buf& b, uint32_t se, uint32_t sd) {
+    for (int i : b.users) {
+      enc[i] = KeySigHint{b.ptr, b.bytes, se};
+      if (dec) dec[i] = KeySigHint{b.ptr, b.bytes, sd};
+    }
+  };
+  if (J.ahead) {
+    for (const auto& b : J.bufs) fill(b, b.ctx->wait_crc(b.slot0, b.tk[0]), b.ctx->wait_crc(b.slot0 + 1, b.tk[1]));
+    J.bufs.clear();
+    return;
+  }
+  // now: chunks of the synchronous slots, each launched and waited for
+  constexpr size_t kPer = (size_t)Context::kSyncSlots / 2;  // buffers (x2 CRCs) in flight per wait
+  std::map<Context*, std::vector<size_t>> order;
+  for (size_t q = 0; q < J.bufs.size(); ++q) order[J.bufs[q].ctx].push_back(q);
+  for (auto& kv : order) {
     Context* ctx = kv.first;
-    std::vector<Job>& jobs = kv.second;
-    for (size_t b = 0; b < jobs.size(); b += kPer) {
-      const size_t e = std::min(jobs.size(), b + kPer);
-      // CRC 2q: the sender's signature of job q; CRC 2q + 1: the receiver's check
+    const std::vector<size_t>& qs = kv.second;
+    for (size_t b0 = 0; b0 < qs.size(); b0 += kPer) {
+      const size_t e = std::min(qs.size(), b0 + kPer);
+      // CRC 2q: the sender's signature of buffer q; CRC 2q + 1: the receiver's check
       std::vector<const void*> d;
       std::vector<uint32_t> len, tk;
       std::vector<int> slot;
-      for (size_t q = b; q < e; ++q)
+      for (size_t i = b0; i < e; ++i) {
+        PresignJob::Buf& b = J.bufs[qs[i]];
         for (int r = 0; r < 2; ++r) {
-          jobs[q].tk[r] = ctx->next_ticket();
-          d.push_back(jobs[q].ptr);
-          len.push_back((uint32_t)std::min(jobs[q].bytes, (size_t)2048));
-          tk.push_back(jobs[q].tk[r]);
-          slot.push_back((int)(2 * (q - b) + r));
+          b.tk[r] = ctx->next_ticket();
+          d.push_back(b.ptr);
+          len.push_back((uint32_t)std::min(b.bytes, (size_t)2048));
+          tk.push_back(b.tk[r]);
+          slot.push_back((int)(2 * (i - b0) + r));
         }
+      }
       for (size_t c = 0; c < d.size(); c += (size_t)kCrcBatchMax) {
         const int cnt = (int)std::min(d.size() - c, (size_t)kCrcBatchMax);
         int st = crc32c_batch_launch(d.data() + c, len.data() + c, slot.data() + c, tk.data() + c, cnt,
                                      ctx->pub_dev(0), ctx->stream(), ctx->prof());
         if (st != kOk) throw CheckError(st, "crc32c batch launch failed");
       }
-      for (size_t q = b; q < e; ++q) {
-        const uint32_t se = ctx->wait_crc((int)(2 * (q - b)), jobs[q].tk[0]);
-        const uint32_t sd = ctx->wait_crc((int)(2 * (q - b) + 1), jobs[q].tk[1]);
-        for (int i : jobs[q].users) {
-          enc[i] = KeySigHint{jobs[q].ptr, jobs[q].bytes, se};
-          if (dec) dec[i] = KeySigHint{jobs[q].ptr, jobs[q].bytes, sd};
-        }
+      for (size_t i = b0; i < e; ++i) {
+        const PresignJob::Buf& b = J.bufs[qs[i]];
+        fill(b, ctx->wait_crc((int)(2 * (i - b0)), b.tk[0]), ctx->wait_crc((int)(2 * (i - b0) + 1), b.tk[1]));
       }
     }
   }
+  J.bufs.clear();
+}
+
+void presign_roundtrip(RemoteNode* const* nodes, const Message* const* msgs, int n, KeySigHint* enc,
+                       KeySigHint* dec) {
+  PresignJob J = presign_launch(nodes, msgs, n, false);
+  presign_finish(J, enc, dec);
 }
 
 // Encode in filter order, position by position over all chains.  The

@@ -160,7 +160,7 @@ int crc32c_launch(const void* d, size_t n, uint32_t* out, hipStream_t st,
                   Profiler* prof = nullptr, PubSlot* pub = nullptr, uint32_t ticket = 0);
 // up to kCrcBatchMax buffers of 1..kCrcSingleBlock bytes, one workgroup each,
 // each CRC published to pub[slot[i]] with ticket[i]
-constexpr int kCrcBatchMax = 64;
+constexpr int kCrcBatchMax = 256;  // 5 KiB of kernel arguments
 int crc32c_batch_launch(const void* const* d, const uint32_t* n, const int* slot, const uint32_t* ticket,
                         int count, PubSlot* pub, hipStream_t st, Profiler* prof);
 
