@@ -77,12 +77,20 @@ constexpr uint32_t kMinSlots = 4096;
 struct CompressLds {
   uint32_t src[kFrag / 4 + 8];
   uint16_t table[kMaxTable];
-  uint32_t minlane[kMinSlots];  // per hash slot: lowest lane of the step that probed it
+  uint32_t minlane[kMinSlots + 1];  // per hash slot: lowest lane of the step that probed it (+ a spare)
 };
+
+// diagnostic builds (-DPSF_DIAG_NOSTORE): the parse emits nothing (timing only)
+#ifdef PSF_DIAG_NOSTORE
+#define PSF_SINK(lane) ((lane) + 64u)
+#else
+#define PSF_SINK(lane) (lane)
+#endif
 
 template <uint32_t kLanes = 64>
 __device__ uint32_t emit_literal(uint8_t* out, uint32_t op, const uint8_t* srcb, uint32_t lit,
                                  uint32_t len, uint32_t lane) {
+  lane = PSF_SINK(lane);
   const uint32_t n = len - 1;
   uint32_t hl = 1;
   if (n < 60) {
@@ -128,6 +136,7 @@ __device__ __forceinline__ void put_copy2(uint8_t* out, uint32_t op, uint32_t of
 }
 
 __device__ uint32_t emit_copy(uint8_t* out, uint32_t op, uint32_t offset, uint32_t len, uint32_t lane) {
+  lane = PSF_SINK(lane);
   if (len >= 68) {  // while (len >= 68) { EmitCopyAtMost64(64); len -= 64; }
     const uint32_t q = (len - 68) / 64 + 1;
     for (uint32_t i = lane; i < q; i += 64) put_copy2(out, op + 3 * i, offset, 64);
@@ -458,6 +467,193 @@ __device__ bool probe_stored(const uint8_t* g, uint32_t len, const uint32_t* ski
   }
 }
 
+// 4 bytes at p of the staged fragment, p clamped to its zero margin
+__device__ __forceinline__ uint32_t ldc(const uint32_t* s, uint32_t p, uint32_t len) {
+  return ld32(s, p < len ? p : len);
+}
+__device__ __forceinline__ uint32_t lane_of(uint32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
+
+// A literal of len <= 60 bytes (one tag byte): lane 0 the tag, lanes
+// 1..len its bytes, one store instruction.
+__device__ __forceinline__ uint32_t emit_lit(uint8_t* out, uint32_t op, const uint8_t* srcb, uint32_t lit,
+                                             uint32_t len, uint32_t lane) {
+  if (len > 60) return emit_literal(out, op, srcb, lit, len, lane);
+  const uint8_t b = srcb[lit + (lane ? lane - 1 : 0)];
+  lane = PSF_SINK(lane);
+  if (lane <= len) out[op + lane] = lane ? b : (uint8_t)((len - 1) << 2);
+  return op + 1 + len;
+}
+// EmitCopy (1.1.8) of a copy that fits one tag, one store instruction; the
+// rest go to emit_copy
+__device__ __forceinline__ uint32_t emit_copy_fast(uint8_t* out, uint32_t op, uint32_t offset, uint32_t len,
+                                                   uint32_t lane) {
+  if (len < 12 && offset < 2048) {  // COPY_1_BYTE_OFFSET
+    const uint8_t b = lane ? (uint8_t)offset : (uint8_t)(1 + ((len - 4) << 2) + ((offset >> 3) & 0xe0));
+    lane = PSF_SINK(lane);
+    if (lane < 2) out[op + lane] = b;
+    return op + 2;
+  }
+  if (len <= 64) {  // COPY_2_BYTE_OFFSET
+    const uint8_t b = lane ? (uint8_t)(offset >> (8 * (lane - 1))) : (uint8_t)(2 + ((len - 1) << 2));
+    lane = PSF_SINK(lane);
+    if (lane < 3) out[op + lane] = b;
+    return op + 3;
+  }
+  return emit_copy(out, op, offset, len, lane);
+}
+
+#ifdef PSF_DIAG_COUNT
+#define PSF_CNT(i) (cnt[i] += 1)
+#else
+#define PSF_CNT(i) ((void)0)
+#endif
+
+// The exact 1.1.8 parse of one staged fragment by one wave (CompressFragment,
+// snappy.cc): tags to out, returns {tag bytes, start of the final literal}.
+// One wave issues about one vector instruction per 4 cycles, so the parse is
+// bound by its instruction count per tag; the common paths are short:
+//  * copies: each lane holds the 4 bytes at ip + off + lane and at
+//    cand + off + lane, so one round of reads gives 64 bytes of the match
+//    length, and the bytes at the new ip - 1, ip and ip + 1 come from the
+//    lanes where the match ended;
+//  * after a copy, the table updates, the check whether ip matches at once
+//    and the skip loop's first probe (at ip + 1, which sees those updates)
+//    are issued together, with the first round of the next copy's match
+//    length for both outcomes;
+//  * otherwise the skip loop runs 64 probes per step (positions ip + kSkip[k];
+//    the first two steps' offsets sit in registers), every probe's hash slot,
+//    candidate and the slot's lowest probing lane read together; a lane whose
+//    earlier same-hash lane inserted this step compares with that lane's
+//    bytes; lanes past the first such lane wait for the next step (as in
+//    probe_stored).
+__device__ uint2 parse_fragment(CompressLds& L, const uint32_t* skip, uint32_t skA, uint32_t skB, uint32_t skC,
+                                uint32_t len, uint8_t* __restrict__ out, uint32_t lane
+#ifdef PSF_DIAG_COUNT
+                                , uint32_t* cnt
+#endif
+                                ) {
+  const uint32_t* s = L.src;
+  const uint8_t* srcb = reinterpret_cast<const uint8_t*>(L.src);
+  uint32_t op = 0, next_emit = 0;
+  if (len < 15) return make_uint2(0, 0);
+  const uint32_t shift = hash_shift(len), ip_limit = len - 15;
+  uint32_t ip = 1, kbase = 0;  // the skip loop from ip, at its probe kbase
+  for (;;) {
+    // ---- skip loop steps
+    uint32_t cand;
+    for (;;) {
+      PSF_CNT(0);
+      const uint32_t k = kbase + lane;
+      const uint32_t o0 = kbase == 0 ? skA : kbase == 1 ? skB : skip[k];
+      const uint32_t o1 = kbase == 0 ? skB : kbase == 1 ? skC : skip[k + 1];
+      const bool valid = ip + o1 <= ip_limit;  // else "goto emit_remainder"
+      const uint32_t pos = ip + o0;
+      const uint32_t v = ldc(s, pos, len);
+      const uint32_t h = hash(v, shift);
+      const uint32_t slot = valid ? (h & (kMinSlots - 1)) : kMinSlots;  // invalid lanes: the spare slot
+      const uint32_t c = L.table[h];
+      atomicMin(&L.minlane[slot], lane);
+      asm volatile("" ::: "memory");
+      const uint32_t fl = L.minlane[slot];
+      asm volatile("" ::: "memory");
+      L.minlane[slot] = 0xffffffffu;  // clean for the next step
+      const uint32_t wc = ld32(s, c);
+      const uint32_t first = valid ? fl : lane;
+      const uint64_t vm = __ballot(valid);
+      const uint64_t em = __ballot(valid && first < lane);
+      int limit = 63, jc = 64, jm = 0;
+      bool exact_pair = false;
+      if (em) {
+        jc = __builtin_ctzll(em);
+        jm = (int)lane_of(first, jc);
+        exact_pair = lane_of(h, jm) == lane_of(h, jc);
+        limit = jc;
+      }
+      const uint32_t vjm = lane_of(v, jm);
+      const bool pair = exact_pair && (int)lane == jc;  // sees lane jm's insert: compares with its bytes
+      const bool m = valid && (int)lane <= limit && v == (pair ? vjm : wc);
+      const uint64_t mm = __ballot(m);
+      const int last = mm ? __builtin_ctzll(mm) : limit;
+      const bool overwritten = exact_pair && (int)lane == jm && jc <= last;
+      if (valid && (int)lane <= last && !overwritten) L.table[h] = (uint16_t)pos;
+      if (mm) {
+        const int ks = __builtin_ctzll(mm);
+        cand = (exact_pair && ks == jc) ? lane_of(pos, jm) : lane_of(c, ks);
+        ip = lane_of(pos, ks);
+        break;
+      }
+      const uint64_t lim_mask = limit >= 63 ? ~0ull : ((1ull << (limit + 1)) - 1);
+      if ((vm & lim_mask) != lim_mask) goto remainder;
+      kbase += (uint32_t)limit + 1;
+    }
+    op = emit_lit(out, op, srcb, next_emit, ip - next_emit, lane);
+    // ---- copies
+    {
+      uint32_t off = 3, wa = 0, wb = 0;  // lane 0 of the first round: byte ip + 3 (known equal)
+      bool have = false;
+      for (;;) {
+        uint32_t k;
+        for (;;) {
+          const uint32_t pb = ip + off + lane;
+          if (!have) {
+            wb = ldc(s, pb, len);
+            wa = ldc(s, cand + off + lane, len);
+          }
+          have = false;
+          const uint64_t bad = __ballot(pb >= len || ((wa ^ wb) & 0xffu) != 0);
+          if (bad) {
+            k = (uint32_t)__builtin_ctzll(bad);  // >= 1: lane 0 is a byte known equal
+            break;
+          }
+          off += 63;  // the next round's lane 0 is this round's lane 63
+          PSF_CNT(1);
+        }
+        const uint32_t prev = lane_of(wb, k - 1), cur = lane_of(wb, k);
+        uint32_t nxt = lane_of(wb, k < 63 ? k + 1 : 63);
+        op = emit_copy_fast(out, op, ip - cand, off + k, lane);
+        ip += off + k;
+        next_emit = ip;
+        if (ip >= ip_limit) goto remainder;
+        if (k == 63) nxt = uni(ldc(s, ip + 1, len));
+        const uint32_t hp = hash(prev, shift), hc = hash(cur, shift), hn = hash(nxt, shift);
+        if (lane == 0) L.table[hp] = (uint16_t)(ip - 1);
+        const uint32_t c = L.table[hc];
+        if (lane == 0) L.table[hc] = (uint16_t)ip;
+        const uint32_t c1 = L.table[hn];  // the skip loop's probe 0 at ip + 1, if ip does not match
+        wb = ldc(s, ip + lane, len);
+        const uint32_t wb1 = ldc(s, ip + 1 + lane, len);
+        wa = ldc(s, c + lane, len);
+        const uint32_t wa1 = ldc(s, c1 + lane, len);
+        PSF_CNT(2);
+        if (lane_of(wa, 0) == cur) {  // a copy from ip at once; its first round is loaded
+          PSF_CNT(3);
+          cand = uni(c);
+          off = 0;
+          have = true;
+          continue;
+        }
+        ip += 1;  // the skip loop from ip + 1: probe 0 is made iff ip + 1 <= ip_limit
+        if (ip + 1 > ip_limit) goto remainder;
+        if (lane == 0) L.table[hn] = (uint16_t)ip;
+        if (lane_of(wa1, 0) == nxt) {  // probe 0 matches: a one-byte literal, then a copy
+          PSF_CNT(4);
+          cand = uni(c1);
+          op = emit_lit(out, op, srcb, next_emit, 1, lane);
+          wa = wa1;
+          wb = wb1;
+          off = 0;
+          have = true;
+          continue;
+        }
+        kbase = 1;
+        break;
+      }
+    }
+  }
+remainder:
+  return make_uint2(op, next_emit);
+}
+
 // K-parse: persistent workgroups of 8 waves (the parse's LDS footprint allows
 // one per CU), each over its stripe of the fragments (b, b + G, b + 2G, ...)
 // in rounds of 8: every wave probes one fragment; then each fragment that
@@ -472,6 +668,10 @@ __global__ __launch_bounds__(kCThreads) void snappy_parse(const SnappyCJobs J, u
   const uint32_t wave = tid >> 6, lane = tid & 63;
   constexpr uint32_t W = kCThreads / 64;
   for (uint32_t i = tid; i < (uint32_t)kSkipN; i += kCThreads) skip[i] = kSkip.v[i];
+  const uint32_t sk0 = kSkip.v[lane], sk1 = kSkip.v[lane + 1], sk2 = kSkip.v[lane + 2];  // the first skip steps' offsets
+#ifdef PSF_DIAG_COUNT
+  uint32_t cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
   if (J.znext)  // the next launch chain's counters (stream order publishes them)
     for (uint32_t i = blockIdx.x * kCThreads + tid; i < J.zwords; i += gridDim.x * kCThreads) J.znext[i] = 0;
   __syncthreads();
@@ -498,7 +698,7 @@ __global__ __launch_bounds__(kCThreads) void snappy_parse(const SnappyCJobs J, u
     for (uint32_t w = 0; w < W; ++w) need |= s_need[w] << w;
     __syncthreads();  // (the probe maps are overwritten by the parses)
     if (!need) continue;
-    for (uint32_t i = tid; i < kMinSlots; i += kCThreads) L.minlane[i] = 0xffffffffu;  // each parse step cleans up after itself
+    for (uint32_t i = tid; i <= kMinSlots; i += kCThreads) L.minlane[i] = 0xffffffffu;  // each parse step cleans up after itself
     // ---- parse the fragments that matched, one after another
     while (need) {
       const uint32_t w = __builtin_ctz(need);
@@ -523,6 +723,7 @@ __global__ __launch_bounds__(kCThreads) void snappy_parse(const SnappyCJobs J, u
       for (uint32_t i = tid; i < (1u << (32 - shift)) / 2; i += kCThreads) t32[i] = 0;
       __syncthreads();
       if (wave == 0) {
+#ifdef PSF_PARSE_OLD
         uint8_t* out = scratch + (size_t)f * kSnappyFragOut;
         uint32_t op = 0, next_emit = 0;
         if (len >= 15) {
@@ -627,12 +828,25 @@ __global__ __launch_bounds__(kCThreads) void snappy_parse(const SnappyCJobs J, u
           }
         }
       remainder:
+#else
+        const uint2 r = parse_fragment(L, skip, sk0, sk1, sk2, len, scratch + (size_t)f * kSnappyFragOut, lane
+#ifdef PSF_DIAG_COUNT
+                                       , cnt
+#endif
+                                       );
+        const uint32_t op = r.x, next_emit = r.y;
+#endif
         if (lane == 0) J.finfo[f] = ((uint64_t)op << 32) | next_emit;
         PSF_TRACE(f, 1);
       }
       __syncthreads();
     }
   }
+#ifdef PSF_DIAG_COUNT
+  if (blockIdx.x == 0 && tid == 0)
+    printf("parse counts wg0: steps %u ext_rounds %u copies %u immediate %u probe0 %u\n", cnt[0], cnt[1], cnt[2],
+           cnt[3], cnt[4]);
+#endif
 }
 
 // ---- K-scan: one workgroup per stream.  Fragment offsets = the varint

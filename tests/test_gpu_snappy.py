@@ -34,6 +34,13 @@ def _inputs(rng, n, kind):
                          50).tobytes()[:n]
     if kind == "zeros":
         return bytes(n)
+    if kind == "alpha4":  # short matches everywhere, many same-hash probes in a skip step
+        return rng.integers(0, 4, n, dtype=np.uint8).tobytes()
+    if kind == "periodic":  # long copies (>= 64 bytes: several match-length rounds)
+        p = rng.integers(0, 256, int(rng.integers(5, 300)), dtype=np.uint8)
+        x = np.resize(p, n)
+        x[rng.integers(0, max(n, 1), n // 500 + 1)] ^= 1  # sparse breaks
+        return x.tobytes()
     if kind == "text":
         words = [b"param", b"server", b"filter", b"key", b"value", b"  ", b"\n"]
         return b"".join(words[i] for i in rng.integers(0, len(words), n // 4 + 1))[:n]
@@ -52,7 +59,7 @@ def test_compress_matches_snappy_1_1_8_fixtures(ctx):
         assert back == x, k
 
 
-@pytest.mark.parametrize("kind", ["random", "keys", "codes", "runs", "zeros", "text"])
+@pytest.mark.parametrize("kind", ["random", "keys", "codes", "runs", "zeros", "text", "alpha4", "periodic"])
 def test_compress_random_sizes_vs_port(ctx, port, kind):
     rng = np.random.default_rng(len(kind) * 7 + ord(kind[0]))
     for n in [1, 14, 15, 16, 17, 63, 64, 65, 255, 256, 257, 4095, 65535, 65536, 65537, 300001, 3 << 20]:
