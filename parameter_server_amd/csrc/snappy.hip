@@ -70,14 +70,23 @@ __device__ __forceinline__ uint32_t ld32(const uint32_t* s, uint32_t p) {
 
 __device__ __forceinline__ uint32_t hash(uint32_t v, int shift) { return (v * kMul) >> shift; }
 
-constexpr uint32_t kMinSlots = 4096;
+// a pointer the caller knows is device memory, as a global-address-space one
+// (plain vector loads, not flat ones, which also count against the LDS
+// counter and make every LDS wait wait for them)
+template <typename T>
+__device__ __forceinline__ const __attribute__((address_space(1))) T* gbl(const void* p) {
+  return (const __attribute__((address_space(1))) T*)reinterpret_cast<uintptr_t>(p);
+}
 
-// the parse of one fragment (kSkip is kept beside it, in LDS: no
-// vector-memory wait in the loop)
-struct CompressLds {
-  uint32_t src[kFrag / 4 + 8];
-  uint16_t table[kMaxTable];
-  uint32_t minlane[kMinSlots + 1];  // per hash slot: lowest lane of the step that probed it (+ a spare)
+// K-parse: kParseWaves waves per workgroup parse one fragment each, reading
+// the fragment from memory (L1/L2) and keeping only the hash table and the
+// skip loop's per-step slot words in LDS: 36 KiB per wave.
+constexpr uint32_t kParseWaves = 4;
+constexpr uint32_t kMinSlots = 1024;
+static_assert((kParseWaves - 1) * kMaxTable * 2 >= kFrag + 16, "a staged fragment fits the other tables");
+struct ParseLds {
+  uint16_t table[kParseWaves][kMaxTable];  // (one fragment alone is staged in tables 1..3)
+  uint32_t minlane[kParseWaves][kMinSlots + 1];  // per hash slot: lowest lane of the step that probed it (+ a spare)
 };
 
 // diagnostic builds (-DPSF_DIAG_NOSTORE): the parse emits nothing (timing only)
@@ -327,7 +336,7 @@ constexpr uint32_t kProbeMax = 6 * 64;  // probes a skip loop from ip = 1 can ma
 // same dword as g[0])
 __device__ __forceinline__ uint32_t gld32(const uint8_t* g, uint32_t p) {
   const uintptr_t a = reinterpret_cast<uintptr_t>(g + p);
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+  const auto w = gbl<uint32_t>(reinterpret_cast<const void*>(a & ~(uintptr_t)3));
   return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(a & 3));
 }
 // the table entry of hash h: 0 when never inserted (the table's initial 0)
@@ -362,7 +371,7 @@ struct ProbeLds {  // the probe phase: per wave, the table as a map and every pr
   uint32_t val[kCThreads / 64][kProbeMax];
 };
 union CompressPhaseLds {
-  CompressLds p;
+  ParseLds p;
   ProbeLds q;
 };
 
@@ -413,7 +422,7 @@ __device__ void copy_bytes(uint8_t* __restrict__ dst, const uint8_t* __restrict_
 // first one whose hash an earlier lane of the step also has see the table as
 // it was, that lane sees the earlier lane's insert; later lanes wait for the
 // next step.  Returns whether the loop ends without a match (one literal).
-__device__ bool probe_stored(const uint8_t* g, uint32_t len, const uint32_t* skip, uint64_t* m, uint32_t* pv,
+__device__ __forceinline__ bool probe_stored(const uint8_t* g, uint32_t len, const uint32_t* skip, uint64_t* m, uint32_t* pv,
                              uint32_t lane) {
   if (len < 15) return true;
   const uint32_t shift = hash_shift(len), ip_limit = len - 15, ip = 1;
@@ -467,21 +476,50 @@ __device__ bool probe_stored(const uint8_t* g, uint32_t len, const uint32_t* ski
   }
 }
 
-// 4 bytes at p of the staged fragment, p clamped to its zero margin
+// The 4 bytes at p of the fragment g[0, len) (len >= 15), without reading a
+// dword that holds no byte of g[0, len): past len - 4 the word is the last
+// one shifted right (its low byte is still the byte at p); p >= len reads as
+// len - 1.
+__device__ __forceinline__ uint32_t gw32(const uint8_t* g, uint32_t p, uint32_t len) {
+  p = p < len ? p : len - 1;
+  const uint32_t q = p < len - 4 ? p : len - 4;
+  const uintptr_t a = reinterpret_cast<uintptr_t>(g + q);
+  const auto w = gbl<uint32_t>(reinterpret_cast<const void*>(a & ~(uintptr_t)3));
+  const uint32_t sh = (uint32_t)(a & 3);
+  const uint32_t lo = w[0];
+  const uint32_t hi = sh ? w[1] : 0u;
+  return __builtin_amdgcn_alignbyte(hi, lo, sh) >> (8 * (p - q));
+}
+__device__ __forceinline__ uint32_t lane_of(uint32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
+// the same from a fragment staged in LDS (16 zero bytes after it)
 __device__ __forceinline__ uint32_t ldc(const uint32_t* s, uint32_t p, uint32_t len) {
   return ld32(s, p < len ? p : len);
 }
-__device__ __forceinline__ uint32_t lane_of(uint32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
+// the parse's source: the fragment in memory (g) or staged in LDS (s)
+template <bool kLds>
+__device__ __forceinline__ uint32_t srcw(const uint8_t* g, const uint32_t* s, uint32_t p, uint32_t len) {
+  return kLds ? ldc(s, p, len) : gw32(g, p, len);
+}
 
-// A literal of len <= 60 bytes (one tag byte): lane 0 the tag, lanes
-// 1..len its bytes, one store instruction.
-__device__ __forceinline__ uint32_t emit_lit(uint8_t* out, uint32_t op, const uint8_t* srcb, uint32_t lit,
-                                             uint32_t len, uint32_t lane) {
-  if (len > 60) return emit_literal(out, op, srcb, lit, len, lane);
-  const uint8_t b = srcb[lit + (lane ? lane - 1 : 0)];
-  lane = PSF_SINK(lane);
-  if (lane <= len) out[op + lane] = lane ? b : (uint8_t)((len - 1) << 2);
-  return op + 1 + len;
+// The literal g[lit, lit + len) at op: for len <= 60 one tag byte (lane 0)
+// and the bytes (lanes 1..len), one store instruction; else the tag and a
+// wave copy.
+template <bool kLds>
+__device__ __forceinline__ uint32_t emit_lit(uint8_t* out, uint32_t op, const uint8_t* g, const uint32_t* s,
+                                             uint32_t glen, uint32_t lit, uint32_t len, uint32_t lane) {
+  if (len <= 60) {
+    uint32_t i = lit + (lane ? lane - 1 : 0);
+    i = i < glen ? i : glen - 1;
+    const uint8_t b = kLds ? reinterpret_cast<const uint8_t*>(s)[i] : gbl<uint8_t>(g)[i];
+    lane = PSF_SINK(lane);
+    if (lane <= len) out[op + lane] = lane ? b : (uint8_t)((len - 1) << 2);
+    return op + 1 + len;
+  }
+  const uint32_t hl = literal_tag(out + op, len, PSF_SINK(lane));
+#ifndef PSF_DIAG_NOSTORE
+  copy_bytes<64>(out + op + hl, g + lit, len, lane);
+#endif
+  return op + hl + len;
 }
 // EmitCopy (1.1.8) of a copy that fits one tag, one store instruction; the
 // rest go to emit_copy
@@ -508,10 +546,13 @@ __device__ __forceinline__ uint32_t emit_copy_fast(uint8_t* out, uint32_t op, ui
 #define PSF_CNT(i) ((void)0)
 #endif
 
-// The exact 1.1.8 parse of one staged fragment by one wave (CompressFragment,
+// The exact 1.1.8 parse of one fragment g[0, len) by one wave (CompressFragment,
 // snappy.cc): tags to out, returns {tag bytes, start of the final literal}.
-// One wave issues about one vector instruction per 4 cycles, so the parse is
-// bound by its instruction count per tag; the common paths are short:
+// The fragment is read from memory (what the probe touched is in L1 / L2); the
+// hash table and the skip loop's slot words are the wave's own LDS.  One wave
+// issues about one vector instruction per 4 cycles, so the parse is bound by
+// its instruction count and its dependent reads per tag; the common paths are
+// short:
 //  * copies: each lane holds the 4 bytes at ip + off + lane and at
 //    cand + off + lane, so one round of reads gives 64 bytes of the match
 //    length, and the bytes at the new ip - 1, ip and ip + 1 come from the
@@ -524,22 +565,24 @@ __device__ __forceinline__ uint32_t emit_copy_fast(uint8_t* out, uint32_t op, ui
 //    the first two steps' offsets sit in registers), every probe's hash slot,
 //    candidate and the slot's lowest probing lane read together; a lane whose
 //    earlier same-hash lane inserted this step compares with that lane's
-//    bytes; lanes past the first such lane wait for the next step (as in
-//    probe_stored).
-__device__ uint2 parse_fragment(CompressLds& L, const uint32_t* skip, uint32_t skA, uint32_t skB, uint32_t skC,
-                                uint32_t len, uint8_t* __restrict__ out, uint32_t lane
+//    bytes; lanes past the first lane with an earlier lane in its slot wait
+//    for the next step (as in probe_stored).
+template <bool kLds>
+__device__ __forceinline__ uint2 parse_fragment(uint16_t* __restrict__ table, uint32_t* __restrict__ minlane,
+                                                const uint32_t* skip, uint32_t skA, uint32_t skB, uint32_t skC,
+                                                const uint8_t* __restrict__ g, const uint32_t* s, uint32_t len,
+                                                uint8_t* __restrict__ out, uint32_t lane
 #ifdef PSF_DIAG_COUNT
-                                , uint32_t* cnt
+                                                , uint32_t* cnt
 #endif
-                                ) {
-  const uint32_t* s = L.src;
-  const uint8_t* srcb = reinterpret_cast<const uint8_t*>(L.src);
+) {
   uint32_t op = 0, next_emit = 0;
   if (len < 15) return make_uint2(0, 0);
   const uint32_t shift = hash_shift(len), ip_limit = len - 15;
   uint32_t ip = 1, kbase = 0;  // the skip loop from ip, at its probe kbase
   for (;;) {
-    // ---- skip loop steps
+    // ---- skip loop steps (loading the next step's probe bytes ahead
+    // measured slower: 16.6 against 15.9 ms for 128 MiB of sorted keys)
     uint32_t cand;
     for (;;) {
       PSF_CNT(0);
@@ -548,16 +591,16 @@ __device__ uint2 parse_fragment(CompressLds& L, const uint32_t* skip, uint32_t s
       const uint32_t o1 = kbase == 0 ? skB : kbase == 1 ? skC : skip[k + 1];
       const bool valid = ip + o1 <= ip_limit;  // else "goto emit_remainder"
       const uint32_t pos = ip + o0;
-      const uint32_t v = ldc(s, pos, len);
+      const uint32_t v = srcw<kLds>(g, s, pos, len);
       const uint32_t h = hash(v, shift);
       const uint32_t slot = valid ? (h & (kMinSlots - 1)) : kMinSlots;  // invalid lanes: the spare slot
-      const uint32_t c = L.table[h];
-      atomicMin(&L.minlane[slot], lane);
+      const uint32_t c = table[h];
+      atomicMin(&minlane[slot], lane);
       asm volatile("" ::: "memory");
-      const uint32_t fl = L.minlane[slot];
+      const uint32_t fl = minlane[slot];
       asm volatile("" ::: "memory");
-      L.minlane[slot] = 0xffffffffu;  // clean for the next step
-      const uint32_t wc = ld32(s, c);
+      minlane[slot] = 0xffffffffu;  // clean for the next step
+      const uint32_t wc = srcw<kLds>(g, s, c, len);
       const uint32_t first = valid ? fl : lane;
       const uint64_t vm = __ballot(valid);
       const uint64_t em = __ballot(valid && first < lane);
@@ -575,7 +618,7 @@ __device__ uint2 parse_fragment(CompressLds& L, const uint32_t* skip, uint32_t s
       const uint64_t mm = __ballot(m);
       const int last = mm ? __builtin_ctzll(mm) : limit;
       const bool overwritten = exact_pair && (int)lane == jm && jc <= last;
-      if (valid && (int)lane <= last && !overwritten) L.table[h] = (uint16_t)pos;
+      if (valid && (int)lane <= last && !overwritten) table[h] = (uint16_t)pos;
       if (mm) {
         const int ks = __builtin_ctzll(mm);
         cand = (exact_pair && ks == jc) ? lane_of(pos, jm) : lane_of(c, ks);
@@ -586,7 +629,7 @@ __device__ uint2 parse_fragment(CompressLds& L, const uint32_t* skip, uint32_t s
       if ((vm & lim_mask) != lim_mask) goto remainder;
       kbase += (uint32_t)limit + 1;
     }
-    op = emit_lit(out, op, srcb, next_emit, ip - next_emit, lane);
+    op = emit_lit<kLds>(out, op, g, s, len, next_emit, ip - next_emit, lane);
     // ---- copies
     {
       uint32_t off = 3, wa = 0, wb = 0;  // lane 0 of the first round: byte ip + 3 (known equal)
@@ -596,8 +639,8 @@ __device__ uint2 parse_fragment(CompressLds& L, const uint32_t* skip, uint32_t s
         for (;;) {
           const uint32_t pb = ip + off + lane;
           if (!have) {
-            wb = ldc(s, pb, len);
-            wa = ldc(s, cand + off + lane, len);
+            wb = srcw<kLds>(g, s, pb, len);
+            wa = srcw<kLds>(g, s, cand + off + lane, len);
           }
           have = false;
           const uint64_t bad = __ballot(pb >= len || ((wa ^ wb) & 0xffu) != 0);
@@ -614,17 +657,17 @@ __device__ uint2 parse_fragment(CompressLds& L, const uint32_t* skip, uint32_t s
         ip += off + k;
         next_emit = ip;
         if (ip >= ip_limit) goto remainder;
-        if (k == 63) nxt = uni(ldc(s, ip + 1, len));
-        const uint32_t hp = hash(prev, shift), hc = hash(cur, shift), hn = hash(nxt, shift);
-        if (lane == 0) L.table[hp] = (uint16_t)(ip - 1);
-        const uint32_t c = L.table[hc];
-        if (lane == 0) L.table[hc] = (uint16_t)ip;
-        const uint32_t c1 = L.table[hn];  // the skip loop's probe 0 at ip + 1, if ip does not match
-        wb = ldc(s, ip + lane, len);
-        const uint32_t wb1 = ldc(s, ip + 1 + lane, len);
-        wa = ldc(s, c + lane, len);
-        const uint32_t wa1 = ldc(s, c1 + lane, len);
         PSF_CNT(2);
+        if (k == 63) nxt = uni(srcw<kLds>(g, s, ip + 1, len));
+        const uint32_t hp = hash(prev, shift), hc = hash(cur, shift), hn = hash(nxt, shift);
+        if (lane == 0) table[hp] = (uint16_t)(ip - 1);
+        const uint32_t c = table[hc];
+        if (lane == 0) table[hc] = (uint16_t)ip;
+        const uint32_t c1 = table[hn];  // the skip loop's probe 0 at ip + 1, if ip does not match
+        wb = srcw<kLds>(g, s, ip + lane, len);
+        const uint32_t wb1 = srcw<kLds>(g, s, ip + 1 + lane, len);
+        wa = srcw<kLds>(g, s, c + lane, len);
+        const uint32_t wa1 = srcw<kLds>(g, s, c1 + lane, len);
         if (lane_of(wa, 0) == cur) {  // a copy from ip at once; its first round is loaded
           PSF_CNT(3);
           cand = uni(c);
@@ -634,11 +677,11 @@ __device__ uint2 parse_fragment(CompressLds& L, const uint32_t* skip, uint32_t s
         }
         ip += 1;  // the skip loop from ip + 1: probe 0 is made iff ip + 1 <= ip_limit
         if (ip + 1 > ip_limit) goto remainder;
-        if (lane == 0) L.table[hn] = (uint16_t)ip;
+        if (lane == 0) table[hn] = (uint16_t)ip;
         if (lane_of(wa1, 0) == nxt) {  // probe 0 matches: a one-byte literal, then a copy
           PSF_CNT(4);
           cand = uni(c1);
-          op = emit_lit(out, op, srcb, next_emit, 1, lane);
+          op = emit_lit<kLds>(out, op, g, s, len, next_emit, 1, lane);
           wa = wa1;
           wb = wb1;
           off = 0;
@@ -654,16 +697,15 @@ remainder:
   return make_uint2(op, next_emit);
 }
 
-// K-parse: persistent workgroups of 8 waves (the parse's LDS footprint allows
-// one per CU), each over its stripe of the fragments (b, b + G, b + 2G, ...)
-// in rounds of 8: every wave probes one fragment; then each fragment that
-// matched is staged in LDS and parsed by wave 0 (tags to its scratch slot).
-// No workgroup depends on another.
+// K-parse: persistent workgroups of 8 waves, each over its stripe of the
+// fragments (b, b + G, b + 2G, ...) in rounds of 8: every wave probes one
+// fragment; then the fragments that matched are parsed by waves
+// 0..kParseWaves-1, one fragment per wave at a time (tags to the fragment's
+// scratch slot).  No workgroup depends on another.
 __global__ __launch_bounds__(kCThreads) void snappy_parse(const SnappyCJobs J, uint8_t* __restrict__ scratch) {
   __shared__ uint32_t skip[kSkipN + 3];
   __shared__ CompressPhaseLds U;
   __shared__ uint32_t s_need[kCThreads / 64];
-  CompressLds& L = U.p;
   const uint32_t tid = threadIdx.x;
   const uint32_t wave = tid >> 6, lane = tid & 63;
   constexpr uint32_t W = kCThreads / 64;
@@ -675,7 +717,6 @@ __global__ __launch_bounds__(kCThreads) void snappy_parse(const SnappyCJobs J, u
   if (J.znext)  // the next launch chain's counters (stream order publishes them)
     for (uint32_t i = blockIdx.x * kCThreads + tid; i < J.zwords; i += gridDim.x * kCThreads) J.znext[i] = 0;
   __syncthreads();
-  uint8_t* srcb = reinterpret_cast<uint8_t*>(L.src);
   const uint32_t G = gridDim.x;
   for (uint32_t r0 = 0; (size_t)r0 * G + blockIdx.x < J.nfrag; r0 += W) {
     // ---- probe: wave w takes fragment (r0 + w) G + b
@@ -698,154 +739,70 @@ __global__ __launch_bounds__(kCThreads) void snappy_parse(const SnappyCJobs J, u
     for (uint32_t w = 0; w < W; ++w) need |= s_need[w] << w;
     __syncthreads();  // (the probe maps are overwritten by the parses)
     if (!need) continue;
-    for (uint32_t i = tid; i <= kMinSlots; i += kCThreads) L.minlane[i] = 0xffffffffu;  // each parse step cleans up after itself
-    // ---- parse the fragments that matched, one after another
-    while (need) {
-      const uint32_t w = __builtin_ctz(need);
-      need &= need - 1;
-      const uint32_t f = (r0 + w) * G + blockIdx.x;
+    // ---- parse.  One fragment (data with few matches: a fragment of
+    // FIXING_FLOAT codes now and then): staged in LDS where the other
+    // tables would be and parsed there by wave 0.  More: wave p < kParseWaves
+    // takes the matched fragments p, p + kParseWaves, ... from memory.
+    if (wave < kParseWaves)
+      for (uint32_t i = lane; i <= kMinSlots; i += 64) U.p.minlane[wave][i] = 0xffffffffu;  // each step cleans up after itself
+    if (__builtin_popcount(need) == 1) {
+      const uint32_t f = (r0 + __builtin_ctz(need)) * G + blockIdx.x;
       const CJob& c = cjob_of(J, f);
       const size_t start = (size_t)(f - c.frag0) * kFrag;
       const uint32_t len = (uint32_t)min((size_t)kFrag, c.n - start);
       const uint8_t* g = c.in + start;
+      uint32_t* src = reinterpret_cast<uint32_t*>(U.p.table[1]);  // tables 1..3: 96 KiB
+      uint8_t* srcb = reinterpret_cast<uint8_t*>(src);
       if (aligned16(g)) {
-        const uint4* g4 = reinterpret_cast<const uint4*>(g);
-        uint4* s4 = reinterpret_cast<uint4*>(L.src);
         const uint32_t nv = len >> 4;
-        for (uint32_t i = tid; i < nv; i += kCThreads) s4[i] = g4[i];
+        for (uint32_t i = tid; i < nv; i += kCThreads) reinterpret_cast<uint4*>(src)[i] = reinterpret_cast<const uint4*>(g)[i];
         if (tid < len - (nv << 4)) srcb[(nv << 4) + tid] = g[(nv << 4) + tid];
       } else {
         for (uint32_t i = tid; i < len; i += kCThreads) srcb[i] = g[i];
       }
       if (tid < 16) srcb[len + tid] = 0;
-      const uint32_t shift = hash_shift(len);
-      uint32_t* t32 = reinterpret_cast<uint32_t*>(L.table);
-      for (uint32_t i = tid; i < (1u << (32 - shift)) / 2; i += kCThreads) t32[i] = 0;
+      uint4* t16 = reinterpret_cast<uint4*>(U.p.table[0]);
+      for (uint32_t j = tid; j < (1u << (32 - hash_shift(len))) / 8; j += kCThreads) t16[j] = make_uint4(0, 0, 0, 0);
       __syncthreads();
       if (wave == 0) {
-#ifdef PSF_PARSE_OLD
-        uint8_t* out = scratch + (size_t)f * kSnappyFragOut;
-        uint32_t op = 0, next_emit = 0;
-        if (len >= 15) {
-          const uint32_t ip_limit = len - 15;
-          uint32_t ip = 1;
-          for (;;) {
-            // ---- skip loop: up to 64 probes per step, first match wins.  Probes are
-            // exact up to the first lane jc whose hash slot an earlier lane of the
-            // step also probed: lanes < jc see the table as it was, and lane jc either
-            // sees that lane's write (same hash; it is the only earlier one, a second
-            // would itself have been jc) or the table (slot alias).  Later lanes are
-            // dropped and the next step starts after jc.
-            uint32_t cand = 0, kbase = 0;
-            // probes 0 and 1 (at ip, ip + 1) first, as uniform values: data
-            // dense in short matches finds most of them there.  Probe 1 sees
-            // probe 0's table write when both hash alike.
-            if (ip + 1 > ip_limit) goto remainder;
-            {
-              const uint32_t v0 = uni(ld32(L.src, ip)), v1 = uni(ld32(L.src, ip + 1));
-              const uint32_t h0 = hash(v0, shift), h1 = hash(v1, shift);
-              const uint32_t c0 = uni(L.table[h0]);
-              const uint32_t c1 = h1 == h0 ? ip : uni(L.table[h1]);
-              const bool m0 = v0 == uni(ld32(L.src, c0));
-              const bool m1 = v1 == uni(ld32(L.src, c1));
-              if (lane == 0) L.table[h0] = (uint16_t)ip;
-              if (m0) {
-                cand = c0;
-                goto matched;
-              }
-              if (ip + 2 > ip_limit) goto remainder;  // probe 1 is past the limit
-              if (lane == 0) L.table[h1] = (uint16_t)(ip + 1);
-              if (m1) {
-                ip += 1;
-                cand = c1;
-                goto matched;
-              }
-              kbase = 2;
-            }
-            for (;;) {
-              const uint32_t k = kbase + lane;
-              const uint32_t pos = ip + skip[k];
-              const bool valid = ip + skip[k + 1] <= ip_limit;  // else "goto emit_remainder"
-              uint32_t v = 0, h = 0, slot = 0;
-              if (valid) {
-                v = ld32(L.src, pos);
-                h = hash(v, shift);
-                slot = h & (kMinSlots - 1);
-                atomicMin(&L.minlane[slot], lane);
-              }
-              asm volatile("" ::: "memory");
-              uint32_t first = valid ? L.minlane[slot] : lane;
-              asm volatile("" ::: "memory");
-              if (valid) L.minlane[slot] = 0xffffffffu;  // clean for the next step
-              const uint64_t vm = __ballot(valid);
-              const uint64_t em = __ballot(valid && first < lane);
-              int limit = 63;  // last exact lane
-              int jc = 64, jm = 0;
-              bool exact_pair = false;
-              if (em) {
-                jc = __builtin_ctzll(em);
-                jm = (int)__builtin_amdgcn_readlane(first, jc);
-                exact_pair = __builtin_amdgcn_readlane(h, jm) == __builtin_amdgcn_readlane(h, jc);
-                limit = jc;
-              }
-              uint32_t c = valid ? L.table[h] : 0;
-              if (exact_pair && (int)lane == jc) c = __builtin_amdgcn_readlane(pos, jm);
-              const bool m = valid && (int)lane <= limit && v == ld32(L.src, c);
-              const uint64_t mm = __ballot(m);
-              const uint64_t lim_mask = limit >= 63 ? ~0ull : ((1ull << (limit + 1)) - 1);
-              const int last = mm ? __builtin_ctzll(mm) : limit;
-              const bool overwritten = exact_pair && (int)lane == jm && jc <= last;
-              if (valid && (int)lane <= last && !overwritten) L.table[h] = (uint16_t)pos;
-              if (mm) {
-                const int ks = __builtin_ctzll(mm);
-                ip = __builtin_amdgcn_readlane(pos, ks);
-                cand = __builtin_amdgcn_readlane(c, ks);
-                break;
-              }
-              if ((vm & lim_mask) != lim_mask) goto remainder;
-              kbase += (uint32_t)limit + 1;
-            }
-          matched:
-            op = emit_literal(out, op, srcb, next_emit, ip - next_emit, lane);
-            // ---- emit copies while the next position matches immediately
-            for (;;) {
-              const uint32_t base = ip;
-              const uint32_t matched = 4 + uni(match_len(srcb, cand + 4, ip + 4, len, lane));
-              ip += matched;
-              op = emit_copy(out, op, base - cand, matched, lane);
-              next_emit = ip;
-              if (ip >= ip_limit) goto remainder;
-              const uint32_t prev = ld32(L.src, ip - 1);
-              const uint32_t cur = uni(ld32(L.src, ip));
-              if (lane == 0) L.table[hash(prev, shift)] = (uint16_t)(ip - 1);
-              const uint32_t ch = hash(cur, shift);
-              cand = uni(L.table[ch]);
-              const uint32_t cb = uni(ld32(L.src, cand));
-              if (lane == 0) L.table[ch] = (uint16_t)ip;
-              if (cur != cb) break;
-            }
-            ip += 1;
-          }
-        }
-      remainder:
-#else
-        const uint2 r = parse_fragment(L, skip, sk0, sk1, sk2, len, scratch + (size_t)f * kSnappyFragOut, lane
+        const uint2 r = parse_fragment<true>(U.p.table[0], U.p.minlane[0], skip, sk0, sk1, sk2, g, src, len,
+                                             scratch + (size_t)f * kSnappyFragOut, lane
 #ifdef PSF_DIAG_COUNT
-                                       , cnt
+                                             , cnt
 #endif
-                                       );
-        const uint32_t op = r.x, next_emit = r.y;
-#endif
-        if (lane == 0) J.finfo[f] = ((uint64_t)op << 32) | next_emit;
-        PSF_TRACE(f, 1);
+        );
+        if (lane == 0) J.finfo[f] = ((uint64_t)r.x << 32) | r.y;
       }
-      __syncthreads();
+    } else if (wave < kParseWaves) {
+      uint16_t* table = U.p.table[wave];
+      uint32_t* minlane = U.p.minlane[wave];
+      uint32_t m = need;
+      for (uint32_t i = 0; m; ++i) {
+        const uint32_t w = __builtin_ctz(m);
+        m &= m - 1;
+        if (i % kParseWaves != wave) continue;
+        const uint32_t f = (r0 + w) * G + blockIdx.x;
+        const CJob& c = cjob_of(J, f);
+        const size_t start = (size_t)(f - c.frag0) * kFrag;
+        const uint32_t len = (uint32_t)min((size_t)kFrag, c.n - start);
+        uint4* t16 = reinterpret_cast<uint4*>(table);
+        for (uint32_t j = lane; j < (1u << (32 - hash_shift(len))) / 8; j += 64) t16[j] = make_uint4(0, 0, 0, 0);
+        asm volatile("" ::: "memory");
+        const uint2 r = parse_fragment<false>(table, minlane, skip, sk0, sk1, sk2, c.in + start, nullptr, len,
+                                              scratch + (size_t)f * kSnappyFragOut, lane
+#ifdef PSF_DIAG_COUNT
+                                              , cnt
+#endif
+        );
+        if (lane == 0) J.finfo[f] = ((uint64_t)r.x << 32) | r.y;
+      }
     }
+    __syncthreads();  // (the next round's probe maps overwrite the tables)
   }
 #ifdef PSF_DIAG_COUNT
-  if (blockIdx.x == 0 && tid == 0)
-    printf("parse counts wg0: steps %u ext_rounds %u copies %u immediate %u probe0 %u\n", cnt[0], cnt[1], cnt[2],
-           cnt[3], cnt[4]);
+  if (blockIdx.x == 0 && lane == 0 && wave < kParseWaves)
+    printf("parse counts wg0 wave %u: steps %u ext_rounds %u copies %u immediate %u probe0 %u\n", wave, cnt[0],
+           cnt[1], cnt[2], cnt[3], cnt[4]);
 #endif
 }
 

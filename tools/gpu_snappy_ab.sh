@@ -11,7 +11,7 @@ fi
 for v in "$@"; do
   if [ "$v" = base ]; then unset PSF_LIBRARY_VARIANT; else export PSF_LIBRARY_VARIANT=tools/variants/$v/libpsf.so; fi
   echo "== $v"
-  timeout -k 10 200 python3 tools/bench_snappy.py --mib 128 --no-cpu --no-check --reps 2 --only $P > $O/b_$v.log 2>&1 || exit 1
+  timeout -k 10 200 python3 tools/bench_snappy.py --mib 128 --no-cpu --no-check --reps ${REPS:-2} --only $P > $O/b_$v.log 2>&1 || exit 1
   grep payload $O/b_$v.log | python3 -c "
 import sys, json
 for l in sys.stdin:
