@@ -74,7 +74,7 @@ def main():
         rec = {"payload": name, "bytes": nbytes, "compressed": int(s.numel()),
                "ratio": round(s.numel() / nbytes, 4),
                "gpu_compress_GBps": round(nbytes / tc / 1e9, 2),
-               "gpu_uncompress_GBps": round(nbytes / td / 1e9, 2)}
+               "gpu_uncompress_GBps": None if a.no_check else round(nbytes / td / 1e9, 2)}
         for k, (nl, ms, _) in prof.items():
             rec[f"{k}_kernel_ms"] = round(ms / nl, 3)
         if ref is not None:
