@@ -515,6 +515,9 @@ __device__ __forceinline__ uint32_t emit_lit(uint8_t* out, uint32_t op, const ui
     if (lane <= len) out[op + lane] = lane ? b : (uint8_t)((len - 1) << 2);
     return op + 1 + len;
   }
+  // a staged fragment: 16-byte stores composed from LDS (a wave issues them
+  // back to back); from memory: the wave copy (loads before stores)
+  if (kLds) return emit_literal(out, op, reinterpret_cast<const uint8_t*>(s), lit, len, lane);
   const uint32_t hl = literal_tag(out + op, len, PSF_SINK(lane));
 #ifndef PSF_DIAG_NOSTORE
   copy_bytes<64>(out + op + hl, g + lit, len, lane);
@@ -901,6 +904,8 @@ __global__ __launch_bounds__(kPlaceT) void snappy_place(const SnappyCJobs J, con
 // ------------------------------------------------------------------ uncompress
 constexpr uint32_t kWin = 16384;   // compressed bytes per parse window (16 KiB: ~8 waves per CU)
 constexpr uint32_t kInWin = 8192;  // staged compressed bytes in the fragment decoder
+constexpr uint32_t kBatchLit = 16;     // literals the fragment decoder's batches take (longer ones: one by one)
+constexpr uint32_t kBatchMargin = 96;  // staged bytes past p a batch reads: 64 tag starts + a tag + kBatchLit
 constexpr uint64_t kNone = ~0ull;
 constexpr uint32_t kFlagInvalid = 1, kFlagSerial = 2, kFlagScan = 4, kFlagHeader = 8;
 constexpr uint64_t kFullLit = 65536 + 3;  // a 64 KiB fragment stored as one literal (tag 0xF4 + 2 length bytes)
@@ -1882,11 +1887,62 @@ __global__ __launch_bounds__(256) void snappy_dfrag(const SnappyDJobs J) {
         uint64_t p = p0, wb = p0;
         uint32_t s = stage(ib32, in, C, wb, kSpan, lane);
         uint32_t o = 0;
+        const uint8_t* ibb = reinterpret_cast<const uint8_t*>(ib32);
         while (o < end) {
-          if (p + 8 > wb + kSpan) {
+          if (p + kBatchMargin > wb + kSpan) {
             wb = p;
             s = stage(ib32, in, C, wb, kSpan, lane);
           }
+          // ---- a batch: the tags that start in [p, p + 64).  Every lane
+          // decodes the tag that would start at p + lane; one scalar walk
+          // picks the true chain (output offset and lane of tag k into lane
+          // k); then every literal of the batch is written at once (lane k:
+          // tag k's bytes) and the copies one after another in tag order (a
+          // copy reads only output before it: earlier literals, done, and
+          // earlier copies, done in order).  The walk stops at the
+          // fragment's end and before a tag it does not take (a literal
+          // longer than kBatchLit bytes); that one goes the single way below.
+          {
+            const uint32_t qb = s + (uint32_t)(p - wb);
+            const Tag tl = lds_tag(ib32, qb + lane, p + lane);
+            const uint32_t adv = (uint32_t)(tl.next - (p + lane)), tlen = (uint32_t)tl.len;
+            const uint64_t simple = __ballot(!tl.lit || tl.len <= kBatchLit);
+            uint32_t q = 0, nt = 0, vo = 0, vq = 0;
+            while (q < 64 && o < end && ((simple >> q) & 1)) {
+              vo = lane == nt ? o : vo;
+              vq = lane == nt ? q : vq;
+              o += __builtin_amdgcn_readlane(tlen, q);
+              q += __builtin_amdgcn_readlane(adv, q);
+              ++nt;
+            }
+            if (nt) {
+              const bool mine = lane < nt;
+              const uint32_t src = mine ? vq : 0;  // tag k's lane
+              const uint32_t klit = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * src, tl.lit ? 1 : 0);
+              const uint32_t klen = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * src, (int)tlen);
+              const uint32_t khl = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * src, (int)tl.hl);
+              const uint32_t koff = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * src, (int)tl.off);
+              if (mine && klit) {
+                const uint8_t* d = ibb + qb + src + khl;
+                for (uint32_t j = 0; j < klen; ++j) ob[vo + j] = d[j];
+              }
+              uint64_t cm = __ballot(mine && !klit);
+              while (cm) {
+                const uint32_t k = (uint32_t)__builtin_ctzll(cm);
+                cm &= cm - 1;
+                const uint32_t ko = __builtin_amdgcn_readlane(vo, k);
+                const uint32_t L = __builtin_amdgcn_readlane(klen, k), off = __builtin_amdgcn_readlane(koff, k);
+                if (off >= L) {
+                  if (lane < L) ob[ko + lane] = ob[ko - off + lane];
+                } else if (lane < L) {
+                  ob[ko + lane] = ob[ko - off + lane % off];
+                }
+              }
+            }
+            p += q;
+            if (o >= end || q >= 64) continue;
+          }
+          // ---- one tag the general way
           const Tag t = lds_tag(ib32, s + (p - wb), p);
           const uint32_t L = (uint32_t)t.len;
           if (t.lit) {
