@@ -967,6 +967,17 @@ __device__ __forceinline__ Tag decode_tag(uint64_t x, uint64_t p) {
   return t;
 }
 
+__device__ __forceinline__ uint32_t lane_of32(uint32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ uint64_t lane_of64(uint64_t v, uint32_t l) {
+  return ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32) | __builtin_amdgcn_readlane((uint32_t)v, l);
+}
+// lane l's 64-bit v, in every lane (l per lane)
+__device__ __forceinline__ uint64_t bperm64(uint32_t l, uint64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * l, (int)(uint32_t)v);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * l, (int)(uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+
 // tag at LDS byte q of w (one two-dword read; q + 8 bytes must be staged)
 __device__ __forceinline__ Tag lds_tag(const uint32_t* w, uint64_t q, uint64_t p) {
   const uint32_t i = (uint32_t)(q >> 2);
@@ -1673,7 +1684,43 @@ __device__ void dlink_body(const uint8_t* __restrict__ in, uint64_t C, uint32_t 
 // K1: speculative parse of each window from each of its first 64 byte offsets
 // (lane l from offset l).  A window's true entry is one of them unless a literal
 // carried the chain further in; for those K2 walks until it meets lane 0's chain.
-__device__ void dscan_body(const SnappyDJobs& J, uint32_t ji, uint32_t w, uint32_t* b32, uint32_t* bm) {
+constexpr uint32_t kEarly = 1024;  // bytes of a window where K1's starts are expected to meet lane 0's chain
+
+// The chain of tags from p (relative to the staged window) to the first
+// position >= wl, walked by the wave in batches: every lane decodes the tag
+// that would start at p + lane, one scalar walk picks the chain's tags in
+// [p, p + 64).  Adds the output to o, returns the exit position.  kRecord:
+// lane 0's chain of K1 -- each tag into the bitmap, its output count before
+// it into cum (and cum0 below kEarly).
+template <bool kRecord>
+__device__ uint64_t scan_walk(const uint32_t* b32, uint32_t s, uint32_t wl, uint64_t p, uint64_t& o, uint32_t lane,
+                              uint32_t* bm, uint32_t* __restrict__ cum, uint32_t* cum0) {
+  while (p < wl) {
+    const uint64_t pl = min(p + lane, (uint64_t)wl);
+    const Tag tl = lds_tag(b32, s + pl, pl);
+    const uint64_t adv = tl.next - pl;
+    uint32_t q = 0, nt = 0, vq = 0;
+    uint64_t vo = 0;
+    while (q < 64 && p + q < wl) {
+      vo = lane == nt ? o : vo;
+      vq = lane == nt ? q : vq;
+      o += lane_of64(tl.len, q);
+      q += (uint32_t)min(lane_of64(adv, q), (uint64_t)64);
+      ++nt;
+    }
+    if (kRecord && lane < nt) {
+      const uint64_t r = p + vq;
+      atomicOr(&bm[r >> 5], 1u << (r & 31));
+      cum[r] = (uint32_t)vo;
+      if (r < kEarly) cum0[r] = (uint32_t)vo;
+    }
+    const uint32_t ql = lane_of32(vq, nt - 1);
+    p += ql + lane_of64(adv, ql);
+  }
+  return p;
+}
+
+__device__ void dscan_body(const SnappyDJobs& J, uint32_t ji, uint32_t w, uint32_t* b32, uint32_t* bm, uint32_t* cum0) {
   const DJob& D = J.j[ji];
   const DScr S = dscr(J, D, ji);
   if (!(*S.flags & kFlagScan)) return;  // K0 linked the stream already
@@ -1690,22 +1737,57 @@ __device__ void dscan_body(const SnappyDJobs& J, uint32_t ji, uint32_t w, uint32
   const uint32_t s = stage(b32, in, C, base, wl + 16, lane);
   for (uint32_t i = lane; i < kWin / 32; i += 64) bm[i] = 0;
   __syncthreads();
-  uint64_t p = lane, o = 0;
-  bool alive = p < wl;
+  // ---- lane 0's chain (from offset 0) in batches: its tags into the
+  // bitmap, each tag's output count before it into cum (K2), and for the
+  // first kEarly bytes into cum0 (the other starts meet it there)
+  uint64_t o = 0;
+  const uint64_t exit0 = scan_walk<true>(b32, s, wl, 0, o, lane, bm, cum + base, cum0);
+  const uint64_t total0 = o;
+  __syncthreads();
+  // ---- the other starts: each lane steps its own chain until it lands on
+  // lane 0's (its exit is then lane 0's and its total follows from cum0),
+  // leaves the window, or passes kEarly bytes.  Starts on one chain that
+  // never meets lane 0's (sorted keys: the chain that reads every copy's
+  // offset byte as a 3-byte literal) stop at the same first position past
+  // kEarly; each such position is walked to the end once, in batches.
+  uint64_t p = lane;
+  o = 0;
+  bool alive = lane > 0 && p < wl;
+  bool pending = false;
+  uint64_t ex = lane == 0 ? exit0 : p, tot = lane == 0 ? total0 : 0;
   while (__ballot(alive)) {
     if (alive) {
-      if (lane == 0) {
-        atomicOr(&bm[p >> 5], 1u << (p & 31));
-        cum[base + p] = (uint32_t)o;
+      if (p < kEarly && ((bm[p >> 5] >> (p & 31)) & 1)) {
+        ex = exit0;
+        tot = o + total0 - cum0[p];
+        alive = false;
+      } else {
+        const Tag t = lds_tag(b32, s + p, p);
+        o += t.len;
+        p = t.next;
+        if (p >= wl) {
+          ex = p;
+          tot = o;
+          alive = false;
+        } else if (p >= kEarly) {
+          pending = true;
+          alive = false;
+        }
       }
-      const Tag t = lds_tag(b32, s + p, p);
-      o += t.len;
-      p = t.next;
-      alive = p < wl;
     }
   }
-  wexit[(size_t)w * kStarts + lane] = base + p;
-  wtotal[(size_t)w * kStarts + lane] = o;
+  for (uint64_t pm = __ballot(pending); pm; pm = __ballot(pending)) {
+    const uint64_t P = lane_of64(p, (uint32_t)__builtin_ctzll(pm));
+    uint64_t oP = 0;
+    const uint64_t eP = scan_walk<false>(b32, s, wl, P, oP, lane, nullptr, nullptr, nullptr);
+    if (pending && p == P) {
+      ex = eP;
+      tot = o + oP;
+      pending = false;
+    }
+  }
+  wexit[(size_t)w * kStarts + lane] = base + ex;
+  wtotal[(size_t)w * kStarts + lane] = tot;
   __syncthreads();
   uint32_t* gb = bitmap + (size_t)w * (kWin / 32);
   for (uint32_t i = lane; i < kWin / 32; i += 64) gb[i] = bm[i];
@@ -1744,21 +1826,44 @@ __device__ void dindex_body(const SnappyDJobs& J, uint32_t ji, uint32_t w, uint3
   }
   const uint32_t s = stage(b32, in, C, base, wl + 16, lane);
   __syncthreads();
-  if (lane != 0) return;
   uint64_t p = e - base, o = woff[w];
   uint32_t fl = 0;
   while (p < wl) {
-    const Tag t = lds_tag(b32, s + p, p);
-    if (!t.lit) {
-      if (t.off == 0 || t.off > o) fl |= kFlagInvalid;
-      else if (o - t.off < (o & ~(uint64_t)(kFrag - 1))) fl |= kFlagSerial;
+    // a batch (as in the fragment decoder): every lane decodes the tag that
+    // would start at p + lane, one scalar walk picks the chain's tags in
+    // [p, p + 64) (tag k's lane and output offset into lane k), then lane k
+    // checks tag k
+    const uint64_t pl = min(p + lane, (uint64_t)wl);
+    const Tag tl = lds_tag(b32, s + pl, pl);
+    const uint64_t adv = tl.next - pl;
+    uint32_t q = 0, nt = 0, vq = 0;
+    uint64_t vo = 0;
+    while (q < 64 && p + q < wl) {
+      vo = lane == nt ? o : vo;
+      vq = lane == nt ? q : vq;
+      o += lane_of64(tl.len, q);
+      q += (uint32_t)min(lane_of64(adv, q), (uint64_t)64);
+      ++nt;
     }
-    if ((o & (kFrag - 1)) == 0) fragpos[o / kFrag] = base + p;
-    if (o / kFrag != (o + t.len - 1) / kFrag) fl |= kFlagSerial;
-    o += t.len;
-    p = t.next;
+    const bool mine = lane < nt;
+    const uint32_t src = mine ? vq : 0;
+    const bool lit = __builtin_amdgcn_ds_bpermute(4 * src, tl.lit ? 1 : 0) != 0;
+    const uint32_t off = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * src, (int)tl.off);
+    const uint64_t len = bperm64(src, tl.len);
+    bool inval = false, serial = false;
+    if (mine) {
+      if (!lit) {
+        if (off == 0 || off > vo) inval = true;
+        else if (vo - off < (vo & ~(uint64_t)(kFrag - 1))) serial = true;
+      }
+      if ((vo & (kFrag - 1)) == 0) fragpos[vo / kFrag] = base + p + src;
+      if (vo / kFrag != (vo + len - 1) / kFrag) serial = true;
+    }
+    if (__ballot(inval)) fl |= kFlagInvalid;
+    if (__ballot(serial)) fl |= kFlagSerial;
+    p = nt ? p + lane_of32(vq, nt - 1) + lane_of64(adv, lane_of32(vq, nt - 1)) : p;
   }
-  if (fl) atomicOr(flags, fl);
+  if (fl && lane == 0) atomicOr(flags, fl);
 }
 
 // K1, K2 and K3 as three ordinary launches: stream order is the barrier
@@ -1777,12 +1882,13 @@ __device__ __forceinline__ void dslow_needs(const SnappyDJobs& J, bool& scan, bo
 __global__ __launch_bounds__(64) void snappy_dscan(const SnappyDJobs J) {
   __shared__ uint32_t b32[(kWin + 32) / 4];
   __shared__ uint32_t bm[kWin / 32];
+  __shared__ uint32_t cum0[kEarly];
   bool scan, index;
   dslow_needs(J, scan, index);
   if (!scan) return;
   for (uint32_t w = blockIdx.x; w < J.nwin; w += gridDim.x) {
     const uint32_t ji = djob_win(J, w);
-    dscan_body(J, ji, w - J.j[ji].win0, b32, bm);
+    dscan_body(J, ji, w - J.j[ji].win0, b32, bm, cum0);
   }
 }
 // K2: one workgroup per stream links its windows
