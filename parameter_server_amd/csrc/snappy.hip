@@ -971,6 +971,29 @@ __device__ __forceinline__ uint32_t lane_of32(uint32_t v, uint32_t l) { return _
 __device__ __forceinline__ uint64_t lane_of64(uint64_t v, uint32_t l) {
   return ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32) | __builtin_amdgcn_readlane((uint32_t)v, l);
 }
+// The tag starts of a batch: lane l holds the (clamped) advance a of the tag
+// that would start at p + l; from offset 0 the chain goes l -> l + a(l).
+// Returns the bit mask of the chain's offsets below 64 that start before
+// `lim` (relative to p) and lie in `ok`: a few scalar instructions per tag.
+__device__ __forceinline__ uint64_t batch_mask(uint32_t a, uint64_t lim, uint64_t ok) {
+  uint64_t M = 0;
+  for (uint32_t q = 0; q < 64 && q < lim && ((ok >> q) & 1);) {
+    M |= 1ull << q;
+    q += __builtin_amdgcn_readlane(a, q);
+  }
+  return M;
+}
+// exclusive sum over the wave's lanes below this one
+__device__ __forceinline__ uint32_t wave_excl_sum(uint32_t v, uint32_t lane) {
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if ((int)lane >= d) x += y;
+  }
+  return x - v;
+}
+
 // lane l's 64-bit v, in every lane (l per lane)
 __device__ __forceinline__ uint64_t bperm64(uint32_t l, uint64_t v) {
   const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * l, (int)(uint32_t)v);
@@ -1699,23 +1722,20 @@ __device__ uint64_t scan_walk(const uint32_t* b32, uint32_t s, uint32_t wl, uint
     const uint64_t pl = min(p + lane, (uint64_t)wl);
     const Tag tl = lds_tag(b32, s + pl, pl);
     const uint64_t adv = tl.next - pl;
-    uint32_t q = 0, nt = 0, vq = 0;
-    uint64_t vo = 0;
-    while (q < 64 && p + q < wl) {
-      vo = lane == nt ? o : vo;
-      vq = lane == nt ? q : vq;
-      o += lane_of64(tl.len, q);
-      q += (uint32_t)min(lane_of64(adv, q), (uint64_t)64);
-      ++nt;
-    }
-    if (kRecord && lane < nt) {
-      const uint64_t r = p + vq;
+    const uint64_t M = batch_mask((uint32_t)min(adv, (uint64_t)64), wl - p, ~0ull);
+    const bool tag = (M >> lane) & 1;
+    // a tag's output offset in the batch: every tag before the last has a
+    // length <= 64 (it ends inside the batch)
+    const uint32_t rel = wave_excl_sum(tag ? (uint32_t)min(tl.len, (uint64_t)64) : 0u, lane);
+    if (kRecord && tag) {
+      const uint64_t r = p + lane;
       atomicOr(&bm[r >> 5], 1u << (r & 31));
-      cum[r] = (uint32_t)vo;
-      if (r < kEarly) cum0[r] = (uint32_t)vo;
+      cum[r] = (uint32_t)(o + rel);
+      if (r < kEarly) cum0[r] = (uint32_t)(o + rel);
     }
-    const uint32_t ql = lane_of32(vq, nt - 1);
-    p += ql + lane_of64(adv, ql);
+    const uint32_t last = 63 - __builtin_clzll(M);
+    o += lane_of32(rel, last) + lane_of64(tl.len, last);
+    p += last + lane_of64(adv, last);
   }
   return p;
 }
@@ -1829,39 +1849,27 @@ __device__ void dindex_body(const SnappyDJobs& J, uint32_t ji, uint32_t w, uint3
   uint64_t p = e - base, o = woff[w];
   uint32_t fl = 0;
   while (p < wl) {
-    // a batch (as in the fragment decoder): every lane decodes the tag that
-    // would start at p + lane, one scalar walk picks the chain's tags in
-    // [p, p + 64) (tag k's lane and output offset into lane k), then lane k
-    // checks tag k
+    // a batch (as in K1): lane l checks the chain's tag at p + l, if any
     const uint64_t pl = min(p + lane, (uint64_t)wl);
     const Tag tl = lds_tag(b32, s + pl, pl);
     const uint64_t adv = tl.next - pl;
-    uint32_t q = 0, nt = 0, vq = 0;
-    uint64_t vo = 0;
-    while (q < 64 && p + q < wl) {
-      vo = lane == nt ? o : vo;
-      vq = lane == nt ? q : vq;
-      o += lane_of64(tl.len, q);
-      q += (uint32_t)min(lane_of64(adv, q), (uint64_t)64);
-      ++nt;
-    }
-    const bool mine = lane < nt;
-    const uint32_t src = mine ? vq : 0;
-    const bool lit = __builtin_amdgcn_ds_bpermute(4 * src, tl.lit ? 1 : 0) != 0;
-    const uint32_t off = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * src, (int)tl.off);
-    const uint64_t len = bperm64(src, tl.len);
+    const uint64_t M = batch_mask((uint32_t)min(adv, (uint64_t)64), wl - p, ~0ull);
+    const bool tag = (M >> lane) & 1;
+    const uint64_t vo = o + wave_excl_sum(tag ? (uint32_t)min(tl.len, (uint64_t)64) : 0u, lane);
     bool inval = false, serial = false;
-    if (mine) {
-      if (!lit) {
-        if (off == 0 || off > vo) inval = true;
-        else if (vo - off < (vo & ~(uint64_t)(kFrag - 1))) serial = true;
+    if (tag) {
+      if (!tl.lit) {
+        if (tl.off == 0 || tl.off > vo) inval = true;
+        else if (vo - tl.off < (vo & ~(uint64_t)(kFrag - 1))) serial = true;
       }
-      if ((vo & (kFrag - 1)) == 0) fragpos[vo / kFrag] = base + p + src;
-      if (vo / kFrag != (vo + len - 1) / kFrag) serial = true;
+      if ((vo & (kFrag - 1)) == 0) fragpos[vo / kFrag] = base + pl;
+      if (vo / kFrag != (vo + tl.len - 1) / kFrag) serial = true;
     }
     if (__ballot(inval)) fl |= kFlagInvalid;
     if (__ballot(serial)) fl |= kFlagSerial;
-    p = nt ? p + lane_of32(vq, nt - 1) + lane_of64(adv, lane_of32(vq, nt - 1)) : p;
+    const uint32_t last = 63 - __builtin_clzll(M);
+    o = lane_of64(vo, last) + lane_of64(tl.len, last);
+    p += last + lane_of64(adv, last);
   }
   if (fl && lane == 0) atomicOr(flags, fl);
 }
@@ -2030,9 +2038,10 @@ __global__ __launch_bounds__(256) void snappy_dfrag(const SnappyDJobs J) {
           }
           // ---- a batch: the tags that start in [p, p + 64).  Every lane
           // decodes the tag that would start at p + lane; one scalar walk
-          // picks the true chain (output offset and lane of tag k into lane
-          // k); then every literal of the batch is written at once (lane k:
-          // tag k's bytes) and the copies one after another in tag order (a
+          // marks the chain's tag starts (batch_mask) and one wave prefix sum
+          // gives each its output offset; then every literal of the batch is
+          // written at once (by the lane of its tag) and the copies one after
+          // another in tag order (a
           // copy reads only output before it: earlier literals, done, and
           // earlier copies, done in order).  The walk stops at the
           // fragment's end and before a tag it does not take (a literal
@@ -2040,42 +2049,32 @@ __global__ __launch_bounds__(256) void snappy_dfrag(const SnappyDJobs J) {
           {
             const uint32_t qb = s + (uint32_t)(p - wb);
             const Tag tl = lds_tag(ib32, qb + lane, p + lane);
-            const uint32_t adv = (uint32_t)(tl.next - (p + lane)), tlen = (uint32_t)tl.len;
-            const uint64_t simple = __ballot(!tl.lit || tl.len <= kBatchLit);
-            uint32_t q = 0, nt = 0, vo = 0, vq = 0;
-            while (q < 64 && o < end && ((simple >> q) & 1)) {
-              vo = lane == nt ? o : vo;
-              vq = lane == nt ? q : vq;
-              o += __builtin_amdgcn_readlane(tlen, q);
-              q += __builtin_amdgcn_readlane(adv, q);
-              ++nt;
-            }
-            if (nt) {
-              const bool mine = lane < nt;
-              const uint32_t src = mine ? vq : 0;  // tag k's lane
-              const uint32_t klit = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * src, tl.lit ? 1 : 0);
-              const uint32_t klen = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * src, (int)tlen);
-              const uint32_t khl = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * src, (int)tl.hl);
-              const uint32_t koff = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * src, (int)tl.off);
-              if (mine && klit) {
-                const uint8_t* d = ibb + qb + src + khl;
-                for (uint32_t j = 0; j < klen; ++j) ob[vo + j] = d[j];
+            const uint32_t adv = (uint32_t)min(tl.next - (p + lane), (uint64_t)64);
+            const uint32_t tlen = (uint32_t)min(tl.len, (uint64_t)64);
+            const uint64_t M0 = batch_mask(adv, 64, __ballot(!tl.lit || tl.len <= kBatchLit));
+            const bool tag0 = (M0 >> lane) & 1;
+            const uint32_t vo = o + wave_excl_sum(tag0 ? tlen : 0u, lane);
+            const uint64_t M = M0 & __ballot(vo < end);  // tags past the fragment's end are not its own
+            if (M) {
+              const bool tag = (M >> lane) & 1;
+              if (tag && tl.lit) {
+                const uint8_t* d = ibb + qb + lane + tl.hl;
+                for (uint32_t j = 0; j < tlen; ++j) ob[vo + j] = d[j];
               }
-              uint64_t cm = __ballot(mine && !klit);
-              while (cm) {
+              for (uint64_t cm = __ballot(tag && !tl.lit); cm; cm &= cm - 1) {
                 const uint32_t k = (uint32_t)__builtin_ctzll(cm);
-                cm &= cm - 1;
-                const uint32_t ko = __builtin_amdgcn_readlane(vo, k);
-                const uint32_t L = __builtin_amdgcn_readlane(klen, k), off = __builtin_amdgcn_readlane(koff, k);
+                const uint32_t ko = lane_of32(vo, k), L = lane_of32(tlen, k), off = lane_of32(tl.off, k);
                 if (off >= L) {
                   if (lane < L) ob[ko + lane] = ob[ko - off + lane];
                 } else if (lane < L) {
                   ob[ko + lane] = ob[ko - off + lane % off];
                 }
               }
+              const uint32_t last = 63 - __builtin_clzll(M);
+              o = lane_of32(vo, last) + lane_of32(tlen, last);
+              p += last + lane_of32(adv, last);
+              if (o >= end || last + lane_of32(adv, last) >= 64) continue;
             }
-            p += q;
-            if (o >= end || q >= 64) continue;
           }
           // ---- one tag the general way
           const Tag t = lds_tag(ib32, s + (p - wb), p);
