@@ -677,6 +677,7 @@ int psf_nodes_roundtrip_ex(psf_node* const* snd, psf_node* const* rcv, const psf
     // previous iteration's last encode, collected when the iteration starts
     psf::PresignJob next = psf::presign_launch(s.data(), tp.data(), iters ? n : 0, true);
     for (int it = 0; it < iters; ++it) {
+      PSF_HPROF(14);
       {
         PSF_HPROF(12);
         std::fill(eh.begin(), eh.end(), psf::KeySigHint{});
@@ -696,7 +697,10 @@ int psf_nodes_roundtrip_ex(psf_node* const* snd, psf_node* const* rcv, const psf
           PSF_HPROF(1);
           psf::encode_batch(s.data() + b, mp.data() + b, e - b, eh.data() + b);
         }
-        if (e == n && it + 1 < iters) next = psf::presign_launch(s.data(), tp.data(), n, true);
+        if (e == n && it + 1 < iters) {
+          PSF_HPROF(13);
+          next = psf::presign_launch(s.data(), tp.data(), n, true);
+        }
         {
           PSF_HPROF(5);
           for (int i = b; i < e; ++i) {

@@ -197,11 +197,12 @@ struct PresignJob {
     Context* ctx;
     const uint8_t* ptr;
     size_t bytes;
-    std::vector<int> users;
+    int first, last;  // the messages with this key buffer: first, next[first], ..., last
     uint32_t tk[2];
     int slot0;
   };
   std::vector<Buf> bufs;
+  std::vector<int> next;  // per message: the next message of its buffer, or -1
   bool ahead = false;
 };
 PresignJob presign_launch(RemoteNode* const* nodes, const Message* const* msgs, int n, bool ahead);

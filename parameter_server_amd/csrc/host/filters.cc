@@ -605,22 +605,38 @@ struct SigBatch {
 };
 }  // namespace
 
+// The distinct contexts of a batch, in order of first appearance (a batch
+// almost always has one: a linear scan beats a map).
+static int ctx_index(std::vector<Context*>& ctxs, Context* c) {
+  for (size_t i = 0; i < ctxs.size(); ++i)
+    if (ctxs[i] == c) return (int)i;
+  ctxs.push_back(c);
+  return (int)ctxs.size() - 1;
+}
+
 static void launch_signatures(RemoteNode* const* nodes, Message* const* msgs, const std::vector<int>& idx,
                               bool defer, SigBatch* sb, const KeySigHint* hints = nullptr) {
   sb->sigs.assign(idx.size(), 0u);
   sb->chunks.clear();
-  std::map<Context*, std::vector<size_t>> dev;
+  std::vector<Context*> ctxs;
+  std::vector<std::vector<size_t>> dev;
   for (size_t k = 0; k < idx.size(); ++k) {
     const Buffer& key = msgs[idx[k]]->key;
     const size_t len = std::min(key.bytes, (size_t)2048);
-    if (hints && hints[idx[k]].matches(key)) sb->sigs[k] = hints[idx[k]].crc;
-    else if (key.loc == Loc::kHost || nodes[idx[k]]->ctx()->device() < 0) sb->sigs[k] = crc32c_host(key.ptr, len);
-    else dev[nodes[idx[k]]->ctx()].push_back(k);
+    if (hints && hints[idx[k]].matches(key)) {
+      sb->sigs[k] = hints[idx[k]].crc;
+    } else if (key.loc == Loc::kHost || nodes[idx[k]]->ctx()->device() < 0) {
+      sb->sigs[k] = crc32c_host(key.ptr, len);
+    } else {
+      const int c = ctx_index(ctxs, nodes[idx[k]]->ctx());
+      if ((size_t)c >= dev.size()) dev.emplace_back();
+      dev[c].push_back(k);
+    }
   }
   constexpr size_t kDeferCap = (size_t)(Context::kPresignSlot0 - Context::kDeferSlot0);
-  for (auto& kv : dev) {
-    Context* ctx = kv.first;
-    const std::vector<size_t>& ks = kv.second;
+  for (size_t ci = 0; ci < dev.size(); ++ci) {
+    Context* ctx = ctxs[ci];
+    const std::vector<size_t>& ks = dev[ci];
     const bool keep = defer && ks.size() <= kDeferCap;  // all of this context's batches in flight at once
     for (size_t b = 0; b < ks.size(); b += (size_t)kCrcBatchMax) {
       const size_t e = std::min(ks.size(), b + (size_t)kCrcBatchMax);
@@ -648,41 +664,62 @@ static void launch_signatures(RemoteNode* const* nodes, Message* const* msgs, co
 
 PresignJob presign_launch(RemoteNode* const* nodes, const Message* const* msgs, int n, bool ahead) {
   PresignJob J;
-  std::map<std::pair<const uint8_t*, size_t>, size_t> seen;  // key buffer -> buffer index
+  J.bufs.reserve(n);
+  J.next.assign(n, -1);
+  // key buffer -> J.bufs index: open addressing over (ptr, bytes, context)
+  size_t cap = 16;
+  while (cap < 2 * (size_t)n) cap <<= 1;
+  std::vector<int> tab(cap, -1);
   for (int i = 0; i < n; ++i) {
     const Message& m = *msgs[i];
     if (!m.has_key() || m.key.loc != Loc::kDevice || !Filter::find(FilterConfig::KEY_CACHING, const_cast<Message*>(&m)))
       continue;
     Context* ctx = nodes[i]->ctx();
     if (ctx->device() < 0) continue;
-    const auto id = std::make_pair((const uint8_t*)m.key.ptr, m.key.bytes);
-    auto it = seen.find(id);
-    if (it != seen.end() && J.bufs[it->second].ctx == ctx) {
-      J.bufs[it->second].users.push_back(i);
-      continue;
+    const uint64_t h0 = (uint64_t)reinterpret_cast<uintptr_t>(m.key.ptr) * 0x9E3779B97F4A7C15ull ^ m.key.bytes;
+    for (size_t h = (size_t)(h0 >> 17) & (cap - 1);; h = (h + 1) & (cap - 1)) {
+      const int q = tab[h];
+      if (q < 0) {
+        tab[h] = (int)J.bufs.size();
+        J.bufs.push_back(PresignJob::Buf{ctx, m.key.ptr, m.key.bytes, i, i, {0, 0}, -1});
+        break;
+      }
+      PresignJob::Buf& b = J.bufs[q];
+      if (b.ptr == m.key.ptr && b.bytes == m.key.bytes && b.ctx == ctx) {
+        J.next[b.last] = i;
+        b.last = i;
+        break;
+      }
     }
-    seen[id] = J.bufs.size();
-    J.bufs.push_back(PresignJob::Buf{ctx, m.key.ptr, m.key.bytes, {i}, {0, 0}, -1});
   }
   // ahead (the next iteration's, waited for later): the presign slot range,
   // when all of it fits; else the synchronous slots, waited for chunk by chunk
-  std::map<Context*, size_t> per;
-  for (const auto& b : J.bufs) ++per[b.ctx];
+  std::vector<Context*> ctxs;
+  std::vector<size_t> per;
+  for (const auto& b : J.bufs) {
+    const int c = ctx_index(ctxs, b.ctx);
+    if ((size_t)c >= per.size()) per.push_back(0);
+    ++per[c];
+  }
   size_t most = 0;
-  for (const auto& kv : per) most = std::max(most, kv.second);
+  for (size_t k : per) most = std::max(most, k);
   J.ahead = ahead && 2 * most <= (size_t)(Context::kSlots - Context::kPresignSlot0);
   if (!J.ahead) return J;  // launched and waited for in presign_finish
-  std::map<Context*, int> next_slot;
-  std::map<Context*, std::vector<size_t>> order;
-  for (size_t q = 0; q < J.bufs.size(); ++q) order[J.bufs[q].ctx].push_back(q);
-  for (auto& kv : order) {
-    Context* ctx = kv.first;
-    std::vector<const void*> d;
-    std::vector<uint32_t> len, tk;
-    std::vector<int> slot;
+  std::vector<const void*> d;
+  std::vector<uint32_t> len, tk;
+  std::vector<int> slot;
+  d.reserve(2 * J.bufs.size());
+  len.reserve(2 * J.bufs.size());
+  tk.reserve(2 * J.bufs.size());
+  slot.reserve(2 * J.bufs.size());
+  for (Context* ctx : ctxs) {
+    d.clear();
+    len.clear();
+    tk.clear();
+    slot.clear();
     int s = Context::kPresignSlot0;
-    for (size_t q : kv.second) {
-      PresignJob::Buf& b = J.bufs[q];
+    for (PresignJob::Buf& b : J.bufs) {
+      if (b.ctx != ctx) continue;
       b.slot0 = s;
       for (int r = 0; r < 2; ++r) {
         b.tk[r] = ctx->next_ticket();
@@ -705,7 +742,7 @@ PresignJob presign_launch(RemoteNode* const* nodes, const Message* const* msgs, 
 
 void presign_finish(PresignJob& J, KeySigHint* enc, KeySigHint* dec) {
   auto fill = [&](const PresignJob::Buf& b, uint32_t se, uint32_t sd) {
-    for (int i : b.users) {
+    for (int i = b.first; i >= 0; i = J.next[i]) {
       enc[i] = KeySigHint{b.ptr, b.bytes, se};
       if (dec) dec[i] = KeySigHint{b.ptr, b.bytes, sd};
     }
@@ -792,30 +829,36 @@ void encode_batch(RemoteNode* const* nodes, Message* const* msgs, int n, const K
       if (pos < msgs[i]->task.filter.size() && msgs[i]->task.filter[pos].type != FilterConfig::FIXING_FLOAT)
         only_ff = false;
     if (!only_ff) finish_kc();
-    std::map<Context*, std::vector<FfMessage>> ff;
-    std::map<Context*, std::vector<Message*>> cz;
+    // per context (in order of first appearance; a batch almost always has one)
+    std::vector<Context*> ffc, czc;
+    std::vector<std::vector<FfMessage>> ff;
+    std::vector<std::vector<Message*>> cz;
     std::vector<int> kc, kc_sig;
     for (int i = 0; i < n; ++i) {
       if (pos >= msgs[i]->task.filter.size()) continue;
       const FilterConfig& conf = msgs[i]->task.filter[pos];
       Filter* f = nodes[i]->FindFilterOrCreate(conf);
       if (conf.type == FilterConfig::FIXING_FLOAT) {
-        ff[nodes[i]->ctx()].push_back(FfMessage{msgs[i], false});
+        const int c = ctx_index(ffc, nodes[i]->ctx());
+        if ((size_t)c >= ff.size()) ff.emplace_back().reserve(n);
+        ff[c].push_back(FfMessage{msgs[i], false});
       } else if (conf.type == FilterConfig::KEY_CACHING) {
         kc.push_back(i);
         if (KeyCachingFilter::needs_signature(msgs[i], true)) kc_sig.push_back(i);
       } else if (conf.type == FilterConfig::COMPRESSING) {
-        cz[nodes[i]->ctx()].push_back(msgs[i]);
+        const int c = ctx_index(czc, nodes[i]->ctx());
+        if ((size_t)c >= cz.size()) cz.emplace_back();
+        cz[c].push_back(msgs[i]);
       } else {
         f->encode(msgs[i]);
       }
     }
-    for (auto& kv : cz) {
+    for (size_t c = 0; c < cz.size(); ++c) {
       if (later && pos + 1 == maxlen) {  // the last position: left in flight for the caller
         later->snappy.emplace_back();
-        CompressingFilter::encode_messages(kv.first, kv.second, &later->snappy.back());
+        CompressingFilter::encode_messages(czc[c], cz[c], &later->snappy.back());
       } else {
-        CompressingFilter::encode_messages(kv.first, kv.second);
+        CompressingFilter::encode_messages(czc[c], cz[c]);
       }
     }
     if (!kc.empty()) {  // signatures launched now, the caches after the next position's launches
@@ -830,7 +873,7 @@ void encode_batch(RemoteNode* const* nodes, Message* const* msgs, int n, const K
     }
     {
       PSF_HPROF(3);
-      for (auto& kv : ff) FixingFloatFilter::encode_messages(kv.first, kv.second, /*lazy=*/true);
+      for (size_t c = 0; c < ff.size(); ++c) FixingFloatFilter::encode_messages(ffc[c], ff[c], /*lazy=*/true);
     }
   }
   finish_kc();
@@ -843,9 +886,10 @@ void decode_batch(RemoteNode* const* nodes, Message* const* msgs, int n, const K
     msgs[i]->predecoded.clear();
   }
   for (size_t r = 0; r < maxlen; ++r) {  // r-th filter from the end of every chain
-    std::map<Context*, std::vector<FfMessage>> ff;
-    std::map<Context*, std::vector<Message*>> cz;
-    std::map<Context*, std::vector<RemoteNode*>> cz_nodes;
+    std::vector<Context*> ffc, czc;
+    std::vector<std::vector<FfMessage>> ff;
+    std::vector<std::vector<Message*>> cz;
+    std::vector<std::vector<RemoteNode*>> cz_nodes;
     std::vector<int> kc, kc_sig;
     for (int i = 0; i < n; ++i) {
       const size_t len = msgs[i]->task.filter.size();
@@ -853,18 +897,25 @@ void decode_batch(RemoteNode* const* nodes, Message* const* msgs, int n, const K
       const FilterConfig& conf = msgs[i]->task.filter[len - 1 - r];
       Filter* f = nodes[i]->FindFilterOrCreate(conf);
       if (conf.type == FilterConfig::FIXING_FLOAT) {
-        ff[nodes[i]->ctx()].push_back(FfMessage{msgs[i], f->defer_dequant()});
+        const int c = ctx_index(ffc, nodes[i]->ctx());
+        if ((size_t)c >= ff.size()) ff.emplace_back().reserve(n);
+        ff[c].push_back(FfMessage{msgs[i], f->defer_dequant()});
       } else if (conf.type == FilterConfig::KEY_CACHING) {
         kc.push_back(i);
         if (KeyCachingFilter::needs_signature(msgs[i], false)) kc_sig.push_back(i);
       } else if (conf.type == FilterConfig::COMPRESSING) {
-        cz[nodes[i]->ctx()].push_back(msgs[i]);
-        cz_nodes[nodes[i]->ctx()].push_back(nodes[i]);
+        const int c = ctx_index(czc, nodes[i]->ctx());
+        if ((size_t)c >= cz.size()) {
+          cz.emplace_back();
+          cz_nodes.emplace_back();
+        }
+        cz[c].push_back(msgs[i]);
+        cz_nodes[c].push_back(nodes[i]);
       } else {
         f->decode(msgs[i]);
       }
     }
-    for (auto& kv : cz) CompressingFilter::decode_messages(kv.first, kv.second, &cz_nodes[kv.first]);
+    for (size_t c = 0; c < cz.size(); ++c) CompressingFilter::decode_messages(czc[c], cz[c], &cz_nodes[c]);
     if (!kc.empty()) {
       PSF_HPROF(8);
       SigBatch sb;
@@ -879,7 +930,7 @@ void decode_batch(RemoteNode* const* nodes, Message* const* msgs, int n, const K
     }
     {
       PSF_HPROF(7);
-      for (auto& kv : ff) FixingFloatFilter::decode_messages(kv.first, kv.second);
+      for (size_t c = 0; c < ff.size(); ++c) FixingFloatFilter::decode_messages(ffc[c], ff[c]);
     }
   }
 }

@@ -12,7 +12,8 @@ os.environ.setdefault("PSF_LIBRARY_VARIANT", os.path.join(ROOT, "tools", "varian
 sys.path.insert(0, ROOT)
 NAMES = {0: "copy tmpl->msg", 1: "encode_batch", 2: "enc sig launch", 3: "enc FF", 4: "enc KC finish",
          5: "copy delivered", 6: "decode_batch", 7: "dec FF", 8: "dec KC", 9: "ff_encode_batch_launch",
-         10: "ff_decode_batch_launch", 11: "crc32c_batch_launch", 12: "presign"}
+         10: "ff_decode_batch_launch", 11: "crc32c_batch_launch", 12: "presign", 13: "presign_launch (next)",
+         14: "iteration (all)"}
 
 
 def main():
