@@ -1638,33 +1638,60 @@ __global__ __launch_bounds__(256) void snappy_dspec(const SnappyDJobs J) {
 }
 
 
-// K2: link the windows along the true chain (one lane).  Every step costs
-// one memory latency: windows are entered in increasing order, so the
-// first-entry bookkeeping stays in registers, and the bitmap word and the
-// next tag's bytes (two aligned dwords) are loaded together.
+// K2: link the windows along the true chain.  The walk is one chain (every
+// lane holds the same values); K1's tables of the next kLinkAhead windows
+// (exit and output count per start offset) are copied into LDS together, so a
+// window entered at one of its first 64 bytes costs one LDS read and one
+// memory latency per kLinkAhead windows.  Other entries step tag by tag until
+// they meet lane 0's chain (bitmap word and the next tag's bytes loaded
+// together).  Windows are entered in increasing order, so the first-entry
+// bookkeeping stays in registers.
+constexpr uint32_t kLinkAhead = 16;
 __device__ void dlink_body(const uint8_t* __restrict__ in, uint64_t C, uint32_t hdr, uint64_t dsize,
                            const uint32_t* __restrict__ bitmap, const uint32_t* __restrict__ cum,
                            const uint64_t* __restrict__ wexit, const uint64_t* __restrict__ wtotal, uint32_t nwin,
-                           uint64_t* __restrict__ wentry, uint64_t* __restrict__ woff, uint32_t* __restrict__ flags) {
-  for (uint32_t i = threadIdx.x; i < nwin; i += 64) wentry[i] = kNone;
+                           uint64_t* __restrict__ wentry, uint64_t* __restrict__ woff, uint32_t* __restrict__ flags,
+                           uint64_t* lex, uint64_t* ltot) {
+  const uint32_t lane = threadIdx.x;
+  for (uint32_t i = lane; i < nwin; i += 64) wentry[i] = kNone;
   __syncthreads();
-  if (threadIdx.x != 0) return;
   uint64_t p = hdr, o = 0;
   int64_t last_w = -1;  // highest window whose entry is recorded
   bool bad = false;
   const uintptr_t ia = reinterpret_cast<uintptr_t>(in);
+  uint32_t tw = 0;  // first window of the tables in LDS
+  bool have = false;
   while (p < C) {
     const uint64_t rel = p - hdr;
     const uint32_t w = (uint32_t)(rel / kWin);
     const uint64_t off = rel - (uint64_t)w * kWin;
     if ((int64_t)w > last_w) {
-      wentry[w] = p;
-      woff[w] = o;
+      if (lane == 0) {
+        wentry[w] = p;
+        woff[w] = o;
+      }
       last_w = w;
     }
     if (off < kStarts) {  // parsed exactly by K1's lane `off`
-      o += wtotal[(size_t)w * kStarts + off];
-      p = wexit[(size_t)w * kStarts + off];
+      if (!have || w - tw >= kLinkAhead) {
+        have = true;
+        tw = w;
+        uint64_t e[kLinkAhead], t[kLinkAhead];
+#pragma unroll
+        for (uint32_t j = 0; j < kLinkAhead; ++j) {
+          const size_t r = (size_t)min(w + j, nwin - 1) * kStarts + lane;
+          e[j] = wexit[r];
+          t[j] = wtotal[r];
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < kLinkAhead; ++j) {
+          lex[j * kStarts + lane] = e[j];
+          ltot[j * kStarts + lane] = t[j];
+        }
+      }
+      const uint32_t q = (w - tw) * kStarts + (uint32_t)off;
+      o += ltot[q];
+      p = lex[q];
     } else {
       // bitmap word and the 8 bytes at p, loaded together
       const uint32_t bw = bitmap[rel >> 5];
@@ -1700,8 +1727,7 @@ __device__ void dlink_body(const uint8_t* __restrict__ in, uint64_t C, uint32_t 
       break;
     }
   }
-  if (bad || p != C || o != dsize) *flags = kFlagInvalid;
-  else *flags = 0;
+  if (lane == 0) *flags = (bad || p != C || o != dsize) ? kFlagInvalid : 0;
 }
 
 // K1: speculative parse of each window from each of its first 64 byte offsets
@@ -1901,11 +1927,13 @@ __global__ __launch_bounds__(64) void snappy_dscan(const SnappyDJobs J) {
 }
 // K2: one workgroup per stream links its windows
 __global__ __launch_bounds__(64) void snappy_dlink(const SnappyDJobs J) {
+  __shared__ uint64_t lex[kLinkAhead * kStarts], ltot[kLinkAhead * kStarts];
   for (uint32_t ji = blockIdx.x; ji < J.njobs; ji += gridDim.x) {
     const DScr S = dscr(J, J.j[ji], ji);
     if (*S.flags & kFlagScan) {
       const DJob& D = J.j[ji];
-      dlink_body(D.in, D.C, D.hdr, D.dsize, S.bitmap, S.cum, S.wexit, S.wtotal, D.nwin, S.wentry, S.woff, S.flags);
+      dlink_body(D.in, D.C, D.hdr, D.dsize, S.bitmap, S.cum, S.wexit, S.wtotal, D.nwin, S.wentry, S.woff, S.flags,
+                 lex, ltot);
     }
   }
 }
