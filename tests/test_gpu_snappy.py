@@ -292,3 +292,51 @@ def test_compress_stream_past_inline_scan(ctx, port):
     assert got == want
     back = ctx.snappy_uncompress(_dev(want)).cpu().numpy().tobytes()
     assert back == xb
+
+
+@pytest.mark.parametrize("kind", ["random", "keys", "codes", "runs", "alpha4", "periodic", "text"])
+def test_mutated_multifragment_streams_vs_port(ctx, port, kind):
+    """Multi-fragment streams (3-128 fragments) with one or two edits past the
+    header (a byte overwritten, deleted or inserted, or the tail cut): the
+    batched scan, linker, index and fragment decoder reach RawUncompress's
+    verdict (snappy.cc's SnappyDecoder, through oracle/snappy_port.c) and, on
+    a stream that still parses, its exact output.  The fixtures in
+    snappy_dec.npz are single-fragment; these reach the per-lane tag checks of
+    every kernel of the multi-fragment path."""
+    from parameter_server_amd._lib import PSF_ERR_CHECK, PsfError
+    rng = np.random.default_rng(1000 + len(kind) * 31 + ord(kind[1]))
+    nbad = ngood = 0
+    for t in range(30):
+        n = int(rng.integers(150_000, 1_600_000)) if t % 10 != 9 else 8 << 20
+        x = _inputs(rng, n, kind)
+        s = bytearray(port.snappy_compress(x))
+        hdr = 1
+        while s[hdr - 1] & 0x80:
+            hdr += 1
+        for _ in range(1 + t % 2):
+            i = int(rng.integers(hdr, len(s)))
+            op = int(rng.integers(0, 4)) if t else 0
+            if op == 0:
+                s[i] = (s[i] + int(rng.integers(1, 256))) & 255
+            elif op == 1:
+                del s[i]
+            elif op == 2:
+                s.insert(i, int(rng.integers(0, 256)))
+            else:
+                del s[i:]
+        s = bytes(s)
+        st, want = port.snappy_uncompress(s, cap=1 << 24)
+        assert st != -2
+        try:
+            got = ctx.snappy_uncompress(_dev(s)).cpu().numpy().tobytes()
+            ok = True
+        except PsfError as e:
+            assert e.code == PSF_ERR_CHECK
+            ok = False
+        assert ok == (st == 0), (kind, t, st)
+        if ok:
+            assert got == want, (kind, t)
+            ngood += 1
+        else:
+            nbad += 1
+    assert nbad > 0
