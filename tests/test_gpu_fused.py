@@ -141,3 +141,77 @@ def test_fused_decode_device_range_from_encode(ctx, port):
                 (np.arange(x.size, dtype=np.int64) * 3).tobytes(), i
     finally:
         F.set_clock(None)
+
+
+def _tag_positions(s, p):
+    out = []
+    while p < len(s):
+        out.append(p)
+        c = s[p]
+        if c & 3 == 0:
+            ln, h = (c >> 2) + 1, 1
+            if ln > 60:
+                ln = int.from_bytes(s[p + 1:p + 1 + ln - 60], "little") + 1
+                h += (c >> 2) - 59
+            p += h + ln
+        else:
+            p += (2, 3, 5)[(c & 3) - 1]
+    return out
+
+
+@pytest.mark.parametrize("kind", ["random", "match", "dense", "mixed"])
+def test_fused_decode_mutated_streams(ctx, port, kind):
+    """A compressed code stream with a byte overwritten (a literal's or a
+    tag's), deleted or inserted, or its tail cut: the fused decode (batched)
+    and the unfused one (single message) both reject what RawUncompress
+    rejects (snappy.cc's SnappyDecoder via oracle/snappy_port.c) and
+    otherwise agree byte for byte
+    — with the restatement's dequantised codes when the stream still holds
+    the array's length."""
+    from parameter_server_amd import PsfError
+    from parameter_server_amd import filter as F
+    rng = np.random.default_rng(500 + len(kind))
+    nval, mm = 9 * 65536 + 321, (-2.0, 3.0)
+    codes = _codes(kind, nval, 1, 7 + len(kind))
+    s0 = port.snappy_compress(codes.tobytes())
+    hdr = 1
+    while s0[hdr - 1] & 0x80:
+        hdr += 1
+    tags = _tag_positions(s0, hdr)
+    nbad = 0
+    for t in range(15):
+        s = bytearray(s0)
+        i, op = int(rng.integers(hdr, len(s))), t % 5
+        if op == 4:  # a tag byte (length, kind or offset change)
+            i, op = int(tags[int(rng.integers(0, len(tags)))]), 0
+        if op == 0:
+            s[i] = (s[i] + int(rng.integers(1, 256))) & 255
+        elif op == 1:
+            del s[i]
+        elif op == 2:
+            s.insert(i, int(rng.integers(0, 256)))
+        else:
+            del s[i:]
+        s = bytes(s)
+        st, out = port.snappy_uncompress(s, cap=1 << 24)
+        res = []
+        for fused in (True, False):
+            m = _message(F, s, nval, 1, DT_FLOAT, mm, codes.size)
+            nd = F.RemoteNode(ctx)
+            try:
+                if fused:
+                    F.RemoteNode.decode_many([nd], [m])
+                else:
+                    nd.decode(m)
+                res.append(nd.value(m, 0).cpu().numpy().tobytes())
+            except PsfError:
+                res.append(None)
+        if st != 0:
+            assert res == [None, None], (kind, t, op)
+            nbad += 1
+            continue
+        assert res[0] == res[1], (kind, t, op)
+        if len(out) == codes.size:
+            st2, dec = port.ff_decode(np.frombuffer(out, np.uint8), 1, mm[0], mm[1], np.float32)
+            assert st2 == 0 and res[0] == dec.tobytes(), (kind, t, op)
+    assert nbad > 0
