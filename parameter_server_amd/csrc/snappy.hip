@@ -1086,15 +1086,19 @@ __device__ __forceinline__ bool header_matches(const uint8_t* __restrict__ in, u
 }
 
 // d[0, len) = s[0, len) for any alignment of either, by 256 lanes: byte
-// stores up to the first 16-aligned destination chunk, then chunks composed
-// from the 5 aligned source dwords that cover them (funnel shifts), 4 chunks
-// per lane per step with all loads issued before the stores (a wave's memory
-// counter retires in order: a load behind a store waits for it).  The loads
-// are unconditional (clamped), the stores predicated, so the compiler keeps
-// exact wait counts.
+// stores up to the first 4-aligned destination dword, then lane-contiguous
+// dwords (each load and store instruction covers 256 contiguous bytes), each
+// funnel-shifted from the two aligned source dwords that cover it, 16 per lane
+// per step with all loads issued before the stores (a wave's memory counter
+// retires in order: a load behind a store waits for it).  The loads are
+// unconditional (clamped), the stores predicated, so the compiler keeps exact
+// wait counts.  (Round 3: 16-byte chunks from five dword loads each ran the
+// 128 MiB stored stream at 3.7 TB/s, tools/ab_dq.sh.)  U = dwords in flight
+// per lane: 16 in K-spec, fewer in K4, whose occupancy its decoder sets.
+template <int U = 16>
 __device__ __forceinline__ void copy_g2g(uint8_t* __restrict__ d, const uint8_t* __restrict__ s, uint32_t len,
                                          uint32_t tid) {
-  uint32_t head = (uint32_t)(-reinterpret_cast<uintptr_t>(d) & 15);
+  uint32_t head = (uint32_t)(-reinterpret_cast<uintptr_t>(d) & 3);
   if (head > len) head = len;
   if (tid < head) d[tid] = s[tid];
   d += head;
@@ -1102,33 +1106,24 @@ __device__ __forceinline__ void copy_g2g(uint8_t* __restrict__ d, const uint8_t*
   len -= head;
   const uintptr_t sa = reinterpret_cast<uintptr_t>(s);
   const uint32_t sh = (uint32_t)(sa & 3) * 8;
-  const uint32_t* a = reinterpret_cast<const uint32_t*>(sa & ~(uintptr_t)3);
-  const uint32_t nv = len >> 4;
-  constexpr int U = 4;
-  for (uint32_t i0 = 0; i0 < nv; i0 += U * 256) {
-    uint32_t w[U][5];
+  const auto a = gbl<uint32_t>(reinterpret_cast<const void*>(sa & ~(uintptr_t)3));  // global, not flat, loads
+  auto* o = reinterpret_cast<__attribute__((address_space(1))) uint32_t*>(reinterpret_cast<uintptr_t>(d));
+  const uint32_t ng = len >> 2;
+  for (uint32_t g0 = 0; g0 < ng; g0 += U * 256) {
+    uint32_t w0[U], w1[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const uint32_t i = min(i0 + u * 256 + tid, nv - 1);
-      const uint32_t* q = a + 4 * i;
-      w[u][0] = q[0];
-      w[u][1] = q[1];
-      w[u][2] = q[2];
-      w[u][3] = q[3];
-      w[u][4] = q[sh ? 4 : 3];  // the fifth dword lies inside the source only when it is needed
+      const uint32_t g = min(g0 + u * 256 + tid, ng - 1);
+      w0[u] = a[g];
+      w1[u] = a[sh ? g + 1 : g];  // the next dword lies inside the source only when it is needed
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const uint32_t i = i0 + u * 256 + tid;
-      uint4 v;
-      v.x = sh ? __builtin_amdgcn_alignbit(w[u][1], w[u][0], sh) : w[u][0];
-      v.y = sh ? __builtin_amdgcn_alignbit(w[u][2], w[u][1], sh) : w[u][1];
-      v.z = sh ? __builtin_amdgcn_alignbit(w[u][3], w[u][2], sh) : w[u][2];
-      v.w = sh ? __builtin_amdgcn_alignbit(w[u][4], w[u][3], sh) : w[u][3];
-      if (i < nv) reinterpret_cast<uint4*>(d)[i] = v;
+      const uint32_t g = g0 + u * 256 + tid;
+      if (g < ng) o[g] = sh ? __builtin_amdgcn_alignbit(w1[u], w0[u], sh) : w0[u];
     }
   }
-  for (uint32_t i = (nv << 4) + tid; i < len; i += 256) d[i] = s[i];
+  for (uint32_t i = (ng << 2) + tid; i < len; i += 256) d[i] = s[i];
 }
 
 // Last-workgroup election by one device-scope counter.  No fence: what the
@@ -1269,17 +1264,13 @@ __device__ __forceinline__ void dq_store(V* o, uint32_t w, const V* lut, const D
 // dwords of codes l, l + 256, ..., each funnel-shifted from the two aligned
 // dwords that cover it (the second lies inside the source whenever it is
 // needed), 8 in flight before any store.
-template <typename V, int NB>
+template <typename V, int NB, int U>
 __device__ void dq_bytes(const uint8_t* __restrict__ s, V* __restrict__ v, uint32_t len, const V* lut,
                          const DqParams& P, uint32_t tid) {
   const uintptr_t sa = reinterpret_cast<uintptr_t>(s);
   const uint32_t sh = (uint32_t)(sa & 3) * 8;
-  const uint32_t* a = reinterpret_cast<const uint32_t*>(sa & ~(uintptr_t)3);
+  const auto a = gbl<uint32_t>(reinterpret_cast<const void*>(sa & ~(uintptr_t)3));  // global, not flat, loads
   const uint32_t ng = len >> 2;
-#ifndef PSF_DQ_U
-#define PSF_DQ_U 8  // groups in flight per lane (4 / 8 / 16 measured equal within 1 %, tools/ab_dq.sh)
-#endif
-  constexpr int U = PSF_DQ_U;
   for (uint32_t g0 = 0; g0 < ng; g0 += U * 256) {
     uint32_t w0[U], w1[U];
 #pragma unroll
@@ -1314,20 +1305,24 @@ __device__ __forceinline__ void dq_prepare(const DJob& D, double* lut64, uint32_
 }
 
 // Output fragment bytes [o0, o0 + len) of stream D, whose codes are at s, to
-// their values (after dq_prepare).
+// their values (after dq_prepare).  U = code dwords in flight per lane: K-spec
+// (global loads, C5 + COMPRESSING) measured 4 / 8 / 12 / 16 / 32 at
+// 119 / 113 / 112 / 110 / 110 us (tools/ab_dq.sh); K4 keeps 8 (its decoder's
+// registers set its occupancy).
+template <int U = 16>
 __device__ __forceinline__ void dq_frag(const DJob& D, const uint8_t* s, uint64_t o0, uint32_t len,
                                         const double* lut64, uint32_t tid) {
   const DqParams P = dq_params(D);
   const uint64_t first = o0 / D.fnb;  // 65536 is a multiple of nb
   if (D.fdbl) {
     double* v = static_cast<double*>(D.fv) + first;
-    if (D.fnb == 1) dq_bytes<double, 1>(s, v, len, lut64, P, tid);
-    else dq_bytes<double, 2>(s, v, len, lut64, P, tid);
+    if (D.fnb == 1) dq_bytes<double, 1, U>(s, v, len, lut64, P, tid);
+    else dq_bytes<double, 2, U>(s, v, len, lut64, P, tid);
   } else {
     float* v = static_cast<float*>(D.fv) + first;
     const float* lut = reinterpret_cast<const float*>(lut64);
-    if (D.fnb == 1) dq_bytes<float, 1>(s, v, len, lut, P, tid);
-    else dq_bytes<float, 2>(s, v, len, lut, P, tid);
+    if (D.fnb == 1) dq_bytes<float, 1, U>(s, v, len, lut, P, tid);
+    else dq_bytes<float, 2, U>(s, v, len, lut, P, tid);
   }
 }
 
@@ -2032,7 +2027,7 @@ __global__ __launch_bounds__(256) void snappy_dfrag(const SnappyDJobs J) {
   if (flags[2]) {  // K-spec decoded the whole stream and gave the verdict
     if (D.fv && end && !S.fdone[k]) {  // a fragment it placed as codes: their values
       dq_prepare(D, s_lut, tid);
-      dq_frag(D, out + o0, o0, end, s_lut, tid);
+      dq_frag<8>(D, out + o0, o0, end, s_lut, tid);
     }
     return;
   }
@@ -2050,7 +2045,7 @@ __global__ __launch_bounds__(256) void snappy_dfrag(const SnappyDJobs J) {
     if (decode_few(in, C, p0, end, out + o0, tid, F) != kNone) {
       // (a fragment of a few tags: done)
     } else if (t0.lit && t0.len == end) {
-      copy_g2g(out + o0, in + p0 + t0.hl, end, tid);
+      copy_g2g<4>(out + o0, in + p0 + t0.hl, end, tid);
     } else {
       if (tid < 64) {
         const uint32_t lane = tid;
@@ -2143,7 +2138,7 @@ __global__ __launch_bounds__(256) void snappy_dfrag(const SnappyDJobs J) {
   if (D.fv && f == 0 && end && (redo || !S.fdone[k])) {  // values of the codes placed here or by K-spec
     __syncthreads();
     dq_prepare(D, s_lut, tid);
-    dq_frag(D, out + o0, o0, end, s_lut, tid);
+    dq_frag<8>(D, out + o0, o0, end, s_lut, tid);
   }
   PSF_DTRACE(k, 2);
   if (!last_block(S.ctr + 2, D.nfo ? D.nfo : 1, &s_last)) return;
@@ -2152,7 +2147,7 @@ __global__ __launch_bounds__(256) void snappy_dfrag(const SnappyDJobs J) {
     if (D.fv) {
       __syncthreads();
       dq_prepare(D, s_lut, tid);
-      for (uint64_t o = 0; o < dsize; o += kFrag) dq_frag(D, out + o, o, (uint32_t)min((uint64_t)kFrag, dsize - o), s_lut, tid);
+      for (uint64_t o = 0; o < dsize; o += kFrag) dq_frag<8>(D, out + o, o, (uint32_t)min((uint64_t)kFrag, dsize - o), s_lut, tid);
     }
     __syncthreads();
   }
