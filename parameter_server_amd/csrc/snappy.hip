@@ -391,7 +391,8 @@ __device__ void copy_bytes(uint8_t* __restrict__ dst, const uint8_t* __restrict_
   if (tid < head) dst[tid] = s[tid];
   const uint32_t nc = (len - head) >> 4;
   const uintptr_t sp = reinterpret_cast<uintptr_t>(s + head);
-  const uint4* s16 = reinterpret_cast<const uint4*>(sp & ~(uintptr_t)15);
+  typedef uint32_t V4 __attribute__((ext_vector_type(4)));
+  const auto s16 = gbl<V4>(reinterpret_cast<const void*>(sp & ~(uintptr_t)15));  // global, not flat, loads
   const uint32_t sh = (uint32_t)(sp & 15);
   const uint32_t lim = nc + (sh ? 1u : 0u);  // blocks that hold source bytes
   uint4* d16 = reinterpret_cast<uint4*>(dst + head);
@@ -400,7 +401,9 @@ __device__ void copy_bytes(uint8_t* __restrict__ dst, const uint8_t* __restrict_
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t c = c0 + (u * W + wv) * 63 + lane;
-      lo[u] = c < lim ? s16[c] : make_uint4(0, 0, 0, 0);
+      V4 x = {0, 0, 0, 0};
+      if (c < lim) x = s16[c];
+      lo[u] = make_uint4(x[0], x[1], x[2], x[3]);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -1958,7 +1961,8 @@ __device__ void literal_to_lds(uint8_t* ob, uint32_t o, const uint8_t* __restric
   if (lane < head) ob[o + lane] = in[src + lane];
   const uint32_t nc = (L - head) >> 4;
   const uintptr_t sp = reinterpret_cast<uintptr_t>(in + src + head);
-  const uint4* s16 = reinterpret_cast<const uint4*>(sp & ~(uintptr_t)15);
+  typedef uint32_t V4 __attribute__((ext_vector_type(4)));
+  const auto s16 = gbl<V4>(reinterpret_cast<const void*>(sp & ~(uintptr_t)15));  // global, not flat, loads
   const uint32_t sh = (uint32_t)(sp & 15);
   uint4* d16 = reinterpret_cast<uint4*>(ob + o + head);
   constexpr int U = 8;
@@ -1967,8 +1971,12 @@ __device__ void literal_to_lds(uint8_t* ob, uint32_t o, const uint8_t* __restric
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t c = c0 + u * 64 + lane;
-      lo[u] = c < nc ? s16[c] : make_uint4(0, 0, 0, 0);
-      hi[u] = (c < nc && sh) ? s16[c + 1] : lo[u];
+      V4 x = {0, 0, 0, 0};
+      if (c < nc) x = s16[c];
+      V4 y = x;
+      if (c < nc && sh) y = s16[c + 1];
+      lo[u] = make_uint4(x[0], x[1], x[2], x[3]);
+      hi[u] = make_uint4(y[0], y[1], y[2], y[3]);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
