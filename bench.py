@@ -99,6 +99,9 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--no-128m", action="store_true", help="c2: skip the configs[1] 2^27 measurement")
+    ap.add_argument("--no-c4", action="store_true",
+                    help="c2: skip the companion C4 measurement (cross-range spill) reported as config_c4")
+    ap.add_argument("--c4-m", type=int, default=1 << 21, help="c2's companion C4 line: keys per stream")
     ap.add_argument("--streams", type=int, default=64, help="c1/c4: push streams in total")
     ap.add_argument("--servers", type=int, default=8, help="c4/c5: server key ranges (>= N)")
     ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c3miss", "c4", "c5"])
@@ -194,9 +197,10 @@ def cpu_baseline(args, nb: int):
         return f
 
     if cfg == "c2":
-        x = rng.standard_normal(1 << 24).astype(np.float32)
+        # the line's own size: one message of args.n f32 values (2^28 = 1 GiB)
+        x = rng.standard_normal(args.n, dtype=np.float32)
         tasks, payload = [ff_rt(x)], x.nbytes
-        what = f"FIXING_FLOAT(nb={nb}) encode+decode of 2^24 f32 (64 MiB)"
+        what = f"FIXING_FLOAT(nb={nb}) encode+decode of {args.n} f32 ({x.nbytes >> 20} MiB, the line's size)"
     elif cfg in ("c3", "c3miss"):
         m = 1 << 22
         keys = np.unique(np.random.default_rng(3).integers(0, 10**9, m + m // 8, dtype=np.uint64))[:m]
@@ -270,6 +274,26 @@ def pmc_traffic(kernel: str, n: int, nb: int, config: str):
 
 
 # ------------------------------------------------------------- workloads --
+def c4_args(args):
+    """the C4 companion measurement of a c2 run: 64 streams, EvenDivide(8)
+    (the default --streams / --servers), repeat sends"""
+    a4 = argparse.Namespace(**vars(args))
+    a4.config, a4.m, a4.compress, a4.miss = "c4", args.c4_m, False, False
+    return a4
+
+
+def c4_config(args, world_pg: int, backend_pg: str) -> dict:
+    a4 = c4_args(args)
+    return {"workload": WORKLOADS["c4"].format(nb=args.nb, streams=a4.streams, servers=a4.servers, m=a4.m,
+                                               sends="repeat sends (key cache hit)", cmp=""),
+            "scaling": "strong" if world_pg > 1 else "weak",
+            "world_size": world_pg, "backend": backend_pg,
+            "parallelism": f"{a4.servers} servers in blocks over {world_pg} rank(s); "
+                           + ("cross-range slices in one all-to-all-v per step" if world_pg > 1
+                              else "every slice local (no exchange at world 1)"),
+            "measured": False}
+
+
 def build_workload(args, F, ctx, rank, world, dev, g, n):
     """Returns (run(k), payload bytes per step on this rank, n values, extra)."""
     import torch
@@ -428,8 +452,11 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dist.barrier()
         if rank == 0:
-            print(json.dumps({"launch_check": True, "n_gpus": world_pg, "world_size": world_pg,
-                              "backend": backend_pg, "config": {"workload": args.config}}), flush=True)
+            line = {"launch_check": True, "n_gpus": world_pg, "world_size": world_pg,
+                    "backend": backend_pg, "config": {"workload": args.config}}
+            if args.config == "c2" and not args.no_c4:  # the companion line a real run adds (not measured here)
+                line["config_c4"] = c4_config(args, world_pg, backend_pg)
+            print(json.dumps(line), flush=True)
         if world > 1:
             dist.destroy_process_group()
         return
@@ -538,6 +565,38 @@ def main():
         el2 = max_over_ranks(el2)
         also = {"n_values_per_gpu": 1 << 27, "value": round(world * args.steps * payload2 / el2 / GIB, 2),
                 "ms_per_step": round(el2 / args.steps * 1e3, 4)}
+        del run2
+
+    # the C4 push path (BASELINE configs[3]) in the same process: at N > 1 its
+    # cross-range slices travel by RCCL all-to-all-v, so a multi-GPU run of
+    # the default command measures the spill too (executor.cc:134-146 over
+    # assigner.h:17-28's partition); at N = 1 every slice is local
+    c4 = None
+    if args.config == "c2" and not args.no_c4:
+        if "run" in locals():
+            del run
+        a4 = c4_args(args)
+        run4, payload4, _, extra4 = build_workload(a4, F, ctx, rank, world, dev, g, 0)
+        run4(args.warmup)
+        torch.cuda.synchronize()
+        r4 = extra4["router"]
+        if r4.exchange is not None:
+            r4.exchange.bytes_sent = 0
+        el4, _ = timed(run4, args.steps, world, dist, ctx)
+        spill4 = r4.exchange.bytes_sent if r4.exchange is not None else 0
+        el4 = max_over_ranks(el4)
+        tot4 = float(payload4)
+        if world > 1:
+            t = torch.tensor([tot4], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
+            dist.all_reduce(t)
+            tot4 = float(t.item())
+        c4 = c4_config(args, world_pg, backend_pg)
+        c4.update({"measured": True, "value": round(args.steps * tot4 / el4 / GIB, 2),
+                   "ms_per_step": round(el4 / args.steps * 1e3, 4),
+                   "payload_bytes_per_step_per_gpu_rank0": payload4,
+                   "key_bytes_elided_per_step_rank0": extra4["key_bytes_elided"],
+                   "spill_bytes_per_step_rank0": spill4 // max(args.steps, 1)})
+        del run4, r4, extra4
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -594,6 +653,8 @@ def main():
             line["config"]["spill_bytes_per_step_rank0"] = spill // max(args.steps, 1)
         if also:
             line["config_128M"] = also
+        if c4:
+            line["config_c4"] = c4
         print(json.dumps(line), flush=True)
 
     if world > 1:

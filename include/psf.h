@@ -51,7 +51,7 @@ extern "C" {
 #define PSF_ERR_HIP (-4)         /* HIP runtime failure                           */
 #define PSF_ERR_CHECK (-5)       /* other reference CHECK (signature mismatch ...) */
 #define PSF_ERR_UNSUPPORTED (-6)
-#define PSF_ERR_TIMEOUT (-7)     /* a device-side wait hit its cap; the launch gave up */
+#define PSF_ERR_TIMEOUT (-7)     /* reserved: no entry point returns it (libpsf has no device-side waits) */
 
 /* ---- task.proto DataType / filter.proto Type values -------------------- */
 #define PSF_DT_UINT64 8
@@ -90,8 +90,18 @@ int psf_default_device(void);
  * filter calls under Executor::node_mu_ (executor.cc:110,143,170). */
 typedef struct psf_context psf_context;
 /* own_stream=1: a private non-blocking stream; own_stream=0: kernels go on
- * `stream` as given (NULL = the legacy default stream).  device < 0 gives a
- * host-only context (host-resident buffers; codecs needing HBM fail). */
+ * `stream` as given (NULL = the legacy default stream); own_stream=2
+ * (PSF_STREAM_SHARED, stream NULL): one of the device's 4 process-wide
+ * streams, round robin -- what the reference-side adapter uses, so hundreds of
+ * per-peer contexts do not alias hundreds of streams onto the hardware queues
+ * (each context still keeps its own order on its stream).  device < 0 gives a
+ * host-only context (host-resident buffers; codecs needing HBM fail).  A
+ * context may be used from any thread (one at a time): every entry point
+ * makes the context's device current for the call and restores the
+ * caller's. */
+#define PSF_STREAM_GIVEN 0
+#define PSF_STREAM_OWN 1
+#define PSF_STREAM_SHARED 2
 int psf_context_create(int device, void* stream, int own_stream, psf_context** out);
 int psf_context_destroy(psf_context* ctx);
 /* Waits for the context's stream; also resolves the min/max a batched encode
@@ -423,14 +433,22 @@ int psf_router_encoded(psf_router* r, int i, int32_t* stream, int* server, psf_m
 #define PSF_WAIT_NUM 3
 int psf_context_host_stats(psf_context* ctx, int64_t* wait_ns, int64_t* waits);
 int psf_context_host_stats_reset(psf_context* ctx);
-/* The context's caching allocator: released codec buffers are kept for reuse
- * on free lists bounded per context (default 8 GiB of HBM, 1 GiB of pinned
- * host memory); a release past the cap frees the least recently released
- * blocks first.  out[8] = {HBM cached, HBM cap, HBM allocated (live +
- * cached), HBM evictions, pinned cached, pinned cap, pinned allocated,
- * pinned evictions}. */
+/* The caching allocator: released codec buffers are kept for reuse on free
+ * lists bounded per DEVICE -- one cap shared by every context on the device
+ * (default 8 GiB of HBM, 1 GiB of pinned host memory); a release past the cap
+ * frees the least recently released blocks of the whole device first, and an
+ * allocation that fails drops every cached block of the device and retries.
+ * psf_context_set_cache_limit sets the cap of the context's device (=
+ * psf_set_device_cache_limit).  psf_context_memory_stats: out[8] = {HBM
+ * cached, HBM cap, HBM allocated (live + cached), HBM evictions, pinned
+ * cached, pinned cap, pinned allocated, pinned evictions} of the context's
+ * stream (shared by the contexts on a shared stream); caps per device.
+ * psf_device_memory_stats: out[10] = the same 8 for the whole device, then
+ * the live streams with a cache share and the shared streams created. */
 int psf_context_set_cache_limit(psf_context* ctx, uint64_t hbm_bytes, uint64_t pinned_bytes);
 int psf_context_memory_stats(psf_context* ctx, uint64_t* out);
+int psf_set_device_cache_limit(int device, uint64_t hbm_bytes, uint64_t pinned_bytes);
+int psf_device_memory_stats(int device, uint64_t* out);
 /* router phase timers: out[0] steps (encodes), out[1] host ns inside encode,
  * out[2] host ns inside the decodes (both include the waits above) */
 int psf_router_host_stats(psf_router* r, int64_t* out);

@@ -23,8 +23,11 @@
 // (remote_node.cc:7-15), the calls of one instance are serialised by its
 // Customer's Executor::node_mu_ (executor.cc:110,143,170), and different
 // Customers' executor threads run their instances concurrently (SURVEY.md
-// §8(b)).  So every adapter instance owns its libpsf context -- a private HIP
-// stream, workspace and allocator -- and no lock is shared between instances.
+// §8(b)).  So every adapter instance owns its libpsf context -- its own
+// workspace and order of work, on one of the device's 4 shared HIP streams
+// (PSF_STREAM_SHARED: hundreds of peers do not alias hundreds of streams onto
+// the hardware queues) -- and no lock is shared between instances.  The cached
+// memory of all of them is bounded once per device (psf_set_device_cache_limit).
 //
 // Filters adapted: all four -- KEY_CACHING, FIXING_FLOAT, COMPRESSING
 // (snappy 1.1.8-identical streams) and NOISE.  (Device-resident messages go
@@ -37,6 +40,7 @@
 #include <mutex>
 #include <string>
 #include <tuple>
+#include <vector>
 
 #include "psf.h"
 
@@ -46,12 +50,12 @@ namespace psf_hip {
 inline void Check(int st) { CHECK_EQ(st, PSF_OK) << "libpsf: " << psf_last_error(); }
 
 // One filter instance's libpsf state: a context on the process's device
-// (psf_default_device: PSF_DEVICE, else 0) with its own non-blocking stream,
-// and a RemoteNode holding the libpsf filter instances.
+// (psf_default_device: PSF_DEVICE, else 0) on one of the device's shared
+// streams, and a RemoteNode holding the libpsf filter instances.
 class Bound {
  protected:
   Bound() {
-    Check(psf_context_create(psf_default_device(), nullptr, 1, &ctx_));
+    Check(psf_context_create(psf_default_device(), nullptr, PSF_STREAM_SHARED, &ctx_));
     Check(psf_node_create(ctx_, &node_));
   }
   ~Bound() {
@@ -260,8 +264,8 @@ class KeyCachingFilter : public Filter, Bound {
 // RemoteNode::EncodeMessage / DecodeMessage (remote_node.cc:17-29) do with the
 // per-type instances FindFilterOrCreate keeps (remote_node.cc:7-15), in one
 // call.  One Chain per RemoteNode (a member the RemoteNode patch adds,
-// INTEGRATION.md), so one libpsf context -- device psf_default_device(), a
-// private stream, workspace and allocator -- serves all of that peer's
+// INTEGRATION.md), so one libpsf context -- device psf_default_device(), one
+// of the device's shared streams, its own workspace -- serves all of that peer's
 // filters, and the arrays stay in HBM from the first filter to the last:
 // encode stages each host array in once (the first filter that touches it)
 // and only the chain's result comes back as new SArray<char>s; decode stages
@@ -300,14 +304,18 @@ class Chain {
     if (!Handles(t)) return false;
     std::lock_guard<std::mutex> l(mu_);
     if (!ctx_) {
-      Check(psf_context_create(psf_default_device(), nullptr, 1, &ctx_));
+      Check(psf_context_create(psf_default_device(), nullptr, PSF_STREAM_SHARED, &ctx_));
       Check(psf_node_create(ctx_, &node_));
     }
     psf_message* m = nullptr;
     Check(psf_msg_create(t.request(), t.has_param(), t.has_param() && t.param().push(), t.key_channel(),
                          t.has_key_range(), t.key_range().begin(), t.key_range().end(), &m));
     const bool had_key = msg->has_key();
+    // the inputs stay referenced until the chain's one sync: their H2D copies
+    // run in flight on the stream, and a received zero-copy frame or a pinned
+    // SArray from a pool must not be freed or reused under them
     const SArray<char> key_in = msg->key;
+    const std::vector<SArray<char>> values_in = msg->value;
     if (had_key) Check(psf_msg_set_key(m, msg->key.data(), msg->key.size(), PSF_DT_CHAR, PSF_LOC_HOST));
     for (size_t i = 0; i < msg->value.size(); ++i) {
       const int vt = i < (size_t)t.value_type_size() ? (int)t.value_type(i) : 0;

@@ -9,6 +9,9 @@
 #include "filter/filter.h"
 #include "psf_ps_filter.h"
 
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
 #include <chrono>
 #include <map>
 #include <memory>
@@ -111,6 +114,71 @@ double psadapter_ff_threads(int nthreads, int reps, const void* x, size_t bytes,
   for (int r : rc)
     if (r) return -1.0;
   return s;
+}
+
+// `n` per-filter FIXING_FLOAT adapter instances on one device (a server with
+// n worker peers: RemoteNode keeps one instance per type per peer,
+// remote_node.cc:7-15), `rounds` passes over them, instance i's message
+// length cycling through distinct sizes in [min_values, max_values].  After
+// every message the device-wide allocator stats are read; out[0] = the peak
+// of the device's cached HBM, out[1] = the device cap, out[2] = the peak of
+// the device's live streams, out[3] = shared streams, out[4] = evictions,
+// out[5] = the largest allocated HBM seen.  Returns 0, or -1 when a round
+// trip's decoded values differ from the first pass's for the same size (the
+// decode is deterministic given the seed) or a CHECK failed.
+int psadapter_many_instances(int n, int rounds, const float* x, size_t min_values, size_t max_values,
+                             uint64_t* out) {
+  psf_set_clock(1, 4242);
+  std::vector<std::unique_ptr<psf_hip::FixingFloatFilter>> fs;
+  for (int i = 0; i < n; ++i) fs.emplace_back(new psf_hip::FixingFloatFilter());
+  const size_t span = max_values - min_values + 1;
+  std::vector<uint8_t> codes(max_values);
+  std::vector<float> dec(max_values);
+  float range[2];
+  for (int k = 0; k < 6; ++k) out[k] = 0;
+  for (int r = 0; r < rounds; ++r)
+    for (int i = 0; i < n; ++i) {
+      const size_t m = min_values + ((size_t)(i + 1) * 7919u + (size_t)r * 104729u) % span;
+      if (ff_roundtrip(*fs[i], x, m * 4, 9, 1, 0, 0.f, 0, 0.f, codes.data(), range, dec.data()) != 0) return -1;
+      for (size_t j = 0; j < m; j += 997)  // decoded values lie in the range
+        if (!(dec[j] >= range[0] && dec[j] <= range[1])) {
+          g_err = "decoded value outside [min, max]";
+          return -1;
+        }
+      uint64_t st[10];
+      if (psf_device_memory_stats(psf_default_device(), st) != PSF_OK) return -1;
+      out[0] = std::max(out[0], st[0]);
+      out[1] = st[1];
+      out[2] = std::max(out[2], st[8]);
+      out[3] = st[9];
+      out[4] = st[3];
+      out[5] = std::max(out[5], st[2]);
+    }
+  return 0;
+}
+
+// a FIXING_FLOAT instance created (its context lazily made on first use) on
+// one thread and used from another: the reference's Submit encodes on the
+// app thread and PickActiveMsg decodes on the executor thread
+// (executor.cc:143, 219); the second thread's current device is set to
+// `other_device` first, so a libpsf entry that did not make its context's
+// device current would allocate on the wrong GPU.
+int psadapter_ff_cross_thread(const void* x, size_t bytes, int nb, int64_t seed, int other_device, void* codes,
+                              float* range, void* dec) {
+  psf_set_clock(1, seed);
+  std::unique_ptr<psf_hip::FixingFloatFilter> f(new psf_hip::FixingFloatFilter());
+  int rc = 0;
+  std::thread t([&] {
+    if (hipSetDevice(other_device) != hipSuccess) {
+      rc = -3;
+      return;
+    }
+    rc = ff_roundtrip(*f, x, bytes, 9, nb, 0, 0.f, 0, 0.f, codes, range, dec);
+    int cur = -1;
+    if (rc == 0 && (hipGetDevice(&cur) != hipSuccess || cur != other_device)) rc = -4;  // restored
+  });
+  t.join();
+  return rc;
 }
 
 // COMPRESSING: one message with keys (if kbytes) and one value array.

@@ -3,9 +3,14 @@
  * arithmetic, used ONLY by tests/, __graft_entry__.smoke() and bench.py's
  * cpu_baseline leg as the checker / CPU baseline.  Never linked into libpsf.
  *
- * Pinned against the reference itself: tests/golden/ fixtures are produced by
- * oracle/_ref/libpsref.so (the reference's unmodified headers) and
- * oracle/make_golden.py asserts this file reproduces them byte-for-byte.
+ * PARITY UNPINNED for FIXING_FLOAT (and the KEY_CACHING / COMPRESSING glue
+ * restated in oracle/chain.py): the reference holds no vectors for them
+ * (src/test/fixing_float_test.cc asserts nothing) and its filter headers need
+ * glog / Eigen / the protobuf runtime, absent here, so it cannot be built.
+ * tests/golden/ff_cases.* and scenarios.json are this restatement's own
+ * record (tests/golden/make_golden.py).  Pinned to the reference itself:
+ * CRC32C only (oracle/_ref/libcrc32c_ref.so, compiled from its crc32c.cc);
+ * snappy to the 1.1.8 library, NOISE to libstdc++.
  *
  * Every function cites the reference lines it restates.
  */

@@ -20,7 +20,8 @@ PSF_ERR_BIN = -3
 PSF_ERR_HIP = -4
 PSF_ERR_CHECK = -5
 PSF_ERR_UNSUPPORTED = -6
-PSF_ERR_TIMEOUT = -7  # (no current entry point returns it)
+PSF_ERR_TIMEOUT = -7  # reserved: no entry point returns it
+PSF_STREAM_GIVEN, PSF_STREAM_OWN, PSF_STREAM_SHARED = 0, 1, 2
 
 DT_UINT64, DT_FLOAT, DT_DOUBLE, DT_CHAR = 8, 9, 10, 11
 KEY_CACHING, COMPRESSING, FIXING_FLOAT, NOISE = 1, 2, 3, 4
@@ -143,6 +144,8 @@ SIGNATURES = {
     "psf_context_host_stats_reset": ([vp], C.c_int),
     "psf_context_set_cache_limit": ([vp, u64, u64], C.c_int),
     "psf_context_memory_stats": ([vp, C.POINTER(u64)], C.c_int),
+    "psf_set_device_cache_limit": ([C.c_int, u64, u64], C.c_int),
+    "psf_device_memory_stats": ([C.c_int, C.POINTER(u64)], C.c_int),
     "psf_router_num_results": ([vp], C.c_int),
     "psf_router_result": ([vp, C.c_int, PI, C.POINTER(vp)], C.c_int),
     "psf_router_num_encoded": ([vp], C.c_int),

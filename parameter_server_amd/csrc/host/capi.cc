@@ -1,6 +1,7 @@
 // extern "C" boundary of libpsf (include/psf.h).
 #include "../../../include/psf.h"
 
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -35,6 +36,18 @@ template <typename F> int guarded(F&& f) {
     g_last_error = e.what();
     return PSF_ERR_CHECK;
   }
+}
+
+// the same, with the context's device current on the calling thread for the
+// call (hipMalloc, hipEventCreate and the per-device kernel tables follow the
+// thread's current device, not the stream's): a context on device k may be
+// used from any thread -- the reference encodes on the app thread and decodes
+// on the executor thread (executor.cc:143, 219)
+template <typename F> int guarded(psf::Context* c, F&& f) {
+  return guarded([&] {
+    psf::DeviceScope ds(c ? c->device() : -1);
+    return f();
+  });
 }
 
 psf::FilterConfig* fc_at(psf_message* msg, int idx) {
@@ -77,7 +90,12 @@ int psf_default_device(void) {
   if (e && *e) {
     char* end = nullptr;
     const long v = strtol(e, &end, 10);
-    if (end && *end == 0 && v >= 0 && v < 1024) d = (int)v;
+    if (end && *end == 0 && v >= 0 && v < 1024) {
+      d = (int)v;
+    } else {  // a typo would send every server process to GPU 0 silently: say so
+      g_last_error = std::string("PSF_DEVICE='") + e + "' is not a device index; using device 0";
+      fprintf(stderr, "libpsf: warning: %s\n", g_last_error.c_str());
+    }
   }
   int expect = -1;
   g_default_device.compare_exchange_strong(expect, d);
@@ -86,8 +104,9 @@ int psf_default_device(void) {
 
 int psf_context_create(int device, void* stream, int own_stream, psf_context** out) {
   return guarded([&] {
-    if (!out) return PSF_ERR_ARG;
-    *out = new psf_context{new psf::Context(device, static_cast<hipStream_t>(stream), own_stream != 0)};
+    if (!out || own_stream < 0 || own_stream > PSF_STREAM_SHARED) return PSF_ERR_ARG;
+    if (own_stream == PSF_STREAM_SHARED && stream) return PSF_ERR_ARG;
+    *out = new psf_context{new psf::Context(device, static_cast<hipStream_t>(stream), own_stream)};
     return PSF_OK;
   });
 }
@@ -98,10 +117,10 @@ int psf_context_destroy(psf_context* ctx) {
   return PSF_OK;
 }
 int psf_context_sync(psf_context* ctx) {
-  return guarded([&] { ctx->impl->sync_checked(); return PSF_OK; });
+  return guarded(ctx ? ctx->impl : nullptr, [&] { ctx->impl->sync_checked(); return PSF_OK; });
 }
 int psf_copy_to_host(psf_context* ctx, void* dst, const void* src, size_t bytes) {
-  return guarded([&] {
+  return guarded(ctx ? ctx->impl : nullptr, [&] {
     if (!ctx || (bytes && (!dst || !src))) return PSF_ERR_ARG;
     if (bytes == 0) return PSF_OK;
     psf::Context& c = *ctx->impl;
@@ -113,7 +132,7 @@ int psf_copy_to_host(psf_context* ctx, void* dst, const void* src, size_t bytes)
 }
 
 int psf_copy_to_host_async(psf_context* ctx, void* dst, const void* src, size_t bytes) {
-  return guarded([&] {
+  return guarded(ctx ? ctx->impl : nullptr, [&] {
     if (!ctx || (bytes && (!dst || !src))) return PSF_ERR_ARG;
     if (bytes == 0) return PSF_OK;
     psf::Context& c = *ctx->impl;
@@ -126,7 +145,7 @@ int psf_copy_to_host_async(psf_context* ctx, void* dst, const void* src, size_t 
 // a pinned host buffer from the context's pool; the handle owns it (and keeps
 // the pool alive after the context is gone)
 int psf_host_buffer_alloc(psf_context* ctx, size_t bytes, void** ptr, void** handle) {
-  return guarded([&] {
+  return guarded(ctx ? ctx->impl : nullptr, [&] {
     if (!ctx || !ptr || !handle) return PSF_ERR_ARG;
     psf::Context& c = *ctx->impl;
     if (c.device() < 0) return PSF_ERR_ARG;
@@ -144,7 +163,7 @@ int psf_host_buffer_release(void* handle) {
 // ---------------------------------------------------------------- kernels
 int psf_ff_encode(psf_context* ctx, const void* d_values, size_t n, int value_type,
                   int num_bytes, psf_fixed_point* fp, int32_t seed, void* d_code) {
-  return guarded([&] {
+  return guarded(ctx ? ctx->impl : nullptr, [&] {
     if (!ctx || !fp) return PSF_ERR_ARG;
     if (num_bytes <= 0 || num_bytes >= 8) return PSF_ERR_NBYTES;
     if (value_type != PSF_DT_FLOAT && value_type != PSF_DT_DOUBLE) return PSF_ERR_ARG;
@@ -172,7 +191,7 @@ int psf_ff_encode(psf_context* ctx, const void* d_values, size_t n, int value_ty
 int psf_ff_encode_async(psf_context* ctx, const void* d_values, size_t n, int value_type,
                         int num_bytes, const psf_fixed_point* preset, int32_t seed,
                         void* d_code, float* d_range, int32_t* d_status) {
-  return guarded([&] {
+  return guarded(ctx ? ctx->impl : nullptr, [&] {
     if (!ctx) return PSF_ERR_ARG;
     psf::FixedPoint pre{0, 0, 0.f, 0.f};
     if (preset) pre = psf::FixedPoint{preset->has_min, preset->has_max, preset->min_value, preset->max_value};
@@ -184,7 +203,7 @@ int psf_ff_encode_async(psf_context* ctx, const void* d_values, size_t n, int va
 
 int psf_ff_decode(psf_context* ctx, const void* d_code, size_t n, int value_type,
                   int num_bytes, float min_value, float max_value, void* d_values) {
-  return guarded([&] {
+  return guarded(ctx ? ctx->impl : nullptr, [&] {
     if (!ctx) return PSF_ERR_ARG;
     if (!((double)max_value - (double)min_value > 0)) return PSF_ERR_BIN;
     return psf::ff_decode_launch(d_code, n, value_type, num_bytes, nullptr, min_value, max_value,
@@ -194,7 +213,7 @@ int psf_ff_decode(psf_context* ctx, const void* d_code, size_t n, int value_type
 
 int psf_ff_decode_async(psf_context* ctx, const void* d_code, size_t n, int value_type,
                         int num_bytes, const float* d_range, void* d_values) {
-  return guarded([&] {
+  return guarded(ctx ? ctx->impl : nullptr, [&] {
     if (!ctx || !d_range) return PSF_ERR_ARG;
     return psf::ff_decode_launch(d_code, n, value_type, num_bytes, d_range, 0.f, 0.f, d_values,
                                  ctx->impl->stream(), ctx->impl->prof());
@@ -202,7 +221,7 @@ int psf_ff_decode_async(psf_context* ctx, const void* d_code, size_t n, int valu
 }
 
 int psf_crc32c(psf_context* ctx, const void* d_data, size_t bytes, uint32_t* crc) {
-  return guarded([&] {
+  return guarded(ctx ? ctx->impl : nullptr, [&] {
     if (!ctx || !crc) return PSF_ERR_ARG;
     psf::Context& c = *ctx->impl;
     if (bytes == 0) { *crc = 0; return PSF_OK; }  // crc32c("") == 0
@@ -223,7 +242,7 @@ int psf_key_signature(psf_context* ctx, const void* d_keys, size_t bytes, uint32
 size_t psf_snappy_max_compressed_length(size_t n) { return psf::snappy_max_compressed(n); }
 
 int psf_snappy_compress(psf_context* ctx, const void* d_in, size_t n, void* d_out, size_t* out_len) {
-  return guarded([&] {
+  return guarded(ctx ? ctx->impl : nullptr, [&] {
     if (!ctx || !d_out || !out_len || (n && !d_in) || n > 0xffffffffull) return PSF_ERR_ARG;
     psf::Context& c = *ctx->impl;
     if (c.device() < 0) return PSF_ERR_ARG;
@@ -259,7 +278,7 @@ static psf::Buffer device_view(const void* p, size_t n) {
 }
 
 int psf_snappy_uncompressed_length(psf_context* ctx, const void* d_in, size_t n, size_t* out_len) {
-  return guarded([&] {
+  return guarded(ctx ? ctx->impl : nullptr, [&] {
     if (!ctx || !out_len || (n && !d_in)) return PSF_ERR_ARG;
     psf::Context& c = *ctx->impl;
     if (c.device() < 0) return PSF_ERR_ARG;
@@ -272,7 +291,7 @@ int psf_snappy_uncompressed_length(psf_context* ctx, const void* d_in, size_t n,
 
 int psf_snappy_uncompress(psf_context* ctx, const void* d_in, size_t n, void* d_out, size_t out_cap,
                           size_t* out_len) {
-  return guarded([&] {
+  return guarded(ctx ? ctx->impl : nullptr, [&] {
     if (!ctx || !out_len || (n && !d_in)) return PSF_ERR_ARG;
     psf::Context& c = *ctx->impl;
     if (c.device() < 0) return PSF_ERR_ARG;
@@ -292,7 +311,7 @@ int psf_snappy_uncompress(psf_context* ctx, const void* d_in, size_t n, void* d_
 }
 
 int psf_node_create(psf_context* ctx, psf_node** out) {
-  return guarded([&] {
+  return guarded(ctx ? ctx->impl : nullptr, [&] {
     if (!ctx || !out) return PSF_ERR_ARG;
     *out = new psf_node{new psf::RemoteNode(ctx->impl)};
     return PSF_OK;
@@ -305,14 +324,14 @@ int psf_node_destroy(psf_node* node) {
   return PSF_OK;
 }
 int psf_node_encode(psf_node* node, psf_message* msg) {
-  return guarded([&] {
+  return guarded(node ? node->impl->ctx() : nullptr, [&] {
     if (!node || !msg) return PSF_ERR_ARG;
     node->impl->EncodeMessage(&msg->m);
     return PSF_OK;
   });
 }
 int psf_node_decode(psf_node* node, psf_message* msg) {
-  return guarded([&] {
+  return guarded(node ? node->impl->ctx() : nullptr, [&] {
     if (!node || !msg) return PSF_ERR_ARG;
     node->impl->DecodeMessage(&msg->m);
     return PSF_OK;
@@ -539,7 +558,7 @@ int psf_range_even_divide(uint64_t begin, uint64_t end, uint64_t n, uint64_t i,
 
 int psf_msg_slice(psf_context* ctx, const psf_message* msg, const uint64_t* bounds, int nranges,
                   int key_bytes, psf_message** outs, int* valid) {
-  return guarded([&] {
+  return guarded(ctx ? ctx->impl : nullptr, [&] {
     if (!ctx || !msg || nranges < 0 || (nranges && (!bounds || !outs || !valid))) return PSF_ERR_ARG;
     std::vector<psf::KeyRange> krs(nranges);
     for (int i = 0; i < nranges; ++i) krs[i] = psf::KeyRange{bounds[i], bounds[i + 1]};
@@ -556,7 +575,7 @@ int psf_msg_slice(psf_context* ctx, const psf_message* msg, const uint64_t* boun
 
 int psf_msgs_slice(psf_context* ctx, const psf_message* const* msgs, int nmsgs, const uint64_t* bounds,
                    int nranges, int key_bytes, psf_message** outs, int* valid) {
-  return guarded([&] {
+  return guarded(ctx ? ctx->impl : nullptr, [&] {
     if (!ctx || nmsgs < 0 || nranges < 0 || (nmsgs && !msgs) || (nranges && (!bounds || !outs || !valid)))
       return PSF_ERR_ARG;
     std::vector<psf::KeyRange> krs(nranges);
@@ -580,7 +599,7 @@ int psf_msgs_slice(psf_context* ctx, const psf_message* const* msgs, int nmsgs, 
 
 int psf_node_roundtrip_ex(psf_node* snd, psf_node* rcv, const psf_message* const* tmpls, int ntmpl,
                           int iters, psf_message** enc_out, psf_message** dec_out) {
-  return guarded([&] {
+  return guarded(snd ? snd->impl->ctx() : nullptr, [&] {
     if (!snd || !rcv || !tmpls || ntmpl <= 0 || iters < 0) return PSF_ERR_ARG;
     psf_message* last_enc = nullptr;
     psf_message* last_dec = nullptr;
@@ -620,7 +639,7 @@ int psf_node_roundtrip(psf_node* snd, psf_node* rcv, const psf_message* const* t
 }
 
 int psf_nodes_encode(psf_node* const* nodes, psf_message* const* msgs, int n) {
-  return guarded([&] {
+  return guarded((nodes && n > 0 && nodes[0]) ? nodes[0]->impl->ctx() : nullptr, [&] {
     if (n < 0 || (n && (!nodes || !msgs))) return PSF_ERR_ARG;
     std::vector<psf::RemoteNode*> nd(n);
     std::vector<psf::Message*> ms(n);
@@ -634,7 +653,7 @@ int psf_nodes_encode(psf_node* const* nodes, psf_message* const* msgs, int n) {
   });
 }
 int psf_nodes_decode(psf_node* const* nodes, psf_message* const* msgs, int n) {
-  return guarded([&] {
+  return guarded((nodes && n > 0 && nodes[0]) ? nodes[0]->impl->ctx() : nullptr, [&] {
     if (n < 0 || (n && (!nodes || !msgs))) return PSF_ERR_ARG;
     std::vector<psf::RemoteNode*> nd(n);
     std::vector<psf::Message*> ms(n);
@@ -650,7 +669,7 @@ int psf_nodes_decode(psf_node* const* nodes, psf_message* const* msgs, int n) {
 int psf_nodes_roundtrip_ex(psf_node* const* snd, psf_node* const* rcv, const psf_message* const* tmpls, int n,
                            const int* phase_end, int nphases, int iters, psf_message** enc_out,
                            psf_message** dec_out) {
-  return guarded([&] {
+  return guarded((snd && n > 0 && snd[0]) ? snd[0]->impl->ctx() : nullptr, [&] {
     if (n <= 0 || iters < 0 || !snd || !rcv || !tmpls) return PSF_ERR_ARG;
     std::vector<int> ends;
     if (phase_end && nphases > 0) {
@@ -732,7 +751,7 @@ int psf_nodes_roundtrip(psf_node* const* snd, psf_node* const* rcv, const psf_me
 
 int psf_spill_pack(psf_context* ctx, psf_message* const* msgs, const int* dest, const int* server, int n,
                    int world, int64_t* sizes, psf_spill** out) {
-  return guarded([&] {
+  return guarded(ctx ? ctx->impl : nullptr, [&] {
     if (!ctx || !sizes || !out || n < 0 || world <= 0 || (n && (!msgs || !dest || !server))) return PSF_ERR_ARG;
     std::vector<psf::Message*> ms(n);
     for (int i = 0; i < n; ++i) {
@@ -746,7 +765,7 @@ int psf_spill_pack(psf_context* ctx, psf_message* const* msgs, const int* dest, 
   });
 }
 int psf_spill_fill(psf_spill* plan, void* sendbuf) {
-  return guarded([&] {
+  return guarded(plan ? reinterpret_cast<psf::SpillPlan*>(plan)->context() : nullptr, [&] {
     if (!plan) return PSF_ERR_ARG;
     reinterpret_cast<psf::SpillPlan*>(plan)->fill(sendbuf);
     return PSF_OK;
@@ -758,7 +777,7 @@ int psf_spill_destroy(psf_spill* plan) {
 }
 int psf_spill_unpack(psf_context* ctx, const void* recvbuf, int world, const int64_t* sizes, psf_message** outs,
                      int* servers, int cap, int* n) {
-  return guarded([&] {
+  return guarded(ctx ? ctx->impl : nullptr, [&] {
     if (!ctx || !sizes || !n || world <= 0 || cap < 0 || (cap && (!outs || !servers))) return PSF_ERR_ARG;
     int64_t total = 0;
     for (int r = 0; r < 2 * world; ++r) total += sizes[r];
@@ -781,7 +800,7 @@ int psf_spill_unpack(psf_context* ctx, const void* recvbuf, int world, const int
 
 int psf_router_create(psf_context* ctx, const uint64_t* bounds, int nservers, int rank, int world, int loopback,
                       psf_router** out) {
-  return guarded([&] {
+  return guarded(ctx ? ctx->impl : nullptr, [&] {
     if (!ctx || !bounds || !out || nservers <= 0) return PSF_ERR_ARG;
     std::vector<psf::KeyRange> krs(nservers);
     for (int i = 0; i < nservers; ++i) krs[i] = psf::KeyRange{bounds[i], bounds[i + 1]};
@@ -798,10 +817,10 @@ static psf::PushRouter* R(psf_router* r) {
   return reinterpret_cast<psf::PushRouter*>(r);
 }
 int psf_router_keep_encoded(psf_router* r, int on) {
-  return guarded([&] { R(r)->keep_encoded(on != 0); return PSF_OK; });
+  return guarded(r ? reinterpret_cast<psf::PushRouter*>(r)->context() : nullptr, [&] { R(r)->keep_encoded(on != 0); return PSF_OK; });
 }
 int psf_router_encode(psf_router* r, psf_message* const* streams, int n, int64_t* sizes) {
-  return guarded([&] {
+  return guarded(r ? reinterpret_cast<psf::PushRouter*>(r)->context() : nullptr, [&] {
     if (n < 0 || (n && !streams) || !sizes) return PSF_ERR_ARG;
     std::vector<const psf::Message*> ms(n);
     for (int i = 0; i < n; ++i) {
@@ -813,20 +832,20 @@ int psf_router_encode(psf_router* r, psf_message* const* streams, int n, int64_t
   });
 }
 int psf_router_fill(psf_router* r, void* sendbuf) {
-  return guarded([&] { R(r)->fill(sendbuf); return PSF_OK; });
+  return guarded(r ? reinterpret_cast<psf::PushRouter*>(r)->context() : nullptr, [&] { R(r)->fill(sendbuf); return PSF_OK; });
 }
 int psf_router_decode_local(psf_router* r) {
-  return guarded([&] { R(r)->decode_local(); return PSF_OK; });
+  return guarded(r ? reinterpret_cast<psf::PushRouter*>(r)->context() : nullptr, [&] { R(r)->decode_local(); return PSF_OK; });
 }
 int psf_router_decode_received(psf_router* r, const void* recvbuf, const int64_t* sizes_in) {
-  return guarded([&] {
+  return guarded(r ? reinterpret_cast<psf::PushRouter*>(r)->context() : nullptr, [&] {
     if (!sizes_in) return PSF_ERR_ARG;
     R(r)->decode_received(static_cast<const uint8_t*>(recvbuf), sizes_in);
     return PSF_OK;
   });
 }
 int psf_router_step(psf_router* r, psf_message* const* streams, int n, int iters) {
-  return guarded([&] {
+  return guarded(r ? reinterpret_cast<psf::PushRouter*>(r)->context() : nullptr, [&] {
     if (n < 0 || (n && !streams) || iters < 0) return PSF_ERR_ARG;
     psf::PushRouter* pr = R(r);
     std::vector<const psf::Message*> ms(n);
@@ -850,7 +869,7 @@ int psf_router_step(psf_router* r, psf_message* const* streams, int n, int iters
   });
 }
 int psf_router_host_stats(psf_router* r, int64_t* out) {
-  return guarded([&] {
+  return guarded(r ? reinterpret_cast<psf::PushRouter*>(r)->context() : nullptr, [&] {
     if (!out) return PSF_ERR_ARG;
     psf::PushRouter* pr = R(r);
     out[0] = pr->stat_steps;
@@ -860,17 +879,17 @@ int psf_router_host_stats(psf_router* r, int64_t* out) {
   });
 }
 int psf_router_host_stats_reset(psf_router* r) {
-  return guarded([&] {
+  return guarded(r ? reinterpret_cast<psf::PushRouter*>(r)->context() : nullptr, [&] {
     psf::PushRouter* pr = R(r);
     pr->stat_steps = pr->stat_encode_ns = pr->stat_decode_ns = 0;
     return PSF_OK;
   });
 }
 int psf_router_num_results(psf_router* r) {
-  return guarded([&] { return (int)R(r)->results().size(); });
+  return guarded(r ? reinterpret_cast<psf::PushRouter*>(r)->context() : nullptr, [&] { return (int)R(r)->results().size(); });
 }
 int psf_router_result(psf_router* r, int i, int* server, psf_message** out) {
-  return guarded([&] {
+  return guarded(r ? reinterpret_cast<psf::PushRouter*>(r)->context() : nullptr, [&] {
     const auto& res = R(r)->results();
     if (i < 0 || i >= (int)res.size() || !out) return PSF_ERR_ARG;
     if (server) *server = res[i].first;
@@ -879,10 +898,10 @@ int psf_router_result(psf_router* r, int i, int* server, psf_message** out) {
   });
 }
 int psf_router_num_encoded(psf_router* r) {
-  return guarded([&] { return (int)R(r)->encoded().size(); });
+  return guarded(r ? reinterpret_cast<psf::PushRouter*>(r)->context() : nullptr, [&] { return (int)R(r)->encoded().size(); });
 }
 int psf_router_encoded(psf_router* r, int i, int32_t* stream, int* server, psf_message** out) {
-  return guarded([&] {
+  return guarded(r ? reinterpret_cast<psf::PushRouter*>(r)->context() : nullptr, [&] {
     const auto& e = R(r)->encoded();
     if (i < 0 || i >= (int)e.size() || !out) return PSF_ERR_ARG;
     if (stream) *stream = e[i].stream;
@@ -906,19 +925,38 @@ int psf_context_host_stats_reset(psf_context* ctx) {
   return PSF_OK;
 }
 int psf_context_set_cache_limit(psf_context* ctx, uint64_t hbm_bytes, uint64_t pinned_bytes) {
-  return guarded([&] {
+  return guarded(ctx ? ctx->impl : nullptr, [&] {
     if (!ctx) return PSF_ERR_ARG;
     ctx->impl->set_cache_limit(hbm_bytes, pinned_bytes);
     return PSF_OK;
   });
 }
 int psf_context_memory_stats(psf_context* ctx, uint64_t* out) {
-  return guarded([&] {
+  return guarded(ctx ? ctx->impl : nullptr, [&] {
     if (!ctx || !out) return PSF_ERR_ARG;
     const psf::Context::MemoryStats m = ctx->impl->memory_stats();
     const uint64_t v[8] = {m.dev_cached, m.dev_cap, m.dev_allocated, m.dev_evictions,
                            m.host_cached, m.host_cap, m.host_allocated, m.host_evictions};
     for (int i = 0; i < 8; ++i) out[i] = v[i];
+    return PSF_OK;
+  });
+}
+int psf_set_device_cache_limit(int device, uint64_t hbm_bytes, uint64_t pinned_bytes) {
+  return guarded([&] {
+    if (device < 0) return PSF_ERR_ARG;
+    psf::set_device_cache_limit(device, hbm_bytes, pinned_bytes);
+    return PSF_OK;
+  });
+}
+int psf_device_memory_stats(int device, uint64_t* out) {
+  return guarded([&] {
+    if (device < 0 || !out) return PSF_ERR_ARG;
+    const psf::DeviceMemoryStats d = psf::device_memory_stats(device);
+    const psf::Context::MemoryStats& m = d.m;
+    const uint64_t v[10] = {m.dev_cached, m.dev_cap, m.dev_allocated, m.dev_evictions,
+                            m.host_cached, m.host_cap, m.host_allocated, m.host_evictions,
+                            d.holders, d.shared_streams};
+    for (int i = 0; i < 10; ++i) out[i] = v[i];
     return PSF_OK;
   });
 }
@@ -972,7 +1010,7 @@ int psf_fc_uncompressed(const psf_message* msg, int idx, int i, uint64_t* size) 
 
 // ------------------------------------------------- server-side consumers
 int psf_node_set_defer_dequant(psf_node* node, int enable) {
-  return guarded([&] {
+  return guarded(node ? node->impl->ctx() : nullptr, [&] {
     if (!node) return PSF_ERR_ARG;
     node->impl->set_defer_dequant(enable != 0);
     return PSF_OK;
@@ -987,7 +1025,7 @@ int psf_msg_pending(const psf_message* msg, int i, int* num_bytes, float* min_va
   return PSF_OK;
 }
 int psf_msg_materialize(psf_context* ctx, psf_message* msg) {
-  return guarded([&] {
+  return guarded(ctx ? ctx->impl : nullptr, [&] {
     if (!ctx || !msg) return PSF_ERR_ARG;
     psf::materialize(ctx->impl, &msg->m);
     return PSF_OK;
@@ -996,7 +1034,7 @@ int psf_msg_materialize(psf_context* ctx, psf_message* msg) {
 int psf_ordered_match(psf_context* ctx, const uint64_t* d_src_key, size_t nsrc, const void* d_src_val,
                       const uint64_t* d_dst_key, size_t ndst, void* d_dst_val, int k, int value_type,
                       int op, size_t* n) {
-  return guarded([&] {
+  return guarded(ctx ? ctx->impl : nullptr, [&] {
     if (!ctx || !n || k <= 0 || op < 0 || op > 4) return PSF_ERR_ARG;
     if (value_type != PSF_DT_FLOAT && value_type != PSF_DT_DOUBLE) return PSF_ERR_ARG;
     *n = psf::ordered_match_raw(ctx->impl, d_src_key, nsrc, d_src_val, psf::PendingDequant{}, d_dst_key,
@@ -1007,7 +1045,7 @@ int psf_ordered_match(psf_context* ctx, const uint64_t* d_src_key, size_t nsrc, 
 int psf_ff_decode_match(psf_context* ctx, const uint64_t* d_src_key, size_t nsrc, const void* d_code,
                         int num_bytes, float min_value, float max_value, const uint64_t* d_dst_key,
                         size_t ndst, void* d_dst_val, int k, int op, size_t* n) {
-  return guarded([&] {
+  return guarded(ctx ? ctx->impl : nullptr, [&] {
     if (!ctx || !n || k <= 0 || op < 0 || op > 4) return PSF_ERR_ARG;
     if (num_bytes <= 0 || num_bytes >= 8) return PSF_ERR_NBYTES;
     if (!((double)max_value - (double)min_value > 0)) return PSF_ERR_BIN;
@@ -1019,7 +1057,7 @@ int psf_ff_decode_match(psf_context* ctx, const uint64_t* d_src_key, size_t nsrc
 }
 int psf_msg_ordered_match(psf_context* ctx, const psf_message* msg, int i, const uint64_t* d_dst_key,
                           size_t ndst, void* d_dst_val, int k, int value_type, int op, size_t* n) {
-  return guarded([&] {
+  return guarded(ctx ? ctx->impl : nullptr, [&] {
     if (!ctx || !msg || !n || op < 0 || op > 4) return PSF_ERR_ARG;
     if (value_type != PSF_DT_FLOAT && value_type != PSF_DT_DOUBLE) return PSF_ERR_ARG;
     *n = psf::ordered_match(ctx->impl, msg->m, i, d_dst_key, ndst, d_dst_val, value_type, k, op);
@@ -1028,7 +1066,7 @@ int psf_msg_ordered_match(psf_context* ctx, const psf_message* msg, int i, const
 }
 int psf_kvmap_create(psf_context* ctx, size_t capacity, int lr_type, double alpha, double beta,
                      double lambda1, double lambda2, psf_kvmap** out) {
-  return guarded([&] {
+  return guarded(ctx ? ctx->impl : nullptr, [&] {
     if (!ctx || !out || (lr_type != 1 && lr_type != 2)) return PSF_ERR_ARG;
     psf::FtrlConfig c;
     c.lr_type = lr_type;
@@ -1047,35 +1085,35 @@ int psf_kvmap_destroy(psf_kvmap* map) {
   return PSF_OK;
 }
 int psf_kvmap_set_value(psf_kvmap* map, const psf_message* msg) {
-  return guarded([&] {
+  return guarded(map ? map->ctx : nullptr, [&] {
     if (!map || !msg) return PSF_ERR_ARG;
     map->impl->set_value(msg->m);
     return PSF_OK;
   });
 }
 int psf_kvmap_get_value(psf_kvmap* map, psf_message* msg) {
-  return guarded([&] {
+  return guarded(map ? map->ctx : nullptr, [&] {
     if (!map || !msg) return PSF_ERR_ARG;
     map->impl->get_value(&msg->m);
     return PSF_OK;
   });
 }
 int psf_kvmap_push(psf_kvmap* map, const uint64_t* d_keys, size_t n, const float* d_grad) {
-  return guarded([&] {
+  return guarded(map ? map->ctx : nullptr, [&] {
     if (!map || (n && (!d_keys || !d_grad))) return PSF_ERR_ARG;
     map->impl->push(d_keys, n, d_grad, psf::PendingDequant{});
     return PSF_OK;
   });
 }
 int psf_kvmap_pull(psf_kvmap* map, const uint64_t* d_keys, size_t n, float* d_w) {
-  return guarded([&] {
+  return guarded(map ? map->ctx : nullptr, [&] {
     if (!map || (n && (!d_keys || !d_w))) return PSF_ERR_ARG;
     map->impl->pull(d_keys, n, d_w);
     return PSF_OK;
   });
 }
 int psf_kvmap_stats(psf_kvmap* map, int64_t* nnz, double* weight_sum, double* delta_sum, uint64_t* size) {
-  return guarded([&] {
+  return guarded(map ? map->ctx : nullptr, [&] {
     if (!map) return PSF_ERR_ARG;
     const psf::KvMapFtrl::Stats s = map->impl->stats();
     if (nnz) *nnz = s.nnz;

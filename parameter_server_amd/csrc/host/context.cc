@@ -5,82 +5,47 @@
 #include <time.h>
 
 #include <atomic>
+#include <algorithm>
 #include <iterator>
 #include <list>
-#include <unordered_map>
+#include <map>
 #include <vector>
 
 namespace psf {
 
-// The stream plus a stream-ordered caching allocator for codec outputs.  A
-// buffer whose last reference drops goes back on a free list of its size class
-// and is handed to a later allocation on the same stream, so stream order
-// alone protects it (no per-message hipMallocAsync/hipFreeAsync packets in the
-// queue).  Shared by every Buffer the context allocates, so it outlives the
-// Context if buffers do.
+// The stream a context launches on, plus its share of the device's caching
+// allocator for codec outputs.  A buffer whose last reference drops goes back
+// on a free list and is handed to a later allocation on the SAME stream, so
+// stream order alone protects it (no per-message hipMallocAsync/hipFreeAsync
+// packets in the queue).  Shared by every Buffer the context allocates, so it
+// outlives the Context if buffers do.
 //
-// The free lists are bounded: the bytes they hold (HBM and pinned host memory
-// alike) stay under a per-context cap (Context::kDefaultCache*, or
-// psf_context_set_cache_limit).  A release that would pass the cap first
-// frees the least recently released blocks, after the stream has drained (a
-// block on a free list may still be in use by queued kernels).  A server that
-// sees many distinct message sizes therefore keeps at most the cap cached,
+// The free lists are bounded per DEVICE, not per context (DevicePool): the
+// bytes cached by every holder on a device (HBM and pinned host memory alike)
+// stay under one cap (Context::kDefaultCache*, psf_set_device_cache_limit).  A
+// release that would pass the cap first frees the least recently released
+// blocks of the whole device, whichever holder released them, each after its
+// own stream has drained (a block on a free list may still be in use by
+// kernels queued before its release); an hipMalloc that fails drops every
+// cached block of the device and tries again.  So a server with many peers
+// (one context per peer, or per filter instance) keeps at most the cap cached
 // on top of what its live messages hold.
-struct Context::StreamHolder {
+struct Context::StreamHolder : std::enable_shared_from_this<Context::StreamHolder> {
   int device;
   hipStream_t stream;
   bool own;
-  std::mutex mu;
-  struct Pool {
-    struct Entry {
-      size_t cls;
-      void* p;
-    };
-    std::list<Entry> lru;  // released blocks, oldest first
-    std::unordered_map<size_t, std::vector<std::list<Entry>::iterator>> by_class;  // per class, oldest first
-    size_t cached = 0, allocated = 0, cap = 0;
-    uint64_t evictions = 0;
-    void* take(size_t cls) {
-      auto it = by_class.find(cls);
-      if (it == by_class.end() || it->second.empty()) return nullptr;
-      auto e = it->second.back();  // the most recently released
-      it->second.pop_back();
-      void* p = e->p;
-      lru.erase(e);
-      cached -= cls;
-      return p;
-    }
-    // the blocks to free so that `extra` more cached bytes fit the cap
-    void make_room(size_t extra, std::vector<Entry>* out) {
-      while (!lru.empty() && cached + extra > cap) {
-        Entry e = lru.front();
-        auto& v = by_class[e.cls];
-        v.erase(v.begin());  // the class's oldest is the overall oldest of its class
-        lru.pop_front();
-        cached -= e.cls;
-        allocated -= e.cls;
-        ++evictions;
-        out->push_back(e);
-      }
-    }
-    void give(size_t cls, void* p) {
-      lru.push_back(Entry{cls, p});
-      by_class[cls].push_back(std::prev(lru.end()));
-      cached += cls;
-    }
-  };
-  Pool dev, host;
-
-  StreamHolder(int d, hipStream_t s, bool o) : device(d), stream(s), own(o) {
-    dev.cap = kDefaultCacheBytes;
-    host.cap = kDefaultPinnedCacheBytes;
-  }
+  bool retired = false;  // its context is gone: releases are freed, not cached
+  // this holder's share (under the pool's lock)
+  uint64_t dev_cached = 0, dev_allocated = 0, dev_evictions = 0;
+  uint64_t host_cached = 0, host_allocated = 0, host_evictions = 0;
+  StreamHolder(int d, hipStream_t s, bool o) : device(d), stream(s), own(o) {}
   ~StreamHolder() {
-    (void)hipSetDevice(device);
+    int cur = -1;  // (no DeviceScope: a destructor must not throw)
+    (void)hipGetDevice(&cur);
+    if (cur != device) (void)hipSetDevice(device);
     (void)hipStreamSynchronize(stream);
-    for (auto& e : dev.lru) (void)hipFree(e.p);
-    for (auto& e : host.lru) (void)hipHostFree(e.p);
     if (own) (void)hipStreamDestroy(stream);
+    if (cur >= 0 && cur != device) (void)hipSetDevice(cur);
   }
   static size_t size_class(size_t bytes) {
     if (bytes <= 4096) return 4096;
@@ -91,112 +56,249 @@ struct Context::StreamHolder {
     }
     return (bytes + (1u << 20) - 1) & ~(size_t)((1u << 20) - 1);  // 1 MiB granules
   }
-  // release `evict` (taken out of a pool under the lock) once the stream has drained
-  void free_blocks(const std::vector<Pool::Entry>& evict, bool pinned) {
-    if (evict.empty()) return;
-    (void)hipStreamSynchronize(stream);
-    for (const auto& e : evict) (void)(pinned ? hipHostFree(e.p) : hipFree(e.p));
-  }
-  void* get(size_t cls) {
-    {
-      std::lock_guard<std::mutex> l(mu);
-      if (void* p = dev.take(cls)) return p;
-    }
-    void* p = nullptr;
-    hipError_t e = hipMalloc(&p, cls);
-    if (e != hipSuccess) {  // out of HBM: drop every cached block, then once more
-      (void)hipGetLastError();
-      std::vector<Pool::Entry> evict;
-      {
-        std::lock_guard<std::mutex> l(mu);
-        const size_t c = dev.cap;
-        dev.cap = 0;
-        dev.make_room(0, &evict);
-        dev.cap = c;
-      }
-      free_blocks(evict, false);
-      PSF_HIP_CHECK(hipMalloc(&p, cls));
-    }
-    std::lock_guard<std::mutex> l(mu);
-    dev.allocated += cls;
+  void* get(size_t cls);
+  void put(size_t cls, void* p);
+  void* get_pinned(size_t cls);
+  void put_pinned(size_t cls, void* p);
+  void retire();  // the context is gone: free this holder's cached blocks
+};
+
+namespace {
+typedef Context::StreamHolder Holder;
+
+struct PoolEntry {
+  size_t cls;
+  void* p;
+  std::shared_ptr<Holder> h;  // keeps the stream alive until the block is freed
+};
+
+// released blocks of one kind (HBM or pinned) on one device
+struct PoolSide {
+  bool pinned;
+  std::list<PoolEntry> lru;  // oldest first
+  // per (holder, class): the entries, oldest first
+  std::map<std::pair<const Holder*, size_t>, std::vector<std::list<PoolEntry>::iterator>> by_key;
+  uint64_t cached = 0, allocated = 0, cap = 0, evictions = 0;
+  uint64_t& h_cached(Holder* h) { return pinned ? h->host_cached : h->dev_cached; }
+  uint64_t& h_allocated(Holder* h) { return pinned ? h->host_allocated : h->dev_allocated; }
+  uint64_t& h_evictions(Holder* h) { return pinned ? h->host_evictions : h->dev_evictions; }
+
+  void* take(Holder* h, size_t cls) {
+    auto it = by_key.find({h, cls});
+    if (it == by_key.end() || it->second.empty()) return nullptr;
+    auto e = it->second.back();  // the most recently released
+    it->second.pop_back();
+    if (it->second.empty()) by_key.erase(it);
+    void* p = e->p;
+    lru.erase(e);
+    cached -= cls;
+    h_cached(h) -= cls;
     return p;
   }
-  void put(size_t cls, void* p) {
-    std::vector<Pool::Entry> evict;
-    bool drop = false;
-    {
-      std::lock_guard<std::mutex> l(mu);
-      if (cls > dev.cap) {  // larger than the whole cache: not kept
-        drop = true;
-        dev.allocated -= cls;
-        ++dev.evictions;
-      } else {
-        dev.make_room(cls, &evict);
-        dev.give(cls, p);
-      }
-    }
-    if (drop) evict.push_back(Pool::Entry{cls, p});
-    free_blocks(evict, false);
+  void unlink(std::list<PoolEntry>::iterator e, std::vector<PoolEntry>* out) {
+    auto k = by_key.find({e->h.get(), e->cls});
+    auto& v = k->second;
+    v.erase(std::find(v.begin(), v.end(), e));
+    if (v.empty()) by_key.erase(k);
+    cached -= e->cls;
+    allocated -= e->cls;
+    ++evictions;
+    h_cached(e->h.get()) -= e->cls;
+    h_allocated(e->h.get()) -= e->cls;
+    ++h_evictions(e->h.get());
+    out->push_back(std::move(*e));
+    lru.erase(e);
   }
-  void* get_pinned(size_t cls) {
-    {
-      std::lock_guard<std::mutex> l(mu);
-      if (void* p = host.take(cls)) return p;
-    }
-    void* p = nullptr;
-    PSF_HIP_CHECK(hipHostMalloc(&p, cls, hipHostMallocMapped | hipHostMallocCoherent));
-    std::lock_guard<std::mutex> l(mu);
-    host.allocated += cls;
-    return p;
+  // the blocks to free so that `extra` more cached bytes fit the cap
+  void make_room(uint64_t extra, std::vector<PoolEntry>* out) {
+    while (!lru.empty() && cached + extra > cap) unlink(lru.begin(), out);
   }
-  void put_pinned(size_t cls, void* p) {
-    std::vector<Pool::Entry> evict;
-    bool drop = false;
-    {
-      std::lock_guard<std::mutex> l(mu);
-      if (cls > host.cap) {
-        drop = true;
-        host.allocated -= cls;
-        ++host.evictions;
-      } else {
-        host.make_room(cls, &evict);
-        host.give(cls, p);
-      }
+  void drop_holder(const Holder* h, std::vector<PoolEntry>* out) {
+    for (auto e = lru.begin(); e != lru.end();) {
+      auto n = std::next(e);
+      if (e->h.get() == h) unlink(e, out);
+      e = n;
     }
-    if (drop) evict.push_back(Pool::Entry{cls, p});
-    free_blocks(evict, true);
   }
-  void set_caps(size_t dev_cap, size_t host_cap) {
-    std::vector<Pool::Entry> ed, eh;
-    {
-      std::lock_guard<std::mutex> l(mu);
-      dev.cap = dev_cap;
-      host.cap = host_cap;
-      dev.make_room(0, &ed);
-      host.make_room(0, &eh);
-    }
-    free_blocks(ed, false);
-    free_blocks(eh, true);
-  }
-  void stats(MemoryStats* s) {
-    std::lock_guard<std::mutex> l(mu);
-    s->dev_cached = dev.cached;
-    s->dev_cap = dev.cap;
-    s->dev_allocated = dev.allocated;
-    s->dev_evictions = dev.evictions;
-    s->host_cached = host.cached;
-    s->host_cap = host.cap;
-    s->host_allocated = host.allocated;
-    s->host_evictions = host.evictions;
+  void give(std::shared_ptr<Holder> h, size_t cls, void* p) {
+    Holder* raw = h.get();
+    lru.push_back(PoolEntry{cls, p, std::move(h)});
+    by_key[{raw, cls}].push_back(std::prev(lru.end()));
+    cached += cls;
+    h_cached(raw) += cls;
   }
 };
 
-void Context::set_cache_limit(size_t dev_bytes, size_t pinned_bytes) {
-  if (holder_) holder_->set_caps(dev_bytes, pinned_bytes);
+struct DevicePool {
+  std::mutex mu;
+  PoolSide dev{false}, host{true};
+  uint64_t holders = 0;  // live stream holders on the device
+  std::vector<std::shared_ptr<Holder>> shared;  // the device's shared streams (psf_context_create own_stream=2)
+  size_t next_shared = 0;
+  DevicePool() {
+    dev.cap = Context::kDefaultCacheBytes;
+    host.cap = Context::kDefaultPinnedCacheBytes;
+  }
+};
+
+constexpr int kMaxDevices = 64;
+DevicePool* device_pool(int device) {
+  static DevicePool* pools[kMaxDevices];
+  static std::mutex mu;
+  if (device < 0 || device >= kMaxDevices) throw CheckError(kErrArg, "device index out of range");
+  std::lock_guard<std::mutex> l(mu);
+  if (!pools[device]) pools[device] = new DevicePool();  // process lifetime
+  return pools[device];
 }
+
+// free evicted blocks, each after its holder's stream has drained
+void free_entries(std::vector<PoolEntry>& ev, bool pinned) {
+  if (ev.empty()) return;
+  DeviceScope ds(ev.front().h->device, true);
+  const Holder* synced = nullptr;
+  for (auto& e : ev) {
+    if (e.h.get() != synced) {
+      (void)hipStreamSynchronize(e.h->stream);
+      synced = e.h.get();
+    }
+    (void)(pinned ? hipHostFree(e.p) : hipFree(e.p));
+  }
+  ev.clear();  // (drops the holder references after the frees)
+}
+}  // namespace
+
+void* Holder::get(size_t cls) {
+  DevicePool* pool = device_pool(device);
+  {
+    std::lock_guard<std::mutex> l(pool->mu);
+    if (void* p = pool->dev.take(this, cls)) return p;
+  }
+  void* p = nullptr;
+  DeviceScope ds(device);
+  hipError_t e = hipMalloc(&p, cls);
+  if (e != hipSuccess) {  // out of HBM: drop every cached block of the device, then once more
+    (void)hipGetLastError();
+    std::vector<PoolEntry> ev;
+    {
+      std::lock_guard<std::mutex> l(pool->mu);
+      const uint64_t c = pool->dev.cap;
+      pool->dev.cap = 0;
+      pool->dev.make_room(0, &ev);
+      pool->dev.cap = c;
+    }
+    free_entries(ev, false);
+    PSF_HIP_CHECK(hipMalloc(&p, cls));
+  }
+  std::lock_guard<std::mutex> l(pool->mu);
+  pool->dev.allocated += cls;
+  dev_allocated += cls;
+  return p;
+}
+
+void* Holder::get_pinned(size_t cls) {
+  DevicePool* pool = device_pool(device);
+  {
+    std::lock_guard<std::mutex> l(pool->mu);
+    if (void* p = pool->host.take(this, cls)) return p;
+  }
+  void* p = nullptr;
+  DeviceScope ds(device);
+  PSF_HIP_CHECK(hipHostMalloc(&p, cls, hipHostMallocMapped | hipHostMallocCoherent));
+  std::lock_guard<std::mutex> l(pool->mu);
+  pool->host.allocated += cls;
+  host_allocated += cls;
+  return p;
+}
+
+// (called from Buffer deleters: never throws)
+static void release(Holder* h, PoolSide DevicePool::*side, size_t cls, void* p) {
+  DevicePool* pool = device_pool(h->device);
+  std::vector<PoolEntry> ev;
+  PoolSide& s = pool->*side;
+  {
+    std::lock_guard<std::mutex> l(pool->mu);
+    if (h->retired || cls > s.cap) {  // not kept: freed once the stream drains
+      s.allocated -= cls;
+      ++s.evictions;
+      s.h_allocated(h) -= cls;
+      ++s.h_evictions(h);
+      ev.push_back(PoolEntry{cls, p, h->shared_from_this()});
+    } else {
+      s.make_room(cls, &ev);
+      s.give(h->shared_from_this(), cls, p);
+    }
+  }
+  free_entries(ev, s.pinned);
+}
+void Holder::put(size_t cls, void* p) { release(this, &DevicePool::dev, cls, p); }
+void Holder::put_pinned(size_t cls, void* p) { release(this, &DevicePool::host, cls, p); }
+
+void Holder::retire() {
+  DevicePool* pool = device_pool(device);
+  std::vector<PoolEntry> ed, eh;
+  {
+    std::lock_guard<std::mutex> l(pool->mu);
+    retired = true;
+    pool->dev.drop_holder(this, &ed);
+    pool->host.drop_holder(this, &eh);
+    --pool->holders;
+  }
+  free_entries(ed, false);
+  free_entries(eh, true);
+}
+
+static void set_device_caps(int device, uint64_t dev_cap, uint64_t host_cap) {
+  DevicePool* pool = device_pool(device);
+  std::vector<PoolEntry> ed, eh;
+  {
+    std::lock_guard<std::mutex> l(pool->mu);
+    pool->dev.cap = dev_cap;
+    pool->host.cap = host_cap;
+    pool->dev.make_room(0, &ed);
+    pool->host.make_room(0, &eh);
+  }
+  free_entries(ed, false);
+  free_entries(eh, true);
+}
+
+void Context::set_cache_limit(size_t dev_bytes, size_t pinned_bytes) {
+  if (device_ >= 0) set_device_caps(device_, dev_bytes, pinned_bytes);
+}
+void set_device_cache_limit(int device, uint64_t dev_bytes, uint64_t pinned_bytes) {
+  set_device_caps(device, dev_bytes, pinned_bytes);
+}
+
 Context::MemoryStats Context::memory_stats() const {
   MemoryStats s;
-  if (holder_) holder_->stats(&s);
+  if (!holder_) return s;
+  DevicePool* pool = device_pool(device_);
+  std::lock_guard<std::mutex> l(pool->mu);
+  const Holder& h = *holder_;
+  s.dev_cached = h.dev_cached;
+  s.dev_cap = pool->dev.cap;
+  s.dev_allocated = h.dev_allocated;
+  s.dev_evictions = h.dev_evictions;
+  s.host_cached = h.host_cached;
+  s.host_cap = pool->host.cap;
+  s.host_allocated = h.host_allocated;
+  s.host_evictions = h.host_evictions;
+  return s;
+}
+
+DeviceMemoryStats device_memory_stats(int device) {
+  DeviceMemoryStats s;
+  DevicePool* pool = device_pool(device);
+  std::lock_guard<std::mutex> l(pool->mu);
+  s.m.dev_cached = pool->dev.cached;
+  s.m.dev_cap = pool->dev.cap;
+  s.m.dev_allocated = pool->dev.allocated;
+  s.m.dev_evictions = pool->dev.evictions;
+  s.m.host_cached = pool->host.cached;
+  s.m.host_cap = pool->host.cap;
+  s.m.host_allocated = pool->host.allocated;
+  s.m.host_evictions = pool->host.evictions;
+  s.holders = pool->holders;
+  s.shared_streams = pool->shared.size();
   return s;
 }
 
@@ -204,14 +306,34 @@ Context::MemoryStats Context::memory_stats() const {
 // uncompress: the control words of kSnappyBatchMax streams
 static constexpr size_t kZeroBytes[Context::kZeroKinds] = {65536, 2048};
 
-Context::Context(int device, hipStream_t stream, bool own) : device_(device), stream_(nullptr) {
+Context::Context(int device, hipStream_t stream, int mode) : device_(device), stream_(nullptr) {
   if (device < 0) return;  // host-only context: host-resident buffers, no HIP calls
-  PSF_HIP_CHECK(hipSetDevice(device));
-  if (own) stream = nullptr;
-  if (own) PSF_HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-  stream_ = stream;
-  // constructed in place: a temporary StreamHolder would destroy the stream
-  holder_ = std::shared_ptr<StreamHolder>(new StreamHolder(device, stream, own));
+  DeviceScope ds(device);
+  DevicePool* pool = device_pool(device);
+  if (mode == kStreamShared) {
+    // one of the device's kSharedStreams streams, round robin: contexts keep
+    // their own order on it, and a process with hundreds of contexts does not
+    // alias hundreds of streams onto GPU_MAX_HW_QUEUES hardware queues
+    std::lock_guard<std::mutex> l(pool->mu);
+    if (pool->shared.size() < (size_t)kSharedStreams) {
+      hipStream_t s = nullptr;
+      PSF_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+      pool->shared.push_back(std::shared_ptr<StreamHolder>(new StreamHolder(device, s, true)));
+      ++pool->holders;
+    }
+    holder_ = pool->shared[pool->next_shared++ % pool->shared.size()];
+    stream_ = holder_->stream;
+  } else {
+    const bool own = mode == kStreamOwn;
+    if (own) stream = nullptr;
+    if (own) PSF_HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    stream_ = stream;
+    // constructed in place: a temporary StreamHolder would destroy the stream
+    holder_ = std::shared_ptr<StreamHolder>(new StreamHolder(device, stream, own));
+    std::lock_guard<std::mutex> l(pool->mu);
+    ++pool->holders;
+  }
+  shared_stream_ = mode == kStreamShared;
   PSF_HIP_CHECK(hipMalloc(&d_partials_, 2 * sizeof(uint64_t) * kMaxGrid));
   PSF_HIP_CHECK(hipMalloc(&zero_base_, 2 * (kZeroBytes[0] + kZeroBytes[1])));
   PSF_HIP_CHECK(hipMemset(zero_base_, 0, 2 * (kZeroBytes[0] + kZeroBytes[1])));
@@ -228,7 +350,9 @@ Context::Context(int device, hipStream_t stream, bool own) : device_(device), st
 
 Context::~Context() {
   if (device_ < 0) return;
-  (void)hipSetDevice(device_);
+  int cur = -1;  // (no DeviceScope: a destructor must not throw)
+  (void)hipGetDevice(&cur);
+  if (cur != device_) (void)hipSetDevice(device_);
   (void)hipStreamSynchronize(stream_);
   for (auto& u : ring_uses_) {  // messages may outlive the context: leave their ranges on the host
     auto rb = u.rb.lock();
@@ -245,6 +369,12 @@ Context::~Context() {
   (void)hipFree(zero_base_);
   (void)hipFree(d_slots_);
   (void)hipHostFree(h_slots_);
+  // a private stream's cached blocks go now (buffers still held by messages
+  // are freed when they drop); a shared stream keeps its cache for the
+  // device's other contexts
+  if (!shared_stream_) holder_->retire();
+  holder_.reset();
+  if (cur >= 0 && cur != device_) (void)hipSetDevice(cur);
 }
 
 Buffer Context::alloc(size_t bytes) {
@@ -311,6 +441,7 @@ hipEvent_t Context::take_event() {
     return e;
   }
   hipEvent_t e = nullptr;
+  DeviceScope ds(device_);
   PSF_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   return e;
 }

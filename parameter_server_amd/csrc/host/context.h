@@ -27,6 +27,33 @@ namespace psf {
 
 typedef PubSlot Slot;
 
+// Makes `device` the calling thread's current device for the scope and
+// restores the previous one after (no HIP call when it already is current;
+// device < 0 = host-only, nothing to do).  hipMalloc, hipEventCreate and the
+// per-device kernel tables follow the thread's current device, so every
+// libpsf entry that allocates or launches runs inside one.
+struct DeviceScope {
+  int prev = -1;
+  // nothrow: for destructors and deleters (a failure leaves the device as is)
+  explicit DeviceScope(int device, bool nothrow = false) {
+    if (device < 0) return;
+    int cur = -1;
+    hipError_t e = hipGetDevice(&cur);
+    if (e == hipSuccess && cur == device) return;
+    if (e == hipSuccess) e = hipSetDevice(device);
+    if (e == hipSuccess) {
+      prev = cur;
+    } else if (!nothrow) {
+      throw CheckError(kErrHip, std::string("hipSetDevice: ") + hipGetErrorString(e));
+    }
+  }
+  ~DeviceScope() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  DeviceScope(const DeviceScope&) = delete;
+  DeviceScope& operator=(const DeviceScope&) = delete;
+};
+
 class Context;
 // FIXING_FLOAT side-info of one lazy encode batch: the kernels write
 // {min, max, status, 0} (16 bytes) per array into `dev`; resolve() brings
@@ -52,10 +79,13 @@ class Context {
   static constexpr int kDeferSlot0 = kSyncSlots;
   static constexpr int kPresignSlot0 = 512;
 
-  // own_stream -> a private non-blocking stream owned by the context; else
-  // `stream` as given (nullptr = the legacy default stream).
+  // mode kStreamOwn -> a private non-blocking stream owned by the context;
+  // kStreamGiven -> `stream` as given (nullptr = the legacy default stream);
+  // kStreamShared -> one of the device's kSharedStreams process-wide streams.
   // device < 0 -> host-only context (host-resident buffers; no HIP calls).
-  Context(int device, hipStream_t stream, bool own_stream);
+  enum StreamMode { kStreamGiven = 0, kStreamOwn = 1, kStreamShared = 2 };
+  static constexpr int kSharedStreams = 4;  // = GPU_MAX_HW_QUEUES' default
+  Context(int device, hipStream_t stream, int mode);
   ~Context();
 
   int device() const { return device_; }
@@ -83,8 +113,9 @@ class Context {
   void zero_pair_unused(int kind, const ZeroPair& z) {
     if (z.cur) zero_parity_[kind] ^= 1;
   }
-  // The caching allocator's bounds (bytes kept on the free lists, per
-  // context): HBM and pinned host memory.  Defaults below; see context.cc.
+  // The caching allocator's bounds (bytes kept on the free lists of the
+  // context's DEVICE, shared by every context on it): HBM and pinned host
+  // memory.  Defaults below; see context.cc.
   static constexpr size_t kDefaultCacheBytes = size_t(8) << 30;
   static constexpr size_t kDefaultPinnedCacheBytes = size_t(1) << 30;
   void set_cache_limit(size_t dev_bytes, size_t pinned_bytes);
@@ -92,7 +123,7 @@ class Context {
     uint64_t dev_cached = 0, dev_cap = 0, dev_allocated = 0, dev_evictions = 0;
     uint64_t host_cached = 0, host_cap = 0, host_allocated = 0, host_evictions = 0;
   };
-  MemoryStats memory_stats() const;
+  MemoryStats memory_stats() const;  // this context's stream's share; caps per device
   // pooled timing-free events
   hipEvent_t take_event();
   void give_event(hipEvent_t e);
@@ -146,6 +177,8 @@ class Context {
     for (int w = 0; w < kWaitNum; ++w) wait_ns_[w] = wait_n_[w] = 0;
   }
 
+  struct StreamHolder;  // a stream + its share of the device's caching allocator (context.cc)
+
  private:
   Profiler prof_;
   int64_t wait_ns_[kWaitNum] = {0, 0, 0}, wait_n_[kWaitNum] = {0, 0, 0};
@@ -159,8 +192,8 @@ class Context {
     uint64_t start, n;
   };
   std::deque<RingUse> ring_uses_;
-  struct StreamHolder;
   int device_;
+  bool shared_stream_ = false;
   hipStream_t stream_;
   std::shared_ptr<StreamHolder> holder_;
   void* d_partials_ = nullptr;
@@ -174,6 +207,14 @@ class Context {
   Buffer noise_f32_, noise_f64_;
   std::mutex mu_;
 };
+
+// the device-wide view of the caching allocator (psf_device_memory_stats)
+struct DeviceMemoryStats {
+  Context::MemoryStats m;
+  uint64_t holders = 0, shared_streams = 0;
+};
+DeviceMemoryStats device_memory_stats(int device);
+void set_device_cache_limit(int device, uint64_t dev_bytes, uint64_t pinned_bytes);
 
 // monotonic nanoseconds (host waits, router phase timers)
 int64_t now_ns();

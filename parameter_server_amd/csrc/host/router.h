@@ -22,6 +22,7 @@ class PushRouter {
   // ranges: the S server key ranges (contiguous); server s lives on rank
   // s * world / S.  loopback: local slices go through the exchange too.
   PushRouter(Context* ctx, const std::vector<KeyRange>& ranges, int rank, int world, bool loopback);
+  Context* context() const { return ctx_; }
   ~PushRouter();
 
   // Slice + encode every stream's message (templates are copied, as the

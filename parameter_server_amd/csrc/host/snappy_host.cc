@@ -255,7 +255,7 @@ void SnappyBatch::finish() {
     }
     const Slot& h = *c_.pub_host(j.slot);
     if (h.status != kOk) {
-      if (bad == kOk || h.status == kErrTimeout) bad = h.status;
+      bad = h.status;
       continue;
     }
     j.out.bytes = h.size;
@@ -268,7 +268,6 @@ void SnappyBatch::finish() {
   }
   jobs_.clear();
   launched_ = 0;
-  if (bad == kErrTimeout) throw CheckError(kErrTimeout, "snappy: a device-side wait hit its cap");
   if (bad != kOk) throw CheckError(kErrCheck, "CHECK(snappy::RawUncompress(src, src_size, data_))");
 }
 

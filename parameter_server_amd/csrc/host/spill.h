@@ -12,6 +12,7 @@ class SpillPlan {
  public:
   // message i goes to rank dest[i], addressed to server server[i]
   SpillPlan(Context* ctx, Message* const* msgs, const int* dest, const int* server, int n, int world);
+  Context* context() const { return ctx_; }
   // per rank r: sizes()[2r] = meta bytes, sizes()[2r+1] = payload bytes
   const std::vector<int64_t>& sizes() const { return sizes_; }
   uint64_t total() const { return total_; }

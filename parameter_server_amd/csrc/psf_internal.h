@@ -20,7 +20,7 @@ constexpr int kErrBin = -3;
 constexpr int kErrHip = -4;
 constexpr int kErrCheck = -5;
 constexpr int kErrUnsupported = -6;
-constexpr int kErrTimeout = -7;  // a device-side wait hit its cap (the launch gave up)
+constexpr int kErrTimeout = -7;  // reserved (PSF_ERR_TIMEOUT): no kernel waits on another, none returns it
 constexpr int kErrHeaderHint = -100;  // internal: a snappy stream's header differs from the size hint
 
 // task.proto DataType values used by the codecs

@@ -35,6 +35,26 @@ def set_clock(t: Optional[int]) -> None:
     lib().psf_set_clock(0 if t is None else 1, 0 if t is None else int(t))
 
 
+def device_memory_stats(device: int = 0) -> dict:
+    """The device-wide caching allocator (every context on `device`): bytes
+    cached / cap / allocated and evictions for HBM ("hbm_*") and pinned host
+    memory ("pinned_*"), the live streams with a cache share and the shared
+    streams created (psf_device_memory_stats)."""
+    out = (C.c_uint64 * 10)()
+    check(lib().psf_device_memory_stats(device, out))
+    keys = ("cached", "cap", "allocated", "evictions")
+    return {**{f"hbm_{k}": out[i] for i, k in enumerate(keys)},
+            **{f"pinned_{k}": out[4 + i] for i, k in enumerate(keys)},
+            "streams": out[8], "shared_streams": out[9]}
+
+
+def set_device_cache_limit(device: int, hbm_bytes: int, pinned_bytes: int) -> None:
+    check(lib().psf_set_device_cache_limit(device, hbm_bytes, pinned_bytes))
+
+
+DEFAULT_CACHE_LIMIT = (8 << 30, 1 << 30)  # Context::kDefaultCache*Bytes
+
+
 class Context:
     def __init__(self, device: int = 0, stream: Optional[torch.cuda.Stream] = None):
         self.device = device
@@ -83,8 +103,9 @@ class Context:
         check(lib().psf_context_set_cache_limit(self.h, hbm_bytes, pinned_bytes))
 
     def memory_stats(self) -> dict:
-        """The caching allocator: bytes cached / cap / allocated and evictions,
-        for HBM ("hbm_*") and pinned host memory ("pinned_*")."""
+        """This context's share of the device's caching allocator: bytes cached
+        / allocated and evictions, for HBM ("hbm_*") and pinned host memory
+        ("pinned_*"); the caps ("*_cap") are the device's."""
         out = (C.c_uint64 * 8)()
         check(lib().psf_context_memory_stats(self.h, out))
         keys = ("cached", "cap", "allocated", "evictions")

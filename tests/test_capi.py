@@ -95,6 +95,8 @@ def test_default_device_knob():
     env = dict(os.environ, PSF_DEVICE="5")
     out = subprocess.check_output([sys.executable, "-c", code], cwd=ROOT, env=env).decode().split()
     assert out == ["5", "True", "0", "3"]
-    env["PSF_DEVICE"] = "junk"
-    out = subprocess.check_output([sys.executable, "-c", code], cwd=ROOT, env=env).decode().split()
-    assert out[0] == "0"
+    for bad in ("junk", "1 ", "-1"):  # malformed: device 0, with a warning on stderr
+        env["PSF_DEVICE"] = bad
+        r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True)
+        assert r.returncode == 0 and r.stdout.split()[0] == "0"
+        assert "PSF_DEVICE" in r.stderr and "warning" in r.stderr

@@ -190,3 +190,55 @@ def test_adapter_key_caching_vs_restatement(harness, port):
         want = w.key.size == k.size and w.key.tobytes() == k.tobytes()
         assert bool(got[i]) == want, i
     assert rc[-1] == 2 and not got[5] and sent[1] == 0 and sent[5] == 0
+
+
+def test_adapter_256_instances_one_device_budget(harness):
+    """A server with 256 worker peers: 256 per-filter FIXING_FLOAT adapter
+    instances on one device, message sizes cycling.  The cached HBM of all of
+    them together stays under the ONE device cap (psf_device_memory_stats), and
+    their contexts share the device's 4 streams instead of 256 private ones."""
+    import torch  # noqa: F401  (HIP runtime up before the harness)
+
+    from parameter_server_amd import filter as F
+    L = harness
+    L.psadapter_many_instances.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_size_t, C.c_size_t,
+                                           C.POINTER(C.c_uint64)]
+    L.psadapter_many_instances.restype = C.c_int
+    cap = 96 << 20
+    F.set_device_cache_limit(0, cap, 32 << 20)
+    try:
+        x = np.random.default_rng(3).standard_normal(1 << 21).astype(np.float32)
+        out = (C.c_uint64 * 6)()
+        rc = L.psadapter_many_instances(256, 3, x.ctypes.data, 1 << 16, 1 << 21, out)
+        assert rc == 0, L.psadapter_last_error()
+        peak_cached, dev_cap, streams, shared, evictions, peak_alloc = list(out)
+        assert dev_cap == cap
+        assert peak_cached <= cap, (peak_cached, cap)
+        assert evictions > 0  # 256 instances x distinct sizes would cache far more than 96 MiB
+        assert shared <= 4 and streams <= 16, (streams, shared)
+    finally:
+        F.set_device_cache_limit(0, *F.DEFAULT_CACHE_LIMIT)
+
+
+def test_adapter_context_used_from_another_thread(harness, port):
+    """An instance created on one thread and run from another (the
+    reference's app thread encodes, the executor thread decodes): every
+    libpsf entry makes the context's device current and restores the
+    thread's own.  With one GPU this runs on device 0 on both threads."""
+    import torch
+    L = harness
+    L.psadapter_ff_cross_thread.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.c_int64, C.c_int, C.c_void_p,
+                                            C.POINTER(C.c_float), C.c_void_p]
+    L.psadapter_ff_cross_thread.restype = C.c_int
+    other = 1 if torch.cuda.device_count() > 1 else 0
+    x = np.random.default_rng(5).standard_normal(300_007).astype(np.float32)
+    codes = np.zeros(x.size, np.uint8)
+    dec = np.zeros_like(x)
+    rng = (C.c_float * 2)()
+    rc = L.psadapter_ff_cross_thread(x.ctypes.data, x.nbytes, 1, 99, other, codes.ctypes.data, rng,
+                                     dec.ctypes.data)
+    assert rc == 0, (rc, L.psadapter_last_error())
+    st, pc, mn, mx = port.ff_encode(x, 1, 99)
+    assert st == 0 and np.array_equal(codes, pc)
+    st, pd = port.ff_decode(pc, 1, mn, mx, np.float32)
+    assert dec.tobytes() == pd.tobytes()

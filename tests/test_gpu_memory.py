@@ -1,4 +1,4 @@
-"""GPU: the per-context caching allocator is bounded.
+"""GPU: the caching allocator is bounded (one cap per device).
 
 A long-running server sees many distinct message sizes; the buffers its
 codecs release stay cached for reuse only up to the context's cap (HBM and
@@ -22,7 +22,8 @@ def test_cache_bounded_over_1000_sizes(port):
     st = ctx.memory_stats()
     assert st["hbm_cap"] == 8 << 30 and st["pinned_cap"] == 1 << 30
     cap = 64 << 20
-    ctx.set_cache_limit(cap, 16 << 20)
+    ctx.set_cache_limit(cap, 16 << 20)  # the device's cap: every context on device 0
+    assert F.device_memory_stats(0)["hbm_cap"] == cap
     worker, server = F.RemoteNode(ctx), F.RemoteNode(ctx)
     big = torch.randn(10_000_000, device="cuda")
     F.set_clock(7)
@@ -46,6 +47,7 @@ def test_cache_bounded_over_1000_sizes(port):
             del m, w
             st = ctx.memory_stats()
             assert st["hbm_cached"] <= cap, (i, st)
+            assert F.device_memory_stats(0)["hbm_cached"] <= cap, i
             peak_alloc = max(peak_alloc, st["hbm_allocated"])
         ctx.sync()
         st = ctx.memory_stats()
@@ -60,3 +62,4 @@ def test_cache_bounded_over_1000_sizes(port):
         assert st["hbm_cached"] == 0 and st["hbm_allocated"] == 0 and st["pinned_cached"] == 0, st
     finally:
         F.set_clock(None)
+        F.set_device_cache_limit(0, *F.DEFAULT_CACHE_LIMIT)

@@ -248,3 +248,33 @@ def test_push_router_world2_same_gpu():
         assert ok is True, ok
         # the key-cache hit step sends no keys: fewer spill bytes than the miss step
         assert 0 < sent[1] - sent[0] < sent[0]
+
+
+@pytest.mark.parametrize("gpus", [1, 2])
+def test_bench_default_reports_c4_spill(gpus):
+    """bench.py's default command (c2) with its companion C4 line, small sizes:
+    at --gpus 2 (two ranks sharing cuda:0 over gloo, the rehearsal knobs) the
+    C4 slices for the other rank's servers travel in the all-to-all-v and
+    config_c4 reports the spilled bytes; at --gpus 1 nothing spills."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PSF_DIST_BACKEND="gloo", PSF_SAME_GPU="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(gpus), "--n", str(1 << 20),
+                          "--c4-m", str(1 << 14), "--steps", "3", "--warmup", "1", "--no-cpu-baseline",
+                          "--no-profile", "--no-128m"], env=env, capture_output=True, text=True, timeout=110)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [json.loads(x) for x in out.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    ln = lines[0]
+    assert ln["n_gpus"] == gpus and ln["value"] > 0
+    c4 = ln["config_c4"]
+    assert c4["measured"] and c4["value"] > 0 and c4["world_size"] == gpus
+    if gpus == 2:
+        assert c4["backend"] == "gloo" and c4["scaling"] == "strong"
+        assert c4["spill_bytes_per_step_rank0"] > 0
+    else:
+        assert c4["spill_bytes_per_step_rank0"] == 0

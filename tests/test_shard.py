@@ -245,6 +245,26 @@ def test_bench_launcher_gloo_world2():
     assert lines[0]["n_gpus"] == 2 and lines[0]["world_size"] == 2 and lines[0]["backend"] == "gloo"
 
 
+def test_bench_launcher_default_carries_config_c4():
+    """The default (c2) multi-GPU command also runs C4's cross-range spill and
+    reports it as config_c4 (its world size, backend, strong scaling)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PSF_DIST_BACKEND="gloo")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--launch-check"],
+                         env=env, capture_output=True, text=True, timeout=180)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [json.loads(x) for x in out.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    c4 = lines[0]["config_c4"]
+    assert c4["world_size"] == 2 and c4["backend"] == "gloo" and c4["scaling"] == "strong"
+    assert "all-to-all-v" in c4["parallelism"]
+
+
 def test_slice_many_host_keys_matches_restatement():
     """psf_msgs_slice (many messages, one synchronisation) == the restatement."""
     from oracle import slicing
