@@ -573,7 +573,7 @@ __device__ __forceinline__ void encode_tile_f32_nb1(const float v[4][4], const Q
 // L1/L2-hit load and a funnel shift) -- then quantise, add, pack, store.
 template <typename V, int NB>
 __device__ __forceinline__ void encode_full_tile(const V v[4][4], const QuantParams& q, const EncodeParams& p,
-                                                 uint8_t* __restrict__ out, size_t gb) {
+                                                 uint8_t* __restrict__ out, size_t gb, size_t gs) {
   uint32_t b4[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
@@ -582,7 +582,7 @@ __device__ __forceinline__ void encode_full_tile(const V v[4][4], const QuantPar
     b4[u] = __builtin_amdgcn_alignbit(w.y, w.x, k & 31u) & 0xFu;
   }
   if (NB == 1 && sizeof(V) == 4) {
-    encode_tile_f32_nb1(reinterpret_cast<const float(*)[4]>(v), q, b4, reinterpret_cast<uint32_t*>(out) + gb);
+    encode_tile_f32_nb1(reinterpret_cast<const float(*)[4]>(v), q, b4, reinterpret_cast<uint32_t*>(out) + gs);
     return;
   }
   uint32_t fl[4][4];
@@ -592,7 +592,7 @@ __device__ __forceinline__ void encode_full_tile(const V v[4][4], const QuantPar
     uint64_t r[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) r[j] = (uint64_t)(uint32_t)(fl[u][j] + ((b4[u] >> j) & 1u));
-    store_codes<NB>(out, gb + u * kBlock, r);
+    store_codes<NB>(out, gs + u * kBlock, r);
   }
 }
 
@@ -650,13 +650,13 @@ __global__ __launch_bounds__(kBlock) void ff_encode(const V* __restrict__ x, siz
 
   if (kVec) {
     if (t0 < tf) {
-      encode_full_tile<V, NB>(first, q, p, out, t0 * kTileGroups + threadIdx.x);
+      encode_full_tile<V, NB>(first, q, p, out, t0 * kTileGroups + threadIdx.x, t0 * kTileGroups + threadIdx.x);
       for (size_t t = t0 + 1; t < tf; ++t) {
         const size_t gb = t * kTileGroups + threadIdx.x;
         V v[4][4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) Vec4<V>::load(x + 4 * (gb + u * kBlock), v[u]);
-        encode_full_tile<V, NB>(v, q, p, out, gb);
+        encode_full_tile<V, NB>(v, q, p, out, gb, gb);
       }
     }
     // the partial last tile of the array, if this workgroup owns it: the LCG
@@ -907,6 +907,108 @@ __device__ __forceinline__ void tile_range_of(size_t ntiles, uint32_t wg, uint32
   t1 = t0 + per < ntiles ? t0 + per : ntiles;
 }
 
+// ---- codes written into a stored snappy stream (COMPRESSING next) ----------
+// FfJob::flags bit 2: the job's codes go to the layout of psf_internal.h's
+// StoredLayout (fragment k's 64 KiB at hdr + 65539 k + 3, tags and the varint
+// header written here too), so COMPRESSING leaves a stream whose fragments
+// all come out stored where it is.  A full tile's codes (4 KiB per tile at
+// nb = 1; a tile never straddles a fragment at nb 1 or 2) are staged in LDS
+// and written as aligned dwords, each composed from two LDS dwords (the
+// stream position is misaligned by hdr + 3k + 3 mod 4).  The dword that
+// straddles two tiles is written whole by the workgroup that processed both
+// (the previous tile's last code dword carried over); at a workgroup's first
+// and last tile, and in the partial tile and the ragged tail, each side
+// writes its own bytes of it with byte stores.
+constexpr uint32_t kFlagStored = 4u;
+
+// bytes of a full tile's codes
+template <int NB>
+constexpr uint32_t tile_code_bytes() { return (uint32_t)kTileGroups * 4u * NB; }
+
+// payload byte b of a stored stream (and, at a fragment's first byte, the
+// fragment's tag and -- fragment 0 -- the header before it), one thread
+__device__ __forceinline__ void stored_put_byte(uint8_t* __restrict__ out, const StoredLayout& L, uint32_t b,
+                                                uint8_t v) {
+  out[stored_pos(L, b)] = v;
+  if ((b & 65535u) == 0) {
+    const uint32_t k = b >> 16;
+    const uint64_t p0 = k ? stored_frag_tag(L, k) : 0, p1 = stored_frag_data(L, k);
+    for (uint64_t P = p0; P < p1; ++P) out[P] = stored_prefix_byte(L, k, P);
+  }
+}
+
+// the NB * 4 code bytes of group g (partial tile, ragged tail)
+template <int NB>
+__device__ __forceinline__ void stored_put_group(uint8_t* __restrict__ out, const StoredLayout& L, size_t g,
+                                                 const uint64_t r[4]) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    uint64_t v = r[e];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      stored_put_byte(out, L, (uint32_t)((size_t)NB * (4 * g + e) + j), (uint8_t)(v & 0xFF));
+      v >>= 8;
+    }
+  }
+}
+
+// tile t's codes (in LDS: `lds`, tile_code_bytes<NB>() bytes) to the stream.
+// carry: the previous tile's last code dword, valid when prev_here (this
+// workgroup processed tile t - 1 just before); next_here: it processes t + 1
+// next (and writes the dword the two share).
+template <int NB>
+__device__ __forceinline__ void stored_tile_out(uint8_t* __restrict__ out, const StoredLayout& L, size_t t,
+                                                const uint32_t* lds, uint32_t carry, bool prev_here,
+                                                bool next_here) {
+  constexpr uint32_t Lt = tile_code_bytes<NB>();
+  const uint32_t b0 = (uint32_t)(t * Lt);
+  const uint32_t k = b0 >> 16;
+  const uint64_t S = stored_pos(L, b0);
+  const bool first = (b0 & 65535u) == 0;
+  const uint64_t P = first ? (k ? stored_frag_tag(L, k) : 0) : S;  // the bytes this tile owns: [P, Q)
+  const uint64_t Q = S + Lt;
+  const uint64_t D0 = P >> 2, D1 = (Q + 3) >> 2;
+  uint32_t* o32 = reinterpret_cast<uint32_t*>(out);
+  for (uint64_t D = D0 + threadIdx.x; D < D1; D += kBlock) {
+    const int64_t c = (int64_t)(4 * D) - (int64_t)S;  // payload offset (in the tile) of the dword's byte 0
+    if (c >= 0 && c + 4 <= (int64_t)Lt) {
+      const uint32_t i = (uint32_t)c >> 2, sh = (uint32_t)c & 3u;
+      o32[D] = sh ? __builtin_amdgcn_alignbyte(lds[i + 1], lds[i], sh) : lds[i];
+      continue;
+    }
+    // an edge dword: header / tag bytes, the neighbour tiles' bytes
+    const bool head = 4 * D < P, tail = 4 * D + 4 > Q;
+    if (tail && next_here) continue;  // the next tile writes it whole
+    const bool whole = !(head && !prev_here) && !tail;
+    uint32_t w = 0, mask = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+      const uint64_t X = 4 * D + j;
+      uint32_t byte = 0;
+      if (X < P) {
+        if (!prev_here) continue;
+        byte = (carry >> (8 * (4 - (uint32_t)(P - X)))) & 0xFFu;  // the previous tile's last bytes
+      } else if (X >= Q) {
+        continue;
+      } else if (X < S) {
+        byte = stored_prefix_byte(L, k, X);
+      } else {
+        const uint32_t cb = (uint32_t)(X - S);
+        byte = (lds[cb >> 2] >> (8 * (cb & 3u))) & 0xFFu;
+      }
+      w |= byte << (8 * j);
+      mask |= 1u << j;
+    }
+    if (whole) {
+      o32[D] = w;
+    } else {
+#pragma unroll
+      for (uint32_t j = 0; j < 4; ++j)
+        if (mask & (1u << j)) out[4 * D + j] = (uint8_t)(w >> (8 * j));
+    }
+  }
+}
+
 template <typename V, int CAP>
 __global__ __launch_bounds__(kBlock) void ff_minmax_batch(FfBatchT<CAP> B) {
   typedef typename KeyOf<V>::K K;
@@ -1073,9 +1175,30 @@ __global__ __launch_bounds__(kBlock) void ff_encode_batch(FfBatchT<CAP> B) {
   p.k17 = B.k17;
   p.a_lane = B.a_lane;
   p.c_lane = B.c_lane;
-  for (size_t t = t0; t < tf; ++t) {
-    if (t != t0) load_tile(t);
-    encode_full_tile<V, NB>(v, q, p, out, t * kTileGroups + threadIdx.x);
+  const bool stored = (NB == 1 || NB == 2) && (J.flags & kFlagStored);
+  const StoredLayout L = stored_layout((uint32_t)(n * NB));
+  if constexpr (NB == 1 || NB == 2) {
+    if (stored) {
+      // codes staged per tile in LDS (two buffers: one barrier per tile), then
+      // written to their stream positions (stored_tile_out)
+      __shared__ uint32_t stage[2][tile_code_bytes<NB>() / 4];
+      uint32_t carry = 0;
+      for (size_t t = t0; t < tf; ++t) {
+        if (t != t0) load_tile(t);
+        uint32_t* buf = stage[(t - t0) & 1];
+        encode_full_tile<V, NB>(v, q, p, reinterpret_cast<uint8_t*>(buf), t * kTileGroups + threadIdx.x,
+                                threadIdx.x);
+        __syncthreads();
+        stored_tile_out<NB>(out, L, t, buf, carry, t > t0, t + 1 < tf);
+        carry = buf[tile_code_bytes<NB>() / 4 - 1];
+      }
+    }
+  }
+  if (!stored) {
+    for (size_t t = t0; t < tf; ++t) {
+      if (t != t0) load_tile(t);
+      encode_full_tile<V, NB>(v, q, p, out, t * kTileGroups + threadIdx.x, t * kTileGroups + threadIdx.x);
+    }
   }
   for (size_t t = (t0 > tf ? t0 : tf); t < t1; ++t) {
     const size_t gb = t * kTileGroups + threadIdx.x;
@@ -1089,7 +1212,8 @@ __global__ __launch_bounds__(kBlock) void ff_encode_batch(FfBatchT<CAP> B) {
         else Vec4<V>::loadu(x + 4 * g, v);
         uint64_t r[4];
         quant_group<V, NB>(v, q, su, p.k17, r);
-        store_codes<NB>(out, g, r);
+        if (stored) stored_put_group<NB>(out, L, g, r);
+        else store_codes<NB>(out, g, r);
       }
       su = step17(p.a_lane, p.c_lane, su);
     }
@@ -1099,7 +1223,11 @@ __global__ __launch_bounds__(kBlock) void ff_encode_batch(FfBatchT<CAP> B) {
     uint32_t st = lcg_jump(J.u.e.seed, tail);
     for (size_t i = tail; i < n; ++i) {
       uint64_t r = quant_floor<V, NB>(x[i], q) + lcg_bit(st);
-      for (int j = 0; j < NB; ++j) { out[i * NB + j] = (uint8_t)(r & 0xFF); r >>= 8; }
+      for (int j = 0; j < NB; ++j) {
+        if (stored) stored_put_byte(out, L, (uint32_t)(i * NB + j), (uint8_t)(r & 0xFF));
+        else out[i * NB + j] = (uint8_t)(r & 0xFF);
+        r >>= 8;
+      }
     }
   }
 }
@@ -1488,6 +1616,10 @@ static int encode_batch_cap(int value_type, int nb, const FfArray* arrs, int cou
     J.mn = a.preset.min_value;
     J.mx = a.preset.max_value;
     J.flags = (a.preset.has_min ? 1u : 0u) | (a.preset.has_max ? 2u : 0u) | ((uint32_t)(a.slot + 1) << 16);
+    if (a.stored) {
+      if ((nb != 1 && nb != 2) || (reinterpret_cast<uintptr_t>(a.out) & 3)) return kErrArg;
+      J.flags |= kFlagStored;
+    }
     J.u.e.seed = a.seed;
     J.u.e.lcg_pos = lcg_cycle().pos[a.seed & kMask17];
     J.ticket = a.ticket;

@@ -302,9 +302,9 @@ DeviceMemoryStats device_memory_stats(int device) {
   return s;
 }
 
-// compress: the look-back words of up to 8191 fragments (512 MiB per launch);
-// uncompress: the control words of kSnappyBatchMax streams
-static constexpr size_t kZeroBytes[Context::kZeroKinds] = {65536, 2048};
+// uncompress: the control words of kSnappyBatchMax streams (the compressor
+// keeps no zeroed state: kZeroCompress is unused)
+static constexpr size_t kZeroBytes[Context::kZeroKinds] = {0, 2048};
 
 Context::Context(int device, hipStream_t stream, int mode) : device_(device), stream_(nullptr) {
   if (device < 0) return;  // host-only context: host-resident buffers, no HIP calls

@@ -122,7 +122,25 @@ struct FfJob {
   Buffer in, out;
   size_t elems;
   const float* range = nullptr;  // decode: the encode's device {min, max}
+  bool stored = false;           // encode: codes into a stored snappy stream (COMPRESSING next)
 };
+
+// Whether msg's COMPRESSING encode comes right after its FIXING_FLOAT encode
+// on the values (only KEY_CACHING, which touches keys, in between): then the
+// codes are written in the stored-stream layout the compressor leaves in
+// place when no fragment has a match (psf_internal.h StoredLayout).
+bool compressing_follows(const Message* msg) {
+  bool after = false;
+  for (const auto& f : msg->task.filter) {
+    if (f.type == FilterConfig::FIXING_FLOAT) {
+      after = true;
+    } else if (after) {
+      if (f.type == FilterConfig::COMPRESSING) return true;
+      if (f.type != FilterConfig::KEY_CACHING) return false;
+    }
+  }
+  return false;
+}
 
 // the value arrays FixingFloatFilter::convert touches in one message
 // (fixing_float.h:24-47); false when num_bytes == 0 (the filter does nothing)
@@ -180,7 +198,8 @@ void for_each_batch(std::vector<FfJob>& jobs, size_t b, size_t e, bool encode, F
   std::map<std::pair<int, int>, std::vector<size_t>> groups;
   for (size_t q = b; q < e; ++q) {
     FfJob& j = jobs[q];
-    if (e - b > 1 && ff_batchable(j.in.ptr, j.out.ptr, j.elems, j.nb, j.type, encode))
+    // a stored-layout output is written by the batched kernel only, even alone
+    if ((e - b > 1 || j.stored) && ff_batchable(j.in.ptr, j.out.ptr, j.elems, j.nb, j.type, encode))
       groups[{j.type, j.nb}].push_back(q);
     else
       launch_one(q);
@@ -189,7 +208,7 @@ void for_each_batch(std::vector<FfJob>& jobs, size_t b, size_t e, bool encode, F
     for (size_t k = 0; k < g.second.size(); k += kFfBatchMax) {
       std::vector<size_t> part(g.second.begin() + k,
                                g.second.begin() + std::min(g.second.size(), k + (size_t)kFfBatchMax));
-      if (part.size() == 1) launch_one(part[0]);
+      if (part.size() == 1 && !jobs[part[0]].stored) launch_one(part[0]);
       else launch_batch(part);
     }
   }
@@ -238,9 +257,21 @@ void FixingFloatFilter::encode_messages(Context* ctx, std::vector<FfMessage>& ms
         tickets[q - base] = ctx->next_ticket();
       }
       out_bytes[q - base] = j.elems * (size_t)j.nb;
+      j.stored = ctx->device() >= 0 && (j.nb == 1 || j.nb == 2) && out_bytes[q - base] < (1ull << 32) &&
+                 j.in.loc == Loc::kDevice && (reinterpret_cast<uintptr_t>(j.in.ptr) % (j.type == kFloat ? 4 : 8)) == 0 &&
+                 compressing_follows(j.msg);
+      // the whole stored stream, and 64 bytes for the compressor's aligned
+      // reads past a fragment's end
+      if (j.stored) out_bytes[q - base] = stored_stream_bytes(stored_layout((uint32_t)out_bytes[q - base])) + 64;
       seeds[q - base] = (uint32_t)ff_clock_seed();  // `int seed = time(NULL)`, per array
     }
     alloc_outputs(ctx, jobs, base, end, out_bytes);
+    for (size_t q = base; q < end; ++q) {
+      FfJob& j = jobs[q];
+      if (!j.stored) continue;
+      j.out.bytes = j.elems * (size_t)j.nb;  // the payload; COMPRESSING reads it in the stream layout
+      j.out.layout = kLayoutStored;
+    }
     std::shared_ptr<RangeBatch> rb;
     float* ring_dev = nullptr;
     if (nlazy) {
@@ -260,6 +291,10 @@ void FixingFloatFilter::encode_messages(Context* ctx, std::vector<FfMessage>& ms
     };
     auto one = [&](size_t q) {
       FfJob& j = jobs[q];
+      if (j.stored) {  // (not batchable after all: plain codes, in the larger buffer)
+        j.stored = false;
+        j.out.layout = kLayoutPlain;
+      }
       const uint32_t t = tickets[q - base];
       float* r = range_of(q);
       int s = ff_encode_launch(j.in.ptr, j.elems, j.type, j.nb, presets[q - base], seeds[q - base], j.out.ptr,
@@ -274,7 +309,7 @@ void FixingFloatFilter::encode_messages(Context* ctx, std::vector<FfMessage>& ms
         const FfJob& j = jobs[q];
         const uint32_t t = tickets[q - base];
         arrs.push_back(FfArray{j.in.ptr, j.out.ptr, j.elems, presets[q - base], seeds[q - base],
-                               t ? (int)(q - base) : -1, t, range_of(q), ring_of(q)});
+                               t ? (int)(q - base) : -1, t, range_of(q), ring_of(q), j.stored});
       }
       Buffer scratch = ctx->alloc(ff_batch_partials_bytes(arrs.data(), (int)arrs.size()));
       PSF_HPROF(9);

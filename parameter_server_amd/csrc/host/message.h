@@ -99,11 +99,16 @@ class StableList {
 
 enum class Loc : int { kHost = 0, kDevice = 1 };
 
+// Buffer::layout: kLayoutStored -- `bytes` payload bytes written into the
+// stored snappy stream layout at ptr (psf_internal.h StoredLayout): FIXING_FLOAT
+// output that only COMPRESSING (next in the chain) reads
+enum BufferLayout : uint8_t { kLayoutPlain = 0, kLayoutStored = 1 };
 struct Buffer {
   std::shared_ptr<void> owner;  // null => caller-owned memory (caller keeps it alive)
   uint8_t* ptr = nullptr;
   size_t bytes = 0;
   Loc loc = Loc::kDevice;
+  BufferLayout layout = kLayoutPlain;
   bool empty() const { return bytes == 0; }
   void clear() { owner.reset(); ptr = nullptr; bytes = 0; }
 };

@@ -128,12 +128,8 @@ void SnappyBatch::launch(size_t b, size_t e) {
       int st = kOk;
       if (comp && !cj.empty()) {
         Buffer scratch = c_.alloc(snappy_compress_batch_scratch(cj.data(), (int)cj.size()));
-        size_t nfrag = 0;
-        for (const SnappyCJob& q : cj) nfrag += (q.n + 65535) / 65536;
-        const ZeroPair z = c_.zero_pair(Context::kZeroCompress, nfrag * 8 + 8);
         st = snappy_compress_batch_launch(cj.data(), (int)cj.size(), scratch.ptr, c_.stream(), c_.prof(),
-                                          c_.pub_dev(0), z);
-        if (st != kOk) c_.zero_pair_unused(Context::kZeroCompress, z);
+                                          c_.pub_dev(0));
         cj.clear();
       } else if (!comp && !dj.empty()) {
         Tail t;
@@ -159,7 +155,7 @@ void SnappyBatch::launch(size_t b, size_t e) {
     for (size_t i = b; i < e; ++i) {
       Job& j = jobs_[i];
       if (j.compress != comp) continue;
-      if (comp) cj.push_back(SnappyCJob{j.in.ptr, j.in.bytes, j.out.ptr, j.slot, j.ticket});
+      if (comp) cj.push_back(SnappyCJob{j.in.ptr, j.in.bytes, j.out.ptr, j.slot, j.ticket, j.in.layout == kLayoutStored});
       else {
         dj.push_back(SnappyDJob{j.in.ptr, j.in.bytes, j.hdr, j.out.bytes, j.out.ptr, j.slot, j.ticket, j.dq});
         di.push_back(i);
@@ -259,7 +255,14 @@ void SnappyBatch::finish() {
       continue;
     }
     j.out.bytes = h.size;
-    if (j.dq.values) {
+    if (j.compress && h.pad == kStoredInPlace) {
+      // every fragment came out stored: the stream FIXING_FLOAT wrote is the
+      // result (snappy.hip K-place), the compressor's buffer goes unused
+      Buffer o = j.in;
+      o.bytes = h.size;
+      o.layout = kLayoutPlain;
+      *j.dst = o;
+    } else if (j.dq.values) {
       *j.dst = j.values;
       *j.fused = true;
     } else {

@@ -137,6 +137,7 @@ struct FfArray {
   uint32_t ticket;
   float* range;       // device {min, max, status} for a lazy reader, or null
   float* range_host;  // the same into host-mapped memory, or null
+  bool stored = false;  // out is a stored snappy stream (StoredLayout; nb 1 or 2)
 };
 struct FfDecArray {
   const void* code;
@@ -188,6 +189,64 @@ int noise_apply_launch(void* v, const void* z, size_t n, int value_type, float m
 // snappy.hip: COMPRESSING (snappy 1.1.8 raw format).  `out` holds at least
 // snappy_max_compressed(n) bytes; the stream length is published to pub->size.
 constexpr uint32_t kSnappyFragOut = 76544;  // >= MaxCompressedLength(64 KiB), 256-aligned
+
+// The snappy 1.1.8 stream of data without matches -- what RawCompress writes
+// for incompressible input such as FIXING_FLOAT codes: varint32(n), then per
+// 64 KiB fragment one literal (tag + bytes).  A full fragment's tag is the 3
+// bytes 0xF4 0xFF 0xFF (EmitLiteral of 65536 bytes), so fragment k's bytes
+// start at hdr + 65539 k + 3; the last fragment has its own tag.  FIXING_FLOAT
+// writes its codes straight into this layout when COMPRESSING follows
+// (Buffer::kLayoutStored), and COMPRESSING leaves a stream whose fragments all
+// come out stored where it is (snappy.hip K-place).
+constexpr uint32_t kStoredFragBytes = 65536 + 3;
+__host__ __device__ __forceinline__ uint32_t snappy_varint_len(uint64_t v) {
+  uint32_t n = 1;
+  for (; v >= 128; v >>= 7) ++n;
+  return n;
+}
+// EmitLiteral's tag bytes for a literal of len >= 1 bytes
+__host__ __device__ __forceinline__ uint32_t snappy_literal_tag_len(uint32_t len) {
+  const uint32_t m = len - 1;
+  return m < 60 ? 1u : m < 256 ? 2u : m < 65536 ? 3u : m < (1u << 24) ? 4u : 5u;
+}
+struct StoredLayout {
+  uint32_t hdr;     // varint bytes
+  uint32_t tl;      // the last fragment's tag bytes
+  uint32_t last;    // index of the last fragment
+  uint32_t nbytes;  // payload bytes (n < 2^32)
+};
+__host__ __device__ __forceinline__ StoredLayout stored_layout(uint32_t nbytes) {
+  StoredLayout s;
+  s.hdr = snappy_varint_len(nbytes);
+  s.last = (nbytes - 1) >> 16;
+  s.tl = snappy_literal_tag_len(nbytes - (s.last << 16));
+  s.nbytes = nbytes;
+  return s;
+}
+// stream bytes of the whole stored stream
+__host__ __device__ __forceinline__ uint64_t stored_stream_bytes(const StoredLayout& s) {
+  return (uint64_t)s.hdr + (uint64_t)s.last * kStoredFragBytes + s.tl + (s.nbytes - (s.last << 16));
+}
+// where fragment k's tag starts, and its bytes
+__host__ __device__ __forceinline__ uint64_t stored_frag_tag(const StoredLayout& s, uint32_t k) {
+  return (uint64_t)s.hdr + (uint64_t)k * kStoredFragBytes;
+}
+__host__ __device__ __forceinline__ uint64_t stored_frag_data(const StoredLayout& s, uint32_t k) {
+  return stored_frag_tag(s, k) + (k == s.last ? s.tl : 3u);
+}
+// stream position of payload byte b
+__host__ __device__ __forceinline__ uint64_t stored_pos(const StoredLayout& s, uint32_t b) {
+  return stored_frag_data(s, b >> 16) + (b & 65535u);
+}
+// the stream byte at P, a header / tag byte before fragment k's data
+__host__ __device__ __forceinline__ uint8_t stored_prefix_byte(const StoredLayout& s, uint32_t k, uint64_t P) {
+  if (P < s.hdr) return (uint8_t)(((s.nbytes >> (7 * P)) & 127u) | (P + 1 < s.hdr ? 128u : 0u));
+  const uint32_t i = (uint32_t)(P - stored_frag_tag(s, k));
+  const uint32_t m = (k == s.last ? s.nbytes - (k << 16) : 65536u) - 1;
+  const uint32_t tl = k == s.last ? s.tl : 3u;
+  if (i == 0) return tl == 1 ? (uint8_t)(m << 2) : (uint8_t)((59 + tl - 1) << 2);
+  return (uint8_t)(m >> (8 * (i - 1)));
+}
 size_t snappy_max_compressed(size_t n);
 size_t snappy_compress_scratch(size_t n);
 int snappy_compress_launch(const void* in, size_t n, void* out, void* scratch, hipStream_t st,
@@ -207,7 +266,12 @@ struct SnappyCJob {
   void* out;  // snappy_max_compressed(n) bytes
   int slot;
   uint32_t ticket;
+  // `in` is a StoredLayout stream of n payload bytes (FIXING_FLOAT wrote it):
+  // when every fragment comes out stored the stream is left where it is and
+  // published with pub->pad = kStoredInPlace (out untouched); else out as usual
+  bool stored = false;
 };
+constexpr uint32_t kStoredInPlace = 1;
 // A pair of device regions of `bytes` each that replaces a launch's memset of
 // its small control state: `cur` is zero when the launch starts (the previous
 // launch of the same kind cleared it), and the launch clears `next` for the
@@ -219,7 +283,7 @@ struct ZeroPair {
 };
 size_t snappy_compress_batch_scratch(const SnappyCJob* jobs, int njobs);
 int snappy_compress_batch_launch(const SnappyCJob* jobs, int njobs, void* scratch, hipStream_t st,
-                                 Profiler* prof, PubSlot* pub_base, const ZeroPair& z = ZeroPair{});
+                                 Profiler* prof, PubSlot* pub_base);
 // FIXING_FLOAT's decode fused into the uncompress (decode_batch, when a
 // COMPRESSING array's next decode is FIXING_FLOAT): the stream holds codes of
 // nb bytes (1 or 2), and `values` receives dsize / nb dequantised values

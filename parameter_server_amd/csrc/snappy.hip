@@ -295,20 +295,26 @@ __device__ __forceinline__ void prefetch_frag(const uint8_t* __restrict__ in, si
 // Several streams compress in one launch chain (the COMPRESSING arrays of a
 // batch of messages): fragments are numbered across the streams.
 struct CJob {
-  const uint8_t* in;
+  const uint8_t* in;  // the input; a stored job: the StoredLayout stream FIXING_FLOAT wrote
   uint8_t* dst;
   uint64_t n;
-  uint32_t frag0, nfrag, hdr, slot, ticket, pad;
+  uint32_t frag0, nfrag, hdr, slot, ticket, stored;
 };
 struct SnappyCJobs {
   CJob j[kSnappyBatchMax];
   PubSlot* pub;
   uint32_t njobs, nfrag;
-  uint64_t* finfo;   // per fragment: op (tag bytes) << 32 | next_emit (start of the final literal)
-  uint64_t* offset;  // per fragment: its offset in the stream (K-scan)
-  uint32_t* znext;   // (unused: the compressor keeps no zeroed state)
-  uint32_t zwords;
+  uint64_t* finfo;     // per fragment: op (tag bytes) << 32 | next_emit (start of the final literal)
+  uint64_t* offset;    // per fragment: its offset in the stream (K-scan)
+  uint32_t* in_place;  // per job (K-scan streams): every fragment stored, the stream left in `in`
 };
+// fragment k's input bytes: consecutive 64 KiB blocks, or in a stored job the
+// fragment's literal in the StoredLayout stream
+__device__ __forceinline__ const uint8_t* frag_src(const CJob& c, uint32_t k) {
+  if (!c.stored) return c.in + (size_t)k * kFrag;
+  const StoredLayout L = stored_layout((uint32_t)c.n);
+  return c.in + stored_frag_data(L, k);
+}
 __device__ __forceinline__ uint32_t cjob_index(const SnappyCJobs& J, uint32_t g) {
   uint32_t i = 0;
   while (i + 1 < J.njobs && g >= J.j[i + 1].frag0) ++i;
@@ -734,6 +740,50 @@ __device__ __forceinline__ void stage_frag(const uint8_t* __restrict__ g, uint32
   if (tid < len - (nv << 4)) srcb[(nv << 4) + tid] = g[(nv << 4) + tid];
 }
 
+// the same for a fragment at any alignment (a stored job's literal sits at
+// hdr + 65539 k + 3): each lane composes its 16-byte LDS blocks from two
+// aligned source blocks (the stored stream is allocated with 64 bytes to
+// spare); bytes past len are zero
+template <uint32_t T>
+__device__ __forceinline__ void stage_frag_shifted(const uint8_t* __restrict__ g, uint32_t len, uint32_t* src,
+                                                   uint32_t tid) {
+  typedef uint32_t V4 __attribute__((ext_vector_type(4)));
+  const uintptr_t a = reinterpret_cast<uintptr_t>(g);
+  const uint32_t sh = (uint32_t)(a & 15);
+  const auto s16 = gbl<V4>(reinterpret_cast<const void*>(a & ~(uintptr_t)15));
+  uint4* d4 = reinterpret_cast<uint4*>(src);
+  const uint32_t nb = (len + 15) >> 4;
+  constexpr uint32_t U = kFrag / 16 / T;
+  for (uint32_t i0 = 0; i0 < nb; i0 += U * T) {
+    V4 lo[U], hi[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint32_t i = i0 + u * T + tid;
+      if (i < nb) {
+        lo[u] = s16[i];
+        hi[u] = s16[i + 1];
+      }
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint32_t i = i0 + u * T + tid;
+      if (i >= nb) continue;
+      uint4 w = funnel16(make_uint4(lo[u][0], lo[u][1], lo[u][2], lo[u][3]),
+                         make_uint4(hi[u][0], hi[u][1], hi[u][2], hi[u][3]), sh);
+      if (16 * i + 16 > len) {  // the block holding the end: zero past len
+        const uint32_t keep = len - 16 * i;  // 1..15
+        uint32_t* wp = reinterpret_cast<uint32_t*>(&w);
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) {
+          const uint32_t kb = keep > 4 * q ? (keep - 4 * q < 4 ? keep - 4 * q : 4) : 0;
+          wp[q] &= kb >= 4 ? 0xFFFFFFFFu : ((1u << (8 * kb)) - 1u);
+        }
+      }
+      d4[i] = w;
+    }
+  }
+}
+
 // K-parse: persistent workgroups of 8 waves, each over its stripe of the
 // fragments (b, b + G, b + 2G, ...) in rounds of 8: every wave probes one
 // fragment; then the fragments that matched are parsed by waves
@@ -751,8 +801,6 @@ __global__ __launch_bounds__(kCThreads) void snappy_parse(const SnappyCJobs J, u
 #ifdef PSF_DIAG_COUNT
   uint32_t cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
-  if (J.znext)  // the next launch chain's counters (stream order publishes them)
-    for (uint32_t i = blockIdx.x * kCThreads + tid; i < J.zwords; i += gridDim.x * kCThreads) J.znext[i] = 0;
   __syncthreads();
   const uint32_t G = gridDim.x;
   for (uint32_t r0 = 0; (size_t)r0 * G + blockIdx.x < J.nfrag; r0 += W) {
@@ -765,7 +813,7 @@ __global__ __launch_bounds__(kCThreads) void snappy_parse(const SnappyCJobs J, u
         const CJob& c = cjob_of(J, f);
         const size_t start = (size_t)(f - c.frag0) * kFrag;
         const uint32_t len = (uint32_t)min((size_t)kFrag, c.n - start);
-        need = !probe_stored(c.in + start, len, skip, U.q.map[wave], U.q.val[wave], lane);
+        need = !probe_stored(frag_src(c, f - c.frag0), len, skip, U.q.map[wave], U.q.val[wave], lane);
         if (!need && lane == 0) J.finfo[f] = 0;  // no tags, the final literal from byte 0
         PSF_TRACE_T(f, 4, wave * 64);
       }
@@ -787,11 +835,13 @@ __global__ __launch_bounds__(kCThreads) void snappy_parse(const SnappyCJobs J, u
       const CJob& c = cjob_of(J, f);
       const size_t start = (size_t)(f - c.frag0) * kFrag;
       const uint32_t len = (uint32_t)min((size_t)kFrag, c.n - start);
-      const uint8_t* g = c.in + start;
+      const uint8_t* g = frag_src(c, f - c.frag0);
       uint32_t* src = reinterpret_cast<uint32_t*>(U.p.table[1]);  // tables 1..3: 96 KiB
       uint8_t* srcb = reinterpret_cast<uint8_t*>(src);
       if (aligned16(g)) {
         stage_frag<kCThreads>(g, len, src, tid);
+      } else if (c.stored) {
+        stage_frag_shifted<kCThreads>(g, len, src, tid);
       } else {
         for (uint32_t i = tid; i < len; i += kCThreads) srcb[i] = g[i];
       }
@@ -823,7 +873,7 @@ __global__ __launch_bounds__(kCThreads) void snappy_parse(const SnappyCJobs J, u
         uint4* t16 = reinterpret_cast<uint4*>(table);
         for (uint32_t j = lane; j < (1u << (32 - hash_shift(len))) / 8; j += 64) t16[j] = make_uint4(0, 0, 0, 0);
         asm volatile("" ::: "memory");
-        const uint2 r = parse_fragment<false>(table, minlane, skip, sk0, sk1, sk2, c.in + start, nullptr, len,
+        const uint2 r = parse_fragment<false>(table, minlane, skip, sk0, sk1, sk2, frag_src(c, f - c.frag0), nullptr, len,
                                               scratch + (size_t)f * kSnappyFragOut, lane
 #ifdef PSF_DIAG_COUNT
                                               , cnt
@@ -848,11 +898,23 @@ constexpr uint32_t kScanT = 1024;
 __global__ __launch_bounds__(kScanT) void snappy_scan(const SnappyCJobs J) {
   __shared__ uint64_t wsum[kScanT / 64];
   __shared__ uint64_t s_base;
+  __shared__ uint32_t s_any;
   const CJob& c = J.j[blockIdx.x];
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  if (tid == 0) s_base = c.hdr;
-  if (tid < c.hdr) c.dst[tid] = (uint8_t)(((uint32_t)c.n >> (7 * tid)) | (tid + 1 < c.hdr ? 128u : 0u));
+  if (tid == 0) {
+    s_base = c.hdr;
+    s_any = 0;
+  }
   __syncthreads();
+  uint32_t any = 0;  // a fragment with tags (not stored from byte 0)
+  for (uint32_t k = tid; k < c.nfrag; k += kScanT) any |= J.finfo[c.frag0 + k] != 0 ? 1u : 0u;
+  if (any) s_any = 1;
+  __syncthreads();
+  // a stored job whose fragments all came out stored: the stream FIXING_FLOAT
+  // wrote is the result (header and tags included); nothing moves
+  const bool in_place = c.stored && !s_any;
+  if (tid == 0) J.in_place[blockIdx.x] = in_place ? 1u : 0u;
+  if (!in_place && tid < c.hdr) c.dst[tid] = (uint8_t)(((uint32_t)c.n >> (7 * tid)) | (tid + 1 < c.hdr ? 128u : 0u));
   for (uint32_t k0 = 0; k0 < c.nfrag; k0 += kScanT) {
     const uint32_t k = k0 + tid;
     uint64_t v = 0;
@@ -880,6 +942,7 @@ __global__ __launch_bounds__(kScanT) void snappy_scan(const SnappyCJobs J) {
     PubSlot* pub = J.pub + c.slot;
     pub->size = s_base;
     pub->status = kOk;
+    pub->pad = in_place ? kStoredInPlace : 0u;
     publish_ticket(pub, c.ticket);
   }
 }
@@ -894,8 +957,10 @@ constexpr uint32_t kPlaceT = 256;
 constexpr uint32_t kInlineScan = 4096;
 __global__ __launch_bounds__(kPlaceT) void snappy_place(const SnappyCJobs J, const uint8_t* __restrict__ scratch) {
   __shared__ uint64_t s_part[kPlaceT / 64];
+  __shared__ uint32_t s_any[kPlaceT / 64];
   const uint32_t f = blockIdx.x, tid = threadIdx.x;
-  const CJob& c = cjob_of(J, f);
+  const uint32_t ji = cjob_index(J, f);
+  const CJob& c = J.j[ji];
   const uint32_t k = f - c.frag0;
   const size_t start = (size_t)k * kFrag;
   const uint32_t len = (uint32_t)min((size_t)kFrag, c.n - start);
@@ -904,31 +969,52 @@ __global__ __launch_bounds__(kPlaceT) void snappy_place(const SnappyCJobs J, con
   PSF_TRACE(f, 2);
   uint64_t off;
   if (J.offset) {
+    if (J.in_place[ji]) return;  // K-scan found every fragment stored: the stream is in place
     off = J.offset[f];
   } else {
+    // the lengths of the fragments before this one (all full), and -- for a
+    // stored job -- whether any fragment of the stream has tags
     uint64_t part = 0;
-    for (uint32_t i = tid; i < k; i += kPlaceT) part += frag_len(J.finfo[c.frag0 + i], kFrag);
+    uint32_t any = 0;
+    for (uint32_t i = tid; i < c.nfrag; i += kPlaceT) {
+      const uint64_t fi = J.finfo[c.frag0 + i];
+      if (i < k) part += frag_len(fi, kFrag);
+      any |= fi != 0 ? 1u : 0u;
+    }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
-    if ((tid & 63) == 0) s_part[tid >> 6] = part;
+    for (int o = 32; o > 0; o >>= 1) {
+      part += __shfl_xor(part, o, 64);
+      any |= __shfl_xor(any, o, 64);
+    }
+    if ((tid & 63) == 0) {
+      s_part[tid >> 6] = part;
+      s_any[tid >> 6] = any;
+    }
     __syncthreads();
     off = c.hdr;
-    for (uint32_t w = 0; w < kPlaceT / 64; ++w) off += s_part[w];
-    if (k == 0 && tid < c.hdr)
+    any = 0;
+    for (uint32_t w = 0; w < kPlaceT / 64; ++w) {
+      off += s_part[w];
+      any |= s_any[w];
+    }
+    const bool in_place = c.stored && !any;
+    if (k == 0 && tid < c.hdr && !in_place)
       c.dst[tid] = (uint8_t)(((uint32_t)c.n >> (7 * tid)) | (tid + 1 < c.hdr ? 128u : 0u));
     if (k + 1 == c.nfrag && tid == 0 && J.pub) {
       PubSlot* pub = J.pub + c.slot;
       pub->size = off + frag_len(info, len);
       pub->status = kOk;
+      pub->pad = in_place ? kStoredInPlace : 0u;
       publish_ticket(pub, c.ticket);
     }
+    if (in_place) return;  // FIXING_FLOAT wrote the stream, header and tags included
   }
   uint8_t* d = c.dst + off;
   if (op) copy_bytes<kPlaceT>(d, scratch + (size_t)f * kSnappyFragOut, op, tid);
   if (ne < len) {
     d += op;
     d += literal_tag(d, len - ne, tid);
-    copy_bytes<kPlaceT>(d, c.in + start + ne, len - ne, tid);
+    copy_bytes<kPlaceT>(d, frag_src(c, k) + ne, len - ne, tid);
   }
   PSF_TRACE(f, 3);
 }
@@ -2166,11 +2252,11 @@ __global__ __launch_bounds__(256) void snappy_dfrag(const SnappyDJobs J) {
 
 size_t snappy_max_compressed(size_t n) { return 32 + n + n / 6; }
 
-// scratch: tag slots | finfo | offset (one each per fragment)
+// scratch: tag slots | finfo | offset (one each per fragment) | in_place (per job)
 size_t snappy_compress_batch_scratch(const SnappyCJob* jobs, int njobs) {
   size_t nfrag = 0;
   for (int i = 0; i < njobs; ++i) nfrag += (jobs[i].n + kFrag - 1) / kFrag;
-  return nfrag * kSnappyFragOut + nfrag * 16 + 64;
+  return nfrag * kSnappyFragOut + nfrag * 16 + 4 * kSnappyBatchMax + 64;
 }
 
 size_t snappy_compress_scratch(size_t n) {
@@ -2179,7 +2265,7 @@ size_t snappy_compress_scratch(size_t n) {
 }
 
 int snappy_compress_batch_launch(const SnappyCJob* jobs, int njobs, void* scratch, hipStream_t st, Profiler* prof,
-                                 PubSlot* pub_base, const ZeroPair& z) {
+                                 PubSlot* pub_base) {
   if (njobs <= 0 || njobs > kSnappyBatchMax) return kErrArg;
   SnappyCJobs K{};
   K.pub = pub_base;
@@ -2198,6 +2284,7 @@ int snappy_compress_batch_launch(const SnappyCJob* jobs, int njobs, void* scratc
     for (uint64_t v = q.n; v >= 128; v >>= 7) ++c.hdr;
     c.slot = (uint32_t)q.slot;
     c.ticket = q.ticket;
+    c.stored = q.stored ? 1u : 0u;
     K.nfrag += c.nfrag;
     bytes += (double)q.n;
   }
@@ -2205,7 +2292,7 @@ int snappy_compress_batch_launch(const SnappyCJob* jobs, int njobs, void* scratc
   uint8_t* p = s + (size_t)K.nfrag * kSnappyFragOut;
   K.finfo = reinterpret_cast<uint64_t*>(p);
   K.offset = K.finfo + K.nfrag;
-  (void)z;  // every word the kernels read is written first in the same chain
+  K.in_place = reinterpret_cast<uint32_t*>(K.offset + K.nfrag);  // (every word the kernels read is written first in the chain)
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -2225,7 +2312,7 @@ int snappy_compress_batch_launch(const SnappyCJob* jobs, int njobs, void* scratc
 int snappy_compress_launch(const void* in, size_t n, void* out, void* scratch, hipStream_t st, Profiler* prof,
                            PubSlot* pub, uint32_t ticket) {
   const SnappyCJob j{in, n, out, 0, ticket};
-  return snappy_compress_batch_launch(&j, 1, scratch, st, prof, pub, ZeroPair{});
+  return snappy_compress_batch_launch(&j, 1, scratch, st, prof, pub);
 }
 
 static size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
