@@ -326,10 +326,10 @@ def build_workload(args, F, ctx, rank, world, dev, g, n):
                 lst.append(t)
         tmpls, snd, rcv = req + resp + push, wk + sv + wk, sv + wk + sv
 
-        def run(k):
-            F.RemoteNode.roundtrip_many(snd, rcv, tmpls, k, phase_end=[S, 2 * S, 3 * S])
+        def run(k, wire=False):
+            F.RemoteNode.roundtrip_many(snd, rcv, tmpls, k, phase_end=[S, 2 * S, 3 * S], wire=wire)
         # keys travel with the pull request only; the response and the push hit
-        return run, 32 * m * S, 2 * m * S, {"key_bytes_elided": 16 * m * S}
+        return run, 32 * m * S, 2 * m * S, {"key_bytes_elided": 16 * m * S, "wire": True}
     if args.config in ("c4", "c5"):
         # streams sliced at the server ranges, encoded
         # per destination server, spilled (one all-to-all-v) and decoded
@@ -598,6 +598,18 @@ def main():
                    "spill_bytes_per_step_rank0": spill4 // max(args.steps, 1)})
         del run4, r4, extra4
 
+    # C1 with the wire step in the timed region: every encoded Task serialised
+    # (its computed min/max settled to the host) and parsed by the receiver,
+    # as Van::Send / Recv do after EncodeMessage (van.cc:122-191, 244-269)
+    wire_line = None
+    if extra.get("wire"):
+        run(args.warmup, wire=True)
+        elw, _ = timed(lambda k: run(k, wire=True), args.steps, world, dist, ctx)
+        elw = max_over_ranks(elw)
+        wire_line = {"what": "each encoded Task serialised (min/max settled) and parsed by the receiver",
+                     "value": round(world * args.steps * payload / elw / GIB, 2),
+                     "ms_per_step": round(elw / args.steps * 1e3, 4)}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, nb)
@@ -655,6 +667,8 @@ def main():
             line["config_128M"] = also
         if c4:
             line["config_c4"] = c4
+        if wire_line:
+            line["config_wire"] = wire_line
         print(json.dumps(line), flush=True)
 
     if world > 1:

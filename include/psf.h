@@ -357,6 +357,15 @@ int psf_nodes_roundtrip(psf_node* const* snd, psf_node* const* rcv, const psf_me
 int psf_nodes_roundtrip_ex(psf_node* const* snd, psf_node* const* rcv, const psf_message* const* tmpls, int n,
                            const int* phase_end, int nphases, int iters, psf_message** enc_out,
                            psf_message** dec_out);
+/* The same with options: PSF_RT_WIRE serialises each encoded message's Task
+ * frame (psf_task_serialize: the computed min/max settled to the host first,
+ * as Van::Send does after EncodeMessage, van.cc:122-191) and decodes a
+ * message parsed from it (psf_task_parse) with the data frames as they are
+ * (Van::Recv's zero-copy frames, van.cc:244-269). */
+#define PSF_RT_WIRE 1
+int psf_nodes_roundtrip_opts(psf_node* const* snd, psf_node* const* rcv, const psf_message* const* tmpls, int n,
+                             const int* phase_end, int nphases, int iters, int flags, psf_message** enc_out,
+                             psf_message** dec_out);
 
 /* ---- cross-range spill (multi-GPU split, one all-to-all-v per step) -----
  * Replaces the reference's per-server send loop (src/system/executor.cc:

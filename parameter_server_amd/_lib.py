@@ -101,6 +101,8 @@ SIGNATURES = {
     "psf_node_roundtrip_ex": ([vp, vp, C.POINTER(vp), C.c_int, C.c_int, C.POINTER(vp), C.POINTER(vp)], C.c_int),
     "psf_nodes_roundtrip_ex": ([C.POINTER(vp), C.POINTER(vp), C.POINTER(vp), C.c_int, PI, C.c_int, C.c_int,
                                 C.POINTER(vp), C.POINTER(vp)], C.c_int),
+    "psf_nodes_roundtrip_opts": ([C.POINTER(vp), C.POINTER(vp), C.POINTER(vp), C.c_int, PI, C.c_int, C.c_int,
+                                  C.c_int, C.POINTER(vp), C.POINTER(vp)], C.c_int),
     "psf_range_even_divide": ([u64, u64, u64, u64, C.POINTER(u64), C.POINTER(u64)], C.c_int),
     "psf_msg_slice": ([vp, vp, C.POINTER(u64), C.c_int, C.c_int, C.POINTER(vp), PI], C.c_int),
     "psf_msgs_slice": ([vp, C.POINTER(vp), C.c_int, C.POINTER(u64), C.c_int, C.c_int, C.POINTER(vp), PI],

@@ -669,7 +669,14 @@ int psf_nodes_decode(psf_node* const* nodes, psf_message* const* msgs, int n) {
 int psf_nodes_roundtrip_ex(psf_node* const* snd, psf_node* const* rcv, const psf_message* const* tmpls, int n,
                            const int* phase_end, int nphases, int iters, psf_message** enc_out,
                            psf_message** dec_out) {
+  return psf_nodes_roundtrip_opts(snd, rcv, tmpls, n, phase_end, nphases, iters, 0, enc_out, dec_out);
+}
+int psf_nodes_roundtrip_opts(psf_node* const* snd, psf_node* const* rcv, const psf_message* const* tmpls, int n,
+                             const int* phase_end, int nphases, int iters, int flags, psf_message** enc_out,
+                             psf_message** dec_out) {
   return guarded((snd && n > 0 && snd[0]) ? snd[0]->impl->ctx() : nullptr, [&] {
+    if (flags & ~PSF_RT_WIRE) return PSF_ERR_ARG;
+    const bool wire = (flags & PSF_RT_WIRE) != 0;
     if (n <= 0 || iters < 0 || !snd || !rcv || !tmpls) return PSF_ERR_ARG;
     std::vector<int> ends;
     if (phase_end && nphases > 0) {
@@ -723,7 +730,21 @@ int psf_nodes_roundtrip_ex(psf_node* const* snd, psf_node* const* rcv, const psf
         {
           PSF_HPROF(5);
           for (int i = b; i < e; ++i) {
-            w[i] = m[i];  // delivered copy
+            if (wire) {
+              // Van::Send / Van::Recv (van.cc:122-191, 244-269): the Task
+              // serialised after EncodeMessage (its computed min/max settled
+              // to the host first), parsed by the receiver, the data frames
+              // delivered as they are (zero copy)
+              psf::Task t = m[i].task;
+              t.has_key = !m[i].key.empty();
+              const std::string frame = psf::serialize_task(t);
+              w[i] = psf::Message();
+              psf::parse_task(reinterpret_cast<const uint8_t*>(frame.data()), frame.size(), &w[i].task);
+              w[i].key = m[i].key;
+              w[i].value = m[i].value;
+            } else {
+              w[i] = m[i];  // delivered copy
+            }
             wp[i] = &w[i];
           }
         }

@@ -510,21 +510,23 @@ class RemoteNode:
                                      (C.c_void_p * n)(*[m.h.value for m in msgs]), n))
 
     @staticmethod
-    def roundtrip_many(snd, rcv, tmpls, iters: int, keep_last: bool = False, phase_end=None):
-        """psf_nodes_roundtrip_ex: message i encoded on snd[i], decoded on
+    def roundtrip_many(snd, rcv, tmpls, iters: int, keep_last: bool = False, phase_end=None, wire: bool = False):
+        """psf_nodes_roundtrip_opts: message i encoded on snd[i], decoded on
         rcv[i]; phase_end splits the messages into batches run in order.
-        keep_last: return the last iteration's [(encoded, decoded)] per message."""
+        keep_last: return the last iteration's [(encoded, decoded)] per message.
+        wire: the receiver decodes a message parsed from the serialised Task
+        (side-info settled per phase, as Van::Send after EncodeMessage)."""
         n = len(tmpls)
         for a, b, t in zip(snd, rcv, tmpls):
             a._hold(t)
             b._hold(t)
         enc, dec = (C.c_void_p * n)(), (C.c_void_p * n)()
         pe = None if not phase_end else (C.c_int * len(phase_end))(*phase_end)
-        check(lib().psf_nodes_roundtrip_ex((C.c_void_p * n)(*[nd.h.value for nd in snd]),
-                                           (C.c_void_p * n)(*[nd.h.value for nd in rcv]),
-                                           (C.c_void_p * n)(*[t.h.value for t in tmpls]), n, pe,
-                                           len(phase_end or ()), iters,
-                                           enc if keep_last else None, dec if keep_last else None))
+        check(lib().psf_nodes_roundtrip_opts((C.c_void_p * n)(*[nd.h.value for nd in snd]),
+                                             (C.c_void_p * n)(*[nd.h.value for nd in rcv]),
+                                             (C.c_void_p * n)(*[t.h.value for t in tmpls]), n, pe,
+                                             len(phase_end or ()), iters, 1 if wire else 0,
+                                             enc if keep_last else None, dec if keep_last else None))
         if not keep_last:
             return None
         return [(Message(_handle=C.c_void_p(enc[i]), _refs=tmpls[i]._refs),

@@ -126,14 +126,17 @@ def test_batch_roundtrip_driver(ctx):
     ctx.sync()
 
 
-def test_batch_roundtrip_driver_c1_vs_port(ctx, port):
-    """The timed C1 driver (psf_nodes_roundtrip_ex in three phases, what
+@pytest.mark.parametrize("wire", [False, True])
+def test_batch_roundtrip_driver_c1_vs_port(ctx, port, wire):
+    """The timed C1 driver (psf_nodes_roundtrip_opts in three phases, what
     `bench.py --config c1` runs): 64 ctr minibatch streams of 10^5 sorted keys,
     per step a pull request (keys), pull response (weights) and push
     (gradients) with the ctr filters (online_l1lr.conf:36-53), three steps.
     The last step's encoded messages (KEY_CACHING signature and elision,
     codes, side-info) and decoded messages (keys restored, values) of every
-    stream against the C restatement."""
+    stream against the C restatement.  wire: each encoded Task is serialised
+    (side-info settled) and the receiver decodes a message parsed from it, as
+    Van::Send / Recv do (van.cc:122-191, 244-269)."""
     from parameter_server_amd import FIXING_FLOAT, KEY_CACHING
     from parameter_server_amd import filter as F
     m, S, seed = 100_000, 64, 31337
@@ -161,7 +164,7 @@ def test_batch_roundtrip_driver_c1_vs_port(ctx, port):
     F.set_clock(seed)
     try:
         last = F.RemoteNode.roundtrip_many(wk + sv + wk, sv + wk + sv, req + resp + push, 3, keep_last=True,
-                                           phase_end=[S, 2 * S, 3 * S])
+                                           phase_end=[S, 2 * S, 3 * S], wire=wire)
     finally:
         F.set_clock(None)
     node = lambda msg: wk[0]  # noqa: E731  (any node of the context copies out)
