@@ -27,6 +27,7 @@
 // x86 double->uint64 cast semantics for the degenerate nb>=4 ratios.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <string.h>
 
@@ -864,6 +865,7 @@ struct FfBatchT {
   const uint32_t* lcg_bits;
   Lcg17 k17;
   uint32_t a_lane, c_lane;
+  uint32_t mm_reverse;  // min/max workgroups dispatched in reverse array order
   double ratio;
 };
 static_assert(sizeof(FfBatchT<kBatchSmall>) <= 4096, "the small batch fits 4 KiB of kernel arguments");
@@ -1012,11 +1014,15 @@ __device__ __forceinline__ void stored_tile_out(uint8_t* __restrict__ out, const
 template <typename V, int CAP>
 __global__ __launch_bounds__(kBlock) void ff_minmax_batch(FfBatchT<CAP> B) {
   typedef typename KeyOf<V>::K K;
-  const int jb = batch_job(B, blockIdx.x, true);
+  // mm_reverse: workgroups dispatched last-array-first, so the arrays the
+  // encode reads first are the ones read last here (still in the Infinity
+  // Cache when the encode starts)
+  const uint32_t bb = B.mm_reverse ? B.mm_total - 1 - blockIdx.x : blockIdx.x;
+  const int jb = batch_job(B, bb, true);
   const FfJob& J = B.job[jb];
   const V* __restrict__ x = static_cast<const V*>(J.x);
   const size_t n = J.n;
-  const uint32_t wg = blockIdx.x - B.mm_first[jb];
+  const uint32_t wg = bb - B.mm_first[jb];
   const bool al = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
   const int r = (int)((reinterpret_cast<uintptr_t>(x) & 15) / sizeof(V));
   const V* xa = x - r;
@@ -1073,8 +1079,8 @@ __global__ __launch_bounds__(kBlock) void ff_minmax_batch(FfBatchT<CAP> B) {
   block_minmax(lo, hi);
   if (threadIdx.x == 0) {
     K* pp = reinterpret_cast<K*>(B.partials);
-    pp[blockIdx.x] = lo;
-    pp[B.mm_total + blockIdx.x] = hi;
+    pp[bb] = lo;
+    pp[B.mm_total + bb] = hi;
   }
 }
 
@@ -1567,6 +1573,16 @@ size_t ff_batch_partials_bytes(const FfArray* arrs, int count) {
   return 2 * sizeof(uint64_t) * (wgs + 1);
 }
 
+// PSF_MM_REVERSE (A/B knob, tools/): 1 always, 0 never; unset: never
+static bool mm_reverse_mode(double bytes_mm) {
+  static const int mode = [] {
+    const char* e = getenv("PSF_MM_REVERSE");
+    return e && *e ? atoi(e) : 0;
+  }();
+  (void)bytes_mm;
+  return mode == 1;
+}
+
 template <int CAP>
 static int encode_batch_cap(int value_type, int nb, const FfArray* arrs, int count, void* partials,
                             PubSlot* pub_base, hipStream_t st, Profiler* prof) {
@@ -1648,6 +1664,7 @@ static int encode_batch_cap(int value_type, int nb, const FfArray* arrs, int cou
   }
   B.total = enc;
   B.mm_total = mm;
+  B.mm_reverse = mm_reverse_mode(bytes_mm) ? 1u : 0u;
   if (value_type == kFloat) {
     switch (nb) {
       case 1: launch_encode_batch<float, 1, CAP>(B, enc, st, prof, bytes_mm, bytes_enc); break;
