@@ -378,6 +378,55 @@ __device__ __forceinline__ void store_codes(uint8_t* __restrict__ out, size_t g,
   }
 }
 
+// ---- codes written into a stored snappy stream (COMPRESSING next) ----------
+// FfJob::flags bit 2: the job's codes go to the layout of psf_internal.h's
+// StoredLayout -- fragment k's 64 KiB at hdr + 65539 k + 3, its literal tag
+// before it, the varint header first -- so COMPRESSING leaves a stream whose
+// fragments all come out stored where it is (snappy.hip K-place).  A group's
+// code dword(s) land misaligned by (hdr + 3k + 3) mod 4: one unaligned
+// global store (gfx950 runs in unaligned mode: as fast as the aligned stream,
+// tools/ustore_probe.hip), and the lane that stores a fragment's first bytes
+// also writes its tag (and the header).
+constexpr uint32_t kFlagStored = 4u;
+typedef uint32_t __attribute__((aligned(1))) u32_unaligned;
+typedef uint64_t __attribute__((aligned(1))) u64_unaligned;
+
+// the header / tag bytes before fragment k's payload
+__device__ __noinline__ void stored_put_prefix(uint8_t* __restrict__ out, const StoredLayout& L, uint32_t k) {
+  const uint64_t p0 = k ? stored_frag_tag(L, k) : 0, p1 = stored_frag_data(L, k);
+  for (uint64_t P = p0; P < p1; ++P) out[P] = stored_prefix_byte(L, k, P);
+}
+
+// payload byte b (the ragged tail), one thread
+__device__ __forceinline__ void stored_put_byte(uint8_t* __restrict__ out, const StoredLayout& L, uint32_t b,
+                                                uint8_t v) {
+  out[stored_pos(L, b)] = v;
+  if ((b & 65535u) == 0) stored_put_prefix(out, L, b >> 16);
+}
+
+// the 4 * NB code bytes of group g (NB 1 or 2: a group never straddles a fragment)
+template <int NB>
+__device__ __forceinline__ void store_codes_stored(uint8_t* __restrict__ out, const StoredLayout& L, size_t g,
+                                                   uint32_t w0, uint32_t w1) {
+  const uint32_t b = (uint32_t)(g * 4 * NB);
+  uint8_t* p = out + stored_pos(L, b);
+  if (NB == 1) *reinterpret_cast<u32_unaligned*>(p) = w0;
+  else *reinterpret_cast<u64_unaligned*>(p) = (uint64_t)w0 | ((uint64_t)w1 << 32);
+  if (__builtin_expect((b & 65535u) == 0, 0)) stored_put_prefix(out, L, b >> 16);
+}
+template <int NB>
+__device__ __forceinline__ void store_codes_stored(uint8_t* __restrict__ out, const StoredLayout& L, size_t g,
+                                                   const uint64_t r[4]) {
+  if (NB == 1) {
+    const uint32_t w = (uint32_t)(r[0] & 0xFF) | ((uint32_t)(r[1] & 0xFF) << 8) |
+                       ((uint32_t)(r[2] & 0xFF) << 16) | ((uint32_t)(r[3] & 0xFF) << 24);
+    store_codes_stored<1>(out, L, g, w, 0u);
+  } else {
+    store_codes_stored<2>(out, L, g, (uint32_t)(r[0] & 0xFFFF) | ((uint32_t)(r[1] & 0xFFFF) << 16),
+                          (uint32_t)(r[2] & 0xFFFF) | ((uint32_t)(r[3] & 0xFFFF) << 16));
+  }
+}
+
 // The quantiser.  Reference (fixing_float.h:80-82):
 //   tmp = (proj - min_v) / bin * ratio;  r = (uint64)floor(tmp) + boolrand
 // Only floor(tmp) matters, so the f64 division is skipped unless it can change
@@ -524,8 +573,10 @@ __device__ __forceinline__ uint64_t lcg_bit(uint32_t& s) {
 // them, whose t is 0 or within 1e-4 of ratio, inside the band.  Codes <=
 // ratio = 254, so the packed LCG bits add without carries.  A lane that fails
 // redoes its 16 values with the reference's double sequence.
+template <bool kStored = false>
 __device__ __forceinline__ void encode_tile_f32_nb1(const float v[4][4], const QuantParams& q,
-                                                    const uint32_t b4[4], uint32_t* __restrict__ out) {
+                                                    const uint32_t b4[4], uint32_t* __restrict__ out,
+                                                    const StoredLayout* L = nullptr, size_t gs = 0) {
   typedef float f32x2 __attribute__((ext_vector_type(2)));
   const f32x2 mn2 = {q.min_f, q.min_f}, sc2 = {q.scale_f, q.scale_f};
   uint32_t lo = 0x7F800000u, hi = 0u;
@@ -565,16 +616,21 @@ __device__ __forceinline__ void encode_tile_f32_nb1(const float v[4][4], const Q
       }
   }
 #pragma unroll
-  for (int u = 0; u < 4; ++u) out[u * kBlock] = w[u] + ((b4[u] * 0x204081u) & 0x01010101u);
+  for (int u = 0; u < 4; ++u) {
+    const uint32_t c = w[u] + ((b4[u] * 0x204081u) & 0x01010101u);
+    if (kStored) store_codes_stored<1>(reinterpret_cast<uint8_t*>(out), *L, gs + u * kBlock, c, 0u);
+    else out[u * kBlock] = c;
+  }
 }
 
 // One full tile of this lane (groups gb, gb+256, gb+512, gb+768): LCG bits
 // from the cycle table -- group g (elements 4g..4g+3) uses the states
 // s_{4g+1..4g+4} = x_{pos+4g+1..4}, four consecutive table bits (one 8-byte
 // L1/L2-hit load and a funnel shift) -- then quantise, add, pack, store.
-template <typename V, int NB>
+template <typename V, int NB, bool kStored = false>
 __device__ __forceinline__ void encode_full_tile(const V v[4][4], const QuantParams& q, const EncodeParams& p,
-                                                 uint8_t* __restrict__ out, size_t gb, size_t gs) {
+                                                 uint8_t* __restrict__ out, size_t gb, size_t gs,
+                                                 const StoredLayout* L = nullptr) {
   uint32_t b4[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
@@ -583,7 +639,9 @@ __device__ __forceinline__ void encode_full_tile(const V v[4][4], const QuantPar
     b4[u] = __builtin_amdgcn_alignbit(w.y, w.x, k & 31u) & 0xFu;
   }
   if (NB == 1 && sizeof(V) == 4) {
-    encode_tile_f32_nb1(reinterpret_cast<const float(*)[4]>(v), q, b4, reinterpret_cast<uint32_t*>(out) + gs);
+    if (kStored) encode_tile_f32_nb1<true>(reinterpret_cast<const float(*)[4]>(v), q, b4,
+                                           reinterpret_cast<uint32_t*>(out), L, gs);
+    else encode_tile_f32_nb1(reinterpret_cast<const float(*)[4]>(v), q, b4, reinterpret_cast<uint32_t*>(out) + gs);
     return;
   }
   uint32_t fl[4][4];
@@ -593,7 +651,8 @@ __device__ __forceinline__ void encode_full_tile(const V v[4][4], const QuantPar
     uint64_t r[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) r[j] = (uint64_t)(uint32_t)(fl[u][j] + ((b4[u] >> j) & 1u));
-    store_codes<NB>(out, gs + u * kBlock, r);
+    if constexpr (kStored && (NB == 1 || NB == 2)) store_codes_stored<NB>(out, *L, gs + u * kBlock, r);
+    else store_codes<NB>(out, gs + u * kBlock, r);
   }
 }
 
@@ -909,108 +968,6 @@ __device__ __forceinline__ void tile_range_of(size_t ntiles, uint32_t wg, uint32
   t1 = t0 + per < ntiles ? t0 + per : ntiles;
 }
 
-// ---- codes written into a stored snappy stream (COMPRESSING next) ----------
-// FfJob::flags bit 2: the job's codes go to the layout of psf_internal.h's
-// StoredLayout (fragment k's 64 KiB at hdr + 65539 k + 3, tags and the varint
-// header written here too), so COMPRESSING leaves a stream whose fragments
-// all come out stored where it is.  A full tile's codes (4 KiB per tile at
-// nb = 1; a tile never straddles a fragment at nb 1 or 2) are staged in LDS
-// and written as aligned dwords, each composed from two LDS dwords (the
-// stream position is misaligned by hdr + 3k + 3 mod 4).  The dword that
-// straddles two tiles is written whole by the workgroup that processed both
-// (the previous tile's last code dword carried over); at a workgroup's first
-// and last tile, and in the partial tile and the ragged tail, each side
-// writes its own bytes of it with byte stores.
-constexpr uint32_t kFlagStored = 4u;
-
-// bytes of a full tile's codes
-template <int NB>
-constexpr uint32_t tile_code_bytes() { return (uint32_t)kTileGroups * 4u * NB; }
-
-// payload byte b of a stored stream (and, at a fragment's first byte, the
-// fragment's tag and -- fragment 0 -- the header before it), one thread
-__device__ __forceinline__ void stored_put_byte(uint8_t* __restrict__ out, const StoredLayout& L, uint32_t b,
-                                                uint8_t v) {
-  out[stored_pos(L, b)] = v;
-  if ((b & 65535u) == 0) {
-    const uint32_t k = b >> 16;
-    const uint64_t p0 = k ? stored_frag_tag(L, k) : 0, p1 = stored_frag_data(L, k);
-    for (uint64_t P = p0; P < p1; ++P) out[P] = stored_prefix_byte(L, k, P);
-  }
-}
-
-// the NB * 4 code bytes of group g (partial tile, ragged tail)
-template <int NB>
-__device__ __forceinline__ void stored_put_group(uint8_t* __restrict__ out, const StoredLayout& L, size_t g,
-                                                 const uint64_t r[4]) {
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    uint64_t v = r[e];
-#pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      stored_put_byte(out, L, (uint32_t)((size_t)NB * (4 * g + e) + j), (uint8_t)(v & 0xFF));
-      v >>= 8;
-    }
-  }
-}
-
-// tile t's codes (in LDS: `lds`, tile_code_bytes<NB>() bytes) to the stream.
-// carry: the previous tile's last code dword, valid when prev_here (this
-// workgroup processed tile t - 1 just before); next_here: it processes t + 1
-// next (and writes the dword the two share).
-template <int NB>
-__device__ __forceinline__ void stored_tile_out(uint8_t* __restrict__ out, const StoredLayout& L, size_t t,
-                                                const uint32_t* lds, uint32_t carry, bool prev_here,
-                                                bool next_here) {
-  constexpr uint32_t Lt = tile_code_bytes<NB>();
-  const uint32_t b0 = (uint32_t)(t * Lt);
-  const uint32_t k = b0 >> 16;
-  const uint64_t S = stored_pos(L, b0);
-  const bool first = (b0 & 65535u) == 0;
-  const uint64_t P = first ? (k ? stored_frag_tag(L, k) : 0) : S;  // the bytes this tile owns: [P, Q)
-  const uint64_t Q = S + Lt;
-  const uint64_t D0 = P >> 2, D1 = (Q + 3) >> 2;
-  uint32_t* o32 = reinterpret_cast<uint32_t*>(out);
-  for (uint64_t D = D0 + threadIdx.x; D < D1; D += kBlock) {
-    const int64_t c = (int64_t)(4 * D) - (int64_t)S;  // payload offset (in the tile) of the dword's byte 0
-    if (c >= 0 && c + 4 <= (int64_t)Lt) {
-      const uint32_t i = (uint32_t)c >> 2, sh = (uint32_t)c & 3u;
-      o32[D] = sh ? __builtin_amdgcn_alignbyte(lds[i + 1], lds[i], sh) : lds[i];
-      continue;
-    }
-    // an edge dword: header / tag bytes, the neighbour tiles' bytes
-    const bool head = 4 * D < P, tail = 4 * D + 4 > Q;
-    if (tail && next_here) continue;  // the next tile writes it whole
-    const bool whole = !(head && !prev_here) && !tail;
-    uint32_t w = 0, mask = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < 4; ++j) {
-      const uint64_t X = 4 * D + j;
-      uint32_t byte = 0;
-      if (X < P) {
-        if (!prev_here) continue;
-        byte = (carry >> (8 * (4 - (uint32_t)(P - X)))) & 0xFFu;  // the previous tile's last bytes
-      } else if (X >= Q) {
-        continue;
-      } else if (X < S) {
-        byte = stored_prefix_byte(L, k, X);
-      } else {
-        const uint32_t cb = (uint32_t)(X - S);
-        byte = (lds[cb >> 2] >> (8 * (cb & 3u))) & 0xFFu;
-      }
-      w |= byte << (8 * j);
-      mask |= 1u << j;
-    }
-    if (whole) {
-      o32[D] = w;
-    } else {
-#pragma unroll
-      for (uint32_t j = 0; j < 4; ++j)
-        if (mask & (1u << j)) out[4 * D + j] = (uint8_t)(w >> (8 * j));
-    }
-  }
-}
-
 template <typename V, int CAP>
 __global__ __launch_bounds__(kBlock) void ff_minmax_batch(FfBatchT<CAP> B) {
   typedef typename KeyOf<V>::K K;
@@ -1185,18 +1142,10 @@ __global__ __launch_bounds__(kBlock) void ff_encode_batch(FfBatchT<CAP> B) {
   const StoredLayout L = stored_layout((uint32_t)(n * NB));
   if constexpr (NB == 1 || NB == 2) {
     if (stored) {
-      // codes staged per tile in LDS (two buffers: one barrier per tile), then
-      // written to their stream positions (stored_tile_out)
-      __shared__ uint32_t stage[2][tile_code_bytes<NB>() / 4];
-      uint32_t carry = 0;
       for (size_t t = t0; t < tf; ++t) {
         if (t != t0) load_tile(t);
-        uint32_t* buf = stage[(t - t0) & 1];
-        encode_full_tile<V, NB>(v, q, p, reinterpret_cast<uint8_t*>(buf), t * kTileGroups + threadIdx.x,
-                                threadIdx.x);
-        __syncthreads();
-        stored_tile_out<NB>(out, L, t, buf, carry, t > t0, t + 1 < tf);
-        carry = buf[tile_code_bytes<NB>() / 4 - 1];
+        const size_t gb = t * kTileGroups + threadIdx.x;
+        encode_full_tile<V, NB, true>(v, q, p, out, gb, gb, &L);
       }
     }
   }
@@ -1218,8 +1167,12 @@ __global__ __launch_bounds__(kBlock) void ff_encode_batch(FfBatchT<CAP> B) {
         else Vec4<V>::loadu(x + 4 * g, v);
         uint64_t r[4];
         quant_group<V, NB>(v, q, su, p.k17, r);
-        if (stored) stored_put_group<NB>(out, L, g, r);
-        else store_codes<NB>(out, g, r);
+        if constexpr (NB == 1 || NB == 2) {
+          if (stored) store_codes_stored<NB>(out, L, g, r);
+          else store_codes<NB>(out, g, r);
+        } else {
+          store_codes<NB>(out, g, r);
+        }
       }
       su = step17(p.a_lane, p.c_lane, su);
     }
