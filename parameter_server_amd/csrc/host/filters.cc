@@ -260,9 +260,9 @@ void FixingFloatFilter::encode_messages(Context* ctx, std::vector<FfMessage>& ms
       j.stored = ctx->device() >= 0 && (j.nb == 1 || j.nb == 2) && out_bytes[q - base] < (1ull << 32) &&
                  j.in.loc == Loc::kDevice && (reinterpret_cast<uintptr_t>(j.in.ptr) % (j.type == kFloat ? 4 : 8)) == 0 &&
                  compressing_follows(j.msg);
-      // the whole stored stream, and 64 bytes for the compressor's aligned
-      // reads past a fragment's end
-      if (j.stored) out_bytes[q - base] = stored_stream_bytes(stored_layout((uint32_t)out_bytes[q - base])) + 64;
+      // the whole stored stream (64 bytes to spare for the compressor's
+      // aligned reads past a fragment's end) and its probe sheet
+      if (j.stored) out_bytes[q - base] = stored_alloc_bytes(stored_layout((uint32_t)out_bytes[q - base]));
       seeds[q - base] = (uint32_t)ff_clock_seed();  // `int seed = time(NULL)`, per array
     }
     alloc_outputs(ctx, jobs, base, end, out_bytes);
@@ -270,7 +270,7 @@ void FixingFloatFilter::encode_messages(Context* ctx, std::vector<FfMessage>& ms
       FfJob& j = jobs[q];
       if (!j.stored) continue;
       j.out.bytes = j.elems * (size_t)j.nb;  // the payload; COMPRESSING reads it in the stream layout
-      j.out.layout = kLayoutStored;
+      j.out.layout = j.nb == 1 ? kLayoutStored1 : kLayoutStored2;
     }
     std::shared_ptr<RangeBatch> rb;
     float* ring_dev = nullptr;

@@ -155,7 +155,7 @@ void SnappyBatch::launch(size_t b, size_t e) {
     for (size_t i = b; i < e; ++i) {
       Job& j = jobs_[i];
       if (j.compress != comp) continue;
-      if (comp) cj.push_back(SnappyCJob{j.in.ptr, j.in.bytes, j.out.ptr, j.slot, j.ticket, j.in.layout == kLayoutStored});
+      if (comp) cj.push_back(SnappyCJob{j.in.ptr, j.in.bytes, j.out.ptr, j.slot, j.ticket, (uint32_t)j.in.layout});
       else {
         dj.push_back(SnappyDJob{j.in.ptr, j.in.bytes, j.hdr, j.out.bytes, j.out.ptr, j.slot, j.ticket, j.dq});
         di.push_back(i);

@@ -42,25 +42,7 @@ namespace {
 constexpr uint32_t kFrag = 65536;     // snappy kBlockSize
 constexpr uint32_t kMaxTable = 16384;  // kMaxHashTableSize
 constexpr uint32_t kMul = 0x1e35a7bdu;
-constexpr int kSkipN = 6 * 64 + 1;  // a skip loop ends before probe 270
-
-// cum[k]: offset of probe k from the start of a skip loop (skip starts at 32,
-// each probe advances by skip>>5 and then skip += skip>>5).
-struct SkipCum {
-  uint32_t v[kSkipN];
-};
-constexpr SkipCum make_skip() {
-  SkipCum s{};
-  uint32_t skip = 32, cum = 0;
-  for (int k = 0; k < kSkipN; ++k) {
-    s.v[k] = cum;
-    const uint32_t step = skip >> 5;
-    skip += step;
-    cum += step;
-  }
-  return s;
-}
-__constant__ SkipCum kSkip = make_skip();
+__constant__ SkipCum kSkip = make_skip();  // (psf_internal.h)
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
@@ -298,7 +280,7 @@ struct CJob {
   const uint8_t* in;  // the input; a stored job: the StoredLayout stream FIXING_FLOAT wrote
   uint8_t* dst;
   uint64_t n;
-  uint32_t frag0, nfrag, hdr, slot, ticket, stored;
+  uint32_t frag0, nfrag, hdr, slot, ticket, stored;  // stored: the job's FIXING_FLOAT num_bytes (0: plain input)
 };
 struct SnappyCJobs {
   CJob j[kSnappyBatchMax];
@@ -314,6 +296,13 @@ __device__ __forceinline__ const uint8_t* frag_src(const CJob& c, uint32_t k) {
   if (!c.stored) return c.in + (size_t)k * kFrag;
   const StoredLayout L = stored_layout((uint32_t)c.n);
   return c.in + stored_frag_data(L, k);
+}
+// fragment k's probe sheet (psf_internal.h), or null
+__device__ __forceinline__ const uint32_t* frag_sheet(const CJob& c, uint32_t k) {
+  if (!c.stored) return nullptr;
+  const StoredLayout L = stored_layout((uint32_t)c.n);
+  if (!stored_sheet_valid(L, c.stored, k)) return nullptr;
+  return reinterpret_cast<const uint32_t*>(c.in + stored_sheet_offset(L) + (size_t)k * kSheetBytes);
 }
 __device__ __forceinline__ uint32_t cjob_index(const SnappyCJobs& J, uint32_t g) {
   uint32_t i = 0;
@@ -432,17 +421,30 @@ __device__ void copy_bytes(uint8_t* __restrict__ dst, const uint8_t* __restrict_
 // it was, that lane sees the earlier lane's insert; later lanes wait for the
 // next step.  Returns whether the loop ends without a match (one literal).
 __device__ __forceinline__ bool probe_stored(const uint8_t* g, uint32_t len, const uint32_t* skip, uint64_t* m, uint32_t* pv,
-                             uint32_t lane) {
+                             uint32_t lane, const uint32_t* sheet) {
   if (len < 15) return true;
   const uint32_t shift = hash_shift(len), ip_limit = len - 15, ip = 1;
-  // every probe's bytes (probe k is made iff ip + skip[k + 1] <= ip_limit)
+  // every probe's bytes (probe k is made iff ip + skip[k + 1] <= ip_limit):
+  // one row of the fragment's probe sheet when FIXING_FLOAT wrote one, else
+  // gathered from the fragment
   uint32_t pre[kProbeMax / 64];
+  uint32_t v_at0;
+  if (sheet) {
+    const auto sh = gbl<uint32_t>(sheet);
 #pragma unroll
-  for (uint32_t r = 0; r < kProbeMax / 64; ++r) {
-    const uint32_t k = r * 64 + lane;
-    pre[r] = ip + skip[k + 1] <= ip_limit ? gld32(g, ip + skip[k]) : 0;
+    for (uint32_t r = 0; r < kProbeMax / 64; ++r) {
+      const uint32_t k = r * 64 + lane;
+      pre[r] = ip + skip[k + 1] <= ip_limit ? sh[k] : 0;
+    }
+    v_at0 = uni(sh[kSheetAt0]);
+  } else {
+#pragma unroll
+    for (uint32_t r = 0; r < kProbeMax / 64; ++r) {
+      const uint32_t k = r * 64 + lane;
+      pre[r] = ip + skip[k + 1] <= ip_limit ? gld32(g, ip + skip[k]) : 0;
+    }
+    v_at0 = uni(gld32(g, 0));
   }
-  const uint32_t v_at0 = uni(gld32(g, 0));
   for (uint32_t i = lane; i < kMapSlots; i += 64) m[i] = 0;
 #pragma unroll
   for (uint32_t r = 0; r < kProbeMax / 64; ++r) pv[r * 64 + lane] = pre[r];
@@ -813,7 +815,8 @@ __global__ __launch_bounds__(kCThreads) void snappy_parse(const SnappyCJobs J, u
         const CJob& c = cjob_of(J, f);
         const size_t start = (size_t)(f - c.frag0) * kFrag;
         const uint32_t len = (uint32_t)min((size_t)kFrag, c.n - start);
-        need = !probe_stored(frag_src(c, f - c.frag0), len, skip, U.q.map[wave], U.q.val[wave], lane);
+        need = !probe_stored(frag_src(c, f - c.frag0), len, skip, U.q.map[wave], U.q.val[wave], lane,
+                             frag_sheet(c, f - c.frag0));
         if (!need && lane == 0) J.finfo[f] = 0;  // no tags, the final literal from byte 0
         PSF_TRACE_T(f, 4, wave * 64);
       }
@@ -2284,7 +2287,8 @@ int snappy_compress_batch_launch(const SnappyCJob* jobs, int njobs, void* scratc
     for (uint64_t v = q.n; v >= 128; v >>= 7) ++c.hdr;
     c.slot = (uint32_t)q.slot;
     c.ticket = q.ticket;
-    c.stored = q.stored ? 1u : 0u;
+    c.stored = q.stored;
+    if (c.stored > 2) return kErrArg;
     K.nfrag += c.nfrag;
     bytes += (double)q.n;
   }
