@@ -427,7 +427,8 @@ __device__ __forceinline__ void stored_sheet_run(uint8_t* __restrict__ out, cons
                                                  uint32_t w0, uint32_t w1) {
   constexpr int32_t RB = 256 * NB;  // the run's payload bytes
   const uint32_t lane = threadIdx.x & 63;
-  const uint32_t b = (uint32_t)((g - lane) * 4 * NB);
+  // the run's first payload byte: the same in every lane (scalar from here)
+  const uint32_t b = __builtin_amdgcn_readfirstlane((uint32_t)((g - lane) * 4 * NB));
   const uint32_t k = b >> 16, R = b & 65535u;
   uint32_t* sheet = reinterpret_cast<uint32_t*>(out + stored_sheet_offset(L) + (size_t)k * kSheetBytes);
   const uint32_t flen = k == L.last ? L.nbytes - (k << 16) : 65536u;
@@ -1099,7 +1100,9 @@ __global__ __launch_bounds__(kBlock) void ff_minmax_batch(FfBatchT<CAP> B) {
   }
 }
 
-template <typename V, int NB, int CAP>
+// kStored: the instantiation launched when a job of the batch writes a
+// stored stream (its extra registers stay out of the plain one's occupancy)
+template <typename V, int NB, int CAP, bool kStored>
 __global__ __launch_bounds__(kBlock) void ff_encode_batch(FfBatchT<CAP> B) {
   const int jb = batch_job(B, blockIdx.x, false);
   const FfJob& J = B.job[jb];
@@ -1196,9 +1199,9 @@ __global__ __launch_bounds__(kBlock) void ff_encode_batch(FfBatchT<CAP> B) {
   p.k17 = B.k17;
   p.a_lane = B.a_lane;
   p.c_lane = B.c_lane;
-  const bool stored = (NB == 1 || NB == 2) && (J.flags & kFlagStored);
+  const bool stored = kStored && (NB == 1 || NB == 2) && (J.flags & kFlagStored);
   const StoredLayout L = stored_layout((uint32_t)(n * NB));
-  if constexpr (NB == 1 || NB == 2) {
+  if constexpr (kStored && (NB == 1 || NB == 2)) {
     if (stored) {
       for (size_t t = t0; t < tf; ++t) {
         if (t != t0) load_tile(t);
@@ -1225,7 +1228,7 @@ __global__ __launch_bounds__(kBlock) void ff_encode_batch(FfBatchT<CAP> B) {
         else Vec4<V>::loadu(x + 4 * g, v);
         uint64_t r[4];
         quant_group<V, NB>(v, q, su, p.k17, r);
-        if constexpr (NB == 1 || NB == 2) {
+        if constexpr (kStored && (NB == 1 || NB == 2)) {
           if (stored) store_codes_stored<NB>(out, L, g, r, false);  // (no sheet: a partial tile)
           else store_codes<NB>(out, g, r);
         } else {
@@ -1241,7 +1244,7 @@ __global__ __launch_bounds__(kBlock) void ff_encode_batch(FfBatchT<CAP> B) {
     for (size_t i = tail; i < n; ++i) {
       uint64_t r = quant_floor<V, NB>(x[i], q) + lcg_bit(st);
       for (int j = 0; j < NB; ++j) {
-        if (stored) stored_put_byte(out, L, (uint32_t)(i * NB + j), (uint8_t)(r & 0xFF));
+        if (kStored && stored) stored_put_byte(out, L, (uint32_t)(i * NB + j), (uint8_t)(r & 0xFF));
         else out[i * NB + j] = (uint8_t)(r & 0xFF);
         r >>= 8;
       }
@@ -1522,7 +1525,12 @@ static void launch_encode_batch(FfBatchT<CAP>& B, uint32_t enc_total, hipStream_
     hipLaunchKernelGGL((ff_minmax_batch<V, CAP>), dim3(B.mm_total), dim3(kBlock), 0, st, B);
   }
   ProfScope pe(prof, kKEncode, st, bytes_enc);
-  hipLaunchKernelGGL((ff_encode_batch<V, NB, CAP>), dim3(enc_total), dim3(kBlock), 0, st, B);
+  bool stored = false;
+  for (int i = 0; i < B.njobs; ++i) stored |= (B.job[i].flags & kFlagStored) != 0;
+  if (stored && (NB == 1 || NB == 2))
+    hipLaunchKernelGGL((ff_encode_batch<V, NB, CAP, true>), dim3(enc_total), dim3(kBlock), 0, st, B);
+  else
+    hipLaunchKernelGGL((ff_encode_batch<V, NB, CAP, false>), dim3(enc_total), dim3(kBlock), 0, st, B);
 }
 
 static size_t tiles_of(size_t n) { return ((n >> 2) + kTileGroups - 1) / kTileGroups; }
