@@ -392,7 +392,7 @@ typedef uint32_t __attribute__((aligned(1))) u32_unaligned;
 typedef uint64_t __attribute__((aligned(1))) u64_unaligned;
 
 // the header / tag bytes before fragment k's payload
-__device__ __noinline__ void stored_put_prefix(uint8_t* __restrict__ out, const StoredLayout& L, uint32_t k) {
+__device__ __forceinline__ void stored_put_prefix(uint8_t* __restrict__ out, const StoredLayout& L, uint32_t k) {
   const uint64_t p0 = k ? stored_frag_tag(L, k) : 0, p1 = stored_frag_data(L, k);
   for (uint64_t P = p0; P < p1; ++P) out[P] = stored_prefix_byte(L, k, P);
 }

@@ -268,7 +268,7 @@ constexpr SkipCum make_skip() {
 }
 // first[j]: the first probe i whose position 1 + cum[i] is >= 256 j
 struct ProbeFirst {
-  uint16_t v[257];
+  uint32_t v[257];  // (dwords: scalar loads)
 };
 constexpr ProbeFirst make_probe_first() {
   ProbeFirst f{};
@@ -276,7 +276,7 @@ constexpr ProbeFirst make_probe_first() {
   int i = 0;
   for (int j = 0; j <= 256; ++j) {
     while (i < (int)kSheetProbes && 1 + s.v[i] < 256u * (uint32_t)j) ++i;
-    f.v[j] = (uint16_t)i;
+    f.v[j] = (uint32_t)i;
   }
   return f;
 }
