@@ -388,6 +388,7 @@ __device__ __forceinline__ void store_codes(uint8_t* __restrict__ out, size_t g,
 // tools/ustore_probe.hip), and the lane that stores a fragment's first bytes
 // also writes its tag (and the header).
 constexpr uint32_t kFlagStored = 4u;
+constexpr uint32_t kFlagNoSheet = 8u;
 typedef uint32_t __attribute__((aligned(1))) u32_unaligned;
 typedef uint64_t __attribute__((aligned(1))) u64_unaligned;
 
@@ -426,6 +427,7 @@ template <int NB>
 __device__ __forceinline__ void stored_sheet_run(uint8_t* __restrict__ out, const StoredLayout& L, size_t g,
                                                  uint32_t w0, uint32_t w1) {
   constexpr int32_t RB = 256 * NB;  // the run's payload bytes
+  if (L.nosheet) return;  // A/B: no sheet
   const uint32_t lane = threadIdx.x & 63;
   // the run's first payload byte: the same in every lane (scalar from here)
   const uint32_t b = __builtin_amdgcn_readfirstlane((uint32_t)((g - lane) * 4 * NB));
@@ -1203,10 +1205,12 @@ __global__ __launch_bounds__(kBlock) void ff_encode_batch(FfBatchT<CAP> B) {
   const StoredLayout L = stored_layout((uint32_t)(n * NB));
   if constexpr (kStored && (NB == 1 || NB == 2)) {
     if (stored) {
+      StoredLayout Ls = L;
+      Ls.nosheet = (J.flags & kFlagNoSheet) ? 1u : 0u;
       for (size_t t = t0; t < tf; ++t) {
         if (t != t0) load_tile(t);
         const size_t gb = t * kTileGroups + threadIdx.x;
-        encode_full_tile<V, NB, true>(v, q, p, out, gb, gb, &L);
+        encode_full_tile<V, NB, true>(v, q, p, out, gb, gb, &Ls);
       }
     }
   }
@@ -1592,6 +1596,14 @@ size_t ff_batch_partials_bytes(const FfArray* arrs, int count) {
   return 2 * sizeof(uint64_t) * (wgs + 1);
 }
 
+bool stored_sheet_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("PSF_STORED_SHEET");
+    return !(e && *e == '0');
+  }();
+  return on;
+}
+
 // PSF_MM_REVERSE (A/B knob, tools/): 1 always, 0 never; unset: never
 static bool mm_reverse_mode(double bytes_mm) {
   static const int mode = [] {
@@ -1653,7 +1665,7 @@ static int encode_batch_cap(int value_type, int nb, const FfArray* arrs, int cou
     J.flags = (a.preset.has_min ? 1u : 0u) | (a.preset.has_max ? 2u : 0u) | ((uint32_t)(a.slot + 1) << 16);
     if (a.stored) {
       if ((nb != 1 && nb != 2) || (reinterpret_cast<uintptr_t>(a.out) & 3)) return kErrArg;
-      J.flags |= kFlagStored;
+      J.flags |= kFlagStored | (stored_sheet_enabled() ? 0u : kFlagNoSheet);
     }
     J.u.e.seed = a.seed;
     J.u.e.lcg_pos = lcg_cycle().pos[a.seed & kMask17];

@@ -214,13 +214,18 @@ struct StoredLayout {
   uint32_t tl;      // the last fragment's tag bytes
   uint32_t last;    // index of the last fragment
   uint32_t nbytes;  // payload bytes (n < 2^32)
+  uint32_t nosheet; // (A/B knob below: the writer skips the probe sheet)
 };
+// A/B knob (tools/): PSF_STORED_SHEET=0 -- no probe sheet (the compressor's
+// probe gathers from the fragment); read once per process
+bool stored_sheet_enabled();
 __host__ __device__ __forceinline__ StoredLayout stored_layout(uint32_t nbytes) {
   StoredLayout s;
   s.hdr = snappy_varint_len(nbytes);
   s.last = (nbytes - 1) >> 16;
   s.tl = snappy_literal_tag_len(nbytes - (s.last << 16));
   s.nbytes = nbytes;
+  s.nosheet = 0;
   return s;
 }
 // stream bytes of the whole stored stream

@@ -301,7 +301,7 @@ __device__ __forceinline__ const uint8_t* frag_src(const CJob& c, uint32_t k) {
 __device__ __forceinline__ const uint32_t* frag_sheet(const CJob& c, uint32_t k) {
   if (!c.stored) return nullptr;
   const StoredLayout L = stored_layout((uint32_t)c.n);
-  if (!stored_sheet_valid(L, c.stored, k)) return nullptr;
+  if ((c.stored & 0x100u) || !stored_sheet_valid(L, c.stored & 0xFFu, k)) return nullptr;
   return reinterpret_cast<const uint32_t*>(c.in + stored_sheet_offset(L) + (size_t)k * kSheetBytes);
 }
 __device__ __forceinline__ uint32_t cjob_index(const SnappyCJobs& J, uint32_t g) {
@@ -2289,6 +2289,7 @@ int snappy_compress_batch_launch(const SnappyCJob* jobs, int njobs, void* scratc
     c.ticket = q.ticket;
     c.stored = q.stored;
     if (c.stored > 2) return kErrArg;
+    if (c.stored && !stored_sheet_enabled()) c.stored |= 0x100u;  // (A/B knob: no sheet written)
     K.nfrag += c.nfrag;
     bytes += (double)q.n;
   }
