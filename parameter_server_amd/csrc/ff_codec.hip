@@ -388,7 +388,6 @@ __device__ __forceinline__ void store_codes(uint8_t* __restrict__ out, size_t g,
 // tools/ustore_probe.hip), and the lane that stores a fragment's first bytes
 // also writes its tag (and the header).
 constexpr uint32_t kFlagStored = 4u;
-constexpr uint32_t kFlagNoSheet = 8u;
 typedef uint32_t __attribute__((aligned(1))) u32_unaligned;
 typedef uint64_t __attribute__((aligned(1))) u64_unaligned;
 
@@ -415,63 +414,9 @@ __device__ __forceinline__ void store_codes_stored(uint8_t* __restrict__ out, co
   else *reinterpret_cast<u64_unaligned*>(p) = (uint64_t)w0 | ((uint64_t)w1 << 32);
   if (__builtin_expect((b & 65535u) == 0, 0)) stored_put_prefix(out, L, b >> 16);
 }
-__constant__ SkipCum kProbeCum = make_skip();              // (psf_internal.h)
-__constant__ ProbeFirst kProbeFirst = make_probe_first();
-
-// One wave's run of 64 groups of a full tile (lane l: group g = g0 + l, its
-// code dwords w0 (, w1); all lanes active) into its fragment's probe sheet:
-// every probe window [1 + cum[i], + 4) that overlaps the run, its bytes taken
-// from the lanes that hold them (two dword permutes); a window that straddles
-// two runs gets each run's bytes by byte stores.
-template <int NB>
-__device__ __forceinline__ void stored_sheet_run(uint8_t* __restrict__ out, const StoredLayout& L, size_t g,
-                                                 uint32_t w0, uint32_t w1) {
-  constexpr int32_t RB = 256 * NB;  // the run's payload bytes
-  if (L.nosheet) return;  // A/B: no sheet
-  const uint32_t lane = threadIdx.x & 63;
-  // the run's first payload byte: the same in every lane (scalar from here)
-  const uint32_t b = __builtin_amdgcn_readfirstlane((uint32_t)((g - lane) * 4 * NB));
-  const uint32_t k = b >> 16, R = b & 65535u;
-  uint32_t* sheet = reinterpret_cast<uint32_t*>(out + stored_sheet_offset(L) + (size_t)k * kSheetBytes);
-  const uint32_t flen = k == L.last ? L.nbytes - (k << 16) : 65536u;
-  if (R == 0 && lane == 0) sheet[kSheetAt0] = w0;  // the fragment's first 4 bytes
-  const uint32_t ilo = kProbeFirst.v[R ? (R >> 8) - 1 : 0], ihi = kProbeFirst.v[(R + RB) >> 8];
-  for (uint32_t i0 = ilo; i0 < ihi; i0 += 64) {
-    const uint32_t i = i0 + lane;
-    const uint32_t pos = i < ihi ? 1 + kProbeCum.v[i] : R + 4 * RB;
-    const int32_t r0 = (int32_t)pos - (int32_t)R;
-    const int32_t d0 = r0 >> 2;  // floor
-    const int32_t da = d0 < 0 ? 0 : (d0 > 64 * NB - 1 ? 64 * NB - 1 : d0);
-    const int32_t db = d0 + 1 < 0 ? 0 : (d0 + 1 > 64 * NB - 1 ? 64 * NB - 1 : d0 + 1);
-    uint32_t a, c;
-    if (NB == 1) {
-      a = __shfl(w0, da, 64);
-      c = __shfl(w0, db, 64);
-    } else {
-      const uint32_t a0 = __shfl(w0, da >> 1, 64), a1 = __shfl(w1, da >> 1, 64);
-      const uint32_t c0 = __shfl(w0, db >> 1, 64), c1 = __shfl(w1, db >> 1, 64);
-      a = (da & 1) ? a1 : a0;
-      c = (db & 1) ? c1 : c0;
-    }
-    if (i >= ihi || r0 <= -4 || r0 >= RB || pos + 4 > flen) continue;  // no byte here / never probed
-    if (r0 >= 0 && r0 + 4 <= RB) {
-      sheet[i] = __builtin_amdgcn_alignbyte(c, a, (uint32_t)r0 & 3u);
-    } else {
-      uint8_t* wb = reinterpret_cast<uint8_t*>(sheet + i);
-#pragma unroll
-      for (int32_t j = 0; j < 4; ++j) {
-        const int32_t o = r0 + j;
-        if (o < 0 || o >= RB) continue;
-        const uint32_t src = (o >> 2) == d0 ? a : c;
-        wb[j] = (uint8_t)(src >> (8 * (o & 3)));
-      }
-    }
-  }
-}
-
 template <int NB>
 __device__ __forceinline__ void store_codes_stored(uint8_t* __restrict__ out, const StoredLayout& L, size_t g,
-                                                   const uint64_t r[4], bool full_run) {
+                                                   const uint64_t r[4]) {
   uint32_t w0, w1 = 0;
   if (NB == 1) {
     w0 = (uint32_t)(r[0] & 0xFF) | ((uint32_t)(r[1] & 0xFF) << 8) | ((uint32_t)(r[2] & 0xFF) << 16) |
@@ -481,7 +426,6 @@ __device__ __forceinline__ void store_codes_stored(uint8_t* __restrict__ out, co
     w1 = (uint32_t)(r[2] & 0xFFFF) | ((uint32_t)(r[3] & 0xFFFF) << 16);
   }
   store_codes_stored<NB>(out, L, g, w0, w1);
-  if (full_run) stored_sheet_run<NB>(out, L, g, w0, w1);
 }
 
 // The quantiser.  Reference (fixing_float.h:80-82):
@@ -675,12 +619,8 @@ __device__ __forceinline__ void encode_tile_f32_nb1(const float v[4][4], const Q
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const uint32_t c = w[u] + ((b4[u] * 0x204081u) & 0x01010101u);
-    if (kStored) {
-      store_codes_stored<1>(reinterpret_cast<uint8_t*>(out), *L, gs + u * kBlock, c, 0u);
-      stored_sheet_run<1>(reinterpret_cast<uint8_t*>(out), *L, gs + u * kBlock, c, 0u);
-    } else {
-      out[u * kBlock] = c;
-    }
+    if (kStored) store_codes_stored<1>(reinterpret_cast<uint8_t*>(out), *L, gs + u * kBlock, c, 0u);
+    else out[u * kBlock] = c;
   }
 }
 
@@ -712,7 +652,7 @@ __device__ __forceinline__ void encode_full_tile(const V v[4][4], const QuantPar
     uint64_t r[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) r[j] = (uint64_t)(uint32_t)(fl[u][j] + ((b4[u] >> j) & 1u));
-    if constexpr (kStored && (NB == 1 || NB == 2)) store_codes_stored<NB>(out, *L, gs + u * kBlock, r, true);
+    if constexpr (kStored && (NB == 1 || NB == 2)) store_codes_stored<NB>(out, *L, gs + u * kBlock, r);
     else store_codes<NB>(out, gs + u * kBlock, r);
   }
 }
@@ -1205,12 +1145,10 @@ __global__ __launch_bounds__(kBlock) void ff_encode_batch(FfBatchT<CAP> B) {
   const StoredLayout L = stored_layout((uint32_t)(n * NB));
   if constexpr (kStored && (NB == 1 || NB == 2)) {
     if (stored) {
-      StoredLayout Ls = L;
-      Ls.nosheet = (J.flags & kFlagNoSheet) ? 1u : 0u;
       for (size_t t = t0; t < tf; ++t) {
         if (t != t0) load_tile(t);
         const size_t gb = t * kTileGroups + threadIdx.x;
-        encode_full_tile<V, NB, true>(v, q, p, out, gb, gb, &Ls);
+        encode_full_tile<V, NB, true>(v, q, p, out, gb, gb, &L);
       }
     }
   }
@@ -1233,7 +1171,7 @@ __global__ __launch_bounds__(kBlock) void ff_encode_batch(FfBatchT<CAP> B) {
         uint64_t r[4];
         quant_group<V, NB>(v, q, su, p.k17, r);
         if constexpr (kStored && (NB == 1 || NB == 2)) {
-          if (stored) store_codes_stored<NB>(out, L, g, r, false);  // (no sheet: a partial tile)
+          if (stored) store_codes_stored<NB>(out, L, g, r);
           else store_codes<NB>(out, g, r);
         } else {
           store_codes<NB>(out, g, r);
@@ -1596,14 +1534,6 @@ size_t ff_batch_partials_bytes(const FfArray* arrs, int count) {
   return 2 * sizeof(uint64_t) * (wgs + 1);
 }
 
-bool stored_sheet_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("PSF_STORED_SHEET");
-    return !(e && *e == '0');
-  }();
-  return on;
-}
-
 // PSF_MM_REVERSE (A/B knob, tools/): 1 always, 0 never; unset: never
 static bool mm_reverse_mode(double bytes_mm) {
   static const int mode = [] {
@@ -1665,7 +1595,7 @@ static int encode_batch_cap(int value_type, int nb, const FfArray* arrs, int cou
     J.flags = (a.preset.has_min ? 1u : 0u) | (a.preset.has_max ? 2u : 0u) | ((uint32_t)(a.slot + 1) << 16);
     if (a.stored) {
       if ((nb != 1 && nb != 2) || (reinterpret_cast<uintptr_t>(a.out) & 3)) return kErrArg;
-      J.flags |= kFlagStored | (stored_sheet_enabled() ? 0u : kFlagNoSheet);
+      J.flags |= kFlagStored;
     }
     J.u.e.seed = a.seed;
     J.u.e.lcg_pos = lcg_cycle().pos[a.seed & kMask17];

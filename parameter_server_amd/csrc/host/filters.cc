@@ -261,7 +261,7 @@ void FixingFloatFilter::encode_messages(Context* ctx, std::vector<FfMessage>& ms
                  j.in.loc == Loc::kDevice && (reinterpret_cast<uintptr_t>(j.in.ptr) % (j.type == kFloat ? 4 : 8)) == 0 &&
                  compressing_follows(j.msg);
       // the whole stored stream (64 bytes to spare for the compressor's
-      // aligned reads past a fragment's end) and its probe sheet
+      // aligned reads past a fragment's end)
       if (j.stored) out_bytes[q - base] = stored_alloc_bytes(stored_layout((uint32_t)out_bytes[q - base]));
       seeds[q - base] = (uint32_t)ff_clock_seed();  // `int seed = time(NULL)`, per array
     }

@@ -100,8 +100,7 @@ class StableList {
 enum class Loc : int { kHost = 0, kDevice = 1 };
 
 // Buffer::layout: kLayoutStored1 / 2 -- `bytes` payload bytes written into the
-// stored snappy stream layout at ptr, and its probe sheet after it
-// (psf_internal.h StoredLayout), by FIXING_FLOAT with num_bytes 1 / 2: output
+// stored snappy stream layout at ptr (psf_internal.h StoredLayout), by FIXING_FLOAT with num_bytes 1 / 2: output
 // that only COMPRESSING (next in the chain) reads
 enum BufferLayout : uint8_t { kLayoutPlain = 0, kLayoutStored1 = 1, kLayoutStored2 = 2 };
 struct Buffer {

@@ -214,18 +214,13 @@ struct StoredLayout {
   uint32_t tl;      // the last fragment's tag bytes
   uint32_t last;    // index of the last fragment
   uint32_t nbytes;  // payload bytes (n < 2^32)
-  uint32_t nosheet; // (A/B knob below: the writer skips the probe sheet)
 };
-// A/B knob (tools/): PSF_STORED_SHEET=0 -- no probe sheet (the compressor's
-// probe gathers from the fragment); read once per process
-bool stored_sheet_enabled();
 __host__ __device__ __forceinline__ StoredLayout stored_layout(uint32_t nbytes) {
   StoredLayout s;
   s.hdr = snappy_varint_len(nbytes);
   s.last = (nbytes - 1) >> 16;
   s.tl = snappy_literal_tag_len(nbytes - (s.last << 16));
   s.nbytes = nbytes;
-  s.nosheet = 0;
   return s;
 }
 // stream bytes of the whole stored stream
@@ -243,18 +238,7 @@ __host__ __device__ __forceinline__ uint64_t stored_frag_data(const StoredLayout
 __host__ __device__ __forceinline__ uint64_t stored_pos(const StoredLayout& s, uint32_t b) {
   return stored_frag_data(s, b >> 16) + (b & 65535u);
 }
-// The probe sheet of a stored stream: per fragment, the 4 payload bytes at
-// every position snappy 1.1.8's first skip loop probes (1 + kSkip[i], the
-// offsets below) and at 0 -- what the compressor's probe would otherwise
-// gather from 122 of a fragment's 512 cache lines.  FIXING_FLOAT writes it
-// beside the stream while the codes are in its registers; the compressor
-// reads one coalesced row per fragment (snappy.hip probe_stored).  Only
-// fragments whose payload came from full FIXING_FLOAT tiles have one.
-constexpr int kSkipN = 6 * 64 + 1;         // a skip loop from ip = 1 ends before probe 270
-constexpr uint32_t kSheetProbes = 6 * 64;  // probe slots 0..383, then the word at 0
-constexpr uint32_t kSheetAt0 = kSheetProbes;
-constexpr uint32_t kSheetWords = 392;
-constexpr uint32_t kSheetBytes = 4 * kSheetWords;
+constexpr int kSkipN = 6 * 64 + 1;  // a skip loop from ip = 1 ends before probe 270
 // cum[k]: offset of probe k from the start of a skip loop (skip starts at 32,
 // each probe advances by skip>>5 and then skip += skip>>5)
 struct SkipCum {
@@ -271,36 +255,8 @@ constexpr SkipCum make_skip() {
   }
   return s;
 }
-// first[j]: the first probe i whose position 1 + cum[i] is >= 256 j
-struct ProbeFirst {
-  uint32_t v[257];  // (dwords: scalar loads)
-};
-constexpr ProbeFirst make_probe_first() {
-  ProbeFirst f{};
-  const SkipCum s = make_skip();
-  int i = 0;
-  for (int j = 0; j <= 256; ++j) {
-    while (i < (int)kSheetProbes && 1 + s.v[i] < 256u * (uint32_t)j) ++i;
-    f.v[j] = (uint32_t)i;
-  }
-  return f;
-}
-__host__ __device__ __forceinline__ uint64_t stored_sheet_offset(const StoredLayout& s) {
-  return (stored_stream_bytes(s) + 64 + 255) & ~(uint64_t)255;
-}
 __host__ __device__ __forceinline__ uint64_t stored_alloc_bytes(const StoredLayout& s) {
-  return stored_sheet_offset(s) + (uint64_t)(s.last + 1) * kSheetBytes;
-}
-// payload bytes FIXING_FLOAT writes from full tiles of 1024 groups (nb 1, 2):
-// the fragments wholly inside have a probe sheet
-__host__ __device__ __forceinline__ uint32_t stored_sheet_bytes_covered(const StoredLayout& s, uint32_t nb) {
-  const uint32_t groups = s.nbytes / nb / 4;
-  return (groups / 1024u) * 1024u * 4u * nb;
-}
-__host__ __device__ __forceinline__ bool stored_sheet_valid(const StoredLayout& s, uint32_t nb, uint32_t k) {
-  const uint32_t cov = stored_sheet_bytes_covered(s, nb);
-  const uint64_t end = k == s.last ? (uint64_t)s.nbytes : ((uint64_t)k + 1) << 16;
-  return end <= cov;
+  return stored_stream_bytes(s) + 64;  // the compressor's aligned reads past a fragment's end
 }
 
 // the stream byte at P, a header / tag byte before fragment k's data
@@ -331,10 +287,10 @@ struct SnappyCJob {
   void* out;  // snappy_max_compressed(n) bytes
   int slot;
   uint32_t ticket;
-  // nonzero: `in` is a StoredLayout stream of n payload bytes that FIXING_FLOAT
-  // wrote with num_bytes = stored (and its probe sheet after it): when every
-  // fragment comes out stored the stream is left where it is and published
-  // with pub->pad = kStoredInPlace (out untouched); else out as usual
+  // nonzero: `in` is a StoredLayout stream of n payload bytes (FIXING_FLOAT
+  // wrote it): when every fragment comes out stored the stream is left where
+  // it is and published with pub->pad = kStoredInPlace (out untouched); else
+  // out as usual
   uint32_t stored = 0;
 };
 constexpr uint32_t kStoredInPlace = 1;

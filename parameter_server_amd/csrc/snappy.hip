@@ -280,7 +280,7 @@ struct CJob {
   const uint8_t* in;  // the input; a stored job: the StoredLayout stream FIXING_FLOAT wrote
   uint8_t* dst;
   uint64_t n;
-  uint32_t frag0, nfrag, hdr, slot, ticket, stored;  // stored: the job's FIXING_FLOAT num_bytes (0: plain input)
+  uint32_t frag0, nfrag, hdr, slot, ticket, stored;  // stored: `in` is a StoredLayout stream
 };
 struct SnappyCJobs {
   CJob j[kSnappyBatchMax];
@@ -296,13 +296,6 @@ __device__ __forceinline__ const uint8_t* frag_src(const CJob& c, uint32_t k) {
   if (!c.stored) return c.in + (size_t)k * kFrag;
   const StoredLayout L = stored_layout((uint32_t)c.n);
   return c.in + stored_frag_data(L, k);
-}
-// fragment k's probe sheet (psf_internal.h), or null
-__device__ __forceinline__ const uint32_t* frag_sheet(const CJob& c, uint32_t k) {
-  if (!c.stored) return nullptr;
-  const StoredLayout L = stored_layout((uint32_t)c.n);
-  if ((c.stored & 0x100u) || !stored_sheet_valid(L, c.stored & 0xFFu, k)) return nullptr;
-  return reinterpret_cast<const uint32_t*>(c.in + stored_sheet_offset(L) + (size_t)k * kSheetBytes);
 }
 __device__ __forceinline__ uint32_t cjob_index(const SnappyCJobs& J, uint32_t g) {
   uint32_t i = 0;
@@ -421,30 +414,17 @@ __device__ void copy_bytes(uint8_t* __restrict__ dst, const uint8_t* __restrict_
 // it was, that lane sees the earlier lane's insert; later lanes wait for the
 // next step.  Returns whether the loop ends without a match (one literal).
 __device__ __forceinline__ bool probe_stored(const uint8_t* g, uint32_t len, const uint32_t* skip, uint64_t* m, uint32_t* pv,
-                             uint32_t lane, const uint32_t* sheet) {
+                             uint32_t lane) {
   if (len < 15) return true;
   const uint32_t shift = hash_shift(len), ip_limit = len - 15, ip = 1;
-  // every probe's bytes (probe k is made iff ip + skip[k + 1] <= ip_limit):
-  // one row of the fragment's probe sheet when FIXING_FLOAT wrote one, else
-  // gathered from the fragment
+  // every probe's bytes (probe k is made iff ip + skip[k + 1] <= ip_limit)
   uint32_t pre[kProbeMax / 64];
-  uint32_t v_at0;
-  if (sheet) {
-    const auto sh = gbl<uint32_t>(sheet);
 #pragma unroll
-    for (uint32_t r = 0; r < kProbeMax / 64; ++r) {
-      const uint32_t k = r * 64 + lane;
-      pre[r] = ip + skip[k + 1] <= ip_limit ? sh[k] : 0;
-    }
-    v_at0 = uni(sh[kSheetAt0]);
-  } else {
-#pragma unroll
-    for (uint32_t r = 0; r < kProbeMax / 64; ++r) {
-      const uint32_t k = r * 64 + lane;
-      pre[r] = ip + skip[k + 1] <= ip_limit ? gld32(g, ip + skip[k]) : 0;
-    }
-    v_at0 = uni(gld32(g, 0));
+  for (uint32_t r = 0; r < kProbeMax / 64; ++r) {
+    const uint32_t k = r * 64 + lane;
+    pre[r] = ip + skip[k + 1] <= ip_limit ? gld32(g, ip + skip[k]) : 0;
   }
+  const uint32_t v_at0 = uni(gld32(g, 0));
   for (uint32_t i = lane; i < kMapSlots; i += 64) m[i] = 0;
 #pragma unroll
   for (uint32_t r = 0; r < kProbeMax / 64; ++r) pv[r * 64 + lane] = pre[r];
@@ -815,8 +795,7 @@ __global__ __launch_bounds__(kCThreads) void snappy_parse(const SnappyCJobs J, u
         const CJob& c = cjob_of(J, f);
         const size_t start = (size_t)(f - c.frag0) * kFrag;
         const uint32_t len = (uint32_t)min((size_t)kFrag, c.n - start);
-        need = !probe_stored(frag_src(c, f - c.frag0), len, skip, U.q.map[wave], U.q.val[wave], lane,
-                             frag_sheet(c, f - c.frag0));
+        need = !probe_stored(frag_src(c, f - c.frag0), len, skip, U.q.map[wave], U.q.val[wave], lane);
         if (!need && lane == 0) J.finfo[f] = 0;  // no tags, the final literal from byte 0
         PSF_TRACE_T(f, 4, wave * 64);
       }
@@ -2287,9 +2266,7 @@ int snappy_compress_batch_launch(const SnappyCJob* jobs, int njobs, void* scratc
     for (uint64_t v = q.n; v >= 128; v >>= 7) ++c.hdr;
     c.slot = (uint32_t)q.slot;
     c.ticket = q.ticket;
-    c.stored = q.stored;
-    if (c.stored > 2) return kErrArg;
-    if (c.stored && !stored_sheet_enabled()) c.stored |= 0x100u;  // (A/B knob: no sheet written)
+    c.stored = q.stored ? 1u : 0u;
     K.nfrag += c.nfrag;
     bytes += (double)q.n;
   }

@@ -112,72 +112,3 @@ def test_stored_layout_streams_vs_port(ctx, port, batched):
             assert rcv.value(w, 0).cpu().numpy().tobytes() == dec, c
     finally:
         F.set_clock(None)
-
-
-def _skip_cum(n=384):
-    v, skip, cum = [], 32, 0
-    for _ in range(n):
-        v.append(cum)
-        step = skip >> 5
-        skip += step
-        cum += step
-    return v
-
-
-def _varint_len(v):
-    n = 1
-    while v >= 128:
-        v >>= 7
-        n += 1
-    return n
-
-
-def _tag_len(m):  # EmitLiteral's tag bytes for a literal of m bytes
-    m -= 1
-    return 1 if m < 60 else 2 if m < 256 else 3 if m < 65536 else 4
-
-
-@pytest.mark.parametrize("n,nb", [(12 * 65536 + 4096 * 3, 1), (20 * 65536, 1), (9 * 32768 + 5000, 2)])
-def test_probe_sheet_rows(ctx, port, n, nb):
-    """The probe sheet FIXING_FLOAT writes beside the stored stream
-    (psf_internal.h): per fragment wholly written by full tiles, the 4 code
-    bytes at every position 1.1.8's first skip loop probes (1 + cum[i]) and at
-    0 -- what the compressor's probe reads instead of gathering them from the
-    fragment.  Read back past the stream (the compressor left the stream in
-    place: every fragment of random codes is stored)."""
-    from parameter_server_amd import filter as F
-    F.set_clock(SEED)
-    try:
-        x = np.random.default_rng(n).standard_normal(n).astype(np.float32)
-        m = _msg(F, x, nb)
-        F.RemoteNode(ctx).encode(m)
-        ctx.sync()
-        st, codes, mn, mx = port.ff_encode(x, nb, SEED)
-        nbytes = codes.size
-        vp, vn, vl = m.value_ptr(0)
-        assert vn == len(port.snappy_compress(codes.tobytes()))
-        last = (nbytes - 1) >> 16
-        stream = _varint_len(nbytes) + last * 65539 + _tag_len(nbytes - (last << 16)) + nbytes - (last << 16)
-        sheet_off = (stream + 64 + 255) // 256 * 256
-        nfrag = last + 1
-        raw = F.copy_out(vp, sheet_off + nfrag * 1568, vl, "cuda:0").cpu().numpy()
-        covered = (nbytes // nb // 4 // 1024) * 1024 * 4 * nb
-        cum = _skip_cum()
-        checked = 0
-        for k in range(nfrag):
-            end = nbytes if k == last else (k + 1) << 16
-            if end > covered:
-                continue
-            flen = end - (k << 16)
-            row = raw[sheet_off + k * 1568: sheet_off + (k + 1) * 1568].view(np.uint32)
-            frag = codes[k << 16: end]
-            assert row[384] == frag[:4].view(np.uint32)[0], k
-            for i, c in enumerate(cum):
-                pos = 1 + c
-                if pos + 4 > flen:
-                    break
-                assert row[i] == frag[pos:pos + 4].copy().view(np.uint32)[0], (k, i, pos)
-                checked += 1
-        assert checked > 200
-    finally:
-        F.set_clock(None)
