@@ -385,8 +385,8 @@ __device__ __forceinline__ void store_codes(uint8_t* __restrict__ out, size_t g,
 // fragments all come out stored where it is (snappy.hip K-place).  A group's
 // code dword(s) land misaligned by (hdr + 3k + 3) mod 4: one unaligned
 // global store (gfx950 runs in unaligned mode: as fast as the aligned stream,
-// tools/ustore_probe.hip), and the lane that stores a fragment's first bytes
-// also writes its tag (and the header).
+// tools/ustore_probe.hip); the tags and the header are constants, written by
+// the job's first workgroup while it encodes.
 constexpr uint32_t kFlagStored = 4u;
 typedef uint32_t __attribute__((aligned(1))) u32_unaligned;
 typedef uint64_t __attribute__((aligned(1))) u64_unaligned;
@@ -401,7 +401,6 @@ __device__ __forceinline__ void stored_put_prefix(uint8_t* __restrict__ out, con
 __device__ __forceinline__ void stored_put_byte(uint8_t* __restrict__ out, const StoredLayout& L, uint32_t b,
                                                 uint8_t v) {
   out[stored_pos(L, b)] = v;
-  if ((b & 65535u) == 0) stored_put_prefix(out, L, b >> 16);
 }
 
 // the 4 * NB code bytes of group g (NB 1 or 2: a group never straddles a fragment)
@@ -412,7 +411,6 @@ __device__ __forceinline__ void store_codes_stored(uint8_t* __restrict__ out, co
   uint8_t* p = out + stored_pos(L, b);
   if (NB == 1) *reinterpret_cast<u32_unaligned*>(p) = w0;
   else *reinterpret_cast<u64_unaligned*>(p) = (uint64_t)w0 | ((uint64_t)w1 << 32);
-  if (__builtin_expect((b & 65535u) == 0, 0)) stored_put_prefix(out, L, b >> 16);
 }
 template <int NB>
 __device__ __forceinline__ void store_codes_stored(uint8_t* __restrict__ out, const StoredLayout& L, size_t g,
@@ -1145,6 +1143,8 @@ __global__ __launch_bounds__(kBlock) void ff_encode_batch(FfBatchT<CAP> B) {
   const StoredLayout L = stored_layout((uint32_t)(n * NB));
   if constexpr (kStored && (NB == 1 || NB == 2)) {
     if (stored) {
+      if (wg == 0)  // every fragment's tag, and the header
+        for (uint32_t k = threadIdx.x; k <= L.last; k += kBlock) stored_put_prefix(out, L, k);
       for (size_t t = t0; t < tf; ++t) {
         if (t != t0) load_tile(t);
         const size_t gb = t * kTileGroups + threadIdx.x;
