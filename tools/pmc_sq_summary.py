@@ -25,7 +25,7 @@ def main():
             k = r["Kernel_Name"]
             if "psf::" not in k:
                 continue
-            name = k.split("(")[0].split("::")[-1]
+            name = k.replace("(anonymous namespace)::", "").split("(")[0].split("::")[-1]
             tot[name][r["Counter_Name"]] += float(r["Counter_Value"])
             disp[name].add((path, r.get("Dispatch_Id")))
     out = {}
