@@ -160,6 +160,16 @@ size_t psf_snappy_max_compressed_length(size_t n);
  * bytes; *out_len = stream length.  Synchronous.  n < 2^32. */
 int psf_snappy_compress(psf_context* ctx, const void* d_in, size_t n, void* d_out, size_t* out_len);
 /* snappy::GetUncompressedLength: PSF_ERR_CHECK when the header is malformed. */
+/* COMPRESSING of a stream already in the stored layout -- varint32(n), then
+ * per 64 KiB fragment snappy's literal tag and the fragment's bytes, what
+ * 1.1.8 writes for data without matches (FIXING_FLOAT writes its codes so
+ * when COMPRESSING follows it): compressed where it is, byte-identical to
+ * RawCompress of the n payload bytes; *out_len = the stream's length.  The
+ * buffer holds cap >= psf_snappy_stored_capacity(n) bytes (the stream can
+ * grow: a short match may cost more than the literal it replaces).
+ * Synchronous. */
+int psf_snappy_compress_stored(psf_context* ctx, void* d_buf, size_t n, size_t cap, size_t* out_len);
+size_t psf_snappy_stored_capacity(size_t n);
 int psf_snappy_uncompressed_length(psf_context* ctx, const void* d_in, size_t n, size_t* out_len);
 /* snappy::RawUncompress into d_out (out_cap >= the declared length, else
  * PSF_ERR_ARG); PSF_ERR_CHECK when RawUncompress would return false. */

@@ -65,6 +65,8 @@ SIGNATURES = {
     "psf_snappy_max_compressed_length": ([sz], sz),
     "psf_snappy_compress": ([vp, vp, sz, vp, C.POINTER(sz)], C.c_int),
     "psf_snappy_uncompressed_length": ([vp, vp, sz, C.POINTER(sz)], C.c_int),
+    "psf_snappy_compress_stored": ([vp, vp, sz, sz, C.POINTER(sz)], C.c_int),
+    "psf_snappy_stored_capacity": ([sz], sz),
     "psf_snappy_uncompress": ([vp, vp, sz, vp, sz, C.POINTER(sz)], C.c_int),
     "psf_node_create": ([vp, C.POINTER(vp)], C.c_int),
     "psf_node_destroy": ([vp], C.c_int),

@@ -269,6 +269,34 @@ int psf_snappy_compress(psf_context* ctx, const void* d_in, size_t n, void* d_ou
   });
 }
 
+// A stored-layout stream (psf_internal.h StoredLayout: what FIXING_FLOAT
+// writes when COMPRESSING follows) compressed where it is.
+int psf_snappy_compress_stored(psf_context* ctx, void* d_buf, size_t n, size_t cap, size_t* out_len) {
+  return guarded(ctx ? ctx->impl : nullptr, [&] {
+    if (!ctx || !d_buf || !out_len || n == 0 || n > 0xffffffffull) return PSF_ERR_ARG;
+    psf::Context& c = *ctx->impl;
+    if (c.device() < 0) return PSF_ERR_ARG;
+    if (cap < psf::stored_alloc_bytes(psf::stored_layout((uint32_t)n))) return PSF_ERR_ARG;
+    psf::Buffer src;
+    src.ptr = static_cast<uint8_t*>(d_buf);
+    src.bytes = n;
+    src.loc = psf::Loc::kDevice;
+    src.layout = psf::kLayoutStored1;
+    psf::Buffer out;
+    psf::SnappyBatch b(c);
+    b.compress(src, &out);
+    b.flush();
+    c.sync();
+    if (out.ptr != src.ptr) throw psf::CheckError(PSF_ERR_CHECK, "stored stream not compressed in place");
+    *out_len = out.bytes;
+    return PSF_OK;
+  });
+}
+
+size_t psf_snappy_stored_capacity(size_t n) {
+  return n && n <= 0xffffffffull ? (size_t)psf::stored_alloc_bytes(psf::stored_layout((uint32_t)n)) : 0;
+}
+
 static psf::Buffer device_view(const void* p, size_t n) {
   psf::Buffer b;
   b.ptr = static_cast<uint8_t*>(const_cast<void*>(p));

@@ -987,21 +987,23 @@ __global__ __launch_bounds__(kPlaceT) void snappy_place(const SnappyCJobs J, con
 // ---- stored jobs: the stream is compacted where FIXING_FLOAT wrote it.
 // Fragments before the first one with tags (k0) are in place, header and
 // tags included (and with no such fragment the whole stream is: the common
-// case, FIXING_FLOAT codes); fragment k >= k0 moves down to its offset D_k
-// (<= its stored position).  Fragment k's write [D_k, D_k+1) can only reach
-// into the final literal of fragment k - 1 (and earlier ones), never past
-// it, so:
-//   K-save          every fragment k >= k0 copies the part of its final
-//                   literal at or after D_k+1 (what later fragments will
-//                   overwrite) aside; it also settles D_k (inline sum, or
-//                   K-scan's) and publishes the stream length;
-//   K-place-stored  fragment k >= k0 reads its literal (the saved part from
+// case, FIXING_FLOAT codes); fragment k >= k0 moves to its offset D_k, down
+// when the fragments with tags came out shorter than a literal, up when
+// longer (a 1.1.8 parse can lose a few bytes to a short match; the buffer
+// holds snappy_max_compressed(n)).  Fragment k alone writes [D_k, D_k+1), so
+// the bytes of its final literal outside that range are the ones other
+// fragments can overwrite:
+//   K-save          every fragment k >= k0 copies those bytes aside; it also
+//                   settles D_k (inline sum, or K-scan's) and publishes the
+//                   stream length;
+//   K-place-stored  fragment k >= k0 reads its literal (the saved bytes from
 //                   aside) into LDS, then writes its tags and literal at D_k.
 // No workgroup waits for another.
-__device__ __forceinline__ uint64_t stored_frag_offset(const SnappyCJobs& J, const CJob& c, uint32_t k, uint32_t tid,
-                                                       uint64_t* s_part, uint32_t* s_first, uint32_t* first_out) {
+__device__ __forceinline__ uint64_t stored_frag_offset(const SnappyCJobs& J, const CJob& c, uint32_t ji, uint32_t k,
+                                                       uint32_t tid, uint64_t* s_part, uint32_t* s_first,
+                                                       uint32_t* first_out) {
   if (J.scanned) {
-    *first_out = J.k0[&c - J.j];
+    *first_out = J.k0[ji];
     return J.offset[c.frag0 + k];
   }
   uint64_t part = 0;
@@ -1035,17 +1037,18 @@ __global__ __launch_bounds__(kPlaceT) void snappy_save(const SnappyCJobs J) {
   __shared__ uint64_t s_part[kPlaceT / 64];
   __shared__ uint32_t s_first[kPlaceT / 64];
   const uint32_t f = blockIdx.x, tid = threadIdx.x;
-  const CJob& c = cjob_of(J, f);
+  const uint32_t ji = cjob_index(J, f);  // (an index: a pointer into J would copy J to scratch)
+  const CJob& c = J.j[ji];
   if (!c.stored) return;
   const uint32_t k = f - c.frag0;
   const uint32_t len = (uint32_t)min((size_t)kFrag, c.n - (size_t)k * kFrag);
   const uint64_t info = J.finfo[f];
   uint32_t k0;
-  const uint64_t off = stored_frag_offset(J, c, k, tid, s_part, s_first, &k0);
+  const uint64_t off = stored_frag_offset(J, c, ji, k, tid, s_part, s_first, &k0);
   const uint64_t next = off + frag_len(info, len);  // D_k+1
   if (!J.scanned) {
     if (tid == 0) J.offset[f] = off;
-    if (k == 0 && tid == 0) J.k0[&c - J.j] = k0;
+    if (k == 0 && tid == 0) J.k0[ji] = k0;
     if (k + 1 == c.nfrag && tid == 0 && J.pub) {
       PubSlot* pub = J.pub + c.slot;
       pub->size = next;
@@ -1054,15 +1057,21 @@ __global__ __launch_bounds__(kPlaceT) void snappy_save(const SnappyCJobs J) {
       publish_ticket(pub, c.ticket);
     }
   }
-  if (k < k0 || k + 1 == c.nfrag) return;  // in place / nothing after it writes here
+  if (k < k0) return;  // in place
   const uint32_t ne = (uint32_t)info;
   if (ne >= len) return;
   const StoredLayout L = stored_layout((uint32_t)c.n);
   const uint64_t lit = stored_frag_data(L, k) + ne;  // the final literal's bytes in the stream
   const uint64_t end = stored_frag_data(L, k) + len;
+  uint8_t* slot = J.saved + (size_t)f * (kFrag + 64);
+  // what the other fragments' writes can reach: before D_k (fragment k - 1's,
+  // when the stream grew) and from D_k+1 on (the later ones')
+  if (off > lit) {
+    const uint64_t e = off < end ? off : end;
+    copy_bytes<kPlaceT>(slot, c.in + lit, (uint32_t)(e - lit), tid);
+  }
   const uint64_t cut = next > lit ? next : lit;
-  if (cut >= end) return;
-  copy_bytes<kPlaceT>(J.saved + (size_t)f * (kFrag + 64) + (cut - lit), c.in + cut, (uint32_t)(end - cut), tid);
+  if (cut < end) copy_bytes<kPlaceT>(slot + (cut - lit), c.in + cut, (uint32_t)(end - cut), tid);
 }
 
 // dst[0, n) = LDS s[0, n) (s 16-byte aligned, 16 bytes readable past n),
@@ -1088,10 +1097,11 @@ __device__ __forceinline__ void lds_to_global(uint8_t* __restrict__ dst, const u
 __global__ __launch_bounds__(kPlaceT) void snappy_place_stored(const SnappyCJobs J, const uint8_t* __restrict__ scratch) {
   __shared__ uint32_t s_lit[(kFrag + 64) / 4];
   const uint32_t f = blockIdx.x, tid = threadIdx.x;
-  const CJob& c = cjob_of(J, f);
+  const uint32_t ji = cjob_index(J, f);
+  const CJob& c = J.j[ji];
   if (!c.stored) return;
   const uint32_t k = f - c.frag0;
-  const uint32_t k0 = J.k0[&c - J.j];
+  const uint32_t k0 = J.k0[ji];
   if (k < k0) return;  // in place
   const uint32_t len = (uint32_t)min((size_t)kFrag, c.n - (size_t)k * kFrag);
   const uint64_t info = J.finfo[f];
@@ -1102,10 +1112,11 @@ __global__ __launch_bounds__(kPlaceT) void snappy_place_stored(const SnappyCJobs
   const StoredLayout L = stored_layout((uint32_t)c.n);
   const uint32_t n = len - ne;  // the final literal
   if (n) {
-    // the literal into LDS: bytes before D_k+1 from the stream (nothing
-    // overwrites them), the rest from K-save's copy
+    // the literal into LDS: bytes in [D_k, D_k+1) from the stream (only this
+    // workgroup writes there, after this), the rest from K-save's copy
     const uint64_t lit = stored_frag_data(L, k) + ne;
-    const uint32_t na = k + 1 == c.nfrag ? n : (uint32_t)(next > lit ? min<uint64_t>(next - lit, n) : 0);
+    const uint32_t nz = off > lit ? (uint32_t)min<uint64_t>(off - lit, n) : 0;  // [0, nz): saved
+    const uint32_t na = (uint32_t)(next > lit ? min<uint64_t>(next - lit, n) : 0);  // [na, n): saved
     const uint8_t* sv = J.saved + (size_t)f * (kFrag + 64);
     typedef uint32_t V4 __attribute__((ext_vector_type(4)));
     const uintptr_t a = reinterpret_cast<uintptr_t>(out + lit);
@@ -1115,16 +1126,34 @@ __global__ __launch_bounds__(kPlaceT) void snappy_place_stored(const SnappyCJobs
     uint4* l16 = reinterpret_cast<uint4*>(s_lit);
     uint8_t* lb = reinterpret_cast<uint8_t*>(s_lit);
     const uint32_t nb = (n + 15) >> 4;
-    for (uint32_t b = tid; b < nb; b += kPlaceT) {
-      const uint32_t o = 16 * b;
-      if (o + 16 <= na) {
-        const V4 lo = s16[b], hi = s16[b + 1];
-        l16[b] = funnel16(make_uint4(lo[0], lo[1], lo[2], lo[3]), make_uint4(hi[0], hi[1], hi[2], hi[3]), sh);
-      } else if (o >= na) {
-        const V4 x = v16[b];
-        l16[b] = make_uint4(x[0], x[1], x[2], x[3]);
-      } else {  // the block that holds the cut
-        for (uint32_t i = o; i < o + 16 && i < n; ++i) lb[i] = i < na ? out[lit + i] : sv[i];
+    // a round's loads are all issued before its LDS stores (8 blocks per
+    // lane in flight, not one memory latency per block)
+    constexpr uint32_t U = 8;
+    for (uint32_t b0 = 0; b0 < nb; b0 += U * kPlaceT) {
+      V4 lo[U], hi[U];
+#pragma unroll
+      for (uint32_t u = 0; u < U; ++u) {
+        const uint32_t b = b0 + u * kPlaceT + tid, o = 16 * b;
+        if (b >= nb) continue;
+        if (o >= nz && o + 16 <= na) {
+          lo[u] = s16[b];
+          hi[u] = s16[b + 1];
+        } else if (o >= na || o + 16 <= nz) {
+          lo[u] = v16[b];
+        }
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < U; ++u) {
+        const uint32_t b = b0 + u * kPlaceT + tid, o = 16 * b;
+        if (b >= nb) continue;
+        if (o >= nz && o + 16 <= na) {
+          l16[b] = funnel16(make_uint4(lo[u][0], lo[u][1], lo[u][2], lo[u][3]),
+                            make_uint4(hi[u][0], hi[u][1], hi[u][2], hi[u][3]), sh);
+        } else if (o >= na || o + 16 <= nz) {
+          l16[b] = make_uint4(lo[u][0], lo[u][1], lo[u][2], lo[u][3]);
+        } else {  // a block that holds a cut
+          for (uint32_t i = o; i < o + 16 && i < n; ++i) lb[i] = (i >= nz && i < na) ? out[lit + i] : sv[i];
+        }
       }
     }
   }

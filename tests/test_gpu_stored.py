@@ -30,6 +30,11 @@ def _values(kind, n, dt, seed, nb):
     elif kind == "allcomp":
         x[:] = 1.0
         x[::7] = -1.0  # (a range: bin > 0)
+    elif kind == "firstcomp":  # fragment 0 shrinks to a few bytes: every later one moves ~64 KiB down
+        x[:per] = 0.0
+    elif kind == "everyother":  # every other fragment compressible
+        for f in range(0, n // per + 1, 2):
+            x[f * per:(f + 1) * per] = 0.75
     return x
 
 
@@ -64,6 +69,10 @@ CASES = [  # kind, n values, nb, dtype
     ("onecomp", 9 * 32768 + 7, 2, np.float32),
     ("lastcomp", 6 * 65536 + 5000, 1, np.float32),
     ("allcomp", 4 * 65536 + 17, 1, np.float32),
+    ("firstcomp", 10 * 65536 + 99, 1, np.float32),
+    ("firstcomp", 6 * 32768 + 3, 2, np.float32),
+    ("everyother", 9 * 65536 + 1234, 1, np.float32),
+    ("everyother", 5 * 32768, 2, F64),
 ]
 
 
@@ -112,3 +121,104 @@ def test_stored_layout_streams_vs_port(ctx, port, batched):
             assert rcv.value(w, 0).cpu().numpy().tobytes() == dec, c
     finally:
         F.set_clock(None)
+
+
+def test_stored_layout_long_stream_scan_path(ctx, port):
+    """A stream of 4100 fragments (more than kInlineScan: offsets from the
+    per-stream scan launch) with compressible fragments at 1000 and 3000:
+    compacted in place, byte-identical to 1.1.8's stream."""
+    from parameter_server_amd import filter as F
+    F.set_clock(SEED)
+    try:
+        n = 4100 * 65536 + 77
+        x = np.random.default_rng(9).standard_normal(n).astype(np.float32)
+        x[1000 * 65536:1001 * 65536] = 0.5
+        x[3000 * 65536 + 100:3000 * 65536 + 40000] = -0.25
+        m = _msg(F, x, 1)
+        F.RemoteNode(ctx).encode(m)
+        ctx.sync()
+        stream, _ = _want(port, x, 1)
+        vp, vn, vl = m.value_ptr(0)
+        got = F.copy_out(vp, vn, vl, "cuda:0").cpu().numpy().tobytes()
+        assert got == stream, (len(got), len(stream))
+    finally:
+        F.set_clock(None)
+
+
+def _skip_cum(n=384):
+    """offset of the skip loop's probe k from where it starts (1.1.8: skip
+    starts at 32, each probe advances by skip >> 5, then skip += skip >> 5)"""
+    v, skip, cum = [], 32, 0
+    for _ in range(n):
+        v.append(cum)
+        step = skip >> 5
+        skip += step
+        cum += step
+    return v
+
+
+def _stored_layout(payload):
+    """varint(n) + per 64 KiB fragment: literal tag + bytes (1.1.8's stream of
+    data without matches)"""
+    n = len(payload)
+    out = bytearray()
+    v = n
+    while v >= 128:
+        out.append((v & 127) | 128)
+        v >>= 7
+    out.append(v)
+    for k in range(0, n, 65536):
+        frag = payload[k:k + 65536]
+        m = len(frag) - 1
+        if m < 60:
+            out.append(m << 2)
+        elif m < 256:
+            out += bytes([60 << 2, m])
+        else:
+            out += bytes([61 << 2, m & 255, m >> 8])
+        out += frag
+    return bytes(out)
+
+
+def _planted(nfrag, plant, seed, tail=0, zeros=()):
+    """random bytes; in fragment k of `plant` the 4 bytes at the skip loop's
+    probe 150 copy those at probe 10 (one 4-byte match, far: the fragment
+    comes out 2 bytes longer than a literal); fragments in `zeros` zero"""
+    cum = _skip_cum()
+    b = np.random.default_rng(seed).integers(0, 256, nfrag * 65536 + tail, dtype=np.uint8)
+    for k in plant:
+        p, q = k * 65536 + 1 + cum[10], k * 65536 + 1 + cum[150]
+        b[q:q + 4] = b[p:p + 4]
+        b[q + 4] = b[p + 4] ^ 0x5A
+    for k in zeros:
+        b[k * 65536:(k + 1) * 65536] = 0
+    return b.tobytes()
+
+
+@pytest.mark.parametrize("case", ["grow", "grow_every", "shrink_then_grow", "grow_then_shrink", "grow_tail"])
+def test_compress_stored_in_place(ctx, port, case):
+    """psf_snappy_compress_stored: a stored-layout stream compressed where it
+    is, for streams whose fragments with tags come out longer than literals
+    (the later fragments move up, past the 3-byte tags) and shorter (they
+    move down, across whole fragments), byte-identical to 1.1.8."""
+    import ctypes as C
+
+    from parameter_server_amd._lib import check, lib
+    payload = {
+        "grow": lambda: _planted(12, [2, 3, 5, 8], 1),
+        "grow_every": lambda: _planted(20, range(20), 2),
+        "shrink_then_grow": lambda: _planted(14, [4, 5, 6, 7, 9], 3, zeros=[1]),
+        "grow_then_shrink": lambda: _planted(14, [1, 2, 3, 4], 4, zeros=[8, 9]),
+        "grow_tail": lambda: _planted(9, [0, 1, 2, 3, 4, 5, 6, 7], 5, tail=3000),
+    }[case]()
+    want = port.snappy_compress(payload)
+    stored = _stored_layout(payload)
+    if case.startswith("grow"):
+        assert len(want) > len(stored), "the planted matches made no fragment longer"
+    cap = lib().psf_snappy_stored_capacity(len(payload))
+    buf = torch.zeros(cap, dtype=torch.uint8, device="cuda:0")
+    buf[:len(stored)] = torch.frombuffer(bytearray(stored), dtype=torch.uint8).cuda()
+    out_len = C.c_size_t()
+    check(lib().psf_snappy_compress_stored(ctx.h, C.c_void_p(buf.data_ptr()), len(payload), cap, C.byref(out_len)))
+    got = buf[:out_len.value].cpu().numpy().tobytes()
+    assert got == want, (case, len(got), len(want))
