@@ -270,13 +270,18 @@ int psf_snappy_compress(psf_context* ctx, const void* d_in, size_t n, void* d_ou
 }
 
 // A stored-layout stream (psf_internal.h StoredLayout: what FIXING_FLOAT
-// writes when COMPRESSING follows) compressed where it is.
+// writes when COMPRESSING follows) compressed: left where it is when every
+// fragment comes out stored, else placed by the compressor and copied back.
+static size_t stored_capacity(size_t n) {
+  const size_t st = (size_t)psf::stored_alloc_bytes(psf::stored_layout((uint32_t)n));
+  const size_t mx = psf::snappy_max_compressed(n);
+  return st > mx ? st : mx;
+}
 int psf_snappy_compress_stored(psf_context* ctx, void* d_buf, size_t n, size_t cap, size_t* out_len) {
   return guarded(ctx ? ctx->impl : nullptr, [&] {
     if (!ctx || !d_buf || !out_len || n == 0 || n > 0xffffffffull) return PSF_ERR_ARG;
     psf::Context& c = *ctx->impl;
-    if (c.device() < 0) return PSF_ERR_ARG;
-    if (cap < psf::stored_alloc_bytes(psf::stored_layout((uint32_t)n))) return PSF_ERR_ARG;
+    if (c.device() < 0 || cap < stored_capacity(n)) return PSF_ERR_ARG;
     psf::Buffer src;
     src.ptr = static_cast<uint8_t*>(d_buf);
     src.bytes = n;
@@ -286,16 +291,15 @@ int psf_snappy_compress_stored(psf_context* ctx, void* d_buf, size_t n, size_t c
     psf::SnappyBatch b(c);
     b.compress(src, &out);
     b.flush();
+    if (out.ptr != src.ptr && out.bytes)
+      PSF_HIP_CHECK(hipMemcpyAsync(d_buf, out.ptr, out.bytes, hipMemcpyDeviceToDevice, c.stream()));
     c.sync();
-    if (out.ptr != src.ptr) throw psf::CheckError(PSF_ERR_CHECK, "stored stream not compressed in place");
     *out_len = out.bytes;
     return PSF_OK;
   });
 }
 
-size_t psf_snappy_stored_capacity(size_t n) {
-  return n && n <= 0xffffffffull ? (size_t)psf::stored_alloc_bytes(psf::stored_layout((uint32_t)n)) : 0;
-}
+size_t psf_snappy_stored_capacity(size_t n) { return n && n <= 0xffffffffull ? stored_capacity(n) : 0; }
 
 static psf::Buffer device_view(const void* p, size_t n) {
   psf::Buffer b;

@@ -50,8 +50,7 @@ void SnappyBatch::compress(const Buffer& src, Buffer* dst) {
   j.compress = true;
   j.in = c_.to_device(src);
   j.dst = dst;
-  // a stored-layout input (FIXING_FLOAT's output) is compacted where it is
-  if (j.in.layout == kLayoutPlain) j.out = c_.alloc(snappy_max_compressed(src.bytes));
+  j.out = c_.alloc(snappy_max_compressed(src.bytes));
   j.slot = (int)jobs_.size();
   j.ticket = c_.next_ticket();
   jobs_.push_back(std::move(j));
@@ -257,8 +256,8 @@ void SnappyBatch::finish() {
     }
     j.out.bytes = h.size;
     if (j.compress && h.pad == kStoredInPlace) {
-      // a stored-layout input: the stream is compacted where FIXING_FLOAT
-      // wrote it (snappy.hip K-save / K-place-stored)
+      // every fragment came out stored: the stream FIXING_FLOAT wrote is the
+      // result (snappy.hip K-place), the compressor's buffer goes unused
       Buffer o = j.in;
       o.bytes = h.size;
       o.layout = kLayoutPlain;

@@ -255,14 +255,8 @@ constexpr SkipCum make_skip() {
   }
   return s;
 }
-// the buffer: room for the stream COMPRESSING may make of it in place (up
-// to snappy_max_compressed(n) = 32 + n + n / 6, when fragments with tags
-// come out longer than literals), and 64 bytes for the compressor's aligned
-// reads past a fragment's end
 __host__ __device__ __forceinline__ uint64_t stored_alloc_bytes(const StoredLayout& s) {
-  const uint64_t mx = 32 + (uint64_t)s.nbytes + s.nbytes / 6;
-  const uint64_t st = stored_stream_bytes(s);
-  return (mx > st ? mx : st) + 64;
+  return stored_stream_bytes(s) + 64;  // the compressor's aligned reads past a fragment's end
 }
 
 // the stream byte at P, a header / tag byte before fragment k's data

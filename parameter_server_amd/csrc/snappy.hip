@@ -286,12 +286,9 @@ struct SnappyCJobs {
   CJob j[kSnappyBatchMax];
   PubSlot* pub;
   uint32_t njobs, nfrag;
-  uint64_t* finfo;   // per fragment: op (tag bytes) << 32 | next_emit (start of the final literal)
-  uint64_t* offset;  // per fragment: its offset in the stream (K-scan: every job's; K-save: stored jobs')
-  uint32_t scanned;  // K-scan ran (offset holds every fragment's)
-  uint32_t* k0;      // per stored job: its first fragment with tags (nfrag: none, the stream is in place)
-  uint8_t* saved;    // per fragment (stored jobs): kFrag + 64 bytes, K-save's copy of a literal's clobbered end
-  uint32_t has_stored, has_plain;
+  uint64_t* finfo;     // per fragment: op (tag bytes) << 32 | next_emit (start of the final literal)
+  uint64_t* offset;    // per fragment: its offset in the stream (K-scan)
+  uint32_t* in_place;  // per job (K-scan streams): every fragment stored, the stream left in `in`
 };
 // fragment k's input bytes: consecutive 64 KiB blocks, or in a stored job the
 // fragment's literal in the StoredLayout stream
@@ -888,19 +885,18 @@ __global__ __launch_bounds__(kScanT) void snappy_scan(const SnappyCJobs J) {
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   if (tid == 0) {
     s_base = c.hdr;
-    s_any = 0xFFFFFFFFu;
+    s_any = 0;
   }
   __syncthreads();
-  // a stored job's stream stays where FIXING_FLOAT wrote it (header and
-  // tags included): K-save / K-place-stored move what follows its first
-  // fragment with tags, if any; a plain job's header goes to dst
-  uint32_t first = c.nfrag;
-  for (uint32_t k = tid; k < c.nfrag; k += kScanT)
-    if (J.finfo[c.frag0 + k] != 0) first = min(first, k);
-  if (first < c.nfrag) atomicMin(&s_any, first);
+  uint32_t any = 0;  // a fragment with tags (not stored from byte 0)
+  for (uint32_t k = tid; k < c.nfrag; k += kScanT) any |= J.finfo[c.frag0 + k] != 0 ? 1u : 0u;
+  if (any) s_any = 1;
   __syncthreads();
-  if (tid == 0 && c.stored) J.k0[blockIdx.x] = s_any;
-  if (!c.stored && tid < c.hdr) c.dst[tid] = (uint8_t)(((uint32_t)c.n >> (7 * tid)) | (tid + 1 < c.hdr ? 128u : 0u));
+  // a stored job whose fragments all came out stored: the stream FIXING_FLOAT
+  // wrote is the result (header and tags included); nothing moves
+  const bool in_place = c.stored && !s_any;
+  if (tid == 0) J.in_place[blockIdx.x] = in_place ? 1u : 0u;
+  if (!in_place && tid < c.hdr) c.dst[tid] = (uint8_t)(((uint32_t)c.n >> (7 * tid)) | (tid + 1 < c.hdr ? 128u : 0u));
   for (uint32_t k0 = 0; k0 < c.nfrag; k0 += kScanT) {
     const uint32_t k = k0 + tid;
     uint64_t v = 0;
@@ -928,7 +924,7 @@ __global__ __launch_bounds__(kScanT) void snappy_scan(const SnappyCJobs J) {
     PubSlot* pub = J.pub + c.slot;
     pub->size = s_base;
     pub->status = kOk;
-    pub->pad = c.stored ? kStoredInPlace : 0u;
+    pub->pad = in_place ? kStoredInPlace : 0u;
     publish_ticket(pub, c.ticket);
   }
 }
@@ -943,9 +939,10 @@ constexpr uint32_t kPlaceT = 256;
 constexpr uint32_t kInlineScan = 4096;
 __global__ __launch_bounds__(kPlaceT) void snappy_place(const SnappyCJobs J, const uint8_t* __restrict__ scratch) {
   __shared__ uint64_t s_part[kPlaceT / 64];
+  __shared__ uint32_t s_any[kPlaceT / 64];
   const uint32_t f = blockIdx.x, tid = threadIdx.x;
-  const CJob& c = cjob_of(J, f);
-  if (c.stored) return;  // (K-save / K-place-stored)
+  const uint32_t ji = cjob_index(J, f);
+  const CJob& c = J.j[ji];
   const uint32_t k = f - c.frag0;
   const size_t start = (size_t)k * kFrag;
   const uint32_t len = (uint32_t)min((size_t)kFrag, c.n - start);
@@ -953,26 +950,46 @@ __global__ __launch_bounds__(kPlaceT) void snappy_place(const SnappyCJobs J, con
   const uint32_t op = (uint32_t)(info >> 32), ne = (uint32_t)info;
   PSF_TRACE(f, 2);
   uint64_t off;
-  if (J.scanned) {
+  if (J.offset) {
+    if (J.in_place[ji]) return;  // K-scan found every fragment stored: the stream is in place
     off = J.offset[f];
   } else {
+    // the lengths of the fragments before this one (all full), and -- for a
+    // stored job -- whether any fragment of the stream has tags
     uint64_t part = 0;
-    for (uint32_t i = tid; i < k; i += kPlaceT) part += frag_len(J.finfo[c.frag0 + i], kFrag);
+    uint32_t any = 0;
+    for (uint32_t i = tid; i < c.nfrag; i += kPlaceT) {
+      const uint64_t fi = J.finfo[c.frag0 + i];
+      if (i < k) part += frag_len(fi, kFrag);
+      any |= fi != 0 ? 1u : 0u;
+    }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
-    if ((tid & 63) == 0) s_part[tid >> 6] = part;
+    for (int o = 32; o > 0; o >>= 1) {
+      part += __shfl_xor(part, o, 64);
+      any |= __shfl_xor(any, o, 64);
+    }
+    if ((tid & 63) == 0) {
+      s_part[tid >> 6] = part;
+      s_any[tid >> 6] = any;
+    }
     __syncthreads();
     off = c.hdr;
-    for (uint32_t w = 0; w < kPlaceT / 64; ++w) off += s_part[w];
-    if (k == 0 && tid < c.hdr)
+    any = 0;
+    for (uint32_t w = 0; w < kPlaceT / 64; ++w) {
+      off += s_part[w];
+      any |= s_any[w];
+    }
+    const bool in_place = c.stored && !any;
+    if (k == 0 && tid < c.hdr && !in_place)
       c.dst[tid] = (uint8_t)(((uint32_t)c.n >> (7 * tid)) | (tid + 1 < c.hdr ? 128u : 0u));
     if (k + 1 == c.nfrag && tid == 0 && J.pub) {
       PubSlot* pub = J.pub + c.slot;
       pub->size = off + frag_len(info, len);
       pub->status = kOk;
-      pub->pad = 0u;
+      pub->pad = in_place ? kStoredInPlace : 0u;
       publish_ticket(pub, c.ticket);
     }
+    if (in_place) return;  // FIXING_FLOAT wrote the stream, header and tags included
   }
   uint8_t* d = c.dst + off;
   if (op) copy_bytes<kPlaceT>(d, scratch + (size_t)f * kSnappyFragOut, op, tid);
@@ -982,189 +999,6 @@ __global__ __launch_bounds__(kPlaceT) void snappy_place(const SnappyCJobs J, con
     copy_bytes<kPlaceT>(d, frag_src(c, k) + ne, len - ne, tid);
   }
   PSF_TRACE(f, 3);
-}
-
-// ---- stored jobs: the stream is compacted where FIXING_FLOAT wrote it.
-// Fragments before the first one with tags (k0) are in place, header and
-// tags included (and with no such fragment the whole stream is: the common
-// case, FIXING_FLOAT codes); fragment k >= k0 moves to its offset D_k, down
-// when the fragments with tags came out shorter than a literal, up when
-// longer (a 1.1.8 parse can lose a few bytes to a short match; the buffer
-// holds snappy_max_compressed(n)).  Fragment k alone writes [D_k, D_k+1), so
-// the bytes of its final literal outside that range are the ones other
-// fragments can overwrite:
-//   K-save          every fragment k >= k0 copies those bytes aside; it also
-//                   settles D_k (inline sum, or K-scan's) and publishes the
-//                   stream length;
-//   K-place-stored  fragment k >= k0 reads its literal (the saved bytes from
-//                   aside) into LDS, then writes its tags and literal at D_k.
-// No workgroup waits for another.
-__device__ __forceinline__ uint64_t stored_frag_offset(const SnappyCJobs& J, const CJob& c, uint32_t ji, uint32_t k,
-                                                       uint32_t tid, uint64_t* s_part, uint32_t* s_first,
-                                                       uint32_t* first_out) {
-  if (J.scanned) {
-    *first_out = J.k0[ji];
-    return J.offset[c.frag0 + k];
-  }
-  uint64_t part = 0;
-  uint32_t first = c.nfrag;
-  for (uint32_t i = tid; i < c.nfrag; i += kPlaceT) {
-    const uint64_t fi = J.finfo[c.frag0 + i];
-    if (i < k) part += frag_len(fi, kFrag);
-    if (fi != 0) first = min(first, i);
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    part += __shfl_xor(part, o, 64);
-    first = min(first, (uint32_t)__shfl_xor(first, o, 64));
-  }
-  if ((tid & 63) == 0) {
-    s_part[tid >> 6] = part;
-    s_first[tid >> 6] = first;
-  }
-  __syncthreads();
-  uint64_t off = c.hdr;
-  first = c.nfrag;
-  for (uint32_t w = 0; w < kPlaceT / 64; ++w) {
-    off += s_part[w];
-    first = min(first, s_first[w]);
-  }
-  *first_out = first;
-  return off;
-}
-
-__global__ __launch_bounds__(kPlaceT) void snappy_save(const SnappyCJobs J) {
-  __shared__ uint64_t s_part[kPlaceT / 64];
-  __shared__ uint32_t s_first[kPlaceT / 64];
-  const uint32_t f = blockIdx.x, tid = threadIdx.x;
-  const uint32_t ji = cjob_index(J, f);  // (an index: a pointer into J would copy J to scratch)
-  const CJob& c = J.j[ji];
-  if (!c.stored) return;
-  const uint32_t k = f - c.frag0;
-  const uint32_t len = (uint32_t)min((size_t)kFrag, c.n - (size_t)k * kFrag);
-  const uint64_t info = J.finfo[f];
-  uint32_t k0;
-  const uint64_t off = stored_frag_offset(J, c, ji, k, tid, s_part, s_first, &k0);
-  const uint64_t next = off + frag_len(info, len);  // D_k+1
-  if (!J.scanned) {
-    if (tid == 0) J.offset[f] = off;
-    if (k == 0 && tid == 0) J.k0[ji] = k0;
-    if (k + 1 == c.nfrag && tid == 0 && J.pub) {
-      PubSlot* pub = J.pub + c.slot;
-      pub->size = next;
-      pub->status = kOk;
-      pub->pad = kStoredInPlace;
-      publish_ticket(pub, c.ticket);
-    }
-  }
-  if (k < k0) return;  // in place
-  const uint32_t ne = (uint32_t)info;
-  if (ne >= len) return;
-  const StoredLayout L = stored_layout((uint32_t)c.n);
-  const uint64_t lit = stored_frag_data(L, k) + ne;  // the final literal's bytes in the stream
-  const uint64_t end = stored_frag_data(L, k) + len;
-  uint8_t* slot = J.saved + (size_t)f * (kFrag + 64);
-  // what the other fragments' writes can reach: before D_k (fragment k - 1's,
-  // when the stream grew) and from D_k+1 on (the later ones')
-  if (off > lit) {
-    const uint64_t e = off < end ? off : end;
-    copy_bytes<kPlaceT>(slot, c.in + lit, (uint32_t)(e - lit), tid);
-  }
-  const uint64_t cut = next > lit ? next : lit;
-  if (cut < end) copy_bytes<kPlaceT>(slot + (cut - lit), c.in + cut, (uint32_t)(end - cut), tid);
-}
-
-// dst[0, n) = LDS s[0, n) (s 16-byte aligned, 16 bytes readable past n),
-// dst at any alignment: 16-byte stores composed from LDS dwords
-template <uint32_t T>
-__device__ __forceinline__ void lds_to_global(uint8_t* __restrict__ dst, const uint32_t* s, uint32_t n, uint32_t tid) {
-  const uint8_t* sb = reinterpret_cast<const uint8_t*>(s);
-  const uint32_t head = (uint32_t)(-reinterpret_cast<uintptr_t>(dst) & 15);
-  if (head >= n) {
-    for (uint32_t i = tid; i < n; i += T) dst[i] = sb[i];
-    return;
-  }
-  if (tid < head) dst[tid] = sb[tid];
-  const uint32_t nb = (n - head) >> 4;
-  uint4* d16 = reinterpret_cast<uint4*>(dst + head);
-  for (uint32_t b = tid; b < nb; b += T) {
-    const uint32_t o = head + 16 * b;
-    d16[b] = make_uint4(ld32(s, o), ld32(s, o + 4), ld32(s, o + 8), ld32(s, o + 12));
-  }
-  for (uint32_t i = head + 16 * nb + tid; i < n; i += T) dst[i] = sb[i];
-}
-
-__global__ __launch_bounds__(kPlaceT) void snappy_place_stored(const SnappyCJobs J, const uint8_t* __restrict__ scratch) {
-  __shared__ uint32_t s_lit[(kFrag + 64) / 4];
-  const uint32_t f = blockIdx.x, tid = threadIdx.x;
-  const uint32_t ji = cjob_index(J, f);
-  const CJob& c = J.j[ji];
-  if (!c.stored) return;
-  const uint32_t k = f - c.frag0;
-  const uint32_t k0 = J.k0[ji];
-  if (k < k0) return;  // in place
-  const uint32_t len = (uint32_t)min((size_t)kFrag, c.n - (size_t)k * kFrag);
-  const uint64_t info = J.finfo[f];
-  const uint32_t op = (uint32_t)(info >> 32), ne = (uint32_t)info;
-  const uint64_t off = J.offset[f];
-  const uint64_t next = off + frag_len(info, len);
-  uint8_t* out = const_cast<uint8_t*>(c.in);  // the stored stream (FIXING_FLOAT's buffer) is the output
-  const StoredLayout L = stored_layout((uint32_t)c.n);
-  const uint32_t n = len - ne;  // the final literal
-  if (n) {
-    // the literal into LDS: bytes in [D_k, D_k+1) from the stream (only this
-    // workgroup writes there, after this), the rest from K-save's copy
-    const uint64_t lit = stored_frag_data(L, k) + ne;
-    const uint32_t nz = off > lit ? (uint32_t)min<uint64_t>(off - lit, n) : 0;  // [0, nz): saved
-    const uint32_t na = (uint32_t)(next > lit ? min<uint64_t>(next - lit, n) : 0);  // [na, n): saved
-    const uint8_t* sv = J.saved + (size_t)f * (kFrag + 64);
-    typedef uint32_t V4 __attribute__((ext_vector_type(4)));
-    const uintptr_t a = reinterpret_cast<uintptr_t>(out + lit);
-    const uint32_t sh = (uint32_t)(a & 15);
-    const auto s16 = gbl<V4>(reinterpret_cast<const void*>(a & ~(uintptr_t)15));
-    const auto v16 = gbl<V4>(sv);
-    uint4* l16 = reinterpret_cast<uint4*>(s_lit);
-    uint8_t* lb = reinterpret_cast<uint8_t*>(s_lit);
-    const uint32_t nb = (n + 15) >> 4;
-    // a round's loads are all issued before its LDS stores (8 blocks per
-    // lane in flight, not one memory latency per block)
-    constexpr uint32_t U = 8;
-    for (uint32_t b0 = 0; b0 < nb; b0 += U * kPlaceT) {
-      V4 lo[U], hi[U];
-#pragma unroll
-      for (uint32_t u = 0; u < U; ++u) {
-        const uint32_t b = b0 + u * kPlaceT + tid, o = 16 * b;
-        if (b >= nb) continue;
-        if (o >= nz && o + 16 <= na) {
-          lo[u] = s16[b];
-          hi[u] = s16[b + 1];
-        } else if (o >= na || o + 16 <= nz) {
-          lo[u] = v16[b];
-        }
-      }
-#pragma unroll
-      for (uint32_t u = 0; u < U; ++u) {
-        const uint32_t b = b0 + u * kPlaceT + tid, o = 16 * b;
-        if (b >= nb) continue;
-        if (o >= nz && o + 16 <= na) {
-          l16[b] = funnel16(make_uint4(lo[u][0], lo[u][1], lo[u][2], lo[u][3]),
-                            make_uint4(hi[u][0], hi[u][1], hi[u][2], hi[u][3]), sh);
-        } else if (o >= na || o + 16 <= nz) {
-          l16[b] = make_uint4(lo[u][0], lo[u][1], lo[u][2], lo[u][3]);
-        } else {  // a block that holds a cut
-          for (uint32_t i = o; i < o + 16 && i < n; ++i) lb[i] = (i >= nz && i < na) ? out[lit + i] : sv[i];
-        }
-      }
-    }
-  }
-  __syncthreads();  // every read of this fragment's bytes before any write over them
-  uint8_t* d = out + off;
-  if (op) copy_bytes<kPlaceT>(d, scratch + (size_t)f * kSnappyFragOut, op, tid);
-  if (n) {
-    d += op;
-    d += literal_tag(d, n, tid);
-    lds_to_global<kPlaceT>(d, s_lit, n, tid);
-  }
 }
 
 // ------------------------------------------------------------------ uncompress
@@ -2400,17 +2234,11 @@ __global__ __launch_bounds__(256) void snappy_dfrag(const SnappyDJobs J) {
 
 size_t snappy_max_compressed(size_t n) { return 32 + n + n / 6; }
 
-// scratch: tag slots | finfo | offset (one each per fragment) | k0 (per job)
-// | (a batch with stored jobs) the literal ends K-save copies aside, kFrag +
-// 64 bytes per fragment
+// scratch: tag slots | finfo | offset (one each per fragment) | in_place (per job)
 size_t snappy_compress_batch_scratch(const SnappyCJob* jobs, int njobs) {
   size_t nfrag = 0;
-  bool stored = false;
-  for (int i = 0; i < njobs; ++i) {
-    nfrag += (jobs[i].n + kFrag - 1) / kFrag;
-    stored |= jobs[i].stored != 0;
-  }
-  return nfrag * kSnappyFragOut + nfrag * 16 + 4 * kSnappyBatchMax + 64 + 256 + (stored ? nfrag * (kFrag + 64) : 0);
+  for (int i = 0; i < njobs; ++i) nfrag += (jobs[i].n + kFrag - 1) / kFrag;
+  return nfrag * kSnappyFragOut + nfrag * 16 + 4 * kSnappyBatchMax + 64;
 }
 
 size_t snappy_compress_scratch(size_t n) {
@@ -2446,9 +2274,7 @@ int snappy_compress_batch_launch(const SnappyCJob* jobs, int njobs, void* scratc
   uint8_t* p = s + (size_t)K.nfrag * kSnappyFragOut;
   K.finfo = reinterpret_cast<uint64_t*>(p);
   K.offset = K.finfo + K.nfrag;
-  K.k0 = reinterpret_cast<uint32_t*>(K.offset + K.nfrag);  // (every word the kernels read is written first in the chain)
-  K.saved = reinterpret_cast<uint8_t*>(K.k0) + 4 * kSnappyBatchMax + 64;
-  K.saved += (size_t)(-reinterpret_cast<uintptr_t>(K.saved) & 255);
+  K.in_place = reinterpret_cast<uint32_t*>(K.offset + K.nfrag);  // (every word the kernels read is written first in the chain)
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -2458,18 +2284,10 @@ int snappy_compress_batch_launch(const SnappyCJob* jobs, int njobs, void* scratc
   ProfScope ps(prof, kKSnappyCompress, st, bytes);
   uint32_t longest = 0;
   for (int i = 0; i < njobs; ++i) longest = std::max(longest, K.j[i].nfrag);
-  K.scanned = longest > kInlineScan ? 1u : 0u;  // else K-place / K-save sum the lengths themselves
-  for (int i = 0; i < njobs; ++i) {
-    K.has_stored |= K.j[i].stored;
-    K.has_plain |= K.j[i].stored ? 0u : 1u;
-  }
+  if (longest <= kInlineScan) K.offset = nullptr;  // K-place sums the lengths itself
   hipLaunchKernelGGL(snappy_parse, dim3(grid), dim3(kCThreads), 0, st, K, s);
-  if (K.scanned) hipLaunchKernelGGL(snappy_scan, dim3(K.njobs), dim3(kScanT), 0, st, K);
-  if (K.has_plain) hipLaunchKernelGGL(snappy_place, dim3(K.nfrag), dim3(kPlaceT), 0, st, K, s);
-  if (K.has_stored) {
-    hipLaunchKernelGGL(snappy_save, dim3(K.nfrag), dim3(kPlaceT), 0, st, K);
-    hipLaunchKernelGGL(snappy_place_stored, dim3(K.nfrag), dim3(kPlaceT), 0, st, K, s);
-  }
+  if (K.offset) hipLaunchKernelGGL(snappy_scan, dim3(K.njobs), dim3(kScanT), 0, st, K);
+  hipLaunchKernelGGL(snappy_place, dim3(K.nfrag), dim3(kPlaceT), 0, st, K, s);
   return launch_status();
 }
 

@@ -199,10 +199,9 @@ def _planted(nfrag, plant, seed, tail=0, zeros=()):
 
 @pytest.mark.parametrize("case", ["grow", "grow_every", "shrink_then_grow", "grow_then_shrink", "grow_tail"])
 def test_compress_stored_in_place(ctx, port, case):
-    """psf_snappy_compress_stored: a stored-layout stream compressed where it
-    is, for streams whose fragments with tags come out longer than literals
-    (the later fragments move up, past the 3-byte tags) and shorter (they
-    move down, across whole fragments), byte-identical to 1.1.8."""
+    """psf_snappy_compress_stored: a stored-layout stream compressed, for
+    streams whose fragments with tags come out longer than literals and
+    shorter (down by whole fragments), byte-identical to 1.1.8."""
     import ctypes as C
 
     from parameter_server_amd._lib import check, lib
