@@ -923,7 +923,8 @@ struct FfBatchT {
   const uint32_t* lcg_bits;
   Lcg17 k17;
   uint32_t a_lane, c_lane;
-  uint32_t mm_reverse;  // min/max workgroups dispatched in reverse array order
+  uint32_t mm_reverse;     // min/max workgroups dispatched in reverse array order
+  uint32_t mm_total_done;  // (host) the min/max pass already ran in a merged launch
   double ratio;
 };
 static_assert(sizeof(FfBatchT<kBatchSmall>) <= 4096, "the small batch fits 4 KiB of kernel arguments");
@@ -967,13 +968,15 @@ __device__ __forceinline__ void tile_range_of(size_t ntiles, uint32_t wg, uint32
   t1 = t0 + per < ntiles ? t0 + per : ntiles;
 }
 
+// the batched kernels' bodies take their workgroup index: a merged launch
+// (ff_dec_mm_batch) runs a decode batch and a min/max batch side by side
 template <typename V, int CAP>
-__global__ __launch_bounds__(kBlock) void ff_minmax_batch(FfBatchT<CAP> B) {
+__device__ __forceinline__ void minmax_batch_body(const FfBatchT<CAP>& B, uint32_t block) {
   typedef typename KeyOf<V>::K K;
   // mm_reverse: workgroups dispatched last-array-first, so the arrays the
   // encode reads first are the ones read last here (still in the Infinity
   // Cache when the encode starts)
-  const uint32_t bb = B.mm_reverse ? B.mm_total - 1 - blockIdx.x : blockIdx.x;
+  const uint32_t bb = B.mm_reverse ? B.mm_total - 1 - block : block;
   const int jb = batch_job(B, bb, true);
   const FfJob& J = B.job[jb];
   const V* __restrict__ x = static_cast<const V*>(J.x);
@@ -1038,6 +1041,10 @@ __global__ __launch_bounds__(kBlock) void ff_minmax_batch(FfBatchT<CAP> B) {
     pp[bb] = lo;
     pp[B.mm_total + bb] = hi;
   }
+}
+template <typename V, int CAP>
+__global__ __launch_bounds__(kBlock) void ff_minmax_batch(FfBatchT<CAP> B) {
+  minmax_batch_body<V, CAP>(B, blockIdx.x);
 }
 
 // kStored: the instantiation launched when a job of the batch writes a
@@ -1195,13 +1202,13 @@ __global__ __launch_bounds__(kBlock) void ff_encode_batch(FfBatchT<CAP> B) {
 }
 
 template <typename V, int NB, int CAP>
-__global__ __launch_bounds__(kBlock) void ff_decode_batch(FfBatchT<CAP> B) {
-  const int jb = batch_job(B, blockIdx.x, false);
+__device__ __forceinline__ void decode_batch_body(const FfBatchT<CAP>& B, uint32_t block) {
+  const int jb = batch_job(B, block, false);
   const FfJob& J = B.job[jb];
   const uint8_t* __restrict__ code = static_cast<const uint8_t*>(J.x);
   V* __restrict__ out = static_cast<V*>(J.out);
   const size_t n = J.n;
-  const uint32_t wg = blockIdx.x - B.first[jb];
+  const uint32_t wg = block - B.first[jb];
   float mn_f = J.mn, mx_f = J.mx;
   if (J.u.range) { mn_f = J.u.range[0]; mx_f = J.u.range[1]; }
   const double min_v = (double)mn_f, max_v = (double)mx_f;
@@ -1225,6 +1232,18 @@ __global__ __launch_bounds__(kBlock) void ff_decode_batch(FfBatchT<CAP> B) {
       out[i] = dequant<V>(r, ratio, bin, min_v);
     }
   }
+}
+template <typename V, int NB, int CAP>
+__global__ __launch_bounds__(kBlock) void ff_decode_batch(FfBatchT<CAP> B) {
+  decode_batch_body<V, NB, CAP>(B, blockIdx.x);
+}
+// One launch for a decode batch and an independent min/max batch (the round
+// trip driver's decode of one phase and the next phase's first encode pass:
+// psf_nodes_roundtrip_opts): workgroups [0, D.total) decode, the rest fold.
+template <typename V, int NB>
+__global__ __launch_bounds__(kBlock) void ff_dec_mm_batch(FfBatchT<kBatchSmall> D, FfBatchT<kBatchSmall> M) {
+  if (blockIdx.x < D.total) decode_batch_body<V, NB, kBatchSmall>(D, blockIdx.x);
+  else minmax_batch_body<V, kBatchSmall>(M, blockIdx.x - D.total);
 }
 
 // ------------------------------------------------------------ launchers ----
@@ -1462,7 +1481,7 @@ bool ff_batchable(const void* x, const void* out, size_t n, int nb, int value_ty
 template <typename V, int NB, int CAP>
 static void launch_encode_batch(FfBatchT<CAP>& B, uint32_t enc_total, hipStream_t st, Profiler* prof,
                                 double bytes_mm, double bytes_enc) {
-  if (B.mm_total) {
+  if (B.mm_total && !B.mm_total_done) {
     ProfScope ps(prof, kKMinmax, st, bytes_mm);
     hipLaunchKernelGGL((ff_minmax_batch<V, CAP>), dim3(B.mm_total), dim3(kBlock), 0, st, B);
   }
@@ -1545,8 +1564,13 @@ static bool mm_reverse_mode(double bytes_mm) {
 }
 
 template <int CAP>
+static int fill_decode_batch(FfBatchT<CAP>& B, int value_type, int nb, const FfDecArray* arrs, int count,
+                             double* bytes_out);
+
+template <int CAP>
 static int encode_batch_cap(int value_type, int nb, const FfArray* arrs, int count, void* partials,
-                            PubSlot* pub_base, hipStream_t st, Profiler* prof) {
+                            PubSlot* pub_base, hipStream_t st, Profiler* prof, const FfDecArray* dec, int ndec,
+                            int dec_nb) {
   static FfBatchT<CAP> B;  // host staging of the kernel arguments (launches are serialised per thread)
   static std::mutex mu;
   std::lock_guard<std::mutex> lock(mu);
@@ -1626,6 +1650,39 @@ static int encode_batch_cap(int value_type, int nb, const FfArray* arrs, int cou
   B.total = enc;
   B.mm_total = mm;
   B.mm_reverse = mm_reverse_mode(bytes_mm) ? 1u : 0u;
+  if (ndec > 0) {
+    // the pending decode batch: in the min/max launch when both are small
+    // (one launch instead of two), else on its own first
+    const bool merge = CAP == kBatchSmall && ndec <= kBatchSmall && B.mm_total > 0 && dec_nb >= 1 && dec_nb <= 3;
+    if (!merge) {
+      const int ds = ff_decode_batch_launch(value_type, dec_nb, dec, ndec, st, prof);
+      if (ds != kOk) return ds;
+    } else if constexpr (CAP == kBatchSmall) {
+      static FfBatchT<kBatchSmall> D;
+      double bytes_dec = 0;
+      const int fs = fill_decode_batch<kBatchSmall>(D, value_type, dec_nb, dec, ndec, &bytes_dec);
+      if (fs != kOk) return fs;
+      const FfBatchT<kBatchSmall>& M = B;
+      const dim3 grid(D.total + M.mm_total);
+      {
+        ProfScope pm(prof, kKDecodeMinmax, st, bytes_dec + bytes_mm);
+        if (value_type == kFloat) {
+          switch (dec_nb) {
+            case 1: hipLaunchKernelGGL((ff_dec_mm_batch<float, 1>), grid, dim3(kBlock), 0, st, D, M); break;
+            case 2: hipLaunchKernelGGL((ff_dec_mm_batch<float, 2>), grid, dim3(kBlock), 0, st, D, M); break;
+            default: hipLaunchKernelGGL((ff_dec_mm_batch<float, 3>), grid, dim3(kBlock), 0, st, D, M); break;
+          }
+        } else {
+          switch (dec_nb) {
+            case 1: hipLaunchKernelGGL((ff_dec_mm_batch<double, 1>), grid, dim3(kBlock), 0, st, D, M); break;
+            case 2: hipLaunchKernelGGL((ff_dec_mm_batch<double, 2>), grid, dim3(kBlock), 0, st, D, M); break;
+            default: hipLaunchKernelGGL((ff_dec_mm_batch<double, 3>), grid, dim3(kBlock), 0, st, D, M); break;
+          }
+        }
+      }
+      B.mm_total_done = 1;  // the encode launch below skips the min/max pass
+    }
+  }
   if (value_type == kFloat) {
     switch (nb) {
       case 1: launch_encode_batch<float, 1, CAP>(B, enc, st, prof, bytes_mm, bytes_enc); break;
@@ -1643,20 +1700,21 @@ static int encode_batch_cap(int value_type, int nb, const FfArray* arrs, int cou
 }
 
 int ff_encode_batch_launch(int value_type, int nb, const FfArray* arrs, int count, void* partials,
-                           PubSlot* pub_base, hipStream_t st, Profiler* prof) {
-  if (count <= 0) return kOk;
+                           PubSlot* pub_base, hipStream_t st, Profiler* prof, const FfDecArray* dec, int ndec,
+                           int dec_nb) {
+  if (count <= 0) return ndec > 0 ? ff_decode_batch_launch(value_type, dec_nb, dec, ndec, st, prof) : kOk;
   if (count > kFfBatchMax) return kErrArg;
   if (value_type != kFloat && value_type != kDouble) return kErrArg;
-  return count <= kBatchSmall ? encode_batch_cap<kBatchSmall>(value_type, nb, arrs, count, partials, pub_base, st, prof)
-                              : encode_batch_cap<kFfBatchMax>(value_type, nb, arrs, count, partials, pub_base, st, prof);
+  return count <= kBatchSmall
+             ? encode_batch_cap<kBatchSmall>(value_type, nb, arrs, count, partials, pub_base, st, prof, dec, ndec, dec_nb)
+             : encode_batch_cap<kFfBatchMax>(value_type, nb, arrs, count, partials, pub_base, st, prof, dec, ndec,
+                                             dec_nb);
 }
 
+// a decode batch's kernel arguments
 template <int CAP>
-static int decode_batch_cap(int value_type, int nb, const FfDecArray* arrs, int count, hipStream_t st,
-                            Profiler* prof) {
-  static FfBatchT<CAP> B;
-  static std::mutex mu;
-  std::lock_guard<std::mutex> lock(mu);
+static int fill_decode_batch(FfBatchT<CAP>& B, int value_type, int nb, const FfDecArray* arrs, int count,
+                             double* bytes_out) {
   memset(&B, 0, sizeof(B));
   for (int i = 0; i < CAP; ++i) B.first[i] = B.mm_first[i] = ~0u;
   B.njobs = count;
@@ -1679,6 +1737,20 @@ static int decode_batch_cap(int value_type, int nb, const FfDecArray* arrs, int 
     bytes += (double)arrs[i].n * (vsz + nb);
   }
   B.total = wg;
+  *bytes_out = bytes;
+  return kOk;
+}
+
+template <int CAP>
+static int decode_batch_cap(int value_type, int nb, const FfDecArray* arrs, int count, hipStream_t st,
+                            Profiler* prof) {
+  static FfBatchT<CAP> B;
+  static std::mutex mu;
+  std::lock_guard<std::mutex> lock(mu);
+  double bytes = 0;
+  const int fs = fill_decode_batch<CAP>(B, value_type, nb, arrs, count, &bytes);
+  if (fs != kOk) return fs;
+  const uint32_t wg = B.total;
   ProfScope ps(prof, kKDecode, st, bytes);
   if (value_type == kFloat) {
     switch (nb) {

@@ -726,6 +726,35 @@ int psf_nodes_roundtrip_opts(psf_node* const* snd, psf_node* const* rcv, const p
       s[i] = snd[i]->impl;
       r[i] = rcv[i]->impl;
     }
+    // a phase's FIXING_FLOAT decode is held back until the next phase's
+    // first encode launch (one launch instead of two); whatever is still held
+    // is launched before returning, also on an error
+    std::set<psf::Context*> dctx;
+    for (int i = 0; i < n; ++i) {
+      dctx.insert(s[i]->ctx());
+      dctx.insert(r[i]->ctx());
+    }
+    struct DeferScope {
+      std::set<psf::Context*>& cs;
+      explicit DeferScope(std::set<psf::Context*>& c) : cs(c) {
+        for (psf::Context* x : cs) x->defer_decodes = x->device() >= 0;
+      }
+      void finish() {
+        for (psf::Context* x : cs) {
+          x->defer_decodes = false;
+          x->flush_deferred();
+        }
+      }
+      ~DeferScope() {
+        for (psf::Context* x : cs) {
+          x->defer_decodes = false;
+          try {
+            x->flush_deferred();
+          } catch (...) {
+          }
+        }
+      }
+    } defer(dctx);
     std::vector<psf::Message> m(n), w(n);
     std::vector<psf::Message*> mp(n), wp(n);
     std::vector<const psf::Message*> tp(n);
@@ -787,6 +816,7 @@ int psf_nodes_roundtrip_opts(psf_node* const* snd, psf_node* const* rcv, const p
         b = e;
       }
     }
+    defer.finish();
     std::set<psf::Context*> ctxs;  // CHECK_GT(bin, 0) of the lazily encoded ranges
     for (int i = 0; i < n; ++i) ctxs.insert(s[i]->ctx());
     for (psf::Context* c : ctxs) c->check_ranges();
@@ -1041,7 +1071,7 @@ int psf_profile_read(psf_context* ctx, int k, int64_t* launches, double* total_m
 const char* psf_profile_kernel_name(int k) {
   static const char* names[] = {"ff_minmax_partials", "ff_encode", "ff_decode", "crc32c_chunks",
                                 "noise_add", "snappy_compress", "snappy_decompress", "ordered_match",
-                                "kvmap_push", "kvmap_get"};
+                                "kvmap_push", "kvmap_get", "ff_decode_minmax"};
   return (k >= 0 && k < psf::kKNum) ? names[k] : "?";
 }
 

@@ -559,6 +559,15 @@ void Context::check_ranges() {
   if (bad) throw CheckError(kErrBin, "CHECK_GT(bin, 0)");
 }
 
+void Context::flush_deferred() {
+  if (deferred.arrs.empty()) return;
+  const int st = ff_decode_batch_launch(deferred.value_type, deferred.nb, deferred.arrs.data(),
+                                        (int)deferred.arrs.size(), stream_, &prof_);
+  deferred.arrs.clear();
+  deferred.keep.clear();
+  if (st != kOk) throw CheckError(st, "ff_decode batch launch failed");
+}
+
 Buffer Context::to_device(const Buffer& b) {
   if (b.loc == Loc::kDevice || b.empty()) return b;
   Buffer d = alloc(b.bytes);

@@ -163,6 +163,20 @@ class Context {
   std::mutex& mu() { return mu_; }
   Profiler* prof() { return &prof_; }
 
+  // A FIXING_FLOAT decode batch held back (psf_nodes_roundtrip_opts turns
+  // this on for its own duration): the next batched encode on the context
+  // launches it together with its min/max pass, or flush_deferred() on its
+  // own.  `keep` holds the batch's buffers until it is launched (the caching
+  // allocator's stream order covers only launched work).
+  struct DeferredDecode {
+    int value_type = 0, nb = 0;
+    std::vector<FfDecArray> arrs;
+    std::vector<Buffer> keep;
+  };
+  bool defer_decodes = false;
+  DeferredDecode deferred;
+  void flush_deferred();
+
   // Host time spent blocked on the device, by cause (psf_context_host_stats):
   // stream synchronisations, waits on a kernel's published side-info, and
   // slice-position read-backs.

@@ -313,8 +313,17 @@ void FixingFloatFilter::encode_messages(Context* ctx, std::vector<FfMessage>& ms
       }
       Buffer scratch = ctx->alloc(ff_batch_partials_bytes(arrs.data(), (int)arrs.size()));
       PSF_HPROF(9);
+      // a held-back decode of the same value type goes along with this
+      // batch's min/max pass (independent arrays)
+      Context::DeferredDecode& d = ctx->deferred;
+      const bool take = !d.arrs.empty() && d.value_type == jobs[part[0]].type;
       int s = ff_encode_batch_launch(jobs[part[0]].type, jobs[part[0]].nb, arrs.data(), (int)arrs.size(),
-                                     scratch.ptr, ctx->pub_dev(0), st, ctx->prof());
+                                     scratch.ptr, ctx->pub_dev(0), st, ctx->prof(), take ? d.arrs.data() : nullptr,
+                                     take ? (int)d.arrs.size() : 0, take ? d.nb : 0);
+      if (take) {
+        d.arrs.clear();
+        d.keep.clear();
+      }
       if (s != kOk) throw CheckError(s, "ff_encode batch launch failed");
     };
     for_each_batch(jobs, base, end, true, one, batch);
@@ -427,8 +436,22 @@ void FixingFloatFilter::decode_messages(Context* ctx, std::vector<FfMessage>& ms
       arrs.push_back(FfDecArray{j.in.ptr, j.out.ptr, j.elems, j.fp->min_value, j.fp->max_value, j.range});
     }
     PSF_HPROF(10);
-    int s = ff_decode_batch_launch(jobs[part[0]].type, jobs[part[0]].nb, arrs.data(), (int)arrs.size(), st,
-                                   ctx->prof());
+    const int type = jobs[part[0]].type, nb = jobs[part[0]].nb;
+    Context::DeferredDecode& d = ctx->deferred;
+    if (ctx->defer_decodes && (d.arrs.empty() || (d.value_type == type && d.nb == nb)) &&
+        d.arrs.size() + arrs.size() <= 64) {
+      // held back: the next batched encode's min/max launch takes it along
+      d.value_type = type;
+      d.nb = nb;
+      d.arrs.insert(d.arrs.end(), arrs.begin(), arrs.end());
+      for (size_t q : part) {
+        d.keep.push_back(jobs[q].in);
+        d.keep.push_back(jobs[q].out);
+      }
+      return;
+    }
+    ctx->flush_deferred();
+    int s = ff_decode_batch_launch(type, nb, arrs.data(), (int)arrs.size(), st, ctx->prof());
     if (s != kOk) throw CheckError(s, "ff_decode batch launch failed");
   };
   for_each_batch(jobs, 0, jobs.size(), false, one, batch);

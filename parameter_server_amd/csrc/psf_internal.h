@@ -69,7 +69,7 @@ __device__ __forceinline__ void publish_crc(PubSlot* s, uint32_t crc, uint32_t t
 // Kernel launch profiler: HIP events recorded on the launch stream around
 // each kernel, plus the kernel's algorithmic HBM bytes.
 enum KernelId { kKMinmax = 0, kKEncode, kKDecode, kKCrc, kKNoise, kKSnappyCompress,
-                kKSnappyDecompress, kKMatch, kKKvPush, kKKvGet, kKNum };
+                kKSnappyDecompress, kKMatch, kKKvPush, kKKvGet, kKDecodeMinmax, kKNum };
 class Profiler {
  public:
   ~Profiler();
@@ -148,8 +148,12 @@ struct FfDecArray {
 };
 bool ff_batchable(const void* x, const void* out, size_t n, int nb, int value_type, bool encode);
 size_t ff_batch_partials_bytes(const FfArray* arrs, int count);
+// dec / ndec / dec_nb: a FIXING_FLOAT decode batch of the same value type,
+// independent of these arrays, launched together with their min/max pass
+// when both fit one small batch (ff_dec_mm_batch), else just before it
 int ff_encode_batch_launch(int value_type, int nb, const FfArray* arrs, int count, void* partials,
-                           PubSlot* pub_base, hipStream_t st, Profiler* prof);
+                           PubSlot* pub_base, hipStream_t st, Profiler* prof, const FfDecArray* dec = nullptr,
+                           int ndec = 0, int dec_nb = 0);
 int ff_decode_batch_launch(int value_type, int nb, const FfDecArray* arrs, int count, hipStream_t st,
                            Profiler* prof);
 

@@ -1,9 +1,11 @@
-#!/bin/bash
-# C1 (the device ctr triple): batch/parity tests, host time per section, the bench line at two step counts
-cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out
-if [ -z "$NOTEST" ]; then timeout -k 10 300 python -u -m pytest tests/test_gpu_batch.py tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread 2>&1 | tail -3; fi
-timeout -k 10 200 python tools/host_prof.py 2>&1 | grep -v amdgpu
-for s in 20 200; do
-timeout -k 10 300 python bench.py --config c1 --no-cpu-baseline --steps $s 2>&1 | grep -v amdgpu | python -c "import json,sys; d=json.loads(sys.stdin.read()); print($s, d['value'], d['ms_per_step'], json.dumps(d['host']))"
-done
-timeout -k 10 300 python bench.py --config c1 --no-cpu-baseline --no-profile 2>&1 | grep -v amdgpu | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('noprof', d['value'], d['ms_per_step'])"
+# C1 (ctr triple x 64 streams): the bench line (with config_wire) and the
+# host-section profile (diagnostic build tools/variants/hprof).
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+O=gpurun_out/${1:-c1}; mkdir -p $O
+timeout -k 10 300 python bench.py --config c1 --no-cpu-baseline > $O/bench_c1.json 2> $O/bench_c1.err || { tail -20 $O/bench_c1.err; exit 1; }
+python -c "import json,sys; d=json.load(open(sys.argv[1])); print('c1', d['value'], d['ms_per_step'], d['host'], d.get('config_wire')); print({k: (v['launches'], v['avg_us']) for k, v in d['roofline']['kernels'].items()})" $O/bench_c1.json
+if [ -f tools/variants/hprof/libpsf.so ]; then
+  timeout -k 10 200 python tools/host_prof.py > $O/hprof_c1.txt 2>&1 || exit 1
+  cat $O/hprof_c1.txt
+fi
