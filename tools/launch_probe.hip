@@ -1,0 +1,102 @@
+// Probe: host time per kernel launch against the size of the kernel-argument
+// struct (16 B .. 16 KiB), launched back to back on one stream (an empty
+// kernel that reads one word of its arguments), and the same five launches
+// replayed as a hipGraph.  Prints microseconds of host time per launch.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+
+#include <chrono>
+
+template <int N>
+struct Big {
+  unsigned v[N];
+};
+template <int N>
+__global__ void k(Big<N> b, unsigned* out) {
+  if (threadIdx.x == 0 && b.v[N - 1] == 0xdeadbeefu) out[blockIdx.x] = b.v[0];
+}
+
+static double now_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+template <int N>
+void run(hipStream_t st, unsigned* d) {
+  static Big<N> b;
+  for (int i = 0; i < N; ++i) b.v[i] = i;
+  for (int i = 0; i < 50; ++i) hipLaunchKernelGGL(k<N>, dim3(64), dim3(256), 0, st, b, d);
+  hipStreamSynchronize(st);
+  const int R = 2000;
+  double best = 1e30;
+  for (int rep = 0; rep < 3; ++rep) {
+    const double t0 = now_us();
+    for (int i = 0; i < R; ++i) {
+      b.v[0] = i;
+      hipLaunchKernelGGL(k<N>, dim3(64), dim3(256), 0, st, b, d);
+    }
+    const double t1 = now_us();
+    hipStreamSynchronize(st);
+    const double t2 = now_us();
+    if ((t1 - t0) / R < best) best = (t1 - t0) / R;
+    if (rep == 2) printf("kernarg %6zu B: host %.2f us/launch (enqueue), %.2f us/launch incl. drain\n", sizeof(Big<N>), best, (t2 - t0) / R);
+  }
+}
+
+template <int N>
+void run_graph(hipStream_t st, unsigned* d) {
+  static Big<N> b;
+  hipGraph_t g;
+  hipGraphExec_t ge;
+  hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal);
+  for (int j = 0; j < 5; ++j) hipLaunchKernelGGL(k<N>, dim3(64), dim3(256), 0, st, b, d);
+  hipStreamEndCapture(st, &g);
+  hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+  size_t nn = 0;
+  hipGraphGetNodes(g, nullptr, &nn);
+  hipGraphNode_t nodes[8];
+  hipGraphGetNodes(g, nodes, &nn);
+  for (int i = 0; i < 20; ++i) hipGraphLaunch(ge, st);
+  hipStreamSynchronize(st);
+  const int R = 400;
+  const double t0 = now_us();
+  for (int i = 0; i < R; ++i) {
+    b.v[0] = i;  // new arguments for every node, as a replay with updated jobs would need
+    for (size_t j = 0; j < nn; ++j) {
+      hipKernelNodeParams p;
+      hipGraphKernelNodeGetParams(nodes[j], &p);
+      void* args[2] = {&b, &d};
+      p.kernelParams = args;
+      hipGraphExecKernelNodeSetParams(ge, nodes[j], &p);
+    }
+    hipGraphLaunch(ge, st);
+  }
+  const double t1 = now_us();
+  hipStreamSynchronize(st);
+  const double t2 = now_us();
+  printf("graph of 5, kernarg %6zu B, params updated: host %.2f us per 5 launches, %.2f incl. drain\n", sizeof(Big<N>),
+         (t1 - t0) / R, (t2 - t0) / R);
+  const double t3 = now_us();
+  for (int i = 0; i < R; ++i) hipGraphLaunch(ge, st);
+  const double t4 = now_us();
+  hipStreamSynchronize(st);
+  printf("graph of 5, kernarg %6zu B, replay only: host %.2f us per 5 launches\n", sizeof(Big<N>), (t4 - t3) / R);
+  hipGraphExecDestroy(ge);
+  hipGraphDestroy(g);
+}
+
+int main() {
+  hipStream_t st;
+  hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+  unsigned* d;
+  hipMalloc(&d, 64 * 4);
+  run<4>(st, d);
+  run<64>(st, d);
+  run<256>(st, d);
+  run<1024>(st, d);
+  run<2048>(st, d);
+  run<4096>(st, d);
+  run_graph<4>(st, d);
+  run_graph<1024>(st, d);
+  hipFree(d);
+  return 0;
+}
