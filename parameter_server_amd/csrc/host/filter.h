@@ -49,7 +49,11 @@ class KeyCachingFilter : public Filter {
   void encode_with(Message* msg, uint32_t sig);
   void decode_with(Message* msg, uint32_t sig);
   static bool needs_signature(Message* msg, bool encode);
-  size_t cache_size() const { return cache_.size(); }
+  size_t cache_size() const {  // live entries (a cleared entry is kept, reset)
+    size_t n = 0;
+    for (const auto& kv : cache_) n += kv.second.key.empty() ? 0 : 1;
+    return n;
+  }
 
  private:
   struct CacheKey {

@@ -75,7 +75,10 @@ void KeyCachingFilter::encode_with(Message* msg, uint32_t sig) {
     e.sig = sig;
     e.key = msg->key;
   }
-  if (conf->clear_cache_if_done && is_done(msg->task)) cache_.erase(ck);
+  // cache_.erase(ck): the entry is reset instead (an absent entry and a reset
+  // one read the same, sig 0 with no key, and the node is not freed and
+  // reallocated every round trip)
+  if (conf->clear_cache_if_done && is_done(msg->task)) e = Entry{};
 }
 
 void KeyCachingFilter::decode(Message* msg) {  // key_caching.h:36-60
@@ -102,7 +105,7 @@ void KeyCachingFilter::decode_with(Message* msg, uint32_t got) {
     if (sig != e.sig) throw CheckError(kErrCheck, "KEY_CACHING: cache miss on decode");
     msg->set_key(e.key);
   }
-  if (conf->clear_cache_if_done && is_done(msg->task)) cache_.erase(ck);
+  if (conf->clear_cache_if_done && is_done(msg->task)) e = Entry{};  // (as in encode_with)
 }
 
 // -------------------------------------------------------- FIXING_FLOAT ----
@@ -192,22 +195,41 @@ void alloc_outputs(Context* ctx, std::vector<FfJob>& jobs, size_t b, size_t e,
 }
 
 // jobs [b, e) grouped for batched launches: same (type, nb), batchable
-template <typename F>
-void for_each_batch(std::vector<FfJob>& jobs, size_t b, size_t e, bool encode, F&& launch_one,
-                    std::function<void(std::vector<size_t>&)> launch_batch) {
-  std::map<std::pair<int, int>, std::vector<size_t>> groups;
+// (groups in a flat list: a batch almost always has one)
+template <typename F, typename G>
+void for_each_batch(std::vector<FfJob>& jobs, size_t b, size_t e, bool encode, F&& launch_one, G&& launch_batch) {
+  struct Group {
+    int type, nb;
+    std::vector<size_t> q;
+  };
+  std::vector<Group> groups;
   for (size_t q = b; q < e; ++q) {
     FfJob& j = jobs[q];
     // a stored-layout output is written by the batched kernel only, even alone
-    if ((e - b > 1 || j.stored) && ff_batchable(j.in.ptr, j.out.ptr, j.elems, j.nb, j.type, encode))
-      groups[{j.type, j.nb}].push_back(q);
-    else
+    if ((e - b > 1 || j.stored) && ff_batchable(j.in.ptr, j.out.ptr, j.elems, j.nb, j.type, encode)) {
+      Group* g = nullptr;
+      for (auto& x : groups)
+        if (x.type == j.type && x.nb == j.nb) g = &x;
+      if (!g) {
+        groups.push_back(Group{j.type, j.nb, {}});
+        g = &groups.back();
+        g->q.reserve(e - b);
+      }
+      g->q.push_back(q);
+    } else {
       launch_one(q);
+    }
   }
+  std::sort(groups.begin(), groups.end(),  // (type, nb) order, as before
+            [](const Group& x, const Group& y) { return x.type != y.type ? x.type < y.type : x.nb < y.nb; });
   for (auto& g : groups) {
-    for (size_t k = 0; k < g.second.size(); k += kFfBatchMax) {
-      std::vector<size_t> part(g.second.begin() + k,
-                               g.second.begin() + std::min(g.second.size(), k + (size_t)kFfBatchMax));
+    if (g.q.size() <= (size_t)kFfBatchMax) {
+      if (g.q.size() == 1 && !jobs[g.q[0]].stored) launch_one(g.q[0]);
+      else launch_batch(g.q);
+      continue;
+    }
+    for (size_t k = 0; k < g.q.size(); k += kFfBatchMax) {
+      std::vector<size_t> part(g.q.begin() + k, g.q.begin() + std::min(g.q.size(), k + (size_t)kFfBatchMax));
       if (part.size() == 1 && !jobs[part[0]].stored) launch_one(part[0]);
       else launch_batch(part);
     }

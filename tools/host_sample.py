@@ -33,6 +33,8 @@ def main():
     dt = (time.perf_counter() - t0) / steps * 1e6
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     n = S.sampler_stop(os.path.join(ROOT, "gpurun_out", "host_samples.txt").encode())
+    import shutil  # the library the addresses belong to, for the report
+    shutil.copy(os.path.join(ROOT, "parameter_server_amd", "libpsf.so"), os.path.join(ROOT, "gpurun_out", "host_samples_libpsf.so"))
     print(f"step {dt:.1f} us, {n} samples")
 
 

@@ -16,6 +16,15 @@ __global__ void k(Big<N> b, unsigned* out) {
   if (threadIdx.x == 0 && b.v[N - 1] == 0xdeadbeefu) out[blockIdx.x] = b.v[0];
 }
 
+// a kernel that keeps the GPU busy for about `cycles` clocks
+template <int N>
+__global__ void busy(Big<N> b, unsigned* out, long long cycles) {
+  const long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < cycles) {
+  }
+  if (threadIdx.x == 0 && b.v[N - 1] == 0xdeadbeefu) out[blockIdx.x] = b.v[0];
+}
+
 static double now_us() {
   return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -84,6 +93,31 @@ void run_graph(hipStream_t st, unsigned* d) {
   hipGraphDestroy(g);
 }
 
+// five different kernels (template instances) of ~10 us each, back to back
+// as a C1 iteration issues them, 40 rounds: host time per launch while the
+// GPU is busy
+template <int N>
+void run_busy(hipStream_t st, unsigned* d) {
+  static Big<N + 4> b;  // (the larger instances read a prefix of it)
+  const long long cyc = 10 * 100;  // wall_clock64 runs at 100 MHz: 10 us
+  for (int i = 0; i < 10; ++i) hipLaunchKernelGGL(busy<N>, dim3(256), dim3(256), 0, st, *reinterpret_cast<Big<N>*>(&b), d, cyc);
+  hipStreamSynchronize(st);
+  const int R = 40;
+  const double t0 = now_us();
+  for (int i = 0; i < R; ++i) {
+    hipLaunchKernelGGL(busy<N>, dim3(256), dim3(256), 0, st, *reinterpret_cast<Big<N>*>(&b), d, cyc);
+    hipLaunchKernelGGL(busy<N + 1>, dim3(256), dim3(256), 0, st, *reinterpret_cast<Big<N + 1>*>(&b), d, cyc);
+    hipLaunchKernelGGL(busy<N + 2>, dim3(256), dim3(256), 0, st, *reinterpret_cast<Big<N + 2>*>(&b), d, cyc);
+    hipLaunchKernelGGL(busy<N + 3>, dim3(256), dim3(256), 0, st, *reinterpret_cast<Big<N + 3>*>(&b), d, cyc);
+    hipLaunchKernelGGL(busy<N + 4>, dim3(256), dim3(256), 0, st, *reinterpret_cast<Big<N + 4>*>(&b), d, cyc);
+  }
+  const double t1 = now_us();
+  hipStreamSynchronize(st);
+  const double t2 = now_us();
+  printf("busy GPU, 5 kernels x %d rounds, kernarg %zu B: host %.2f us/launch (enqueue), GPU %.2f us/launch\n", R,
+         sizeof(Big<N>), (t1 - t0) / (5 * R), (t2 - t0) / (5 * R));
+}
+
 int main() {
   hipStream_t st;
   hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
@@ -95,6 +129,8 @@ int main() {
   run<1024>(st, d);
   run<2048>(st, d);
   run<4096>(st, d);
+  run_busy<4>(st, d);
+  run_busy<1024>(st, d);
   run_graph<4>(st, d);
   run_graph<1024>(st, d);
   hipFree(d);

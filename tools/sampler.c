@@ -1,10 +1,11 @@
 // Diagnostic: a sampling profiler for the host side of a run (no perf on the
-// GPU box).  sampler_start(us) arms ITIMER_PROF; each SIGPROF that lands on
-// the thread that called sampler_start records up to 8 return addresses
-// (backtrace(), primed before arming).  sampler_stop(path) disarms and writes
+// GPU box).  sampler_start(us) arms a POSIX CLOCK_MONOTONIC timer aimed at
+// the calling thread (ITIMER_PROF only ticks at the scheduler's rate, a few
+// ms); each SIGPROF records up to 8 return addresses (backtrace(), primed
+// before arming).  Wall-clock sampling: blocked time is sampled too.  sampler_stop(path) disarms and writes
 // the samples plus /proc/self/maps to `path`; tools/sampler_report.py
 // resolves them against the built libraries.  Build:
-//   gcc -O2 -shared -fPIC -o tools/libsampler.so tools/sampler.c
+//   gcc -O2 -shared -fPIC -o tools/libsampler.so tools/sampler.c -lrt
 #define _GNU_SOURCE
 #include <execinfo.h>
 #include <signal.h>
@@ -13,6 +14,7 @@
 #include <string.h>
 #include <sys/syscall.h>
 #include <sys/time.h>
+#include <time.h>
 #include <unistd.h>
 
 #define MAXS 200000
@@ -22,6 +24,7 @@ static unsigned char g_depth[MAXS];
 static atomic_int g_n;
 static pid_t g_tid;
 static atomic_int g_other;
+static timer_t g_timer;
 
 static void on_prof(int sig, siginfo_t* si, void* uc) {
   (void)sig;
@@ -48,17 +51,21 @@ int sampler_start(int period_us) {
   sa.sa_flags = SA_SIGINFO | SA_RESTART;
   sigemptyset(&sa.sa_mask);
   if (sigaction(SIGPROF, &sa, NULL)) return -1;
-  struct itimerval it;
+  struct sigevent ev;
+  memset(&ev, 0, sizeof ev);
+  ev.sigev_notify = SIGEV_THREAD_ID;
+  ev.sigev_signo = SIGPROF;
+  ev._sigev_un._tid = g_tid;
+  if (timer_create(CLOCK_MONOTONIC, &ev, &g_timer)) return -2;
+  struct itimerspec it;
   it.it_interval.tv_sec = 0;
-  it.it_interval.tv_usec = period_us;
+  it.it_interval.tv_nsec = (long)period_us * 1000;
   it.it_value = it.it_interval;
-  return setitimer(ITIMER_PROF, &it, NULL);
+  return timer_settime(g_timer, 0, &it, NULL);
 }
 
 int sampler_stop(const char* path) {
-  struct itimerval it;
-  memset(&it, 0, sizeof it);
-  setitimer(ITIMER_PROF, &it, NULL);
+  timer_delete(g_timer);
   signal(SIGPROF, SIG_IGN);
   FILE* f = fopen(path, "w");
   if (!f) return -1;

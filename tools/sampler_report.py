@@ -24,10 +24,16 @@ def load(path):
     return samples, maps
 
 
+LIBDIR = None  # directory holding the sampled run's copy of libpsf.so (host_samples_libpsf.so)
+
+
 class Symbols:
     def __init__(self, path):
         self.addrs, self.names = [], []
         local = path
+        if LIBDIR and os.path.basename(path) == "libpsf.so" and os.path.exists(os.path.join(LIBDIR, "host_samples_libpsf.so")):
+            path = os.path.join(LIBDIR, "host_samples_libpsf.so")
+            local = path
         if "/gpurun" in path or "graft" in path or not os.path.exists(path):
             base = os.path.basename(path)
             for cand in (os.path.join(ROOT, "parameter_server_amd", base), os.path.join(ROOT, "tools", base)):
@@ -54,11 +60,17 @@ class Symbols:
 
 
 def main():
-    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    argv = sys.argv[1:]
+    if "--top" in argv:
+        i = argv.index("--top")
+        argv = argv[:i] + argv[i + 2:]
+    args = [a for a in argv if not a.startswith("--")]
     top = 40
     if "--top" in sys.argv:
         top = int(sys.argv[sys.argv.index("--top") + 1])
     path = args[0] if args else os.path.join(ROOT, "gpurun_out", "host_samples.txt")
+    global LIBDIR
+    LIBDIR = os.path.dirname(os.path.abspath(path))
     samples, maps = load(path)
     base = {}
     for lo, hi, off, p in maps:
@@ -105,5 +117,45 @@ def main():
         print(f"{100 * c / n:6.2f}%  {nm[:150]}")
 
 
+
+
+def by_first_own_frame(path, lib="libpsf", top=30):
+    """samples charged to the innermost frame in `lib` (its own time plus the
+    library / runtime calls it makes); samples with no such frame in the
+    recorded depth are counted as '(deeper)'"""
+    global LIBDIR
+    LIBDIR = os.path.dirname(os.path.abspath(path))
+    samples, maps = load(path)
+    base = {}
+    for lo, hi, off, p in maps:
+        if off == 0 and p not in base:
+            base[p] = lo
+    syms = {}
+    cache = {}
+    c = collections.Counter()
+    for fr in samples:
+        name = "(deeper)"
+        for d, a in enumerate(fr[2:]):
+            if a not in cache:
+                cache[a] = None
+                for lo, hi, off, p in maps:
+                    if lo <= a - 1 < hi and lib in p:
+                        if p not in syms:
+                            syms[p] = Symbols(p)
+                        cache[a] = syms[p].name(a - 1 - base.get(p, lo))
+                        break
+            if cache[a]:
+                name = cache[a]
+                break
+        c[name] += 1
+    n = len(samples)
+    for nm, k in c.most_common(top):
+        print(f"{100 * k / n:6.2f}%  {nm[:160]}")
+
+
 if __name__ == "__main__":
-    main()
+    if "--own" in sys.argv:
+        a = [x for x in sys.argv[1:] if not x.startswith("--")]
+        by_first_own_frame(a[0] if a else os.path.join(ROOT, "gpurun_out", "host_samples.txt"))
+    else:
+        main()
