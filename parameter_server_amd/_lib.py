@@ -164,7 +164,7 @@ SIGNATURES = {
 
 KERNELS = ("ff_minmax_partials", "ff_encode", "ff_decode", "crc32c_chunks", "noise_add",
            "snappy_compress", "snappy_decompress", "ordered_match", "kvmap_push", "kvmap_get",
-           "ff_decode_minmax")
+           "ff_decode_minmax", "ff_minmax_encode")
 OP_ASSIGN, OP_PLUS, OP_MINUS, OP_TIMES, OP_DIVIDE = 0, 1, 2, 3, 4
 
 _lib = None

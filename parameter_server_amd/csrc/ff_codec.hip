@@ -930,6 +930,7 @@ struct FfBatchT {
 static_assert(sizeof(FfBatchT<kBatchSmall>) <= 4096, "the small batch fits 4 KiB of kernel arguments");
 static_assert(sizeof(FfBatchT<kFfBatchMax>) <= 32000, "the large batch fits the kernel-argument segment");
 static_assert(kMinmaxGrid <= 0xFFFF, "FfJob::mm_nwg is 16 bits");
+static_assert(kBatchSmall == kFusedArrays, "one ready counter per array of a small batch");
 
 
 // the job whose [first, first + count) workgroup range holds b: a fully
@@ -970,14 +971,40 @@ __device__ __forceinline__ void tile_range_of(size_t ntiles, uint32_t wg, uint32
 
 // the batched kernels' bodies take their workgroup index: a merged launch
 // (ff_dec_mm_batch) runs a decode batch and a min/max batch side by side
+// ---- the in-launch hand-off of ff_fused_batch: an array's min/max items
+// (its share of the min/max grid) are claimed and folded by the array's own
+// encode workgroups, which then wait until every item is folded.  Per-XCD L2s
+// are not coherent and a CU's L1 is never refreshed by another CU's stores
+// (MI355X_MICROARCH.md, inter-workgroup visibility): each partial is stored
+// write-through (an agent-scope atomic store, `sc1`), the storing wave drains
+// its stores, then one lane adds to the array's ready counter (agent scope);
+// a waiting workgroup polls that counter with `sc1` loads, joins a barrier and
+// loads the partials `sc1`.  Every item is claimed by a workgroup that is
+// already running before anyone waits for it, so no dispatch order can
+// deadlock it.  Per array one 128-byte line of counters: [0] claims, [1]
+// items folded, [2] workgroups done -- the last one done zeroes the line for
+// the next launch on the stream.  Bounded: a wait that outlasts kHandoffTicks
+// gives up and the array reports kErrHip.
+#ifdef PSF_FUSED_DEBUG
+constexpr uint64_t kHandoffTicks = 20000000ull;
+#else
+constexpr uint64_t kHandoffTicks = 200000000ull;  // 2 s of the 100 MHz wall clock
+#endif
+constexpr uint32_t kFusedLine = 32;               // u32 per array's counter line
+__device__ __forceinline__ bool wait_ready(const uint32_t* c, uint32_t want) {
+  const uint64_t t0 = wall_clock64();
+  while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+    if (wall_clock64() - t0 > kHandoffTicks) return false;
+    __builtin_amdgcn_s_sleep(8);
+  }
+  return true;
+}
+
+// min/max partial bb (of job jb) of a batch; ready: ff_fused_batch's counter
+// of folded items (null: a plain launch, the kernel boundary publishes it)
 template <typename V, int CAP>
-__device__ __forceinline__ void minmax_batch_body(const FfBatchT<CAP>& B, uint32_t block) {
+__device__ __forceinline__ void minmax_item(const FfBatchT<CAP>& B, int jb, uint32_t bb, uint32_t* ready) {
   typedef typename KeyOf<V>::K K;
-  // mm_reverse: workgroups dispatched last-array-first, so the arrays the
-  // encode reads first are the ones read last here (still in the Infinity
-  // Cache when the encode starts)
-  const uint32_t bb = B.mm_reverse ? B.mm_total - 1 - block : block;
-  const int jb = batch_job(B, bb, true);
   const FfJob& J = B.job[jb];
   const V* __restrict__ x = static_cast<const V*>(J.x);
   const size_t n = J.n;
@@ -1038,9 +1065,24 @@ __device__ __forceinline__ void minmax_batch_body(const FfBatchT<CAP>& B, uint32
   block_minmax(lo, hi);
   if (threadIdx.x == 0) {
     K* pp = reinterpret_cast<K*>(B.partials);
-    pp[bb] = lo;
-    pp[B.mm_total + bb] = hi;
+    if (ready) {
+      __hip_atomic_store(&pp[bb], lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&pp[B.mm_total + bb], hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_fetch_add(ready, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      pp[bb] = lo;
+      pp[B.mm_total + bb] = hi;
+    }
   }
+}
+template <typename V, int CAP>
+__device__ __forceinline__ void minmax_batch_body(const FfBatchT<CAP>& B, uint32_t block) {
+  // mm_reverse: workgroups dispatched last-array-first, so the arrays the
+  // encode reads first are the ones read last here (still in the Infinity
+  // Cache when the encode starts)
+  const uint32_t bb = B.mm_reverse ? B.mm_total - 1 - block : block;
+  minmax_item<V, CAP>(B, batch_job(B, bb, true), bb, nullptr);
 }
 template <typename V, int CAP>
 __global__ __launch_bounds__(kBlock) void ff_minmax_batch(FfBatchT<CAP> B) {
@@ -1049,14 +1091,16 @@ __global__ __launch_bounds__(kBlock) void ff_minmax_batch(FfBatchT<CAP> B) {
 
 // kStored: the instantiation launched when a job of the batch writes a
 // stored stream (its extra registers stay out of the plain one's occupancy)
+// fused: ff_fused_batch's counter lines (this array's min/max items are folded
+// by its encode workgroups in the same launch); returns the job
 template <typename V, int NB, int CAP, bool kStored>
-__global__ __launch_bounds__(kBlock) void ff_encode_batch(FfBatchT<CAP> B) {
-  const int jb = batch_job(B, blockIdx.x, false);
+__device__ __forceinline__ int encode_batch_body(const FfBatchT<CAP>& B, uint32_t block, uint32_t* fused) {
+  const int jb = batch_job(B, block, false);
   const FfJob& J = B.job[jb];
   const V* __restrict__ x = static_cast<const V*>(J.x);
   uint8_t* __restrict__ out = static_cast<uint8_t*>(J.out);
   const size_t n = J.n;
-  const uint32_t wg = blockIdx.x - B.first[jb];
+  const uint32_t wg = block - B.first[jb];
   const uint32_t nwg = batch_nwg(B, jb);
   const uint32_t mm_wg0 = B.mm_first[jb];
   const size_t ngroups = n >> 2;
@@ -1083,14 +1127,47 @@ __global__ __launch_bounds__(kBlock) void ff_encode_batch(FfBatchT<CAP> B) {
   };
   if (t0 < tf) load_tile(t0);
   float mn_f = J.mn, mx_f = J.mx;
+  bool late = false;  // the in-launch hand-off gave up (never expected)
   if (J.mm_nwg) {
     typedef typename KeyOf<V>::K K;
-    const K* pp = reinterpret_cast<const K*>(B.partials);
+    K* pp = reinterpret_cast<K*>(B.partials);
     K lo = KeyOf<V>::kLoId, hi = KeyOf<V>::kHiId;
-    for (uint32_t i = threadIdx.x; i < J.mm_nwg; i += kBlock) {
-      const K a = pp[mm_wg0 + i], b = pp[B.mm_total + mm_wg0 + i];
-      lo = a < lo ? a : lo;
-      hi = b > hi ? b : hi;
+    if (fused) {
+      uint32_t* c = fused + kFusedLine * jb;
+      __shared__ uint32_t s_item, s_late;
+      for (uint32_t k = 0;; ++k) {  // claim this array's min/max items until none is left
+        if (threadIdx.x == 0) s_item = __hip_atomic_fetch_add(&c[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        const uint32_t item = s_item;
+        __syncthreads();
+        if (item >= J.mm_nwg) break;
+#ifdef PSF_FUSED_DEBUG
+        if (k > J.mm_nwg) {
+          if (threadIdx.x == 0) printf("fused: job %d wg %u claim loop k=%u item=%u mm_nwg=%u\n", jb, wg, k, item, (uint32_t)J.mm_nwg);
+          break;
+        }
+#endif
+        minmax_item<V, CAP>(B, jb, mm_wg0 + item, &c[1]);
+      }
+      if (threadIdx.x == 0) s_late = wait_ready(&c[1], J.mm_nwg) ? 0u : 1u;
+#ifdef PSF_FUSED_DEBUG
+      if (threadIdx.x == 0 && s_late)
+        printf("fused: job %d wg %u timed out: claims %u ready %u done %u want %u\n", jb, wg, c[0], c[1], c[2], (uint32_t)J.mm_nwg);
+#endif
+      __syncthreads();
+      late = s_late != 0;
+      for (uint32_t i = threadIdx.x; i < J.mm_nwg; i += kBlock) {
+        const K a = __hip_atomic_load(&pp[mm_wg0 + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const K b = __hip_atomic_load(&pp[B.mm_total + mm_wg0 + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        lo = a < lo ? a : lo;
+        hi = b > hi ? b : hi;
+      }
+    } else {
+      for (uint32_t i = threadIdx.x; i < J.mm_nwg; i += kBlock) {
+        const K a = pp[mm_wg0 + i], b = pp[B.mm_total + mm_wg0 + i];
+        lo = a < lo ? a : lo;
+        hi = b > hi ? b : hi;
+      }
     }
     block_minmax(lo, hi);
     float cmn, cmx;
@@ -1117,7 +1194,7 @@ __global__ __launch_bounds__(kBlock) void ff_encode_batch(FfBatchT<CAP> B) {
   q.scale_f = (float)q.scale;
   q.fast = q.bin < __builtin_huge_val();
   if (wg == 0 && threadIdx.x == 0) {
-    const int status = (q.bin > 0) ? kOk : kErrBin;
+    const int status = late ? kErrHip : (q.bin > 0) ? kOk : kErrBin;
     if (J.lazy != kNoLazy) {
       float* r = B.range_base + 4 * (uint32_t)J.lazy;  // read by a later decode on this stream
       r[0] = mn_f;
@@ -1138,7 +1215,7 @@ __global__ __launch_bounds__(kBlock) void ff_encode_batch(FfBatchT<CAP> B) {
       publish_ticket(ps, J.ticket);
     }
   }
-  if (!(q.bin > 0)) return;  // CHECK_GT(bin, 0), fixing_float.h:71
+  if (!(q.bin > 0) || late) return jb;  // CHECK_GT(bin, 0), fixing_float.h:71
 
   EncodeParams p{};  // the per-launch constants the tile code reads
   p.lcg_bits = B.lcg_bits;
@@ -1199,6 +1276,12 @@ __global__ __launch_bounds__(kBlock) void ff_encode_batch(FfBatchT<CAP> B) {
       }
     }
   }
+  return jb;
+}
+
+template <typename V, int NB, int CAP, bool kStored>
+__global__ __launch_bounds__(kBlock) void ff_encode_batch(FfBatchT<CAP> B) {
+  encode_batch_body<V, NB, CAP, kStored>(B, blockIdx.x, nullptr);
 }
 
 template <typename V, int NB, int CAP>
@@ -1244,6 +1327,31 @@ template <typename V, int NB>
 __global__ __launch_bounds__(kBlock) void ff_dec_mm_batch(FfBatchT<kBatchSmall> D, FfBatchT<kBatchSmall> M) {
   if (blockIdx.x < D.total) decode_batch_body<V, NB, kBatchSmall>(D, blockIdx.x);
   else minmax_batch_body<V, kBatchSmall>(M, blockIdx.x - D.total);
+}
+// One launch for a small batch's min/max and encode, with a pending decode
+// batch of the same value type and num_bytes in front (the round trip
+// driver's decode of one phase): workgroups [0, D.total) decode, the rest
+// encode, each array's encode workgroups folding its min/max items first (the
+// hand-off above); the last of an array's workgroups to finish zeroes its
+// counter line.
+template <typename V, int NB, bool kStored>
+__global__ __launch_bounds__(kBlock) void ff_fused_batch(FfBatchT<kBatchSmall> D, FfBatchT<kBatchSmall> B, uint32_t* ctl) {
+  if (blockIdx.x < D.total) {
+    decode_batch_body<V, NB, kBatchSmall>(D, blockIdx.x);
+    return;
+  }
+  const int jb = encode_batch_body<V, NB, kBatchSmall, kStored>(B, blockIdx.x - D.total, ctl);
+  if (B.job[jb].mm_nwg) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t* c = ctl + kFusedLine * jb;
+      if (__hip_atomic_fetch_add(&c[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == batch_nwg(B, jb) - 1) {
+        __hip_atomic_store(&c[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&c[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&c[2], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
 }
 
 // ------------------------------------------------------------ launchers ----
@@ -1567,10 +1675,32 @@ template <int CAP>
 static int fill_decode_batch(FfBatchT<CAP>& B, int value_type, int nb, const FfDecArray* arrs, int count,
                              double* bytes_out);
 
+// PSF_FF_FUSED (A/B knob, tools/): 1 runs a small batch's min/max and encode
+// in one launch (ff_fused_batch); unset / 0: two launches
+static bool fused_mode() {
+  static const bool on = [] {
+    const char* e = getenv("PSF_FF_FUSED");
+    return e && *e == '1';
+  }();
+  return on;
+}
+
+template <typename V, int NB>
+static void launch_fused(const FfBatchT<kBatchSmall>& D, const FfBatchT<kBatchSmall>& B, dim3 grid, hipStream_t st,
+                         FfFusedCtl* fc, bool stored) {
+  if constexpr (NB == 1 || NB == 2) {
+    if (stored) {
+      hipLaunchKernelGGL((ff_fused_batch<V, NB, true>), grid, dim3(kBlock), 0, st, D, B, fc->ctl);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((ff_fused_batch<V, NB, false>), grid, dim3(kBlock), 0, st, D, B, fc->ctl);
+}
+
 template <int CAP>
 static int encode_batch_cap(int value_type, int nb, const FfArray* arrs, int count, void* partials,
                             PubSlot* pub_base, hipStream_t st, Profiler* prof, const FfDecArray* dec, int ndec,
-                            int dec_nb) {
+                            int dec_nb, FfFusedCtl* fused) {
   static FfBatchT<CAP> B;  // host staging of the kernel arguments (launches are serialised per thread)
   static std::mutex mu;
   std::lock_guard<std::mutex> lock(mu);
@@ -1650,6 +1780,40 @@ static int encode_batch_cap(int value_type, int nb, const FfArray* arrs, int cou
   B.total = enc;
   B.mm_total = mm;
   B.mm_reverse = mm_reverse_mode(bytes_mm) ? 1u : 0u;
+  if constexpr (CAP == kBatchSmall) {
+    // min/max, encode and the pending decode (same num_bytes) in one launch
+    if (fused && fused->ctl && B.mm_total > 0 && (ndec <= 0 || (ndec <= kBatchSmall && dec_nb == nb)) &&
+        fused_mode()) {
+      static FfBatchT<kBatchSmall> D;
+      double bytes_dec = 0;
+      if (ndec > 0) {
+        const int fs = fill_decode_batch<kBatchSmall>(D, value_type, dec_nb, dec, ndec, &bytes_dec);
+        if (fs != kOk) return fs;
+      } else {
+        memset(&D, 0, sizeof(D));
+      }
+      bool stored = false;
+      for (int i = 0; i < count; ++i) stored |= (B.job[i].flags & kFlagStored) != 0;
+      const dim3 grid(D.total + enc);  // (the min/max items run in the encode workgroups)
+      {
+        ProfScope pf(prof, kKFused, st, bytes_dec + bytes_mm + bytes_enc);
+        if (value_type == kFloat) {
+          switch (nb) {
+            case 1: launch_fused<float, 1>(D, B, grid, st, fused, stored); break;
+            case 2: launch_fused<float, 2>(D, B, grid, st, fused, stored); break;
+            default: launch_fused<float, 3>(D, B, grid, st, fused, stored); break;
+          }
+        } else {
+          switch (nb) {
+            case 1: launch_fused<double, 1>(D, B, grid, st, fused, stored); break;
+            case 2: launch_fused<double, 2>(D, B, grid, st, fused, stored); break;
+            default: launch_fused<double, 3>(D, B, grid, st, fused, stored); break;
+          }
+        }
+      }
+      return launch_status();
+    }
+  }
   if (ndec > 0) {
     // the pending decode batch: in the min/max launch when both are small
     // (one launch instead of two), else on its own first
@@ -1701,14 +1865,14 @@ static int encode_batch_cap(int value_type, int nb, const FfArray* arrs, int cou
 
 int ff_encode_batch_launch(int value_type, int nb, const FfArray* arrs, int count, void* partials,
                            PubSlot* pub_base, hipStream_t st, Profiler* prof, const FfDecArray* dec, int ndec,
-                           int dec_nb) {
+                           int dec_nb, FfFusedCtl* fused) {
   if (count <= 0) return ndec > 0 ? ff_decode_batch_launch(value_type, dec_nb, dec, ndec, st, prof) : kOk;
   if (count > kFfBatchMax) return kErrArg;
   if (value_type != kFloat && value_type != kDouble) return kErrArg;
-  return count <= kBatchSmall
-             ? encode_batch_cap<kBatchSmall>(value_type, nb, arrs, count, partials, pub_base, st, prof, dec, ndec, dec_nb)
-             : encode_batch_cap<kFfBatchMax>(value_type, nb, arrs, count, partials, pub_base, st, prof, dec, ndec,
-                                             dec_nb);
+  return count <= kBatchSmall ? encode_batch_cap<kBatchSmall>(value_type, nb, arrs, count, partials, pub_base, st, prof,
+                                                              dec, ndec, dec_nb, fused)
+                              : encode_batch_cap<kFfBatchMax>(value_type, nb, arrs, count, partials, pub_base, st, prof,
+                                                              dec, ndec, dec_nb, nullptr);
 }
 
 // a decode batch's kernel arguments

@@ -1071,7 +1071,8 @@ int psf_profile_read(psf_context* ctx, int k, int64_t* launches, double* total_m
 const char* psf_profile_kernel_name(int k) {
   static const char* names[] = {"ff_minmax_partials", "ff_encode", "ff_decode", "crc32c_chunks",
                                 "noise_add", "snappy_compress", "snappy_decompress", "ordered_match",
-                                "kvmap_push", "kvmap_get", "ff_decode_minmax"};
+                                "kvmap_push", "kvmap_get", "ff_decode_minmax", "ff_minmax_encode"};
+  static_assert(sizeof(names) / sizeof(names[0]) == psf::kKNum, "one name per kernel id");
   return (k >= 0 && k < psf::kKNum) ? names[k] : "?";
 }
 
@@ -1208,3 +1209,14 @@ int psf_kvmap_stats(psf_kvmap* map, int64_t* nnz, double* weight_sum, double* de
 }
 
 }  // extern "C"
+
+// diagnostic: the context's ff_fused_batch counter words (after a sync)
+extern "C" int psf_debug_fused_ctl(psf_context* ctx, uint32_t* out, int n) {
+  return guarded(ctx ? ctx->impl : nullptr, [&] {
+    psf::FfFusedCtl* f = ctx->impl->fused();
+    if (!f || n < 0 || (size_t)n * 4 > psf::kFusedCtlBytes) return PSF_ERR_ARG;
+    ctx->impl->sync();
+    PSF_HIP_CHECK(hipMemcpy(out, f->ctl, (size_t)n * 4, hipMemcpyDeviceToHost));
+    return PSF_OK;
+  });
+}

@@ -337,6 +337,8 @@ Context::Context(int device, hipStream_t stream, int mode) : device_(device), st
   PSF_HIP_CHECK(hipMalloc(&d_partials_, 2 * sizeof(uint64_t) * kMaxGrid));
   PSF_HIP_CHECK(hipMalloc(&zero_base_, 2 * (kZeroBytes[0] + kZeroBytes[1])));
   PSF_HIP_CHECK(hipMemset(zero_base_, 0, 2 * (kZeroBytes[0] + kZeroBytes[1])));
+  PSF_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&fused_.ctl), kFusedCtlBytes));
+  PSF_HIP_CHECK(hipMemset(fused_.ctl, 0, kFusedCtlBytes));
   PSF_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&d_slots_), sizeof(Slot) * kSlots));
   PSF_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_slots_), sizeof(Slot) * kSlots,
                               hipHostMallocMapped | hipHostMallocCoherent));
@@ -367,6 +369,7 @@ Context::~Context() {
   (void)hipHostFree(lazy_h_);
   (void)hipFree(d_partials_);
   (void)hipFree(zero_base_);
+  (void)hipFree(fused_.ctl);
   (void)hipFree(d_slots_);
   (void)hipHostFree(h_slots_);
   // a private stream's cached blocks go now (buffers still held by messages

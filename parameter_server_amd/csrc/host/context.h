@@ -129,6 +129,7 @@ class Context {
   void give_event(hipEvent_t e);
 
   void* partials() const { return d_partials_; }
+  FfFusedCtl* fused() { return fused_.ctl ? &fused_ : nullptr; }  // ff_fused_batch's counters
   Slot* d_slots() const { return d_slots_; }
   // host-mapped, coherent publish slots: kernels write through pub_dev(i),
   // the host reads pub_host(i)
@@ -217,6 +218,7 @@ class Context {
   uint32_t ticket_ = 0;
   std::vector<hipEvent_t> events_;
   void* zero_base_ = nullptr;
+  FfFusedCtl fused_;
   int zero_parity_[kZeroKinds] = {0, 0};
   Buffer noise_f32_, noise_f64_;
   std::mutex mu_;

@@ -341,7 +341,7 @@ void FixingFloatFilter::encode_messages(Context* ctx, std::vector<FfMessage>& ms
       const bool take = !d.arrs.empty() && d.value_type == jobs[part[0]].type;
       int s = ff_encode_batch_launch(jobs[part[0]].type, jobs[part[0]].nb, arrs.data(), (int)arrs.size(),
                                      scratch.ptr, ctx->pub_dev(0), st, ctx->prof(), take ? d.arrs.data() : nullptr,
-                                     take ? (int)d.arrs.size() : 0, take ? d.nb : 0);
+                                     take ? (int)d.arrs.size() : 0, take ? d.nb : 0, ctx->fused());
       if (take) {
         d.arrs.clear();
         d.keep.clear();

@@ -69,7 +69,7 @@ __device__ __forceinline__ void publish_crc(PubSlot* s, uint32_t crc, uint32_t t
 // Kernel launch profiler: HIP events recorded on the launch stream around
 // each kernel, plus the kernel's algorithmic HBM bytes.
 enum KernelId { kKMinmax = 0, kKEncode, kKDecode, kKCrc, kKNoise, kKSnappyCompress,
-                kKSnappyDecompress, kKMatch, kKKvPush, kKKvGet, kKDecodeMinmax, kKNum };
+                kKSnappyDecompress, kKMatch, kKKvPush, kKKvGet, kKDecodeMinmax, kKFused, kKNum };
 class Profiler {
  public:
   ~Profiler();
@@ -146,14 +146,23 @@ struct FfDecArray {
   float mn, mx;
   const float* range;  // device {min, max} written by the encode, or null (use mn, mx)
 };
+// A context's state for ff_fused_batch (a small batch's min/max, encode and a
+// pending decode in one launch): a 128-byte line of device counters per array
+// slot, zero between launches (the kernel zeroes what it used)
+constexpr int kFusedArrays = 64;  // = kBatchSmall (ff_codec.hip)
+struct FfFusedCtl {
+  uint32_t* ctl = nullptr;
+};
+constexpr size_t kFusedCtlBytes = 128 * kFusedArrays;
 bool ff_batchable(const void* x, const void* out, size_t n, int nb, int value_type, bool encode);
 size_t ff_batch_partials_bytes(const FfArray* arrs, int count);
 // dec / ndec / dec_nb: a FIXING_FLOAT decode batch of the same value type,
 // independent of these arrays, launched together with their min/max pass
 // when both fit one small batch (ff_dec_mm_batch), else just before it
+// fused: the context's FfFusedCtl (null: min/max and encode in two launches)
 int ff_encode_batch_launch(int value_type, int nb, const FfArray* arrs, int count, void* partials,
                            PubSlot* pub_base, hipStream_t st, Profiler* prof, const FfDecArray* dec = nullptr,
-                           int ndec = 0, int dec_nb = 0);
+                           int ndec = 0, int dec_nb = 0, FfFusedCtl* fused = nullptr);
 int ff_decode_batch_launch(int value_type, int nb, const FfDecArray* arrs, int count, hipStream_t st,
                            Profiler* prof);
 
