@@ -980,8 +980,8 @@ __device__ __forceinline__ void tile_range_of(size_t ntiles, uint32_t wg, uint32
 // its stores, then one lane adds to the array's ready counter (agent scope);
 // a waiting workgroup polls that counter with `sc1` loads, joins a barrier and
 // loads the partials `sc1`.  Every item is claimed by a workgroup that is
-// already running before anyone waits for it, so no dispatch order can
-// deadlock it.  Per array one 128-byte line of counters: [0] claims, [1]
+// already running before anyone waits for it (a workgroup claims once, before
+// it waits), so no dispatch order can deadlock it.  Per array one 128-byte line of counters: [0] claims, [1]
 // items folded, [2] workgroups done -- the last one done zeroes the line for
 // the next launch on the stream.  Bounded: a wait that outlasts kHandoffTicks
 // gives up and the array reports kErrHip.
@@ -1135,27 +1135,23 @@ __device__ __forceinline__ int encode_batch_body(const FfBatchT<CAP>& B, uint32_
     if (fused) {
       uint32_t* c = fused + kFusedLine * jb;
       __shared__ uint32_t s_item, s_late;
-      for (uint32_t k = 0;; ++k) {  // claim this array's min/max items until none is left
-        if (threadIdx.x == 0) s_item = __hip_atomic_fetch_add(&c[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __syncthreads();
-        const uint32_t item = s_item;
-        __syncthreads();
-        if (item >= J.mm_nwg) break;
-#ifdef PSF_FUSED_DEBUG
-        if (k > J.mm_nwg) {
-          if (threadIdx.x == 0) printf("fused: job %d wg %u claim loop k=%u item=%u mm_nwg=%u\n", jb, wg, k, item, (uint32_t)J.mm_nwg);
-          break;
-        }
-#endif
-        minmax_item<V, CAP>(B, jb, mm_wg0 + item, &c[1]);
-      }
+      // one claim per workgroup of a run of ceil(items / workgroups) items
+      // (every item then belongs to a workgroup that is running: the first
+      // ones to start take them all); the run's bounds read into scalar
+      // registers, so its loop is uniform for the compiler too
+      const uint32_t per = ((uint32_t)J.mm_nwg + nwg - 1) / nwg;
+      if (threadIdx.x == 0) s_item = __hip_atomic_fetch_add(&c[0], per, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      const uint32_t i0 = __builtin_amdgcn_readfirstlane(s_item);
+      const uint32_t i1 = i0 + per < (uint32_t)J.mm_nwg ? i0 + per : (uint32_t)J.mm_nwg;
+      for (uint32_t item = i0; item < i1; ++item) minmax_item<V, CAP>(B, jb, mm_wg0 + item, &c[1]);
       if (threadIdx.x == 0) s_late = wait_ready(&c[1], J.mm_nwg) ? 0u : 1u;
 #ifdef PSF_FUSED_DEBUG
-      if (threadIdx.x == 0 && s_late)
+      if (threadIdx.x == 0 && s_late != 0)
         printf("fused: job %d wg %u timed out: claims %u ready %u done %u want %u\n", jb, wg, c[0], c[1], c[2], (uint32_t)J.mm_nwg);
 #endif
       __syncthreads();
-      late = s_late != 0;
+      late = __builtin_amdgcn_readfirstlane(s_late) != 0;
       for (uint32_t i = threadIdx.x; i < J.mm_nwg; i += kBlock) {
         const K a = __hip_atomic_load(&pp[mm_wg0 + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const K b = __hip_atomic_load(&pp[B.mm_total + mm_wg0 + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1675,15 +1671,21 @@ template <int CAP>
 static int fill_decode_batch(FfBatchT<CAP>& B, int value_type, int nb, const FfDecArray* arrs, int count,
                              double* bytes_out);
 
-// PSF_FF_FUSED (A/B knob, tools/): 1 runs a small batch's min/max and encode
-// in one launch (ff_fused_batch); unset / 0: two launches
+// PSF_FF_FUSED (A/B knob, tools/): 0 keeps a small batch's min/max and
+// encode in two launches
 static bool fused_mode() {
   static const bool on = [] {
     const char* e = getenv("PSF_FF_FUSED");
-    return e && *e == '1';
+    return !(e && *e == '0');
   }();
   return on;
 }
+// ff_fused_batch only for batches of at most this many encode workgroups:
+// its waiting workgroups hold their slots (and poll), which a launch-bound
+// batch of small arrays (C1: 832) does not notice and one of large arrays
+// does (C5, 8 x 2^24 values, 16384 workgroups: 1.08 ms against 0.20 in two
+// launches, tools/ab_fused.sh r04)
+constexpr uint32_t kFusedMaxEncWgs = 2048;
 
 template <typename V, int NB>
 static void launch_fused(const FfBatchT<kBatchSmall>& D, const FfBatchT<kBatchSmall>& B, dim3 grid, hipStream_t st,
@@ -1782,8 +1784,8 @@ static int encode_batch_cap(int value_type, int nb, const FfArray* arrs, int cou
   B.mm_reverse = mm_reverse_mode(bytes_mm) ? 1u : 0u;
   if constexpr (CAP == kBatchSmall) {
     // min/max, encode and the pending decode (same num_bytes) in one launch
-    if (fused && fused->ctl && B.mm_total > 0 && (ndec <= 0 || (ndec <= kBatchSmall && dec_nb == nb)) &&
-        fused_mode()) {
+    if (fused && fused->ctl && B.mm_total > 0 && enc <= kFusedMaxEncWgs &&
+        (ndec <= 0 || (ndec <= kBatchSmall && dec_nb == nb)) && fused_mode()) {
       static FfBatchT<kBatchSmall> D;
       double bytes_dec = 0;
       if (ndec > 0) {

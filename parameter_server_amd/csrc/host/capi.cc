@@ -637,8 +637,8 @@ int psf_node_roundtrip_ex(psf_node* snd, psf_node* rcv, const psf_message* const
     psf_message* last_dec = nullptr;
     psf::RemoteNode* s = snd->impl;
     psf::RemoteNode* r = rcv->impl;
-    // each iteration's KEY_CACHING CRCs are queued behind the previous
-    // iteration's encode and collected when the iteration starts
+    // each iteration's KEY_CACHING CRCs run on the side stream while the
+    // previous iteration runs, and are collected when the iteration starts
     const psf::Message* t0 = iters ? &tmpls[0]->m : nullptr;
     psf::PresignJob next = psf::presign_launch(&s, &t0, iters ? 1 : 0, true);
     for (int i = 0; i < iters; ++i) {
@@ -646,11 +646,11 @@ int psf_node_roundtrip_ex(psf_node* snd, psf_node* rcv, const psf_message* const
       psf::Message* mp = &m;
       psf::KeySigHint eh, dh;
       psf::presign_finish(next, &eh, &dh);
-      psf::encode_batch(&s, &mp, 1, &eh);  // = EncodeMessage, side-info left on the device
-      if (i + 1 < iters) {
+      if (i + 1 < iters) {  // the next iteration's CRCs, beside this one (side stream)
         const psf::Message* tn = &tmpls[(i + 1) % ntmpl]->m;
         next = psf::presign_launch(&s, &tn, 1, true);
       }
+      psf::encode_batch(&s, &mp, 1, &eh);  // = EncodeMessage, side-info left on the device
       psf::Message w = m;                  // delivered copy (van: Task frame + data frames)
       psf::Message* wp = &w;
       psf::decode_batch(&r, &wp, 1, &dh);  // = DecodeMessage
@@ -760,8 +760,9 @@ int psf_nodes_roundtrip_opts(psf_node* const* snd, psf_node* const* rcv, const p
     std::vector<const psf::Message*> tp(n);
     for (int i = 0; i < n; ++i) tp[i] = &tmpls[i]->m;
     std::vector<psf::KeySigHint> eh(n), dh(n);
-    // every KEY_CACHING CRC of an iteration (all phases): queued behind the
-    // previous iteration's last encode, collected when the iteration starts
+    // every KEY_CACHING CRC of an iteration (all phases): launched on the
+    // context's side stream when the previous iteration starts, collected
+    // when this one starts
     psf::PresignJob next = psf::presign_launch(s.data(), tp.data(), iters ? n : 0, true);
     for (int it = 0; it < iters; ++it) {
       PSF_HPROF(14);
@@ -770,6 +771,10 @@ int psf_nodes_roundtrip_opts(psf_node* const* snd, psf_node* const* rcv, const p
         std::fill(eh.begin(), eh.end(), psf::KeySigHint{});
         std::fill(dh.begin(), dh.end(), psf::KeySigHint{});
         psf::presign_finish(next, eh.data(), dh.data());
+      }
+      if (it + 1 < iters) {  // the next iteration's CRCs, beside this one (side stream)
+        PSF_HPROF(13);
+        next = psf::presign_launch(s.data(), tp.data(), n, true);
       }
       int b = 0;
       for (int e : ends) {  // phase [b, e): encode all, deliver, decode all
@@ -783,10 +788,6 @@ int psf_nodes_roundtrip_opts(psf_node* const* snd, psf_node* const* rcv, const p
         {
           PSF_HPROF(1);
           psf::encode_batch(s.data() + b, mp.data() + b, e - b, eh.data() + b);
-        }
-        if (e == n && it + 1 < iters) {
-          PSF_HPROF(13);
-          next = psf::presign_launch(s.data(), tp.data(), n, true);
         }
         {
           PSF_HPROF(5);

@@ -356,6 +356,10 @@ Context::~Context() {
   (void)hipGetDevice(&cur);
   if (cur != device_) (void)hipSetDevice(device_);
   (void)hipStreamSynchronize(stream_);
+  if (side_) {
+    (void)hipStreamSynchronize(side_);
+    (void)hipStreamDestroy(side_);
+  }
   for (auto& u : ring_uses_) {  // messages may outlive the context: leave their ranges on the host
     auto rb = u.rb.lock();
     if (rb && !rb->done) {
@@ -484,6 +488,15 @@ void Context::wait_ticket(int i, uint32_t ticket) {
   }
 }
 
+hipStream_t Context::side_stream() {
+  if (device_ < 0) throw CheckError(kErrArg, "host-only context has no device stream");
+  if (!side_) {
+    DeviceScope ds(device_);
+    PSF_HIP_CHECK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+  }
+  return side_;
+}
+
 uint32_t Context::wait_crc(int i, uint32_t ticket) {
   if (device_ < 0) throw CheckError(kErrArg, "host-only context has no device workspace");
   const Slot* s = h_slots_ + i;
@@ -497,7 +510,8 @@ uint32_t Context::wait_crc(int i, uint32_t ticket) {
     if ((uint32_t)(w >> 32) == ticket) return (uint32_t)w;
     if ((spin & 255) == 255) {
       hipError_t q = hipStreamQuery(stream_);
-      if (q == hipSuccess) {  // stream drained: the publish must be visible now
+      if (q == hipSuccess && side_) q = hipStreamQuery(side_);  // (presign CRCs run there)
+      if (q == hipSuccess) {  // streams drained: the publish must be visible now
         w = __atomic_load_n(&s->crc_ticket, __ATOMIC_ACQUIRE);
         if ((uint32_t)(w >> 32) == ticket) return (uint32_t)w;
         throw CheckError(kErrHip, "kernel finished without publishing its CRC");

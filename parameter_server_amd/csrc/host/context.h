@@ -90,6 +90,10 @@ class Context {
 
   int device() const { return device_; }
   hipStream_t stream() const { return stream_; }
+  // a second stream of this context for work no kernel of stream() depends
+  // on (the round-trip drivers' KEY_CACHING presign CRCs of the next
+  // iteration's keys, read back through publish slots), created on first use
+  hipStream_t side_stream();
 
   // HBM buffer freed (stream-ordered) when its last reference drops.
   Buffer alloc(size_t bytes);
@@ -210,6 +214,7 @@ class Context {
   int device_;
   bool shared_stream_ = false;
   hipStream_t stream_;
+  hipStream_t side_ = nullptr;
   std::shared_ptr<StreamHolder> holder_;
   void* d_partials_ = nullptr;
   Slot* d_slots_ = nullptr;

@@ -812,8 +812,12 @@ PresignJob presign_launch(RemoteNode* const* nodes, const Message* const* msgs, 
     }
     for (size_t c = 0; c < d.size(); c += (size_t)kCrcBatchMax) {
       const int cnt = (int)std::min(d.size() - c, (size_t)kCrcBatchMax);
+      // on the context's side stream: the keys are the callers' templates, which
+      // no kernel of the main stream writes, and the CRCs are read back
+      // through the publish slots -- so they run beside the current
+      // iteration instead of queueing behind its last encode
       int st = crc32c_batch_launch(d.data() + c, len.data() + c, slot.data() + c, tk.data() + c, cnt,
-                                   ctx->pub_dev(Context::kPresignSlot0), ctx->stream(), ctx->prof());
+                                   ctx->pub_dev(Context::kPresignSlot0), ctx->side_stream(), ctx->prof());
       if (st != kOk) throw CheckError(st, "crc32c batch launch failed");
     }
   }

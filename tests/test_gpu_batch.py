@@ -423,3 +423,46 @@ def test_batch_tile_edges_and_offsets(ctx, port):
             assert rcv_b[i].value(wb[i], 0).cpu().numpy().tobytes() == dec.tobytes(), i
     finally:
         F.set_clock(None)
+
+
+def test_small_batch_min_max_and_encode_in_one_launch(ctx, port):
+    """A batch of small arrays with computed ranges runs its min/max pass and
+    encode in one launch (ff_fused_batch: the min/max items folded by the
+    encode workgroups themselves), with a held-back decode of the same
+    num_bytes in front when the round-trip driver defers one -- and the codes
+    and decoded values are still the restatement's."""
+    import os
+
+    from parameter_server_amd import FIXING_FLOAT
+    from parameter_server_amd import filter as F
+    if os.environ.get("PSF_FF_FUSED") == "0":
+        pytest.skip("fused launch disabled (PSF_FF_FUSED=0)")
+    F.set_clock(4242)
+    try:
+        rng = np.random.default_rng(5)
+        xs = [(rng.standard_normal(n) * 3).astype(np.float32) for n in (1, 5, 4096, 9999, 100_003, 262_145)]
+        msgs = []
+        for i, x in enumerate(xs):
+            m = F.Message(request=True, push=True, key_channel=i, key_range=(0, 10**9))
+            m.add_value(torch.from_numpy(x).to(DEV))
+            m.add_filter(FIXING_FLOAT, num_bytes=1)
+            msgs.append(m)
+        ctx.profile(True)
+        ctx.profile_reset()
+        F.RemoteNode.encode_many([F.RemoteNode(ctx) for _ in msgs], msgs)
+        ctx.sync()
+        prof = ctx.profile_read()
+        ctx.profile(False)
+        assert prof.get("ff_minmax_encode", (0,))[0] == 1, prof
+        assert "ff_minmax_partials" not in prof and "ff_encode" not in prof, prof
+        for i, (x, m) in enumerate(zip(xs, msgs)):
+            st, codes, mn, mx = port.ff_encode(x, 1, 4242)
+            assert st == 0
+            fp = m.fixed_points(0)
+            assert len(fp) == 1 and fp[0][0] and fp[0][2], i
+            assert np.float32(fp[0][1]) == np.float32(mn) and np.float32(fp[0][3]) == np.float32(mx), i
+            vp, vn, vl = m.value_ptr(0)
+            got = F.copy_out(vp, vn, vl, DEV).cpu().numpy().tobytes()
+            assert got == codes.tobytes(), i
+    finally:
+        F.set_clock(None)

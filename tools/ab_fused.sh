@@ -1,11 +1,11 @@
 # A/B of ff_fused_batch (a small batch's min/max + encode + pending decode in
-# one launch, PSF_FF_FUSED=1 default) against two launches (PSF_FF_FUSED=0):
+# one launch, the default) against two launches (PSF_FF_FUSED=0):
 # the batched / parity / adapter tests with it on, then C1 and C3 lines both
 # ways.  Output: gpurun_out/$1/.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 O=gpurun_out/${1:-fused}; mkdir -p $O
-PSF_FF_FUSED=1 timeout -k 10 400 python -u -m pytest tests/test_gpu_batch.py tests/test_gpu_parity.py tests/test_gpu_chain_adapter.py \
+timeout -k 10 400 python -u -m pytest tests/test_gpu_batch.py tests/test_gpu_parity.py tests/test_gpu_chain_adapter.py \
   tests/test_gpu_adapter.py tests/test_gpu_stored.py -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1 \
   || { tail -40 $O/tests.log; exit 1; }
 tail -1 $O/tests.log
