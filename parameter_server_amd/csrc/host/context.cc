@@ -567,12 +567,16 @@ void Context::track(std::shared_ptr<RangeBatch> rb) {
 void Context::check_ranges() {
   std::vector<std::shared_ptr<RangeBatch>> t;
   t.swap(tracked_);
-  bool bad = false;
+  bool bad = false, late = false;
   if (!t.empty()) sync();
   for (auto& rb : t) {
     rb->resolve(true);
-    for (size_t i = 2; i < rb->host.size(); i += 4) bad |= (int32_t)rb->host[i] != kOk;
+    for (size_t i = 2; i < rb->host.size(); i += 4) {
+      bad |= (int32_t)rb->host[i] != kOk;
+      late |= (int32_t)rb->host[i] == kErrHip;
+    }
   }
+  if (late) throw CheckError(kErrHip, "FIXING_FLOAT: in-launch min/max hand-off timed out");
   if (bad) throw CheckError(kErrBin, "CHECK_GT(bin, 0)");
 }
 

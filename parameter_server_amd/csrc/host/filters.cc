@@ -357,6 +357,7 @@ void FixingFloatFilter::encode_messages(Context* ctx, std::vector<FfMessage>& ms
         const Slot& hs = *ctx->pub_host((int)(q - base));
         if (!j.fp->has_min) j.fp->set_min(hs.range[0]);
         if (!j.fp->has_max) j.fp->set_max(hs.range[1]);
+        if (hs.status == kErrHip) throw CheckError(kErrHip, "FIXING_FLOAT: in-launch min/max hand-off timed out");
         if (hs.status != kOk) throw CheckError(kErrBin, "CHECK_GT(bin, 0)");
       } else if (lazy_idx[q - base] >= 0) {
         j.fp->pending = rb;
@@ -383,6 +384,7 @@ void FixedFloatConfig::settle() {
   if (pending_max) set_max(mx);
   pending_idx = -1;
   pending_min = pending_max = false;
+  if ((int32_t)r[2] == kErrHip) throw CheckError(kErrHip, "FIXING_FLOAT: in-launch min/max hand-off timed out");
   if ((int32_t)r[2] != kOk) throw CheckError(kErrBin, "CHECK_GT(bin, 0)");
 }
 
