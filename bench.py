@@ -572,31 +572,40 @@ def main():
     # the default command measures the spill too (executor.cc:134-146 over
     # assigner.h:17-28's partition); at N = 1 every slice is local
     c4 = None
+    c4_failed = False
     if args.config == "c2" and not args.no_c4:
         if "run" in locals():
             del run
-        a4 = c4_args(args)
-        run4, payload4, _, extra4 = build_workload(a4, F, ctx, rank, world, dev, g, 0)
-        run4(args.warmup)
-        torch.cuda.synchronize()
-        r4 = extra4["router"]
-        if r4.exchange is not None:
-            r4.exchange.bytes_sent = 0
-        el4, _ = timed(run4, args.steps, world, dist, ctx)
-        spill4 = r4.exchange.bytes_sent if r4.exchange is not None else 0
-        el4 = max_over_ranks(el4)
-        tot4 = float(payload4)
-        if world > 1:
-            t = torch.tensor([tot4], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
-            dist.all_reduce(t)
-            tot4 = float(t.item())
-        c4 = c4_config(args, world_pg, backend_pg)
-        c4.update({"measured": True, "value": round(args.steps * tot4 / el4 / GIB, 2),
-                   "ms_per_step": round(el4 / args.steps * 1e3, 4),
-                   "payload_bytes_per_step_per_gpu_rank0": payload4,
-                   "key_bytes_elided_per_step_rank0": extra4["key_bytes_elided"],
-                   "spill_bytes_per_step_rank0": spill4 // max(args.steps, 1)})
-        del run4, r4, extra4
+        try:
+            a4 = c4_args(args)
+            run4, payload4, _, extra4 = build_workload(a4, F, ctx, rank, world, dev, g, 0)
+            run4(args.warmup)
+            torch.cuda.synchronize()
+            r4 = extra4["router"]
+            if r4.exchange is not None:
+                r4.exchange.bytes_sent = 0
+            el4, _ = timed(run4, args.steps, world, dist, ctx)
+            spill4 = r4.exchange.bytes_sent if r4.exchange is not None else 0
+            el4 = max_over_ranks(el4)
+            tot4 = float(payload4)
+            if world > 1:
+                t = torch.tensor([tot4], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
+                dist.all_reduce(t)
+                tot4 = float(t.item())
+            c4 = c4_config(args, world_pg, backend_pg)
+            c4.update({"measured": True, "value": round(args.steps * tot4 / el4 / GIB, 2),
+                       "ms_per_step": round(el4 / args.steps * 1e3, 4),
+                       "payload_bytes_per_step_per_gpu_rank0": payload4,
+                       "key_bytes_elided_per_step_rank0": extra4["key_bytes_elided"],
+                       "spill_bytes_per_step_rank0": spill4 // max(args.steps, 1)})
+            del run4, r4, extra4
+        except Exception as e:  # noqa: BLE001 -- the companion must not take the C2 line down with it
+            # (a failure of the spill path is symmetric across ranks: each
+            # rank records it, and the process group is left alone after it)
+            c4_failed = True
+            c4 = c4_config(args, world_pg, backend_pg)
+            c4.update({"measured": False, "error": f"{type(e).__name__}: {e}"[:400]})
+            print(f"bench.py: rank {rank}: config_c4 failed: {e!r}", file=sys.stderr, flush=True)
 
     # C1 with the wire step in the timed region: every encoded Task serialised
     # (its computed min/max settled to the host) and parsed by the receiver,
@@ -671,7 +680,7 @@ def main():
             line["config_wire"] = wire_line
         print(json.dumps(line), flush=True)
 
-    if world > 1:
+    if world > 1 and not c4_failed:
         dist.destroy_process_group()
 
 
