@@ -466,3 +466,39 @@ def test_small_batch_min_max_and_encode_in_one_launch(ctx, port):
             assert got == codes.tobytes(), i
     finally:
         F.set_clock(None)
+
+
+def test_fused_batches_back_to_back(ctx, port):
+    """Twenty batched encodes in a row on one context, each a random mix of
+    small arrays (sizes, num_bytes, f32/f64, computed or half-preset ranges):
+    the fused launch's counter lines are zeroed by each launch for the next,
+    so every batch's codes and ranges equal the restatement's."""
+    from parameter_server_amd import FIXING_FLOAT
+    from parameter_server_amd import filter as F
+    F.set_clock(777)
+    try:
+        rng = np.random.default_rng(11)
+        for it in range(20):
+            nmsg = int(rng.integers(2, 12))
+            nb = int(rng.integers(1, 4))
+            cases, msgs = [], []
+            for i in range(nmsg):
+                n = int(rng.integers(1, 60_000))
+                dt = np.float64 if rng.random() < 0.3 else np.float32
+                x = (rng.standard_normal(n) * (1 + i)).astype(dt)
+                preset = (None, float(x.max()) + 1.0) if rng.random() < 0.2 else None
+                m = F.Message(request=True, push=True, key_channel=i, key_range=(0, 10**9))
+                m.add_value(torch.from_numpy(x).to(DEV))
+                m.add_filter(FIXING_FLOAT, num_bytes=nb, fixed_point=None if preset is None else [preset])
+                cases.append((x, preset))
+                msgs.append(m)
+            F.RemoteNode.encode_many([F.RemoteNode(ctx) for _ in msgs], msgs)
+            ctx.sync()
+            for i, ((x, preset), m) in enumerate(zip(cases, msgs)):
+                st, codes, mn, mx = port.ff_encode(x, nb, 777, None, None if preset is None else preset[1])
+                assert st == 0
+                vp, vn, vl = m.value_ptr(0)
+                got = F.copy_out(vp, vn, vl, DEV).cpu().numpy().tobytes()
+                assert got == codes.tobytes(), (it, i)
+    finally:
+        F.set_clock(None)
