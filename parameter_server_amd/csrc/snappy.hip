@@ -2003,6 +2003,128 @@ __global__ __launch_bounds__(64) void snappy_dlink(const SnappyDJobs J) {
     }
   }
 }
+// K2p: the windows linked in parallel, for a stream whose chain enters every
+// window at one of its first 64 bytes (tag-dense data: every tag is short).
+// Window w's K1 tables are a function on entry offsets: F_w(l) = the next
+// window's entry offset (or the stream's end), with T_w(l) output bytes; the
+// chain's entries are the prefix compositions of these functions from
+// window 0's offset 0.  Each wave composes the functions of a block of windows
+// (lane l follows the chain entered at offset l of the block's first window:
+// one lane permute per window), one wave walks the blocks' compositions, and
+// each wave then re-walks its blocks from their known entries to record every
+// window's entry and output offset -- what K2's one-chain walk records, in
+// blocks instead of windows.  A chain that leaves a window anywhere else (a
+// long literal, an entry past the first 64 bytes) leaves the stream to K2.
+constexpr uint32_t kLinkWaves = 16;
+constexpr uint32_t kLinkMaxBlocks = 128;
+constexpr uint32_t kLinkEnd = 64, kLinkOdd = 65;  // F codes besides an entry offset 0..63
+__device__ __forceinline__ uint32_t link_code(uint64_t x, uint32_t w, uint32_t nwin, uint32_t hdr, uint64_t C) {
+  if (w + 1 == nwin) return x == C ? kLinkEnd : kLinkOdd;
+  if (x < hdr) return kLinkOdd;
+  const uint64_t r = x - hdr, w2 = r / kWin, off = r - w2 * kWin;
+  return (w2 == (uint64_t)w + 1 && off < kStarts) ? (uint32_t)off : kLinkOdd;
+}
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t l) {
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, (int)l, 64);
+  const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), (int)l, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+__global__ __launch_bounds__(kLinkWaves * 64) void snappy_dlinkp(const SnappyDJobs J) {
+  __shared__ uint8_t bF[kLinkMaxBlocks][kStarts];
+  __shared__ uint64_t bT[kLinkMaxBlocks][kStarts];
+  __shared__ uint32_t s_entry[kLinkMaxBlocks];
+  __shared__ uint64_t s_out[kLinkMaxBlocks];
+  __shared__ uint32_t s_ok;
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (uint32_t ji = blockIdx.x; ji < J.njobs; ji += gridDim.x) {
+    const DJob& D = J.j[ji];
+    const DScr S = dscr(J, D, ji);
+    if (!(*S.flags & kFlagScan)) continue;  // (uniform: every wave reads the same word)
+    const uint32_t nwin = D.nwin, hdr = D.hdr;
+    const uint64_t C = D.C;
+    if (nwin == 0) continue;
+    const uint32_t per = max(64u, (nwin + kLinkMaxBlocks - 1) / kLinkMaxBlocks);
+    const uint32_t nb = (nwin + per - 1) / per;
+    // ---- each block's composed function
+    for (uint32_t b = wave; b < nb; b += kLinkWaves) {
+      const uint32_t w0 = b * per, w1 = min(nwin, w0 + per);
+      uint32_t cur = lane;
+      uint64_t acc = 0;
+      for (uint32_t wc = w0; wc < w1; wc += 8) {  // 8 windows' tables in flight
+        uint64_t x[8], t[8];
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) {
+          const uint32_t w = min(wc + k, w1 - 1);
+          x[k] = S.wexit[(size_t)w * kStarts + lane];
+          t[k] = S.wtotal[(size_t)w * kStarts + lane];
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) {
+          if (wc + k >= w1) break;
+          const uint32_t code = link_code(x[k], wc + k, nwin, hdr, C);
+          const uint32_t nc = (uint32_t)__shfl((int)code, (int)(cur & 63), 64);
+          const uint64_t nt = shfl64(t[k], cur & 63);
+          if (cur < kStarts) {
+            acc += nt;
+            cur = nc;
+          } else {
+            cur = kLinkOdd;  // (the end is only ever the last window's)
+          }
+        }
+      }
+      bF[b][lane] = (uint8_t)cur;
+      bT[b][lane] = acc;
+    }
+    __syncthreads();
+    // ---- the blocks' entries along the true chain
+    if (threadIdx.x == 0) {
+      uint32_t e = 0;
+      uint64_t o = 0;
+      for (uint32_t b = 0; b < nb && e < kStarts; ++b) {
+        s_entry[b] = e;
+        s_out[b] = o;
+        o += bT[b][e];
+        e = bF[b][e];
+      }
+      s_ok = e == kLinkEnd ? (o == D.dsize ? 1u : 2u) : 0u;  // 0: K2 walks it
+    }
+    __syncthreads();
+    const uint32_t ok = s_ok;
+    if (ok == 1) {
+      // ---- every window's entry, from its block's
+      for (uint32_t b = wave; b < nb; b += kLinkWaves) {
+        const uint32_t w0 = b * per, w1 = min(nwin, w0 + per);
+        uint32_t e = s_entry[b];
+        uint64_t o = s_out[b];
+        for (uint32_t wc = w0; wc < w1; wc += 8) {
+          uint64_t x[8], t[8];
+#pragma unroll
+          for (uint32_t k = 0; k < 8; ++k) {
+            const uint32_t w = min(wc + k, w1 - 1);
+            x[k] = S.wexit[(size_t)w * kStarts + lane];
+            t[k] = S.wtotal[(size_t)w * kStarts + lane];
+          }
+#pragma unroll
+          for (uint32_t k = 0; k < 8; ++k) {
+            if (wc + k >= w1) break;
+            const uint32_t w = wc + k;
+            if (lane == 0) {
+              S.wentry[w] = hdr + (uint64_t)w * kWin + e;
+              S.woff[w] = o;
+            }
+            const uint32_t code = link_code(x[k], w, nwin, hdr, C);
+            o += lane_of64(t[k], e);
+            e = lane_of32(code, e);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && ok) *S.flags = ok == 2 ? kFlagInvalid : 0;  // (K2 then skips the stream)
+    __syncthreads();
+  }
+}
+
 // K3: windows indexed (streams K0 did not walk to the end)
 __global__ __launch_bounds__(64) void snappy_dindex(const SnappyDJobs J) {
   __shared__ uint32_t b32[(kWin + 32) / 4];
@@ -2390,10 +2512,20 @@ int snappy_uncompress_batch_launch(const SnappyDJob* jobs, int njobs, void* scra
   return launch_tail(K, st);
 }
 
+// PSF_LINK_PARALLEL (A/B knob, tools/): 0 leaves every stream to K2's walk
+static bool link_parallel() {
+  static const bool on = [] {
+    const char* e = getenv("PSF_LINK_PARALLEL");
+    return !(e && *e == '0');
+  }();
+  return on;
+}
+
 // K1-K3 and K4 (+ K5) of a batch whose fast path has run
 static int launch_tail(const SnappyDJobs& K, hipStream_t st) {
   if (K.nwin) {
     hipLaunchKernelGGL(snappy_dscan, dim3(K.nwin), dim3(64), 0, st, K);
+    if (link_parallel()) hipLaunchKernelGGL(snappy_dlinkp, dim3(K.njobs), dim3(kLinkWaves * 64), 0, st, K);
     hipLaunchKernelGGL(snappy_dlink, dim3(K.njobs), dim3(64), 0, st, K);
     hipLaunchKernelGGL(snappy_dindex, dim3(K.nwin), dim3(64), 0, st, K);
   }
