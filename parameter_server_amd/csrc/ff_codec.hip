@@ -1684,8 +1684,10 @@ static bool fused_mode() {
 // its waiting workgroups hold their slots (and poll), which a launch-bound
 // batch of small arrays (C1: 832) does not notice and one of large arrays
 // does (C5, 8 x 2^24 values, 16384 workgroups: 1.08 ms against 0.20 in two
-// launches, tools/ab_fused.sh r04)
-constexpr uint32_t kFusedMaxEncWgs = 2048;
+// launches, tools/ab_fused.sh r04).  1024 keeps the grid about within one
+// round of resident workgroups (5 per CU at its registers); sizes between
+// (C4's 64 slices per rank at N = 8: 2048) are unmeasured and keep two launches.
+constexpr uint32_t kFusedMaxEncWgs = 1024;
 
 template <typename V, int NB>
 static void launch_fused(const FfBatchT<kBatchSmall>& D, const FfBatchT<kBatchSmall>& B, dim3 grid, hipStream_t st,
