@@ -1669,7 +1669,7 @@ static bool mm_reverse_mode(double bytes_mm) {
 
 template <int CAP>
 static int fill_decode_batch(FfBatchT<CAP>& B, int value_type, int nb, const FfDecArray* arrs, int count,
-                             double* bytes_out);
+                             double* bytes_out, size_t tpw = 1);
 
 // PSF_FF_FUSED (A/B knob, tools/): 0 keeps a small batch's min/max and
 // encode in two launches
@@ -1688,6 +1688,18 @@ static bool fused_mode() {
 // round of resident workgroups (5 per CU at its registers); sizes between
 // (C4's 64 slices per rank at N = 8: 2048) are unmeasured and keep two launches.
 constexpr uint32_t kFusedMaxEncWgs = 1024;
+// tiles per decode workgroup inside ff_fused_batch: 4 (C1, tools/ab_fused_tpw.sh
+// r04: the fused kernel 28.1-28.8 us at 1, 27.4-28.5 at 2, 25.6-26.7 at 4,
+// 25.6-26.1 at 8; fewer, longer decode workgroups leave the encode ones their
+// slots sooner); A/B knob PSF_FUSED_DEC_TPW
+static size_t fused_dec_tpw() {
+  static const size_t v = [] {
+    const char* e = getenv("PSF_FUSED_DEC_TPW");
+    const int t = e ? atoi(e) : 0;
+    return t >= 1 && t <= 16 ? (size_t)t : (size_t)4;
+  }();
+  return v;
+}
 
 template <typename V, int NB>
 static void launch_fused(const FfBatchT<kBatchSmall>& D, const FfBatchT<kBatchSmall>& B, dim3 grid, hipStream_t st,
@@ -1791,7 +1803,7 @@ static int encode_batch_cap(int value_type, int nb, const FfArray* arrs, int cou
       static FfBatchT<kBatchSmall> D;
       double bytes_dec = 0;
       if (ndec > 0) {
-        const int fs = fill_decode_batch<kBatchSmall>(D, value_type, dec_nb, dec, ndec, &bytes_dec);
+        const int fs = fill_decode_batch<kBatchSmall>(D, value_type, dec_nb, dec, ndec, &bytes_dec, fused_dec_tpw());
         if (fs != kOk) return fs;
       } else {
         memset(&D, 0, sizeof(D));
@@ -1828,7 +1840,7 @@ static int encode_batch_cap(int value_type, int nb, const FfArray* arrs, int cou
     } else if constexpr (CAP == kBatchSmall) {
       static FfBatchT<kBatchSmall> D;
       double bytes_dec = 0;
-      const int fs = fill_decode_batch<kBatchSmall>(D, value_type, dec_nb, dec, ndec, &bytes_dec);
+      const int fs = fill_decode_batch<kBatchSmall>(D, value_type, dec_nb, dec, ndec, &bytes_dec, kBatchDecTpw);
       if (fs != kOk) return fs;
       const FfBatchT<kBatchSmall>& M = B;
       const dim3 grid(D.total + M.mm_total);
@@ -1882,7 +1894,7 @@ int ff_encode_batch_launch(int value_type, int nb, const FfArray* arrs, int coun
 // a decode batch's kernel arguments
 template <int CAP>
 static int fill_decode_batch(FfBatchT<CAP>& B, int value_type, int nb, const FfDecArray* arrs, int count,
-                             double* bytes_out) {
+                             double* bytes_out, size_t tpw) {
   memset(&B, 0, sizeof(B));
   for (int i = 0; i < CAP; ++i) B.first[i] = B.mm_first[i] = ~0u;
   B.njobs = count;
@@ -1901,7 +1913,7 @@ static int fill_decode_batch(FfBatchT<CAP>& B, int value_type, int nb, const FfD
     J.u.range = arrs[i].range;
     B.first[i] = wg;
     wg += std::min<uint32_t>((uint32_t)tile_grid(arrs[i].n, kStreamGrid),
-                             (uint32_t)std::max<size_t>(1, (tiles_of(arrs[i].n) + kBatchDecTpw - 1) / kBatchDecTpw));
+                             (uint32_t)std::max<size_t>(1, (tiles_of(arrs[i].n) + tpw - 1) / tpw));
     bytes += (double)arrs[i].n * (vsz + nb);
   }
   B.total = wg;
@@ -1916,7 +1928,7 @@ static int decode_batch_cap(int value_type, int nb, const FfDecArray* arrs, int 
   static std::mutex mu;
   std::lock_guard<std::mutex> lock(mu);
   double bytes = 0;
-  const int fs = fill_decode_batch<CAP>(B, value_type, nb, arrs, count, &bytes);
+  const int fs = fill_decode_batch<CAP>(B, value_type, nb, arrs, count, &bytes, kBatchDecTpw);
   if (fs != kOk) return fs;
   const uint32_t wg = B.total;
   ProfScope ps(prof, kKDecode, st, bytes);
