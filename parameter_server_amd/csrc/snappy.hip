@@ -227,7 +227,12 @@ __device__ uint64_t g_dfrag_trace[kTraceFrags * 4];
   } while (0)
 #endif
 
-constexpr uint32_t kCThreads = 512;  // K-parse: 8 waves, parse (0), stage (4-7)
+// K-parse: 12 waves -- a round probes 12 fragments, so 2048 < n <= 3072
+// fragments (C5 + COMPRESSING on a key cache miss: 2048 value + 128 key
+// fragments) still take one round on 256 CUs; 12 waves of its 162 registers
+// fit 3 per SIMD.  Staging a fragment uses the first kStageThreads.
+constexpr uint32_t kCThreads = 768;
+constexpr uint32_t kStageThreads = 512;
 constexpr uint32_t kStageT = 256;    // lanes of the staging waves
 constexpr int kPre = (int)(kFrag / 16 / kStageT);  // uint4 per staging lane that cover one fragment
 // one fragment's share of a lane as one vector value (an array of uint4 would
@@ -766,8 +771,8 @@ __device__ __forceinline__ void stage_frag_shifted(const uint8_t* __restrict__ g
   }
 }
 
-// K-parse: persistent workgroups of 8 waves, each over its stripe of the
-// fragments (b, b + G, b + 2G, ...) in rounds of 8: every wave probes one
+// K-parse: persistent workgroups of 12 waves, each over its stripe of the
+// fragments (b, b + G, b + 2G, ...) in rounds of 12: every wave probes one
 // fragment; then the fragments that matched are parsed by waves
 // 0..kParseWaves-1, one fragment per wave at a time (tags to the fragment's
 // scratch slot).  No workgroup depends on another.
@@ -821,9 +826,9 @@ __global__ __launch_bounds__(kCThreads) void snappy_parse(const SnappyCJobs J, u
       uint32_t* src = reinterpret_cast<uint32_t*>(U.p.table[1]);  // tables 1..3: 96 KiB
       uint8_t* srcb = reinterpret_cast<uint8_t*>(src);
       if (aligned16(g)) {
-        stage_frag<kCThreads>(g, len, src, tid);
+        if (tid < kStageThreads) stage_frag<kStageThreads>(g, len, src, tid);
       } else if (c.stored) {
-        stage_frag_shifted<kCThreads>(g, len, src, tid);
+        if (tid < kStageThreads) stage_frag_shifted<kStageThreads>(g, len, src, tid);
       } else {
         for (uint32_t i = tid; i < len; i += kCThreads) srcb[i] = g[i];
       }
