@@ -90,7 +90,9 @@ def splitmix64_keys(m: int, seed: int):
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default 20; 200 for c1 / c3, whose step is 0.04-0.07 ms: 20 of them "
+                         "time only about 1 ms)")
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--n", type=int, default=1 << 28, help="c2: values per message (per GPU)")
     ap.add_argument("--nb", type=int, default=1, help="FIXING_FLOAT num_bytes")
@@ -112,7 +114,10 @@ def parse(argv=None):
                          "and are compressed with --compress)")
     ap.add_argument("--launch-check", action="store_true",
                     help="start the ranks and the process group only (no GPU work); for CPU tests")
-    return ap.parse_args(argv)
+    a = ap.parse_args(argv)
+    if a.steps is None:
+        a.steps = 200 if a.config in ("c1", "c3", "c3miss") else 20
+    return a
 
 
 # --------------------------------------------------------------- launcher --
