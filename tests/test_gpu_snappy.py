@@ -340,3 +340,30 @@ def test_mutated_multifragment_streams_vs_port(ctx, port, kind):
         else:
             nbad += 1
     assert nbad > 0
+
+
+def test_tag_dense_with_long_literals_roundtrip(ctx, port):
+    """Sorted-key runs (tags of a few bytes) between random runs of 100-400
+    bytes (literals longer than 64 bytes, so some straddle a 16 KiB window
+    start of the stream and the chain enters that window past its first 64
+    bytes): the windows are then linked by K2's walk instead of the parallel
+    prefix (K2p), and the bytes must come back either way -- and the stream
+    is 1.1.8's."""
+    rng = np.random.default_rng(21)
+    parts = []
+    base = 0
+    while sum(len(p) for p in parts) < (6 << 20):
+        k = np.sort(rng.integers(base, base + 10**7, 256)).astype(np.uint64)
+        base += 10**7
+        parts.append(k.tobytes())
+        parts.append(rng.integers(0, 256, int(rng.integers(100, 400)), dtype=np.uint8).tobytes())
+    data = b"".join(parts)
+    x = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
+    s = ctx.snappy_compress(x)
+    want = port.snappy_compress(data)
+    got_s = s.cpu().numpy().tobytes()
+    ok = got_s == want
+    assert ok, (len(got_s), len(want))
+    back = ctx.snappy_uncompress(s).cpu().numpy().tobytes()
+    ok = back == data
+    assert ok
