@@ -359,6 +359,19 @@ __device__ __forceinline__ void map_put(uint64_t* m, uint32_t h, uint32_t pos, u
   }
 }
 
+// the probe's fast path: inserts the 4-byte value v into the set m (entries
+// 1 << 32 | v); returns whether v was there already
+__device__ __forceinline__ bool set_insert(uint64_t* m, uint32_t v) {
+  const uint64_t e = (1ull << 32) | v;
+  uint32_t s = (v * 0x9E3779B1u) >> 22;
+  for (;;) {
+    const uint64_t cur = atomicCAS(reinterpret_cast<unsigned long long*>(&m[s]), 0ull, (unsigned long long)e);
+    if (cur == 0) return false;
+    if (cur == e) return true;
+    s = (s + 1) & (kMapSlots - 1);
+  }
+}
+
 struct ProbeLds {  // the probe phase: per wave, the table as a map and every probe's bytes
   uint64_t map[kCThreads / 64][kMapSlots];
   uint32_t val[kCThreads / 64][kProbeMax];
@@ -423,16 +436,30 @@ __device__ __forceinline__ bool probe_stored(const uint8_t* g, uint32_t len, con
   if (len < 15) return true;
   const uint32_t shift = hash_shift(len), ip_limit = len - 15, ip = 1;
   // every probe's bytes (probe k is made iff ip + skip[k + 1] <= ip_limit)
-  uint32_t pre[kProbeMax / 64];
+  uint32_t pre[kProbeMax / 64], vbits = 0;
 #pragma unroll
   for (uint32_t r = 0; r < kProbeMax / 64; ++r) {
     const uint32_t k = r * 64 + lane;
-    pre[r] = ip + skip[k + 1] <= ip_limit ? gld32(g, ip + skip[k]) : 0;
+    const bool valid = ip + skip[k + 1] <= ip_limit;
+    pre[r] = valid ? gld32(g, ip + skip[k]) : 0;
+    vbits |= (valid ? 1u : 0u) << r;
   }
   const uint32_t v_at0 = uni(gld32(g, 0));
   for (uint32_t i = lane; i < kMapSlots; i += 64) m[i] = 0;
 #pragma unroll
   for (uint32_t r = 0; r < kProbeMax / 64; ++r) pv[r * 64 + lane] = pre[r];
+  // Fast path: a probe matches only a candidate with its own 4 bytes, and
+  // every candidate is position 0 or an earlier probe; when the first 4 bytes
+  // and all probes' 4 bytes are distinct the loop ends without a match.
+  {
+    bool dup = false;
+    if (lane == 0) set_insert(m, v_at0);
+#pragma unroll
+    for (uint32_t r = 0; r < kProbeMax / 64; ++r)
+      if ((vbits >> r) & 1) dup |= set_insert(m, pre[r]);
+    if (!__ballot(dup)) return true;
+    for (uint32_t i = lane; i < kMapSlots; i += 64) m[i] = 0;  // the exact loop below
+  }
   for (uint32_t kbase = 0;;) {
     const uint32_t k = kbase + lane;
     const uint32_t pos = ip + skip[k];
@@ -844,6 +871,7 @@ __global__ __launch_bounds__(kCThreads) void snappy_parse(const SnappyCJobs J, u
 #endif
         );
         if (lane == 0) J.finfo[f] = ((uint64_t)r.x << 32) | r.y;
+        PSF_TRACE(f, 1);
       }
     } else if (wave < kParseWaves) {
       uint16_t* table = U.p.table[wave];
@@ -867,6 +895,7 @@ __global__ __launch_bounds__(kCThreads) void snappy_parse(const SnappyCJobs J, u
 #endif
         );
         if (lane == 0) J.finfo[f] = ((uint64_t)r.x << 32) | r.y;
+        PSF_TRACE_T(f, 1, wave * 64);
       }
     }
     __syncthreads();  // (the next round's probe maps overwrite the tables)

@@ -46,6 +46,9 @@ def run(mib, kind, dfrag=False):
         x = (torch.randn(n, device="cuda", generator=g) * 30 + 128).clamp(0, 255).to(torch.uint8)
     elif kind == "keys":
         x = torch.sort(torch.randint(0, 10**9, (n // 8,), device="cuda", generator=g))[0].view(torch.uint8)
+    elif kind == "ff":  # FIXING_FLOAT nb=1 codes of N(0, 1) values, as C5's
+        v = torch.randn(n, device="cuda", generator=g)
+        x = ((v - v.min()) / (v.max() - v.min()) * 255 + 0.5).floor().to(torch.uint8)
     else:
         x = torch.randint(0, 256, (n,), device="cuda", dtype=torch.uint8, generator=g)
     ctx = F.Context(0)
@@ -80,6 +83,10 @@ def run(mib, kind, dfrag=False):
     t0 = t[:, 0].min()
     probe = ns(t[:, 4] - t[:, 0])
     place = ns(t[:, 3] - t[:, 2])
+    mt = t[:, 1] > t[:, 4]  # slot 1 after the probe: the fragment was parsed
+    split = {"parsed_frags": int(mt.sum()),
+             "parse_us": sorted(round(float(a) / 1000, 1) for a in ns(t[mt, 1] - t[mt, 4]))[-8:],
+             "parse_end_us": round(ns(t[mt, 1].max() - t0) / 1000, 1)} if mt.any() else {}
     print(json.dumps({"kind": kind, "mib": mib, "frags": nfrag,
                       "probe_span_us": round(ns(t[:, 4].max() - t0) / 1000, 1),
                       "probe_start_spread_us": round(ns(t[:, 0].max() - t0) / 1000, 1),
@@ -87,7 +94,7 @@ def run(mib, kind, dfrag=False):
                       "probe_to_place_us": round(ns(t[:, 2].min() - t[:, 4].max()) / 1000, 1),
                       "place_span_us": round(ns(t[:, 3].max() - t[:, 2].min()) / 1000, 1),
                       "place_us": q(place),
-                      "place_start_spread_us": round(ns(t[:, 2].max() - t[:, 2].min()) / 1000, 1)}))
+                      "place_start_spread_us": round(ns(t[:, 2].max() - t[:, 2].min()) / 1000, 1), **split}))
 
 
 if __name__ == "__main__":
