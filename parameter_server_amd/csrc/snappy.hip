@@ -1037,7 +1037,16 @@ __global__ __launch_bounds__(kPlaceT) void snappy_place(const SnappyCJobs J, con
 
 // ------------------------------------------------------------------ uncompress
 constexpr uint32_t kWin = 16384;   // compressed bytes per parse window (16 KiB: ~8 waves per CU)
-constexpr uint32_t kInWin = 8192;  // staged compressed bytes in the fragment decoder
+constexpr uint32_t kInWin = 4096;  // staged compressed bytes in the fragment decoder
+// The fragment decoder's output window: the last kRing bytes of the fragment
+// decoded so far sit in an LDS ring; older ones have been flushed to the
+// output.  One decode step (a batch, or one tag; a long literal in pieces of
+// kRingStep) writes at most kRingStep bytes; a step starts with at most
+// kRingFlushAt bytes unflushed, so it overwrites only flushed bytes, and a copy
+// source it cannot find in the ring was flushed before the step.
+constexpr uint32_t kRing = 8192;
+constexpr uint32_t kRingStep = 64 * 64;
+constexpr uint32_t kRingFlushAt = kRing - kRingStep - 64;
 constexpr uint32_t kBatchLit = 16;     // literals the fragment decoder's batches take (longer ones: one by one)
 constexpr uint32_t kBatchMargin = 96;  // staged bytes past p a batch reads: 64 tag starts + a tag + kBatchLit
 constexpr uint64_t kNone = ~0ull;
@@ -1556,7 +1565,8 @@ struct FewLds {
 // RawUncompress would), all 256 lanes copy the literals global to global, then
 // the copies run in order.  Returns the position after the fragment's last
 // tag, or kNone (nothing written) when the fragment is not of that kind.
-// Called by the whole workgroup.
+// Called by the whole workgroup.  U: copy_g2g's dwords in flight per lane.
+template <int U = 16>
 __device__ uint64_t decode_few(const uint8_t* __restrict__ in, uint64_t C, uint64_t p, uint32_t end,
                                uint8_t* __restrict__ d, uint32_t tid, FewLds& F) {
   if (tid == 0) {
@@ -1580,7 +1590,7 @@ __device__ uint64_t decode_few(const uint8_t* __restrict__ in, uint64_t C, uint6
   const uint32_t nt = F.n;
   if (nt == 0) return kNone;
   for (uint32_t i = 0; i < nt; ++i)
-    if (F.src[i] != kNone) copy_g2g(d + F.o[i], in + F.src[i], F.len[i], tid);
+    if (F.src[i] != kNone) copy_g2g<U>(d + F.o[i], in + F.src[i], F.len[i], tid);
   __syncthreads();
   for (uint32_t i = 0; i < nt; ++i) {
     if (F.src[i] != kNone) continue;
@@ -2177,19 +2187,20 @@ __global__ __launch_bounds__(64) void snappy_dindex(const SnappyDJobs J) {
 // flight (8 KiB per memory latency for the wave), bytes at the edges.
 __device__ void literal_to_lds(uint8_t* ob, uint32_t o, const uint8_t* __restrict__ in, uint64_t src, uint32_t L,
                                uint32_t lane) {
+  constexpr uint32_t M = kRing - 1;  // ob is the ring: 16-byte chunks never straddle its end
   const uint32_t head = (16 - (o & 15)) & 15;
   if (head >= L) {
-    for (uint32_t i = lane; i < L; i += 64) ob[o + i] = in[src + i];
+    for (uint32_t i = lane; i < L; i += 64) ob[(o + i) & M] = in[src + i];
     return;
   }
-  if (lane < head) ob[o + lane] = in[src + lane];
+  if (lane < head) ob[(o + lane) & M] = in[src + lane];
   const uint32_t nc = (L - head) >> 4;
   const uintptr_t sp = reinterpret_cast<uintptr_t>(in + src + head);
   typedef uint32_t V4 __attribute__((ext_vector_type(4)));
   const auto s16 = gbl<V4>(reinterpret_cast<const void*>(sp & ~(uintptr_t)15));  // global, not flat, loads
   const uint32_t sh = (uint32_t)(sp & 15);
-  uint4* d16 = reinterpret_cast<uint4*>(ob + o + head);
-  constexpr int U = 8;
+  const uint32_t o16 = o + head;  // 16-aligned
+  constexpr int U = 2;  // (registers: K4's occupancy)
   for (uint32_t c0 = 0; c0 < nc; c0 += U * 64) {
     uint4 lo[U], hi[U];
 #pragma unroll
@@ -2205,11 +2216,36 @@ __device__ void literal_to_lds(uint8_t* ob, uint32_t o, const uint8_t* __restric
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t c = c0 + u * 64 + lane;
-      if (c < nc) d16[c] = funnel16(lo[u], hi[u], sh);
+      if (c < nc) *reinterpret_cast<uint4*>(ob + ((o16 + 16 * c) & M)) = funnel16(lo[u], hi[u], sh);
     }
   }
   const uint32_t t0 = head + 16 * nc;
-  if (lane < L - t0) ob[o + t0 + lane] = in[src + t0 + lane];
+  if (lane < L - t0) ob[(o + t0 + lane) & M] = in[src + t0 + lane];
+}
+
+// The ring's bytes [from, to) of the fragment to d (from a multiple of 16 or
+// to the fragment's end), by one wave.
+__device__ __forceinline__ void ring_flush(const uint8_t* ring, uint8_t* __restrict__ d, uint32_t from, uint32_t to,
+                                           uint32_t lane) {
+  constexpr uint32_t M = kRing - 1;
+  uint32_t i = from;
+  if ((reinterpret_cast<uintptr_t>(d) & 15) == 0) {
+    const uint32_t c1 = to >> 4;
+    for (uint32_t c = (from >> 4) + lane; c < c1; c += 64)
+      reinterpret_cast<uint4*>(d)[c] = *reinterpret_cast<const uint4*>(ring + ((16 * c) & M));
+    i = max(from, c1 << 4);
+  }
+  for (i += lane; i < to; i += 64) d[i] = ring[i & M];
+}
+// Byte x of the fragment d, flushed from the ring by this wave before: an
+// agent-scope load after the wave's stores have landed in L2 (a plain load
+// could hit a line this CU cached while the byte was not yet written).
+__device__ __forceinline__ uint8_t flushed_byte(const uint8_t* d, uint32_t x) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const uintptr_t a = reinterpret_cast<uintptr_t>(d + x);
+  const uint32_t w = __hip_atomic_load(reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+  return (uint8_t)(w >> (8 * (a & 3)));
 }
 
 // K5 body: the verdict; one-lane decode of valid streams K4 could not split
@@ -2236,11 +2272,16 @@ __device__ void dverdict(uint32_t f, uint64_t dsize, PubSlot* pub, uint32_t tick
 
 // K4: one workgroup per 64 KiB output fragment whose true position differs
 // from the one K-spec assumed.  A fragment stored as one literal is copied by
-// all 256 lanes; any other is decoded by wave 0 in LDS (tags and short
-// literals read from a staged window of the compressed bytes) and written
-// out by all.  The last workgroup to finish gives the verdict (K5).
-__global__ __launch_bounds__(256) void snappy_dfrag(const SnappyDJobs J) {
-  __shared__ uint32_t ob32[kFrag / 4];
+// all 256 lanes; any other is decoded by wave 0 through an 8 KiB LDS ring of
+// its output (tags and short literals read from a staged window of the
+// compressed bytes; the ring flushed to the output as it fills).  The small
+// LDS footprint and 64 registers let 8 workgroups share a CU: a decode is one
+// wave's dependent chain of LDS and lane operations, so the chip's 2048
+// decoders (one round for 128 MiB) set the rate -- with the whole fragment in
+// LDS, 2 per CU, sorted keys decoded at 11.2 GB/s, with the ring 18.3
+// (tools/ab_ring2.sh).  The last workgroup to finish gives the verdict (K5).
+__global__ __launch_bounds__(256, 8) void snappy_dfrag(const SnappyDJobs J) {
+  __shared__ uint32_t ob32[kRing / 4];
   __shared__ uint32_t ib32[(kInWin + 32) / 4];
   __shared__ uint32_t s_last;
   __shared__ FewLds F;
@@ -2274,7 +2315,7 @@ __global__ __launch_bounds__(256) void snappy_dfrag(const SnappyDJobs J) {
   if (redo) {
     PSF_DTRACE(k, 1);
     const Tag t0 = decode_tag(tag_bytes(in, C, p0), p0);
-    if (decode_few(in, C, p0, end, out + o0, tid, F) != kNone) {
+    if (decode_few<4>(in, C, p0, end, out + o0, tid, F) != kNone) {
       // (a fragment of a few tags: done)
     } else if (t0.lit && t0.len == end) {
       copy_g2g<4>(out + o0, in + p0 + t0.hl, end, tid);
@@ -2282,11 +2323,17 @@ __global__ __launch_bounds__(256) void snappy_dfrag(const SnappyDJobs J) {
       if (tid < 64) {
         const uint32_t lane = tid;
         constexpr uint32_t kSpan = kInWin + 16;  // staged bytes [wb, wb + kSpan)
+        constexpr uint32_t RM = kRing - 1;
+        uint8_t* const d = out + o0;
         uint64_t p = p0, wb = p0;
         uint32_t s = stage(ib32, in, C, wb, kSpan, lane);
-        uint32_t o = 0;
+        uint32_t o = 0, flushed = 0;
         const uint8_t* ibb = reinterpret_cast<const uint8_t*>(ib32);
         while (o < end) {
+          if (o - flushed > kRingFlushAt) {
+            ring_flush(ob, d, flushed, o & ~15u, lane);
+            flushed = o & ~15u;
+          }
           if (p + kBatchMargin > wb + kSpan) {
             wb = p;
             s = stage(ib32, in, C, wb, kSpan, lane);
@@ -2312,26 +2359,36 @@ __global__ __launch_bounds__(256) void snappy_dfrag(const SnappyDJobs J) {
             const uint64_t M = M0 & __ballot(vo < end);  // tags past the fragment's end are not its own
             if (M) {
               const bool tag = (M >> lane) & 1;
+              const uint32_t last = 63 - __builtin_clzll(M);
+              const uint32_t oend = lane_of32(vo, last) + lane_of32(tlen, last);
               if (tag && tl.lit) {
-                const uint8_t* d = ibb + qb + lane + tl.hl;
-                for (uint32_t j = 0; j < tlen; ++j) ob[vo + j] = d[j];
+                const uint8_t* q = ibb + qb + lane + tl.hl;
+                for (uint32_t j = 0; j < tlen; ++j) ob[(vo + j) & RM] = q[j];
               }
               for (uint64_t cm = __ballot(tag && !tl.lit); cm; cm &= cm - 1) {
                 const uint32_t k = (uint32_t)__builtin_ctzll(cm);
                 const uint32_t ko = lane_of32(vo, k), L = lane_of32(tlen, k), off = lane_of32(tl.off, k);
                 if (off >= L) {
-                  if (lane < L) ob[ko + lane] = ob[ko - off + lane];
+                  if (ko - off + kRing >= oend) {
+                    if (lane < L) ob[(ko + lane) & RM] = ob[(ko - off + lane) & RM];
+                  } else {  // older than the ring: flushed
+                    const uint8_t b = flushed_byte(d, ko - off + min(lane, L - 1));
+                    if (lane < L) ob[(ko + lane) & RM] = b;
+                  }
                 } else if (lane < L) {
-                  ob[ko + lane] = ob[ko - off + lane % off];
+                  ob[(ko + lane) & RM] = ob[(ko - off + lane % off) & RM];
                 }
               }
-              const uint32_t last = 63 - __builtin_clzll(M);
-              o = lane_of32(vo, last) + lane_of32(tlen, last);
+              o = oend;
               p += last + lane_of32(adv, last);
               if (o >= end || last + lane_of32(adv, last) >= 64) continue;
             }
           }
-          // ---- one tag the general way
+          // ---- one tag the general way (a step of its own)
+          if (o - flushed > kRingFlushAt) {
+            ring_flush(ob, d, flushed, o & ~15u, lane);
+            flushed = o & ~15u;
+          }
           const Tag t = lds_tag(ib32, s + (p - wb), p);
           const uint32_t L = (uint32_t)t.len;
           if (t.lit) {
@@ -2340,30 +2397,34 @@ __global__ __launch_bounds__(256) void snappy_dfrag(const SnappyDJobs J) {
               wb = src;
               s = stage(ib32, in, C, wb, kSpan, lane);
             }
-            if (src + L <= wb + kSpan) {
-              const uint8_t* q = reinterpret_cast<const uint8_t*>(ib32) + s + (src - wb);
-              for (uint32_t i = lane; i < L; i += 64) ob[o + i] = q[i];
-            } else {
-              literal_to_lds(ob, o, in, src, L, lane);
+            const bool staged = src + L <= wb + kSpan;
+            for (uint32_t q0 = 0; q0 < L; q0 += kRingStep) {  // pieces of one step each
+              const uint32_t n = min(L - q0, kRingStep), oq = o + q0;
+              if (oq - flushed > kRingFlushAt) {
+                ring_flush(ob, d, flushed, oq & ~15u, lane);
+                flushed = oq & ~15u;
+              }
+              if (staged) {
+                const uint8_t* q = reinterpret_cast<const uint8_t*>(ib32) + s + (src - wb) + q0;
+                for (uint32_t i = lane; i < n; i += 64) ob[(oq + i) & RM] = q[i];
+              } else {
+                literal_to_lds(ob, oq, in, src + q0, n, lane);
+              }
             }
-          } else if (t.off >= L) {
-            for (uint32_t i = lane; i < L; i += 64) ob[o + i] = ob[o - t.off + i];
-          } else {
-            for (uint32_t i = lane; i < L; i += 64) ob[o + i] = ob[o - t.off + i % t.off];
+          } else if (t.off >= L) {  // (L <= 64)
+            if (o - t.off + kRing >= o + L) {
+              if (lane < L) ob[(o + lane) & RM] = ob[(o - t.off + lane) & RM];
+            } else {
+              const uint8_t b = flushed_byte(d, o - t.off + min(lane, L - 1));
+              if (lane < L) ob[(o + lane) & RM] = b;
+            }
+          } else if (lane < L) {
+            ob[(o + lane) & RM] = ob[(o - t.off + lane % t.off) & RM];
           }
           o += L;
           p = t.next;
         }
-      }
-      __syncthreads();
-      uint8_t* d = out + o0;
-      if ((reinterpret_cast<uintptr_t>(d) & 15) == 0) {
-        const uint32_t nv = end >> 4;
-        for (uint32_t i = tid; i < nv; i += 256)
-          reinterpret_cast<uint4*>(d)[i] = reinterpret_cast<const uint4*>(ob32)[i];
-        for (uint32_t i = (nv << 4) + tid; i < end; i += 256) d[i] = ob[i];
-      } else {
-        for (uint32_t i = tid; i < end; i += 256) d[i] = ob[i];
+        ring_flush(ob, d, flushed, end, lane);
       }
     }
   }

@@ -367,3 +367,41 @@ def test_tag_dense_with_long_literals_roundtrip(ctx, port):
     back = ctx.snappy_uncompress(s).cpu().numpy().tobytes()
     ok = back == data
     assert ok
+
+
+def _lz_fragments(rng, nfrag, dist):
+    """Per 64 KiB fragment: a random head, then pieces copied from `dist(rng)`
+    bytes back (5-60 bytes each) with 1-3 fresh bytes between them, so the
+    stream is tag-dense and its copies reach back that far."""
+    out = bytearray()
+    for _ in range(nfrag):
+        f = bytearray(rng.integers(0, 256, 256, dtype=np.uint8).tobytes())
+        while len(f) < 65536:
+            d = min(int(dist(rng)), len(f))
+            n = int(rng.integers(5, 61))
+            src = len(f) - d
+            for i in range(n):  # (byte by byte: the copy may overlap itself)
+                f.append(f[src + i])
+            f += rng.integers(0, 256, int(rng.integers(1, 4)), dtype=np.uint8).tobytes()
+        out += f[:65536]
+    return bytes(out)
+
+
+@pytest.mark.parametrize("kind", ["far", "ring_edge"])
+def test_tag_dense_far_copies_roundtrip(ctx, port, kind):
+    """Tag-dense fragments whose copies reach far back (up to 60 KiB, or right
+    around 8 KiB): the fragment decoder keeps the last 8 KiB of its output in
+    LDS and reads older copy sources from the bytes it already wrote out.
+    Compress is 1.1.8's, uncompress gives the bytes back."""
+    rng = np.random.default_rng(77 if kind == "far" else 78)
+    if kind == "far":
+        dist = lambda r: r.integers(1, 60000)  # noqa: E731
+    else:
+        dist = lambda r: 8192 + r.integers(-70, 70)  # noqa: E731
+    data = _lz_fragments(rng, 24, dist)
+    x = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
+    s = ctx.snappy_compress(x)
+    want = port.snappy_compress(data)
+    assert s.cpu().numpy().tobytes() == want
+    back = ctx.snappy_uncompress(s).cpu().numpy().tobytes()
+    assert back == data
