@@ -344,7 +344,7 @@ def test_mutated_multifragment_streams_vs_port(ctx, port, kind):
 
 def test_tag_dense_with_long_literals_roundtrip(ctx, port):
     """Sorted-key runs (tags of a few bytes) between random runs of 100-400
-    bytes (literals longer than 64 bytes, so some straddle a 16 KiB window
+    bytes (literals longer than 64 bytes, so some straddle an 8 KiB window
     start of the stream and the chain enters that window past its first 64
     bytes): the windows are then linked by K2's walk instead of the parallel
     prefix (K2p), and the bytes must come back either way -- and the stream
