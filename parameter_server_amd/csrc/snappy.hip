@@ -1275,12 +1275,14 @@ struct DJob {
   double fratio;
   float fmn, fmx;
   uint32_t fnb, fdbl;
+  uint32_t blk0;  // first linker block of this stream in the linker grids
 };
 struct SnappyDJobs {
   DJob j[kSnappyBatchMax];
-  uint32_t* ctrl;  // 8 words per stream: flags[0..3] (verdict, indexed, decoded by K-spec), counters[4..7]
+  uint32_t* ctrl;  // 8 words per stream: flags[0..3] (verdict, indexed, decoded by K-spec, linked by K2b), counters[4..7]
   PubSlot* pub;
   uint32_t njobs, nfo1, nwin;  // streams; output fragments (at least one per stream); windows
+  uint32_t nblk;               // linker blocks (kLinkPer windows each)
   uint32_t* znext;  // the next launch's zeroed ctrl region (null: none), cleared by K-spec
   uint32_t zwords;
 };
@@ -1856,10 +1858,10 @@ constexpr uint32_t kEarly = 1024;  // bytes of a window where K1's starts are ex
 // that would start at p + lane, one scalar walk picks the chain's tags in
 // [p, p + 64).  Adds the output to o, returns the exit position.  kRecord:
 // lane 0's chain of K1 -- each tag into the bitmap, its output count before
-// it into cum (and cum0 below kEarly).
+// it into cum.
 template <bool kRecord>
 __device__ uint64_t scan_walk(const uint32_t* b32, uint32_t s, uint32_t wl, uint64_t p, uint64_t& o, uint32_t lane,
-                              uint32_t* bm, uint32_t* __restrict__ cum, uint32_t* cum0) {
+                              uint32_t* bm, uint32_t* __restrict__ cum) {
   while (p < wl) {
     const uint64_t pl = min(p + lane, (uint64_t)wl);
     const Tag tl = lds_tag(b32, s + pl, pl);
@@ -1873,7 +1875,6 @@ __device__ uint64_t scan_walk(const uint32_t* b32, uint32_t s, uint32_t wl, uint
       const uint64_t r = p + lane;
       atomicOr(&bm[r >> 5], 1u << (r & 31));
       cum[r] = (uint32_t)(o + rel);
-      if (r < kEarly) cum0[r] = (uint32_t)(o + rel);
     }
     const uint32_t last = 63 - __builtin_clzll(M);
     o += lane_of32(rel, last) + lane_of64(tl.len, last);
@@ -1882,7 +1883,7 @@ __device__ uint64_t scan_walk(const uint32_t* b32, uint32_t s, uint32_t wl, uint
   return p;
 }
 
-__device__ void dscan_body(const SnappyDJobs& J, uint32_t ji, uint32_t w, uint32_t* b32, uint32_t* bm, uint32_t* cum0) {
+__device__ void dscan_body(const SnappyDJobs& J, uint32_t ji, uint32_t w, uint32_t* b32, uint32_t* bm) {
   const DJob& D = J.j[ji];
   const DScr S = dscr(J, D, ji);
   if (!(*S.flags & kFlagScan)) return;  // K0 linked the stream already
@@ -1900,14 +1901,14 @@ __device__ void dscan_body(const SnappyDJobs& J, uint32_t ji, uint32_t w, uint32
   for (uint32_t i = lane; i < kWin / 32; i += 64) bm[i] = 0;
   __syncthreads();
   // ---- lane 0's chain (from offset 0) in batches: its tags into the
-  // bitmap, each tag's output count before it into cum (K2), and for the
-  // first kEarly bytes into cum0 (the other starts meet it there)
+  // bitmap, each tag's output count before it into cum (K2; the other starts
+  // read it back where they meet the chain)
   uint64_t o = 0;
-  const uint64_t exit0 = scan_walk<true>(b32, s, wl, 0, o, lane, bm, cum + base, cum0);
+  const uint64_t exit0 = scan_walk<true>(b32, s, wl, 0, o, lane, bm, cum + base);
   const uint64_t total0 = o;
   __syncthreads();
   // ---- the other starts: each lane steps its own chain until it lands on
-  // lane 0's (its exit is then lane 0's and its total follows from cum0),
+  // lane 0's (its exit is then lane 0's and its total follows from cum),
   // leaves the window, or passes kEarly bytes.  Starts on one chain that
   // never meets lane 0's (sorted keys: the chain that reads every copy's
   // offset byte as a 3-byte literal) stop at the same first position past
@@ -1915,13 +1916,14 @@ __device__ void dscan_body(const SnappyDJobs& J, uint32_t ji, uint32_t w, uint32
   uint64_t p = lane;
   o = 0;
   bool alive = lane > 0 && p < wl;
-  bool pending = false;
+  bool pending = false, met = false;
   uint64_t ex = lane == 0 ? exit0 : p, tot = lane == 0 ? total0 : 0;
   while (__ballot(alive)) {
     if (alive) {
       if (p < kEarly && ((bm[p >> 5] >> (p & 31)) & 1)) {
         ex = exit0;
-        tot = o + total0 - cum0[p];
+        tot = o + total0;  // - cum[p], below
+        met = true;
         alive = false;
       } else {
         const Tag t = lds_tag(b32, s + p, p);
@@ -1938,10 +1940,14 @@ __device__ void dscan_body(const SnappyDJobs& J, uint32_t ji, uint32_t w, uint32
       }
     }
   }
+  // cum[p] where a start met the chain: this wave's own stores above, read
+  // once they have landed in L2 (agent scope: not from a line the CU cached)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (met) tot -= __hip_atomic_load(cum + base + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   for (uint64_t pm = __ballot(pending); pm; pm = __ballot(pending)) {
     const uint64_t P = lane_of64(p, (uint32_t)__builtin_ctzll(pm));
     uint64_t oP = 0;
-    const uint64_t eP = scan_walk<false>(b32, s, wl, P, oP, lane, nullptr, nullptr, nullptr);
+    const uint64_t eP = scan_walk<false>(b32, s, wl, P, oP, lane, nullptr, nullptr);
     if (pending && p == P) {
       ex = eP;
       tot = o + oP;
@@ -2032,13 +2038,12 @@ __device__ __forceinline__ void dslow_needs(const SnappyDJobs& J, bool& scan, bo
 __global__ __launch_bounds__(64) void snappy_dscan(const SnappyDJobs J) {
   __shared__ uint32_t b32[(kWin + 32) / 4];
   __shared__ uint32_t bm[kWin / 32];
-  __shared__ uint32_t cum0[kEarly];
   bool scan, index;
   dslow_needs(J, scan, index);
   if (!scan) return;
   for (uint32_t w = blockIdx.x; w < J.nwin; w += gridDim.x) {
     const uint32_t ji = djob_win(J, w);
-    dscan_body(J, ji, w - J.j[ji].win0, b32, bm, cum0);
+    dscan_body(J, ji, w - J.j[ji].win0, b32, bm);
   }
 }
 // K2: one workgroup per stream links its windows
@@ -2058,15 +2063,22 @@ __global__ __launch_bounds__(64) void snappy_dlink(const SnappyDJobs J) {
 // Window w's K1 tables are a function on entry offsets: F_w(l) = the next
 // window's entry offset (or the stream's end), with T_w(l) output bytes; the
 // chain's entries are the prefix compositions of these functions from
-// window 0's offset 0.  Each wave composes the functions of a block of windows
-// (lane l follows the chain entered at offset l of the block's first window:
-// one lane permute per window), one wave walks the blocks' compositions, and
-// each wave then re-walks its blocks from their known entries to record every
-// window's entry and output offset -- what K2's one-chain walk records, in
-// blocks instead of windows.  A chain that leaves a window anywhere else (a
-// long literal, an entry past the first 64 bytes) leaves the stream to K2.
+// window 0's offset 0.  Three launches compose them in two levels: K2a, one
+// wave per block of kLinkPer windows, composes its block's function (lane l
+// follows the chain entered at offset l of the block's first window: one lane
+// permute per window); K2b, one workgroup per stream, composes the blocks'
+// functions into at most kLinkMaxBlocks superblocks (a wave each), walks
+// those along the true chain and then re-walks each superblock's blocks to
+// record every block's entry; K2c, one wave per block again, re-walks the
+// block's windows from its entry and records each window's entry and output
+// offset -- what K2's one-chain walk records.  A chain that leaves a window
+// anywhere else (a long literal, an entry past the first 64 bytes) leaves the
+// stream to K2.  (Round 4: one workgroup per stream did both levels, 0.47 ms
+// for 128 MiB of sorted keys in 8 KiB windows, its waves' table loads one
+// memory latency per 8 windows.)
 constexpr uint32_t kLinkWaves = 16;
 constexpr uint32_t kLinkMaxBlocks = 128;
+constexpr uint32_t kLinkPer = 16;
 constexpr uint32_t kLinkEnd = 64, kLinkOdd = 65;  // F codes besides an entry offset 0..63
 __device__ __forceinline__ uint32_t link_code(uint64_t x, uint32_t w, uint32_t nwin, uint32_t hdr, uint64_t C) {
   if (w + 1 == nwin) return x == C ? kLinkEnd : kLinkOdd;
@@ -2079,9 +2091,75 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t l) {
   const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), (int)l, 64);
   return ((uint64_t)hi << 32) | lo;
 }
-__global__ __launch_bounds__(kLinkWaves * 64) void snappy_dlinkp(const SnappyDJobs J) {
-  __shared__ uint8_t bF[kLinkMaxBlocks][kStarts];
-  __shared__ uint64_t bT[kLinkMaxBlocks][kStarts];
+// a stream's linker blocks: F (u8 codes) and T rows, each block's entry and
+// output offset; after cum in the stream's scratch (djob_bytes)
+struct LinkBlk {
+  uint64_t *T, *out;
+  uint32_t* entry;
+  uint8_t* F;
+};
+__device__ __forceinline__ uint32_t link_nblk(uint32_t nwin) { return (nwin + kLinkPer - 1) / kLinkPer; }
+__device__ __forceinline__ LinkBlk link_blk(const DJob& D, const DScr& S) {
+  const size_t nb = link_nblk(D.nwin) + 1;
+  LinkBlk B;
+  B.T = reinterpret_cast<uint64_t*>(S.cum + ((D.C + 1) & ~(uint64_t)1));
+  B.out = B.T + nb * kStarts;
+  B.entry = reinterpret_cast<uint32_t*>(B.out + nb);
+  B.F = reinterpret_cast<uint8_t*>(B.entry + nb);
+  return B;
+}
+__device__ __forceinline__ uint32_t djob_blk(const SnappyDJobs& J, uint32_t b) {
+  uint32_t i = 0;
+  while (i + 1 < J.njobs && b >= J.j[i + 1].blk0) ++i;
+  return i;
+}
+// The composition of windows [w0, w1)'s functions applied from entry `cur`
+// (lane l: cur = l), with its output count; 8 windows' tables in flight.
+__device__ __forceinline__ void link_compose(const DScr& S, uint32_t w0, uint32_t w1, uint32_t nwin, uint32_t hdr,
+                                             uint64_t C, uint32_t lane, uint32_t& cur, uint64_t& acc) {
+  for (uint32_t wc = w0; wc < w1; wc += 8) {
+    uint64_t x[8], t[8];
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) {
+      const uint32_t w = min(wc + k, w1 - 1);
+      x[k] = S.wexit[(size_t)w * kStarts + lane];
+      t[k] = S.wtotal[(size_t)w * kStarts + lane];
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) {
+      if (wc + k >= w1) break;
+      const uint32_t code = link_code(x[k], wc + k, nwin, hdr, C);
+      const uint32_t nc = (uint32_t)__shfl((int)code, (int)(cur & 63), 64);
+      const uint64_t nt = shfl64(t[k], cur & 63);
+      if (cur < kStarts) {
+        acc += nt;
+        cur = nc;
+      } else {
+        cur = kLinkOdd;  // (the end is only ever the last window's)
+      }
+    }
+  }
+}
+// K2a: one wave per linker block
+__global__ __launch_bounds__(64) void snappy_dlinka(const SnappyDJobs J) {
+  const uint32_t lane = threadIdx.x;
+  const uint32_t ji = djob_blk(J, blockIdx.x);
+  const DJob& D = J.j[ji];
+  const DScr S = dscr(J, D, ji);
+  if (!(*S.flags & kFlagScan)) return;
+  const uint32_t b = blockIdx.x - D.blk0, w0 = b * kLinkPer, w1 = min(D.nwin, w0 + kLinkPer);
+  if (w0 >= w1) return;
+  uint32_t cur = lane;
+  uint64_t acc = 0;
+  link_compose(S, w0, w1, D.nwin, D.hdr, D.C, lane, cur, acc);
+  const LinkBlk B = link_blk(D, S);
+  B.F[(size_t)b * kStarts + lane] = (uint8_t)cur;
+  B.T[(size_t)b * kStarts + lane] = acc;
+}
+// K2b: one workgroup per stream: the blocks' entries along the true chain
+__global__ __launch_bounds__(kLinkWaves * 64) void snappy_dlinkb(const SnappyDJobs J) {
+  __shared__ uint8_t sF[kLinkMaxBlocks][kStarts];
+  __shared__ uint64_t sT[kLinkMaxBlocks][kStarts];
   __shared__ uint32_t s_entry[kLinkMaxBlocks];
   __shared__ uint64_t s_out[kLinkMaxBlocks];
   __shared__ uint32_t s_ok;
@@ -2090,88 +2168,125 @@ __global__ __launch_bounds__(kLinkWaves * 64) void snappy_dlinkp(const SnappyDJo
     const DJob& D = J.j[ji];
     const DScr S = dscr(J, D, ji);
     if (!(*S.flags & kFlagScan)) continue;  // (uniform: every wave reads the same word)
-    const uint32_t nwin = D.nwin, hdr = D.hdr;
-    const uint64_t C = D.C;
-    if (nwin == 0) continue;
-    const uint32_t per = max(64u, (nwin + kLinkMaxBlocks - 1) / kLinkMaxBlocks);
-    const uint32_t nb = (nwin + per - 1) / per;
-    // ---- each block's composed function
-    for (uint32_t b = wave; b < nb; b += kLinkWaves) {
-      const uint32_t w0 = b * per, w1 = min(nwin, w0 + per);
+    const uint32_t nb = link_nblk(D.nwin);
+    if (nb == 0) continue;
+    const LinkBlk B = link_blk(D, S);
+    const uint32_t per = max(8u, (nb + kLinkMaxBlocks - 1) / kLinkMaxBlocks);
+    const uint32_t ns = (nb + per - 1) / per;
+    // ---- each superblock's composed function
+    for (uint32_t sb = wave; sb < ns; sb += kLinkWaves) {
+      const uint32_t b0 = sb * per, b1 = min(nb, b0 + per);
       uint32_t cur = lane;
       uint64_t acc = 0;
-      for (uint32_t wc = w0; wc < w1; wc += 8) {  // 8 windows' tables in flight
-        uint64_t x[8], t[8];
+      for (uint32_t bc = b0; bc < b1; bc += 8) {
+        uint32_t f[8];
+        uint64_t t[8];
 #pragma unroll
         for (uint32_t k = 0; k < 8; ++k) {
-          const uint32_t w = min(wc + k, w1 - 1);
-          x[k] = S.wexit[(size_t)w * kStarts + lane];
-          t[k] = S.wtotal[(size_t)w * kStarts + lane];
+          const uint32_t b = min(bc + k, b1 - 1);
+          f[k] = B.F[(size_t)b * kStarts + lane];
+          t[k] = B.T[(size_t)b * kStarts + lane];
         }
 #pragma unroll
         for (uint32_t k = 0; k < 8; ++k) {
-          if (wc + k >= w1) break;
-          const uint32_t code = link_code(x[k], wc + k, nwin, hdr, C);
-          const uint32_t nc = (uint32_t)__shfl((int)code, (int)(cur & 63), 64);
+          if (bc + k >= b1) break;
+          const uint32_t nc = (uint32_t)__shfl((int)f[k], (int)(cur & 63), 64);
           const uint64_t nt = shfl64(t[k], cur & 63);
           if (cur < kStarts) {
             acc += nt;
             cur = nc;
           } else {
-            cur = kLinkOdd;  // (the end is only ever the last window's)
+            cur = kLinkOdd;
           }
         }
       }
-      bF[b][lane] = (uint8_t)cur;
-      bT[b][lane] = acc;
+      sF[sb][lane] = (uint8_t)cur;
+      sT[sb][lane] = acc;
     }
     __syncthreads();
-    // ---- the blocks' entries along the true chain
+    // ---- the superblocks' entries along the true chain
     if (threadIdx.x == 0) {
       uint32_t e = 0;
       uint64_t o = 0;
-      for (uint32_t b = 0; b < nb && e < kStarts; ++b) {
-        s_entry[b] = e;
-        s_out[b] = o;
-        o += bT[b][e];
-        e = bF[b][e];
+      for (uint32_t sb = 0; sb < ns && e < kStarts; ++sb) {
+        s_entry[sb] = e;
+        s_out[sb] = o;
+        o += sT[sb][e];
+        e = sF[sb][e];
       }
       s_ok = e == kLinkEnd ? (o == D.dsize ? 1u : 2u) : 0u;  // 0: K2 walks it
     }
     __syncthreads();
     const uint32_t ok = s_ok;
     if (ok == 1) {
-      // ---- every window's entry, from its block's
-      for (uint32_t b = wave; b < nb; b += kLinkWaves) {
-        const uint32_t w0 = b * per, w1 = min(nwin, w0 + per);
-        uint32_t e = s_entry[b];
-        uint64_t o = s_out[b];
-        for (uint32_t wc = w0; wc < w1; wc += 8) {
-          uint64_t x[8], t[8];
+      // ---- every block's entry, from its superblock's
+      for (uint32_t sb = wave; sb < ns; sb += kLinkWaves) {
+        const uint32_t b0 = sb * per, b1 = min(nb, b0 + per);
+        uint32_t e = s_entry[sb];
+        uint64_t o = s_out[sb];
+        for (uint32_t bc = b0; bc < b1; bc += 8) {
+          uint32_t f[8];
+          uint64_t t[8];
 #pragma unroll
           for (uint32_t k = 0; k < 8; ++k) {
-            const uint32_t w = min(wc + k, w1 - 1);
-            x[k] = S.wexit[(size_t)w * kStarts + lane];
-            t[k] = S.wtotal[(size_t)w * kStarts + lane];
+            const uint32_t b = min(bc + k, b1 - 1);
+            f[k] = B.F[(size_t)b * kStarts + lane];
+            t[k] = B.T[(size_t)b * kStarts + lane];
           }
 #pragma unroll
           for (uint32_t k = 0; k < 8; ++k) {
-            if (wc + k >= w1) break;
-            const uint32_t w = wc + k;
+            if (bc + k >= b1) break;
             if (lane == 0) {
-              S.wentry[w] = hdr + (uint64_t)w * kWin + e;
-              S.woff[w] = o;
+              B.entry[bc + k] = e;
+              B.out[bc + k] = o;
             }
-            const uint32_t code = link_code(x[k], w, nwin, hdr, C);
             o += lane_of64(t[k], e);
-            e = lane_of32(code, e);
+            e = lane_of32(f[k], e);
           }
         }
       }
     }
     __syncthreads();
-    if (threadIdx.x == 0 && ok) *S.flags = ok == 2 ? kFlagInvalid : 0;  // (K2 then skips the stream)
+    if (threadIdx.x == 0) {
+      S.flags[3] = ok == 1 ? 1u : 0u;  // K2c's cue
+      if (ok) *S.flags = ok == 2 ? kFlagInvalid : 0;  // (K2 then skips the stream)
+    }
     __syncthreads();
+  }
+}
+// K2c: one wave per linker block of a stream K2b linked: its windows' entries
+__global__ __launch_bounds__(64) void snappy_dlinkc(const SnappyDJobs J) {
+  const uint32_t lane = threadIdx.x;
+  const uint32_t ji = djob_blk(J, blockIdx.x);
+  const DJob& D = J.j[ji];
+  const DScr S = dscr(J, D, ji);
+  if (S.flags[3] != 1) return;
+  const uint32_t b = blockIdx.x - D.blk0, w0 = b * kLinkPer, w1 = min(D.nwin, w0 + kLinkPer);
+  if (w0 >= w1) return;
+  const LinkBlk B = link_blk(D, S);
+  uint32_t e = B.entry[b];
+  uint64_t o = B.out[b];
+  const uint32_t nwin = D.nwin, hdr = D.hdr;
+  for (uint32_t wc = w0; wc < w1; wc += 8) {
+    uint64_t x[8], t[8];
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) {
+      const uint32_t w = min(wc + k, w1 - 1);
+      x[k] = S.wexit[(size_t)w * kStarts + lane];
+      t[k] = S.wtotal[(size_t)w * kStarts + lane];
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) {
+      if (wc + k >= w1) break;
+      const uint32_t w = wc + k;
+      if (lane == 0) {
+        S.wentry[w] = hdr + (uint64_t)w * kWin + e;
+        S.woff[w] = o;
+      }
+      const uint32_t code = link_code(x[k], w, nwin, hdr, D.C);
+      o += lane_of64(t[k], e);
+      e = lane_of32(code, e);
+    }
   }
 }
 
@@ -2526,7 +2641,9 @@ static size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 static size_t djob_bytes(size_t C, size_t dsize) {
   const size_t nwin = (C + kWin - 1) / kWin + 1;
   const size_t nfo = (dsize + kFrag - 1) / kFrag + 1;
-  return align256(nwin * (kWin / 8) + C * 4 + nwin * 8 * (2 * kStarts + 2) + 4 * nfo * 8 + 64);
+  const size_t nblk = (nwin + kLinkPer - 1) / kLinkPer + 1;  // linker blocks (LinkBlk)
+  return align256(nwin * (kWin / 8) + C * 4 + nwin * 8 * (2 * kStarts + 2) + 4 * nfo * 8 + 64 +
+                  nblk * (kStarts * 9 + 12) + 16);
 }
 
 size_t snappy_uncompress_batch_scratch(const SnappyDJob* jobs, int njobs) {
@@ -2572,6 +2689,7 @@ int snappy_uncompress_batch_launch(const SnappyDJob* jobs, int njobs, void* scra
     D.nfo = (uint32_t)((q.dsize + kFrag - 1) / kFrag);
     D.fo0 = K.nfo1;
     D.win0 = K.nwin;
+    D.blk0 = K.nblk;
     D.slot = (uint32_t)q.slot;
     D.ticket = q.ticket;
     if (q.dq.values) {
@@ -2586,6 +2704,7 @@ int snappy_uncompress_batch_launch(const SnappyDJob* jobs, int njobs, void* scra
     }
     K.nfo1 += D.nfo ? D.nfo : 1;  // an empty output still takes one workgroup (header check, verdict)
     K.nwin += D.nwin;
+    K.nblk += (D.nwin + kLinkPer - 1) / kLinkPer;
     data += djob_bytes(q.c, q.dsize);
     bytes += (double)q.c +
              (q.dq.values ? (double)(q.dsize / q.dq.nb) * (q.dq.value_type == kDouble ? 8 : 4) : (double)q.dsize);
@@ -2626,7 +2745,11 @@ static bool link_parallel() {
 static int launch_tail(const SnappyDJobs& K, hipStream_t st) {
   if (K.nwin) {
     hipLaunchKernelGGL(snappy_dscan, dim3(K.nwin), dim3(64), 0, st, K);
-    if (link_parallel()) hipLaunchKernelGGL(snappy_dlinkp, dim3(K.njobs), dim3(kLinkWaves * 64), 0, st, K);
+    if (link_parallel()) {
+      hipLaunchKernelGGL(snappy_dlinka, dim3(K.nblk), dim3(64), 0, st, K);
+      hipLaunchKernelGGL(snappy_dlinkb, dim3(K.njobs), dim3(kLinkWaves * 64), 0, st, K);
+      hipLaunchKernelGGL(snappy_dlinkc, dim3(K.nblk), dim3(64), 0, st, K);
+    }
     hipLaunchKernelGGL(snappy_dlink, dim3(K.njobs), dim3(64), 0, st, K);
     hipLaunchKernelGGL(snappy_dindex, dim3(K.nwin), dim3(64), 0, st, K);
   }
