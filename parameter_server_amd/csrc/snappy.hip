@@ -1059,7 +1059,11 @@ constexpr uint64_t kNone = ~0ull;
 constexpr uint32_t kFlagInvalid = 1, kFlagSerial = 2, kFlagScan = 4, kFlagHeader = 8;
 constexpr uint64_t kFullLit = 65536 + 3;  // a 64 KiB fragment stored as one literal (tag 0xF4 + 2 length bytes)
 constexpr uint32_t kStarts = 64;          // K1 parses from each of the first 64 offsets of a window
-constexpr uint32_t kLitBudget = 512;      // K0's single steps before it hands the stream to K1/K2
+// K0's single steps before it hands the stream to K1/K2: one memory latency
+// each, so a tag-dense stream costs K0 about 1 us per step until handed over
+// (512: K-spec 0.59 ms on sorted keys, 64: 0.10; tools/ab_dec.sh); a stream of
+// stored fragments with a few matches (C5's codes) stays well inside it
+constexpr uint32_t kLitBudget = 64;
 
 struct Tag {
   uint64_t next;  // position after the tag (literal data included)

@@ -1,11 +1,11 @@
 # tag-dense uncompress A/B: the snappy / fused / bounded tests with the
-# current build, then tools/bench_snappy.py (sorted keys, zeros) with each of
+# current build (or tools/variants/$TESTVAR), then tools/bench_snappy.py (sorted keys, zeros) with each of
 # tools/variants/$VARS twice, and a kernel trace of each.  Output: gpurun_out/$1/.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 R=$PWD
 O=gpurun_out/${1:-abdec}; mkdir -p $O
-timeout -k 10 500 python -u -m pytest tests/test_gpu_snappy.py tests/test_gpu_fused.py tests/test_gpu_bounded.py -x -q \
+${TESTVAR:+env PSF_LIBRARY_VARIANT=$R/tools/variants/$TESTVAR/libpsf.so} timeout -k 10 500 python -u -m pytest tests/test_gpu_snappy.py tests/test_gpu_fused.py tests/test_gpu_bounded.py -x -q \
   --timeout 200 --timeout-method thread > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
 tail -1 $O/tests.log
 for rep in 1 2; do
