@@ -217,10 +217,11 @@ template <> struct Shifted<float> {
 #endif
 
 // tiles [t0, t1) owned by this workgroup
-__device__ __forceinline__ void tile_range(size_t ntiles, size_t& t0, size_t& t1) {
+__device__ __forceinline__ void tile_range(size_t ntiles, size_t& t0, size_t& t1, uint32_t b = blockIdx.x) {
   const size_t per = (ntiles + gridDim.x - 1) / gridDim.x;
-  t0 = (size_t)blockIdx.x * per;
+  t0 = (size_t)b * per;
   t1 = t0 + per < ntiles ? t0 + per : ntiles;
+  if (t0 > ntiles) t0 = ntiles;
 }
 
 // ------------------------------------------------------ pass 1: min/max ----
@@ -234,17 +235,25 @@ __device__ __forceinline__ void acc_minmax(V e, K& lo, K& hi) {
 }
 
 // partials layout: K lo[grid], K hi[grid].
+// strided: workgroup b reads tiles b, b + grid, ... (the grid sweeps the
+// array front to back together, so the tiles read last are its end);
+// otherwise a contiguous run of tiles each.
 template <typename V, bool kVec>
 __global__ __launch_bounds__(kBlock) void ff_minmax_partials(const V* __restrict__ x, size_t n,
-                                                              void* __restrict__ partials) {
+                                                              void* __restrict__ partials, uint32_t strided) {
   typedef typename KeyOf<V>::K K;
   K lo = KeyOf<V>::kLoId, hi = KeyOf<V>::kHiId;
   if (kVec) {
     const size_t ngroups = n >> 2;
     const size_t ntiles = (ngroups + kTileGroups - 1) / kTileGroups;
-    size_t t0, t1;
+    size_t t0, t1, dt = 1;
     tile_range(ntiles, t0, t1);
-    for (size_t t = t0; t < t1; ++t) {
+    if (strided) {
+      t0 = blockIdx.x;
+      t1 = ntiles;
+      dt = gridDim.x;
+    }
+    for (size_t t = t0; t < t1; t += dt) {
       const size_t gb = t * kTileGroups + threadIdx.x;
       if ((t + 1) * kTileGroups <= ngroups) {
         V v[4][4];
@@ -336,6 +345,9 @@ struct EncodeParams {
   float* range_host;        // {min, max, status} into host-mapped memory, may be null
   PubSlot* pub;             // host-mapped publish slot, may be null
   uint32_t ticket;
+  // 1: workgroup b takes the tiles of workgroup grid - 1 - b, the array's end
+  // first -- what a strided min/max pass read last (the Infinity Cache's)
+  uint32_t reverse;
 };
 
 // s -> a*s + c, composed k times.
@@ -664,7 +676,9 @@ __global__ __launch_bounds__(kBlock) void ff_encode(const V* __restrict__ x, siz
   const size_t ntiles = (ngroups + kTileGroups - 1) / kTileGroups;
   const size_t nfull = ngroups / kTileGroups;
   size_t t0 = 0, t1 = 0;
-  if (kVec) tile_range(ntiles, t0, t1);
+  if (kVec) {
+    tile_range(ntiles, t0, t1, p.reverse ? gridDim.x - 1 - blockIdx.x : blockIdx.x);
+  }
   const size_t tf = t1 < nfull ? t1 : nfull;  // full tiles are [t0, tf)
   V first[4][4];
   if (kVec && t0 < tf) {
@@ -1428,9 +1442,12 @@ static int tile_grid(size_t n, int cap) {
   return (int)g;
 }
 
+static bool enc_perm_mode();
+
 template <typename V, int NB, bool kVec>
 static void launch_encode(const V* x, size_t n, uint8_t* out, EncodeParams p, hipStream_t st) {
   const int grid = kVec ? tile_grid(n, kStreamGrid) : ff_grid(n);
+  p.reverse = kVec && p.partials && enc_perm_mode() ? 1u : 0u;  // after a strided min/max pass
   lcg_affine_pow(4ull * kBlock, p.a_lane, p.c_lane);
   lcg_affine_pow(4ull * kTileGroups, p.a_tile, p.c_tile);
   lcg_affine_pow((uint64_t)grid * kBlock, p.a_thr, p.c_thr);
@@ -1486,9 +1503,10 @@ static int encode_typed(const V* x, size_t n, int nb, const FixedPoint& preset, 
     const int grid = vec ? tile_grid(n, kMinmaxGrid) : (ff_grid(n) < kMinmaxGrid ? ff_grid(n) : kMinmaxGrid);
     ProfScope ps(prof, kKMinmax, st, (double)n * sizeof(V));
     if (vec)
-      hipLaunchKernelGGL((ff_minmax_partials<V, true>), dim3(grid), dim3(kBlock), 0, st, x, n, partials);
+      hipLaunchKernelGGL((ff_minmax_partials<V, true>), dim3(grid), dim3(kBlock), 0, st, x, n, partials,
+                         enc_perm_mode() ? 1u : 0u);
     else
-      hipLaunchKernelGGL((ff_minmax_partials<V, false>), dim3(grid), dim3(kBlock), 0, st, x, n, partials);
+      hipLaunchKernelGGL((ff_minmax_partials<V, false>), dim3(grid), dim3(kBlock), 0, st, x, n, partials, 0u);
     p.partials = partials;
     p.nparts = grid;
     if (launch_status() != kOk) return kErrHip;
@@ -1665,6 +1683,21 @@ static bool mm_reverse_mode(double bytes_mm) {
   }();
   (void)bytes_mm;
   return mode == 1;
+}
+
+// PSF_ENC_PERM (A/B knob, tools/ab_perm.sh): 0 keeps the min/max pass in
+// contiguous runs per workgroup and the encode in tile order.  On (default):
+// the strided min/max pass sweeps the array front to back (2^28: 159 -> 156
+// us) and the encode starts from the end it read last; the Infinity Cache
+// share that buys is small (encode 220 -> 222 us at 2^28, the 2^27 line
+// 1743 -> 1768 GiB/s; profiles/r04_ab_perm.txt).  (Interleaving the encode
+// over the min/max runs' last chunks instead cost it 219 -> 237 us.)
+static bool enc_perm_mode() {
+  static const bool on = [] {
+    const char* e = getenv("PSF_ENC_PERM");
+    return !(e && *e == '0');
+  }();
+  return on;
 }
 
 template <int CAP>
