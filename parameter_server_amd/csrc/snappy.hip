@@ -20,7 +20,7 @@
 // assumed stored as one literal where a 1.1.8 encoder of incompressible data
 // puts it, checked and copied (K-spec; such a stream is done there).
 // Otherwise tag boundaries are found in parallel: a one-wave linker hops over
-// stored fragments (K0); if it meets too many small tags, every 8 KiB window
+// stored fragments (K0); if it meets too many small tags, every 4 KiB window
 // of the compressed bytes is parsed speculatively from each of its first 64
 // offsets (K1) and one lane links the windows (K2) -- the true chain enters a
 // window on one of those chains almost always, and their bookkeeping gives the
@@ -1038,11 +1038,13 @@ __global__ __launch_bounds__(kPlaceT) void snappy_place(const SnappyCJobs J, con
 // ------------------------------------------------------------------ uncompress
 // compressed bytes per parse window: K1 / K3 are one wave per window whose
 // chain walks are the work, so shorter windows mean more waves at once and
-// shorter walks; K2p's composition grows with the window count.  Sorted keys,
-// 128 MiB: 16 KiB windows 18.2 GB/s, 8 KiB 22.4, 4 KiB 22.7 (tools/ab_win8.sh)
-// -- 8 KiB keeps the window starts (where a long literal sends a stream to
-// K2's serial walk) half as dense as 4 KiB for 1 % less.
-constexpr uint32_t kWin = 8192;
+// shorter walks; the linker's work grows with the window count.  Sorted keys,
+// 128 MiB, with the one-workgroup linker: 16 KiB windows 18.2 GB/s, 8 KiB
+// 22.4, 4 KiB 22.7 (tools/ab_win8.sh); with the three-launch linker (K2a-c)
+// 8 KiB 27.5, 4 KiB 30.0 (tools/ab_dec.sh).  (A literal that carries the
+// chain past a window's first 64 bytes sends the stream to K2's serial walk;
+// smaller windows have more starts to straddle.)
+constexpr uint32_t kWin = 4096;
 constexpr uint32_t kInWin = 4096;  // staged compressed bytes in the fragment decoder
 // The fragment decoder's output window: the last kRing bytes of the fragment
 // decoded so far sit in an LDS ring; older ones have been flushed to the
