@@ -1109,14 +1109,19 @@ __device__ __forceinline__ uint64_t batch_mask(uint32_t a, uint64_t lim, uint64_
   }
   return M;
 }
-// exclusive sum over the wave's lanes below this one
-__device__ __forceinline__ uint32_t wave_excl_sum(uint32_t v, uint32_t lane) {
+// exclusive sum over the wave's lanes below this one, in DPP steps (no LDS
+// round trips: a lane shuffle through ds_bpermute costs one each): the
+// inclusive scan within each row of 16 lanes by row shifts 1, 2, 4, 8 (a lane
+// with no source in its row adds 0), then row 15's total into the next row
+// (row_bcast:15, rows 1 and 3) and lane 31's into rows 2 and 3 (row_bcast:31)
+__device__ __forceinline__ uint32_t wave_excl_sum(uint32_t v, uint32_t) {
   uint32_t x = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(x, d, 64);
-    if ((int)lane >= d) x += y;
-  }
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
   return x - v;
 }
 
