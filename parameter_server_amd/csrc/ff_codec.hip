@@ -1447,7 +1447,10 @@ static bool enc_perm_mode();
 template <typename V, int NB, bool kVec>
 static void launch_encode(const V* x, size_t n, uint8_t* out, EncodeParams p, hipStream_t st) {
   const int grid = kVec ? tile_grid(n, kStreamGrid) : ff_grid(n);
-  p.reverse = kVec && p.partials && enc_perm_mode() ? 1u : 0u;  // after a strided min/max pass
+  // after a strided min/max pass over an array larger than the Infinity
+  // Cache (smaller ones stay on chip whatever the order, and the reversed
+  // order cost C3's 40 MB arrays 9 %: encode 15.8 -> 17.8 us, tools/ab_perm_c13.sh)
+  p.reverse = kVec && p.partials && enc_perm_mode() && (double)n * sizeof(V) > 256.0 * (1 << 20) ? 1u : 0u;
   lcg_affine_pow(4ull * kBlock, p.a_lane, p.c_lane);
   lcg_affine_pow(4ull * kTileGroups, p.a_tile, p.c_tile);
   lcg_affine_pow((uint64_t)grid * kBlock, p.a_thr, p.c_thr);
@@ -1504,7 +1507,7 @@ static int encode_typed(const V* x, size_t n, int nb, const FixedPoint& preset, 
     ProfScope ps(prof, kKMinmax, st, (double)n * sizeof(V));
     if (vec)
       hipLaunchKernelGGL((ff_minmax_partials<V, true>), dim3(grid), dim3(kBlock), 0, st, x, n, partials,
-                         enc_perm_mode() ? 1u : 0u);
+                         enc_perm_mode() && (double)n * sizeof(V) > 256.0 * (1 << 20) ? 1u : 0u);
     else
       hipLaunchKernelGGL((ff_minmax_partials<V, false>), dim3(grid), dim3(kBlock), 0, st, x, n, partials, 0u);
     p.partials = partials;

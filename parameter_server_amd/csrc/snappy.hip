@@ -2154,18 +2154,20 @@ __device__ __forceinline__ void link_compose(const DScr& S, uint32_t w0, uint32_
 // K2a: one wave per linker block
 __global__ __launch_bounds__(64) void snappy_dlinka(const SnappyDJobs J) {
   const uint32_t lane = threadIdx.x;
-  const uint32_t ji = djob_blk(J, blockIdx.x);
-  const DJob& D = J.j[ji];
-  const DScr S = dscr(J, D, ji);
-  if (!(*S.flags & kFlagScan)) return;
-  const uint32_t b = blockIdx.x - D.blk0, w0 = b * kLinkPer, w1 = min(D.nwin, w0 + kLinkPer);
-  if (w0 >= w1) return;
-  uint32_t cur = lane;
-  uint64_t acc = 0;
-  link_compose(S, w0, w1, D.nwin, D.hdr, D.C, lane, cur, acc);
-  const LinkBlk B = link_blk(D, S);
-  B.F[(size_t)b * kStarts + lane] = (uint8_t)cur;
-  B.T[(size_t)b * kStarts + lane] = acc;
+  for (uint32_t g = blockIdx.x; g < J.nblk; g += gridDim.x) {
+    const uint32_t ji = djob_blk(J, g);
+    const DJob& D = J.j[ji];
+    const DScr S = dscr(J, D, ji);
+    if (!(*S.flags & kFlagScan)) continue;
+    const uint32_t b = g - D.blk0, w0 = b * kLinkPer, w1 = min(D.nwin, w0 + kLinkPer);
+    if (w0 >= w1) continue;
+    uint32_t cur = lane;
+    uint64_t acc = 0;
+    link_compose(S, w0, w1, D.nwin, D.hdr, D.C, lane, cur, acc);
+    const LinkBlk B = link_blk(D, S);
+    B.F[(size_t)b * kStarts + lane] = (uint8_t)cur;
+    B.T[(size_t)b * kStarts + lane] = acc;
+  }
 }
 // K2b: one workgroup per stream: the blocks' entries along the true chain
 __global__ __launch_bounds__(kLinkWaves * 64) void snappy_dlinkb(const SnappyDJobs J) {
@@ -2266,13 +2268,14 @@ __global__ __launch_bounds__(kLinkWaves * 64) void snappy_dlinkb(const SnappyDJo
   }
 }
 // K2c: one wave per linker block of a stream K2b linked: its windows' entries
-__global__ __launch_bounds__(64) void snappy_dlinkc(const SnappyDJobs J) {
+// K2c's work for linker block g of the union grid
+__device__ void dlinkc_block(const SnappyDJobs& J, uint32_t g) {
   const uint32_t lane = threadIdx.x;
-  const uint32_t ji = djob_blk(J, blockIdx.x);
+  const uint32_t ji = djob_blk(J, g);
   const DJob& D = J.j[ji];
   const DScr S = dscr(J, D, ji);
   if (S.flags[3] != 1) return;
-  const uint32_t b = blockIdx.x - D.blk0, w0 = b * kLinkPer, w1 = min(D.nwin, w0 + kLinkPer);
+  const uint32_t b = g - D.blk0, w0 = b * kLinkPer, w1 = min(D.nwin, w0 + kLinkPer);
   if (w0 >= w1) return;
   const LinkBlk B = link_blk(D, S);
   uint32_t e = B.entry[b];
@@ -2301,6 +2304,9 @@ __global__ __launch_bounds__(64) void snappy_dlinkc(const SnappyDJobs J) {
   }
 }
 
+__global__ __launch_bounds__(64) void snappy_dlinkc(const SnappyDJobs J) {
+  for (uint32_t g = blockIdx.x; g < J.nblk; g += gridDim.x) dlinkc_block(J, g);
+}
 // K3: windows indexed (streams K0 did not walk to the end)
 __global__ __launch_bounds__(64) void snappy_dindex(const SnappyDJobs J) {
   __shared__ uint32_t b32[(kWin + 32) / 4];
@@ -2752,17 +2758,25 @@ static bool link_parallel() {
   return on;
 }
 
-// K1-K3 and K4 (+ K5) of a batch whose fast path has run
+// K1-K3 and K4 (+ K5) of a batch whose fast path has run.  K2a / K2c / K3
+// loop over their blocks / windows on grids capped at about twice what the
+// chip holds at once (K3: 32 waves per CU), so a stream they have nothing to
+// do for (stored fragments: K-spec decoded it) costs a few thousand
+// workgroups, not one per 4 KiB window.  K1 keeps one workgroup per window:
+// with a capped grid each workgroup's share of windows is fixed and the
+// tag-dense scan lost its dynamic balance (sorted keys, 128 MiB: K1 0.83 ->
+// 0.95 ms at twice its residency, 1.04 at once; tools/ab_dec.sh abcap / abcap2).
+constexpr uint32_t kIndexGrid = 16384, kLinkGrid = 1024;
 static int launch_tail(const SnappyDJobs& K, hipStream_t st) {
   if (K.nwin) {
     hipLaunchKernelGGL(snappy_dscan, dim3(K.nwin), dim3(64), 0, st, K);
     if (link_parallel()) {
-      hipLaunchKernelGGL(snappy_dlinka, dim3(K.nblk), dim3(64), 0, st, K);
+      hipLaunchKernelGGL(snappy_dlinka, dim3(min(K.nblk, kLinkGrid)), dim3(64), 0, st, K);
       hipLaunchKernelGGL(snappy_dlinkb, dim3(K.njobs), dim3(kLinkWaves * 64), 0, st, K);
-      hipLaunchKernelGGL(snappy_dlinkc, dim3(K.nblk), dim3(64), 0, st, K);
+      hipLaunchKernelGGL(snappy_dlinkc, dim3(min(K.nblk, kLinkGrid)), dim3(64), 0, st, K);
     }
     hipLaunchKernelGGL(snappy_dlink, dim3(K.njobs), dim3(64), 0, st, K);
-    hipLaunchKernelGGL(snappy_dindex, dim3(K.nwin), dim3(64), 0, st, K);
+    hipLaunchKernelGGL(snappy_dindex, dim3(min(K.nwin, kIndexGrid)), dim3(64), 0, st, K);
   }
   hipLaunchKernelGGL(snappy_dfrag, dim3(K.nfo1), dim3(256), 0, st, K);
   return launch_status();

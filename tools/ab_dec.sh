@@ -11,7 +11,7 @@ tail -1 $O/tests.log
 for rep in 1 2; do
 for v in $VARS; do
   echo "== $v"
-  PSF_LIBRARY_VARIANT=$R/tools/variants/$v/libpsf.so timeout -k 10 200 python -u tools/bench_snappy.py --mib 128 --no-cpu --only sorted_keys_1e9,zeros 2>&1 | grep payload | cut -c1-170 || exit 1
+  PSF_LIBRARY_VARIANT=$R/tools/variants/$v/libpsf.so timeout -k 10 200 python -u tools/bench_snappy.py --mib 128 --no-cpu --only ${ONLY:-sorted_keys_1e9,zeros} 2>&1 | grep payload | cut -c1-170 || exit 1
 done
 done
 for v in $VARS; do
