@@ -26,6 +26,7 @@ def test_cache_bounded_over_1000_sizes(port):
     assert F.device_memory_stats(0)["hbm_cap"] == cap
     worker, server = F.RemoteNode(ctx), F.RemoteNode(ctx)
     big = torch.randn(10_000_000, device="cuda")
+    torch.cuda.synchronize()  # (big is written on torch's stream; the context runs on its own)
     F.set_clock(7)
     try:
         peak_alloc = 0
