@@ -502,3 +502,37 @@ def test_fused_batches_back_to_back(ctx, port):
                 assert got == codes.tobytes(), (it, i)
     finally:
         F.set_clock(None)
+
+
+def test_batch_tag_dense_key_streams(ctx, port):
+    """Five messages decoded in one batch, each with 2^17 sorted keys (1 MiB,
+    tag-dense once compressed: the window scan, the three-launch linker with
+    several 16-window blocks per stream, the index and the fragment decoder,
+    all over a multi-stream grid) and one value array: keys and values come
+    back exactly, and each compressed key stream is snappy 1.1.8's."""
+    from parameter_server_amd import filter as F
+    rng = np.random.default_rng(31)
+    F.set_clock(4242)
+    try:
+        cases = []
+        for k in range(5):
+            n = (1 << 17) + 977 * k
+            keys = np.unique(rng.integers(0, 10**9, n + n // 8).astype(np.uint64))[:n]
+            x = rng.standard_normal(n).astype(np.float32)
+            cases.append((x, 1, None, keys))
+        snd = [F.RemoteNode(ctx) for _ in cases]
+        rcv = [F.RemoteNode(ctx) for _ in cases]
+        ms = [_message(F, *c, ch=i, compress=True) for i, c in enumerate(cases)]
+        F.RemoteNode.encode_many(snd, ms)
+        ws = [m.clone() for m in ms]
+        F.RemoteNode.decode_many(rcv, ws)
+        ctx.sync()
+        for i, (x, nb, preset, keys) in enumerate(cases):
+            kz = snd[i].key(ms[i]).cpu().numpy().tobytes()
+            assert kz == port.snappy_compress(keys.tobytes()), i
+            assert rcv[i].key(ws[i]).cpu().numpy().view(np.uint64).tobytes() == keys.tobytes(), i
+            st, codes, pmn, pmx = port.ff_encode(x, nb, 4242)
+            st, dec = port.ff_decode(codes, nb, pmn, pmx, x.dtype)
+            assert rcv[i].value(ws[i], 0).cpu().numpy().tobytes() == dec.tobytes(), i
+    finally:
+        F.set_clock(None)
