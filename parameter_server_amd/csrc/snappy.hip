@@ -527,9 +527,15 @@ __device__ __forceinline__ uint32_t srcw(const uint8_t* g, const uint32_t* s, ui
 // The literal g[lit, lit + len) at op: for len <= 60 one tag byte (lane 0)
 // and the bytes (lanes 1..len), one store instruction; else the tag and a
 // wave copy.
+// kDefer: the staged single-fragment parse hands literals longer than
+// kDeferMin to the whole workgroup (defer[0] entries of {out offset of the
+// bytes, lit, len} after it), copied from the fragment in memory after the
+// parse, instead of one wave's 16-byte stores; a full list falls back to them.
+constexpr uint32_t kDeferMax = 8, kDeferMin = 1024;
 template <bool kLds>
 __device__ __forceinline__ uint32_t emit_lit(uint8_t* out, uint32_t op, const uint8_t* g, const uint32_t* s,
-                                             uint32_t glen, uint32_t lit, uint32_t len, uint32_t lane) {
+                                             uint32_t glen, uint32_t lit, uint32_t len, uint32_t lane,
+                                             uint32_t* defer = nullptr) {
   if (len <= 60) {
     uint32_t i = lit + (lane ? lane - 1 : 0);
     i = i < glen ? i : glen - 1;
@@ -540,6 +546,17 @@ __device__ __forceinline__ uint32_t emit_lit(uint8_t* out, uint32_t op, const ui
   }
   // a staged fragment: 16-byte stores composed from LDS (a wave issues them
   // back to back); from memory: the wave copy (loads before stores)
+  if (kLds && defer && len >= kDeferMin && defer[0] < kDeferMax) {
+    const uint32_t hl = literal_tag(out + op, len, PSF_SINK(lane));
+    const uint32_t n = defer[0];
+    if (lane == 0) {
+      defer[1 + 3 * n] = op + hl;
+      defer[2 + 3 * n] = lit;
+      defer[3 + 3 * n] = len;
+      defer[0] = n + 1;
+    }
+    return op + hl + len;
+  }
   if (kLds) return emit_literal(out, op, reinterpret_cast<const uint8_t*>(s), lit, len, lane);
   const uint32_t hl = literal_tag(out + op, len, PSF_SINK(lane));
 #ifndef PSF_DIAG_NOSTORE
@@ -597,7 +614,7 @@ template <bool kLds>
 __device__ __forceinline__ uint2 parse_fragment(uint16_t* __restrict__ table, uint32_t* __restrict__ minlane,
                                                 const uint32_t* skip, uint32_t skA, uint32_t skB, uint32_t skC,
                                                 const uint8_t* __restrict__ g, const uint32_t* s, uint32_t len,
-                                                uint8_t* __restrict__ out, uint32_t lane
+                                                uint8_t* __restrict__ out, uint32_t lane, uint32_t* defer
 #ifdef PSF_DIAG_COUNT
                                                 , uint32_t* cnt
 #endif
@@ -655,7 +672,7 @@ __device__ __forceinline__ uint2 parse_fragment(uint16_t* __restrict__ table, ui
       if ((vm & lim_mask) != lim_mask) goto remainder;
       kbase += (uint32_t)limit + 1;
     }
-    op = emit_lit<kLds>(out, op, g, s, len, next_emit, ip - next_emit, lane);
+    op = emit_lit<kLds>(out, op, g, s, len, next_emit, ip - next_emit, lane, defer);
     // ---- copies
     {
       uint32_t off = 3, wa = 0, wb = 0;  // lane 0 of the first round: byte ip + 3 (known equal)
@@ -807,6 +824,7 @@ __global__ __launch_bounds__(kCThreads) void snappy_parse(const SnappyCJobs J, u
   __shared__ uint32_t skip[kSkipN + 3];
   __shared__ CompressPhaseLds U;
   __shared__ uint32_t s_need[kCThreads / 64];
+  __shared__ uint32_t s_defer[1 + 3 * kDeferMax];
   const uint32_t tid = threadIdx.x;
   const uint32_t wave = tid >> 6, lane = tid & 63;
   constexpr uint32_t W = kCThreads / 64;
@@ -846,6 +864,7 @@ __global__ __launch_bounds__(kCThreads) void snappy_parse(const SnappyCJobs J, u
       for (uint32_t i = lane; i <= kMinSlots; i += 64) U.p.minlane[wave][i] = 0xffffffffu;  // each step cleans up after itself
     if (__builtin_popcount(need) == 1) {
       const uint32_t f = (r0 + __builtin_ctz(need)) * G + blockIdx.x;
+      if (tid == 0) s_defer[0] = 0;
       const CJob& c = cjob_of(J, f);
       const size_t start = (size_t)(f - c.frag0) * kFrag;
       const uint32_t len = (uint32_t)min((size_t)kFrag, c.n - start);
@@ -865,7 +884,7 @@ __global__ __launch_bounds__(kCThreads) void snappy_parse(const SnappyCJobs J, u
       __syncthreads();
       if (wave == 0) {
         const uint2 r = parse_fragment<true>(U.p.table[0], U.p.minlane[0], skip, sk0, sk1, sk2, g, src, len,
-                                             scratch + (size_t)f * kSnappyFragOut, lane
+                                             scratch + (size_t)f * kSnappyFragOut, lane, s_defer
 #ifdef PSF_DIAG_COUNT
                                              , cnt
 #endif
@@ -889,7 +908,7 @@ __global__ __launch_bounds__(kCThreads) void snappy_parse(const SnappyCJobs J, u
         for (uint32_t j = lane; j < (1u << (32 - hash_shift(len))) / 8; j += 64) t16[j] = make_uint4(0, 0, 0, 0);
         asm volatile("" ::: "memory");
         const uint2 r = parse_fragment<false>(table, minlane, skip, sk0, sk1, sk2, frag_src(c, f - c.frag0), nullptr, len,
-                                              scratch + (size_t)f * kSnappyFragOut, lane
+                                              scratch + (size_t)f * kSnappyFragOut, lane, nullptr
 #ifdef PSF_DIAG_COUNT
                                               , cnt
 #endif
@@ -899,6 +918,15 @@ __global__ __launch_bounds__(kCThreads) void snappy_parse(const SnappyCJobs J, u
       }
     }
     __syncthreads();  // (the next round's probe maps overwrite the tables)
+    if (__builtin_popcount(need) == 1 && s_defer[0]) {  // the long literals it handed over
+      const uint32_t f = (r0 + __builtin_ctz(need)) * G + blockIdx.x;
+      const CJob& c = cjob_of(J, f);
+      const uint8_t* g = frag_src(c, f - c.frag0);
+      uint8_t* out = scratch + (size_t)f * kSnappyFragOut;
+      for (uint32_t d = 0; d < s_defer[0]; ++d)
+        copy_bytes<kCThreads>(out + s_defer[1 + 3 * d], g + s_defer[2 + 3 * d], s_defer[3 + 3 * d], tid);
+      __syncthreads();  // (s_defer is reset by the next single parse)
+    }
   }
 #ifdef PSF_DIAG_COUNT
   if (blockIdx.x == 0 && lane == 0 && wave < kParseWaves)
