@@ -5,6 +5,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <sched.h>
+
 #include <algorithm>
 #include <atomic>
 #include <set>
@@ -334,9 +336,35 @@ int psf_snappy_uncompress(psf_context* ctx, const void* d_in, size_t n, void* d_
     if (d > out_cap || (d && !d_out)) return PSF_ERR_ARG;
     psf::Buffer scratch = c.alloc(psf::snappy_uncompress_scratch(n, d));
     const uint32_t ticket = c.next_ticket();
-    int st = psf::snappy_uncompress_launch(d_in, n, hdr, d, d_out, scratch.ptr, c.stream(), c.prof(), c.pub_dev(0),
-                                           ticket);
+    // the fast path (K-spec) first; the scan / link / index / fragment
+    // kernels only if it did not publish the verdict -- a stream of stored
+    // fragments needs none of them (as SnappyBatch::finish does for batches)
+    const psf::SnappyDJob job{d_in, n, hdr, d, d_out, 0, ticket};
+    psf::SnappyTail tail;
+    int st = psf::snappy_uncompress_batch_launch(&job, 1, scratch.ptr, c.stream(), c.prof(), c.pub_dev(0),
+                                                 psf::ZeroPair{}, &tail);
     if (st != PSF_OK) return st;
+    hipEvent_t done = c.take_event();
+    PSF_HIP_CHECK(hipEventRecord(done, c.stream()));
+    bool published = false;
+    for (uint64_t spin = 0;; ++spin) {
+      if ((published = __atomic_load_n(&c.pub_host(0)->ticket, __ATOMIC_ACQUIRE) == ticket)) break;
+      const hipError_t q = hipEventQuery(done);
+      if (q == hipSuccess) {
+        published = __atomic_load_n(&c.pub_host(0)->ticket, __ATOMIC_ACQUIRE) == ticket;
+        break;
+      }
+      if (q != hipErrorNotReady) {
+        c.give_event(done);
+        throw psf::CheckError(PSF_ERR_HIP, std::string("stream failed: ") + hipGetErrorString(q));
+      }
+      if (spin > 4096) sched_yield();
+    }
+    c.give_event(done);
+    if (!published) {
+      st = psf::snappy_uncompress_tail_launch(&tail, c.stream());
+      if (st != PSF_OK) return st;
+    }
     c.wait_ticket(0, ticket);
     return c.pub_host(0)->status;
   });
