@@ -1,5 +1,7 @@
 #include "router.h"
 
+#include <stdlib.h>
+
 #include "slice.h"
 
 namespace psf {
@@ -12,7 +14,9 @@ PushRouter::PushRouter(Context* ctx, const std::vector<KeyRange>& ranges, int ra
     if (ranges[i - 1].end != ranges[i].begin) throw CheckError(kErrArg, "server ranges must be contiguous");
 }
 
-PushRouter::~PushRouter() = default;
+PushRouter::~PushRouter() {
+  if (step_start_) ctx_->give_event(step_start_);
+}
 
 // The key width SliceKOFVMessage<K> slices with (message.h:107-147): the
 // application's K, which the stream's task.key_type records (EncodeType<K>,
@@ -50,6 +54,15 @@ RemoteNode* PushRouter::receiver(int server, int32_t stream) {
 // (message.h:107-147), encode each valid slice on its per-peer node.  The
 // slices copy the stream's Task and share its buffers, as `new
 // Message(msg->task)` plus the zero-copy SArray segments do.
+// PSF_SIDE_SLICE (A/B knob, tools/): 0 keeps the prefetched slicing on the main stream
+static bool side_slice_mode() {
+  static const bool on = [] {
+    const char* e = getenv("PSF_SIDE_SLICE");
+    return !(e && *e == '0');
+  }();
+  return on;
+}
+
 void PushRouter::encode_launch(const Message* const* streams, int n) {
   t_launch_ = now_ns();
   results_.clear();
@@ -58,6 +71,13 @@ void PushRouter::encode_launch(const Message* const* streams, int n) {
   local_server_.clear();
   plan_.reset();
   pend_.finish();  // (a launch without its finish: complete it first)
+  // where the main stream stands before this step's encode: the next step's
+  // slicing (prefetch) waits for this point only -- everything the callers
+  // enqueued before, not this step's encode and decode
+  if (ctx_->device() >= 0 && side_slice_mode()) {  // (a host-only context slices on the host)
+    if (!step_start_) step_start_ = ctx_->take_event();
+    PSF_HIP_CHECK(hipEventRecord(step_start_, ctx_->stream()));
+  }
   std::unique_ptr<SliceJob> job;
   if (next_ && next_->same_inputs(streams, n)) job = std::move(next_);
   next_.reset();
@@ -113,8 +133,14 @@ void PushRouter::encode_finish(int64_t* sizes) {
   stat_encode_ns += now_ns() - t0;
 }
 
+// The next step's slicing on the side stream: it reads only the streams' key
+// buffers (the callers' templates; no kernel of a step writes them) and
+// writes host-mapped records, so it need not queue behind this step's encode
+// and decode -- the host then finds it done when the next step starts instead
+// of waiting for this step's kernels.
 void PushRouter::prefetch(const Message* const* streams, int n) {
-  next_ = slice_begin(ctx_, std::vector<const Message*>(streams, streams + n), ranges_, step_key_bytes(streams, n));
+  next_ = slice_begin(ctx_, std::vector<const Message*>(streams, streams + n), ranges_, step_key_bytes(streams, n),
+                      step_start_);
 }
 
 void PushRouter::fill(void* sendbuf) {

@@ -79,6 +79,7 @@ class PushRouter {
   std::vector<std::pair<int, Message>> results_;
   std::vector<Encoded> enc_;
   std::unique_ptr<SliceJob> next_;
+  hipEvent_t step_start_ = nullptr;  // the main stream at this step's encode launch (prefetch waits on it)
   // the step between encode_launch and encode_finish
   std::vector<Message> slices_;
   std::vector<int> srv_;

@@ -129,7 +129,7 @@ SliceJob::~SliceJob() {
 }
 
 std::unique_ptr<SliceJob> slice_begin(Context* ctx, const std::vector<const Message*>& msgs,
-                                      const std::vector<KeyRange>& krs, int key_bytes) {
+                                      const std::vector<KeyRange>& krs, int key_bytes, hipEvent_t after) {
   if (key_bytes != 8 && key_bytes != 4) throw CheckError(kErrArg, "key type must be 32 or 64 bit");
   const size_t n = krs.size();
   for (size_t i = 1; i < n; ++i)
@@ -172,10 +172,15 @@ std::unique_ptr<SliceJob> slice_begin(Context* ctx, const std::vector<const Mess
   p.nmsg = (int)D;
   p.pos = reinterpret_cast<uint64_t*>(d + desc_b + bnd_b);
   p.sig = reinterpret_cast<uint32_t*>(d + desc_b + bnd_b + pos_b);
-  int s = slice_sig_launch(p, key_bytes, ctx->stream());
+  hipStream_t st = ctx->stream();
+  if (after) {
+    st = ctx->side_stream();
+    PSF_HIP_CHECK(hipStreamWaitEvent(st, after, 0));
+  }
+  int s = slice_sig_launch(p, key_bytes, st);
   if (s != kOk) throw CheckError(s, "slice launch failed");
   job->ev = ctx->take_event();
-  PSF_HIP_CHECK(hipEventRecord(job->ev, ctx->stream()));
+  PSF_HIP_CHECK(hipEventRecord(job->ev, st));
   return job;
 }
 

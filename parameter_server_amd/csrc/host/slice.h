@@ -48,8 +48,11 @@ struct SliceJob {
   bool same_inputs(const Message* const* ms, int n) const;
   ~SliceJob();
 };
+// after: when non-null, the slicing runs on the context's side stream once
+// the main stream has reached `after` (a prefetch that must not queue behind
+// the main stream's later work); else on the main stream
 std::unique_ptr<SliceJob> slice_begin(Context* ctx, const std::vector<const Message*>& msgs,
-                                      const std::vector<KeyRange>& krs, int key_bytes);
+                                      const std::vector<KeyRange>& krs, int key_bytes, hipEvent_t after = nullptr);
 void slice_end(SliceJob& job, std::vector<std::vector<Message>>* outs, std::vector<std::vector<bool>>* valid,
                std::vector<std::vector<KeySigHint>>* hints = nullptr);
 
