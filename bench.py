@@ -341,7 +341,18 @@ def build_workload(args, F, ctx, rank, world, dev, g, n):
         from parameter_server_amd import shard
         if args.servers < world:
             raise SystemExit(f"--servers {args.servers} < {world} ranks")
-        ex = shard.SpillExchange(ctx, device=dev) if world > 1 else None
+        ex = None
+        if world > 1:
+            # libpsf's exchange (one native call per timed region, no device
+            # read-back per step): RCCL over xGMI under the driver's nccl
+            # backend, the host mailbox when ranks share a GPU (rehearsals);
+            # PSF_EXCHANGE=python: torch's all-to-all-v, one Python step each
+            mode = os.environ.get("PSF_EXCHANGE", "native")
+            if mode == "python":
+                ex = shard.SpillExchange(ctx, device=dev)
+            else:
+                same = os.environ.get("PSF_SAME_GPU") == "1" or not str(dev).startswith("cuda")
+                ex = shard.NativeExchange.create(ctx, transport="host" if same else "rccl")
         router = shard.PushRouter(ctx, shard.server_ranges(args.servers), rank, world, ex)
         streams, nloc, payload, elided = {}, 0, 0, 0
         if args.config == "c4":
@@ -442,10 +453,14 @@ def main():
     if not args.launch_check:
         torch.cuda.set_device(local)
     if world > 1:
+        # bounded collectives: a rank that fails mid-run is an error on the
+        # others, not a hang
+        import datetime
+        tmo = datetime.timedelta(seconds=300)
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"), timeout=tmo)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=tmo)
         if dist.get_world_size() != args.gpus:
             raise SystemExit(f"bench.py: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
     world_pg = dist.get_world_size() if world > 1 else 1
@@ -605,12 +620,21 @@ def main():
                        "spill_bytes_per_step_rank0": spill4 // max(args.steps, 1)})
             del run4, r4, extra4
         except Exception as e:  # noqa: BLE001 -- the companion must not take the C2 line down with it
-            # (a failure of the spill path is symmetric across ranks: each
-            # rank records it, and the process group is left alone after it)
             c4_failed = True
             c4 = c4_config(args, world_pg, backend_pg)
             c4.update({"measured": False, "error": f"{type(e).__name__}: {e}"[:400]})
             print(f"bench.py: rank {rank}: config_c4 failed: {e!r}", file=sys.stderr, flush=True)
+        if world > 1:
+            # every rank learns whether any rank's companion failed (the
+            # exchange's waits are bounded, so a failed rank's peers fail too
+            # instead of hanging in it); the line then reports no C4 number
+            flag = torch.tensor([1.0 if c4_failed else 0.0], device=dev if backend == "nccl" else "cpu",
+                                dtype=torch.float64)
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+            if flag.item() > 0 and not c4_failed:
+                c4_failed = True
+                c4 = c4_config(args, world_pg, backend_pg)
+                c4.update({"measured": False, "error": "config_c4 failed on another rank"})
 
     # C1 with the wire step in the timed region: every encoded Task serialised
     # (its computed min/max settled to the host) and parsed by the receiver,
@@ -685,7 +709,7 @@ def main():
             line["config_wire"] = wire_line
         print(json.dumps(line), flush=True)
 
-    if world > 1 and not c4_failed:
+    if world > 1:
         dist.destroy_process_group()
 
 

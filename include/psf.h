@@ -422,7 +422,8 @@ int psf_spill_unpack(psf_context* ctx, const void* recvbuf, int world, const int
  * all-to-all-v, psf_router_decode_local / psf_router_decode_received (the
  * receive buffer is copied into library-owned memory: KEY_CACHING keeps
  * received keys by reference).  psf_router_step runs `iters` whole steps of a
- * world-1 router (no exchange).  Results of the last step: the decoded
+ * world-1 router, or of any router with a native exchange
+ * (psf_router_set_exchange, below).  Results of the last step: the decoded
  * messages with their server (psf_router_result), and with
  * psf_router_keep_encoded(1) the encoded slices (psf_router_encoded); both
  * return new message handles. */
@@ -440,6 +441,39 @@ int psf_router_num_results(psf_router* r);
 int psf_router_result(psf_router* r, int i, int* server, psf_message** out);
 int psf_router_num_encoded(psf_router* r);
 int psf_router_encoded(psf_router* r, int i, int32_t* stream, int* server, psf_message** out);
+
+/* ---- the native exchange of the ranks of one node ------------------------
+ * Replaces the reference's per-server send loop (executor.cc:131-146 ->
+ * Van::Send / Recv, van.cc:122-269) between the servers of one node: each
+ * slice's Task frame (serialised on the host, as Van::Send does) travels
+ * through a host shared-memory mailbox of the node's ranks, its data frames
+ * device to device -- PSF_EXCHANGE_RCCL: RCCL point-to-point over xGMI, one
+ * grouped send/recv per peer per step on the exchange's stream (librccl is
+ * loaded on first use); PSF_EXCHANGE_HOST: through the mailbox (several ranks
+ * on one GPU, or host-only contexts).  FIXING_FLOAT ranges computed on the
+ * device travel on the device too, so a step needs no device->host wait
+ * except COMPRESSING's output lengths.
+ *
+ * psf_exchange_unique_id: rank 0's RCCL id (bytes >= 128), handed to every
+ * rank by the caller.  psf_exchange_create: every rank of the node, same
+ * `name` (a file name; the mailbox lives in PSF_EXCHANGE_DIR, /dev/shm or
+ * TMPDIR), same caps (meta_cap: Task-record bytes a rank posts per step, 0 =
+ * 1 MiB; host_cap: data bytes per step for PSF_EXCHANGE_HOST, 0 = 64 MiB);
+ * returns when every rank has attached.  Waits are bounded by
+ * PSF_EXCHANGE_TIMEOUT_S (default 120 s).  psf_router_set_exchange: the
+ * router's psf_router_step then runs at any world size (and with loopback),
+ * one call for `iters` whole steps.  psf_exchange_stats: out[3] = {bytes
+ * posted for other ranks (records + data), steps, host ns waiting on the
+ * mailbox}. */
+#define PSF_EXCHANGE_RCCL 0
+#define PSF_EXCHANGE_HOST 1
+typedef struct psf_exchange psf_exchange;
+int psf_exchange_unique_id(void* out, size_t bytes);
+int psf_exchange_create(psf_context* ctx, int rank, int world, const char* name, int transport, const void* nccl_id,
+                        uint64_t meta_cap, uint64_t host_cap, psf_exchange** out);
+int psf_exchange_destroy(psf_exchange* ex);
+int psf_exchange_stats(psf_exchange* ex, int64_t* out);
+int psf_router_set_exchange(psf_router* r, psf_exchange* ex);
 
 /* ---- host-side accounting ----------------------------------------------
  * Host time blocked on the device, by cause: PSF_WAIT_SYNC stream

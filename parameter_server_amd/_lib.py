@@ -22,6 +22,7 @@ PSF_ERR_CHECK = -5
 PSF_ERR_UNSUPPORTED = -6
 PSF_ERR_TIMEOUT = -7  # reserved: no entry point returns it
 PSF_STREAM_GIVEN, PSF_STREAM_OWN, PSF_STREAM_SHARED = 0, 1, 2
+PSF_EXCHANGE_RCCL, PSF_EXCHANGE_HOST = 0, 1
 
 DT_UINT64, DT_FLOAT, DT_DOUBLE, DT_CHAR = 8, 9, 10, 11
 KEY_CACHING, COMPRESSING, FIXING_FLOAT, NOISE = 1, 2, 3, 4
@@ -154,6 +155,11 @@ SIGNATURES = {
     "psf_router_result": ([vp, C.c_int, PI, C.POINTER(vp)], C.c_int),
     "psf_router_num_encoded": ([vp], C.c_int),
     "psf_router_encoded": ([vp, C.c_int, C.POINTER(i32), PI, C.POINTER(vp)], C.c_int),
+    "psf_exchange_unique_id": ([vp, sz], C.c_int),
+    "psf_exchange_create": ([vp, C.c_int, C.c_int, C.c_char_p, C.c_int, vp, u64, u64, C.POINTER(vp)], C.c_int),
+    "psf_exchange_destroy": ([vp], C.c_int),
+    "psf_exchange_stats": ([vp, C.POINTER(C.c_int64)], C.c_int),
+    "psf_router_set_exchange": ([vp, vp], C.c_int),
     "psf_profile_enable": ([vp, C.c_int], C.c_int),
     "psf_profile_stride": ([vp, C.c_int], C.c_int),
     "psf_profile_reset": ([vp], C.c_int),

@@ -1004,11 +1004,15 @@ constexpr uint64_t kHandoffTicks = 20000000ull;
 #else
 constexpr uint64_t kHandoffTicks = 200000000ull;  // 2 s of the 100 MHz wall clock
 #endif
+// the bound in force (psf_debug_set_handoff_ticks lowers it, so a test can
+// drive the late path)
+__device__ uint64_t g_handoff_ticks = kHandoffTicks;
 constexpr uint32_t kFusedLine = 32;               // u32 per array's counter line
 __device__ __forceinline__ bool wait_ready(const uint32_t* c, uint32_t want) {
   const uint64_t t0 = wall_clock64();
+  const uint64_t lim = g_handoff_ticks;
   while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
-    if (wall_clock64() - t0 > kHandoffTicks) return false;
+    if (wall_clock64() - t0 > lim) return false;
     __builtin_amdgcn_s_sleep(8);
   }
   return true;
@@ -1993,3 +1997,10 @@ int ff_decode_batch_launch(int value_type, int nb, const FfDecArray* arrs, int c
 }
 
 }  // namespace psf
+
+// diagnostic: the in-launch hand-off's bound in 100 MHz ticks on the current
+// device (0 = the default); a tiny bound drives ff_fused_batch's late path
+extern "C" int psf_debug_set_handoff_ticks(uint64_t ticks) {
+  const uint64_t v = ticks ? ticks : psf::kHandoffTicks;
+  return hipMemcpyToSymbol(HIP_SYMBOL(psf::g_handoff_ticks), &v, sizeof(v)) == hipSuccess ? 0 : -1;
+}

@@ -12,6 +12,7 @@
 #include <set>
 #include <string>
 
+#include "exchange.h"
 #include "filter.h"
 #include "kvstore.h"
 #include "router.h"
@@ -765,17 +766,17 @@ int psf_nodes_roundtrip_opts(psf_node* const* snd, psf_node* const* rcv, const p
     struct DeferScope {
       std::set<psf::Context*>& cs;
       explicit DeferScope(std::set<psf::Context*>& c) : cs(c) {
-        for (psf::Context* x : cs) x->defer_decodes = x->device() >= 0;
+        for (psf::Context* x : cs) x->set_defer_decodes(true);
       }
       void finish() {
         for (psf::Context* x : cs) {
-          x->defer_decodes = false;
+          x->set_defer_decodes(false);
           x->flush_deferred();
         }
       }
       ~DeferScope() {
         for (psf::Context* x : cs) {
-          x->defer_decodes = false;
+          x->set_defer_decodes(false);
           try {
             x->flush_deferred();
           } catch (...) {
@@ -965,6 +966,16 @@ int psf_router_step(psf_router* r, psf_message* const* streams, int n, int iters
       if (!streams[i]) return PSF_ERR_ARG;
       ms[i] = &streams[i]->m;
     }
+    if (pr->exchange()) {  // any world: the native exchange
+      for (int it = 0; it < iters; ++it) {
+        pr->encode_launch(ms.data(), n);
+        if (it + 1 < iters) pr->prefetch(ms.data(), n);
+        pr->exchange_step();
+      }
+      return PSF_OK;
+    }
+    if (pr->world() > 1 || pr->loopback())
+      throw psf::CheckError(PSF_ERR_ARG, "psf_router_step: a router with other ranks needs an exchange");
     std::vector<int64_t> sizes(2 * (size_t)pr->world());
     for (int it = 0; it < iters; ++it) {
       pr->encode_launch(ms.data(), n);
@@ -977,6 +988,44 @@ int psf_router_step(psf_router* r, psf_message* const* streams, int n, int iters
       pr->fill(nullptr);
       pr->decode_local();
     }
+    return PSF_OK;
+  });
+}
+int psf_exchange_unique_id(void* out, size_t bytes) {
+  return guarded([&] {
+    if (!out || bytes < 128) return PSF_ERR_ARG;
+    psf::rccl_unique_id(out);
+    return PSF_OK;
+  });
+}
+int psf_exchange_create(psf_context* ctx, int rank, int world, const char* name, int transport, const void* nccl_id,
+                        uint64_t meta_cap, uint64_t host_cap, psf_exchange** out) {
+  return guarded(ctx ? ctx->impl : nullptr, [&] {
+    if (!ctx || !name || !out || (transport != PSF_EXCHANGE_RCCL && transport != PSF_EXCHANGE_HOST)) return PSF_ERR_ARG;
+    *out = reinterpret_cast<psf_exchange*>(new psf::Exchange(
+        ctx->impl, rank, world, name, transport == PSF_EXCHANGE_RCCL ? psf::Exchange::kRccl : psf::Exchange::kHost,
+        nccl_id, meta_cap, host_cap));
+    return PSF_OK;
+  });
+}
+int psf_exchange_destroy(psf_exchange* ex) {
+  delete reinterpret_cast<psf::Exchange*>(ex);
+  return PSF_OK;
+}
+int psf_exchange_stats(psf_exchange* ex, int64_t* out) {
+  if (!ex || !out) return PSF_ERR_ARG;
+  const psf::Exchange* e = reinterpret_cast<psf::Exchange*>(ex);
+  out[0] = e->bytes_sent;
+  out[1] = e->steps;
+  out[2] = e->wait_ns;
+  return PSF_OK;
+}
+int psf_router_set_exchange(psf_router* r, psf_exchange* ex) {
+  return guarded(r ? reinterpret_cast<psf::PushRouter*>(r)->context() : nullptr, [&] {
+    psf::PushRouter* pr = R(r);
+    psf::Exchange* e = reinterpret_cast<psf::Exchange*>(ex);
+    if (e && (e->context() != pr->context() || e->world() != pr->world())) return PSF_ERR_ARG;
+    pr->set_exchange(e);
     return PSF_OK;
   });
 }

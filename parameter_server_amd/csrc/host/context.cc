@@ -360,6 +360,7 @@ Context::~Context() {
     (void)hipStreamSynchronize(side_);
     (void)hipStreamDestroy(side_);
   }
+  if (side_order_) (void)hipEventDestroy(side_order_);
   for (auto& u : ring_uses_) {  // messages may outlive the context: leave their ranges on the host
     auto rb = u.rb.lock();
     if (rb && !rb->done) {
@@ -497,6 +498,21 @@ hipStream_t Context::side_stream() {
   return side_;
 }
 
+hipStream_t Context::side_stream_after_main() {
+  hipStream_t s = side_stream();
+  if (!side_order_) {
+    DeviceScope ds(device_);
+    PSF_HIP_CHECK(hipEventCreateWithFlags(&side_order_, hipEventDisableTiming));
+  }
+  PSF_HIP_CHECK(hipEventRecord(side_order_, stream_));
+  PSF_HIP_CHECK(hipStreamWaitEvent(s, side_order_, 0));
+  return s;
+}
+
+void Context::reset_fused() {
+  if (fused_.ctl) PSF_HIP_CHECK(hipMemsetAsync(fused_.ctl, 0, kFusedCtlBytes, stream_));
+}
+
 uint32_t Context::wait_crc(int i, uint32_t ticket) {
   if (device_ < 0) throw CheckError(kErrArg, "host-only context has no device workspace");
   const Slot* s = h_slots_ + i;
@@ -532,7 +548,12 @@ void Context::sync() {
 void RangeBatch::resolve(bool synced) {
   if (done) return;
   if (!synced) ctx->sync();  // the kernels' host-mapped stores are visible after it
-  memcpy(host.data(), ring, host.size() * 4);
+  if (ring) {
+    memcpy(host.data(), ring, host.size() * 4);
+  } else {  // records in HBM (received with a spilled slice, spill.cc)
+    DeviceScope ds(ctx->device());
+    PSF_HIP_CHECK(hipMemcpy(host.data(), dev.ptr, host.size() * 4, hipMemcpyDeviceToHost));
+  }
   done = true;
 }
 
@@ -576,7 +597,10 @@ void Context::check_ranges() {
       late |= (int32_t)rb->host[i] == kErrHip;
     }
   }
-  if (late) throw CheckError(kErrHip, "FIXING_FLOAT: in-launch min/max hand-off timed out");
+  if (late) {
+    reset_fused();
+    throw CheckError(kErrHip, "FIXING_FLOAT: in-launch min/max hand-off timed out");
+  }
   if (bad) throw CheckError(kErrBin, "CHECK_GT(bin, 0)");
 }
 
@@ -584,8 +608,7 @@ void Context::flush_deferred() {
   if (deferred.arrs.empty()) return;
   const int st = ff_decode_batch_launch(deferred.value_type, deferred.nb, deferred.arrs.data(),
                                         (int)deferred.arrs.size(), stream_, &prof_);
-  deferred.arrs.clear();
-  deferred.keep.clear();
+  deferred.clear();
   if (st != kOk) throw CheckError(st, "ff_decode batch launch failed");
 }
 

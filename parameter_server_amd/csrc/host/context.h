@@ -11,6 +11,7 @@
 #include <vector>
 #include <mutex>
 #include <string>
+#include <thread>
 
 #include "../psf_internal.h"
 #include "message.h"
@@ -61,7 +62,7 @@ class Context;
 struct RangeBatch {
   Context* ctx = nullptr;
   Buffer dev;                      // read by decodes on ctx's stream
-  const uint32_t* ring = nullptr;  // the same records in ctx's host-mapped ring
+  const uint32_t* ring = nullptr;  // the same records in ctx's host-mapped ring (null: read dev)
   std::vector<uint32_t> host;      // 4 words per array, valid once done
   bool done = false;
   void resolve(bool synced = false);
@@ -94,6 +95,14 @@ class Context {
   // on (the round-trip drivers' KEY_CACHING presign CRCs of the next
   // iteration's keys, read back through publish slots), created on first use
   hipStream_t side_stream();
+  // side_stream(), ordered after everything queued on stream() so far (one
+  // event record + wait): for side work that reads what earlier main-stream
+  // work may have written (presign CRCs of keys a decode produced)
+  hipStream_t side_stream_after_main();
+  // ff_fused_batch's counter lines zeroed on the stream: after an in-launch
+  // hand-off gave up, the aborted launch left them dirty (only the last
+  // workgroup of an array re-zeroes its line)
+  void reset_fused();
 
   // HBM buffer freed (stream-ordered) when its last reference drops.
   Buffer alloc(size_t bytes);
@@ -173,12 +182,26 @@ class Context {
   // launches it together with its min/max pass, or flush_deferred() on its
   // own.  `keep` holds the batch's buffers until it is launched (the caching
   // allocator's stream order covers only launched work).
+  // `ranges` keeps the RangeBatches the arrays' device {min, max} point into.
+  // Deferral is the driver's own: only decodes on the thread that turned it
+  // on are held back (defers_here), so another caller of the context never
+  // gets a buffer whose decode has not been launched.
   struct DeferredDecode {
     int value_type = 0, nb = 0;
     std::vector<FfDecArray> arrs;
     std::vector<Buffer> keep;
+    std::vector<std::shared_ptr<RangeBatch>> ranges;
+    void clear() {
+      arrs.clear();
+      keep.clear();
+      ranges.clear();
+    }
   };
-  bool defer_decodes = false;
+  void set_defer_decodes(bool on) {
+    defer_decodes_ = on && device_ >= 0;
+    defer_owner_ = std::this_thread::get_id();
+  }
+  bool defers_here() const { return defer_decodes_ && defer_owner_ == std::this_thread::get_id(); }
   DeferredDecode deferred;
   void flush_deferred();
 
@@ -215,6 +238,9 @@ class Context {
   bool shared_stream_ = false;
   hipStream_t stream_;
   hipStream_t side_ = nullptr;
+  hipEvent_t side_order_ = nullptr;  // side_stream_after_main's event
+  bool defer_decodes_ = false;
+  std::thread::id defer_owner_;
   std::shared_ptr<StreamHolder> holder_;
   void* d_partials_ = nullptr;
   Slot* d_slots_ = nullptr;

@@ -49,11 +49,7 @@ class KeyCachingFilter : public Filter {
   void encode_with(Message* msg, uint32_t sig);
   void decode_with(Message* msg, uint32_t sig);
   static bool needs_signature(Message* msg, bool encode);
-  size_t cache_size() const {  // live entries (a cleared entry is kept, reset)
-    size_t n = 0;
-    for (const auto& kv : cache_) n += kv.second.key.empty() ? 0 : 1;
-    return n;
-  }
+  size_t cache_size() const { return live_; }  // live entries (a cleared entry may be kept, reset)
 
  private:
   struct CacheKey {
@@ -75,6 +71,13 @@ class KeyCachingFilter : public Filter {
   };
   static bool is_done(const Task& t) { return !t.request || (t.has_param && t.push); }  // :63-67
   uint32_t signature(const Buffer& key);
+  // after entry `e` went from live `was` to its current state: count it, and
+  // once reset entries outnumber live ones (and kMaxIdle), erase them all --
+  // the reference erases at once (key_caching.h:31,57); keeping a reset node
+  // saves an allocation per round trip, this bounds what is kept
+  void account(bool was, const Entry& e);
+  static constexpr size_t kMaxIdle = 4096;
+  size_t live_ = 0;
 
   std::unordered_map<CacheKey, Entry, CacheKeyHash> cache_;
   static constexpr size_t kMaxSigLen = 2048;  // key_caching.h:74

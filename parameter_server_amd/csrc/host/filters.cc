@@ -68,6 +68,7 @@ void KeyCachingFilter::encode_with(Message* msg, uint32_t sig) {
   CacheKey ck{msg->task.key_channel, msg->task.key_range};
   std::lock_guard<std::mutex> l(mu_);
   Entry& e = cache_[ck];
+  const bool was = !e.key.empty();
   const bool hit = e.sig == sig && e.key.bytes == msg->key.bytes;
   if (hit) {
     msg->clear_key();
@@ -77,8 +78,20 @@ void KeyCachingFilter::encode_with(Message* msg, uint32_t sig) {
   }
   // cache_.erase(ck): the entry is reset instead (an absent entry and a reset
   // one read the same, sig 0 with no key, and the node is not freed and
-  // reallocated every round trip)
+  // reallocated every round trip); account() erases reset entries in bulk
   if (conf->clear_cache_if_done && is_done(msg->task)) e = Entry{};
+  account(was, e);
+}
+
+void KeyCachingFilter::account(bool was, const Entry& e) {
+  const bool now = !e.key.empty();
+  live_ = live_ + (now ? 1 : 0) - (was ? 1 : 0);
+  const size_t idle = cache_.size() - live_;
+  if (idle <= kMaxIdle || idle <= live_) return;
+  for (auto it = cache_.begin(); it != cache_.end();) {
+    if (it->second.key.empty()) it = cache_.erase(it);
+    else ++it;
+  }
 }
 
 void KeyCachingFilter::decode(Message* msg) {  // key_caching.h:36-60
@@ -97,15 +110,20 @@ void KeyCachingFilter::decode_with(Message* msg, uint32_t got) {
   CacheKey ck{msg->task.key_channel, msg->task.key_range};
   std::lock_guard<std::mutex> l(mu_);
   Entry& e = cache_[ck];
+  const bool was = !e.key.empty();
   if (msg->has_key()) {
     e.sig = sig;
     e.key = msg->key;
   } else {
     // "the cache is invalid... may ask the sender to resend this task"
-    if (sig != e.sig) throw CheckError(kErrCheck, "KEY_CACHING: cache miss on decode");
+    if (sig != e.sig) {
+      account(was, e);  // (a new, empty entry)
+      throw CheckError(kErrCheck, "KEY_CACHING: cache miss on decode");
+    }
     msg->set_key(e.key);
   }
   if (conf->clear_cache_if_done && is_done(msg->task)) e = Entry{};  // (as in encode_with)
+  account(was, e);
 }
 
 // -------------------------------------------------------- FIXING_FLOAT ----
@@ -342,10 +360,7 @@ void FixingFloatFilter::encode_messages(Context* ctx, std::vector<FfMessage>& ms
       int s = ff_encode_batch_launch(jobs[part[0]].type, jobs[part[0]].nb, arrs.data(), (int)arrs.size(),
                                      scratch.ptr, ctx->pub_dev(0), st, ctx->prof(), take ? d.arrs.data() : nullptr,
                                      take ? (int)d.arrs.size() : 0, take ? d.nb : 0, ctx->fused());
-      if (take) {
-        d.arrs.clear();
-        d.keep.clear();
-      }
+      if (take) d.clear();
       if (s != kOk) throw CheckError(s, "ff_encode batch launch failed");
     };
     for_each_batch(jobs, base, end, true, one, batch);
@@ -357,7 +372,10 @@ void FixingFloatFilter::encode_messages(Context* ctx, std::vector<FfMessage>& ms
         const Slot& hs = *ctx->pub_host((int)(q - base));
         if (!j.fp->has_min) j.fp->set_min(hs.range[0]);
         if (!j.fp->has_max) j.fp->set_max(hs.range[1]);
-        if (hs.status == kErrHip) throw CheckError(kErrHip, "FIXING_FLOAT: in-launch min/max hand-off timed out");
+        if (hs.status == kErrHip) {
+          ctx->reset_fused();
+          throw CheckError(kErrHip, "FIXING_FLOAT: in-launch min/max hand-off timed out");
+        }
         if (hs.status != kOk) throw CheckError(kErrBin, "CHECK_GT(bin, 0)");
       } else if (lazy_idx[q - base] >= 0) {
         j.fp->pending = rb;
@@ -384,7 +402,10 @@ void FixedFloatConfig::settle() {
   if (pending_max) set_max(mx);
   pending_idx = -1;
   pending_min = pending_max = false;
-  if ((int32_t)r[2] == kErrHip) throw CheckError(kErrHip, "FIXING_FLOAT: in-launch min/max hand-off timed out");
+  if ((int32_t)r[2] == kErrHip) {
+    if (rb->ctx) rb->ctx->reset_fused();
+    throw CheckError(kErrHip, "FIXING_FLOAT: in-launch min/max hand-off timed out");
+  }
   if ((int32_t)r[2] != kOk) throw CheckError(kErrBin, "CHECK_GT(bin, 0)");
 }
 
@@ -462,7 +483,7 @@ void FixingFloatFilter::decode_messages(Context* ctx, std::vector<FfMessage>& ms
     PSF_HPROF(10);
     const int type = jobs[part[0]].type, nb = jobs[part[0]].nb;
     Context::DeferredDecode& d = ctx->deferred;
-    if (ctx->defer_decodes && (d.arrs.empty() || (d.value_type == type && d.nb == nb)) &&
+    if (ctx->defers_here() && (d.arrs.empty() || (d.value_type == type && d.nb == nb)) &&
         d.arrs.size() + arrs.size() <= 64) {
       // held back: the next batched encode's min/max launch takes it along
       d.value_type = type;
@@ -471,6 +492,8 @@ void FixingFloatFilter::decode_messages(Context* ctx, std::vector<FfMessage>& ms
       for (size_t q : part) {
         d.keep.push_back(jobs[q].in);
         d.keep.push_back(jobs[q].out);
+        // the device {min, max} j.range points into this batch's records
+        if (jobs[q].range && jobs[q].fp->pending) d.ranges.push_back(jobs[q].fp->pending);
       }
       return;
     }
@@ -799,6 +822,9 @@ PresignJob presign_launch(RemoteNode* const* nodes, const Message* const* msgs, 
     len.clear();
     tk.clear();
     slot.clear();
+    // after what the main stream has queued so far (a decode or copy there
+    // may be producing these keys), not after the work queued from now on
+    hipStream_t side = ctx->side_stream_after_main();
     int s = Context::kPresignSlot0;
     for (PresignJob::Buf& b : J.bufs) {
       if (b.ctx != ctx) continue;
@@ -814,12 +840,12 @@ PresignJob presign_launch(RemoteNode* const* nodes, const Message* const* msgs, 
     }
     for (size_t c = 0; c < d.size(); c += (size_t)kCrcBatchMax) {
       const int cnt = (int)std::min(d.size() - c, (size_t)kCrcBatchMax);
-      // on the context's side stream: the keys are the callers' templates, which
-      // no kernel of the main stream writes, and the CRCs are read back
-      // through the publish slots -- so they run beside the current
-      // iteration instead of queueing behind its last encode
+      // on the context's side stream: the CRCs are read back through the
+      // publish slots, so they run beside the current iteration instead of
+      // queueing behind its encodes (ordered only after the main stream's
+      // position at this launch)
       int st = crc32c_batch_launch(d.data() + c, len.data() + c, slot.data() + c, tk.data() + c, cnt,
-                                   ctx->pub_dev(Context::kPresignSlot0), ctx->side_stream(), ctx->prof());
+                                   ctx->pub_dev(Context::kPresignSlot0), side, ctx->prof());
       if (st != kOk) throw CheckError(st, "crc32c batch launch failed");
     }
   }

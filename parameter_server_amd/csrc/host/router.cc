@@ -149,6 +149,92 @@ void PushRouter::fill(void* sendbuf) {
   plan_.reset();
 }
 
+void PushRouter::exchange_step() {
+  if (!ex_) throw CheckError(kErrArg, "router: no exchange");
+  if (ex_->world() != world_ || ex_->rank() != rank_) throw CheckError(kErrArg, "router: exchange of another world");
+  int64_t t0 = now_ns();
+  pend_.finish();  // COMPRESSING's lengths (the only device wait of the step)
+  std::vector<Message*> remote;
+  std::vector<int> dest, rsrv;
+  for (size_t k = 0; k < slices_.size(); ++k) {
+    if (keep_enc_) enc_.push_back(Encoded{slices_[k].task.key_channel, srv_[k], slices_[k]});
+    const int r = owner(srv_[k]);
+    if (r == rank_ && !loopback_) {
+      local_.push_back(std::move(slices_[k]));
+      local_server_.push_back(srv_[k]);
+    } else {
+      remote.push_back(&slices_[k]);
+      dest.push_back(r);
+      rsrv.push_back(srv_[k]);
+    }
+  }
+  const int W = world_;
+  SpillPlan plan(ctx_, remote.data(), dest.data(), rsrv.data(), (int)remote.size(), W, /*host_meta=*/true);
+  std::vector<int64_t> meta(W), pay(W);
+  std::vector<const uint8_t*> recs(W);
+  std::vector<uint64_t> soff(W), roff(W);
+  for (int r = 0; r < W; ++r) {
+    meta[r] = plan.sizes()[2 * r];
+    pay[r] = plan.sizes()[2 * r + 1];
+    recs[r] = plan.records(r);
+    soff[r] = plan.send_offset(r);
+  }
+  Buffer send;
+  if (plan.total()) {
+    if (ctx_->device() >= 0) {
+      send = ctx_->alloc(plan.total());
+    } else {
+      send.loc = Loc::kHost;
+      send.bytes = plan.total();
+      uint8_t* q = new uint8_t[plan.total()];
+      send.owner = std::shared_ptr<void>(q, [](void* v) { delete[] static_cast<uint8_t*>(v); });
+      send.ptr = q;
+    }
+    plan.fill(send.ptr);
+  }
+  ++stat_steps;
+  stat_encode_ns += now_ns() - t0;
+  t0 = now_ns();
+  ex_->post(meta.data(), pay.data(), recs.data(), send.ptr, soff.data());
+  ex_->gather_meta();
+  uint64_t total = 0;
+  for (int s = 0; s < W; ++s) {
+    roff[s] = total;
+    total += (uint64_t)ex_->pay_in()[s];
+  }
+  Buffer recv;
+  if (total) {
+    if (ctx_->device() >= 0) {
+      recv = ctx_->alloc(total);
+    } else {
+      recv.loc = Loc::kHost;
+      recv.bytes = total;
+      uint8_t* q = new uint8_t[total];
+      recv.owner = std::shared_ptr<void>(q, [](void* v) { delete[] static_cast<uint8_t*>(v); });
+      recv.ptr = q;
+    }
+  }
+  std::vector<Message> ms;
+  std::vector<int> sv;
+  for (int s = 0; s < W; ++s)
+    if (ex_->meta_in()[s])
+      spill_unpack_host(ctx_, ex_->records_in(s), (uint64_t)ex_->meta_in()[s], recv, roff[s],
+                        (uint64_t)ex_->pay_in()[s], &ms, &sv);
+  const int S = (int)ranges_.size();
+  for (int s : sv)
+    if (s < 0 || s >= S || owner(s) != rank_) throw CheckError(kErrCheck, "spill record for a server this rank does not own");
+  ex_->move(send.ptr, soff.data(), recv.ptr, roff.data());
+  decode_into_results(local_, local_server_);  // beside the transfer
+  local_.clear();
+  local_server_.clear();
+  ex_->join_data();
+  // (released only now: the allocator orders reuse on the context's stream,
+  // which has just been made to wait for the transfer that reads it)
+  send.clear();
+  decode_into_results(ms, sv);
+  stat_decode_ns += now_ns() - t0;
+}
+
 // PickActiveMsg on each server (executor.cc:178-219): decode on the server's
 // node for that stream, all of them in one batch.
 void PushRouter::decode_into_results(std::vector<Message>& ms, const std::vector<int>& servers) {

@@ -11,6 +11,7 @@
 #include <utility>
 #include <vector>
 
+#include "exchange.h"
 #include "filter.h"
 #include "slice.h"
 #include "spill.h"
@@ -48,6 +49,18 @@ class PushRouter {
   void fill(void* sendbuf);
   // decode the slices whose server is on this rank
   void decode_local();
+  // The native exchange (exchange.h) the multi-step driver moves slices for
+  // other ranks through; then one whole step after encode_launch() is
+  // exchange_step(): the delivery split, the Task records posted to the
+  // node's mailbox and the data gathered into one send buffer (the computed
+  // FIXING_FLOAT ranges travel on the device), this rank's records read,
+  // the data moved (RCCL, on the exchange's stream) while the local slices
+  // decode, then the received slices decoded where they landed.  No host
+  // wait on the device except COMPRESSING's lengths.
+  void set_exchange(Exchange* ex) { ex_ = ex; }
+  Exchange* exchange() const { return ex_; }
+  bool loopback() const { return loopback_; }
+  void exchange_step();
   // unpack a receive buffer (segments of ranks 0..world-1) and decode it
   void decode_received(const uint8_t* recvbuf, const int64_t* sizes_in);
 
@@ -68,6 +81,7 @@ class PushRouter {
   void decode_into_results(std::vector<Message>& ms, const std::vector<int>& servers);
 
   Context* ctx_;
+  Exchange* ex_ = nullptr;
   std::vector<KeyRange> ranges_;
   int rank_, world_;
   bool loopback_;

@@ -176,6 +176,70 @@ class SpillExchange:
         return res, [servers[i] for i in range(got.value)]
 
 
+class NativeExchange:
+    """libpsf's own exchange of the node's ranks (psf_exchange_*, exchange.h):
+    per step the Task records of the slices for other ranks go through a host
+    shared-memory mailbox and their data frames device to device -- RCCL
+    point-to-point over xGMI (``transport="rccl"``, one communicator made
+    here, once) or the mailbox itself (``"host"``: several ranks on one GPU,
+    or host-only contexts).  A PushRouter with one runs whole steps in one
+    native call at any world size (psf_router_step): no Python per step, no
+    device->host read of sizes or records.  `group` is only used here, to
+    hand rank 0's mailbox name and RCCL id to the other ranks."""
+
+    def __init__(self, ctx, h, rank: int, world: int, transport: str):
+        self.ctx, self.h, self.rank, self.world, self.transport = ctx, h, rank, world, transport
+        self._base = 0
+
+    @classmethod
+    def create(cls, ctx, group=None, transport: str = "rccl", meta_cap: int = 0, host_cap: int = 0):
+        import os
+        import secrets
+
+        import torch.distributed as dist
+
+        from ._lib import PSF_EXCHANGE_HOST, PSF_EXCHANGE_RCCL
+        world, rank = dist.get_world_size(group), dist.get_rank(group)
+        t = {"rccl": PSF_EXCHANGE_RCCL, "host": PSF_EXCHANGE_HOST}[transport]
+        obj = [None]
+        if rank == 0:
+            uid = b""
+            if t == PSF_EXCHANGE_RCCL:
+                buf = (C.c_uint8 * 128)()
+                check(lib().psf_exchange_unique_id(buf, 128))
+                uid = bytes(buf)
+            obj = [(f"psf_ex_{os.getpid()}_{secrets.token_hex(6)}", uid)]
+        src = 0 if group is None else dist.get_global_rank(group, 0)
+        dist.broadcast_object_list(obj, src=src, group=group)
+        name, uid = obj[0]
+        idbuf = (C.c_uint8 * 128).from_buffer_copy(uid) if uid else None
+        h = C.c_void_p()
+        check(lib().psf_exchange_create(ctx.h, rank, world, name.encode(), t, idbuf, meta_cap, host_cap, C.byref(h)))
+        return cls(ctx, h, rank, world, transport)
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().psf_exchange_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+    def stats(self) -> dict:
+        out = (C.c_int64 * 3)()
+        check(lib().psf_exchange_stats(self.h, out))
+        return {"bytes_sent": out[0], "steps": out[1], "wait_s": out[2] / 1e9}
+
+    @property
+    def bytes_sent(self) -> int:
+        """records + data posted for other ranks since the last reset (set to 0)"""
+        return self.stats()["bytes_sent"] - self._base
+
+    @bytes_sent.setter
+    def bytes_sent(self, v: int) -> None:
+        self._base = self.stats()["bytes_sent"] - v
+
+
 class PushRouter:
     """The multi-server push path of one rank (libpsf
     psf_router_*): every local stream's message is sliced at the `ranges` of S
@@ -200,6 +264,9 @@ class PushRouter:
                                       C.byref(h)))
         self.h = h
         self._held = {}
+        self.native = isinstance(exchange, NativeExchange)
+        if self.native:
+            check(lib().psf_router_set_exchange(h, exchange.h))
 
     def __del__(self):
         try:
@@ -219,14 +286,16 @@ class PushRouter:
         msgs = list(streams.values())
         return (C.c_void_p * len(msgs))(*[m.h.value for m in msgs]), len(msgs)
 
-    def run(self, streams, steps: int) -> None:
-        """`steps` whole steps; world 1 without loopback: one native call."""
-        if self.world == 1 and not self.loopback:
+    def run(self, streams, steps: int, keep_encoded: bool = False) -> None:
+        """`steps` whole steps; one native call with a NativeExchange, or at
+        world 1 without loopback."""
+        if self.native or (self.world == 1 and not self.loopback):
+            check(lib().psf_router_keep_encoded(self.h, int(keep_encoded)))
             hs, n = self._handles(streams)
             check(lib().psf_router_step(self.h, hs, n, steps))
             return
         for _ in range(steps):
-            self.step(streams)
+            self.step(streams, keep_encoded)
 
     def step(self, streams, keep_encoded: bool = False) -> None:
         """streams: {stream id: template Message (key_channel = stream id)} of
@@ -235,7 +304,7 @@ class PushRouter:
         L = lib()
         check(L.psf_router_keep_encoded(self.h, int(keep_encoded)))
         hs, n = self._handles(streams)
-        if self.world == 1 and not self.loopback:
+        if self.native or (self.world == 1 and not self.loopback):
             check(L.psf_router_step(self.h, hs, n, 1))
             return
         W = self.world

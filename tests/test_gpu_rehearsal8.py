@@ -1,0 +1,139 @@
+"""GPU: the 8-rank partition of C4 and C5 (BASELINE configs[3], [4]) rehearsed
+on one GPU: world 8, one server per rank (EvenDivide(8), assigner.h:20-22,
+range.h:100-107), every stream sliced per destination server and encoded by
+its per-(stream, server) node (executor.cc:131-146), 7/8 of the slices moved
+to their owner rank in the cross-range spill, decoded there.
+
+* C4: 64 streams x 2^16 sorted uint64 keys, 8 streams per rank,
+  [KEY_CACHING, FIXING_FLOAT nb=1]
+* C5: one stream per rank, 2^14 keys x 128 f32 rows,
+  [KEY_CACHING, FIXING_FLOAT nb=1, COMPRESSING]
+
+Each runs a key-cache miss step (keys travel) then a hit step (keys elided).
+Every decoded slice is checked against the C restatement of the same slice
+(keys restored, values = port.ff_decode of port.ff_encode), every encoded C5
+value stream against the restatement of snappy 1.1.8 over the port's codes,
+and the miss step's spill against the encoded slices: the slices for other
+ranks' servers are exactly 7/8 of all, and what the exchange moved holds
+their frames.  `transport` selects the exchange: "gloo" (torch's gloo
+all-to-all-v, the Python step) or "native" (libpsf's own exchange over host
+shared memory, psf_router_step at world 8 -- one native call per run).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SEED = 1700000000
+WORLD = 8
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, shape, transport, q):
+    import torch
+    import torch.distributed as dist
+
+    import oracle
+    from parameter_server_amd import filter as F
+    from parameter_server_amd import shard
+    from test_gpu_spill import _check_step, _make_streams, _stream_data
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        if shape == "c4":
+            STREAMS, M, DIM, compress = 64, 1 << 16, 1, False
+            sids = [s for s in range(STREAMS) if s % world == rank]
+        else:
+            STREAMS, M, DIM, compress = world, 1 << 14, 128, True
+            sids = [rank]
+        S = world
+        F.set_clock(SEED)
+        ctx = F.Context(0)
+        ranges = shard.server_ranges(S)
+        if transport == "native":
+            ex = shard.NativeExchange.create(ctx, transport="host")
+        else:
+            ex = shard.SpillExchange(ctx, device="cuda:0")
+        router = shard.PushRouter(ctx, ranges, rank, world, ex)
+        streams = _make_streams(F, sids, M, DIM, compress)
+        port_ = oracle.Port()
+        expect = {(rank, s) for s in range(STREAMS)}  # one server per rank: server id == rank
+        sent = []
+        for step in range(2):
+            ex.bytes_sent = 0
+            if transport == "native":
+                router.run(streams, 1, keep_encoded=True)
+            else:
+                router.step(streams, keep_encoded=True)
+            torch.cuda.synchronize()
+            _check_step(F, router.results(), ranges, M, DIM, port_, expect)
+            enc = router.encoded()
+            assert sorted(k for k, _ in enc) == sorted((s, d) for s in sids for d in range(S)), step
+            remote = [(k, m) for k, m in enc if router.owner(k[1]) != rank]
+            assert 8 * len(remote) == 7 * len(enc), (len(remote), len(enc))
+            frame_bytes = 0
+            for (sid, d), m in remote:
+                has_key, _ = m.key_info()
+                assert has_key == (step == 0), (step, sid, d)
+                frame_bytes += m.key_ptr()[1] + m.value_ptr(0)[1]
+            assert ex.bytes_sent >= frame_bytes > 0
+            if compress:
+                keys, vals = _stream_data(rank, M, DIM)
+                for (sid, d), m in enc:
+                    lo, hi = ranges[d]
+                    sel = (keys >= np.uint64(lo)) & (keys < np.uint64(hi))
+                    st, codes, mn, mx = port_.ff_encode(vals.reshape(-1, DIM)[sel].reshape(-1), 1, SEED)
+                    vp, vn, vl = m.value_ptr(0)
+                    got = F.copy_out(vp, vn, vl, "cuda:0").cpu().numpy().tobytes()
+                    assert got == port_.snappy_compress(codes.tobytes()), (step, d)
+            sent.append(ex.bytes_sent)
+        q.put((rank, True, sent))
+    except Exception as e:  # report instead of hanging the parent
+        import traceback
+        q.put((rank, repr(e) + traceback.format_exc()[-2500:], None))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def _run(shape, transport):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, WORLD, port, shape, transport, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in procs:
+            r, ok, sent = q.get(timeout=100)
+            res[r] = (ok, sent)
+    finally:
+        for p in procs:
+            p.join(timeout=20)
+            if p.is_alive():
+                p.kill()
+    return res
+
+
+@pytest.mark.parametrize("transport", ["gloo", "native"])
+@pytest.mark.parametrize("shape", ["c4", "c5"])
+def test_world8_partition_same_gpu(shape, transport):
+    res = _run(shape, transport)
+    assert sorted(res) == list(range(WORLD))
+    for r in range(WORLD):
+        ok, sent = res[r]
+        assert ok is True, (r, ok)
+        assert 0 < sent[1] < sent[0], (r, sent)  # the hit step sends no keys

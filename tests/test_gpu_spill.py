@@ -176,7 +176,7 @@ def test_router_multi_step_driver(dim, compress, m):
     assert hs["steps"] == 6
 
 
-def _spill_worker(rank, world, port, backend, loopback, q):
+def _spill_worker(rank, world, port, backend, loopback, q, native=None):
     import torch
     import torch.distributed as dist
 
@@ -194,7 +194,10 @@ def _spill_worker(rank, world, port, backend, loopback, q):
         F.set_clock(SEED)
         ctx = F.Context(0)
         ranges = shard.server_ranges(S)
-        ex = shard.SpillExchange(ctx, device="cuda:0")
+        if native:
+            ex = shard.NativeExchange.create(ctx, transport=native)
+        else:
+            ex = shard.SpillExchange(ctx, device="cuda:0")
         router = shard.PushRouter(ctx, ranges, rank, world, ex, loopback=loopback)
         streams = _make_streams(F, [s for s in range(STREAMS) if s % world == rank], M, 1, False)
         port_ = oracle.Port()
@@ -215,12 +218,13 @@ def _spill_worker(rank, world, port, backend, loopback, q):
             dist.destroy_process_group()
 
 
-def _run_ranks(world, backend, loopback):
+def _run_ranks(world, backend, loopback, native=None):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_spill_worker, args=(r, world, port, backend, loopback, q)) for r in range(world)]
+    procs = [ctx.Process(target=_spill_worker, args=(r, world, port, backend, loopback, q, native))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = {}
@@ -232,17 +236,22 @@ def _run_ranks(world, backend, loopback):
     return res
 
 
-def test_spill_nccl_world1_loopback():
-    """The RCCL spill path on the device: nccl process group at world 1, every
-    slice packed, moved by all_to_all_single and unpacked before decoding."""
-    res = _run_ranks(1, "nccl", True)
+@pytest.mark.parametrize("native", [None, "rccl"])
+def test_spill_nccl_world1_loopback(native):
+    """The RCCL spill path on the device at world 1, every slice through the
+    exchange: torch's all_to_all_single (the Python step), or libpsf's own
+    exchange (native: the records through the mailbox, the data by RCCL
+    point-to-point on the exchange's stream, psf_router_step)."""
+    res = _run_ranks(1, "nccl", True, native)
     ok, sent = res[0]
     assert ok is True, ok
 
 
-def test_push_router_world2_same_gpu():
-    """Two ranks on cuda:0 over gloo (host-staged), 2 servers per rank."""
-    res = _run_ranks(2, "gloo", False)
+@pytest.mark.parametrize("native", [None, "host"])
+def test_push_router_world2_same_gpu(native):
+    """Two ranks on cuda:0 over gloo (host-staged), 2 servers per rank; native:
+    libpsf's exchange through the host mailbox."""
+    res = _run_ranks(2, "gloo", False, native)
     for r in range(2):
         ok, sent = res[r]
         assert ok is True, ok

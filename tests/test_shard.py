@@ -157,7 +157,7 @@ def test_spill_exchange_gloo_world2():
     assert res == {0: True, 1: True}
 
 
-def _router_worker(rank, world, port, q):
+def _router_worker(rank, world, port, q, native=False):
     import torch.distributed as dist
 
     from bench import splitmix64_keys
@@ -169,7 +169,8 @@ def _router_worker(rank, world, port, q):
     try:
         ctx = F.HostContext()
         ranges = shard.server_ranges(5)  # 5 servers over 2 ranks: blocks of 2 and 3
-        router = shard.PushRouter(ctx, ranges, rank, world, shard.SpillExchange(ctx))
+        ex = shard.NativeExchange.create(ctx, transport="host") if native else shard.SpillExchange(ctx)
+        router = shard.PushRouter(ctx, ranges, rank, world, ex)
         sids = [10 * r + j for r in range(world) for j in range(3)]
         data = {s: (splitmix64_keys(700 + s, 4 + s),) for s in sids}
         data = {s: (k[0], np.random.default_rng(s).standard_normal(2 * k[0].size).astype(np.float32))
@@ -186,8 +187,11 @@ def _router_worker(rank, world, port, q):
             streams[s] = m
         mine = [d for d in range(5) if shard.server_rank(d, 5, world) == rank]
         ok = True
-        for step in range(2):  # miss (keys travel), then hit (keys elided, restored)
-            router.step(streams)
+        for step in range(4):  # miss (keys travel), then hits (keys elided, restored)
+            if native and step == 3:
+                router.run(streams, 3)  # three steps in one call: the mailbox banks alternate
+            else:
+                router.step(streams)
             seen = set()
             for d, w in router.results():
                 s = shard.w_channel(w)
@@ -209,16 +213,19 @@ def _router_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_push_router_gloo_world2_host():
+@pytest.mark.parametrize("native", [False, True])
+def test_push_router_gloo_world2_host(native):
     """The native router (psf_router_*) across two ranks on CPU: 6 streams, 5
     servers (2 on rank 0, 3 on rank 1), host keys, [KEY_CACHING]; every
     server's decoded slices equal the restated slicing, on the miss and the
-    hit step."""
+    hit steps.  native: libpsf's exchange (records and data through the
+    node's mailbox, psf_router_step at world 2) instead of gloo's
+    all-to-all-v."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_router_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_router_worker, args=(r, 2, port, q, native)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=120) for _ in procs)
