@@ -584,9 +584,13 @@ __device__ __forceinline__ uint64_t lcg_bit(uint32_t& s) {
 // them, whose t is 0 or within 1e-4 of ratio, inside the band.  Codes <=
 // ratio = 254, so the packed LCG bits add without carries.  A lane that fails
 // redoes its 16 values with the reference's double sequence.
+// The slow path reloads its values from xg (this lane's group gb: x + 4 gb;
+// an L2 hit) instead of keeping v live through the f64 divides: v is dead
+// once the fast floors are packed, which keeps the kernel at 64 VGPRs.
 template <bool kStored = false>
 __device__ __forceinline__ void encode_tile_f32_nb1(const float v[4][4], const QuantParams& q,
                                                     const uint32_t b4[4], uint32_t* __restrict__ out,
+                                                    const float* __restrict__ xg,
                                                     const StoredLayout* L = nullptr, size_t gs = 0) {
   typedef float f32x2 __attribute__((ext_vector_type(2)));
   const f32x2 mn2 = {q.min_f, q.min_f}, sc2 = {q.scale_f, q.scale_f};
@@ -614,14 +618,15 @@ __device__ __forceinline__ void encode_tile_f32_nb1(const float v[4][4], const Q
   if (__builtin_expect(!fast, 0)) {
     // rare (~0.4 % of lanes): find the values inside the band again and give
     // only those the exact sequence (an f64 divide each)
-#pragma unroll
+#pragma unroll 1
     for (int u = 0; u < 4; ++u)
-#pragma unroll
+#pragma unroll 1
       for (int j = 0; j < 4; ++j) {
+        const float xv = xg[4 * u * kBlock + j];
         bool ok;
-        (void)quant_fast<float, 1>(v[u][j], q, ok);
+        (void)quant_fast<float, 1>(xv, q, ok);
         if (!ok) {
-          const uint32_t c = quant_exact((double)v[u][j], q);
+          const uint32_t c = quant_exact((double)xv, q);
           w[u] = (w[u] & ~(0xFFu << (8 * j))) | (c << (8 * j));
         }
       }
@@ -640,8 +645,8 @@ __device__ __forceinline__ void encode_tile_f32_nb1(const float v[4][4], const Q
 // L1/L2-hit load and a funnel shift) -- then quantise, add, pack, store.
 template <typename V, int NB, bool kStored = false>
 __device__ __forceinline__ void encode_full_tile(const V v[4][4], const QuantParams& q, const EncodeParams& p,
-                                                 uint8_t* __restrict__ out, size_t gb, size_t gs,
-                                                 const StoredLayout* L = nullptr) {
+                                                 const V* __restrict__ x, uint8_t* __restrict__ out, size_t gb,
+                                                 size_t gs, const StoredLayout* L = nullptr) {
   uint32_t b4[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
@@ -650,9 +655,10 @@ __device__ __forceinline__ void encode_full_tile(const V v[4][4], const QuantPar
     b4[u] = __builtin_amdgcn_alignbit(w.y, w.x, k & 31u) & 0xFu;
   }
   if (NB == 1 && sizeof(V) == 4) {
+    const float* xg = reinterpret_cast<const float*>(x) + 4 * gb;
     if (kStored) encode_tile_f32_nb1<true>(reinterpret_cast<const float(*)[4]>(v), q, b4,
-                                           reinterpret_cast<uint32_t*>(out), L, gs);
-    else encode_tile_f32_nb1(reinterpret_cast<const float(*)[4]>(v), q, b4, reinterpret_cast<uint32_t*>(out) + gs);
+                                           reinterpret_cast<uint32_t*>(out), xg, L, gs);
+    else encode_tile_f32_nb1(reinterpret_cast<const float(*)[4]>(v), q, b4, reinterpret_cast<uint32_t*>(out) + gs, xg);
     return;
   }
   uint32_t fl[4][4];
@@ -723,13 +729,13 @@ __global__ __launch_bounds__(kBlock) void ff_encode(const V* __restrict__ x, siz
 
   if (kVec) {
     if (t0 < tf) {
-      encode_full_tile<V, NB>(first, q, p, out, t0 * kTileGroups + threadIdx.x, t0 * kTileGroups + threadIdx.x);
+      encode_full_tile<V, NB>(first, q, p, x, out, t0 * kTileGroups + threadIdx.x, t0 * kTileGroups + threadIdx.x);
       for (size_t t = t0 + 1; t < tf; ++t) {
         const size_t gb = t * kTileGroups + threadIdx.x;
         V v[4][4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) Vec4<V>::load(x + 4 * (gb + u * kBlock), v[u]);
-        encode_full_tile<V, NB>(v, q, p, out, gb, gb);
+        encode_full_tile<V, NB>(v, q, p, x, out, gb, gb);
       }
     }
     // the partial last tile of the array, if this workgroup owns it: the LCG
@@ -1246,14 +1252,14 @@ __device__ __forceinline__ int encode_batch_body(const FfBatchT<CAP>& B, uint32_
       for (size_t t = t0; t < tf; ++t) {
         if (t != t0) load_tile(t);
         const size_t gb = t * kTileGroups + threadIdx.x;
-        encode_full_tile<V, NB, true>(v, q, p, out, gb, gb, &L);
+        encode_full_tile<V, NB, true>(v, q, p, x, out, gb, gb, &L);
       }
     }
   }
   if (!stored) {
     for (size_t t = t0; t < tf; ++t) {
       if (t != t0) load_tile(t);
-      encode_full_tile<V, NB>(v, q, p, out, t * kTileGroups + threadIdx.x, t * kTileGroups + threadIdx.x);
+      encode_full_tile<V, NB>(v, q, p, x, out, t * kTileGroups + threadIdx.x, t * kTileGroups + threadIdx.x);
     }
   }
   for (size_t t = (t0 > tf ? t0 : tf); t < t1; ++t) {
@@ -1293,8 +1299,13 @@ __device__ __forceinline__ int encode_batch_body(const FfBatchT<CAP>& B, uint32_
   return jb;
 }
 
+// PSF_ENC_BATCH_WAVES (A/B knob, tools/build_variants.sh): a minimum of waves
+// per SIMD for the plain batched encode (8: at most 64 registers)
+#ifndef PSF_ENC_BATCH_WAVES
+#define PSF_ENC_BATCH_WAVES 1
+#endif
 template <typename V, int NB, int CAP, bool kStored>
-__global__ __launch_bounds__(kBlock) void ff_encode_batch(FfBatchT<CAP> B) {
+__global__ __launch_bounds__(kBlock, kStored ? 1 : PSF_ENC_BATCH_WAVES) void ff_encode_batch(FfBatchT<CAP> B) {
   encode_batch_body<V, NB, CAP, kStored>(B, blockIdx.x, nullptr);
 }
 

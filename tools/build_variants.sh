@@ -7,7 +7,8 @@ set -e
 cd "$(dirname "$0")/.."
 python -m parameter_server_amd.build > /dev/null
 SRCF=${SRC:-parameter_server_amd/csrc/ff_codec.hip}
-OBJS=$(ls parameter_server_amd/build/*.o | grep -v "/$(basename $SRCF).o$")
+EXCL=${EXCL:-$(basename $SRCF).o}
+OBJS=$(ls parameter_server_amd/build/*.o | grep -v "/$EXCL$")
 name=$1; shift
 mkdir -p tools/variants/$name
 /opt/rocm/bin/hipcc -x hip --offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -Iinclude -Iparameter_server_amd/csrc "$@" \
