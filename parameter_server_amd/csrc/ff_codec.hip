@@ -348,6 +348,10 @@ struct EncodeParams {
   // 1: workgroup b takes the tiles of workgroup grid - 1 - b, the array's end
   // first -- what a strided min/max pass read last (the Infinity Cache's)
   uint32_t reverse;
+  // 1: the full tiles are swept by the whole grid together (workgroup b takes
+  // tiles b, b + grid, ... -- counted from the array's end with `reverse`),
+  // as the strided min/max pass reads them, instead of a contiguous run each
+  uint32_t strided;
 };
 
 // s -> a*s + c, composed k times.
@@ -584,13 +588,9 @@ __device__ __forceinline__ uint64_t lcg_bit(uint32_t& s) {
 // them, whose t is 0 or within 1e-4 of ratio, inside the band.  Codes <=
 // ratio = 254, so the packed LCG bits add without carries.  A lane that fails
 // redoes its 16 values with the reference's double sequence.
-// The slow path reloads its values from xg (this lane's group gb: x + 4 gb;
-// an L2 hit) instead of keeping v live through the f64 divides: v is dead
-// once the fast floors are packed, which keeps the kernel at 64 VGPRs.
 template <bool kStored = false>
 __device__ __forceinline__ void encode_tile_f32_nb1(const float v[4][4], const QuantParams& q,
                                                     const uint32_t b4[4], uint32_t* __restrict__ out,
-                                                    const float* __restrict__ xg,
                                                     const StoredLayout* L = nullptr, size_t gs = 0) {
   typedef float f32x2 __attribute__((ext_vector_type(2)));
   const f32x2 mn2 = {q.min_f, q.min_f}, sc2 = {q.scale_f, q.scale_f};
@@ -618,15 +618,14 @@ __device__ __forceinline__ void encode_tile_f32_nb1(const float v[4][4], const Q
   if (__builtin_expect(!fast, 0)) {
     // rare (~0.4 % of lanes): find the values inside the band again and give
     // only those the exact sequence (an f64 divide each)
-#pragma unroll 1
+#pragma unroll
     for (int u = 0; u < 4; ++u)
-#pragma unroll 1
+#pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float xv = xg[4 * u * kBlock + j];
         bool ok;
-        (void)quant_fast<float, 1>(xv, q, ok);
+        (void)quant_fast<float, 1>(v[u][j], q, ok);
         if (!ok) {
-          const uint32_t c = quant_exact((double)xv, q);
+          const uint32_t c = quant_exact((double)v[u][j], q);
           w[u] = (w[u] & ~(0xFFu << (8 * j))) | (c << (8 * j));
         }
       }
@@ -645,8 +644,8 @@ __device__ __forceinline__ void encode_tile_f32_nb1(const float v[4][4], const Q
 // L1/L2-hit load and a funnel shift) -- then quantise, add, pack, store.
 template <typename V, int NB, bool kStored = false>
 __device__ __forceinline__ void encode_full_tile(const V v[4][4], const QuantParams& q, const EncodeParams& p,
-                                                 const V* __restrict__ x, uint8_t* __restrict__ out, size_t gb,
-                                                 size_t gs, const StoredLayout* L = nullptr) {
+                                                 uint8_t* __restrict__ out, size_t gb, size_t gs,
+                                                 const StoredLayout* L = nullptr) {
   uint32_t b4[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
@@ -655,10 +654,9 @@ __device__ __forceinline__ void encode_full_tile(const V v[4][4], const QuantPar
     b4[u] = __builtin_amdgcn_alignbit(w.y, w.x, k & 31u) & 0xFu;
   }
   if (NB == 1 && sizeof(V) == 4) {
-    const float* xg = reinterpret_cast<const float*>(x) + 4 * gb;
     if (kStored) encode_tile_f32_nb1<true>(reinterpret_cast<const float(*)[4]>(v), q, b4,
-                                           reinterpret_cast<uint32_t*>(out), xg, L, gs);
-    else encode_tile_f32_nb1(reinterpret_cast<const float(*)[4]>(v), q, b4, reinterpret_cast<uint32_t*>(out) + gs, xg);
+                                           reinterpret_cast<uint32_t*>(out), L, gs);
+    else encode_tile_f32_nb1(reinterpret_cast<const float(*)[4]>(v), q, b4, reinterpret_cast<uint32_t*>(out) + gs);
     return;
   }
   uint32_t fl[4][4];
@@ -682,14 +680,31 @@ __global__ __launch_bounds__(kBlock) void ff_encode(const V* __restrict__ x, siz
   const size_t ntiles = (ngroups + kTileGroups - 1) / kTileGroups;
   const size_t nfull = ngroups / kTileGroups;
   size_t t0 = 0, t1 = 0;
+  // the full tiles this workgroup encodes: tfirst, tfirst + tstep, ... (cnt)
+  int64_t tfirst = 0, tstep = 1, cnt = 0;
   if (kVec) {
-    tile_range(ntiles, t0, t1, p.reverse ? gridDim.x - 1 - blockIdx.x : blockIdx.x);
+    if (p.strided) {
+      const int64_t b = blockIdx.x, G = gridDim.x;
+      cnt = b < (int64_t)nfull ? ((int64_t)nfull - b + G - 1) / G : 0;
+      tfirst = p.reverse ? (int64_t)nfull - 1 - b : b;
+      tstep = p.reverse ? -G : G;
+      // the partial last tile: the workgroup whose sweep would reach it next
+      t0 = t1 = ntiles;
+      if (ntiles > nfull && (size_t)blockIdx.x == nfull % gridDim.x) t0 = nfull;
+    } else {
+      tile_range(ntiles, t0, t1, p.reverse ? gridDim.x - 1 - blockIdx.x : blockIdx.x);
+      const size_t tf0 = t1 < nfull ? t1 : nfull;
+      tfirst = (int64_t)t0;
+      cnt = tf0 > t0 ? (int64_t)(tf0 - t0) : 0;
+      if (t0 < tf0) t0 = tf0;  // what is left: the partial tile, if owned
+    }
   }
-  const size_t tf = t1 < nfull ? t1 : nfull;  // full tiles are [t0, tf)
+  const size_t tf = t0;  // (the partial tile loop below runs [max(t0, tf), t1))
   V first[4][4];
-  if (kVec && t0 < tf) {
+  if (kVec && cnt > 0) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) Vec4<V>::load(x + 4 * (t0 * kTileGroups + threadIdx.x + u * kBlock), first[u]);
+    for (int u = 0; u < 4; ++u)
+      Vec4<V>::load(x + 4 * ((size_t)tfirst * kTileGroups + threadIdx.x + u * kBlock), first[u]);
   }
 
   float mn_f = p.preset_min, mx_f = p.preset_max;
@@ -728,14 +743,15 @@ __global__ __launch_bounds__(kBlock) void ff_encode(const V* __restrict__ x, siz
   if (!(q.bin > 0)) return;  // CHECK_GT(bin, 0), fixing_float.h:71
 
   if (kVec) {
-    if (t0 < tf) {
-      encode_full_tile<V, NB>(first, q, p, x, out, t0 * kTileGroups + threadIdx.x, t0 * kTileGroups + threadIdx.x);
-      for (size_t t = t0 + 1; t < tf; ++t) {
-        const size_t gb = t * kTileGroups + threadIdx.x;
+    if (cnt > 0) {
+      const size_t g0 = (size_t)tfirst * kTileGroups + threadIdx.x;
+      encode_full_tile<V, NB>(first, q, p, out, g0, g0);
+      for (int64_t i = 1; i < cnt; ++i) {
+        const size_t gb = (size_t)(tfirst + i * tstep) * kTileGroups + threadIdx.x;
         V v[4][4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) Vec4<V>::load(x + 4 * (gb + u * kBlock), v[u]);
-        encode_full_tile<V, NB>(v, q, p, x, out, gb, gb);
+        encode_full_tile<V, NB>(v, q, p, out, gb, gb);
       }
     }
     // the partial last tile of the array, if this workgroup owns it: the LCG
@@ -1252,14 +1268,14 @@ __device__ __forceinline__ int encode_batch_body(const FfBatchT<CAP>& B, uint32_
       for (size_t t = t0; t < tf; ++t) {
         if (t != t0) load_tile(t);
         const size_t gb = t * kTileGroups + threadIdx.x;
-        encode_full_tile<V, NB, true>(v, q, p, x, out, gb, gb, &L);
+        encode_full_tile<V, NB, true>(v, q, p, out, gb, gb, &L);
       }
     }
   }
   if (!stored) {
     for (size_t t = t0; t < tf; ++t) {
       if (t != t0) load_tile(t);
-      encode_full_tile<V, NB>(v, q, p, x, out, t * kTileGroups + threadIdx.x, t * kTileGroups + threadIdx.x);
+      encode_full_tile<V, NB>(v, q, p, out, t * kTileGroups + threadIdx.x, t * kTileGroups + threadIdx.x);
     }
   }
   for (size_t t = (t0 > tf ? t0 : tf); t < t1; ++t) {
@@ -1380,6 +1396,27 @@ __global__ __launch_bounds__(kBlock) void ff_fused_batch(FfBatchT<kBatchSmall> D
 }
 
 // ------------------------------------------------------------ launchers ----
+// PSF_ENC_STRIDED (A/B knob): 1 = the single-array encode sweeps its full
+// tiles with the whole grid (EncodeParams::strided)
+static bool enc_strided_mode() {
+  static const bool on = [] {
+    const char* e = getenv("PSF_ENC_STRIDED");
+    return e && *e == '1';
+  }();
+  return on;
+}
+// PSF_ENC_LDS (A/B knob): bytes of dynamic LDS each encode workgroup reserves
+// and never touches -- a cap on the encode's resident workgroups per CU
+// (160 KiB / pad), to measure how its streaming rate depends on occupancy
+static size_t enc_lds_pad() {
+  static const size_t v = [] {
+    const char* e = getenv("PSF_ENC_LDS");
+    const long b = e ? atol(e) : 0;
+    return b > 0 && b <= 65536 ? (size_t)b : (size_t)0;
+  }();
+  return v;
+}
+
 static inline void lcg_affine_pow(uint64_t k, uint32_t& A, uint32_t& Cc) {
   uint32_t a = kLcgA, c = kLcgC;
   A = 1u; Cc = 0u;
@@ -1466,6 +1503,7 @@ static void launch_encode(const V* x, size_t n, uint8_t* out, EncodeParams p, hi
   // Cache (smaller ones stay on chip whatever the order, and the reversed
   // order cost C3's 40 MB arrays 9 %: encode 15.8 -> 17.8 us, tools/ab_perm_c13.sh)
   p.reverse = kVec && p.partials && enc_perm_mode() && (double)n * sizeof(V) > 256.0 * (1 << 20) ? 1u : 0u;
+  p.strided = kVec && enc_strided_mode() ? 1u : 0u;
   lcg_affine_pow(4ull * kBlock, p.a_lane, p.c_lane);
   lcg_affine_pow(4ull * kTileGroups, p.a_tile, p.c_tile);
   lcg_affine_pow((uint64_t)grid * kBlock, p.a_thr, p.c_thr);
@@ -1477,7 +1515,7 @@ static void launch_encode(const V* x, size_t n, uint8_t* out, EncodeParams p, hi
     p.k17.c[k] &= kMask17;
   }
   p.lcg_pos = lcg_cycle().pos[p.seed & kMask17];
-  hipLaunchKernelGGL((ff_encode<V, NB, kVec>), dim3(grid), dim3(kBlock), 0, st, x, n, out, p);
+  hipLaunchKernelGGL((ff_encode<V, NB, kVec>), dim3(grid), dim3(kBlock), enc_lds_pad(), st, x, n, out, p);
 }
 
 template <typename V, bool kVec>
@@ -1629,9 +1667,9 @@ static void launch_encode_batch(FfBatchT<CAP>& B, uint32_t enc_total, hipStream_
   bool stored = false;
   for (int i = 0; i < B.njobs; ++i) stored |= (B.job[i].flags & kFlagStored) != 0;
   if (stored && (NB == 1 || NB == 2))
-    hipLaunchKernelGGL((ff_encode_batch<V, NB, CAP, true>), dim3(enc_total), dim3(kBlock), 0, st, B);
+    hipLaunchKernelGGL((ff_encode_batch<V, NB, CAP, true>), dim3(enc_total), dim3(kBlock), enc_lds_pad(), st, B);
   else
-    hipLaunchKernelGGL((ff_encode_batch<V, NB, CAP, false>), dim3(enc_total), dim3(kBlock), 0, st, B);
+    hipLaunchKernelGGL((ff_encode_batch<V, NB, CAP, false>), dim3(enc_total), dim3(kBlock), enc_lds_pad(), st, B);
 }
 
 static size_t tiles_of(size_t n) { return ((n >> 2) + kTileGroups - 1) / kTileGroups; }

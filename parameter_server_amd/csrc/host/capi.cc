@@ -115,7 +115,7 @@ int psf_context_create(int device, void* stream, int own_stream, psf_context** o
 }
 int psf_context_destroy(psf_context* ctx) {
   if (!ctx) return PSF_OK;
-  delete ctx->impl;
+  psf::Context::unref(ctx->impl);  // deleted now, or when its last node / router / exchange / map goes
   delete ctx;
   return PSF_OK;
 }
@@ -375,13 +375,16 @@ int psf_node_create(psf_context* ctx, psf_node** out) {
   return guarded(ctx ? ctx->impl : nullptr, [&] {
     if (!ctx || !out) return PSF_ERR_ARG;
     *out = new psf_node{new psf::RemoteNode(ctx->impl)};
+    psf::Context::ref(ctx->impl);
     return PSF_OK;
   });
 }
 int psf_node_destroy(psf_node* node) {
   if (!node) return PSF_OK;
+  psf::Context* c = node->impl->ctx();
   delete node->impl;
   delete node;
+  psf::Context::unref(c);
   return PSF_OK;
 }
 int psf_node_encode(psf_node* node, psf_message* msg) {
@@ -918,11 +921,15 @@ int psf_router_create(psf_context* ctx, const uint64_t* bounds, int nservers, in
     std::vector<psf::KeyRange> krs(nservers);
     for (int i = 0; i < nservers; ++i) krs[i] = psf::KeyRange{bounds[i], bounds[i + 1]};
     *out = reinterpret_cast<psf_router*>(new psf::PushRouter(ctx->impl, krs, rank, world, loopback != 0));
+    psf::Context::ref(ctx->impl);
     return PSF_OK;
   });
 }
 int psf_router_destroy(psf_router* r) {
+  if (!r) return PSF_OK;
+  psf::Context* c = reinterpret_cast<psf::PushRouter*>(r)->context();
   delete reinterpret_cast<psf::PushRouter*>(r);
+  psf::Context::unref(c);
   return PSF_OK;
 }
 static psf::PushRouter* R(psf_router* r) {
@@ -1005,11 +1012,15 @@ int psf_exchange_create(psf_context* ctx, int rank, int world, const char* name,
     *out = reinterpret_cast<psf_exchange*>(new psf::Exchange(
         ctx->impl, rank, world, name, transport == PSF_EXCHANGE_RCCL ? psf::Exchange::kRccl : psf::Exchange::kHost,
         nccl_id, meta_cap, host_cap));
+    psf::Context::ref(ctx->impl);
     return PSF_OK;
   });
 }
 int psf_exchange_destroy(psf_exchange* ex) {
+  if (!ex) return PSF_OK;
+  psf::Context* c = reinterpret_cast<psf::Exchange*>(ex)->context();
   delete reinterpret_cast<psf::Exchange*>(ex);
+  psf::Context::unref(c);
   return PSF_OK;
 }
 int psf_exchange_stats(psf_exchange* ex, int64_t* out) {
@@ -1237,13 +1248,16 @@ int psf_kvmap_create(psf_context* ctx, size_t capacity, int lr_type, double alph
     c.lambda1 = lambda1;
     c.lambda2 = lambda2;
     *out = new psf_kvmap{new psf::KvMapFtrl(ctx->impl, capacity, c), ctx->impl};
+    psf::Context::ref(ctx->impl);
     return PSF_OK;
   });
 }
 int psf_kvmap_destroy(psf_kvmap* map) {
   if (!map) return PSF_OK;
+  psf::Context* c = map->ctx;
   delete map->impl;
   delete map;
+  psf::Context::unref(c);
   return PSF_OK;
 }
 int psf_kvmap_set_value(psf_kvmap* map, const psf_message* msg) {

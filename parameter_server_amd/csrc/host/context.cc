@@ -369,6 +369,15 @@ Context::~Context() {
     }
   }
   ring_uses_.clear();
+  for (auto& w : dev_records_) {
+    auto rb = w.lock();
+    if (rb && !rb->done) {
+      if (hipMemcpy(rb->host.data(), rb->dev.ptr, rb->host.size() * 4, hipMemcpyDeviceToHost) == hipSuccess)
+        rb->done = true;
+      rb->ctx = nullptr;
+    }
+  }
+  dev_records_.clear();
   tracked_.clear();
   for (hipEvent_t e : events_) (void)hipEventDestroy(e);
   (void)hipHostFree(lazy_h_);
@@ -547,6 +556,10 @@ void Context::sync() {
 
 void RangeBatch::resolve(bool synced) {
   if (done) return;
+  if (!ctx) {  // its context went first and the records could not be read
+    done = true;
+    return;
+  }
   if (!synced) ctx->sync();  // the kernels' host-mapped stores are visible after it
   if (ring) {
     memcpy(host.data(), ring, host.size() * 4);
@@ -578,6 +591,15 @@ float* Context::claim_lazy(const std::shared_ptr<RangeBatch>& rb, int n) {
   const uint64_t at = start % kLazyRing;
   rb->ring = lazy_h_ + 4 * at;
   return reinterpret_cast<float*>(lazy_m_ + 4 * at);
+}
+
+void Context::adopt_device_records(const std::shared_ptr<RangeBatch>& rb) {
+  if (dev_records_.size() >= 1024) {
+    dev_records_.erase(std::remove_if(dev_records_.begin(), dev_records_.end(),
+                                      [](const std::weak_ptr<RangeBatch>& w) { return w.expired(); }),
+                       dev_records_.end());
+  }
+  dev_records_.push_back(rb);
 }
 
 void Context::track(std::shared_ptr<RangeBatch> rb) {

@@ -6,6 +6,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <deque>
 #include <memory>
 #include <vector>
@@ -91,6 +92,21 @@ class Context {
 
   int device() const { return device_; }
   hipStream_t stream() const { return stream_; }
+
+  // Lifetime: the C ABI's handle holds one reference, every node, router,
+  // exchange and KV map made on the context one more; the context is deleted
+  // when the last goes (a binding may destroy them in any order, e.g. a
+  // garbage collector finalising a cycle).
+  std::atomic<int> refs{1};
+  static void ref(Context* c) {
+    if (c) c->refs.fetch_add(1, std::memory_order_relaxed);
+  }
+  static void unref(Context* c) {
+    if (c && c->refs.fetch_sub(1, std::memory_order_acq_rel) == 1) delete c;
+  }
+  // side-info records a received message's decodes read in HBM (spill.cc):
+  // settled to the host if the context goes first
+  void adopt_device_records(const std::shared_ptr<RangeBatch>& rb);
   // a second stream of this context for work no kernel of stream() depends
   // on (the round-trip drivers' KEY_CACHING presign CRCs of the next
   // iteration's keys, read back through publish slots), created on first use
@@ -234,6 +250,7 @@ class Context {
     uint64_t start, n;
   };
   std::deque<RingUse> ring_uses_;
+  std::vector<std::weak_ptr<RangeBatch>> dev_records_;
   int device_;
   bool shared_stream_ = false;
   hipStream_t stream_;

@@ -280,6 +280,7 @@ void spill_unpack_host(Context* ctx, const uint8_t* meta, uint64_t mlen, const B
   rb->dev.bytes = 16ull * nslots;
   rb->dev.loc = Loc::kDevice;
   rb->host.assign(4ull * nslots, 0u);
+  ctx->adopt_device_records(rb);
   for (const Pend& q : pend) {
     Message& m = (*out)[q.msg];
     if (q.f >= m.task.filter.size() || m.task.filter[q.f].type != FilterConfig::FIXING_FLOAT ||

@@ -286,16 +286,18 @@ class PushRouter:
         msgs = list(streams.values())
         return (C.c_void_p * len(msgs))(*[m.h.value for m in msgs]), len(msgs)
 
-    def run(self, streams, steps: int, keep_encoded: bool = False) -> None:
+    def run(self, streams, steps: int, keep_encoded=None) -> None:
         """`steps` whole steps; one native call with a NativeExchange, or at
-        world 1 without loopback."""
+        world 1 without loopback.  keep_encoded: None leaves the router's
+        setting (psf_router_keep_encoded) as it is."""
         if self.native or (self.world == 1 and not self.loopback):
-            check(lib().psf_router_keep_encoded(self.h, int(keep_encoded)))
+            if keep_encoded is not None:
+                check(lib().psf_router_keep_encoded(self.h, int(keep_encoded)))
             hs, n = self._handles(streams)
             check(lib().psf_router_step(self.h, hs, n, steps))
             return
         for _ in range(steps):
-            self.step(streams, keep_encoded)
+            self.step(streams, bool(keep_encoded))
 
     def step(self, streams, keep_encoded: bool = False) -> None:
         """streams: {stream id: template Message (key_channel = stream id)} of

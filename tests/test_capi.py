@@ -100,3 +100,34 @@ def test_default_device_knob():
         r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True)
         assert r.returncode == 0 and r.stdout.split()[0] == "0"
         assert "PSF_DEVICE" in r.stderr and "warning" in r.stderr
+
+
+def test_context_outlives_its_users_whatever_the_destroy_order():
+    """A binding may finalise handles in any order (a garbage collector
+    clearing a cycle): destroying the context before its node and router
+    leaves them usable until they go, and nothing is freed twice."""
+    import ctypes as C
+
+    import numpy as np
+    import torch
+
+    from parameter_server_amd import KEY_CACHING, lib, shard
+    from parameter_server_amd import filter as F
+    from parameter_server_amd._lib import check
+    L = lib()
+    ctx = F.HostContext()
+    node = F.RemoteNode(ctx)
+    router = shard.PushRouter(ctx, shard.server_ranges(3), 0, 1)
+    keys = np.arange(0, 3000, 3, dtype=np.uint64) << np.uint64(50)
+    m = F.Message(request=True, push=True, key_channel=4, key_range=shard.KEY_ALL)
+    m.set_key(torch.from_numpy(keys.view(np.int64).copy()))
+    m.add_filter(KEY_CACHING)
+    check(L.psf_context_destroy(ctx.h))  # the handle goes first
+    ctx.h = C.c_void_p()
+    router.step({4: m})  # still alive through the router's reference
+    assert len(router.results()) == 3
+    node.encode(m)
+    check(L.psf_router_destroy(router.h))
+    router.h = None
+    check(L.psf_node_destroy(node.h))  # the last user: the context goes now
+    node.h = None
