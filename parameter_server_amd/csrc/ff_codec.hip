@@ -348,10 +348,6 @@ struct EncodeParams {
   // 1: workgroup b takes the tiles of workgroup grid - 1 - b, the array's end
   // first -- what a strided min/max pass read last (the Infinity Cache's)
   uint32_t reverse;
-  // 1: the full tiles are swept by the whole grid together (workgroup b takes
-  // tiles b, b + grid, ... -- counted from the array's end with `reverse`),
-  // as the strided min/max pass reads them, instead of a contiguous run each
-  uint32_t strided;
 };
 
 // s -> a*s + c, composed k times.
@@ -680,31 +676,14 @@ __global__ __launch_bounds__(kBlock) void ff_encode(const V* __restrict__ x, siz
   const size_t ntiles = (ngroups + kTileGroups - 1) / kTileGroups;
   const size_t nfull = ngroups / kTileGroups;
   size_t t0 = 0, t1 = 0;
-  // the full tiles this workgroup encodes: tfirst, tfirst + tstep, ... (cnt)
-  int64_t tfirst = 0, tstep = 1, cnt = 0;
   if (kVec) {
-    if (p.strided) {
-      const int64_t b = blockIdx.x, G = gridDim.x;
-      cnt = b < (int64_t)nfull ? ((int64_t)nfull - b + G - 1) / G : 0;
-      tfirst = p.reverse ? (int64_t)nfull - 1 - b : b;
-      tstep = p.reverse ? -G : G;
-      // the partial last tile: the workgroup whose sweep would reach it next
-      t0 = t1 = ntiles;
-      if (ntiles > nfull && (size_t)blockIdx.x == nfull % gridDim.x) t0 = nfull;
-    } else {
-      tile_range(ntiles, t0, t1, p.reverse ? gridDim.x - 1 - blockIdx.x : blockIdx.x);
-      const size_t tf0 = t1 < nfull ? t1 : nfull;
-      tfirst = (int64_t)t0;
-      cnt = tf0 > t0 ? (int64_t)(tf0 - t0) : 0;
-      if (t0 < tf0) t0 = tf0;  // what is left: the partial tile, if owned
-    }
+    tile_range(ntiles, t0, t1, p.reverse ? gridDim.x - 1 - blockIdx.x : blockIdx.x);
   }
-  const size_t tf = t0;  // (the partial tile loop below runs [max(t0, tf), t1))
+  const size_t tf = t1 < nfull ? t1 : nfull;  // full tiles are [t0, tf)
   V first[4][4];
-  if (kVec && cnt > 0) {
+  if (kVec && t0 < tf) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
-      Vec4<V>::load(x + 4 * ((size_t)tfirst * kTileGroups + threadIdx.x + u * kBlock), first[u]);
+    for (int u = 0; u < 4; ++u) Vec4<V>::load(x + 4 * (t0 * kTileGroups + threadIdx.x + u * kBlock), first[u]);
   }
 
   float mn_f = p.preset_min, mx_f = p.preset_max;
@@ -743,11 +722,10 @@ __global__ __launch_bounds__(kBlock) void ff_encode(const V* __restrict__ x, siz
   if (!(q.bin > 0)) return;  // CHECK_GT(bin, 0), fixing_float.h:71
 
   if (kVec) {
-    if (cnt > 0) {
-      const size_t g0 = (size_t)tfirst * kTileGroups + threadIdx.x;
-      encode_full_tile<V, NB>(first, q, p, out, g0, g0);
-      for (int64_t i = 1; i < cnt; ++i) {
-        const size_t gb = (size_t)(tfirst + i * tstep) * kTileGroups + threadIdx.x;
+    if (t0 < tf) {
+      encode_full_tile<V, NB>(first, q, p, out, t0 * kTileGroups + threadIdx.x, t0 * kTileGroups + threadIdx.x);
+      for (size_t t = t0 + 1; t < tf; ++t) {
+        const size_t gb = t * kTileGroups + threadIdx.x;
         V v[4][4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) Vec4<V>::load(x + 4 * (gb + u * kBlock), v[u]);
@@ -1315,13 +1293,8 @@ __device__ __forceinline__ int encode_batch_body(const FfBatchT<CAP>& B, uint32_
   return jb;
 }
 
-// PSF_ENC_BATCH_WAVES (A/B knob, tools/build_variants.sh): a minimum of waves
-// per SIMD for the plain batched encode (8: at most 64 registers)
-#ifndef PSF_ENC_BATCH_WAVES
-#define PSF_ENC_BATCH_WAVES 1
-#endif
 template <typename V, int NB, int CAP, bool kStored>
-__global__ __launch_bounds__(kBlock, kStored ? 1 : PSF_ENC_BATCH_WAVES) void ff_encode_batch(FfBatchT<CAP> B) {
+__global__ __launch_bounds__(kBlock) void ff_encode_batch(FfBatchT<CAP> B) {
   encode_batch_body<V, NB, CAP, kStored>(B, blockIdx.x, nullptr);
 }
 
@@ -1396,27 +1369,6 @@ __global__ __launch_bounds__(kBlock) void ff_fused_batch(FfBatchT<kBatchSmall> D
 }
 
 // ------------------------------------------------------------ launchers ----
-// PSF_ENC_STRIDED (A/B knob): 1 = the single-array encode sweeps its full
-// tiles with the whole grid (EncodeParams::strided)
-static bool enc_strided_mode() {
-  static const bool on = [] {
-    const char* e = getenv("PSF_ENC_STRIDED");
-    return e && *e == '1';
-  }();
-  return on;
-}
-// PSF_ENC_LDS (A/B knob): bytes of dynamic LDS each encode workgroup reserves
-// and never touches -- a cap on the encode's resident workgroups per CU
-// (160 KiB / pad), to measure how its streaming rate depends on occupancy
-static size_t enc_lds_pad() {
-  static const size_t v = [] {
-    const char* e = getenv("PSF_ENC_LDS");
-    const long b = e ? atol(e) : 0;
-    return b > 0 && b <= 65536 ? (size_t)b : (size_t)0;
-  }();
-  return v;
-}
-
 static inline void lcg_affine_pow(uint64_t k, uint32_t& A, uint32_t& Cc) {
   uint32_t a = kLcgA, c = kLcgC;
   A = 1u; Cc = 0u;
@@ -1503,7 +1455,6 @@ static void launch_encode(const V* x, size_t n, uint8_t* out, EncodeParams p, hi
   // Cache (smaller ones stay on chip whatever the order, and the reversed
   // order cost C3's 40 MB arrays 9 %: encode 15.8 -> 17.8 us, tools/ab_perm_c13.sh)
   p.reverse = kVec && p.partials && enc_perm_mode() && (double)n * sizeof(V) > 256.0 * (1 << 20) ? 1u : 0u;
-  p.strided = kVec && enc_strided_mode() ? 1u : 0u;
   lcg_affine_pow(4ull * kBlock, p.a_lane, p.c_lane);
   lcg_affine_pow(4ull * kTileGroups, p.a_tile, p.c_tile);
   lcg_affine_pow((uint64_t)grid * kBlock, p.a_thr, p.c_thr);
@@ -1515,7 +1466,7 @@ static void launch_encode(const V* x, size_t n, uint8_t* out, EncodeParams p, hi
     p.k17.c[k] &= kMask17;
   }
   p.lcg_pos = lcg_cycle().pos[p.seed & kMask17];
-  hipLaunchKernelGGL((ff_encode<V, NB, kVec>), dim3(grid), dim3(kBlock), enc_lds_pad(), st, x, n, out, p);
+  hipLaunchKernelGGL((ff_encode<V, NB, kVec>), dim3(grid), dim3(kBlock), 0, st, x, n, out, p);
 }
 
 template <typename V, bool kVec>
@@ -1667,9 +1618,9 @@ static void launch_encode_batch(FfBatchT<CAP>& B, uint32_t enc_total, hipStream_
   bool stored = false;
   for (int i = 0; i < B.njobs; ++i) stored |= (B.job[i].flags & kFlagStored) != 0;
   if (stored && (NB == 1 || NB == 2))
-    hipLaunchKernelGGL((ff_encode_batch<V, NB, CAP, true>), dim3(enc_total), dim3(kBlock), enc_lds_pad(), st, B);
+    hipLaunchKernelGGL((ff_encode_batch<V, NB, CAP, true>), dim3(enc_total), dim3(kBlock), 0, st, B);
   else
-    hipLaunchKernelGGL((ff_encode_batch<V, NB, CAP, false>), dim3(enc_total), dim3(kBlock), enc_lds_pad(), st, B);
+    hipLaunchKernelGGL((ff_encode_batch<V, NB, CAP, false>), dim3(enc_total), dim3(kBlock), 0, st, B);
 }
 
 static size_t tiles_of(size_t n) { return ((n >> 2) + kTileGroups - 1) / kTileGroups; }

@@ -672,7 +672,7 @@ int psf_node_roundtrip_ex(psf_node* snd, psf_node* rcv, const psf_message* const
     // each iteration's KEY_CACHING CRCs run on the side stream while the
     // previous iteration runs, and are collected when the iteration starts
     const psf::Message* t0 = iters ? &tmpls[0]->m : nullptr;
-    psf::PresignJob next = psf::presign_launch(&s, &t0, iters ? 1 : 0, true);
+    psf::PresignJob next = psf::presign_launch(&s, &t0, iters ? 1 : 0, true, true);
     for (int i = 0; i < iters; ++i) {
       psf::Message m = tmpls[i % ntmpl]->m;  // fresh Task + zero-copy buffers
       psf::Message* mp = &m;
@@ -680,7 +680,7 @@ int psf_node_roundtrip_ex(psf_node* snd, psf_node* rcv, const psf_message* const
       psf::presign_finish(next, &eh, &dh);
       if (i + 1 < iters) {  // the next iteration's CRCs, beside this one (side stream)
         const psf::Message* tn = &tmpls[(i + 1) % ntmpl]->m;
-        next = psf::presign_launch(&s, &tn, 1, true);
+        next = psf::presign_launch(&s, &tn, 1, true, false);
       }
       psf::encode_batch(&s, &mp, 1, &eh);  // = EncodeMessage, side-info left on the device
       psf::Message w = m;                  // delivered copy (van: Task frame + data frames)
@@ -795,7 +795,7 @@ int psf_nodes_roundtrip_opts(psf_node* const* snd, psf_node* const* rcv, const p
     // every KEY_CACHING CRC of an iteration (all phases): launched on the
     // context's side stream when the previous iteration starts, collected
     // when this one starts
-    psf::PresignJob next = psf::presign_launch(s.data(), tp.data(), iters ? n : 0, true);
+    psf::PresignJob next = psf::presign_launch(s.data(), tp.data(), iters ? n : 0, true, true);
     for (int it = 0; it < iters; ++it) {
       PSF_HPROF(14);
       {
@@ -806,7 +806,7 @@ int psf_nodes_roundtrip_opts(psf_node* const* snd, psf_node* const* rcv, const p
       }
       if (it + 1 < iters) {  // the next iteration's CRCs, beside this one (side stream)
         PSF_HPROF(13);
-        next = psf::presign_launch(s.data(), tp.data(), n, true);
+        next = psf::presign_launch(s.data(), tp.data(), n, true, false);
       }
       int b = 0;
       for (int e : ends) {  // phase [b, e): encode all, deliver, decode all

@@ -212,7 +212,11 @@ struct PresignJob {
   std::vector<int> next;  // per message: the next message of its buffer, or -1
   bool ahead = false;
 };
-PresignJob presign_launch(RemoteNode* const* nodes, const Message* const* msgs, int n, bool ahead);
+// after_main: the side stream first waits for the main stream's current
+// position (the first presign of a driver call: the keys may have been
+// written there); false for the later ones of the same call
+PresignJob presign_launch(RemoteNode* const* nodes, const Message* const* msgs, int n, bool ahead,
+                          bool after_main);
 void presign_finish(PresignJob& J, KeySigHint* enc, KeySigHint* dec);
 
 // Run the dequantise a deferred FIXING_FLOAT decode left pending (every

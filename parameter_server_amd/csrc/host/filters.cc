@@ -767,7 +767,8 @@ static void launch_signatures(RemoteNode* const* nodes, Message* const* msgs, co
   }
 }
 
-PresignJob presign_launch(RemoteNode* const* nodes, const Message* const* msgs, int n, bool ahead) {
+PresignJob presign_launch(RemoteNode* const* nodes, const Message* const* msgs, int n, bool ahead,
+                          bool after_main) {
   PresignJob J;
   J.bufs.reserve(n);
   J.next.assign(n, -1);
@@ -822,9 +823,11 @@ PresignJob presign_launch(RemoteNode* const* nodes, const Message* const* msgs, 
     len.clear();
     tk.clear();
     slot.clear();
-    // after what the main stream has queued so far (a decode or copy there
-    // may be producing these keys), not after the work queued from now on
-    hipStream_t side = ctx->side_stream_after_main();
+    // after_main: after what the main stream has queued so far (a decode or
+    // copy there may be producing these keys) -- the driver's first presign;
+    // its later ones read the same template keys, which nothing it queues
+    // writes, and stay free of the iterations in between
+    hipStream_t side = after_main ? ctx->side_stream_after_main() : ctx->side_stream();
     int s = Context::kPresignSlot0;
     for (PresignJob::Buf& b : J.bufs) {
       if (b.ctx != ctx) continue;
@@ -904,7 +907,7 @@ void presign_finish(PresignJob& J, KeySigHint* enc, KeySigHint* dec) {
 
 void presign_roundtrip(RemoteNode* const* nodes, const Message* const* msgs, int n, KeySigHint* enc,
                        KeySigHint* dec) {
-  PresignJob J = presign_launch(nodes, msgs, n, false);
+  PresignJob J = presign_launch(nodes, msgs, n, false, true);
   presign_finish(J, enc, dec);
 }
 
