@@ -11,8 +11,12 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <stdlib.h>
+
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <deque>
 #include <map>
 #include <memory>
 #include <string>
@@ -446,9 +450,18 @@ double psadapter_chain_bench(void* snd, void* rcv, int iters, int nmsg, const ui
                               voff[j + 1] > voff[j] ? val + voff[j] : nullptr, voff[j + 1] - voff[j], vt, nf, ftype,
                               fparam));
   double te = 0, td = 0;
+  // PSAD_FRESH=1: every round's messages in freshly allocated arrays (built
+  // outside the timed region), as an application that allocates a new
+  // gradient array per minibatch produces them; else the same arrays each round
+  const char* fe = getenv("PSAD_FRESH");
+  const bool fresh = fe && *fe == '1';
   try {
     for (int it = 0; it < iters; ++it)
       for (int j = 0; j < nmsg; ++j) {
+        if (fresh && it)
+          tm[j].reset(chain_msg(fl[j], ch, 0, ~0ull, key + koff[j], koff[j + 1] - koff[j],
+                                voff[j + 1] > voff[j] ? val + voff[j] : nullptr, voff[j + 1] - voff[j], vt, nf,
+                                ftype, fparam));
         Message a = *tm[j];  // the application's message (buffers shared, as KVVector::Push passes them)
         Peer* s = static_cast<Peer*>(dir[j] ? rcv : snd);
         Peer* r = static_cast<Peer*>(dir[j] ? snd : rcv);
@@ -468,5 +481,68 @@ double psadapter_chain_bench(void* snd, void* rcv, int iters, int nmsg, const ui
   *enc_s = te / iters;
   *dec_s = td / iters;
   return (te + td) / iters;
+}
+
+// The same rounds with the sender's encodes and the receiver's decodes on two
+// threads, as the reference runs them (EncodeMessage on the application
+// thread under Executor::Submit, DecodeMessage on the receiving executor's
+// thread, executor.cc:143,219): message k+1 is encoded while message k is
+// decoded, so H2D-heavy and D2H-heavy copies share the link in both
+// directions.  One direction only (every dir[j] == 0): a queue of at most
+// two encoded messages between the threads.  Returns seconds per round.
+double psadapter_chain_bench_pipelined(void* snd, void* rcv, int iters, int nmsg, const uint8_t* key,
+                                       const uint64_t* koff, const uint8_t* val, const uint64_t* voff, const int* fl,
+                                       int ch, int vt, int nf, const int* ftype, const int* fparam) {
+  std::vector<std::unique_ptr<Message>> tm;
+  for (int j = 0; j < nmsg; ++j)
+    tm.emplace_back(chain_msg(fl[j], ch, 0, ~0ull, key + koff[j], koff[j + 1] - koff[j],
+                              voff[j + 1] > voff[j] ? val + voff[j] : nullptr, voff[j + 1] - voff[j], vt, nf, ftype,
+                              fparam));
+  std::deque<Message> q;
+  std::mutex mu;
+  std::condition_variable cv;
+  bool failed = false;
+  const int total = iters * nmsg;
+  auto t0 = std::chrono::steady_clock::now();
+  std::thread enc([&] {
+    try {
+      for (int k = 0; k < total; ++k) {
+        Message a = *tm[k % nmsg];
+        static_cast<Peer*>(snd)->encode(&a);
+        std::unique_lock<std::mutex> l(mu);
+        cv.wait(l, [&] { return q.size() < 2 || failed; });
+        if (failed) return;
+        q.push_back(a);
+        cv.notify_all();
+      }
+    } catch (const std::exception& e) {
+      std::lock_guard<std::mutex> l(mu);
+      g_err = e.what();
+      failed = true;
+      cv.notify_all();
+    }
+  });
+  try {
+    for (int k = 0; k < total; ++k) {
+      Message w;
+      {
+        std::unique_lock<std::mutex> l(mu);
+        cv.wait(l, [&] { return !q.empty() || failed; });
+        if (failed) break;
+        w = q.front();
+        q.pop_front();
+        cv.notify_all();
+      }
+      static_cast<Peer*>(rcv)->decode(&w);
+    }
+  } catch (const std::exception& e) {
+    std::lock_guard<std::mutex> l(mu);
+    g_err = e.what();
+    failed = true;
+    cv.notify_all();
+  }
+  enc.join();
+  if (failed) return -1.0;
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() / iters;
 }
 }  // extern "C"

@@ -8,6 +8,12 @@ bench's metric) through encode + decode, H2D and D2H included.
 
   python tools/host_edge_chain.py [--out gpurun_out/host_edge_chain.jsonl]
 
+Each config runs warm twice first, then: "chain" (encode then decode, one
+thread), "chain_two_threads" (the encodes on one thread and the decodes on
+another, as the reference's application and executor threads run them;
+single-direction configs), "per_filter".  PSAD_FRESH=1: new arrays every
+round (an application allocating a new gradient array per minibatch).
+
 Configs: the ctr triple (C1: 10^5 keys, [KEY_CACHING(clear_cache_if_done),
 FIXING_FLOAT nb=1], pull request / pull response / push request), C2 on the
 host (2^27 f32, [FIXING_FLOAT nb=1]), C5 + COMPRESSING (2^20 keys x 128 f32
@@ -38,11 +44,14 @@ def harness():
     L.psadapter_chain_bench.argtypes = [vp, vp, C.c_int, C.c_int, vp, vp, vp, vp, vp, vp, C.c_int, C.c_int,
                                         C.c_int, vp, vp, C.POINTER(C.c_double), C.POINTER(C.c_double)]
     L.psadapter_chain_bench.restype = C.c_double
+    L.psadapter_chain_bench_pipelined.argtypes = [vp, vp, C.c_int, C.c_int, vp, vp, vp, vp, vp, C.c_int, C.c_int,
+                                                  C.c_int, vp, vp]
+    L.psadapter_chain_bench_pipelined.restype = C.c_double
     L.psadapter_last_error.restype = C.c_char_p
     return L
 
 
-def run(L, name, msgs, filters, iters, warm=1):
+def run(L, name, msgs, filters, iters, warm=2):
     """msgs: [(flags, dir, keys u8 array, values u8 array)]"""
     keys = [m[2] for m in msgs]
     vals = [m[3] for m in msgs]
@@ -68,9 +77,16 @@ def run(L, name, msgs, filters, iters, warm=1):
         a[2] = iters
         t = L.psadapter_chain_bench(*a)
         assert t > 0, L.psadapter_last_error()
+        out[mode] = {"gib_s": payload / t / 2**30, "s_per_round": t, "encode_s": e.value, "decode_s": d.value}
+        if mode == "chain" and not any(m[1] for m in msgs):
+            # the encodes and decodes on two threads (app thread / executor thread)
+            tp = L.psadapter_chain_bench_pipelined(W, S, iters, len(msgs), kbuf.ctypes.data, koff.ctypes.data,
+                                                   vbuf.ctypes.data, voff.ctypes.data, fl.ctypes.data, 1, 9,
+                                                   len(filters), ft.ctypes.data, fp.ctypes.data)
+            assert tp > 0, L.psadapter_last_error()
+            out["chain_two_threads"] = {"gib_s": payload / tp / 2**30, "s_per_round": tp}
         L.psadapter_peer_free(W)
         L.psadapter_peer_free(S)
-        out[mode] = {"gib_s": payload / t / 2**30, "s_per_round": t, "encode_s": e.value, "decode_s": d.value}
     return out
 
 
