@@ -168,7 +168,7 @@ def _router_worker(rank, world, port, q, native=False):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         ctx = F.HostContext()
-        ranges = shard.server_ranges(5)  # 5 servers over 2 ranks: blocks of 2 and 3
+        ranges = shard.server_ranges(5)  # 5 servers in blocks over the ranks (2 + 3 at world 2)
         ex = shard.NativeExchange.create(ctx, transport="host") if native else shard.SpillExchange(ctx)
         router = shard.PushRouter(ctx, ranges, rank, world, ex)
         sids = [10 * r + j for r in range(world) for j in range(3)]
@@ -213,25 +213,25 @@ def _router_worker(rank, world, port, q, native=False):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("native", [False, True])
-def test_push_router_gloo_world2_host(native):
-    """The native router (psf_router_*) across two ranks on CPU: 6 streams, 5
-    servers (2 on rank 0, 3 on rank 1), host keys, [KEY_CACHING]; every
-    server's decoded slices equal the restated slicing, on the miss and the
-    hit steps.  native: libpsf's exchange (records and data through the
-    node's mailbox, psf_router_step at world 2) instead of gloo's
-    all-to-all-v."""
+@pytest.mark.parametrize("world,native", [(2, False), (2, True), (4, True)])
+def test_push_router_gloo_world2_host(world, native):
+    """The native router (psf_router_*) across two (four) ranks on CPU: 3
+    streams per rank, 5 servers (in blocks over the ranks), host keys,
+    [KEY_CACHING]; every server's decoded slices equal the restated slicing,
+    on the miss and the hit steps.  native: libpsf's exchange (records and
+    data through the node's mailbox, psf_router_step at world 2 / 4, the last
+    three steps in one call) instead of gloo's all-to-all-v."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_router_worker, args=(r, 2, port, q, native)) for r in range(2)]
+    procs = [ctx.Process(target=_router_worker, args=(r, world, port, q, native)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=120) for _ in procs)
     for p in procs:
         p.join(timeout=60)
-    assert res == {0: True, 1: True}, res
+    assert res == {r: True for r in range(world)}, res
 
 
 def test_bench_launcher_gloo_world2():
