@@ -713,9 +713,9 @@ __global__ __launch_bounds__(kBlock) void ff_encode(const V* __restrict__ x, siz
       reinterpret_cast<int32_t*>(p.range_host)[2] = status;
     }
     if (p.pub) {  // side-info to the host while the grid keeps streaming
-      p.pub->range[0] = mn_f;
-      p.pub->range[1] = mx_f;
-      p.pub->status = status;
+      pub_store(&p.pub->range[0], mn_f);
+      pub_store(&p.pub->range[1], mx_f);
+      pub_store(&p.pub->status, (int32_t)status);
       publish_ticket(p.pub, p.ticket);
     }
   }
@@ -1223,9 +1223,9 @@ __device__ __forceinline__ int encode_batch_body(const FfBatchT<CAP>& B, uint32_
     }
     if (J.flags >> 16) {
       PubSlot* ps = B.pub + ((J.flags >> 16) - 1);
-      ps->range[0] = mn_f;
-      ps->range[1] = mx_f;
-      ps->status = status;
+      pub_store(&ps->range[0], mn_f);
+      pub_store(&ps->range[1], mx_f);
+      pub_store(&ps->status, (int32_t)status);
       publish_ticket(ps, J.ticket);
     }
   }
@@ -1466,7 +1466,7 @@ static void launch_encode(const V* x, size_t n, uint8_t* out, EncodeParams p, hi
     p.k17.c[k] &= kMask17;
   }
   p.lcg_pos = lcg_cycle().pos[p.seed & kMask17];
-  hipLaunchKernelGGL((ff_encode<V, NB, kVec>), dim3(grid), dim3(kBlock), 0, st, x, n, out, p);
+  psf_launch((ff_encode<V, NB, kVec>), dim3(grid), dim3(kBlock), 0, st, x, n, out, p);
 }
 
 template <typename V, bool kVec>
@@ -1508,17 +1508,17 @@ static int encode_typed(const V* x, size_t n, int nb, const FixedPoint& preset, 
                    ((reinterpret_cast<uintptr_t>(out) & (nb == 2 ? 7 : 3)) == 0);
   if (!(preset.has_min && preset.has_max)) {
     const int grid = vec ? tile_grid(n, kMinmaxGrid) : (ff_grid(n) < kMinmaxGrid ? ff_grid(n) : kMinmaxGrid);
-    ProfScope ps(prof, kKMinmax, st, (double)n * sizeof(V));
+    ProfScope ps(prof, kKMinmax, st, (double)n * sizeof(V), true);
     if (vec)
-      hipLaunchKernelGGL((ff_minmax_partials<V, true>), dim3(grid), dim3(kBlock), 0, st, x, n, partials,
+      psf_launch((ff_minmax_partials<V, true>), dim3(grid), dim3(kBlock), 0, st, x, n, partials,
                          enc_perm_mode() && (double)n * sizeof(V) > 256.0 * (1 << 20) ? 1u : 0u);
     else
-      hipLaunchKernelGGL((ff_minmax_partials<V, false>), dim3(grid), dim3(kBlock), 0, st, x, n, partials, 0u);
+      psf_launch((ff_minmax_partials<V, false>), dim3(grid), dim3(kBlock), 0, st, x, n, partials, 0u);
     p.partials = partials;
     p.nparts = grid;
     if (launch_status() != kOk) return kErrHip;
   }
-  ProfScope ps(prof, kKEncode, st, (double)n * (sizeof(V) + nb));
+  ProfScope ps(prof, kKEncode, st, (double)n * (sizeof(V) + nb), true);
   int s = vec ? dispatch_encode_nb<V, true>(x, n, nb, out, p, st)
               : dispatch_encode_nb<V, false>(x, n, nb, out, p, st);
   return s == kOk ? launch_status() : s;
@@ -1550,7 +1550,7 @@ static void launch_decode(const uint8_t* code, size_t n, V* out, const DecodePar
   const size_t tiles = ((n >> 2) + kTileGroups - 1) / kTileGroups;
   const int cap = tiles >= 2 * (size_t)kDecodeGridBig ? kDecodeGridBig : kStreamGrid;
   const int grid = (kVec && NB <= 3) ? tile_grid(n, cap) : ff_grid(n);
-  hipLaunchKernelGGL((ff_decode<V, NB, kVec>), dim3(grid), dim3(kBlock), 0, st, code, n, out, p);
+  psf_launch((ff_decode<V, NB, kVec>), dim3(grid), dim3(kBlock), 0, st, code, n, out, p);
 }
 
 template <typename V, bool kVec>
@@ -1579,7 +1579,7 @@ int ff_decode_launch(const void* code, size_t n, int value_type, int nb, const f
   const bool vec = ((oa & 15) == 0) && ((ca & (nb == 2 ? 7 : 3)) == 0);
   const uint8_t* c = static_cast<const uint8_t*>(code);
   const size_t vsz = value_type == kFloat ? 4 : 8;
-  ProfScope ps(prof, kKDecode, st, (double)n * (nb + vsz));
+  ProfScope ps(prof, kKDecode, st, (double)n * (nb + vsz), true);
   int s;
   if (value_type == kFloat) {
     float* o = static_cast<float*>(out);
@@ -1611,16 +1611,16 @@ template <typename V, int NB, int CAP>
 static void launch_encode_batch(FfBatchT<CAP>& B, uint32_t enc_total, hipStream_t st, Profiler* prof,
                                 double bytes_mm, double bytes_enc) {
   if (B.mm_total && !B.mm_total_done) {
-    ProfScope ps(prof, kKMinmax, st, bytes_mm);
-    hipLaunchKernelGGL((ff_minmax_batch<V, CAP>), dim3(B.mm_total), dim3(kBlock), 0, st, B);
+    ProfScope ps(prof, kKMinmax, st, bytes_mm, true);
+    psf_launch((ff_minmax_batch<V, CAP>), dim3(B.mm_total), dim3(kBlock), 0, st, B);
   }
-  ProfScope pe(prof, kKEncode, st, bytes_enc);
+  ProfScope pe(prof, kKEncode, st, bytes_enc, true);
   bool stored = false;
   for (int i = 0; i < B.njobs; ++i) stored |= (B.job[i].flags & kFlagStored) != 0;
   if (stored && (NB == 1 || NB == 2))
-    hipLaunchKernelGGL((ff_encode_batch<V, NB, CAP, true>), dim3(enc_total), dim3(kBlock), 0, st, B);
+    psf_launch((ff_encode_batch<V, NB, CAP, true>), dim3(enc_total), dim3(kBlock), 0, st, B);
   else
-    hipLaunchKernelGGL((ff_encode_batch<V, NB, CAP, false>), dim3(enc_total), dim3(kBlock), 0, st, B);
+    psf_launch((ff_encode_batch<V, NB, CAP, false>), dim3(enc_total), dim3(kBlock), 0, st, B);
 }
 
 static size_t tiles_of(size_t n) { return ((n >> 2) + kTileGroups - 1) / kTileGroups; }
@@ -1746,11 +1746,11 @@ static void launch_fused(const FfBatchT<kBatchSmall>& D, const FfBatchT<kBatchSm
                          FfFusedCtl* fc, bool stored) {
   if constexpr (NB == 1 || NB == 2) {
     if (stored) {
-      hipLaunchKernelGGL((ff_fused_batch<V, NB, true>), grid, dim3(kBlock), 0, st, D, B, fc->ctl);
+      psf_launch((ff_fused_batch<V, NB, true>), grid, dim3(kBlock), 0, st, D, B, fc->ctl);
       return;
     }
   }
-  hipLaunchKernelGGL((ff_fused_batch<V, NB, false>), grid, dim3(kBlock), 0, st, D, B, fc->ctl);
+  psf_launch((ff_fused_batch<V, NB, false>), grid, dim3(kBlock), 0, st, D, B, fc->ctl);
 }
 
 template <int CAP>
@@ -1852,7 +1852,7 @@ static int encode_batch_cap(int value_type, int nb, const FfArray* arrs, int cou
       for (int i = 0; i < count; ++i) stored |= (B.job[i].flags & kFlagStored) != 0;
       const dim3 grid(D.total + enc);  // (the min/max items run in the encode workgroups)
       {
-        ProfScope pf(prof, kKFused, st, bytes_dec + bytes_mm + bytes_enc);
+        ProfScope pf(prof, kKFused, st, bytes_dec + bytes_mm + bytes_enc, true);
         if (value_type == kFloat) {
           switch (nb) {
             case 1: launch_fused<float, 1>(D, B, grid, st, fused, stored); break;
@@ -1885,18 +1885,18 @@ static int encode_batch_cap(int value_type, int nb, const FfArray* arrs, int cou
       const FfBatchT<kBatchSmall>& M = B;
       const dim3 grid(D.total + M.mm_total);
       {
-        ProfScope pm(prof, kKDecodeMinmax, st, bytes_dec + bytes_mm);
+        ProfScope pm(prof, kKDecodeMinmax, st, bytes_dec + bytes_mm, true);
         if (value_type == kFloat) {
           switch (dec_nb) {
-            case 1: hipLaunchKernelGGL((ff_dec_mm_batch<float, 1>), grid, dim3(kBlock), 0, st, D, M); break;
-            case 2: hipLaunchKernelGGL((ff_dec_mm_batch<float, 2>), grid, dim3(kBlock), 0, st, D, M); break;
-            default: hipLaunchKernelGGL((ff_dec_mm_batch<float, 3>), grid, dim3(kBlock), 0, st, D, M); break;
+            case 1: psf_launch((ff_dec_mm_batch<float, 1>), grid, dim3(kBlock), 0, st, D, M); break;
+            case 2: psf_launch((ff_dec_mm_batch<float, 2>), grid, dim3(kBlock), 0, st, D, M); break;
+            default: psf_launch((ff_dec_mm_batch<float, 3>), grid, dim3(kBlock), 0, st, D, M); break;
           }
         } else {
           switch (dec_nb) {
-            case 1: hipLaunchKernelGGL((ff_dec_mm_batch<double, 1>), grid, dim3(kBlock), 0, st, D, M); break;
-            case 2: hipLaunchKernelGGL((ff_dec_mm_batch<double, 2>), grid, dim3(kBlock), 0, st, D, M); break;
-            default: hipLaunchKernelGGL((ff_dec_mm_batch<double, 3>), grid, dim3(kBlock), 0, st, D, M); break;
+            case 1: psf_launch((ff_dec_mm_batch<double, 1>), grid, dim3(kBlock), 0, st, D, M); break;
+            case 2: psf_launch((ff_dec_mm_batch<double, 2>), grid, dim3(kBlock), 0, st, D, M); break;
+            default: psf_launch((ff_dec_mm_batch<double, 3>), grid, dim3(kBlock), 0, st, D, M); break;
           }
         }
       }
@@ -1971,18 +1971,18 @@ static int decode_batch_cap(int value_type, int nb, const FfDecArray* arrs, int 
   const int fs = fill_decode_batch<CAP>(B, value_type, nb, arrs, count, &bytes, kBatchDecTpw);
   if (fs != kOk) return fs;
   const uint32_t wg = B.total;
-  ProfScope ps(prof, kKDecode, st, bytes);
+  ProfScope ps(prof, kKDecode, st, bytes, true);
   if (value_type == kFloat) {
     switch (nb) {
-      case 1: hipLaunchKernelGGL((ff_decode_batch<float, 1, CAP>), dim3(wg), dim3(kBlock), 0, st, B); break;
-      case 2: hipLaunchKernelGGL((ff_decode_batch<float, 2, CAP>), dim3(wg), dim3(kBlock), 0, st, B); break;
-      default: hipLaunchKernelGGL((ff_decode_batch<float, 3, CAP>), dim3(wg), dim3(kBlock), 0, st, B); break;
+      case 1: psf_launch((ff_decode_batch<float, 1, CAP>), dim3(wg), dim3(kBlock), 0, st, B); break;
+      case 2: psf_launch((ff_decode_batch<float, 2, CAP>), dim3(wg), dim3(kBlock), 0, st, B); break;
+      default: psf_launch((ff_decode_batch<float, 3, CAP>), dim3(wg), dim3(kBlock), 0, st, B); break;
     }
   } else {
     switch (nb) {
-      case 1: hipLaunchKernelGGL((ff_decode_batch<double, 1, CAP>), dim3(wg), dim3(kBlock), 0, st, B); break;
-      case 2: hipLaunchKernelGGL((ff_decode_batch<double, 2, CAP>), dim3(wg), dim3(kBlock), 0, st, B); break;
-      default: hipLaunchKernelGGL((ff_decode_batch<double, 3, CAP>), dim3(wg), dim3(kBlock), 0, st, B); break;
+      case 1: psf_launch((ff_decode_batch<double, 1, CAP>), dim3(wg), dim3(kBlock), 0, st, B); break;
+      case 2: psf_launch((ff_decode_batch<double, 2, CAP>), dim3(wg), dim3(kBlock), 0, st, B); break;
+      default: psf_launch((ff_decode_batch<double, 3, CAP>), dim3(wg), dim3(kBlock), 0, st, B); break;
     }
   }
   return launch_status();

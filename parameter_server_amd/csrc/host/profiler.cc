@@ -27,14 +27,43 @@ hipEvent_t Profiler::take() {
   return e;
 }
 
+void Profiler::pool_push(hipEvent_t e) {
+  if (npool_ + 1 > cappool_) {
+    cappool_ = cappool_ ? 2 * cappool_ : 128;
+    pool_ = static_cast<hipEvent_t*>(realloc(pool_, sizeof(hipEvent_t) * cappool_));
+  }
+  pool_[npool_++] = e;
+}
+
 void Profiler::begin(hipStream_t st) {
   cur_ = take();
   (void)hipEventRecord(cur_, st);
 }
 
+thread_local ExtEvents g_ext_events;
+
+void Profiler::begin_ext() {
+  cur_ = take();
+  cur_b_ = take();
+  g_ext_events = ExtEvents{cur_, cur_b_};
+}
+
 void Profiler::end(KernelId id, hipStream_t st, double alg_bytes) {
-  hipEvent_t b = take();
-  (void)hipEventRecord(b, st);
+  hipEvent_t b;
+  if (cur_b_) {
+    b = cur_b_;
+    cur_b_ = nullptr;
+    if (g_ext_events.a == cur_) {  // the scope launched nothing through psf_launch
+      g_ext_events = ExtEvents{};
+      pool_push(cur_);
+      pool_push(b);
+      cur_ = nullptr;
+      return;
+    }
+  } else {
+    b = take();
+    (void)hipEventRecord(b, st);
+  }
   if (npend_ == cap_) {
     cap_ = cap_ ? 2 * cap_ : 64;
     pend_ = static_cast<Pending*>(realloc(pend_, sizeof(Pending) * cap_));
@@ -53,12 +82,8 @@ void Profiler::collect() {
     launches[p.id] += 1;
     total_ms[p.id] += ms;
     bytes[p.id] += p.bytes;
-    if (npool_ + 2 > cappool_) {
-      cappool_ = cappool_ ? 2 * cappool_ : 128;
-      pool_ = static_cast<hipEvent_t*>(realloc(pool_, sizeof(hipEvent_t) * cappool_));
-    }
-    pool_[npool_++] = p.a;
-    pool_[npool_++] = p.b;
+    pool_push(p.a);
+    pool_push(p.b);
   }
   npend_ = 0;
 }

@@ -2,6 +2,7 @@
 // libpsf.  The public C ABI is include/psf.h.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stddef.h>
 #include <stdint.h>
 
@@ -42,8 +43,9 @@ struct FixedPoint {
 
 // Side-info a kernel publishes to host-mapped coherent memory as soon as it is
 // known (FIXING_FLOAT min/max + CHECK_GT(bin,0) outcome, KEY_CACHING CRC);
-// `ticket` is written last, behind a system-scope fence, so the host can act on
-// it while the rest of the kernel is still streaming.
+// `ticket` is written last, after the other fields' write-through stores
+// have drained, so the host can act on it while the rest of the kernel is
+// still streaming.
 struct PubSlot {
   float range[2];
   int32_t status;
@@ -54,9 +56,20 @@ struct PubSlot {
   uint64_t crc_ticket;   // KEY_CACHING: ticket << 32 | crc, one store
 };
 
+// A slot field written through to host memory (a system-scope store: the
+// write bypasses the XCD's L2 whatever the page's caching).
+template <typename T>
+__device__ __forceinline__ void pub_store(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// The ticket, after the fields this thread wrote with pub_store: draining them
+// (vmcnt: their write-through acknowledged) orders them before the ticket's
+// store.  No system-scope release: on MI355X that writes back and invalidates
+// the XCD's whole L2 (two buffer_wbl2 and a buffer_inv) in the middle of the
+// publishing workgroup, whose tiles then finish last.
 __device__ __forceinline__ void publish_ticket(PubSlot* s, uint32_t ticket) {
-  __threadfence_system();
-  __hip_atomic_store(&s->ticket, ticket, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __hip_atomic_store(&s->ticket, ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // a CRC and its ticket in one 8-byte system-scope store: nothing else needs
@@ -82,6 +95,9 @@ class Profiler {
     for (auto& s : seen_) s = 0;
   }
   void begin(hipStream_t st);
+  // arms g_ext_events for the scope's one launch (psf_launch): the kernel's
+  // own dispatch timestamps, no marker packets in the stream
+  void begin_ext();
   void end(KernelId id, hipStream_t st, double alg_bytes);
   void collect();  // waits for pending events, accumulates
   void reset();
@@ -92,10 +108,11 @@ class Profiler {
  private:
   struct Pending { KernelId id; hipEvent_t a, b; double bytes; };
   hipEvent_t take();
+  void pool_push(hipEvent_t e);
   uint32_t mask_ = 0;
   uint32_t stride_ = 1;
   uint64_t seen_[kKNum] = {0};
-  hipEvent_t cur_ = nullptr;
+  hipEvent_t cur_ = nullptr, cur_b_ = nullptr;
   Pending* pend_ = nullptr;
   int npend_ = 0, cap_ = 0;
   hipEvent_t* pool_ = nullptr;
@@ -105,12 +122,37 @@ class Profiler {
 // RAII bracket around one kernel launch
 struct ProfScope {
   Profiler* p; KernelId id; hipStream_t st; double bytes;
-  ProfScope(Profiler* p_, KernelId id_, hipStream_t st_, double bytes_)
+  // ext: the scope holds exactly one kernel launch, made through psf_launch,
+  // which takes its start / stop from the dispatch itself (hipExtLaunchKernel):
+  // a marker event pair costs the stream about 4 us per record on MI355X
+  // (two barrier packets around the kernel), which a 15 us kernel's step
+  // cannot hide (C3: 4.3 us gaps on both sides of the encode, kernel trace)
+  ProfScope(Profiler* p_, KernelId id_, hipStream_t st_, double bytes_, bool ext = false)
       : p(p_ && p_->sample(id_) ? p_ : nullptr), id(id_), st(st_), bytes(bytes_) {
-    if (p) p->begin(st);
+    if (p) {
+      if (ext) p->begin_ext();
+      else p->begin(st);
+    }
   }
   ~ProfScope() { if (p) p->end(id, st, bytes); }
 };
+
+// hipExtLaunchKernel's start / stop events armed by a ProfScope(ext) for the
+// next psf_launch on this thread
+struct ExtEvents { hipEvent_t a = nullptr, b = nullptr; };
+extern thread_local ExtEvents g_ext_events;
+
+template <typename F, typename... Args>
+inline void psf_launch(F kernel, dim3 grid, dim3 block, uint32_t shm, hipStream_t st, Args... args) {
+  ExtEvents& e = g_ext_events;
+  if (e.a) {
+    hipEvent_t a = e.a, b = e.b;
+    e.a = e.b = nullptr;
+    hipExtLaunchKernelGGL(kernel, grid, block, shm, st, a, b, 0u, args...);
+  } else {
+    hipLaunchKernelGGL(kernel, grid, block, shm, st, args...);
+  }
+}
 
 // ff_codec.hip
 double ff_ratio(int nb);

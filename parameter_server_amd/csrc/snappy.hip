@@ -984,9 +984,9 @@ __global__ __launch_bounds__(kScanT) void snappy_scan(const SnappyCJobs J) {
   }
   if (tid == 0 && J.pub) {
     PubSlot* pub = J.pub + c.slot;
-    pub->size = s_base;
-    pub->status = kOk;
-    pub->pad = in_place ? kStoredInPlace : 0u;
+    pub_store(&pub->size, (uint64_t)s_base);
+    pub_store(&pub->status, (int32_t)kOk);
+    pub_store(&pub->pad, in_place ? (uint32_t)kStoredInPlace : 0u);
     publish_ticket(pub, c.ticket);
   }
 }
@@ -1046,9 +1046,9 @@ __global__ __launch_bounds__(kPlaceT) void snappy_place(const SnappyCJobs J, con
       c.dst[tid] = (uint8_t)(((uint32_t)c.n >> (7 * tid)) | (tid + 1 < c.hdr ? 128u : 0u));
     if (k + 1 == c.nfrag && tid == 0 && J.pub) {
       PubSlot* pub = J.pub + c.slot;
-      pub->size = off + frag_len(info, len);
-      pub->status = kOk;
-      pub->pad = in_place ? kStoredInPlace : 0u;
+      pub_store(&pub->size, (uint64_t)(off + frag_len(info, len)));
+      pub_store(&pub->status, (int32_t)kOk);
+      pub_store(&pub->pad, in_place ? (uint32_t)kStoredInPlace : 0u);
       publish_ticket(pub, c.ticket);
     }
     if (in_place) return;  // FIXING_FLOAT wrote the stream, header and tags included
@@ -1786,8 +1786,8 @@ __global__ __launch_bounds__(256) void snappy_dspec(const SnappyDJobs J) {
       flags[1] = 1;
       flags[2] = 1;  // decoded: the kernels after this one have nothing to do
       if (pub) {
-        pub->status = kOk;
-        pub->size = dsize;
+        pub_store(&pub->status, (int32_t)kOk);
+        pub_store(&pub->size, (uint64_t)dsize);
         publish_ticket(pub, ticket);
       }
     }
@@ -2430,8 +2430,8 @@ __device__ void dserial_body(const uint8_t* __restrict__ in, uint64_t C, uint32_
 }
 __device__ void dverdict(uint32_t f, uint64_t dsize, PubSlot* pub, uint32_t ticket) {
   if (pub) {
-    pub->status = (f & kFlagHeader) ? kErrHeaderHint : (f & kFlagInvalid) ? kErrCheck : kOk;
-    pub->size = dsize;
+    pub_store(&pub->status, (int32_t)((f & kFlagHeader) ? kErrHeaderHint : (f & kFlagInvalid) ? kErrCheck : kOk));
+    pub_store(&pub->size, (uint64_t)dsize);
     publish_ticket(pub, ticket);
   }
 }
