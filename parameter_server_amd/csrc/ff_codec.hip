@@ -1112,7 +1112,8 @@ __global__ __launch_bounds__(kBlock) void ff_minmax_batch(FfBatchT<CAP> B) {
 // fused: ff_fused_batch's counter lines (this array's min/max items are folded
 // by its encode workgroups in the same launch); returns the job
 template <typename V, int NB, int CAP, bool kStored>
-__device__ __forceinline__ int encode_batch_body(const FfBatchT<CAP>& B, uint32_t block, uint32_t* fused) {
+__device__ __forceinline__ int encode_batch_body(const FfBatchT<CAP>& B, uint32_t block, uint32_t* fused,
+                                                 int32_t* sticky = nullptr) {
   const int jb = batch_job(B, block, false);
   const FfJob& J = B.job[jb];
   const V* __restrict__ x = static_cast<const V*>(J.x);
@@ -1229,6 +1230,7 @@ __device__ __forceinline__ int encode_batch_body(const FfBatchT<CAP>& B, uint32_
       publish_ticket(ps, J.ticket);
     }
   }
+  if (late && sticky && threadIdx.x == 0) pub_store(sticky, (int32_t)kErrHip);  // Context::sync throws
   if (!(q.bin > 0) || late) return jb;  // CHECK_GT(bin, 0), fixing_float.h:71
 
   EncodeParams p{};  // the per-launch constants the tile code reads
@@ -1349,12 +1351,13 @@ __global__ __launch_bounds__(kBlock) void ff_dec_mm_batch(FfBatchT<kBatchSmall> 
 // hand-off above); the last of an array's workgroups to finish zeroes its
 // counter line.
 template <typename V, int NB, bool kStored>
-__global__ __launch_bounds__(kBlock) void ff_fused_batch(FfBatchT<kBatchSmall> D, FfBatchT<kBatchSmall> B, uint32_t* ctl) {
+__global__ __launch_bounds__(kBlock) void ff_fused_batch(FfBatchT<kBatchSmall> D, FfBatchT<kBatchSmall> B, uint32_t* ctl,
+                                                         int32_t* sticky) {
   if (blockIdx.x < D.total) {
     decode_batch_body<V, NB, kBatchSmall>(D, blockIdx.x);
     return;
   }
-  const int jb = encode_batch_body<V, NB, kBatchSmall, kStored>(B, blockIdx.x - D.total, ctl);
+  const int jb = encode_batch_body<V, NB, kBatchSmall, kStored>(B, blockIdx.x - D.total, ctl, sticky);
   if (B.job[jb].mm_nwg) {
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1448,13 +1451,8 @@ static int tile_grid(size_t n, int cap) {
 
 static bool enc_perm_mode();
 
-template <typename V, int NB, bool kVec>
-static void launch_encode(const V* x, size_t n, uint8_t* out, EncodeParams p, hipStream_t st) {
-  const int grid = kVec ? tile_grid(n, kStreamGrid) : ff_grid(n);
-  // after a strided min/max pass over an array larger than the Infinity
-  // Cache (smaller ones stay on chip whatever the order, and the reversed
-  // order cost C3's 40 MB arrays 9 %: encode 15.8 -> 17.8 us, tools/ab_perm_c13.sh)
-  p.reverse = kVec && p.partials && enc_perm_mode() && (double)n * sizeof(V) > 256.0 * (1 << 20) ? 1u : 0u;
+// the LCG jump constants of an encode launch over `grid` workgroups
+static void encode_lcg_params(EncodeParams& p, int grid) {
   lcg_affine_pow(4ull * kBlock, p.a_lane, p.c_lane);
   lcg_affine_pow(4ull * kTileGroups, p.a_tile, p.c_tile);
   lcg_affine_pow((uint64_t)grid * kBlock, p.a_thr, p.c_thr);
@@ -1466,6 +1464,16 @@ static void launch_encode(const V* x, size_t n, uint8_t* out, EncodeParams p, hi
     p.k17.c[k] &= kMask17;
   }
   p.lcg_pos = lcg_cycle().pos[p.seed & kMask17];
+}
+
+template <typename V, int NB, bool kVec>
+static void launch_encode(const V* x, size_t n, uint8_t* out, EncodeParams p, hipStream_t st) {
+  const int grid = kVec ? tile_grid(n, kStreamGrid) : ff_grid(n);
+  // after a strided min/max pass over an array larger than the Infinity
+  // Cache (smaller ones stay on chip whatever the order, and the reversed
+  // order cost C3's 40 MB arrays 9 %: encode 15.8 -> 17.8 us, tools/ab_perm_c13.sh)
+  p.reverse = kVec && p.partials && enc_perm_mode() && (double)n * sizeof(V) > 256.0 * (1 << 20) ? 1u : 0u;
+  encode_lcg_params(p, grid);
   psf_launch((ff_encode<V, NB, kVec>), dim3(grid), dim3(kBlock), 0, st, x, n, out, p);
 }
 
@@ -1746,11 +1754,11 @@ static void launch_fused(const FfBatchT<kBatchSmall>& D, const FfBatchT<kBatchSm
                          FfFusedCtl* fc, bool stored) {
   if constexpr (NB == 1 || NB == 2) {
     if (stored) {
-      psf_launch((ff_fused_batch<V, NB, true>), grid, dim3(kBlock), 0, st, D, B, fc->ctl);
+      psf_launch((ff_fused_batch<V, NB, true>), grid, dim3(kBlock), 0, st, D, B, fc->ctl, fc->sticky);
       return;
     }
   }
-  psf_launch((ff_fused_batch<V, NB, false>), grid, dim3(kBlock), 0, st, D, B, fc->ctl);
+  psf_launch((ff_fused_batch<V, NB, false>), grid, dim3(kBlock), 0, st, D, B, fc->ctl, fc->sticky);
 }
 
 template <int CAP>

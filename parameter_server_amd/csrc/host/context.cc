@@ -339,6 +339,13 @@ Context::Context(int device, hipStream_t stream, int mode) : device_(device), st
   PSF_HIP_CHECK(hipMemset(zero_base_, 0, 2 * (kZeroBytes[0] + kZeroBytes[1])));
   PSF_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&fused_.ctl), kFusedCtlBytes));
   PSF_HIP_CHECK(hipMemset(fused_.ctl, 0, kFusedCtlBytes));
+  PSF_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&sticky_h_), 64, hipHostMallocMapped | hipHostMallocCoherent));
+  memset(sticky_h_, 0, 64);
+  {
+    void* d = nullptr;
+    PSF_HIP_CHECK(hipHostGetDevicePointer(&d, sticky_h_, 0));
+    fused_.sticky = static_cast<int32_t*>(d);
+  }
   PSF_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&d_slots_), sizeof(Slot) * kSlots));
   PSF_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_slots_), sizeof(Slot) * kSlots,
                               hipHostMallocMapped | hipHostMallocCoherent));
@@ -384,6 +391,7 @@ Context::~Context() {
   (void)hipFree(d_partials_);
   (void)hipFree(zero_base_);
   (void)hipFree(fused_.ctl);
+  if (sticky_h_) (void)hipHostFree(sticky_h_);
   (void)hipFree(d_slots_);
   (void)hipHostFree(h_slots_);
   // a private stream's cached blocks go now (buffers still held by messages
@@ -550,8 +558,25 @@ uint32_t Context::wait_crc(int i, uint32_t ticket) {
 
 void Context::sync() {
   if (device_ < 0) return;
-  WaitTimer wt(this, kWaitSync);
-  PSF_HIP_CHECK(hipStreamSynchronize(stream_));
+  {
+    WaitTimer wt(this, kWaitSync);
+    PSF_HIP_CHECK(hipStreamSynchronize(stream_));
+  }
+  check_sticky();
+}
+
+void Context::check_sticky() {
+  if (sticky_h_ && __atomic_load_n(sticky_h_, __ATOMIC_ACQUIRE) != 0) handoff_failed();
+}
+
+void Context::handoff_failed() {
+  // the launch may still be running: let it finish so that every workgroup
+  // that gave up has set the sticky word, then take the word and clean the
+  // counter lines for the next launch
+  (void)hipStreamSynchronize(stream_);
+  if (sticky_h_) __atomic_store_n(sticky_h_, 0, __ATOMIC_RELEASE);
+  reset_fused();
+  throw CheckError(kErrHip, "FIXING_FLOAT: in-launch min/max hand-off timed out");
 }
 
 void RangeBatch::resolve(bool synced) {
@@ -619,10 +644,7 @@ void Context::check_ranges() {
       late |= (int32_t)rb->host[i] == kErrHip;
     }
   }
-  if (late) {
-    reset_fused();
-    throw CheckError(kErrHip, "FIXING_FLOAT: in-launch min/max hand-off timed out");
-  }
+  if (late) handoff_failed();
   if (bad) throw CheckError(kErrBin, "CHECK_GT(bin, 0)");
 }
 

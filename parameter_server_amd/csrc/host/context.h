@@ -171,6 +171,12 @@ class Context {
   // the same for a CRC published with its ticket in one word; returns the CRC
   uint32_t wait_crc(int i, uint32_t ticket);
   void sync();
+  // throws kErrHip (once) if a kernel of this context gave up an in-launch
+  // hand-off since the last check; sync() calls it after the stream drains
+  void check_sticky();
+  // an in-launch hand-off gave up: drain the stream, take the sticky word,
+  // clean the counters, throw kErrHip
+  [[noreturn]] void handoff_failed();
   // spin until `e` has completed; the time is counted as wait `w`
   void wait_event(hipEvent_t e, int w);
   // stage a host buffer into HBM (used at the host edge)
@@ -188,7 +194,9 @@ class Context {
   static constexpr uint64_t kLazyRing = 1u << 15;
   float* claim_lazy(const std::shared_ptr<RangeBatch>& rb, int n);
   void check_ranges();
-  void sync_checked() { sync(); check_ranges(); }
+  // (the ranges first: a sticky hand-off error thrown by sync() must not leave
+  // the tracked ranges behind for the next check)
+  void sync_checked() { check_ranges(); sync(); }
 
   std::mutex& mu() { return mu_; }
   Profiler* prof() { return &prof_; }
@@ -267,6 +275,7 @@ class Context {
   std::vector<hipEvent_t> events_;
   void* zero_base_ = nullptr;
   FfFusedCtl fused_;
+  int32_t* sticky_h_ = nullptr;  // fused_.sticky's host side
   int zero_parity_[kZeroKinds] = {0, 0};
   Buffer noise_f32_, noise_f64_;
   std::mutex mu_;

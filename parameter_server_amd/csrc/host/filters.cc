@@ -372,10 +372,7 @@ void FixingFloatFilter::encode_messages(Context* ctx, std::vector<FfMessage>& ms
         const Slot& hs = *ctx->pub_host((int)(q - base));
         if (!j.fp->has_min) j.fp->set_min(hs.range[0]);
         if (!j.fp->has_max) j.fp->set_max(hs.range[1]);
-        if (hs.status == kErrHip) {
-          ctx->reset_fused();
-          throw CheckError(kErrHip, "FIXING_FLOAT: in-launch min/max hand-off timed out");
-        }
+        if (hs.status == kErrHip) ctx->handoff_failed();
         if (hs.status != kOk) throw CheckError(kErrBin, "CHECK_GT(bin, 0)");
       } else if (lazy_idx[q - base] >= 0) {
         j.fp->pending = rb;
@@ -403,7 +400,7 @@ void FixedFloatConfig::settle() {
   pending_idx = -1;
   pending_min = pending_max = false;
   if ((int32_t)r[2] == kErrHip) {
-    if (rb->ctx) rb->ctx->reset_fused();
+    if (rb->ctx) rb->ctx->handoff_failed();
     throw CheckError(kErrHip, "FIXING_FLOAT: in-launch min/max hand-off timed out");
   }
   if ((int32_t)r[2] != kOk) throw CheckError(kErrBin, "CHECK_GT(bin, 0)");

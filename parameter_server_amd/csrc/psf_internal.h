@@ -194,6 +194,9 @@ struct FfDecArray {
 constexpr int kFusedArrays = 64;  // = kBatchSmall (ff_codec.hip)
 struct FfFusedCtl {
   uint32_t* ctl = nullptr;
+  // host-mapped word a workgroup whose hand-off gave up sets to kErrHip
+  // (the array's status can only carry workgroup 0's verdict)
+  int32_t* sticky = nullptr;
 };
 constexpr size_t kFusedCtlBytes = 128 * kFusedArrays;
 bool ff_batchable(const void* x, const void* out, size_t n, int nb, int value_type, bool encode);
