@@ -313,8 +313,12 @@ constexpr SkipCum make_skip() {
   }
   return s;
 }
+// bytes allocated after a stored stream: the compressor's aligned reads past a
+// fragment's end (64), and the room an in-place compressed stream may grow
+// into (snappy.hip kShiftMax)
+constexpr uint32_t kStoredSlack = 192;
 __host__ __device__ __forceinline__ uint64_t stored_alloc_bytes(const StoredLayout& s) {
-  return stored_stream_bytes(s) + 64;  // the compressor's aligned reads past a fragment's end
+  return stored_stream_bytes(s) + kStoredSlack;
 }
 
 // the stream byte at P, a header / tag byte before fragment k's data

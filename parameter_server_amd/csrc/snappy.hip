@@ -293,8 +293,21 @@ struct SnappyCJobs {
   uint32_t njobs, nfrag;
   uint64_t* finfo;     // per fragment: op (tag bytes) << 32 | next_emit (start of the final literal)
   uint64_t* offset;    // per fragment: its offset in the stream (K-scan)
-  uint32_t* in_place;  // per job (K-scan streams): every fragment stored, the stream left in `in`
+  uint32_t* in_place;  // per job (K-scan streams): a PlaceMode
+  uint8_t* stash;      // per fragment of a stored job: its first kStash bytes (K-probe)
 };
+// How K-place treats a stream.  A stored job (FIXING_FLOAT wrote the stored
+// layout) whose fragments all come out stored is the result as it stands.  If
+// some carry tags and every fragment's new start lies 0..kShiftMax bytes after
+// its stored one (the usual case on codes: a fragment with one 4-byte match
+// comes out 2 bytes longer than a literal), the stream is rewritten in place:
+// fragments before the first one with tags stay, the later ones move right,
+// each read whole before it is written.  Otherwise the stream is placed into
+// the job's dst.
+enum PlaceMode : uint32_t { kPlaceCopy = 0, kPlaceStored = 1, kPlaceShift = 2 };
+constexpr uint32_t kStash = 64;
+constexpr int64_t kShiftMax = 64;
+static_assert(kStoredSlack >= 64 + kShiftMax + 8, "the stored stream's room for growth and the stash reads");
 // fragment k's input bytes: consecutive 64 KiB blocks, or in a stored job the
 // fragment's literal in the StoredLayout stream
 __device__ __forceinline__ const uint8_t* frag_src(const CJob& c, uint32_t k) {
@@ -845,7 +858,13 @@ __global__ __launch_bounds__(kCThreads) void snappy_parse(const SnappyCJobs J, u
         const CJob& c = cjob_of(J, f);
         const size_t start = (size_t)(f - c.frag0) * kFrag;
         const uint32_t len = (uint32_t)min((size_t)kFrag, c.n - start);
-        need = !probe_stored(frag_src(c, f - c.frag0), len, skip, U.q.map[wave], U.q.val[wave], lane);
+        const uint8_t* g = frag_src(c, f - c.frag0);
+        // a stored job's fragment may be moved in place by K-place, whose
+        // left neighbour can overwrite its first bytes before it reads them:
+        // keep them (the stream has kStoredSlack bytes after its end)
+        if (c.stored && lane < kStash / 4)
+          reinterpret_cast<uint32_t*>(J.stash + (size_t)f * kStash)[lane] = gld32(g, 4 * lane);
+        need = !probe_stored(g, len, skip, U.q.map[wave], U.q.val[wave], lane);
         if (!need && lane == 0) J.finfo[f] = 0;  // no tags, the final literal from byte 0
         PSF_TRACE_T(f, 4, wave * 64);
       }
@@ -939,10 +958,15 @@ __global__ __launch_bounds__(kCThreads) void snappy_parse(const SnappyCJobs J, u
 // header + the exclusive sum of the fragment lengths; the stream length is
 // published to the host (the bytes are in place once K-place has run).
 constexpr uint32_t kScanT = 1024;
+// how far fragment k's new start lies after its stored one (a stored job)
+__device__ __forceinline__ int64_t stored_shift(const CJob& c, uint32_t k, uint64_t off) {
+  return (int64_t)off - (int64_t)stored_frag_tag(stored_layout((uint32_t)c.n), k);
+}
 __global__ __launch_bounds__(kScanT) void snappy_scan(const SnappyCJobs J) {
   __shared__ uint64_t wsum[kScanT / 64];
   __shared__ uint64_t s_base;
   __shared__ uint32_t s_any;
+  __shared__ int64_t s_lo[kScanT / 64], s_hi[kScanT / 64];
   const CJob& c = J.j[blockIdx.x];
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   if (tid == 0) {
@@ -954,11 +978,7 @@ __global__ __launch_bounds__(kScanT) void snappy_scan(const SnappyCJobs J) {
   for (uint32_t k = tid; k < c.nfrag; k += kScanT) any |= J.finfo[c.frag0 + k] != 0 ? 1u : 0u;
   if (any) s_any = 1;
   __syncthreads();
-  // a stored job whose fragments all came out stored: the stream FIXING_FLOAT
-  // wrote is the result (header and tags included); nothing moves
-  const bool in_place = c.stored && !s_any;
-  if (tid == 0) J.in_place[blockIdx.x] = in_place ? 1u : 0u;
-  if (!in_place && tid < c.hdr) c.dst[tid] = (uint8_t)(((uint32_t)c.n >> (7 * tid)) | (tid + 1 < c.hdr ? 128u : 0u));
+  int64_t lo = 0, hi = 0;  // the fragments' shifts (kPlaceShift's bounds)
   for (uint32_t k0 = 0; k0 < c.nfrag; k0 += kScanT) {
     const uint32_t k = k0 + tid;
     uint64_t v = 0;
@@ -977,32 +997,106 @@ __global__ __launch_bounds__(kScanT) void snappy_scan(const SnappyCJobs J) {
     __syncthreads();
     uint64_t before = s_base;
     for (uint32_t q = 0; q < wave; ++q) before += wsum[q];
-    if (k < c.nfrag) J.offset[c.frag0 + k] = before + x - v;
+    if (k < c.nfrag) {
+      J.offset[c.frag0 + k] = before + x - v;
+      if (c.stored) {
+        const int64_t d = stored_shift(c, k, before + x - v);
+        lo = min(lo, d);
+        hi = max(hi, d);
+      }
+    }
     __syncthreads();
     if (tid == kScanT - 1) s_base = before + x;
     __syncthreads();
   }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = min(lo, (int64_t)__shfl_xor(lo, o, 64));
+    hi = max(hi, (int64_t)__shfl_xor(hi, o, 64));
+  }
+  if (lane == 0) {
+    s_lo[wave] = lo;
+    s_hi[wave] = hi;
+  }
+  __syncthreads();
+  for (uint32_t w = 0; w < kScanT / 64; ++w) {
+    lo = min(lo, s_lo[w]);
+    hi = max(hi, s_hi[w]);
+  }
+  // (the stream's end: its growth must fit the stored stream's slack)
+  const int64_t grow = c.stored ? (int64_t)s_base - (int64_t)stored_stream_bytes(stored_layout((uint32_t)c.n)) : 0;
+  const uint32_t mode = !c.stored ? kPlaceCopy
+                        : !s_any  ? kPlaceStored
+                        : (lo >= 0 && hi <= kShiftMax && grow >= 0 && grow <= kShiftMax) ? kPlaceShift
+                                                                                        : kPlaceCopy;
+  if (tid == 0) J.in_place[blockIdx.x] = mode;
+  if (mode == kPlaceCopy && tid < c.hdr) c.dst[tid] = (uint8_t)(((uint32_t)c.n >> (7 * tid)) | (tid + 1 < c.hdr ? 128u : 0u));
   if (tid == 0 && J.pub) {
     PubSlot* pub = J.pub + c.slot;
     pub_store(&pub->size, (uint64_t)s_base);
     pub_store(&pub->status, (int32_t)kOk);
-    pub_store(&pub->pad, in_place ? (uint32_t)kStoredInPlace : 0u);
+    pub_store(&pub->pad, mode != kPlaceCopy ? (uint32_t)kStoredInPlace : 0u);
     publish_ticket(pub, c.ticket);
   }
 }
 
 // ---- K-place: one workgroup of 256 per fragment
 constexpr uint32_t kPlaceT = 256;
+constexpr int kMoveRows = 17;  // rows of 63 16-byte chunks per wave: 17 x 4 x 63 x 16 >= 64 KiB
+
+// A fragment rewritten in place (kPlaceShift): at d its op tag bytes from tg,
+// then the literal tag and the literal s[0, lit) -- s lies below its new
+// place by at most kShiftMax bytes, so every byte of s is loaded before the
+// workgroup's barrier and stored after it (lane l of a wave loads the aligned
+// block under destination chunk l of its row of 63, as copy_bytes).
+__device__ void place_moved(uint8_t* d, const uint8_t* tg, uint32_t op, const uint8_t* s, uint32_t lit, uint32_t tid) {
+  constexpr uint32_t W = kPlaceT / 64;
+  const uint32_t lane = tid & 63, wv = tid >> 6;
+  uint8_t* dl = d + op + (lit ? lit_tag_len(lit - 1) : 0);
+  const uint32_t head = min(lit, (uint32_t)(-reinterpret_cast<uintptr_t>(dl) & 15));
+  const uint32_t nc = (lit - head) >> 4;
+  const uint32_t t0 = head + 16 * nc;
+  const uint8_t hb = tid < head ? s[tid] : 0;
+  const uint8_t tb = tid < lit - t0 ? s[t0 + tid] : 0;
+  const uintptr_t sp = reinterpret_cast<uintptr_t>(s + head);
+  typedef uint32_t V4 __attribute__((ext_vector_type(4)));
+  const auto s16 = gbl<V4>(reinterpret_cast<const void*>(sp & ~(uintptr_t)15));
+  const uint32_t sh = (uint32_t)(sp & 15);
+  const uint32_t lim = nc + (sh ? 1u : 0u);
+  uint4 lo[kMoveRows];
+#pragma unroll
+  for (int u = 0; u < kMoveRows; ++u) {
+    const uint32_t c = (u * W + wv) * 63 + lane;
+    V4 x = {0, 0, 0, 0};
+    if (c < lim) x = s16[c];
+    lo[u] = make_uint4(x[0], x[1], x[2], x[3]);
+  }
+  __syncthreads();  // every byte of s is in registers
+  if (op) copy_bytes<kPlaceT>(d, tg, op, tid);
+  if (lit) literal_tag(d + op, lit, tid);
+  if (tid < head) dl[tid] = hb;
+  uint4* d16 = reinterpret_cast<uint4*>(dl + head);
+#pragma unroll
+  for (int u = 0; u < kMoveRows; ++u) {
+    const uint32_t c = (u * W + wv) * 63 + lane;
+    const uint4 hi = shfl_down1(lo[u]);
+    if (lane < 63 && c < nc) d16[c] = funnel16(lo[u], hi, sh);
+    __builtin_amdgcn_sched_barrier(0);  // (one row's neighbour blocks live at a time)
+  }
+  if (tid < lit - t0) dl[t0 + tid] = tb;
+}
 
 // Streams of up to kInlineScan fragments need no K-scan: the workgroup of
-// fragment k sums the lengths of fragments 0..k-1 (all full) itself, the
-// workgroup of fragment 0 writes the varint header and the last fragment's
-// publishes the stream length.
+// fragment k sums the lengths of the stream's fragments itself (all full but
+// the last), the workgroup of fragment 0 writes the varint header and the last
+// fragment's publishes the stream length.
 constexpr uint32_t kInlineScan = 4096;
 __global__ __launch_bounds__(kPlaceT) void snappy_place(const SnappyCJobs J, const uint8_t* __restrict__ scratch) {
   __shared__ uint64_t s_part[kPlaceT / 64];
+  __shared__ int64_t s_tot[kPlaceT / 64];
+  __shared__ int64_t s_lo[kPlaceT / 64], s_hi[kPlaceT / 64];
   __shared__ uint32_t s_any[kPlaceT / 64];
-  const uint32_t f = blockIdx.x, tid = threadIdx.x;
+  const uint32_t f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t ji = cjob_index(J, f);
   const CJob& c = J.j[ji];
   const uint32_t k = f - c.frag0;
@@ -1012,27 +1106,36 @@ __global__ __launch_bounds__(kPlaceT) void snappy_place(const SnappyCJobs J, con
   const uint32_t op = (uint32_t)(info >> 32), ne = (uint32_t)info;
   PSF_TRACE(f, 2);
   uint64_t off;
+  uint32_t mode;
   if (J.offset) {
-    if (J.in_place[ji]) return;  // K-scan found every fragment stored: the stream is in place
+    mode = J.in_place[ji];
+    if (mode == kPlaceStored) return;  // K-scan found every fragment stored: the stream is in place
     off = J.offset[f];
   } else {
-    // the lengths of the fragments before this one (all full), and -- for a
-    // stored job -- whether any fragment of the stream has tags
+    // thread t takes fragments [t q, t q + q): their lengths before this
+    // fragment, whether any has tags, and (a stored job) how much longer than
+    // stored they come out -- whose prefix sums are the fragments' shifts
+    const uint32_t q = (c.nfrag + kPlaceT - 1) / kPlaceT;
+    const uint32_t i0 = min(c.nfrag, tid * q), i1 = min(c.nfrag, i0 + q);
     uint64_t part = 0;
     uint32_t any = 0;
-    for (uint32_t i = tid; i < c.nfrag; i += kPlaceT) {
+    int64_t tot = 0;
+    for (uint32_t i = i0; i < i1; ++i) {
       const uint64_t fi = J.finfo[c.frag0 + i];
-      if (i < k) part += frag_len(fi, kFrag);
+      const uint32_t li = (uint32_t)min((size_t)kFrag, c.n - (size_t)i * kFrag);
+      const uint32_t fl = frag_len(fi, li);
+      if (i < k) part += fl;
       any |= fi != 0 ? 1u : 0u;
+      tot += (int64_t)fl - (int64_t)frag_len(0, li);
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
       part += __shfl_xor(part, o, 64);
       any |= __shfl_xor(any, o, 64);
     }
-    if ((tid & 63) == 0) {
-      s_part[tid >> 6] = part;
-      s_any[tid >> 6] = any;
+    if (lane == 0) {
+      s_part[wave] = part;
+      s_any[wave] = any;
     }
     __syncthreads();
     off = c.hdr;
@@ -1041,17 +1144,69 @@ __global__ __launch_bounds__(kPlaceT) void snappy_place(const SnappyCJobs J, con
       off += s_part[w];
       any |= s_any[w];
     }
-    const bool in_place = c.stored && !any;
-    if (k == 0 && tid < c.hdr && !in_place)
+    mode = !c.stored ? kPlaceCopy : !any ? kPlaceStored : kPlaceCopy;
+    int64_t lo = 0, hi = 0;
+    if (c.stored && any) {
+      int64_t x = tot;  // the shift of fragment i0: the exclusive sum of the totals
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int64_t y = __shfl_up(x, o, 64);
+        if ((int)lane >= o) x += y;
+      }
+      if (lane == 63) s_tot[wave] = x;
+      __syncthreads();
+      int64_t run = x - tot;
+      for (uint32_t w = 0; w < wave; ++w) run += s_tot[w];
+      for (uint32_t i = i0; i < i1; ++i) {
+        const uint32_t li = (uint32_t)min((size_t)kFrag, c.n - (size_t)i * kFrag);
+        run += (int64_t)frag_len(J.finfo[c.frag0 + i], li) - (int64_t)frag_len(0, li);
+        lo = min(lo, run);  // (the shift of fragment i + 1, or the growth at the end)
+        hi = max(hi, run);
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        lo = min(lo, (int64_t)__shfl_xor(lo, o, 64));
+        hi = max(hi, (int64_t)__shfl_xor(hi, o, 64));
+      }
+      if (lane == 0) {
+        s_lo[wave] = lo;
+        s_hi[wave] = hi;
+      }
+      __syncthreads();
+      for (uint32_t w = 0; w < kPlaceT / 64; ++w) {
+        lo = min(lo, s_lo[w]);
+        hi = max(hi, s_hi[w]);
+      }
+      if (lo >= 0 && hi <= kShiftMax) mode = kPlaceShift;
+    }
+    if (k == 0 && tid < c.hdr && mode == kPlaceCopy)
       c.dst[tid] = (uint8_t)(((uint32_t)c.n >> (7 * tid)) | (tid + 1 < c.hdr ? 128u : 0u));
     if (k + 1 == c.nfrag && tid == 0 && J.pub) {
       PubSlot* pub = J.pub + c.slot;
       pub_store(&pub->size, (uint64_t)(off + frag_len(info, len)));
       pub_store(&pub->status, (int32_t)kOk);
-      pub_store(&pub->pad, in_place ? (uint32_t)kStoredInPlace : 0u);
+      pub_store(&pub->pad, mode != kPlaceCopy ? (uint32_t)kStoredInPlace : 0u);
       publish_ticket(pub, c.ticket);
     }
-    if (in_place) return;  // FIXING_FLOAT wrote the stream, header and tags included
+    if (mode == kPlaceStored) return;  // FIXING_FLOAT wrote the stream, header and tags included
+  }
+  if (mode == kPlaceShift) {
+    const int64_t dk = stored_shift(c, k, off);
+    if (!info && !dk) return;  // stored where it was written
+    uint8_t* base = const_cast<uint8_t*>(c.in);
+    const uint8_t* src = frag_src(c, k);
+    uint8_t* dl = base + off + op + (ne < len ? lit_tag_len(len - ne - 1) : 0);
+    place_moved(base + off, scratch + (size_t)f * kSnappyFragOut, op, src + ne, len - ne, tid);
+    // the left neighbour's bytes end dk - (stored tag bytes) into this
+    // fragment's own: what the loads above may have seen rewritten comes from
+    // the stash
+    const uint32_t e = min(len, kStash);
+    if (dk > 0 && ne < e) {
+      __syncthreads();
+      if (tid >= ne && tid < e) dl[tid - ne] = J.stash[(size_t)f * kStash + tid];
+    }
+    PSF_TRACE(f, 3);
+    return;
   }
   uint8_t* d = c.dst + off;
   if (op) copy_bytes<kPlaceT>(d, scratch + (size_t)f * kSnappyFragOut, op, tid);
@@ -2617,11 +2772,12 @@ __global__ __launch_bounds__(256, 8) void snappy_dfrag(const SnappyDJobs J) {
 
 size_t snappy_max_compressed(size_t n) { return 32 + n + n / 6; }
 
-// scratch: tag slots | finfo | offset (one each per fragment) | in_place (per job)
+// scratch: tag slots | finfo | offset (one each per fragment) | in_place (per
+// job) | stash (per fragment)
 size_t snappy_compress_batch_scratch(const SnappyCJob* jobs, int njobs) {
   size_t nfrag = 0;
   for (int i = 0; i < njobs; ++i) nfrag += (jobs[i].n + kFrag - 1) / kFrag;
-  return nfrag * kSnappyFragOut + nfrag * 16 + 4 * kSnappyBatchMax + 64;
+  return nfrag * kSnappyFragOut + nfrag * 16 + 4 * kSnappyBatchMax + nfrag * kStash + 64;
 }
 
 size_t snappy_compress_scratch(size_t n) {
@@ -2658,6 +2814,7 @@ int snappy_compress_batch_launch(const SnappyCJob* jobs, int njobs, void* scratc
   K.finfo = reinterpret_cast<uint64_t*>(p);
   K.offset = K.finfo + K.nfrag;
   K.in_place = reinterpret_cast<uint32_t*>(K.offset + K.nfrag);  // (every word the kernels read is written first in the chain)
+  K.stash = reinterpret_cast<uint8_t*>(K.in_place + kSnappyBatchMax);
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)

@@ -182,14 +182,16 @@ def _stored_layout(payload):
     return bytes(out)
 
 
-def _planted(nfrag, plant, seed, tail=0, zeros=()):
+def _planted(nfrag, plant, seed, tail=0, zeros=(), early=()):
     """random bytes; in fragment k of `plant` the 4 bytes at the skip loop's
     probe 150 copy those at probe 10 (one 4-byte match, far: the fragment
-    comes out 2 bytes longer than a literal); fragments in `zeros` zero"""
+    comes out a byte longer than a literal), in fragment k of `early` those
+    at probe 20 copy probe 2 (the final literal starts 25 bytes in, the
+    fragment comes out 1 byte shorter); fragments in `zeros` zero"""
     cum = _skip_cum()
     b = np.random.default_rng(seed).integers(0, 256, nfrag * 65536 + tail, dtype=np.uint8)
-    for k in plant:
-        p, q = k * 65536 + 1 + cum[10], k * 65536 + 1 + cum[150]
+    for k, (a, z) in [(k, (10, 150)) for k in plant] + [(k, (2, 20)) for k in early]:
+        p, q = k * 65536 + 1 + cum[a], k * 65536 + 1 + cum[z]
         b[q:q + 4] = b[p:p + 4]
         b[q + 4] = b[p + 4] ^ 0x5A
     for k in zeros:
@@ -197,11 +199,20 @@ def _planted(nfrag, plant, seed, tail=0, zeros=()):
     return b.tobytes()
 
 
-@pytest.mark.parametrize("case", ["grow", "grow_every", "shrink_then_grow", "grow_then_shrink", "grow_tail"])
+@pytest.mark.parametrize("case", ["grow", "grow_every", "shrink_then_grow", "grow_then_shrink", "grow_tail",
+                                  "grow_early", "grow_over", "grow_short_tail1", "grow_short_tail2", "grow_one_last"])
 def test_compress_stored_in_place(ctx, port, case):
     """psf_snappy_compress_stored: a stored-layout stream compressed, for
     streams whose fragments with tags come out longer than literals and
-    shorter (down by whole fragments), byte-identical to 1.1.8."""
+    shorter (down by whole fragments), byte-identical to 1.1.8.  Streams that
+    grow by at most 64 bytes (and never shrink below a fragment's stored
+    start) are rewritten in place by K-place, the later fragments moved right
+    (snappy.hip kPlaceShift; "grow_early": shifts up to 55 bytes, then
+    fragments whose final literal starts 25 bytes in, so the stash of each
+    fragment's first bytes supplies what the left neighbour may have
+    overwritten inside a final literal; "grow_short_tail*": a last
+    fragment with a 1- or 2-byte tag moved); "grow_over" grows by 70 and is
+    placed by the copy."""
     import ctypes as C
 
     from parameter_server_amd._lib import check, lib
@@ -211,10 +222,15 @@ def test_compress_stored_in_place(ctx, port, case):
         "shrink_then_grow": lambda: _planted(14, [4, 5, 6, 7, 9], 3, zeros=[1]),
         "grow_then_shrink": lambda: _planted(14, [1, 2, 3, 4], 4, zeros=[8, 9]),
         "grow_tail": lambda: _planted(9, [0, 1, 2, 3, 4, 5, 6, 7], 5, tail=3000),
+        "grow_early": lambda: _planted(62, range(0, 55), 6, early=range(55, 59)),
+        "grow_over": lambda: _planted(72, range(0, 70), 7),
+        "grow_short_tail1": lambda: _planted(4, [0, 1, 2], 8, tail=50),
+        "grow_short_tail2": lambda: _planted(4, [1, 2, 3], 9, tail=200),
+        "grow_one_last": lambda: _planted(6, [5], 10, tail=70000 - 65536),
     }[case]()
     want = port.snappy_compress(payload)
     stored = _stored_layout(payload)
-    if case in ("grow", "grow_every", "grow_tail"):
+    if case.startswith("grow_") and case != "grow_then_shrink" or case == "grow":
         assert len(want) > len(stored), "the planted matches made no fragment longer"
     cap = lib().psf_snappy_stored_capacity(len(payload))
     buf = torch.zeros(cap, dtype=torch.uint8, device="cuda:0")
