@@ -294,20 +294,29 @@ struct SnappyCJobs {
   uint64_t* finfo;     // per fragment: op (tag bytes) << 32 | next_emit (start of the final literal)
   uint64_t* offset;    // per fragment: its offset in the stream (K-scan)
   uint32_t* in_place;  // per job (K-scan streams): a PlaceMode
-  uint8_t* stash;      // per fragment of a stored job: its first kStash bytes (K-probe)
+  uint8_t* stash;      // per fragment of a stored job: its first and last kEdge bytes (K-probe)
 };
 // How K-place treats a stream.  A stored job (FIXING_FLOAT wrote the stored
 // layout) whose fragments all come out stored is the result as it stands.  If
-// some carry tags and every fragment's new start lies 0..kShiftMax bytes after
-// its stored one (the usual case on codes: a fragment with one 4-byte match
+// some carry tags and every fragment's new start lies within kShiftMax bytes
+// of its stored one (the usual case on codes: a fragment with one 4-byte match
 // comes out 2 bytes longer than a literal), the stream is rewritten in place:
-// fragments before the first one with tags stay, the later ones move right,
-// each read whole before it is written.  Otherwise the stream is placed into
-// the job's dst.
+// fragments before the first one with tags stay, each later one is moved by
+// its own workgroup (tags from scratch, the final literal from where it lies).
+// A workgroup's writes reach at most kShiftMax bytes into a neighbour's
+// bytes -- the first ones of the next fragment (moved right) or the last ones
+// of the previous (moved left) -- so K-probe keeps every stored fragment's
+// first and last kEdge bytes, and a moved fragment takes those from there.
+// Otherwise the stream is placed into the job's dst.
 enum PlaceMode : uint32_t { kPlaceCopy = 0, kPlaceStored = 1, kPlaceShift = 2 };
-constexpr uint32_t kStash = 64;
+constexpr uint32_t kEdge = 64;
+constexpr uint32_t kStash = 2 * kEdge;  // per fragment: its first kEdge bytes, then its last
+#ifdef PSF_NO_PLACE_SHIFT  // A/B builds: every stream with tags placed by the copy
+constexpr int64_t kShiftMax = -1;
+#else
 constexpr int64_t kShiftMax = 64;
-static_assert(kStoredSlack >= 64 + kShiftMax + 8, "the stored stream's room for growth and the stash reads");
+#endif
+static_assert(kStoredSlack >= 64 + 64 + 8, "the stored stream's room for growth and the stash reads");
 // fragment k's input bytes: consecutive 64 KiB blocks, or in a stored job the
 // fragment's literal in the StoredLayout stream
 __device__ __forceinline__ const uint8_t* frag_src(const CJob& c, uint32_t k) {
@@ -860,10 +869,13 @@ __global__ __launch_bounds__(kCThreads) void snappy_parse(const SnappyCJobs J, u
         const uint32_t len = (uint32_t)min((size_t)kFrag, c.n - start);
         const uint8_t* g = frag_src(c, f - c.frag0);
         // a stored job's fragment may be moved in place by K-place, whose
-        // left neighbour can overwrite its first bytes before it reads them:
-        // keep them (the stream has kStoredSlack bytes after its end)
-        if (c.stored && lane < kStash / 4)
-          reinterpret_cast<uint32_t*>(J.stash + (size_t)f * kStash)[lane] = gld32(g, 4 * lane);
+        // neighbours can overwrite its first or last bytes before it reads
+        // them: keep them (reads past a short last fragment stay inside the
+        // stream's kStoredSlack)
+        if (c.stored && (lane < kEdge / 4 || (lane < kStash / 4 && len >= kEdge))) {
+          const uint32_t p = lane < kEdge / 4 ? 4 * lane : len - kStash + 4 * lane;
+          reinterpret_cast<uint32_t*>(J.stash + (size_t)f * kStash)[lane] = gld32(g, p);
+        }
         need = !probe_stored(g, len, skip, U.q.map[wave], U.q.val[wave], lane);
         if (!need && lane == 0) J.finfo[f] = 0;  // no tags, the final literal from byte 0
         PSF_TRACE_T(f, 4, wave * 64);
@@ -1027,7 +1039,7 @@ __global__ __launch_bounds__(kScanT) void snappy_scan(const SnappyCJobs J) {
   const int64_t grow = c.stored ? (int64_t)s_base - (int64_t)stored_stream_bytes(stored_layout((uint32_t)c.n)) : 0;
   const uint32_t mode = !c.stored ? kPlaceCopy
                         : !s_any  ? kPlaceStored
-                        : (lo >= 0 && hi <= kShiftMax && grow >= 0 && grow <= kShiftMax) ? kPlaceShift
+                        : (lo >= -kShiftMax && hi <= kShiftMax && grow <= kShiftMax) ? kPlaceShift
                                                                                         : kPlaceCopy;
   if (tid == 0) J.in_place[blockIdx.x] = mode;
   if (mode == kPlaceCopy && tid < c.hdr) c.dst[tid] = (uint8_t)(((uint32_t)c.n >> (7 * tid)) | (tid + 1 < c.hdr ? 128u : 0u));
@@ -1042,48 +1054,62 @@ __global__ __launch_bounds__(kScanT) void snappy_scan(const SnappyCJobs J) {
 
 // ---- K-place: one workgroup of 256 per fragment
 constexpr uint32_t kPlaceT = 256;
-constexpr int kMoveRows = 17;  // rows of 63 16-byte chunks per wave: 17 x 4 x 63 x 16 >= 64 KiB
+constexpr int kMoveRows = 6;  // rows of 63 16-byte chunks per wave and pass (58 VGPRs: 8 waves per SIMD)
+constexpr uint32_t kMovePass = kMoveRows * (kPlaceT / 64) * 63;  // chunks per pass (23.6 KiB)
 
 // A fragment rewritten in place (kPlaceShift): at d its op tag bytes from tg,
-// then the literal tag and the literal s[0, lit) -- s lies below its new
-// place by at most kShiftMax bytes, so every byte of s is loaded before the
-// workgroup's barrier and stored after it (lane l of a wave loads the aligned
-// block under destination chunk l of its row of 63, as copy_bytes).
+// then the literal tag and the literal s[0, lit), which moves by D = (its new
+// place - s), |D| small.  The literal goes in passes of kMovePass 16-byte
+// destination chunks (lane l of a wave loads the aligned block under chunk l
+// of its row of 63, as copy_bytes), each pass loaded whole before the
+// workgroup's barrier and stored after it; the passes run from the end when
+// D > 0 (a pass's stores then land only on bytes already read) and from the
+// start when D < 0.  The tags, which may cover the literal's first D bytes,
+// are stored last.
 __device__ void place_moved(uint8_t* d, const uint8_t* tg, uint32_t op, const uint8_t* s, uint32_t lit, uint32_t tid) {
   constexpr uint32_t W = kPlaceT / 64;
   const uint32_t lane = tid & 63, wv = tid >> 6;
   uint8_t* dl = d + op + (lit ? lit_tag_len(lit - 1) : 0);
+  const bool right = dl >= s;
   const uint32_t head = min(lit, (uint32_t)(-reinterpret_cast<uintptr_t>(dl) & 15));
   const uint32_t nc = (lit - head) >> 4;
   const uint32_t t0 = head + 16 * nc;
-  const uint8_t hb = tid < head ? s[tid] : 0;
-  const uint8_t tb = tid < lit - t0 ? s[t0 + tid] : 0;
   const uintptr_t sp = reinterpret_cast<uintptr_t>(s + head);
   typedef uint32_t V4 __attribute__((ext_vector_type(4)));
   const auto s16 = gbl<V4>(reinterpret_cast<const void*>(sp & ~(uintptr_t)15));
   const uint32_t sh = (uint32_t)(sp & 15);
   const uint32_t lim = nc + (sh ? 1u : 0u);
-  uint4 lo[kMoveRows];
-#pragma unroll
-  for (int u = 0; u < kMoveRows; ++u) {
-    const uint32_t c = (u * W + wv) * 63 + lane;
-    V4 x = {0, 0, 0, 0};
-    if (c < lim) x = s16[c];
-    lo[u] = make_uint4(x[0], x[1], x[2], x[3]);
-  }
-  __syncthreads();  // every byte of s is in registers
-  if (op) copy_bytes<kPlaceT>(d, tg, op, tid);
-  if (lit) literal_tag(d + op, lit, tid);
-  if (tid < head) dl[tid] = hb;
   uint4* d16 = reinterpret_cast<uint4*>(dl + head);
+  const uint32_t np = nc ? (nc + kMovePass - 1) / kMovePass : 1;
+  uint8_t hb0 = 0;
+  for (uint32_t i = 0; i < np; ++i) {
+    const uint32_t j = right ? np - 1 - i : i;
+    const uint32_t c0 = j * kMovePass;
+    uint4 lo[kMoveRows];
 #pragma unroll
-  for (int u = 0; u < kMoveRows; ++u) {
-    const uint32_t c = (u * W + wv) * 63 + lane;
-    const uint4 hi = shfl_down1(lo[u]);
-    if (lane < 63 && c < nc) d16[c] = funnel16(lo[u], hi, sh);
-    __builtin_amdgcn_sched_barrier(0);  // (one row's neighbour blocks live at a time)
+    for (int u = 0; u < kMoveRows; ++u) {
+      const uint32_t c = c0 + (u * W + wv) * 63 + lane;
+      V4 x = {0, 0, 0, 0};
+      if (c < lim) x = s16[c];
+      lo[u] = make_uint4(x[0], x[1], x[2], x[3]);
+    }
+    const uint8_t hb = j == 0 && tid < head ? s[tid] : 0;
+    const uint8_t tb = j + 1 == np && tid < lit - t0 ? s[t0 + tid] : 0;
+    __syncthreads();  // this pass's bytes are all in registers
+#pragma unroll
+    for (int u = 0; u < kMoveRows; ++u) {
+      const uint32_t c = c0 + (u * W + wv) * 63 + lane;
+      const uint4 hi = shfl_down1(lo[u]);
+      if (lane < 63 && c < nc) d16[c] = funnel16(lo[u], hi, sh);
+    }
+    if (j + 1 == np && tid < lit - t0) dl[t0 + tid] = tb;
+    if (j == 0) hb0 = hb;
   }
-  if (tid < lit - t0) dl[t0 + tid] = tb;
+  // (pass 0 has been read: last when D > 0; when D < 0 nothing stored below
+  // the literal's new start is read again)
+  if (tid < head) dl[tid] = hb0;
+  if (lit) literal_tag(d + op, lit, tid);
+  if (op) copy_bytes<kPlaceT>(d, tg, op, tid);
 }
 
 // Streams of up to kInlineScan fragments need no K-scan: the workgroup of
@@ -1177,7 +1203,7 @@ __global__ __launch_bounds__(kPlaceT) void snappy_place(const SnappyCJobs J, con
         lo = min(lo, s_lo[w]);
         hi = max(hi, s_hi[w]);
       }
-      if (lo >= 0 && hi <= kShiftMax) mode = kPlaceShift;
+      if (lo >= -kShiftMax && hi <= kShiftMax) mode = kPlaceShift;
     }
     if (k == 0 && tid < c.hdr && mode == kPlaceCopy)
       c.dst[tid] = (uint8_t)(((uint32_t)c.n >> (7 * tid)) | (tid + 1 < c.hdr ? 128u : 0u));
@@ -1191,19 +1217,26 @@ __global__ __launch_bounds__(kPlaceT) void snappy_place(const SnappyCJobs J, con
     if (mode == kPlaceStored) return;  // FIXING_FLOAT wrote the stream, header and tags included
   }
   if (mode == kPlaceShift) {
-    const int64_t dk = stored_shift(c, k, off);
+    const int64_t dk = stored_shift(c, k, off);                       // this fragment's start
+    const int64_t dn = dk + (int64_t)frag_len(info, len) - (int64_t)frag_len(0, len);  // the next one's
     if (!info && !dk) return;  // stored where it was written
     uint8_t* base = const_cast<uint8_t*>(c.in);
     const uint8_t* src = frag_src(c, k);
     uint8_t* dl = base + off + op + (ne < len ? lit_tag_len(len - ne - 1) : 0);
     place_moved(base + off, scratch + (size_t)f * kSnappyFragOut, op, src + ne, len - ne, tid);
-    // the left neighbour's bytes end dk - (stored tag bytes) into this
-    // fragment's own: what the loads above may have seen rewritten comes from
-    // the stash
-    const uint32_t e = min(len, kStash);
-    if (dk > 0 && ne < e) {
+    // the previous fragment's bytes end dk - (stored tag bytes) into this
+    // one's (dk > 0), the next one's start -dn bytes before this one's end
+    // (dn < 0): what the loads above may have seen rewritten there comes
+    // from the stash
+    const uint8_t* st = J.stash + (size_t)f * kStash;
+    const uint32_t e = min(len, kEdge);
+    const bool fix_head = dk > 0 && ne < e;
+    const bool fix_tail = dn < 0 && k + 1 < c.nfrag && len >= kEdge;
+    if (fix_head || fix_tail) {
       __syncthreads();
-      if (tid >= ne && tid < e) dl[tid - ne] = J.stash[(size_t)f * kStash + tid];
+      if (fix_head && tid >= ne && tid < e) dl[tid - ne] = st[tid];
+      const uint32_t p = len - kEdge + (tid - kEdge);
+      if (fix_tail && tid >= kEdge && tid < kStash && p >= ne) dl[p - ne] = st[tid];
     }
     PSF_TRACE(f, 3);
     return;

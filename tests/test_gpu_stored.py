@@ -200,7 +200,8 @@ def _planted(nfrag, plant, seed, tail=0, zeros=(), early=()):
 
 
 @pytest.mark.parametrize("case", ["grow", "grow_every", "shrink_then_grow", "grow_then_shrink", "grow_tail",
-                                  "grow_early", "grow_over", "grow_short_tail1", "grow_short_tail2", "grow_one_last"])
+                                  "grow_early", "grow_over", "grow_short_tail1", "grow_short_tail2", "grow_one_last",
+                                  "shrink_small", "shrink_grow_mixed", "shrink_over"])
 def test_compress_stored_in_place(ctx, port, case):
     """psf_snappy_compress_stored: a stored-layout stream compressed, for
     streams whose fragments with tags come out longer than literals and
@@ -212,7 +213,10 @@ def test_compress_stored_in_place(ctx, port, case):
     fragment's first bytes supplies what the left neighbour may have
     overwritten inside a final literal; "grow_short_tail*": a last
     fragment with a 1- or 2-byte tag moved); "grow_over" grows by 70 and is
-    placed by the copy."""
+    placed by the copy; "shrink_*": fragments 1 byte shorter than
+    literals move left (the stash of each fragment's last bytes supplies what
+    the right neighbour may have overwritten), "shrink_over" shrinks by 70
+    and is placed by the copy."""
     import ctypes as C
 
     from parameter_server_amd._lib import check, lib
@@ -227,6 +231,9 @@ def test_compress_stored_in_place(ctx, port, case):
         "grow_short_tail1": lambda: _planted(4, [0, 1, 2], 8, tail=50),
         "grow_short_tail2": lambda: _planted(4, [1, 2, 3], 9, tail=200),
         "grow_one_last": lambda: _planted(6, [5], 10, tail=70000 - 65536),
+        "shrink_small": lambda: _planted(20, [], 11, early=range(2, 12), tail=900),
+        "shrink_grow_mixed": lambda: _planted(40, range(5, 35, 2), 12, early=[1, 2, 3, 36, 37], tail=64),
+        "shrink_over": lambda: _planted(80, [], 13, early=range(0, 70)),
     }[case]()
     want = port.snappy_compress(payload)
     stored = _stored_layout(payload)
