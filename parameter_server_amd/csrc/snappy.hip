@@ -652,7 +652,7 @@ __device__ __forceinline__ uint2 parse_fragment(uint16_t* __restrict__ table, ui
     for (;;) {
       PSF_CNT(0);
       const uint32_t k = kbase + lane;
-      const uint32_t o0 = kbase == 0 ? skA : kbase == 1 ? skB : skip[k];
+      const uint32_t o0 = kbase == 0 ? skA : kbase == 1 ? skB : kbase == 2 ? skC : skip[k];
       const uint32_t o1 = kbase == 0 ? skB : kbase == 1 ? skC : skip[k + 1];
       const bool valid = ip + o1 <= ip_limit;  // else "goto emit_remainder"
       const uint32_t pos = ip + o0;
@@ -718,21 +718,26 @@ __device__ __forceinline__ uint2 parse_fragment(uint16_t* __restrict__ table, ui
         }
         const uint32_t prev = lane_of(wb, k - 1), cur = lane_of(wb, k);
         uint32_t nxt = lane_of(wb, k < 63 ? k + 1 : 63);
+        uint32_t nxt2 = lane_of(wb, k < 62 ? k + 2 : 63);
         op = emit_copy_fast(out, op, ip - cand, off + k, lane);
         ip += off + k;
         next_emit = ip;
         if (ip >= ip_limit) goto remainder;
         PSF_CNT(2);
         if (k == 63) nxt = uni(srcw<kLds>(g, s, ip + 1, len));
-        const uint32_t hp = hash(prev, shift), hc = hash(cur, shift), hn = hash(nxt, shift);
+        if (k >= 62) nxt2 = uni(srcw<kLds>(g, s, ip + 2, len));
+        const uint32_t hp = hash(prev, shift), hc = hash(cur, shift), hn = hash(nxt, shift), h2 = hash(nxt2, shift);
         if (lane == 0) table[hp] = (uint16_t)(ip - 1);
         const uint32_t c = table[hc];
         if (lane == 0) table[hc] = (uint16_t)ip;
         const uint32_t c1 = table[hn];  // the skip loop's probe 0 at ip + 1, if ip does not match
+        const uint32_t c2 = table[h2];  // its probe 1 at ip + 2 (probe 0's insert aside)
         wb = srcw<kLds>(g, s, ip + lane, len);
         const uint32_t wb1 = srcw<kLds>(g, s, ip + 1 + lane, len);
+        const uint32_t wb2 = srcw<kLds>(g, s, ip + 2 + lane, len);
         wa = srcw<kLds>(g, s, c + lane, len);
         const uint32_t wa1 = srcw<kLds>(g, s, c1 + lane, len);
+        const uint32_t wa2 = srcw<kLds>(g, s, c2 + lane, len);
         if (lane_of(wa, 0) == cur) {  // a copy from ip at once; its first round is loaded
           PSF_CNT(3);
           cand = uni(c);
@@ -753,7 +758,30 @@ __device__ __forceinline__ uint2 parse_fragment(uint16_t* __restrict__ table, ui
           have = true;
           continue;
         }
-        kbase = 1;
+        // probe 1 at ip + 1, made iff ip + 2 <= ip_limit; it sees probe 0's
+        // insert when the hashes agree (its candidate then ip, whose bytes
+        // are nxt).  On sorted keys nearly every skip loop after a copy ends
+        // here (tools/bench_snappy.py --only sorted_keys_1e9 with
+        // -DPSF_DIAG_COUNT: 6346 of 6395 skip steps per fragment matched at
+        // probe 1), so the 64-probe step is skipped.
+        if (ip + 2 > ip_limit) goto remainder;
+        {
+          const bool same = h2 == hn;
+          const uint32_t c2v = same ? ip : c2;
+          if (lane == 0) table[h2] = (uint16_t)(ip + 1);
+          if ((same ? nxt : lane_of(wa2, 0)) == nxt2) {  // a two-byte literal, then a copy
+            PSF_CNT(5);
+            cand = uni(c2v);
+            op = emit_lit<kLds>(out, op, g, s, len, next_emit, 2, lane);
+            ip += 1;
+            wa = same ? wb1 : wa2;
+            wb = wb2;
+            off = 0;
+            have = true;
+            continue;
+          }
+        }
+        kbase = 2;
         break;
       }
     }
@@ -961,8 +989,8 @@ __global__ __launch_bounds__(kCThreads) void snappy_parse(const SnappyCJobs J, u
   }
 #ifdef PSF_DIAG_COUNT
   if (blockIdx.x == 0 && lane == 0 && wave < kParseWaves)
-    printf("parse counts wg0 wave %u: steps %u ext_rounds %u copies %u immediate %u probe0 %u\n", wave, cnt[0],
-           cnt[1], cnt[2], cnt[3], cnt[4]);
+    printf("parse counts wg0 wave %u: steps %u ext_rounds %u copies %u immediate %u probe0 %u probe1 %u\n", wave,
+           cnt[0], cnt[1], cnt[2], cnt[3], cnt[4], cnt[5]);
 #endif
 }
 
