@@ -346,13 +346,14 @@ __device__ __forceinline__ uint32_t hash_shift(uint32_t len) {
 // ---- K-probe
 constexpr uint32_t kMapSlots = 1024;  // per wave: every inserted probe (<= 270) as {hash + 1, position, 4 bytes}
 constexpr uint32_t kProbeMax = 6 * 64;  // probes a skip loop from ip = 1 can make in 64 KiB (< kSkipN)
-// the 4 input bytes at p of a fragment starting at g (any alignment; the
-// dwords read lie inside the fragment's 16-byte margin or before it within the
-// same dword as g[0])
+// the 4 input bytes at p of a fragment starting at g (any alignment): one
+// global_load_dword at the unaligned address -- gfx950 runs in unaligned mode,
+// as the stored-layout code stores rely on (round 4 read two aligned dwords
+// and shifted; the probe's ~270 scattered loads per fragment are bound by the
+// texture unit's cache-line rate, so half the load instructions)
+typedef uint32_t __attribute__((aligned(1))) u32u;
 __device__ __forceinline__ uint32_t gld32(const uint8_t* g, uint32_t p) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(g + p);
-  const auto w = gbl<uint32_t>(reinterpret_cast<const void*>(a & ~(uintptr_t)3));
-  return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(a & 3));
+  return *gbl<u32u>(g + p);
 }
 // the table entry of hash h: 0 when never inserted (the table's initial 0)
 __device__ __forceinline__ uint64_t map_get(const uint64_t* m, uint32_t h) {
@@ -528,12 +529,7 @@ __device__ __forceinline__ bool probe_stored(const uint8_t* g, uint32_t len, con
 __device__ __forceinline__ uint32_t gw32(const uint8_t* g, uint32_t p, uint32_t len) {
   p = p < len ? p : len - 1;
   const uint32_t q = p < len - 4 ? p : len - 4;
-  const uintptr_t a = reinterpret_cast<uintptr_t>(g + q);
-  const auto w = gbl<uint32_t>(reinterpret_cast<const void*>(a & ~(uintptr_t)3));
-  const uint32_t sh = (uint32_t)(a & 3);
-  const uint32_t lo = w[0];
-  const uint32_t hi = sh ? w[1] : 0u;
-  return __builtin_amdgcn_alignbyte(hi, lo, sh) >> (8 * (p - q));
+  return gld32(g, q) >> (8 * (p - q));
 }
 __device__ __forceinline__ uint32_t lane_of(uint32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
 // the same from a fragment staged in LDS (16 zero bytes after it)
