@@ -582,6 +582,17 @@ __device__ __forceinline__ uint32_t emit_lit(uint8_t* out, uint32_t op, const ui
 #endif
   return op + hl + len;
 }
+// The literal of len <= 4 bytes that starts where a copy ended, whose bytes
+// are the low ones of cur (the 4 bytes there, already in a register): no
+// load on the parse's chain before the store (emit_lit would read them back
+// from the fragment first, and the store waits for that read)
+__device__ __forceinline__ uint32_t emit_short_lit(uint8_t* out, uint32_t op, uint32_t cur, uint32_t len,
+                                                   uint32_t lane) {
+  const uint8_t b = lane ? (uint8_t)(cur >> (8 * ((lane - 1) & 3))) : (uint8_t)((len - 1) << 2);
+  lane = PSF_SINK(lane);
+  if (lane <= len) out[op + lane] = b;
+  return op + 1 + len;
+}
 // EmitCopy (1.1.8) of a copy that fits one tag, one store instruction; the
 // rest go to emit_copy
 __device__ __forceinline__ uint32_t emit_copy_fast(uint8_t* out, uint32_t op, uint32_t offset, uint32_t len,
@@ -747,7 +758,7 @@ __device__ __forceinline__ uint2 parse_fragment(uint16_t* __restrict__ table, ui
         if (lane_of(wa1, 0) == nxt) {  // probe 0 matches: a one-byte literal, then a copy
           PSF_CNT(4);
           cand = uni(c1);
-          op = emit_lit<kLds>(out, op, g, s, len, next_emit, 1, lane);
+          op = emit_short_lit(out, op, cur, 1, lane);
           wa = wa1;
           wb = wb1;
           off = 0;
@@ -768,7 +779,7 @@ __device__ __forceinline__ uint2 parse_fragment(uint16_t* __restrict__ table, ui
           if ((same ? nxt : lane_of(wa2, 0)) == nxt2) {  // a two-byte literal, then a copy
             PSF_CNT(5);
             cand = uni(c2v);
-            op = emit_lit<kLds>(out, op, g, s, len, next_emit, 2, lane);
+            op = emit_short_lit(out, op, cur, 2, lane);
             ip += 1;
             wa = same ? wb1 : wa2;
             wb = wb2;
