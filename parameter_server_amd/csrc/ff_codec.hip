@@ -1094,6 +1094,43 @@ __device__ __forceinline__ void minmax_item(const FfBatchT<CAP>& B, int jb, uint
     }
   }
 }
+// The fused hand-off's own-tile path: min/max items bb and, with two, bb + 1
+// are full tiles this workgroup already holds in registers (v, v2): one
+// block reduction for both (and the job's ragged tail when bb is the job's
+// first item), published as minmax_item publishes an item -- the run's
+// min/max in bb's slot, the identity in bb + 1's -- and both counted ready.
+template <typename V, int CAP>
+__device__ __forceinline__ void minmax_run_regs(const FfBatchT<CAP>& B, int jb, uint32_t bb, uint32_t nitems,
+                                                const V v[4][4], const V v2[4][4], uint32_t* ready) {
+  typedef typename KeyOf<V>::K K;
+  const FfJob& J = B.job[jb];
+  K lo = KeyOf<V>::kLoId, hi = KeyOf<V>::kHiId;
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc_minmax<V, K>(v[u][j], lo, hi);
+  if (nitems == 2)
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc_minmax<V, K>(v2[u][j], lo, hi);
+  if (bb == B.mm_first[jb]) {
+    const V* __restrict__ x = static_cast<const V*>(J.x);
+    for (size_t i = ((J.n >> 2) << 2) + threadIdx.x; i < J.n; i += kBlock) acc_minmax<V, K>(x[i], lo, hi);
+  }
+  block_minmax(lo, hi);
+  if (threadIdx.x == 0) {
+    K* pp = reinterpret_cast<K*>(B.partials);
+    __hip_atomic_store(&pp[bb], lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&pp[B.mm_total + bb], hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (nitems == 2) {
+      __hip_atomic_store(&pp[bb + 1], KeyOf<V>::kLoId, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&pp[B.mm_total + bb + 1], KeyOf<V>::kHiId, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(ready, nitems, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
 template <typename V, int CAP>
 __device__ __forceinline__ void minmax_batch_body(const FfBatchT<CAP>& B, uint32_t block) {
   // mm_reverse: workgroups dispatched last-array-first, so the arrays the
@@ -1147,6 +1184,10 @@ __device__ __forceinline__ int encode_batch_body(const FfBatchT<CAP>& B, uint32_
   if (t0 < tf) load_tile(t0);
   float mn_f = J.mn, mx_f = J.mx;
   bool late = false;  // the in-launch hand-off gave up (never expected)
+  // the fused hand-off gave this workgroup exactly its own (full) tiles as
+  // min/max items: their values stay in registers for the encode (v, v2)
+  bool own = false;
+  V v2[4][4];
   if (J.mm_nwg) {
     typedef typename KeyOf<V>::K K;
     K* pp = reinterpret_cast<K*>(B.partials);
@@ -1154,16 +1195,60 @@ __device__ __forceinline__ int encode_batch_body(const FfBatchT<CAP>& B, uint32_
     if (fused) {
       uint32_t* c = fused + kFusedLine * jb;
       __shared__ uint32_t s_item, s_late;
-      // one claim per workgroup of a run of ceil(items / workgroups) items
-      // (every item then belongs to a workgroup that is running: the first
-      // ones to start take them all); the run's bounds read into scalar
-      // registers, so its loop is uniform for the compiler too
       const uint32_t per = ((uint32_t)J.mm_nwg + nwg - 1) / nwg;
-      if (threadIdx.x == 0) s_item = __hip_atomic_fetch_add(&c[0], per, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __syncthreads();
-      const uint32_t i0 = __builtin_amdgcn_readfirstlane(s_item);
-      const uint32_t i1 = i0 + per < (uint32_t)J.mm_nwg ? i0 + per : (uint32_t)J.mm_nwg;
-      for (uint32_t item = i0; item < i1; ++item) minmax_item<V, CAP>(B, jb, mm_wg0 + item, &c[1]);
+      auto items = [&](uint32_t i0, uint32_t i1) {
+        for (uint32_t item = i0; item < i1; ++item) minmax_item<V, CAP>(B, jb, mm_wg0 + item, &c[1]);
+      };
+      if ((size_t)J.mm_nwg == ntiles && nwg <= 32) {
+        // one item a tile, so workgroup w's run of items is its own tiles:
+        // runs are claimed by bit in c[0], this workgroup's own run first
+        // (its values then stay in registers for the encode), then every run
+        // not claimed yet (so no item waits on a workgroup that has not
+        // started; the runs of the ones that have are theirs by then)
+        if (threadIdx.x == 0) s_item = __hip_atomic_fetch_or(&c[0], 1u << wg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        const bool mine = ((__builtin_amdgcn_readfirstlane(s_item) >> wg) & 1u) == 0;
+        __syncthreads();  // (s_item is written again below)
+        if (mine) {
+          own = t0 < t1 && t1 <= tf && t1 - t0 <= 2;
+          if (own) {
+            if (t1 - t0 == 2) {
+              V v0[4][4];  // (load_tile fills v)
+#pragma unroll
+              for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v0[u][j] = v[u][j];
+              load_tile(t0 + 1);
+#pragma unroll
+              for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                  v2[u][j] = v[u][j];
+                  v[u][j] = v0[u][j];
+                }
+            }
+            minmax_run_regs<V, CAP>(B, jb, mm_wg0 + (uint32_t)t0, (uint32_t)(t1 - t0), v, v2, &c[1]);
+          } else {
+            items(min(wg * per, (uint32_t)J.mm_nwg), min(wg * per + per, (uint32_t)J.mm_nwg));
+          }
+        }
+        const uint32_t all = nwg == 32 ? ~0u : (1u << nwg) - 1u;
+        if (threadIdx.x == 0) s_item = __hip_atomic_fetch_or(&c[0], all, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        for (uint32_t left = all & ~__builtin_amdgcn_readfirstlane(s_item); left; left &= left - 1) {
+          const uint32_t r = (uint32_t)__builtin_ctz(left);
+          items(min(r * per, (uint32_t)J.mm_nwg), min(r * per + per, (uint32_t)J.mm_nwg));
+        }
+      } else {
+        // one claim per workgroup of a run of ceil(items / workgroups) items
+        // (every item then belongs to a workgroup that is running: the first
+        // ones to start take them all); the run's bounds read into scalar
+        // registers, so its loop is uniform for the compiler too
+        if (threadIdx.x == 0) s_item = __hip_atomic_fetch_add(&c[0], per, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        const uint32_t i0 = __builtin_amdgcn_readfirstlane(s_item);
+        items(i0, i0 + per < (uint32_t)J.mm_nwg ? i0 + per : (uint32_t)J.mm_nwg);
+      }
       if (threadIdx.x == 0) s_late = wait_ready(&c[1], J.mm_nwg) ? 0u : 1u;
 #ifdef PSF_FUSED_DEBUG
       if (threadIdx.x == 0 && s_late != 0)
@@ -1233,6 +1318,17 @@ __device__ __forceinline__ int encode_batch_body(const FfBatchT<CAP>& B, uint32_
   if (late && sticky && threadIdx.x == 0) pub_store(sticky, (int32_t)kErrHip);  // Context::sync throws
   if (!(q.bin > 0) || late) return jb;  // CHECK_GT(bin, 0), fixing_float.h:71
 
+  // the next full tile: from registers on the own-tile path, else loaded
+  auto next_tile = [&](size_t t) {
+    if (own && t == t0 + 1) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[u][j] = v2[u][j];
+    } else {
+      load_tile(t);
+    }
+  };
   EncodeParams p{};  // the per-launch constants the tile code reads
   p.lcg_bits = B.lcg_bits;
   p.lcg_pos = J.u.e.lcg_pos;
@@ -1246,7 +1342,7 @@ __device__ __forceinline__ int encode_batch_body(const FfBatchT<CAP>& B, uint32_
       if (wg == 0)  // every fragment's tag, and the header
         for (uint32_t k = threadIdx.x; k <= L.last; k += kBlock) stored_put_prefix(out, L, k);
       for (size_t t = t0; t < tf; ++t) {
-        if (t != t0) load_tile(t);
+        if (t != t0) next_tile(t);
         const size_t gb = t * kTileGroups + threadIdx.x;
         encode_full_tile<V, NB, true>(v, q, p, out, gb, gb, &L);
       }
@@ -1254,7 +1350,7 @@ __device__ __forceinline__ int encode_batch_body(const FfBatchT<CAP>& B, uint32_
   }
   if (!stored) {
     for (size_t t = t0; t < tf; ++t) {
-      if (t != t0) load_tile(t);
+      if (t != t0) next_tile(t);
       encode_full_tile<V, NB>(v, q, p, out, t * kTileGroups + threadIdx.x, t * kTileGroups + threadIdx.x);
     }
   }
