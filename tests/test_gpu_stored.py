@@ -247,3 +247,24 @@ def test_compress_stored_in_place(ctx, port, case):
     got = buf[:out_len.value].cpu().numpy().tobytes()
     ok = got == want
     assert ok, (case, len(got), len(want))
+
+
+def test_compress_stored_in_place_scan_path(ctx, port):
+    """A stored-layout stream of 4100 fragments (offsets from the per-stream
+    scan launch, more than kInlineScan) whose three matched fragments grow it
+    by a few bytes: rewritten in place through K-scan's shift bounds
+    (kPlaceShift), byte-identical to 1.1.8."""
+    import ctypes as C
+
+    from parameter_server_amd._lib import check, lib
+    payload = _planted(4100, [3, 2000, 4090], 21, tail=777, early=[1000])
+    want = port.snappy_compress(payload)
+    stored = _stored_layout(payload)
+    cap = lib().psf_snappy_stored_capacity(len(payload))
+    buf = torch.zeros(cap, dtype=torch.uint8, device="cuda:0")
+    buf[:len(stored)] = torch.frombuffer(bytearray(stored), dtype=torch.uint8).cuda()
+    out_len = C.c_size_t()
+    check(lib().psf_snappy_compress_stored(ctx.h, C.c_void_p(buf.data_ptr()), len(payload), cap, C.byref(out_len)))
+    got = buf[:out_len.value].cpu().numpy().tobytes()
+    ok = got == want
+    assert ok, (len(got), len(want))
