@@ -164,8 +164,9 @@ int psf_snappy_compress(psf_context* ctx, const void* d_in, size_t n, void* d_ou
  * per 64 KiB fragment snappy's literal tag and the fragment's bytes, what
  * 1.1.8 writes for data without matches (FIXING_FLOAT writes its codes so
  * when COMPRESSING follows it): on return d_buf holds RawCompress of the n
- * payload bytes (left in place when every fragment comes out stored, else
- * placed and copied back), *out_len its length.  The buffer holds cap >=
+ * payload bytes (left in place when every fragment comes out stored,
+ * rewritten in place when each fragment's start moves by at most 64 bytes,
+ * else placed and copied back), *out_len its length.  The buffer holds cap >=
  * psf_snappy_stored_capacity(n) bytes (the stream can grow: a short match may
  * cost more than the literal it replaces).  Synchronous. */
 int psf_snappy_compress_stored(psf_context* ctx, void* d_buf, size_t n, size_t cap, size_t* out_len);
