@@ -984,8 +984,8 @@ int psf_router_step(psf_router* r, psf_message* const* streams, int n, int iters
     if (pr->world() > 1 || pr->loopback())
       throw psf::CheckError(PSF_ERR_ARG, "psf_router_step: a router with other ranks needs an exchange");
     std::vector<int64_t> sizes(2 * (size_t)pr->world());
+    if (iters > 0) pr->encode_launch(ms.data(), n);
     for (int it = 0; it < iters; ++it) {
-      pr->encode_launch(ms.data(), n);
       // the next step's slicing pass goes ahead of this step's decodes (and
       // of the wait for its COMPRESSING lengths)
       if (it + 1 < iters) pr->prefetch(ms.data(), n);
@@ -993,7 +993,12 @@ int psf_router_step(psf_router* r, psf_message* const* streams, int n, int iters
       for (int64_t s : sizes)
         if (s) throw psf::CheckError(PSF_ERR_ARG, "psf_router_step: slices for other ranks need an exchange");
       pr->fill(nullptr);
-      pr->decode_local();
+      // this step's decodes in flight, the next step's encode queued behind
+      // them, then the wait for the decodes: the device runs on from one
+      // step into the next while the host waits
+      pr->decode_local_launch();
+      if (it + 1 < iters) pr->encode_launch(ms.data(), n);
+      pr->decode_local_finish();
     }
     return PSF_OK;
   });

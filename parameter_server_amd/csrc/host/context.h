@@ -71,15 +71,22 @@ struct RangeBatch {
 
 class Context {
  public:
-  static constexpr int kSlots = 768;
+  static constexpr int kSlots = 1280;
   // slots [0, kSyncSlots) serve launches whose results the host waits for
   // before returning; [kSyncSlots, kPresignSlot0) the KEY_CACHING signatures
   // that a batched encode leaves in flight while later filters launch;
-  // [kPresignSlot0, kSlots) the round-trip drivers' signatures of the next
-  // iteration (presign_launch)
+  // [kPresignSlot0, kPresignEnd) the round-trip drivers' signatures of the
+  // next iteration (presign_launch); [kCompressSlot0, kDecodeSlot0) the
+  // COMPRESSING encodes a batched encode leaves in flight for its caller
+  // (PendingEncode), [kDecodeSlot0, kSlots) the uncompress launches a batched
+  // decode leaves in flight (PendingDecode) -- the router's multi-step driver
+  // holds one of each at once.  Every region holds kSyncSlots.
   static constexpr int kSyncSlots = 256;
   static constexpr int kDeferSlot0 = kSyncSlots;
   static constexpr int kPresignSlot0 = 512;
+  static constexpr int kPresignEnd = 768;
+  static constexpr int kCompressSlot0 = 768;
+  static constexpr int kDecodeSlot0 = 1024;
 
   // mode kStreamOwn -> a private non-blocking stream owned by the context;
   // kStreamGiven -> `stream` as given (nullptr = the legacy default stream);

@@ -124,6 +124,17 @@ class CompressingFilter : public Filter {
   // (Message::predecoded)
   static void decode_messages(Context* ctx, const std::vector<Message*>& msgs,
                               const std::vector<RemoteNode*>* nodes = nullptr);
+  // decode_messages in two halves: the launches (the uncompress kernels in
+  // flight, the publish slots taken), and the wait that assigns the arrays
+  // and marks the fused ones (Message::predecoded)
+  struct DecodeInFlight {
+    std::unique_ptr<SnappyBatch> batch;
+    std::vector<std::unique_ptr<bool[]>> fused;
+    std::vector<Message*> owners;
+  };
+  static void decode_launch(Context* ctx, const std::vector<Message*>& msgs, const std::vector<RemoteNode*>* nodes,
+                            DecodeInFlight* st, int slot0);
+  static void decode_finish(DecodeInFlight* st);
 };
 
 // NOISE, add_noise.h:9-41
@@ -184,7 +195,23 @@ void encode_batch(RemoteNode* const* nodes, Message* const* msgs, int n, const K
                   PendingEncode* pend = nullptr);
 // hints: as encode_batch's, for the receiver's check of keys that arrive
 // (key_caching.h:43): used only while the message's key is that buffer.
-void decode_batch(RemoteNode* const* nodes, Message* const* msgs, int n, const KeySigHint* hints = nullptr);
+// A decode_batch whose first position (the last filter of every chain) is
+// COMPRESSING for every message, left in flight after its uncompress
+// launches (decode_batch's `later` argument): finish() waits for them and
+// runs the chains' remaining positions.  The messages, nodes and hints must
+// outlive finish(); a pending decode that is never finished is finished by
+// its destructor.
+struct PendingDecode {
+  std::vector<RemoteNode*> nodes;
+  std::vector<Message*> msgs;
+  std::vector<KeySigHint> hints;
+  std::vector<CompressingFilter::DecodeInFlight> cz;
+  bool active = false;
+  void finish();
+  ~PendingDecode();
+};
+void decode_batch(RemoteNode* const* nodes, Message* const* msgs, int n, const KeySigHint* hints = nullptr,
+                  PendingDecode* later = nullptr);
 // The in-process round-trip drivers (psf_node(s)_roundtrip_ex) deliver the
 // sender's key buffer itself, zero-copy and unchanged, so every KEY_CACHING
 // CRC of an iteration can be queued up front: per distinct device key buffer

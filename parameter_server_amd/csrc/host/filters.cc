@@ -509,7 +509,9 @@ void CompressingFilter::decode(Message* msg) { decode_messages(ctx_, {msg}); }
 
 void CompressingFilter::encode_messages(Context* ctx, const std::vector<Message*>& msgs,
                                         std::unique_ptr<SnappyBatch>* defer) {  // compressing.h:8-19
-  std::unique_ptr<SnappyBatch> held(new SnappyBatch(*ctx));
+  // (left in flight: its own publish slots, so the caller's decodes and the
+  // next steps' synchronous launches may run meanwhile)
+  std::unique_ptr<SnappyBatch> held(new SnappyBatch(*ctx, defer ? Context::kCompressSlot0 : 0));
   SnappyBatch& batch = *held;
   for (Message* msg : msgs) {
     FilterConfig* conf = find(FilterConfig::COMPRESSING, msg);
@@ -586,10 +588,18 @@ static void fused_ff_plan(Context* ctx, RemoteNode* node, Message* msg, const Fi
 
 void CompressingFilter::decode_messages(Context* ctx, const std::vector<Message*>& msgs,
                                         const std::vector<RemoteNode*>* nodes) {  // compressing.h:20-37
-  SnappyBatch batch(*ctx);
+  DecodeInFlight st;
+  decode_launch(ctx, msgs, nodes, &st, 0);
+  decode_finish(&st);
+}
+
+void CompressingFilter::decode_launch(Context* ctx, const std::vector<Message*>& msgs,
+                                      const std::vector<RemoteNode*>* nodes, DecodeInFlight* st, int slot0) {
+  st->batch.reset(new SnappyBatch(*ctx, slot0));
+  SnappyBatch& batch = *st->batch;
   std::vector<SnappyDequant> plan;
-  std::vector<std::unique_ptr<bool[]>> fused;  // one flag per value array of each message in owners
-  std::vector<Message*> owners;
+  std::vector<std::unique_ptr<bool[]>>& fused = st->fused;  // one flag per value array of each message in owners
+  std::vector<Message*>& owners = st->owners;
   for (size_t m = 0; m < msgs.size(); ++m) {
     Message* msg = msgs[m];
     FilterConfig* conf = find(FilterConfig::COMPRESSING, msg);
@@ -616,8 +626,16 @@ void CompressingFilter::decode_messages(Context* ctx, const std::vector<Message*
       else batch.uncompress(v, &v, &conf->uncompressed_size[k]);
     }
   }
-  batch.flush();
-  for (size_t f = 0; f < owners.size(); ++f) {  // the flags flush() set
+  batch.launch_all();
+}
+
+void CompressingFilter::decode_finish(DecodeInFlight* st) {
+  if (!st->batch) return;
+  std::unique_ptr<SnappyBatch> batch = std::move(st->batch);
+  batch->finish();
+  const std::vector<Message*>& owners = st->owners;
+  const std::vector<std::unique_ptr<bool[]>>& fused = st->fused;
+  for (size_t f = 0; f < owners.size(); ++f) {  // the flags finish() set
     Message* msg = owners[f];
     msg->predecoded.assign(msg->value.size(), 0);
     bool any = false;
@@ -806,7 +824,7 @@ PresignJob presign_launch(RemoteNode* const* nodes, const Message* const* msgs, 
   }
   size_t most = 0;
   for (size_t k : per) most = std::max(most, k);
-  J.ahead = ahead && 2 * most <= (size_t)(Context::kSlots - Context::kPresignSlot0);
+  J.ahead = ahead && 2 * most <= (size_t)(Context::kPresignEnd - Context::kPresignSlot0);
   if (!J.ahead) return J;  // launched and waited for in presign_finish
   std::vector<const void*> d;
   std::vector<uint32_t> len, tk;
@@ -991,13 +1009,73 @@ void encode_batch(RemoteNode* const* nodes, Message* const* msgs, int n, const K
   finish_kc();
 }
 
-void decode_batch(RemoteNode* const* nodes, Message* const* msgs, int n, const KeySigHint* hints) {
-  size_t maxlen = 0;
-  for (int i = 0; i < n; ++i) {
-    maxlen = std::max(maxlen, msgs[i]->task.filter.size());
-    msgs[i]->predecoded.clear();
+// positions [r0, maxlen) of decode_batch (r-th filter from the end of every chain)
+static void decode_positions(RemoteNode* const* nodes, Message* const* msgs, int n, const KeySigHint* hints,
+                             size_t r0);
+
+void decode_batch(RemoteNode* const* nodes, Message* const* msgs, int n, const KeySigHint* hints,
+                  PendingDecode* later) {
+  for (int i = 0; i < n; ++i) msgs[i]->predecoded.clear();
+  if (later && n > 0) {
+    if (later->active) later->finish();
+    // every chain ends in COMPRESSING of value arrays only: its launches now,
+    // the rest in finish().  (A message with keys -- a KEY_CACHING miss,
+    // keys compressed -- is decoded at once: tag-dense key streams need the
+    // uncompress's tail kernels, which finish() would queue behind whatever
+    // the caller launches meanwhile; measured slower, r05u2.)
+    bool all_cz = true;
+    for (int i = 0; i < n && all_cz; ++i)
+      all_cz = !msgs[i]->task.filter.empty() && msgs[i]->task.filter.back().type == FilterConfig::COMPRESSING &&
+               !msgs[i]->has_key();
+    if (all_cz) {
+      std::vector<Context*> czc;
+      std::vector<std::vector<Message*>> cz;
+      std::vector<std::vector<RemoteNode*>> cz_nodes;
+      for (int i = 0; i < n; ++i) {
+        nodes[i]->FindFilterOrCreate(msgs[i]->task.filter.back());
+        const int c = ctx_index(czc, nodes[i]->ctx());
+        if ((size_t)c >= cz.size()) {
+          cz.emplace_back();
+          cz_nodes.emplace_back();
+        }
+        cz[c].push_back(msgs[i]);
+        cz_nodes[c].push_back(nodes[i]);
+      }
+      later->nodes.assign(nodes, nodes + n);
+      later->msgs.assign(msgs, msgs + n);
+      later->hints.clear();
+      if (hints) later->hints.assign(hints, hints + n);
+      later->cz.clear();
+      later->cz.resize(cz.size());
+      later->active = true;
+      for (size_t c = 0; c < cz.size(); ++c)
+        CompressingFilter::decode_launch(czc[c], cz[c], &cz_nodes[c], &later->cz[c], Context::kDecodeSlot0);
+      return;
+    }
   }
-  for (size_t r = 0; r < maxlen; ++r) {  // r-th filter from the end of every chain
+  decode_positions(nodes, msgs, n, hints, 0);
+}
+
+void PendingDecode::finish() {
+  if (!active) return;
+  active = false;
+  for (auto& c : cz) CompressingFilter::decode_finish(&c);
+  cz.clear();
+  decode_positions(nodes.data(), msgs.data(), (int)msgs.size(), hints.empty() ? nullptr : hints.data(), 1);
+}
+
+PendingDecode::~PendingDecode() {
+  try {
+    finish();
+  } catch (...) {  // (a destructor does not throw; the caller that cared finished it)
+  }
+}
+
+static void decode_positions(RemoteNode* const* nodes, Message* const* msgs, int n, const KeySigHint* hints,
+                             size_t r0) {
+  size_t maxlen = 0;
+  for (int i = 0; i < n; ++i) maxlen = std::max(maxlen, msgs[i]->task.filter.size());
+  for (size_t r = r0; r < maxlen; ++r) {  // r-th filter from the end of every chain
     std::vector<Context*> ffc, czc;
     std::vector<std::vector<FfMessage>> ff;
     std::vector<std::vector<Message*>> cz;

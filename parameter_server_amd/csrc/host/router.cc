@@ -256,6 +256,33 @@ void PushRouter::decode_local() {
   local_server_.clear();
 }
 
+void PushRouter::decode_local_launch() {
+  const int64_t t0 = now_ns();
+  decode_local_finish();  // (a launch without its finish: complete it first)
+  dec_msgs_ = std::move(local_);
+  dec_servers_ = std::move(local_server_);
+  local_.clear();
+  local_server_.clear();
+  dec_nodes_.resize(dec_msgs_.size());
+  dec_ptrs_.resize(dec_msgs_.size());
+  for (size_t k = 0; k < dec_msgs_.size(); ++k) {
+    dec_nodes_[k] = receiver(dec_servers_[k], dec_msgs_[k].task.key_channel);
+    dec_ptrs_[k] = &dec_msgs_[k];
+  }
+  decode_batch(dec_nodes_.data(), dec_ptrs_.data(), (int)dec_msgs_.size(), nullptr, &pend_dec_);
+  stat_decode_ns += now_ns() - t0;
+}
+
+void PushRouter::decode_local_finish() {
+  if (dec_msgs_.empty() && !pend_dec_.active) return;
+  const int64_t t0 = now_ns();
+  pend_dec_.finish();
+  for (size_t k = 0; k < dec_msgs_.size(); ++k) results_.emplace_back(dec_servers_[k], std::move(dec_msgs_[k]));
+  dec_msgs_.clear();
+  dec_servers_.clear();
+  stat_decode_ns += now_ns() - t0;
+}
+
 void PushRouter::decode_received(const uint8_t* recvbuf, const int64_t* sizes_in) {
   const int64_t t0 = now_ns();
   uint64_t total = 0;

@@ -49,6 +49,13 @@ class PushRouter {
   void fill(void* sendbuf);
   // decode the slices whose server is on this rank
   void decode_local();
+  // decode_local() in two halves (the multi-step driver queues the next
+  // step's encode in between, so the device goes from this step's decode to
+  // the next step's min/max pass with no wait for the host): the launches --
+  // a chain that ends in COMPRESSING leaves its uncompress in flight -- and
+  // the wait plus the chains' remaining decodes
+  void decode_local_launch();
+  void decode_local_finish();
   // The native exchange (exchange.h) the multi-step driver moves slices for
   // other ranks through; then one whole step after encode_launch() is
   // exchange_step(): the delivery split, the Task records posted to the
@@ -99,6 +106,13 @@ class PushRouter {
   std::vector<int> srv_;
   PendingEncode pend_;
   int64_t t_launch_ = 0;
+  // the step whose decode is in flight (decode_local_launch .. _finish); its
+  // messages outlive pend_dec_, which finishes them if it must
+  std::vector<Message> dec_msgs_;
+  std::vector<int> dec_servers_;
+  std::vector<RemoteNode*> dec_nodes_;
+  std::vector<Message*> dec_ptrs_;
+  PendingDecode pend_dec_;
 };
 
 }  // namespace psf

@@ -51,7 +51,7 @@ void SnappyBatch::compress(const Buffer& src, Buffer* dst) {
   j.in = c_.to_device(src);
   j.dst = dst;
   j.out = c_.alloc(snappy_max_compressed(src.bytes));
-  j.slot = (int)jobs_.size();
+  j.slot = slot0_ + (int)jobs_.size();
   j.ticket = c_.next_ticket();
   jobs_.push_back(std::move(j));
 }
@@ -89,7 +89,7 @@ void SnappyBatch::uncompress(const Buffer& src, Buffer* dst, const uint64_t* siz
   if (jobs_.size() == (size_t)Context::kSyncSlots) flush();
   Job j;
   j.dst = dst;
-  j.slot = (int)jobs_.size();
+  j.slot = slot0_ + (int)jobs_.size();
   j.hinted = hinted;
   if (hinted) j.src = src;
   prepare_uncompress(j, src, hdr, dsize);

@@ -14,7 +14,10 @@ uint32_t snappy_read_header(Context& c, const Buffer& in, uint64_t* len);
 
 class SnappyBatch {
  public:
-  explicit SnappyBatch(Context& c) : c_(c) {}
+  // slot0: the first of the kSyncSlots publish slots its streams use (a
+  // batch left in flight takes its own region, Context::kCompressSlot0 /
+  // kDecodeSlot0)
+  explicit SnappyBatch(Context& c, int slot0 = 0) : slot0_(slot0), c_(c) {}
   // *dst is assigned at flush(); src must stay alive until then
   void compress(const Buffer& src, Buffer* dst);
   // size_hint: the uncompressed length the sender recorded (COMPRESSING's
@@ -54,6 +57,7 @@ class SnappyBatch {
     bool* fused = nullptr;
     int group = -1;       // streams decoded again together when one falls back
   };
+  int slot0_;
   // an uncompress batch launched with its fast path only (SnappyTail): the
   // rest is launched at finish() unless every stream published its verdict
   struct Tail {
