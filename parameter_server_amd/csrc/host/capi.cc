@@ -345,7 +345,7 @@ int psf_snappy_uncompress(psf_context* ctx, const void* d_in, size_t n, void* d_
     int st = psf::snappy_uncompress_batch_launch(&job, 1, scratch.ptr, c.stream(), c.prof(), c.pub_dev(0),
                                                  psf::ZeroPair{}, &tail);
     if (st != PSF_OK) return st;
-    hipEvent_t done = c.take_event();
+    hipEvent_t done = c.take_marker();
     PSF_HIP_CHECK(hipEventRecord(done, c.stream()));
     bool published = false;
     for (uint64_t spin = 0;; ++spin) {
@@ -356,12 +356,12 @@ int psf_snappy_uncompress(psf_context* ctx, const void* d_in, size_t n, void* d_
         break;
       }
       if (q != hipErrorNotReady) {
-        c.give_event(done);
+        c.give_marker(done);
         throw psf::CheckError(PSF_ERR_HIP, std::string("stream failed: ") + hipGetErrorString(q));
       }
       if (spin > 4096) sched_yield();
     }
-    c.give_event(done);
+    c.give_marker(done);
     if (!published) {
       st = psf::snappy_uncompress_tail_launch(&tail, c.stream());
       if (st != PSF_OK) return st;
@@ -975,7 +975,7 @@ int psf_router_step(psf_router* r, psf_message* const* streams, int n, int iters
     }
     if (pr->exchange()) {  // any world: the native exchange
       for (int it = 0; it < iters; ++it) {
-        pr->encode_launch(ms.data(), n);
+        pr->encode_launch(ms.data(), n, it == 0);
         if (it + 1 < iters) pr->prefetch(ms.data(), n);
         pr->exchange_step();
       }
@@ -997,7 +997,7 @@ int psf_router_step(psf_router* r, psf_message* const* streams, int n, int iters
       // them, then the wait for the decodes: the device runs on from one
       // step into the next while the host waits
       pr->decode_local_launch();
-      if (it + 1 < iters) pr->encode_launch(ms.data(), n);
+      if (it + 1 < iters) pr->encode_launch(ms.data(), n, false);
       pr->decode_local_finish();
     }
     return PSF_OK;

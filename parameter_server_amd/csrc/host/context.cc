@@ -387,6 +387,7 @@ Context::~Context() {
   dev_records_.clear();
   tracked_.clear();
   for (hipEvent_t e : events_) (void)hipEventDestroy(e);
+  for (hipEvent_t e : markers_) (void)hipEventDestroy(e);
   (void)hipHostFree(lazy_h_);
   (void)hipFree(d_partials_);
   (void)hipFree(zero_base_);
@@ -473,6 +474,22 @@ hipEvent_t Context::take_event() {
 
 void Context::give_event(hipEvent_t e) {
   if (e) events_.push_back(e);
+}
+
+hipEvent_t Context::take_marker() {
+  if (!markers_.empty()) {
+    hipEvent_t e = markers_.back();
+    markers_.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  DeviceScope ds(device_);
+  PSF_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence));
+  return e;
+}
+
+void Context::give_marker(hipEvent_t e) {
+  if (e) markers_.push_back(e);
 }
 
 void Context::wait_event(hipEvent_t e, int w) {

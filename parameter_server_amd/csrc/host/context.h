@@ -163,6 +163,11 @@ class Context {
   // pooled timing-free events
   hipEvent_t take_event();
   void give_event(hipEvent_t e);
+  // events the host only polls for completion (no data read through them):
+  // recorded without the system-scope fence, which costs the stream about
+  // 2 us more per record (tools/event_gap_probe.hip)
+  hipEvent_t take_marker();
+  void give_marker(hipEvent_t e);
 
   void* partials() const { return d_partials_; }
   FfFusedCtl* fused() { return fused_.ctl ? &fused_ : nullptr; }  // ff_fused_batch's counters
@@ -280,6 +285,7 @@ class Context {
   Slot* m_slots_ = nullptr;
   uint32_t ticket_ = 0;
   std::vector<hipEvent_t> events_;
+  std::vector<hipEvent_t> markers_;
   void* zero_base_ = nullptr;
   FfFusedCtl fused_;
   int32_t* sticky_h_ = nullptr;  // fused_.sticky's host side

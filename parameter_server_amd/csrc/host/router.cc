@@ -15,7 +15,7 @@ PushRouter::PushRouter(Context* ctx, const std::vector<KeyRange>& ranges, int ra
 }
 
 PushRouter::~PushRouter() {
-  if (step_start_) ctx_->give_event(step_start_);
+  if (step_start_) ctx_->give_marker(step_start_);
 }
 
 // The key width SliceKOFVMessage<K> slices with (message.h:107-147): the
@@ -63,7 +63,7 @@ static bool side_slice_mode() {
   return on;
 }
 
-void PushRouter::encode_launch(const Message* const* streams, int n) {
+void PushRouter::encode_launch(const Message* const* streams, int n, bool origin) {
   t_launch_ = now_ns();
   results_.clear();
   enc_.clear();
@@ -74,8 +74,11 @@ void PushRouter::encode_launch(const Message* const* streams, int n) {
   // where the main stream stands before this step's encode: the next step's
   // slicing (prefetch) waits for this point only -- everything the callers
   // enqueued before, not this step's encode and decode
-  if (ctx_->device() >= 0 && side_slice_mode()) {  // (a host-only context slices on the host)
-    if (!step_start_) step_start_ = ctx_->take_event();
+  // (origin false: the multi-step driver's later steps, between which the
+  // caller enqueues nothing -- the first step's point still orders them, and a
+  // marker in the stream costs it ~3 us, tools/event_gap_probe.hip)
+  if (ctx_->device() >= 0 && side_slice_mode() && (origin || !step_start_)) {  // (a host-only context slices on the host)
+    if (!step_start_) step_start_ = ctx_->take_marker();
     PSF_HIP_CHECK(hipEventRecord(step_start_, ctx_->stream()));
   }
   std::unique_ptr<SliceJob> job;

@@ -37,7 +37,9 @@ class PushRouter {
   // whose COMPRESSING launches stay in flight, and the wait for them plus the
   // delivery split (the multi-step driver queues the next step's slicing in
   // between)
-  void encode_launch(const Message* const* streams, int n);
+  // origin: record where the main stream stands for the next prefetch
+  // (false only for the multi-step driver's steps after its first)
+  void encode_launch(const Message* const* streams, int n, bool origin = true);
   void encode_finish(int64_t* sizes);
   // Launch the slicing pass of the NEXT encode() of the same streams now
   // (called once this step's encode launches are queued, so the pass runs

@@ -142,7 +142,7 @@ void SnappyBatch::launch(size_t b, size_t e) {
                                             c_.pub_dev(0), z, &t.t);
         if (st != kOk) c_.zero_pair_unused(Context::kZeroUncompress, z);
         if (st == kOk) {
-          t.done = c_.take_event();
+          t.done = c_.take_marker();
           PSF_HIP_CHECK(hipEventRecord(t.done, c_.stream()));
           t.jobs = di;
           tails_.push_back(std::move(t));
@@ -200,7 +200,7 @@ void SnappyBatch::finish() {
         if (spin > 4096) sched_yield();
       }
     }
-    c_.give_event(t.done);
+    c_.give_marker(t.done);
     if (!all) {
       const int st = snappy_uncompress_tail_launch(&t.t, c_.stream());
       if (st != kOk) throw CheckError(st, "snappy uncompress launch failed");

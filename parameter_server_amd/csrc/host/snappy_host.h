@@ -62,7 +62,10 @@ class SnappyBatch {
   // rest is launched at finish() unless every stream published its verdict
   struct Tail {
     SnappyTail t;
-    hipEvent_t done = nullptr;  // recorded after the fast path
+    // recorded after the fast path (a marker: polled beside the publish
+    // slots; if it completes before a verdict shows, the tail kernels run and
+    // find the stream decoded)
+    hipEvent_t done = nullptr;
     std::vector<size_t> jobs;
     Buffer scratch;             // alive until the tail has been launched
   };
