@@ -100,6 +100,8 @@ def parse(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--prof-stride", type=int, default=0,
+                    help="time every k-th launch of the dominant kernel in the timed region (0: the config's default)")
     ap.add_argument("--no-128m", action="store_true", help="c2: skip the configs[1] 2^27 measurement")
     ap.add_argument("--no-c4", action="store_true",
                     help="c2: skip the companion C4 measurement (cross-range spill) reported as config_c4")
@@ -506,10 +508,12 @@ def main():
         ctx.profile(False)
     dom = max(diag, key=lambda k: diag[k][1]) if diag else None
 
-    # timed region: events only around the dominant kernel (live roofline);
-    # in the many-small-message configs only every 8th launch of it, so the
-    # event pairs do not dominate a step of short kernels
-    stride = 8 if args.config in ("c1", "c4") else 1
+    # timed region: events only around the dominant kernel (live roofline),
+    # on every 4th launch of it (every 8th in the many-small-message configs):
+    # a launch with start / stop events costs the stream a few us around the
+    # kernel (stride 1 against 4, tools/ab_stride.sh r05o: C3 3272 -> 3324,
+    # C5 1684 -> 1701, C5 + COMPRESSING 1383 -> 1391 GiB/s; C2 equal)
+    stride = args.prof_stride or (8 if args.config in ("c1", "c4") else 4)
     router = extra.get("router")
     if router is not None and router.exchange is not None:
         router.exchange.bytes_sent = 0
