@@ -348,11 +348,12 @@ int psf_snappy_uncompress(psf_context* ctx, const void* d_in, size_t n, void* d_
     hipEvent_t done = c.take_marker();
     PSF_HIP_CHECK(hipEventRecord(done, c.stream()));
     bool published = false;
+    const bool force = psf::snappy_force_tail();
     for (uint64_t spin = 0;; ++spin) {
-      if ((published = __atomic_load_n(&c.pub_host(0)->ticket, __ATOMIC_ACQUIRE) == ticket)) break;
+      if (!force && (published = __atomic_load_n(&c.pub_host(0)->ticket, __ATOMIC_ACQUIRE) == ticket)) break;
       const hipError_t q = hipEventQuery(done);
       if (q == hipSuccess) {
-        published = __atomic_load_n(&c.pub_host(0)->ticket, __ATOMIC_ACQUIRE) == ticket;
+        published = !force && __atomic_load_n(&c.pub_host(0)->ticket, __ATOMIC_ACQUIRE) == ticket;
         break;
       }
       if (q != hipErrorNotReady) {

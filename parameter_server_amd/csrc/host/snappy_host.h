@@ -9,6 +9,9 @@
 namespace psf {
 
 uint32_t snappy_parse_header(const uint8_t* p, size_t n, uint64_t* len);
+// tests: the uncompress's tail kernels run even when the fast path published
+// every verdict (psf_debug_force_snappy_tail)
+bool snappy_force_tail();
 // header of a (device or host) buffer; 0 when malformed
 uint32_t snappy_read_header(Context& c, const Buffer& in, uint64_t* len);
 

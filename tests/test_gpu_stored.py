@@ -268,3 +268,49 @@ def test_compress_stored_in_place_scan_path(ctx, port):
     got = buf[:out_len.value].cpu().numpy().tobytes()
     ok = got == want
     assert ok, (len(got), len(want))
+
+
+def test_uncompress_tail_after_decoded_fast_path(ctx, port):
+    """The uncompress's completion marker carries no system-scope fence, so the
+    host may see it before the fast path's verdicts and launch the tail
+    kernels for streams the fast path already decoded.  Forced here for every
+    batch (psf_debug_force_snappy_tail): the tail must leave such streams as
+    they are -- the fused FIXING_FLOAT decode of stored streams (with a
+    compressible fragment, so one fragment sits off its assumed place) and the
+    C ABI's single-stream uncompress of stored and tag-dense streams."""
+    import ctypes as C
+    from parameter_server_amd import lib
+    from parameter_server_amd import filter as F
+    L = lib()
+    L.psf_debug_force_snappy_tail.argtypes = [C.c_int]
+    L.psf_debug_force_snappy_tail.restype = C.c_int
+    F.set_clock(SEED)
+    assert L.psf_debug_force_snappy_tail(1) == 0
+    try:
+        cases = [("random", 6 * 65536 + 77, 1, np.float32), ("onecomp", 12 * 65536 + 333, 1, np.float32),
+                 ("everyother", 9 * 65536 + 1234, 1, np.float32), ("random", 3 * 32768 + 2049, 2, np.float32)]
+        xs = [_values(kind, n, dt, 900 + k, nb) for k, (kind, n, nb, dt) in enumerate(cases)]
+        msgs = [_msg(F, x, c[2]) for x, c in zip(xs, cases)]
+        snd = [F.RemoteNode(ctx) for _ in msgs]
+        F.RemoteNode.encode_many(snd, msgs)
+        ctx.sync()
+        clones = [m.clone() for m in msgs]
+        rcv = [F.RemoteNode(ctx) for _ in msgs]
+        F.RemoteNode.decode_many(rcv, clones)
+        ctx.sync()
+        for x, c, m, w, r in zip(xs, cases, msgs, clones, rcv):
+            stream, dec = _want(port, x, c[2])
+            vp, vn, vl = m.value_ptr(0)
+            assert F.copy_out(vp, vn, vl, "cuda:0").cpu().numpy().tobytes() == stream, c
+            assert r.value(w, 0).cpu().numpy().tobytes() == dec, c
+            # the single-stream C ABI path
+            back = ctx.snappy_uncompress(torch.from_numpy(np.frombuffer(stream, np.uint8).copy()).cuda())
+            st, codes, _, _ = port.ff_encode(x, c[2], SEED)
+            assert back.cpu().numpy().tobytes() == codes.tobytes(), c
+        keys = np.sort(np.random.default_rng(3).integers(0, 10**9, 300000, dtype=np.uint64)).tobytes()
+        z = port.snappy_compress(keys)
+        back = ctx.snappy_uncompress(torch.from_numpy(np.frombuffer(z, np.uint8).copy()).cuda())
+        assert back.cpu().numpy().tobytes() == keys
+    finally:
+        assert L.psf_debug_force_snappy_tail(0) == 0
+        F.set_clock(None)
