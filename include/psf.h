@@ -474,7 +474,43 @@ int psf_exchange_create(psf_context* ctx, int rank, int world, const char* name,
                         uint64_t meta_cap, uint64_t host_cap, psf_exchange** out);
 int psf_exchange_destroy(psf_exchange* ex);
 int psf_exchange_stats(psf_exchange* ex, int64_t* out);
+/* out[4] = {data bytes handed to ncclSend, ncclSend calls, data bytes copied
+ * by the runtime instead (the self slice; PSF_EXCHANGE_HOST: the mailbox
+ * copies), 1 if a step failed on this rank (every later call fails at once,
+ * and so do the peers' waits)} */
+int psf_exchange_data_stats(psf_exchange* ex, int64_t* out);
+/* the router keeps a reference: the exchange may be destroyed first */
 int psf_router_set_exchange(psf_router* r, psf_exchange* ex);
+
+/* ---- the pull leg of the partition (CS-2) --------------------------------
+ * A pull of every stream's keys from the server group, answered per server
+ * range and merged back into key order -- Executor::Submit of the request
+ * (executor.cc:108-147), Parameter::ProcessRequest on each server
+ * (parameter.cc:5-31: the response is a copy of the request and
+ * KVMap::GetValue appends the values, kv_map.h:69-77), Executor::Reply
+ * (executor.cc:150-167: task.request = false, encoded on the server's node
+ * for the requester), and KVVector::SetValue on the requester
+ * (kv_vector.h:129-212: the response's values matched into the stream's
+ * zeroed key-ordered array).  Each request template has task.request = 1,
+ * param.push = 0, UINT64 keys, no values, and its own key_channel.
+ * psf_router_set_store: the KV map of this rank's servers (the router keeps
+ * a reference).  psf_router_pull: `iters` whole pulls (native exchange, or a
+ * world-1 router).  A caller-driven exchange instead runs
+ * psf_router_pull_encode -> psf_router_fill -> all-to-all-v ->
+ * psf_router_pull_serve -> psf_router_fill -> all-to-all-v ->
+ * psf_router_pull_finish (sizes as psf_router_encode's).  Results: per
+ * request stream, a message with its keys and one FLOAT value array in key
+ * order (psf_router_pulled; a new handle), until the next pull.  With
+ * psf_router_keep_encoded(1), psf_router_encoded lists the encoded requests
+ * this rank sent and the encoded responses its servers sent
+ * (task.request tells them apart). */
+int psf_router_set_store(psf_router* r, psf_kvmap* store);
+int psf_router_pull(psf_router* r, psf_message* const* requests, int n, int iters);
+int psf_router_pull_encode(psf_router* r, psf_message* const* requests, int n, int64_t* sizes);
+int psf_router_pull_serve(psf_router* r, const void* recvbuf, const int64_t* sizes_in, int64_t* sizes);
+int psf_router_pull_finish(psf_router* r, const void* recvbuf, const int64_t* sizes_in);
+int psf_router_num_pulled(psf_router* r);
+int psf_router_pulled(psf_router* r, int i, int32_t* stream, psf_message** out);
 
 /* ---- host-side accounting ----------------------------------------------
  * Host time blocked on the device, by cause: PSF_WAIT_SYNC stream

@@ -160,6 +160,14 @@ SIGNATURES = {
     "psf_exchange_destroy": ([vp], C.c_int),
     "psf_exchange_stats": ([vp, C.POINTER(C.c_int64)], C.c_int),
     "psf_router_set_exchange": ([vp, vp], C.c_int),
+    "psf_exchange_data_stats": ([vp, C.POINTER(C.c_int64)], C.c_int),
+    "psf_router_set_store": ([vp, vp], C.c_int),
+    "psf_router_pull": ([vp, C.POINTER(vp), C.c_int, C.c_int], C.c_int),
+    "psf_router_pull_encode": ([vp, C.POINTER(vp), C.c_int, C.POINTER(C.c_int64)], C.c_int),
+    "psf_router_pull_serve": ([vp, vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64)], C.c_int),
+    "psf_router_pull_finish": ([vp, vp, C.POINTER(C.c_int64)], C.c_int),
+    "psf_router_num_pulled": ([vp], C.c_int),
+    "psf_router_pulled": ([vp, C.c_int, C.POINTER(i32), C.POINTER(vp)], C.c_int),
     "psf_profile_enable": ([vp, C.c_int], C.c_int),
     "psf_profile_stride": ([vp, C.c_int], C.c_int),
     "psf_profile_reset": ([vp], C.c_int),

@@ -1024,9 +1024,8 @@ int psf_exchange_create(psf_context* ctx, int rank, int world, const char* name,
 }
 int psf_exchange_destroy(psf_exchange* ex) {
   if (!ex) return PSF_OK;
-  psf::Context* c = reinterpret_cast<psf::Exchange*>(ex)->context();
-  delete reinterpret_cast<psf::Exchange*>(ex);
-  psf::Context::unref(c);
+  // deleted now, or when the last router using it goes
+  psf::Exchange::unref(reinterpret_cast<psf::Exchange*>(ex));
   return PSF_OK;
 }
 int psf_exchange_stats(psf_exchange* ex, int64_t* out) {
@@ -1037,12 +1036,81 @@ int psf_exchange_stats(psf_exchange* ex, int64_t* out) {
   out[2] = e->wait_ns;
   return PSF_OK;
 }
+int psf_exchange_data_stats(psf_exchange* ex, int64_t* out) {
+  if (!ex || !out) return PSF_ERR_ARG;
+  const psf::Exchange* e = reinterpret_cast<psf::Exchange*>(ex);
+  out[0] = e->rccl_bytes;
+  out[1] = e->rccl_sends;
+  out[2] = e->copied_bytes;
+  out[3] = e->failed() ? 1 : 0;
+  return PSF_OK;
+}
 int psf_router_set_exchange(psf_router* r, psf_exchange* ex) {
   return guarded(r ? reinterpret_cast<psf::PushRouter*>(r)->context() : nullptr, [&] {
     psf::PushRouter* pr = R(r);
     psf::Exchange* e = reinterpret_cast<psf::Exchange*>(ex);
     if (e && (e->context() != pr->context() || e->world() != pr->world())) return PSF_ERR_ARG;
     pr->set_exchange(e);
+    return PSF_OK;
+  });
+}
+int psf_router_set_store(psf_router* r, psf_kvmap* store) {
+  return guarded(r ? reinterpret_cast<psf::PushRouter*>(r)->context() : nullptr, [&] {
+    psf::PushRouter* pr = R(r);
+    if (store && store->impl->context() != pr->context()) return PSF_ERR_ARG;
+    pr->set_store(store ? store->impl : nullptr);
+    return PSF_OK;
+  });
+}
+static std::vector<const psf::Message*> msg_ptrs(psf_message* const* ms, int n) {
+  if (n < 0 || (n && !ms)) throw psf::CheckError(PSF_ERR_ARG, "bad message array");
+  std::vector<const psf::Message*> v(n);
+  for (int i = 0; i < n; ++i) {
+    if (!ms[i]) throw psf::CheckError(PSF_ERR_ARG, "null message");
+    v[i] = &ms[i]->m;
+  }
+  return v;
+}
+int psf_router_pull(psf_router* r, psf_message* const* requests, int n, int iters) {
+  return guarded(r ? reinterpret_cast<psf::PushRouter*>(r)->context() : nullptr, [&] {
+    if (iters < 0) return PSF_ERR_ARG;
+    psf::PushRouter* pr = R(r);
+    const std::vector<const psf::Message*> ms = msg_ptrs(requests, n);
+    for (int it = 0; it < iters; ++it) pr->pull_step(ms.data(), n, it == 0);
+    return PSF_OK;
+  });
+}
+int psf_router_pull_encode(psf_router* r, psf_message* const* requests, int n, int64_t* sizes) {
+  return guarded(r ? reinterpret_cast<psf::PushRouter*>(r)->context() : nullptr, [&] {
+    if (!sizes) return PSF_ERR_ARG;
+    const std::vector<const psf::Message*> ms = msg_ptrs(requests, n);
+    R(r)->pull_encode(ms.data(), n, sizes);
+    return PSF_OK;
+  });
+}
+int psf_router_pull_serve(psf_router* r, const void* recvbuf, const int64_t* sizes_in, int64_t* sizes) {
+  return guarded(r ? reinterpret_cast<psf::PushRouter*>(r)->context() : nullptr, [&] {
+    if (!sizes_in || !sizes) return PSF_ERR_ARG;
+    R(r)->pull_serve(static_cast<const uint8_t*>(recvbuf), sizes_in, sizes);
+    return PSF_OK;
+  });
+}
+int psf_router_pull_finish(psf_router* r, const void* recvbuf, const int64_t* sizes_in) {
+  return guarded(r ? reinterpret_cast<psf::PushRouter*>(r)->context() : nullptr, [&] {
+    if (!sizes_in) return PSF_ERR_ARG;
+    R(r)->pull_finish(static_cast<const uint8_t*>(recvbuf), sizes_in);
+    return PSF_OK;
+  });
+}
+int psf_router_num_pulled(psf_router* r) {
+  return guarded(r ? reinterpret_cast<psf::PushRouter*>(r)->context() : nullptr, [&] { return (int)R(r)->pulled().size(); });
+}
+int psf_router_pulled(psf_router* r, int i, int32_t* stream, psf_message** out) {
+  return guarded(r ? reinterpret_cast<psf::PushRouter*>(r)->context() : nullptr, [&] {
+    const auto& p = R(r)->pulled();
+    if (i < 0 || i >= (int)p.size() || !out) return PSF_ERR_ARG;
+    if (stream) *stream = p[i].stream;
+    *out = new psf_message{p[i].msg};
     return PSF_OK;
   });
 }
@@ -1260,10 +1328,8 @@ int psf_kvmap_create(psf_context* ctx, size_t capacity, int lr_type, double alph
 }
 int psf_kvmap_destroy(psf_kvmap* map) {
   if (!map) return PSF_OK;
-  psf::Context* c = map->ctx;
-  delete map->impl;
+  psf::KvMapFtrl::unref(map->impl);  // (drops the context reference with the map)
   delete map;
-  psf::Context::unref(c);
   return PSF_OK;
 }
 int psf_kvmap_set_value(psf_kvmap* map, const psf_message* msg) {
@@ -1307,6 +1373,12 @@ int psf_kvmap_stats(psf_kvmap* map, int64_t* nnz, double* weight_sum, double* de
 }
 
 }  // extern "C"
+
+// test knob: the RCCL exchange's self slice through ncclSend / ncclRecv to self
+extern "C" int psf_debug_exchange_self_p2p(int on) {
+  psf::set_exchange_self_p2p(on != 0);
+  return PSF_OK;
+}
 
 // diagnostic: the context's ff_fused_batch counter words (after a sync)
 extern "C" int psf_debug_fused_ctl(psf_context* ctx, uint32_t* out, int n) {

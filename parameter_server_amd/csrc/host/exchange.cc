@@ -84,7 +84,8 @@ struct Exchange::Shared {
   uint32_t world;
   uint64_t meta_cap, host_cap, box_bytes;
   std::atomic<uint32_t> attached;
-  uint8_t pad0[128 - 36];
+  std::atomic<uint32_t> failed;  // 0, or 1 + the first rank whose step failed (Exchange::fail)
+  uint8_t pad0[128 - 40];
   struct Ctl {
     std::atomic<uint64_t> posted;    // steps this rank has posted
     std::atomic<uint64_t> consumed;  // steps this rank has read from every source
@@ -109,11 +110,37 @@ Exchange::RankBox* Exchange::box(int r, int bank) const {
   return reinterpret_cast<RankBox*>(base_ + kHeader + ((uint64_t)r * 2 + bank) * box_bytes_);
 }
 
+namespace {
+std::atomic<bool> g_self_p2p{false};
+}
+void set_exchange_self_p2p(bool on) { g_self_p2p.store(on, std::memory_order_relaxed); }
+
+void Exchange::unref(Exchange* e) {
+  if (!e || e->refs.fetch_sub(1, std::memory_order_acq_rel) != 1) return;
+  Context* c = e->ctx_;
+  delete e;
+  Context::unref(c);
+}
+
+void Exchange::check_failed() const {
+  if (!failed_.empty()) throw CheckError(kErrCheck, "exchange: an earlier step failed on this rank: " + failed_);
+  const uint32_t f = sh_ ? sh_->failed.load(std::memory_order_acquire) : 0;
+  if (f) throw CheckError(kErrCheck, "exchange: rank " + std::to_string(f - 1) + " failed a step");
+}
+
+void Exchange::fail(const std::string& why) {
+  if (failed_.empty()) failed_ = why.empty() ? "unknown error" : why;
+  uint32_t none = 0;
+  if (sh_) sh_->failed.compare_exchange_strong(none, (uint32_t)rank_ + 1, std::memory_order_acq_rel);
+  gathered_ = false;
+}
+
 void Exchange::wait_until(const std::atomic<uint64_t>* v, uint64_t want, const char* what, int who) {
   if (v->load(std::memory_order_acquire) >= want) return;
   const int64_t t0 = now_ns();
   for (uint64_t spin = 0;; ++spin) {
     if (v->load(std::memory_order_acquire) >= want) break;
+    if ((spin & 255) == 0) check_failed();
     if (spin > 2048) {
       sched_yield();
       if ((spin & 1023) == 0 && (double)(now_ns() - t0) * 1e-9 > timeout_s_)
@@ -248,6 +275,7 @@ Exchange::~Exchange() {
 
 void Exchange::post(const int64_t* meta, const int64_t* pay, const uint8_t* const* records, const uint8_t* send,
                     const uint64_t* soff) {
+  check_failed();
   if (gathered_) throw CheckError(kErrArg, "exchange: post() before the last step's move()");
   const uint64_t k = step_;
   const int bank = (int)(k & 1);
@@ -291,6 +319,7 @@ void Exchange::post(const int64_t* meta, const int64_t* pay, const uint8_t* cons
 }
 
 void Exchange::gather_meta() {
+  check_failed();
   if (gathered_) return;
   const uint64_t k = step_ - 1;
   if (step_ == 0) throw CheckError(kErrArg, "exchange: gather before post");
@@ -310,6 +339,7 @@ const uint8_t* Exchange::records_in(int s) const {
 }
 
 void Exchange::move(const uint8_t* send, const uint64_t* soff, uint8_t* recv, const uint64_t* roff) {
+  check_failed();
   if (!gathered_) gather_meta();
   const uint64_t k = step_ - 1;
   const int bank = (int)(k & 1);
@@ -318,6 +348,7 @@ void Exchange::move(const uint8_t* send, const uint64_t* soff, uint8_t* recv, co
       if (!pay_in_[s]) continue;
       RankBox* b = box(s, bank);
       const uint8_t* h = b->records() + meta_cap_ + b->pay_off[rank_];
+      copied_bytes += pay_in_[s];
       if (ctx_->device() >= 0)
         PSF_HIP_CHECK(hipMemcpyAsync(recv + roff[s], h, (size_t)pay_in_[s], hipMemcpyHostToDevice, ctx_->stream()));
       else
@@ -331,15 +362,24 @@ void Exchange::move(const uint8_t* send, const uint64_t* soff, uint8_t* recv, co
     hipStream_t st = ctx_->stream();
     PSF_HIP_CHECK(hipEventRecord(ev_sent_, st));  // the send buffer is filled
     PSF_HIP_CHECK(hipStreamWaitEvent(cstream_, ev_sent_, 0));
-    if (pay_in_[rank_])
+    // the self slice: a device copy, or (test knob) a send / recv to self in
+    // the group like every other peer's
+    const bool self_p2p = g_self_p2p.load(std::memory_order_relaxed);
+    if (pay_in_[rank_] && !self_p2p) {
       PSF_HIP_CHECK(hipMemcpyAsync(recv + roff[rank_], send + soff[rank_], (size_t)pay_in_[rank_],
                                    hipMemcpyDeviceToDevice, cstream_));
+      copied_bytes += pay_in_[rank_];
+    }
     const Rccl& R = rccl();
     ncclComm_t c = static_cast<ncclComm_t>(comm_);
     nccl_check(R.group_start(), "ncclGroupStart");
     for (int p = 0; p < world_; ++p) {
-      if (p == rank_) continue;
-      if (mine->pay[p]) nccl_check(R.send(send + soff[p], (size_t)mine->pay[p], ncclUint8, p, c, cstream_), "ncclSend");
+      if (p == rank_ && !self_p2p) continue;
+      if (mine->pay[p]) {
+        nccl_check(R.send(send + soff[p], (size_t)mine->pay[p], ncclUint8, p, c, cstream_), "ncclSend");
+        rccl_bytes += mine->pay[p];
+        ++rccl_sends;
+      }
       if (pay_in_[p]) nccl_check(R.recv(recv + roff[p], (size_t)pay_in_[p], ncclUint8, p, c, cstream_), "ncclRecv");
     }
     nccl_check(R.group_end(), "ncclGroupEnd");

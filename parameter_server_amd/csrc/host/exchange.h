@@ -43,6 +43,14 @@ class Exchange {
   Exchange(Context* ctx, int rank, int world, const std::string& path, Transport t, const void* nccl_id,
            uint64_t meta_cap, uint64_t host_cap);
   ~Exchange();
+  // Lifetime (as Context's): the C ABI's handle holds one reference, a router
+  // using the exchange one more (psf_router_set_exchange); the last unref
+  // deletes the exchange and drops its context reference.
+  std::atomic<int> refs{1};
+  static void ref(Exchange* e) {
+    if (e) e->refs.fetch_add(1, std::memory_order_relaxed);
+  }
+  static void unref(Exchange* e);
   Context* context() const { return ctx_; }
   int rank() const { return rank_; }
   int world() const { return world_; }
@@ -69,16 +77,27 @@ class Exchange {
   // the context's stream waits (on the device) for move()'s data; the work
   // queued on it between move() and join_data() overlaps the transfer
   void join_data();
+  // A step that failed between post() and move() leaves the mailbox
+  // protocol broken for every rank: fail() marks this exchange and the
+  // mailbox failed, so the next call here -- and every peer's next wait --
+  // throws at once (naming the rank and the cause) instead of timing out.
+  void fail(const std::string& why);
+  bool failed() const { return !failed_.empty(); }
 
   int64_t bytes_sent = 0;  // data + Task records posted for other ranks
   int64_t steps = 0;
   int64_t wait_ns = 0;     // host time in mailbox waits
+  // data-path accounting: bytes handed to ncclSend and the send calls made
+  // (kRccl), bytes copied by the runtime instead (the self slice; kHost:
+  // the mailbox copies in)
+  int64_t rccl_bytes = 0, rccl_sends = 0, copied_bytes = 0;
 
   struct Shared;   // the mailbox header (exchange.cc)
   struct RankBox;  // one bank of one rank
 
  private:
   RankBox* box(int r, int bank) const;
+  void check_failed() const;
   void wait_until(const std::atomic<uint64_t>* v, uint64_t want, const char* what, int who);
 
   Context* ctx_;
@@ -93,6 +112,7 @@ class Exchange {
   bool gathered_ = false;
   std::vector<int64_t> meta_in_, pay_in_;
   double timeout_s_ = 120.0;
+  std::string failed_;
   // kRccl
   void* comm_ = nullptr;
   hipStream_t cstream_ = nullptr;
@@ -102,5 +122,11 @@ class Exchange {
 // The 128-byte ncclUniqueId of a new RCCL communicator (rank 0 makes it,
 // every rank passes it to Exchange).  Loads librccl on first use.
 void rccl_unique_id(void* out128);
+
+// Test knob (psf_debug_exchange_self_p2p): a kRccl exchange sends the self
+// slice through ncclSend / ncclRecv to its own rank inside the step's group
+// instead of a device copy, so a world-1 loopback run executes the grouped
+// point-to-point path the node's other ranks take.
+void set_exchange_self_p2p(bool on);
 
 }  // namespace psf

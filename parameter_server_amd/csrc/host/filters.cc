@@ -463,7 +463,29 @@ void FixingFloatFilter::decode_messages(Context* ctx, std::vector<FfMessage>& ms
     j.elems = j.in.bytes / (size_t)j.nb;
     out_bytes[q] = j.elems * (j.type == kFloat ? 4 : 8);
   }
-  alloc_outputs(ctx, jobs, 0, jobs.size(), out_bytes);
+  // outputs: the message's destination for the array when it names one of
+  // the right size (Message::value_dest), else library memory
+  std::vector<size_t> need;
+  std::vector<size_t> need_bytes;
+  for (size_t q = 0; q < jobs.size(); ++q) {
+    FfJob& j = jobs[q];
+    const Buffer* d = (size_t)j.i < j.msg->value_dest.size() ? &j.msg->value_dest[j.i] : nullptr;
+    if (d && d->ptr && d->loc == Loc::kDevice && d->bytes == out_bytes[q]) {
+      j.out = *d;
+    } else {
+      need.push_back(q);
+      need_bytes.push_back(out_bytes[q]);
+    }
+  }
+  if (need.size() == jobs.size()) {
+    alloc_outputs(ctx, jobs, 0, jobs.size(), out_bytes);
+  } else if (!need.empty()) {
+    std::vector<FfJob> tmp;
+    tmp.reserve(need.size());
+    for (size_t q : need) tmp.push_back(jobs[q]);
+    alloc_outputs(ctx, tmp, 0, tmp.size(), need_bytes);
+    for (size_t t = 0; t < need.size(); ++t) jobs[need[t]].out = tmp[t].out;
+  }
   auto one = [&](size_t q) {
     FfJob& j = jobs[q];
     int s = ff_decode_launch(j.in.ptr, j.elems, j.type, j.nb, j.range, j.fp->min_value, j.fp->max_value,

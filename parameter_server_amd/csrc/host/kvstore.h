@@ -29,6 +29,20 @@ class KvMapFtrl {
     uint64_t size;
   };
   KvMapFtrl(Context* ctx, size_t capacity, const FtrlConfig& conf);
+  // Lifetime (as Context's): the C ABI's handle holds one reference, a router
+  // serving pulls from the map one more; the last unref deletes the map and
+  // drops its context reference.
+  std::atomic<int> refs{1};
+  static void ref(KvMapFtrl* m) {
+    if (m) m->refs.fetch_add(1, std::memory_order_relaxed);
+  }
+  static void unref(KvMapFtrl* m) {
+    if (!m || m->refs.fetch_sub(1, std::memory_order_acq_rel) != 1) return;
+    Context* c = m->ctx_;
+    delete m;
+    Context::unref(c);
+  }
+  Context* context() const { return ctx_; }
 
   // KVMap::SetValue (kv_map.h:80-91) of a push message: keys + one value array
   void set_value(const Message& msg);

@@ -189,6 +189,12 @@ struct Message {
   // value arrays whose FIXING_FLOAT decode already ran, fused into the
   // COMPRESSING decode before it (decode_batch); empty, or one per value array
   std::vector<uint8_t> predecoded;
+  // where a FIXING_FLOAT decode writes value array i (empty, or one entry per
+  // value array; an entry of the decoded size names device memory the caller
+  // owns -- e.g. the array's place in a pull's key-ordered result -- and any
+  // other entry is ignored).  Only a hint: the decode that cannot use it
+  // allocates, and the caller checks where value[i] landed.
+  std::vector<Buffer> value_dest;
   bool key_frame_seen = false;          // Van::Recv bookkeeping (psf_msg_recv_frame)
 
   bool is_pending(size_t i) const { return i < pending.size() && pending[i].nb != 0; }

@@ -11,8 +11,11 @@
 #include <utility>
 #include <vector>
 
+#include <functional>
+
 #include "exchange.h"
 #include "filter.h"
+#include "kvstore.h"
 #include "slice.h"
 #include "spill.h"
 
@@ -66,12 +69,56 @@ class PushRouter {
   // the data moved (RCCL, on the exchange's stream) while the local slices
   // decode, then the received slices decoded where they landed.  No host
   // wait on the device except COMPRESSING's lengths.
-  void set_exchange(Exchange* ex) { ex_ = ex; }
+  // (the router holds a reference: the exchange outlives it whatever the
+  // order the handles are destroyed in)
+  void set_exchange(Exchange* ex) {
+    Exchange::ref(ex);
+    Exchange::unref(ex_);
+    ex_ = ex;
+  }
   Exchange* exchange() const { return ex_; }
   bool loopback() const { return loopback_; }
   void exchange_step();
   // unpack a receive buffer (segments of ranks 0..world-1) and decode it
   void decode_received(const uint8_t* recvbuf, const int64_t* sizes_in);
+
+  // ---- the pull leg (SURVEY.md §3 CS-2, §8(e) "on the pull side") ----
+  // A pull of every stream's keys from the server group: each request is
+  // sliced at the server ranges and encoded on the sender's per-(stream,
+  // server) node (Executor::Submit, executor.cc:108-147); each server decodes
+  // its slice on its per-(server, stream) node, answers it as
+  // Parameter::ProcessRequest does for a pull (parameter.cc:5-31: the
+  // response is a copy of the request, KVMap::GetValue appends the values,
+  // kv_map.h:69-77) and encodes the response on that same node with
+  // task.request = false (Executor::Reply, executor.cc:150-167) -- KEY_CACHING
+  // hits and elides the keys, FIXING_FLOAT computes the slice's own min/max;
+  // the response travels back to the requesting rank, which decodes it on the
+  // node that sent the request (keys restored from its cache) and merges it
+  // into the stream's key-ordered value array (KVVector::SetValue,
+  // kv_vector.h:129-212: ParallelOrderedMatch of the slice's sorted keys into
+  // the stream's zeroed array -- the slice is a contiguous run of those keys,
+  // so the match is the run's offset; the FIXING_FLOAT decode writes there
+  // directly).
+  // store: the KVMap of this rank's servers (the router holds a reference)
+  void set_store(KvMapFtrl* store) {
+    KvMapFtrl::ref(store);
+    KvMapFtrl::unref(store_);
+    store_ = store;
+  }
+  KvMapFtrl* store() const { return store_; }
+  // one whole pull step: through the native exchange (any world), or all
+  // local (world 1 without loopback)
+  void pull_step(const Message* const* reqs, int n, bool origin = true);
+  // the same in three phases around a caller-driven all-to-all-v (sizes as
+  // encode(); fill() writes each send buffer): the requests out, the
+  // requests served and the responses out, the responses merged
+  void pull_encode(const Message* const* reqs, int n, int64_t* sizes);
+  void pull_serve(const uint8_t* recvbuf, const int64_t* sizes_in, int64_t* sizes);
+  void pull_finish(const uint8_t* recvbuf, const int64_t* sizes_in);
+  // per requesting stream: its keys and the pulled values in key order
+  // (value_type FLOAT), valid until the next pull
+  struct Pulled { int32_t stream; Message msg; };
+  const std::vector<Pulled>& pulled() const { return pulled_; }
 
   // decoded messages of the last step: (server, message)
   const std::vector<std::pair<int, Message>>& results() const { return results_; }
@@ -88,9 +135,29 @@ class PushRouter {
   RemoteNode* sender(int32_t stream, int server);
   RemoteNode* receiver(int server, int32_t stream);
   void decode_into_results(std::vector<Message>& ms, const std::vector<int>& servers);
+  // messages received in one exchange round: (message, server, source rank)
+  struct Inbox {
+    std::vector<Message> msgs;
+    std::vector<int> server, src;
+  };
+  // One round of the native exchange: out[i] to rank dest[i] for server
+  // srv[i]; `beside` is queued while the data moves; the received messages
+  // are appended to *in with their data joined on the context's stream.
+  // own_servers: a received server must be this rank's (requests); else it
+  // must be the source rank's (pull responses).
+  void exchange_round(const std::vector<Message*>& out, const std::vector<int>& dest, const std::vector<int>& srv,
+                      const std::function<void()>& beside, Inbox* in, bool own_servers);
+  void check_inbox(const Inbox& in, size_t from, bool own_servers) const;
+  // pull phases (see pull_step)
+  void pull_begin(const Message* const* reqs, int n, bool origin, Inbox* local, std::vector<Message*>* remote,
+                  std::vector<int>* dest, std::vector<int>* rsrv);
+  void pull_answer(Inbox& reqs, Inbox* local, std::vector<Message>* resp, std::vector<Message*>* remote,
+                   std::vector<int>* dest, std::vector<int>* rsrv);
+  void pull_merge(Inbox& resp);
 
   Context* ctx_;
   Exchange* ex_ = nullptr;
+  KvMapFtrl* store_ = nullptr;
   std::vector<KeyRange> ranges_;
   int rank_, world_;
   bool loopback_;
@@ -106,6 +173,18 @@ class PushRouter {
   // the step between encode_launch and encode_finish
   std::vector<Message> slices_;
   std::vector<int> srv_;
+  // per slice: its stream (index into the step's streams), first key and
+  // key count within the stream's key array
+  std::vector<int> sl_stream_;
+  std::vector<uint64_t> sl_koff_, sl_nkeys_;
+  // the pull in progress: (stream channel, server) -> (stream index, slice)
+  std::map<std::pair<int32_t, int>, std::pair<int, size_t>> ppos_;
+  std::vector<uint64_t> pout_off_;  // per stream: its array's offset in pout_
+  Buffer pout_;
+  std::vector<Pulled> pulled_;
+  std::vector<uint64_t> pl_koff_, pl_nkeys_;  // the pull's slices (copies of sl_*)
+  Inbox preq_local_, presp_local_;  // the caller-driven pull's local deliveries
+  std::vector<Message> presp_;      // its responses (sent from plan_)
   PendingEncode pend_;
   int64_t t_launch_ = 0;
   // the step whose decode is in flight (decode_local_launch .. _finish); its

@@ -295,9 +295,10 @@ void spill_unpack_host(Context* ctx, const uint8_t* meta, uint64_t mlen, const B
 }
 
 int spill_unpack(Context* ctx, const Buffer& rbuf, int world, const int64_t* sizes, std::vector<Message>* out,
-                 std::vector<int>* servers) {
+                 std::vector<int>* servers, std::vector<int>* srcs) {
   out->clear();
   servers->clear();
+  if (srcs) srcs->clear();
   const uint8_t* recv = rbuf.ptr;
   uint64_t at = 0;
   std::vector<uint8_t> meta;
@@ -354,9 +355,31 @@ int spill_unpack(Context* ctx, const Buffer& rbuf, int world, const int64_t* siz
       }
       while (f < fl.size()) m.value.push_back(frame());
       servers->push_back((int)h[1]);
+      if (srcs) srcs->push_back(s);
     }
   }
   return (int)out->size();
+}
+
+void device_copies(Context* ctx, const std::vector<DeviceCopy>& copies, uint8_t* dst) {
+  if (copies.empty()) return;
+  if (ctx->device() < 0) {
+    for (const DeviceCopy& c : copies) memcpy(dst + c.dst_off, c.src, c.len);
+    return;
+  }
+  std::vector<SpillCopy> tbl(copies.size());
+  uint64_t chunk = 0;
+  for (size_t k = 0; k < copies.size(); ++k) {
+    tbl[k] = SpillCopy{copies[k].src, copies[k].dst_off, copies[k].len, chunk};
+    chunk += (copies[k].len + kSpillChunk - 1) / kSpillChunk;
+  }
+  const size_t bytes = tbl.size() * sizeof(SpillCopy);
+  Buffer d = ctx->alloc(bytes);
+  hipStream_t st = ctx->stream();
+  PSF_HIP_CHECK(hipMemcpyAsync(d.ptr, tbl.data(), bytes, hipMemcpyHostToDevice, st));
+  // (pageable source: the runtime has staged it when the call returns)
+  int s = spill_gather_launch(reinterpret_cast<const SpillCopy*>(d.ptr), (int)tbl.size(), chunk, dst, st);
+  if (s != kOk) throw CheckError(s, "device copy gather launch failed");
 }
 
 }  // namespace psf

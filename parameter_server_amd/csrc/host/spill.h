@@ -50,8 +50,16 @@ class SpillPlan {
 // sources 0..world-1 back to back, sizes as the senders reported them).  The
 // messages' frames point into `recv` and share its owner (recv.owner null:
 // the caller keeps the memory alive).
+// srcs (optional): the source rank of each message
 int spill_unpack(Context* ctx, const Buffer& recv, int world, const int64_t* sizes, std::vector<Message>* out,
-                 std::vector<int>* servers);
+                 std::vector<int>* servers, std::vector<int>* srcs = nullptr);
+// a table of device copies (src, dst_off, len) into dst, in one gather launch
+// on the context's stream (the sources must stay alive until it has run)
+struct DeviceCopy {
+  const uint8_t* src;
+  uint64_t dst_off, len;
+};
+void device_copies(Context* ctx, const std::vector<DeviceCopy>& copies, uint8_t* dst);
 // The receive side of a host_meta plan: rank s's records (host memory, mlen
 // bytes) describe the data at [pay_at, pay_at + plen) of `recv`; the messages
 // are appended to out / servers with their frames pointing into `recv`

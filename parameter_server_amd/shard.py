@@ -230,6 +230,14 @@ class NativeExchange:
         check(lib().psf_exchange_stats(self.h, out))
         return {"bytes_sent": out[0], "steps": out[1], "wait_s": out[2] / 1e9}
 
+    def data_stats(self) -> dict:
+        """the data path: bytes handed to ncclSend and the send calls made
+        (rccl), bytes the runtime copied instead (the self slice, or the
+        host mailbox), and whether a step failed on this rank"""
+        out = (C.c_int64 * 4)()
+        check(lib().psf_exchange_data_stats(self.h, out))
+        return {"rccl_bytes": out[0], "rccl_sends": out[1], "copied_bytes": out[2], "failed": bool(out[3])}
+
     @property
     def bytes_sent(self) -> int:
         """records + data posted for other ranks since the last reset (set to 0)"""
@@ -319,6 +327,55 @@ class PushRouter:
         recv = ex.move(list(sizes), sizes_in, after_send=lambda: check(L.psf_router_decode_local(self.h)))
         check(L.psf_router_decode_received(self.h, C.c_void_p(recv.data_ptr()),
                                            (C.c_int64 * (2 * W))(*sizes_in)))
+
+    def set_store(self, kvmap) -> None:
+        """The KV map (filter.KVMap) answering the pulls addressed to this
+        rank's servers (KVMap::GetValue, kv_map.h:69-77)."""
+        self._store = kvmap
+        check(lib().psf_router_set_store(self.h, kvmap.h if kvmap is not None else None))
+
+    def pull(self, requests, steps: int = 1, keep_encoded=None) -> None:
+        """`steps` pulls of every request stream's keys ({stream id: template
+        Message with request=True, push=False, keys only}) from the server
+        group: sliced per server, answered from each server's store, merged
+        back in key order (pulled()).  One native call with a NativeExchange
+        or at world 1; else the three phases around the SpillExchange's
+        all-to-all-v."""
+        L = lib()
+        if keep_encoded is not None:
+            check(L.psf_router_keep_encoded(self.h, int(keep_encoded)))
+        hs, n = self._handles(requests)
+        if self.native or (self.world == 1 and not self.loopback):
+            check(L.psf_router_pull(self.h, hs, n, steps))
+            return
+        W, ex = self.world, self.exchange
+        for _ in range(steps):
+            sizes = (C.c_int64 * (2 * W))()
+            check(L.psf_router_pull_encode(self.h, hs, n, sizes))
+            sizes_in = ex.sizes(sizes)
+            buf = ex.send_buffer(sum(sizes))
+            check(L.psf_router_fill(self.h, C.c_void_p(buf.data_ptr())))
+            recv = ex.move(list(sizes), sizes_in)
+            out = (C.c_int64 * (2 * W))()
+            check(L.psf_router_pull_serve(self.h, C.c_void_p(recv.data_ptr()), (C.c_int64 * (2 * W))(*sizes_in),
+                                          out))
+            back_in = ex.sizes(out)
+            buf = ex.send_buffer(sum(out))
+            check(L.psf_router_fill(self.h, C.c_void_p(buf.data_ptr())))
+            recv = ex.move(list(out), back_in)
+            check(L.psf_router_pull_finish(self.h, C.c_void_p(recv.data_ptr()), (C.c_int64 * (2 * W))(*back_in)))
+
+    def pulled(self):
+        """[(stream, Message)] of the last pull: the stream's keys and one
+        float array of the pulled values in key order."""
+        from .filter import Message
+        L = lib()
+        out = []
+        for i in range(check(L.psf_router_num_pulled(self.h))):
+            st, h = C.c_int32(), C.c_void_p()
+            check(L.psf_router_pulled(self.h, i, C.byref(st), C.byref(h)))
+            out.append((st.value, Message(_handle=h)))
+        return out
 
     def host_stats(self, reset: bool = False) -> dict:
         """Host phase timers since the last reset: encodes, and seconds spent

@@ -128,6 +128,85 @@ def _run(shape, transport):
     return res
 
 
+def _pull_worker(rank, world, port, transport, q):
+    """The pull leg at world 8 (CS-2 per server range): 64 request streams
+    (8 per rank) of 2^14 keys, one server per rank answering from its own KV
+    map; a miss pull then a hit pull.  Each server rank works out, for every
+    stream, the port's decode of the port's encode of its weights for that
+    stream's slice; the expected slices reach the requesting ranks through
+    gloo (all_gather_object), which check their key-ordered arrays."""
+    import torch
+    import torch.distributed as dist
+
+    import oracle
+    from parameter_server_amd import filter as F
+    from parameter_server_amd import shard
+    from test_gpu_pull import _keys, check_encoded, check_pulled, expected_slices, make_requests, seed_store
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        STREAMS, M, S = 64, 1 << 14, world
+        sids = [s for s in range(STREAMS) if s % world == rank]
+        F.set_clock(SEED)
+        ctx = F.Context(0)
+        ranges = shard.server_ranges(S)
+        if transport == "native":
+            ex = shard.NativeExchange.create(ctx, transport="host")
+        else:
+            ex = shard.SpillExchange(ctx, device="cuda:0")
+        router = shard.PushRouter(ctx, ranges, rank, world, ex)
+        kv = F.KVMap(ctx, capacity=STREAMS * M // world * 2)
+        router.set_store(kv)
+        lo, hi = ranges[rank]
+        allk = np.concatenate([_keys(s, M) for s in range(STREAMS)])
+        seed_store(F, kv, allk[(allk >= np.uint64(lo)) & (allk < np.uint64(hi))])
+        port_ = oracle.Port()
+        mine = {s: expected_slices(kv, _keys(s, M), ranges, [rank], port_)[rank] for s in range(STREAMS)}
+        every = [None] * world
+        dist.all_gather_object(every, mine)
+        data = {s: (_keys(s, M), {d: every[d][s] for d in range(S)}) for s in sids}
+        served = {s: (None, {rank: mine[s]}) for s in range(STREAMS)}
+        reqs = make_requests(F, sids, M)
+        for step in range(2):
+            router.pull(reqs, 1, keep_encoded=True)
+            torch.cuda.synchronize()
+            check_pulled(F, router.pulled(), data, ranges)
+            nreq, nresp = check_encoded(F, router.encoded(), step, served, port_, {rank})
+            assert nreq == len(sids) * S and nresp == STREAMS, (nreq, nresp)
+        q.put((rank, True, None))
+    except Exception as e:  # report instead of hanging the parent
+        import traceback
+        q.put((rank, repr(e) + traceback.format_exc()[-2500:], None))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("transport", ["gloo", "native"])
+def test_world8_pull_same_gpu(transport):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pull_worker, args=(r, WORLD, port, transport, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in procs:
+            r, ok, _ = q.get(timeout=100)
+            res[r] = ok
+    finally:
+        for p in procs:
+            p.join(timeout=20)
+            if p.is_alive():
+                p.kill()
+    assert sorted(res) == list(range(WORLD))
+    for r in range(WORLD):
+        assert res[r] is True, (r, res[r])
+
+
 @pytest.mark.parametrize("transport", ["gloo", "native"])
 @pytest.mark.parametrize("shape", ["c4", "c5"])
 def test_world8_partition_same_gpu(shape, transport):

@@ -84,6 +84,7 @@ def _check_step(F, got, ranges, m, dim, port, expect):
         assert kgot.tobytes() == keys[sel].tobytes(), (d, sid)
         assert vgot.tobytes() == dec.tobytes(), (d, sid)
     assert seen == expect
+    assert len(got) == len(expect), "a step's results hold each (server, stream) once"
     return seen
 
 
@@ -177,13 +178,23 @@ def test_router_multi_step_driver(dim, compress, m):
 
 
 def _spill_worker(rank, world, port, backend, loopback, q, native=None):
+    import ctypes as C
+
     import torch
     import torch.distributed as dist
 
     import oracle
     from parameter_server_amd import filter as F
     from parameter_server_amd import shard
+    from parameter_server_amd._lib import lib
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    self_p2p = native == "rccl_p2p"
+    if self_p2p:
+        native = "rccl"
+        L = lib()
+        L.psf_debug_exchange_self_p2p.argtypes = [C.c_int]
+        L.psf_debug_exchange_self_p2p.restype = C.c_int
+        assert L.psf_debug_exchange_self_p2p(1) == 0
     try:
         torch.cuda.set_device(0)
         if backend == "nccl":
@@ -209,11 +220,15 @@ def _spill_worker(rank, world, port, backend, loopback, q, native=None):
             torch.cuda.synchronize()
             _check_step(F, router.results(), ranges, M, 1, port_, expect)
             sent.append(ex.bytes_sent)
+        if native:
+            sent.append(ex.data_stats())
         q.put((rank, True, sent))
     except Exception as e:  # report instead of hanging the parent
         import traceback
         q.put((rank, repr(e) + traceback.format_exc()[-1500:], None))
     finally:
+        if self_p2p:
+            L.psf_debug_exchange_self_p2p(0)
         if dist.is_initialized():
             dist.destroy_process_group()
 
@@ -236,15 +251,27 @@ def _run_ranks(world, backend, loopback, native=None):
     return res
 
 
-@pytest.mark.parametrize("native", [None, "rccl"])
+@pytest.mark.parametrize("native", [None, "rccl", "rccl_p2p"])
 def test_spill_nccl_world1_loopback(native):
     """The RCCL spill path on the device at world 1, every slice through the
     exchange: torch's all_to_all_single (the Python step), or libpsf's own
-    exchange (native: the records through the mailbox, the data by RCCL
-    point-to-point on the exchange's stream, psf_router_step)."""
+    exchange (native: the records through the mailbox, the data on the
+    exchange's stream, psf_router_step).  rccl_p2p: the self slice goes
+    through ncclSend / ncclRecv to self inside the step's group
+    (psf_debug_exchange_self_p2p) -- the grouped point-to-point code the
+    node's other ranks run (executor.cc:134-146's per-server sends) -- and
+    every decoded slice still equals the port's."""
     res = _run_ranks(1, "nccl", True, native)
     ok, sent = res[0]
     assert ok is True, ok
+    if native:
+        ds = sent[-1]
+        assert not ds["failed"]
+        if native == "rccl_p2p":
+            # every data byte of both steps went through ncclSend, none copied
+            assert ds["rccl_sends"] == 2 and ds["rccl_bytes"] > 0 and ds["copied_bytes"] == 0, ds
+        else:
+            assert ds["rccl_sends"] == 0 and ds["copied_bytes"] > 0, ds
 
 
 @pytest.mark.parametrize("native", [None, "host"])
