@@ -354,3 +354,77 @@ def test_push_router_u32_keys_host():
     wide.set_key(torch.from_numpy(np.arange(4, dtype=np.int64)), key_type=DT_UINT64)
     with pytest.raises(PsfError):
         router.step({3: m, 6: wide})
+
+
+def _failfast_worker(rank, world, port, q):
+    import time
+
+    import torch.distributed as dist
+
+    from bench import splitmix64_keys
+    from parameter_server_amd import KEY_CACHING
+    from parameter_server_amd import filter as F
+    from parameter_server_amd import shard
+    from parameter_server_amd._lib import PsfError
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PSF_EXCHANGE_TIMEOUT_S="60")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = []
+    try:
+        ctx = F.HostContext()
+        # a misconfigured rank: rank 1 splits the key space into 4 servers,
+        # rank 0 into 2 -- rank 0's slices for its server 1 land on rank 1,
+        # which under its own split does not host a server 1
+        ranges = shard.server_ranges(2 if rank == 0 else 4)
+        ex = shard.NativeExchange.create(ctx, transport="host")
+        router = shard.PushRouter(ctx, ranges, rank, world, ex)
+        keys = splitmix64_keys(500, 4 + rank)
+        # rank 1's keys and key range in its own servers' half: it sends rank 0
+        # nothing (slices whose range misses the key range are not sent)
+        kr = shard.KEY_ALL
+        if rank == 1:
+            keys = np.unique(keys | np.uint64(1 << 63))
+            kr = (1 << 63, (1 << 64) - 1)
+        m = F.Message(request=True, push=True, key_channel=rank, key_range=kr)
+        m.set_key(torch.from_numpy(keys.view(np.int64).copy()))
+        m.add_value(torch.ones(keys.size, dtype=torch.float32))
+        m.add_filter(KEY_CACHING)
+        for step in range(3):
+            t0 = time.perf_counter()
+            try:
+                router.run({rank: m}, 1)
+                out.append(("ok", 0.0))
+            except PsfError as e:
+                out.append((str(e), time.perf_counter() - t0))
+        out.append(("stats", ex.data_stats()["failed"]))
+        q.put((rank, out))
+    except Exception as e:  # report instead of hanging the parent
+        import traceback
+        q.put((rank, repr(e) + traceback.format_exc()[-1500:]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_exchange_fails_fast_on_every_rank():
+    """A step that fails between post and move (here: a record for a server
+    the rank does not host) marks the exchange failed: the failing rank's
+    next call and the peer's next wait raise at once, naming the cause or the
+    rank, instead of hanging until PSF_EXCHANGE_TIMEOUT_S."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_failfast_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    r0, r1 = res[0], res[1]
+    assert isinstance(r1, list), r1
+    assert "does not own" in r1[0][0], r1
+    assert all("earlier step failed" in str(msg) for msg, _ in r1[1:3]), r1
+    assert r1[3] == ("stats", True), r1
+    assert isinstance(r0, list), r0
+    # rank 0's own steps are sound: its first wait on rank 1 raises at once
+    fails = [(msg, dt) for msg, dt in r0[:3] if msg != "ok"]
+    assert fails and "rank 1 failed" in fails[0][0] and all(dt < 10 for _, dt in fails), r0
