@@ -20,6 +20,7 @@
 #include <new>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
 #include <utility>
 #include <vector>
 
@@ -53,6 +54,13 @@ class StableList {
   StableList(const StableList& o) { append(o); }
   StableList& operator=(const StableList& o) {
     if (this != &o) { clear(); append(o); }
+    return *this;
+  }
+  // moving the list moves its elements (the inline ones to new addresses:
+  // stability holds while a list grows, not across a move of the list)
+  StableList(StableList&& o) noexcept { take(o); }
+  StableList& operator=(StableList&& o) noexcept {
+    if (this != &o) { clear(); take(o); }
     return *this;
   }
   ~StableList() { clear(); }
@@ -89,6 +97,13 @@ class StableList {
  private:
   void append(const StableList& o) {
     for (size_t i = 0; i < o.n_; ++i) emplace_back(o[i]);
+  }
+  void take(StableList& o) noexcept {
+    const size_t k = o.n_ < N ? o.n_ : N;
+    for (size_t i = 0; i < k; ++i) new (inl() + i) T(std::move(o.inl()[i]));
+    extra_ = std::move(o.extra_);
+    n_ = o.n_;
+    o.clear();
   }
   T* inl() { return std::launder(reinterpret_cast<T*>(buf_)); }
   const T* inl() const { return std::launder(reinterpret_cast<const T*>(buf_)); }
@@ -211,5 +226,8 @@ struct Message {
     if (!task.has_key_range) { task.has_key_range = true; task.key_range = KeyRange::All(); }
   }
 };
+// the batched drivers keep messages in vectors: growing one must move them,
+// not copy every Task (and its side-info references) again
+static_assert(std::is_nothrow_move_constructible<Message>::value, "Message moves cheaply");
 
 }  // namespace psf

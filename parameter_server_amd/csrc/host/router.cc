@@ -43,13 +43,13 @@ static int step_key_bytes(const Message* const* streams, int n) {
 }
 
 RemoteNode* PushRouter::sender(int32_t stream, int server) {
-  auto& p = senders_[{stream, server}];
+  auto& p = senders_[(uint64_t)(uint32_t)stream << 32 | (uint32_t)server];
   if (!p) p.reset(new RemoteNode(ctx_));
   return p.get();
 }
 
 RemoteNode* PushRouter::receiver(int server, int32_t stream) {
-  auto& p = receivers_[{(int32_t)server, (int)stream}];
+  auto& p = receivers_[(uint64_t)(uint32_t)server << 32 | (uint32_t)stream];
   if (!p) p.reset(new RemoteNode(ctx_));
   return p.get();
 }
@@ -94,7 +94,10 @@ void PushRouter::encode_launch(const Message* const* streams, int n, bool origin
   std::vector<std::vector<Message>> parts;
   std::vector<std::vector<bool>> ok;
   std::vector<std::vector<KeySigHint>> hints;
-  slice_end(*job, &parts, &ok, &hints);
+  {
+    PSF_HPROF(12);
+    slice_end(*job, &parts, &ok, &hints);
+  }
   job.reset();
   const int S = (int)ranges_.size();
   slices_.clear();
@@ -120,13 +123,18 @@ void PushRouter::encode_launch(const Message* const* streams, int n, bool origin
     }
   std::vector<Message*> mp(slices_.size());
   for (size_t k = 0; k < slices_.size(); ++k) mp[k] = &slices_[k];
-  encode_batch(nodes.data(), mp.data(), (int)slices_.size(), sh.data(), &pend_);
+  {
+    PSF_HPROF(13);
+    encode_batch(nodes.data(), mp.data(), (int)slices_.size(), sh.data(), &pend_);
+  }
   stat_encode_ns += now_ns() - t_launch_;
 }
 
 void PushRouter::encode_finish(int64_t* sizes) {
   const int64_t t0 = now_ns();
   pend_.finish();
+  local_.reserve(local_.size() + slices_.size());
+  local_server_.reserve(local_server_.size() + slices_.size());
   std::vector<Message*> remote;
   std::vector<int> dest, rsrv;
   for (size_t k = 0; k < slices_.size(); ++k) {
@@ -153,6 +161,7 @@ void PushRouter::encode_finish(int64_t* sizes) {
 // and decode -- the host then finds it done when the next step starts instead
 // of waiting for this step's kernels.
 void PushRouter::prefetch(const Message* const* streams, int n) {
+  PSF_HPROF(1);
   next_ = slice_begin(ctx_, std::vector<const Message*>(streams, streams + n), ranges_, step_key_bytes(streams, n),
                       step_start_);
 }
@@ -167,6 +176,8 @@ void PushRouter::exchange_step() {
   if (!ex_) throw CheckError(kErrArg, "router: no exchange");
   const int64_t t0 = now_ns();
   pend_.finish();  // COMPRESSING's lengths (the only device wait of the step)
+  local_.reserve(local_.size() + slices_.size());
+  local_server_.reserve(local_server_.size() + slices_.size());
   std::vector<Message*> remote;
   std::vector<int> dest, rsrv;
   for (size_t k = 0; k < slices_.size(); ++k) {
@@ -275,6 +286,7 @@ void PushRouter::decode_into_results(std::vector<Message>& ms, const std::vector
     mp[k] = &ms[k];
   }
   decode_batch(nodes.data(), mp.data(), (int)ms.size());
+  results_.reserve(results_.size() + ms.size());
   for (size_t k = 0; k < ms.size(); ++k) results_.emplace_back(servers[k], std::move(ms[k]));
 }
 
@@ -299,18 +311,21 @@ void PushRouter::decode_local_launch() {
     dec_nodes_[k] = receiver(dec_servers_[k], dec_msgs_[k].task.key_channel);
     dec_ptrs_[k] = &dec_msgs_[k];
   }
+  PSF_HPROF(0);
   decode_batch(dec_nodes_.data(), dec_ptrs_.data(), (int)dec_msgs_.size(), nullptr, &pend_dec_);
   stat_decode_ns += now_ns() - t0;
 }
 
 void PushRouter::decode_local_finish() {
   if (dec_msgs_.empty() && !pend_dec_.active) return;
+  PSF_HPROF(5);
   const int64_t t0 = now_ns();
   pend_dec_.finish();
   // the step's results are exactly its local decodes (the multi-step driver
   // has already queued the next step's encode_launch, which cleared results_
   // while this step's decodes were in flight: replace, never append)
   results_.clear();
+  results_.reserve(dec_msgs_.size());
   for (size_t k = 0; k < dec_msgs_.size(); ++k) results_.emplace_back(dec_servers_[k], std::move(dec_msgs_[k]));
   dec_msgs_.clear();
   dec_servers_.clear();

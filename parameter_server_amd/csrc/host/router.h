@@ -7,6 +7,7 @@
 // push streams at once, with no per-slice host work outside this library.
 #pragma once
 #include <map>
+#include <unordered_map>
 #include <memory>
 #include <utility>
 #include <vector>
@@ -162,7 +163,8 @@ class PushRouter {
   int rank_, world_;
   bool loopback_;
   bool keep_enc_ = false;
-  std::map<std::pair<int32_t, int>, std::unique_ptr<RemoteNode>> senders_, receivers_;
+  // per (stream channel, server) / (server, stream channel), keyed (a << 32) | b
+  std::unordered_map<uint64_t, std::unique_ptr<RemoteNode>> senders_, receivers_;
   std::vector<Message> local_;
   std::vector<int> local_server_;
   std::unique_ptr<SpillPlan> plan_;

@@ -29,18 +29,21 @@ def main():
     F.set_clock(12345)
     g = torch.Generator(device="cuda:0")
     g.manual_seed(1)
-    a = bench.parse(["--config", "c1"])
+    a = bench.parse(["--config", "c1"] + sys.argv[1:])
     run, payload, nloc, extra = bench.build_workload(a, F, ctx, 0, 1, "cuda:0", g, a.n)
     run(20)
     torch.cuda.synchronize()
     fn(ns, n, 1)
-    steps = 200
+    steps = 200 if a.config == "c1" else 40
     t0 = time.perf_counter()
     run(steps)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps * 1e6
     fn(ns, n, 1)
     print(f"step {dt:.1f} us")
+    if a.config in ("c4", "c5"):
+        NAMES.update({0: "router decode_batch", 1: "router prefetch (slice_begin)", 5: "router decode finish",
+                      12: "router slice_end", 13: "router encode_batch"})
     for i in range(16):
         if n[i]:
             print(f"{NAMES.get(i, i):28s} {ns[i] / steps / 1e3:8.2f} us/step  calls/step {n[i] / steps:.1f}")
