@@ -69,6 +69,12 @@ WORKLOADS = {
           "keys: pull request (keys, [KEY_CACHING, FIXING_FLOAT num_bytes={nb}]), pull response (keys elided "
           "+ f32 weights), push (keys elided + f32 gradients, [KEY_CACHING(clear_cache_if_done), "
           "FIXING_FLOAT num_bytes={nb}]), each batched over the streams",
+    "c4pull": "C4's partition on the pull side (SURVEY.md CS-2, §8(e)): {streams} pull request streams in total "
+              "(stream s on rank s % N), each {m} sorted unique uint64 keys spread over 2^64 (splitmix64), sliced "
+              "at the EvenDivide({servers}) server ranges, per-(stream, server) [KEY_CACHING, FIXING_FLOAT "
+              "num_bytes={nb}]; each server answers its slices from its KVMap (GetValue), encodes the response "
+              "(keys elided on the cache hit, min/max per slice), the requester decodes it into the stream's "
+              "key-ordered array; repeat pulls (key cache hit)",
     "c5": "C5 (BASELINE configs[4]) per GPU: one stream of {m} uint64 keys spread over 2^64 "
           "(splitmix64) + embedding rows dim=128 f32, sliced at the EvenDivide({servers}) server ranges "
           "(k = 128 values per key), per-(stream, server) [KEY_CACHING, FIXING_FLOAT num_bytes={nb}{cmp}], "
@@ -90,6 +96,8 @@ def splitmix64_keys(m: int, seed: int):
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--no-host-floor", action="store_true",
+                    help="c4 / c5: skip the host-cost run (the same step with 4096 keys per stream)")
     ap.add_argument("--steps", type=int, default=None,
                     help="timed steps (default 20; 200 for c1 / c3, whose step is 0.04-0.07 ms: 20 of them "
                          "time only about 1 ms)")
@@ -108,7 +116,7 @@ def parse(argv=None):
     ap.add_argument("--c4-m", type=int, default=1 << 21, help="c2's companion C4 line: keys per stream")
     ap.add_argument("--streams", type=int, default=64, help="c1/c4: push streams in total")
     ap.add_argument("--servers", type=int, default=8, help="c4/c5: server key ranges (>= N)")
-    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c3miss", "c4", "c5"])
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c3miss", "c4", "c4pull", "c5"])
     ap.add_argument("--m", type=int, default=None, help="keys per message (c1 1e5, c3 10M, c4 2^21, c5 2^20)")
     ap.add_argument("--compress", action="store_true", help="append COMPRESSING to the chain (c5)")
     ap.add_argument("--miss", action="store_true",
@@ -229,6 +237,35 @@ def cpu_baseline(args, nb: int):
         what = (f"{ns} ctr minibatches (pull request, pull response, push; [KEY_CACHING, "
                 f"FIXING_FLOAT(nb={nb})]) of {m} keys + f32, one core (the reference's filters run "
                 f"serialised per Customer)")
+    elif cfg == "c4pull":
+        # per slice: the request's CRC, the server's GetValue (a lookup per key
+        # in a sorted key table, numpy), the response's CRC and FIXING_FLOAT
+        # round trip (keys elided: a cache hit on both sides)
+        from parameter_server_amd import shard
+        ranges = shard.server_ranges(args.servers)
+        bounds = np.array([r[0] for r in ranges] + [ranges[-1][1]], dtype=np.uint64)
+        m = args.m or (1 << 21)
+        nstreams = min(args.streams, CPU_THREADS_MAX)
+        tk = np.unique(np.concatenate([splitmix64_keys(m, 4 + s) for s in range(nstreams)]))
+        tw = rng.standard_normal(tk.size).astype(np.float32)
+
+        def pull_slice(keys):
+            def f():
+                P.key_signature(keys)  # request encode (hit)
+                w = tw[np.searchsorted(tk, keys)]  # KVMap::GetValue
+                P.key_signature(keys)  # response encode (hit)
+                ff_rt(w)()
+            return f
+        for s in range(nstreams):
+            keys = splitmix64_keys(m, 4 + s)
+            pos = np.searchsorted(keys, bounds)
+            for d in range(args.servers):
+                lo, hi = int(pos[d]), int(pos[d + 1])
+                if hi > lo:
+                    tasks.append(pull_slice(keys[lo:hi]))
+            payload += 20 * keys.size
+        what = (f"{nstreams} pull stream(s) of {m} keys sliced over {args.servers} servers: request CRC, "
+                f"GetValue (sorted-table lookup), response CRC + FIXING_FLOAT(nb={nb}) round trip per slice")
     else:  # c4 / c5: the per-(stream, server) slices, one thread per slice up to 16
         from parameter_server_amd import shard
         ranges = shard.server_ranges(args.servers)
@@ -250,7 +287,7 @@ def cpu_baseline(args, nb: int):
             payload += keys.nbytes + x.nbytes
         what = (f"{nstreams} stream(s) of {m} keys (dim {dim}) sliced over {args.servers} servers, "
                 f"[KEY_CACHING, FIXING_FLOAT(nb={nb}){', COMPRESSING' if args.compress else ''}] per slice")
-    if cfg in ("c4", "c5"):
+    if cfg in ("c4", "c4pull", "c5"):
         try:
             avail = len(os.sched_getaffinity(0))
         except AttributeError:
@@ -337,6 +374,46 @@ def build_workload(args, F, ctx, rank, world, dev, g, n):
             F.RemoteNode.roundtrip_many(snd, rcv, tmpls, k, phase_end=[S, 2 * S, 3 * S], wire=wire)
         # keys travel with the pull request only; the response and the push hit
         return run, 32 * m * S, 2 * m * S, {"key_bytes_elided": 16 * m * S, "wire": True}
+    if args.config == "c4pull":
+        # the pull leg over C4's partition: requests out, per-range responses
+        # answered from each rank's KVMap, merged back in key order
+        import numpy as np
+
+        from parameter_server_amd import shard
+        if args.servers < world:
+            raise SystemExit(f"--servers {args.servers} < {world} ranks")
+        ex = None
+        if world > 1:
+            same = os.environ.get("PSF_SAME_GPU") == "1" or not str(dev).startswith("cuda")
+            ex = shard.NativeExchange.create(ctx, transport="host" if same else "rccl")
+        ranges = shard.server_ranges(args.servers)
+        router = shard.PushRouter(ctx, ranges, rank, world, ex)
+        m = args.m or (1 << 21)
+        sids = list(range(rank, args.streams, world))
+        allk = np.unique(np.concatenate([splitmix64_keys(m, 4 + s) for s in range(args.streams)]))
+        mine = [d for d in range(args.servers) if router.owner(d) == rank]
+        lo, hi = ranges[mine[0]][0], ranges[mine[-1]][1]
+        own = allk[(allk >= np.uint64(lo)) & ((allk < np.uint64(hi)) | (np.uint64(hi) == np.uint64(0)))]
+        kv = F.KVMap(ctx, capacity=max(1024, 2 * own.size))
+        if own.size:
+            kt = torch.from_numpy(own.view("int64")).to(dev)
+            kv.push(kt, torch.randn(own.size, device=dev, generator=g, dtype=torch.float32))
+        router.set_store(kv)
+        reqs, payload = {}, 0
+        for sid in sids:
+            keys = torch.from_numpy(splitmix64_keys(m, 4 + sid).view("int64")).to(dev)
+            t = F.Message(request=True, push=False, key_channel=sid, key_range=shard.KEY_ALL)
+            t.set_key(keys)
+            t.add_filter(KEY_CACHING)
+            t.add_filter(FIXING_FLOAT, num_bytes=nb)
+            reqs[sid] = t
+            payload += 20 * keys.numel()  # request keys 8 B + response keys 8 B and value 4 B per key
+        nloc = payload // 20
+
+        def run(k):
+            router.pull(reqs, k)
+        # keys travel with the first pull only; later requests and every response hit
+        return run, payload, nloc, {"router": router, "key_bytes_elided": 16 * nloc, "store": kv}
     if args.config in ("c4", "c5"):
         # streams sliced at the server ranges, encoded
         # per destination server, spilled (one all-to-all-v) and decoded
@@ -513,7 +590,7 @@ def main():
     # a launch with start / stop events costs the stream a few us around the
     # kernel (stride 1 against 4, tools/ab_stride.sh r05o: C3 3272 -> 3324,
     # C5 1684 -> 1701, C5 + COMPRESSING 1383 -> 1391 GiB/s; C2 equal)
-    stride = args.prof_stride or (8 if args.config in ("c1", "c4") else 4)
+    stride = args.prof_stride or (8 if args.config in ("c1", "c4", "c4pull") else 4)
     router = extra.get("router")
     if router is not None and router.exchange is not None:
         router.exchange.bytes_sent = 0
@@ -539,6 +616,23 @@ def main():
             rs = router.host_stats()
             host["router_encode_ms_per_step"] = round(rs["encode_s"] / args.steps * 1e3, 4)
             host["router_decode_ms_per_step"] = round(rs["decode_s"] / args.steps * 1e3, 4)
+            # wall - blocked counts the time the host spends inside launch
+            # calls while the device is behind (the launch queue is full) as
+            # "active"; the host's own cost per step is measured apart: the
+            # same streams and servers with 4096 keys each (every kernel a
+            # few us), where the step is the host's
+            if args.config in ("c4", "c4pull", "c5") and not args.no_host_floor:
+                a_f = argparse.Namespace(**vars(args))
+                a_f.m = 64 if args.config == "c5" else 4096
+                run_f, _, _, extra_f = build_workload(a_f, F, ctx, rank, world, dev, g, 0)
+                run_f(args.warmup)
+                el_f, _ = timed(run_f, args.steps, world, dist, ctx)
+                host["floor_ms_per_step"] = round(el_f / args.steps * 1e3, 4)
+                host["floor_what"] = (f"the same {1 if args.config == 'c5' else args.streams} stream(s) x "
+                                      f"{args.servers} servers with {a_f.m} keys per stream: the host's own "
+                                      "cost of a step (slicing, per-slice Task / filter work, launches)")
+                host["floor_over_kernel"] = round(host["floor_ms_per_step"] / kern_ms, 3) if kern_ms else None
+                del run_f, extra_f
 
     def max_over_ranks(v):
         if world == 1:
@@ -657,7 +751,7 @@ def main():
         cpu = cpu_baseline(args, nb)
 
     if rank == 0:
-        m_default = {"c1": 100_000, "c4": 1 << 21, "c5": 1 << 20}.get(args.config, 1 << 21)
+        m_default = {"c1": 100_000, "c4": 1 << 21, "c4pull": 1 << 21, "c5": 1 << 20}.get(args.config, 1 << 21)
         line = {
             "metric": "GiB/s key-value payload through filter encode+decode, device-resident",
             "value": round(value, 2),
@@ -669,12 +763,14 @@ def main():
             "higher_is_better": True,
             # C4's 64 streams are split over the ranks (total work fixed): strong
             # scaling once there is more than one rank
-            "scaling": "strong" if args.config == "c4" and world_pg > 1 else "weak",
+            "scaling": "strong" if args.config in ("c4", "c4pull") and world_pg > 1 else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic: f32 N(0,1) values, seed 1+rank, FIXING_FLOAT LCG seed 12345"
                     + {"c2": "", "c5": "; sorted unique uint64 keys splitmix64(4+rank+i)",
                        "c4": "; sorted unique uint64 keys splitmix64(4+stream+i)",
+                       "c4pull": "; sorted unique uint64 keys splitmix64(4+stream+i), KVMap weights one FTRL "
+                                 "update of N(0,1) gradients",
                        "c1": "; sorted unique uint64 keys from [0,1e9) per stream"}.get(
                         args.config, "; sorted unique uint64 keys from [0,1e9)"),
             "config": {
@@ -692,7 +788,7 @@ def main():
                 "backend": backend_pg,
                 "parallelism": f"server key-range shards x{world} (EvenDivide), " + (
                     f"{args.servers} servers, cross-range spill: one all-to-all-v per step"
-                    if args.config in ("c4", "c5") and world > 1 else "no data-path collective"),
+                    if args.config in ("c4", "c4pull", "c5") and world > 1 else "no data-path collective"),
             },
             "roofline": roofline,
             "cpu_baseline": cpu,

@@ -1076,7 +1076,7 @@ int psf_router_pull(psf_router* r, psf_message* const* requests, int n, int iter
     if (iters < 0) return PSF_ERR_ARG;
     psf::PushRouter* pr = R(r);
     const std::vector<const psf::Message*> ms = msg_ptrs(requests, n);
-    for (int it = 0; it < iters; ++it) pr->pull_step(ms.data(), n, it == 0);
+    for (int it = 0; it < iters; ++it) pr->pull_step(ms.data(), n, it == 0, it + 1 < iters);
     return PSF_OK;
   });
 }

@@ -115,6 +115,43 @@ void KvMapFtrl::get_value(Message* msg) {  // kv_map.h:69-77
   if (!msg->pending.empty()) msg->pending.resize(msg->value.size());
 }
 
+void KvMapFtrl::get_values(Message* const* msgs, int n) {
+  if (n == 1) return get_value(msgs[0]);
+  auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  size_t bytes = 0;
+  for (int i = 0; i < n; ++i) bytes += up(msgs[i]->key.bytes / 8 * 4);
+  Buffer blk = bytes ? ctx_->alloc(bytes) : Buffer();
+  std::vector<KvGetJob> jobs;
+  std::vector<Buffer> keep;
+  uint64_t total = 0, off = 0;
+  for (int i = 0; i < n; ++i) {
+    Message* msg = msgs[i];
+    const size_t k = msg->key.bytes / 8;
+    Buffer out;
+    if (k) {
+      out = blk;
+      out.ptr = blk.ptr + off;
+      out.bytes = k * 4;
+      Buffer kb = ctx_->to_device(msg->key);
+      jobs.push_back(KvGetJob{reinterpret_cast<const uint64_t*>(kb.ptr), reinterpret_cast<float*>(out.ptr), total, k});
+      keep.push_back(kb);
+      total += k;
+      off += up(k * 4);
+    }
+    msg->value.push_back(out);  // msg->add_value(val): value_type FLOAT
+    msg->task.value_type.push_back(kFloat);
+    if (!msg->pending.empty()) msg->pending.resize(msg->value.size());
+  }
+  if (jobs.empty()) return;
+  Buffer d = ctx_->alloc(jobs.size() * sizeof(KvGetJob));
+  PSF_HIP_CHECK(hipMemcpyAsync(d.ptr, jobs.data(), jobs.size() * sizeof(KvGetJob), hipMemcpyHostToDevice,
+                               ctx_->stream()));
+  int s = kvmap_get_batch_launch(table_.ptr, cap_, reinterpret_cast<const KvGetJob*>(d.ptr), (int)jobs.size(), total,
+                                 ctx_->stream(), ctx_->prof());
+  if (s != kOk) throw CheckError(s, "kvmap get launch failed");
+  // (keep / d: released stream-ordered after the launch)
+}
+
 size_t ordered_match_raw(Context* ctx, const uint64_t* src_key, size_t nsrc, const void* src_val,
                          const PendingDequant& pd, const uint64_t* dst_key, size_t ndst, void* dst_val,
                          int value_type, int k, int op) {

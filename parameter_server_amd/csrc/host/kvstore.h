@@ -48,6 +48,8 @@ class KvMapFtrl {
   void set_value(const Message& msg);
   // KVMap::GetValue (kv_map.h:69-77): appends the float array of w
   void get_value(Message* msg);
+  // get_value of n messages in one launch (their outputs share one block)
+  void get_values(Message* const* msgs, int n);
   // raw device arrays (grad: float, or FIXING_FLOAT codes when pd.nb != 0)
   void push(const uint64_t* keys, size_t n, const void* src, const PendingDequant& pd);
   void pull(const uint64_t* keys, size_t n, float* out);

@@ -354,7 +354,8 @@ void PushRouter::decode_received(const uint8_t* recvbuf, const int64_t* sizes_in
 // out the key-ordered results; split the slices into the ones this rank's
 // servers answer (delivered as they are) and the ones for other ranks.
 void PushRouter::pull_begin(const Message* const* reqs, int n, bool origin, Inbox* local,
-                            std::vector<Message*>* remote, std::vector<int>* dest, std::vector<int>* rsrv) {
+                            std::vector<Message*>* remote, std::vector<int>* dest, std::vector<int>* rsrv,
+                            bool prefetch_next) {
   if (!store_) throw CheckError(kErrArg, "router: a pull needs the servers' store (psf_router_set_store)");
   if (store_->context() != ctx_) throw CheckError(kErrArg, "router: the store lives on another context");
   for (int i = 0; i < n; ++i) {
@@ -369,6 +370,7 @@ void PushRouter::pull_begin(const Message* const* reqs, int n, bool origin, Inbo
         throw CheckError(kErrArg, "router: the streams of one pull need distinct key channels (kv_vector.h:120)");
   }
   encode_launch(reqs, n, origin);
+  if (prefetch_next) prefetch(reqs, n);
   pend_.finish();  // COMPRESSING's lengths
   // the results: one HBM block, each stream's float array at a 256-aligned offset
   auto up = [](uint64_t x) { return (x + 255) & ~(uint64_t)255; };
@@ -442,6 +444,7 @@ void PushRouter::pull_answer(Inbox& reqs, Inbox* local, std::vector<Message>* re
   decode_batch(nodes.data(), mp.data(), (int)n);
   resp->clear();
   resp->resize(n);
+  std::vector<KeySigHint> hints(n);
   for (size_t k = 0; k < n; ++k) {
     const Message& q = reqs.msgs[k];
     Message& r = (*resp)[k];  // `new Message(*request)`
@@ -450,12 +453,17 @@ void PushRouter::pull_answer(Inbox& reqs, Inbox* local, std::vector<Message>* re
     r.value = q.value;
     r.pending = q.pending;
     if (r.task.has_param && r.task.push) throw CheckError(kErrArg, "router: a push slice in a pull");
-    store_->get_value(&r);
     r.task.request = false;  // executor.cc:155
     mp[k] = &r;
+    // the response's KEY_CACHING signature is the request's: the decode just
+    // checked (keys sent) or restored (keys cached under that signature) this
+    // very key buffer, so no CRC launch and no wait for one
+    const FilterConfig* kc = Filter::find(FilterConfig::KEY_CACHING, &r.task);
+    if (kc && kc->has_signature && !r.key.empty()) hints[k] = KeySigHint{r.key.ptr, r.key.bytes, kc->signature};
   }
+  store_->get_values(mp.data(), (int)n);  // KVMap::GetValue of every response, one launch
   PendingEncode pend;
-  encode_batch(nodes.data(), mp.data(), (int)n, nullptr, &pend);
+  encode_batch(nodes.data(), mp.data(), (int)n, hints.data(), &pend);
   pend.finish();
   for (size_t k = 0; k < n; ++k) {
     const int src = reqs.src[k];
@@ -495,7 +503,9 @@ void PushRouter::pull_merge(Inbox& resp) {
     Buffer dst = pout_;
     dst.ptr = pout_.ptr + pout_off_[stream[k]] + pl_koff_[slice[k]] * 4;
     dst.bytes = nk * 4;
-    if (nk && m.value.size() == 1) m.value_dest.assign(1, dst);
+    // (the batched decode writes 16-byte groups: a slice that starts inside
+    // one is decoded aside and copied in with the others, one gather launch)
+    if (nk && m.value.size() == 1 && (reinterpret_cast<uintptr_t>(dst.ptr) & 15) == 0) m.value_dest.assign(1, dst);
   }
   decode_batch(nodes.data(), mp.data(), (int)n);
   std::vector<DeviceCopy> copies;
@@ -519,14 +529,14 @@ void PushRouter::pull_merge(Inbox& resp) {
   // (the copies' sources are freed stream-ordered after the launch)
 }
 
-void PushRouter::pull_step(const Message* const* reqs, int n, bool origin) {
+void PushRouter::pull_step(const Message* const* reqs, int n, bool origin, bool prefetch_next) {
   const int64_t t0 = now_ns();
   if (!ex_ && (world_ > 1 || loopback_))
     throw CheckError(kErrArg, "router: a pull with other ranks needs an exchange");
   Inbox reqs_in;
   std::vector<Message*> remote;
   std::vector<int> dest, rsrv;
-  pull_begin(reqs, n, origin, &reqs_in, &remote, &dest, &rsrv);
+  pull_begin(reqs, n, origin, &reqs_in, &remote, &dest, &rsrv, prefetch_next);
   stat_encode_ns += now_ns() - t0;
   const int64_t t1 = now_ns();
   if (ex_) exchange_round(remote, dest, rsrv, nullptr, &reqs_in, true);

@@ -109,7 +109,9 @@ class PushRouter {
   KvMapFtrl* store() const { return store_; }
   // one whole pull step: through the native exchange (any world), or all
   // local (world 1 without loopback)
-  void pull_step(const Message* const* reqs, int n, bool origin = true);
+  // prefetch_next: queue the next pull's slicing of the same requests on the
+  // side stream (the multi-step driver, as prefetch() for pushes)
+  void pull_step(const Message* const* reqs, int n, bool origin = true, bool prefetch_next = false);
   // the same in three phases around a caller-driven all-to-all-v (sizes as
   // encode(); fill() writes each send buffer): the requests out, the
   // requests served and the responses out, the responses merged
@@ -151,7 +153,7 @@ class PushRouter {
   void check_inbox(const Inbox& in, size_t from, bool own_servers) const;
   // pull phases (see pull_step)
   void pull_begin(const Message* const* reqs, int n, bool origin, Inbox* local, std::vector<Message*>* remote,
-                  std::vector<int>* dest, std::vector<int>* rsrv);
+                  std::vector<int>* dest, std::vector<int>* rsrv, bool prefetch_next = false);
   void pull_answer(Inbox& reqs, Inbox* local, std::vector<Message>* resp, std::vector<Message*>* remote,
                    std::vector<int>* dest, std::vector<int>* rsrv);
   void pull_merge(Inbox& resp);

@@ -426,6 +426,36 @@ __global__ __launch_bounds__(kBlock) void kvmap_get_kernel(const KvSlot* __restr
   }
 }
 
+__device__ __forceinline__ float kv_lookup(const KvSlot* __restrict__ table, uint64_t mask, unsigned long long key) {
+  uint64_t h = kv_hash(key) & mask;
+  for (uint64_t probe = 0; probe <= mask; ++probe) {
+    const unsigned long long cur = table[h].key;
+    if (cur == key) return table[h].w;
+    if (cur == kEmptyKey) break;
+    h = (h + 1) & mask;
+  }
+  return 0.0f;
+}
+
+// The same over a batch of key arrays (a pull step's responses): element i of
+// the concatenation belongs to the last job whose `first` is <= i.
+__global__ __launch_bounds__(kBlock) void kvmap_get_batch_kernel(const KvSlot* __restrict__ table, uint64_t mask,
+                                                                 const KvGetJob* __restrict__ jobs, int njobs,
+                                                                 uint64_t total) {
+  const size_t stride = (size_t)gridDim.x * kBlock;
+  for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < total; i += stride) {
+    int lo = 0, hi = njobs - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (jobs[mid].first <= i) lo = mid;
+      else hi = mid - 1;
+    }
+    const KvGetJob& j = jobs[lo];
+    const uint64_t e = i - j.first;
+    j.out[e] = kv_lookup(table, mask, j.keys[e]);
+  }
+}
+
 // Re-insert every occupied slot of `from` into the empty table `to` (growth).
 __global__ __launch_bounds__(kBlock) void kvmap_rehash_kernel(const KvSlot* __restrict__ from, size_t nfrom,
                                                               KvSlot* to, uint64_t mask) {
@@ -509,4 +539,13 @@ int kvmap_get_launch(const void* table, size_t cap, const uint64_t* keys, size_t
   return launch_status();
 }
 
+
+int kvmap_get_batch_launch(const void* table, size_t cap, const KvGetJob* d_jobs, int njobs, uint64_t total,
+                           hipStream_t st, Profiler* prof) {
+  if (njobs <= 0 || total == 0) return kOk;
+  ProfScope ps(prof, kKKvGet, st, (double)total * (8.0 + 32.0 + 4.0));
+  hipLaunchKernelGGL(kvmap_get_batch_kernel, dim3(grid_for(total)), dim3(kBlock), 0, st,
+                     static_cast<const KvSlot*>(table), (uint64_t)cap - 1, d_jobs, njobs, total);
+  return launch_status();
+}
 }  // namespace psf

@@ -439,5 +439,15 @@ int kvmap_push_launch(void* table, size_t cap, const uint64_t* keys, size_t n, c
                       Profiler* prof);
 int kvmap_get_launch(const void* table, size_t cap, const uint64_t* keys, size_t n, float* out,
                      hipStream_t st, Profiler* prof);
+// GetValue of many key arrays in one launch: job j looks up keys[0, n) into
+// out; `first` = the sum of the earlier jobs' n (jobs in device memory, in
+// that order); total = the sum of all n
+struct KvGetJob {
+  const uint64_t* keys;
+  float* out;
+  uint64_t first, n;
+};
+int kvmap_get_batch_launch(const void* table, size_t cap, const KvGetJob* d_jobs, int njobs, uint64_t total,
+                           hipStream_t st, Profiler* prof);
 
 }  // namespace psf
