@@ -436,7 +436,8 @@ void FixingFloatFilter::decode_messages(Context* ctx, std::vector<FfMessage>& ms
         // encoded on this context's stream: the kernel reads {min, max} where
         // the encode left them (CHECK_GT(bin, 0) is reported when settled)
         j.range = fp.device_range();
-        jobs[keep++] = j;
+        if (keep != q) jobs[keep] = std::move(j);
+        ++keep;
         continue;
       }
       fp.settle();
@@ -450,7 +451,8 @@ void FixingFloatFilter::decode_messages(Context* ctx, std::vector<FfMessage>& ms
         msg->pending[j.i] = PendingDequant{j.nb, fp.min_value, fp.max_value};
         continue;
       }
-      jobs[keep++] = j;
+      if (keep != q) jobs[keep] = std::move(j);
+      ++keep;
     }
     jobs.resize(keep);
   }

@@ -91,36 +91,24 @@ void PushRouter::encode_launch(const Message* const* streams, int n, bool origin
   const int kb = step_key_bytes(streams, n);
   if (job && job->key_bytes != kb) job.reset();
   if (!job) job = slice_begin(ctx_, std::vector<const Message*>(streams, streams + n), ranges_, kb);
-  std::vector<std::vector<Message>> parts;
-  std::vector<std::vector<bool>> ok;
-  std::vector<std::vector<KeySigHint>> hints;
-  {
-    PSF_HPROF(12);
-    slice_end(*job, &parts, &ok, &hints);
-  }
-  job.reset();
-  const int S = (int)ranges_.size();
   slices_.clear();
   srv_.clear();
   sl_stream_.clear();
   sl_koff_.clear();
   sl_nkeys_.clear();
-  slices_.reserve((size_t)n * S);
   std::vector<KeySigHint> sh;
-  sh.reserve((size_t)n * S);
-  std::vector<RemoteNode*> nodes;
-  for (int i = 0; i < n; ++i)
-    for (int d = 0; d < S; ++d) {
-      if (!ok[i][d]) continue;  // the range misses the message's key range: not sent
-      const Buffer& k = parts[i][d].key;
-      sl_stream_.push_back(i);
-      sl_koff_.push_back(k.bytes ? (uint64_t)(k.ptr - streams[i]->key.ptr) / (uint64_t)kb : 0);
-      sl_nkeys_.push_back(k.bytes / (uint64_t)kb);
-      slices_.push_back(std::move(parts[i][d]));
-      sh.push_back(hints[i][d]);
-      nodes.push_back(sender(streams[i]->task.key_channel, d));
-      srv_.push_back(d);
-    }
+  {
+    PSF_HPROF(12);
+    // only the slices that are sent, built where they stay (slices_)
+    slice_end_flat(*job, &slices_, &sl_stream_, &srv_, &sh, &sl_koff_);
+  }
+  job.reset();
+  std::vector<RemoteNode*> nodes(slices_.size());
+  sl_nkeys_.resize(slices_.size());
+  for (size_t k = 0; k < slices_.size(); ++k) {
+    sl_nkeys_[k] = slices_[k].key.bytes / (uint64_t)kb;
+    nodes[k] = sender(streams[sl_stream_[k]]->task.key_channel, srv_[k]);
+  }
   std::vector<Message*> mp(slices_.size());
   for (size_t k = 0; k < slices_.size(); ++k) mp[k] = &slices_[k];
   {

@@ -59,33 +59,44 @@ void host_lower_bounds(const Message& msg, int key_bytes, const std::vector<uint
   }
 }
 
+// whether slice i of msg is sent: the range meets the message's key range
+// (SetIntersection(...).empty() means not sent)
+bool slice_valid(const Message& msg, const KeyRange& kr) {
+  const KeyRange mr = msg.task.has_key_range ? msg.task.key_range : KeyRange{0, 0};
+  const uint64_t ib = std::max(kr.begin, mr.begin), ie = std::min(kr.end, mr.end);
+  return ib < ie;
+}
+
+// fill the (task-copied) slice ret of a valid range from its split positions
+void fill_slice(const Message& msg, int key_bytes, size_t lo, size_t hi, Message* ret) {
+  const size_t nkeys = msg.key.bytes / (size_t)key_bytes;
+  if (nkeys == 0) return;  // "to void be divided by 0"
+  // SArray::Segment (shared_array_inl.h:135): a range end that does not fit
+  // K wraps in the (K) cast and lands before the range's begin
+  if (lo > hi) throw CheckError(kErrCheck, "CHECK(range.valid())");
+  ret->set_key(segment(msg.key, lo * key_bytes, (hi - lo) * key_bytes));
+  ret->task.key_type = key_bytes == 8 ? 8 : 7;  // EncodeType<K>: UINT64 / UINT32
+  ret->task.has_key_type = true;
+  ret->value.reserve(msg.value.size());
+  for (const Buffer& v : msg.value) {
+    const size_t k = v.bytes / nkeys;  // bytes per key
+    if (nkeys * k != v.bytes) throw CheckError(kErrCheck, "CHECK_EQ(key.size() * k, v.size())");
+    ret->value.push_back(segment(v, lo * k, (hi - lo) * k));
+  }
+}
+
 // build the slices of one message from its split positions
 void build_slices(const Message& msg, const std::vector<KeyRange>& krs, int key_bytes, const uint64_t* pos,
                   std::vector<Message>* outs, std::vector<bool>* valid) {
   const size_t n = krs.size();
   outs->assign(n, Message());
   valid->assign(n, false);
-  const KeyRange mr = msg.task.has_key_range ? msg.task.key_range : KeyRange{0, 0};
-  const size_t nkeys = msg.key.bytes / (size_t)key_bytes;
   for (size_t i = 0; i < n; ++i) {
     Message& ret = (*outs)[i];
     ret.task = msg.task;  // `new Message(msg->task)`, executor.cc:129
-    const uint64_t ib = std::max(krs[i].begin, mr.begin), ie = std::min(krs[i].end, mr.end);
-    if (ib >= ie) continue;  // SetIntersection(...).empty(): not sent
+    if (!slice_valid(msg, krs[i])) continue;
     (*valid)[i] = true;
-    if (nkeys == 0) continue;  // "to void be divided by 0"
-    const size_t lo = pos[i], hi = pos[i + 1];
-    // SArray::Segment (shared_array_inl.h:135): a range end that does not fit
-    // K wraps in the (K) cast and lands before the range's begin
-    if (lo > hi) throw CheckError(kErrCheck, "CHECK(range.valid())");
-    ret.set_key(segment(msg.key, lo * key_bytes, (hi - lo) * key_bytes));
-    ret.task.key_type = key_bytes == 8 ? 8 : 7;  // EncodeType<K>: UINT64 / UINT32
-    ret.task.has_key_type = true;
-    for (const Buffer& v : msg.value) {
-      const size_t k = v.bytes / nkeys;  // bytes per key
-      if (nkeys * k != v.bytes) throw CheckError(kErrCheck, "CHECK_EQ(key.size() * k, v.size())");
-      ret.value.push_back(segment(v, lo * k, (hi - lo) * k));
-    }
+    fill_slice(msg, key_bytes, pos[i], pos[i + 1], &ret);
   }
 }
 }  // namespace
@@ -184,10 +195,10 @@ std::unique_ptr<SliceJob> slice_begin(Context* ctx, const std::vector<const Mess
   return job;
 }
 
-void slice_end(SliceJob& job, std::vector<std::vector<Message>>* outs, std::vector<std::vector<bool>>* valid,
-               std::vector<std::vector<KeySigHint>>* hints) {
+// the device pass's results into job.pos; returns the signatures (or null)
+static const uint32_t* slice_collect(SliceJob& job) {
   if (job.ended) throw CheckError(kErrArg, "slice job already ended");
-  const size_t M = job.msgs.size(), n = job.krs.size(), nb = n + 1, D = job.dev.size();
+  const size_t n = job.krs.size(), nb = n + 1, D = job.dev.size();
   const uint32_t* sig = nullptr;
   if (D) {
     job.ctx->wait_event(job.ev, Context::kWaitSlice);
@@ -197,6 +208,40 @@ void slice_end(SliceJob& job, std::vector<std::vector<Message>>* outs, std::vect
     for (size_t q = 0; q < D; ++q) std::copy(pos + q * nb, pos + (q + 1) * nb, job.pos.begin() + job.dev[q] * nb);
   }
   job.ended = true;
+  return sig;
+}
+
+void slice_end_flat(SliceJob& job, std::vector<Message>* out, std::vector<int>* stream, std::vector<int>* server,
+                    std::vector<KeySigHint>* hints, std::vector<uint64_t>* first_key) {
+  const uint32_t* sig = slice_collect(job);
+  const size_t M = job.msgs.size(), n = job.krs.size(), nb = n + 1;
+  std::vector<int> dev_index(M, -1);
+  for (size_t q = 0; q < job.dev.size(); ++q) dev_index[job.dev[q]] = (int)q;
+  out->reserve(out->size() + M * n);
+  for (size_t m = 0; m < M; ++m) {
+    const Message& msg = *job.msgs[m];
+    const uint64_t* pos = job.pos.data() + m * nb;
+    for (size_t i = 0; i < n; ++i) {
+      if (!slice_valid(msg, job.krs[i])) continue;
+      out->emplace_back();
+      Message& ret = out->back();
+      ret.task = msg.task;  // `new Message(msg->task)`, executor.cc:129
+      fill_slice(msg, job.key_bytes, pos[i], pos[i + 1], &ret);
+      stream->push_back((int)m);
+      server->push_back((int)i);
+      first_key->push_back(ret.key.bytes ? pos[i] : 0);
+      KeySigHint h;
+      if (sig && dev_index[m] >= 0 && !ret.key.empty())
+        h = KeySigHint{ret.key.ptr, ret.key.bytes, sig[(size_t)dev_index[m] * n + i]};
+      hints->push_back(h);
+    }
+  }
+}
+
+void slice_end(SliceJob& job, std::vector<std::vector<Message>>* outs, std::vector<std::vector<bool>>* valid,
+               std::vector<std::vector<KeySigHint>>* hints) {
+  const uint32_t* sig = slice_collect(job);
+  const size_t M = job.msgs.size(), n = job.krs.size(), nb = n + 1, D = job.dev.size();
   outs->assign(M, {});
   valid->assign(M, {});
   for (size_t m = 0; m < M; ++m)

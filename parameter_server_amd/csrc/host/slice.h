@@ -55,5 +55,10 @@ std::unique_ptr<SliceJob> slice_begin(Context* ctx, const std::vector<const Mess
                                       const std::vector<KeyRange>& krs, int key_bytes, hipEvent_t after = nullptr);
 void slice_end(SliceJob& job, std::vector<std::vector<Message>>* outs, std::vector<std::vector<bool>>* valid,
                std::vector<std::vector<KeySigHint>>* hints = nullptr);
+// slice_end with the valid slices only, appended flat to *out (message by
+// message, ranges in order): per slice its message's index, its range's
+// index, its signature hint and the index of its first key in the message
+void slice_end_flat(SliceJob& job, std::vector<Message>* out, std::vector<int>* stream, std::vector<int>* server,
+                    std::vector<KeySigHint>* hints, std::vector<uint64_t>* first_key);
 
 }  // namespace psf
