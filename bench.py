@@ -305,16 +305,36 @@ def cpu_baseline(args, nb: int):
     }
 
 
-def pmc_traffic(kernel: str, n: int, nb: int, config: str):
+def line_key(args):
+    """The name tools/pmc_traffic.py gives this run's line, when it runs at the
+    line's default sizes (the PMC passes' shape), else None."""
+    if args.nb != 1 or args.miss:
+        return None
+    c = args.config
+    if c == "c2":
+        return "c2" if args.n == 1 << 28 else None
+    if c == "c1":
+        return "c1" if args.m in (None, 100_000) and args.streams == 64 else None
+    if c == "c3":
+        return "c3" if args.m in (None, 10_000_000) else None
+    if c in ("c4", "c4pull"):
+        return c if args.m in (None, 1 << 21) and args.streams == 64 and args.servers == 8 else None
+    if c == "c5":
+        return ("c5z" if args.compress else "c5") if args.m in (None, 1 << 20) and args.servers == 8 else None
+    return None
+
+
+def pmc_traffic(kernel: str, args):
+    """HBM bytes per launch of `kernel` on this line, from the PMC passes in
+    profiles/pmc_traffic.json (tools/pmc_traffic.py), or None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    key = line_key(args)
     try:
         d = json.load(open(path))
     except (OSError, ValueError):
         return None
-    e = d.get(kernel)
-    if not e or e.get("config", "c2") != config or e.get("n") != n or e.get("nb") != nb:
-        return None
-    return e.get("hbm_bytes_per_launch")
+    e = d.get("lines", {}).get(key or "", {}).get("kernels", {}).get(kernel)
+    return e.get("hbm_bytes_per_launch") if e else None
 
 
 # ------------------------------------------------------------- workloads --
@@ -658,7 +678,9 @@ def main():
         roofline = {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": pmc_traffic(dom, n, nb, args.config),
+            "traffic": pmc_traffic(dom, args),
+            "traffic_source": "profiles/pmc_traffic.json (rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this line)"
+                              if pmc_traffic(dom, args) else None,
             "kernel": dom,
             "avg_us": round(avg_s * 1e6, 2),
             "alg_bytes_per_launch": int(per_launch_bytes),

@@ -515,6 +515,10 @@ void PushRouter::pull_merge(Inbox& resp) {
   }
   device_copies(ctx_, copies, pout_.ptr);
   // (the copies' sources are freed stream-ordered after the launch)
+  // every slice sent was answered (the reference's sent_req_tracker would
+  // wait for the rest forever; here it is an error)
+  if (!ppos_.empty())
+    throw CheckError(kErrCheck, "pull: " + std::to_string(ppos_.size()) + " slice(s) got no response");
 }
 
 void PushRouter::pull_step(const Message* const* reqs, int n, bool origin, bool prefetch_next) {
