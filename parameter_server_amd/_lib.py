@@ -192,7 +192,10 @@ def lib() -> C.CDLL:
             raise ImportError(f"{LIB_PATH} is missing: run `python -m parameter_server_amd.build` "
                               "(there is no CPU fallback)")
         L = C.CDLL(LIB_PATH)
+        variant = LIB_PATH != os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpsf.so")
         for name, (args, res) in SIGNATURES.items():
+            if variant and not hasattr(L, name):
+                continue  # an older build loaded for an A/B run lacks the newer entry points
             f = getattr(L, name)
             f.argtypes = args
             f.restype = res
