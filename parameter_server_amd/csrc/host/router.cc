@@ -2,6 +2,8 @@
 
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "slice.h"
 
 namespace psf {
@@ -449,7 +451,17 @@ void PushRouter::pull_answer(Inbox& reqs, Inbox* local, std::vector<Message>* re
     const FilterConfig* kc = Filter::find(FilterConfig::KEY_CACHING, &r.task);
     if (kc && kc->has_signature && !r.key.empty()) hints[k] = KeySigHint{r.key.ptr, r.key.bytes, kc->signature};
   }
-  store_->get_values(mp.data(), (int)n);  // KVMap::GetValue of every response, one launch
+  // KVMap::GetValue of every response in one launch, grouped by server: the
+  // streams' slices for one server share most of their keys, so a server's
+  // lookups run back to back and find the table lines they touch on chip
+  std::vector<Message*> by_server(mp.begin(), mp.end());
+  {
+    std::vector<size_t> ord(n);
+    for (size_t k = 0; k < n; ++k) ord[k] = k;
+    std::stable_sort(ord.begin(), ord.end(), [&](size_t a, size_t b) { return reqs.server[a] < reqs.server[b]; });
+    for (size_t k = 0; k < n; ++k) by_server[k] = mp[ord[k]];
+  }
+  store_->get_values(by_server.data(), (int)n);
   PendingEncode pend;
   encode_batch(nodes.data(), mp.data(), (int)n, hints.data(), &pend);
   pend.finish();

@@ -19,6 +19,8 @@
 // Compiled with -ffp-contract=off like every codec file: the reference's float
 // expressions are evaluated operation by operation (g++/x86-64 SSE, no FMA).
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <stdint.h>
 
 #include "psf_internal.h"
@@ -438,21 +440,62 @@ __device__ __forceinline__ float kv_lookup(const KvSlot* __restrict__ table, uin
 }
 
 // The same over a batch of key arrays (a pull step's responses): element i of
-// the concatenation belongs to the last job whose `first` is <= i.
+// the concatenation belongs to the last job whose `first` is <= i.  A
+// workgroup takes chunks of kGetPer x kBlock consecutive elements and finds
+// the chunk's first job once (a uniform search); each lane then steps to the
+// next job where its element crosses a boundary.  Four lookups per lane are
+// in flight at once: each first probe is one 16-byte load of {key, w}, and
+// only a probe that lands on another key walks on (linear probing).
+constexpr int kGetPer = 16;
 __global__ __launch_bounds__(kBlock) void kvmap_get_batch_kernel(const KvSlot* __restrict__ table, uint64_t mask,
                                                                  const KvGetJob* __restrict__ jobs, int njobs,
                                                                  uint64_t total) {
-  const size_t stride = (size_t)gridDim.x * kBlock;
-  for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < total; i += stride) {
+  const uint64_t chunk = (uint64_t)kBlock * kGetPer;
+  for (uint64_t base = (uint64_t)blockIdx.x * chunk; base < total; base += (uint64_t)gridDim.x * chunk) {
     int lo = 0, hi = njobs - 1;
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
-      if (jobs[mid].first <= i) lo = mid;
+      if (jobs[mid].first <= base) lo = mid;
       else hi = mid - 1;
     }
-    const KvGetJob& j = jobs[lo];
-    const uint64_t e = i - j.first;
-    j.out[e] = kv_lookup(table, mask, j.keys[e]);
+    int j = lo;
+    uint64_t jend = jobs[j].first + jobs[j].n;
+#pragma unroll 1
+    for (int k = 0; k < kGetPer; k += 4) {
+      unsigned long long key[4];
+      float* dst[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint64_t i = base + (uint64_t)(k + u) * kBlock + threadIdx.x;
+        dst[u] = nullptr;
+        key[u] = kEmptyKey;
+        if (i < total) {
+          while (i >= jend) {
+            ++j;
+            jend = jobs[j].first + jobs[j].n;
+          }
+          const uint64_t e = i - jobs[j].first;
+          key[u] = jobs[j].keys[e];
+          dst[u] = jobs[j].out + e;
+        }
+      }
+      uint64_t h[4];
+      uint4 sl[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        h[u] = kv_hash(key[u]) & mask;
+        sl[u] = *reinterpret_cast<const uint4*>(&table[h[u]]);  // {key, w, z}
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (!dst[u]) continue;
+        const unsigned long long cur = (unsigned long long)sl[u].x | ((unsigned long long)sl[u].y << 32);
+        float w = 0.0f;
+        if (cur == key[u]) w = __uint_as_float(sl[u].z);
+        else if (cur != kEmptyKey) w = kv_lookup(table, mask, key[u]);  // (rare: a collision)
+        *dst[u] = w;
+      }
+    }
   }
 }
 
@@ -544,7 +587,9 @@ int kvmap_get_batch_launch(const void* table, size_t cap, const KvGetJob* d_jobs
                            hipStream_t st, Profiler* prof) {
   if (njobs <= 0 || total == 0) return kOk;
   ProfScope ps(prof, kKKvGet, st, (double)total * (8.0 + 32.0 + 4.0));
-  hipLaunchKernelGGL(kvmap_get_batch_kernel, dim3(grid_for(total)), dim3(kBlock), 0, st,
+  const uint64_t chunks = (total + (uint64_t)kBlock * kGetPer - 1) / ((uint64_t)kBlock * kGetPer);
+  const unsigned grid = (unsigned)std::min<uint64_t>(chunks, (uint64_t)kMaxGrid * 4);
+  hipLaunchKernelGGL(kvmap_get_batch_kernel, dim3(grid), dim3(kBlock), 0, st,
                      static_cast<const KvSlot*>(table), (uint64_t)cap - 1, d_jobs, njobs, total);
   return launch_status();
 }
