@@ -447,6 +447,11 @@ __device__ __forceinline__ float kv_lookup(const KvSlot* __restrict__ table, uin
 // in flight at once: each first probe is one 16-byte load of {key, w}, and
 // only a probe that lands on another key walks on (linear probing).
 constexpr int kGetPer = 16;
+#ifndef PSF_GET_INFLIGHT
+#define PSF_GET_INFLIGHT 8  // lookups in flight per lane (A/B knob: 4 / 8 / 16 gave 2008 / 1970 / 2814 us at C4pull, r06h)
+#endif
+constexpr int kGetFly = PSF_GET_INFLIGHT;
+static_assert(kGetPer % kGetFly == 0, "whole rounds of lookups per chunk");
 __global__ __launch_bounds__(kBlock) void kvmap_get_batch_kernel(const KvSlot* __restrict__ table, uint64_t mask,
                                                                  const KvGetJob* __restrict__ jobs, int njobs,
                                                                  uint64_t total) {
@@ -461,11 +466,11 @@ __global__ __launch_bounds__(kBlock) void kvmap_get_batch_kernel(const KvSlot* _
     int j = lo;
     uint64_t jend = jobs[j].first + jobs[j].n;
 #pragma unroll 1
-    for (int k = 0; k < kGetPer; k += 4) {
-      unsigned long long key[4];
-      float* dst[4];
+    for (int k = 0; k < kGetPer; k += kGetFly) {
+      unsigned long long key[kGetFly];
+      float* dst[kGetFly];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < kGetFly; ++u) {
         const uint64_t i = base + (uint64_t)(k + u) * kBlock + threadIdx.x;
         dst[u] = nullptr;
         key[u] = kEmptyKey;
@@ -479,15 +484,15 @@ __global__ __launch_bounds__(kBlock) void kvmap_get_batch_kernel(const KvSlot* _
           dst[u] = jobs[j].out + e;
         }
       }
-      uint64_t h[4];
-      uint4 sl[4];
+      uint64_t h[kGetFly];
+      uint4 sl[kGetFly];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < kGetFly; ++u) {
         h[u] = kv_hash(key[u]) & mask;
         sl[u] = *reinterpret_cast<const uint4*>(&table[h[u]]);  // {key, w, z}
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < kGetFly; ++u) {
         if (!dst[u]) continue;
         const unsigned long long cur = (unsigned long long)sl[u].x | ((unsigned long long)sl[u].y << 32);
         float w = 0.0f;
