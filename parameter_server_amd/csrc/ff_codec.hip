@@ -58,10 +58,30 @@ constexpr int kMinmaxGrid = PSF_MINMAX_GRID;  // partials the encode kernel fold
 #endif
 constexpr int kStreamGrid = PSF_STREAM_GRID;
 constexpr int kDecodeGridBig = 2 * PSF_STREAM_GRID;
-constexpr uint32_t kMask17 = 0x1FFFFu;   // LCG state kept mod 2^17 (see quant_group)
-struct Lcg17 { uint32_t a[4], c[4]; };   // affine maps for 1..4 LCG steps, mod 2^17
+constexpr uint32_t kMask17 = 0x1FFFFu;   // the LCG bits the encoder uses depend on the state mod 2^17
 
 // ------------------------------------------------------------ helpers ------
+#ifdef PSF_WG_TRACE
+// diagnostic builds only (tools/c3real_probe.hip): per-workgroup s_memrealtime
+// stamps (entry, quantiser ready, last store done) and the XCC / HW ids
+__device__ uint64_t* g_wg_trace;
+#define PSF_STAMP(v) const uint64_t v = __builtin_amdgcn_s_memrealtime()
+#define PSF_TRACE_END(a, b)                                                                           \
+  do {                                                                                               \
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");                                             \
+    __syncthreads();                                                                                 \
+    if (threadIdx.x == 0) {                                                                          \
+      uint64_t* tr = g_wg_trace + 4 * blockIdx.x;                                                    \
+      tr[0] = a;                                                                                     \
+      tr[1] = b;                                                                                     \
+      tr[2] = __builtin_amdgcn_s_memrealtime();                                                      \
+      tr[3] = (uint64_t)__builtin_amdgcn_s_getreg(6164) << 32 | (uint32_t)__builtin_amdgcn_s_getreg(63492); \
+    }                                                                                                \
+  } while (0)
+#else
+#define PSF_STAMP(v)
+#define PSF_TRACE_END(a, b)
+#endif
 __device__ __forceinline__ uint32_t f32_key(float f) {
   uint32_t u = __float_as_uint(f);
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
@@ -110,6 +130,12 @@ template <typename K> __device__ __forceinline__ K wave_max(K v) {
   return v;
 }
 
+// A workgroup barrier for an LDS hand-off only: it waits for this wave's LDS
+// operations (lgkmcnt), not for its global loads.  __syncthreads' release
+// fence waits for every outstanding load (vmcnt(0)), which held the encode's
+// partials fold until its first tile had arrived.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // Block-wide (256 threads = 4 waves) min/max of keys; result valid in all threads.
 template <typename K>
 __device__ __forceinline__ void block_minmax(K& lo, K& hi) {
@@ -118,14 +144,14 @@ __device__ __forceinline__ void block_minmax(K& lo, K& hi) {
   hi = wave_max(hi);
   const int wid = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) { s_lo[wid] = lo; s_hi[wid] = hi; }
-  __syncthreads();
+  lds_barrier();
   lo = s_lo[0]; hi = s_hi[0];
 #pragma unroll
   for (int w = 1; w < kBlock / 64; ++w) {
     lo = s_lo[w] < lo ? s_lo[w] : lo;
     hi = s_hi[w] > hi ? s_hi[w] : hi;
   }
-  __syncthreads();
+  lds_barrier();
 }
 
 // 4-element vector access of V.  Cache policy (tools/bw_probe3.hip, emulated
@@ -291,32 +317,50 @@ __global__ __launch_bounds__(kBlock) void ff_minmax_partials(const V* __restrict
   }
 }
 
-// Fold the partials (every workgroup of the encode kernel does this; <= 1024
-// pairs, L2-resident).  Returns min/max in the reference's FilterConfig
-// representation (float), fixing_float.h:57-64.
+// The min/max partials every workgroup of the encode kernel folds (<= 1024
+// pairs, L2-resident), in two steps: load (into registers, kMinmaxGrid /
+// kBlock pairs a thread) before the first tile's loads, fold after them.  The
+// order matters: loads return in issue order, and C3's partials, loaded behind
+// 2048 workgroups' first tiles (32 MB), arrived 5.7 us (median) into a 12 us
+// kernel, holding every workgroup's quantiser that long.  (Scalar loads, which
+// a CU pair's scalar cache would serve from one fetch, were slower still: the
+// scalar path took 12-38 us to deliver 8 KB to 2048 workgroups.)  The fold
+// returns min/max in the reference's FilterConfig representation (float),
+// fixing_float.h:57-64.
 template <typename V>
-__device__ __forceinline__ void fold_partials(const void* partials, int nparts, float& mn_f,
-                                              float& mx_f) {
+struct Partials {
   typedef typename KeyOf<V>::K K;
-  const K* p = reinterpret_cast<const K*>(partials);
-  K lo = KeyOf<V>::kLoId, hi = KeyOf<V>::kHiId;
-  for (int i = threadIdx.x; i < nparts; i += kBlock) {
-    K a = p[i], b = p[nparts + i];
-    lo = a < lo ? a : lo;
-    hi = b > hi ? b : hi;
+  static constexpr int kPer = (kMinmaxGrid + kBlock - 1) / kBlock;
+  K lo[kPer], hi[kPer];
+  __device__ __forceinline__ void load(const void* partials, int nparts) {
+    const K* p = reinterpret_cast<const K*>(partials);
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int i = (int)threadIdx.x + k * kBlock;
+      lo[k] = i < nparts ? p[i] : KeyOf<V>::kLoId;
+      hi[k] = i < nparts ? p[nparts + i] : KeyOf<V>::kHiId;
+    }
   }
-  block_minmax(lo, hi);
-  if (sizeof(V) == 4) {
-    // all-NaN / empty: lo stays at the identity, which decodes to a NaN
-    float lo_v = key_f32((uint32_t)lo), hi_v = key_f32((uint32_t)hi);
-    mn_f = lo_v;
-    mx_f = (float)((double)hi_v + 1e-6);
-  } else {
-    double lo_v = key_f64((uint64_t)lo), hi_v = key_f64((uint64_t)hi);
-    mn_f = (float)lo_v;
-    mx_f = (float)(hi_v + 1e-6);
+  __device__ __forceinline__ void fold(float& mn_f, float& mx_f) const {
+    K l = lo[0], h = hi[0];
+#pragma unroll
+    for (int k = 1; k < kPer; ++k) {
+      l = lo[k] < l ? lo[k] : l;
+      h = hi[k] > h ? hi[k] : h;
+    }
+    block_minmax(l, h);
+    if (sizeof(V) == 4) {
+      // all-NaN / empty: l stays at the identity, which decodes to a NaN
+      float lo_v = key_f32((uint32_t)l), hi_v = key_f32((uint32_t)h);
+      mn_f = lo_v;
+      mx_f = (float)((double)hi_v + 1e-6);
+    } else {
+      double lo_v = key_f64((uint64_t)l), hi_v = key_f64((uint64_t)h);
+      mn_f = (float)lo_v;
+      mx_f = (float)(hi_v + 1e-6);
+    }
   }
-}
+};
 
 // x86-64 g++ lowering of static_cast<uint64>(double) for the values that can
 // arise here (|d| < 2^63 or NaN): negatives wrap through int64, NaN's low 56
@@ -333,10 +377,7 @@ struct EncodeParams {
   int has_min, has_max;
   float preset_min, preset_max;
   uint32_t seed;
-  uint32_t a_lane, c_lane;  // LCG affine map (mod 2^17) advancing one group-row (kBlock groups)
-  uint32_t a_tile, c_tile;  // ... one tile (kTileGroups groups)
   uint32_t a_thr, c_thr;    // scalar path (full 32-bit): nthreads elements
-  Lcg17 k17;                // 1..4 steps, mod 2^17
   const uint32_t* lcg_bits; // bit k = !bit16(x_k), x_k the k-th state of the mod-2^17 cycle from 0
   uint32_t lcg_pos;         // position of the seed on that cycle: seed = x_pos (mod 2^17)
   double ratio;
@@ -546,55 +587,61 @@ __device__ __forceinline__ uint64_t quant_floor(V xv, const QuantParams& q) {
   return quant_exact(x, q);
 }
 
-// Only bit 16 of the LCG state is ever observed, and (a*s + c) mod 2^17 depends
-// only on s mod 2^17, so the vector path carries the state mod 2^17 and steps
-// it with full-rate 24-bit multiplies.  k17[k] = affine map for k+1 steps.
-
-__device__ __forceinline__ uint32_t step17(uint32_t a, uint32_t c, uint32_t s) {
-  // hipcc lowers a*s to the quarter-rate v_mul_lo_u32 even when both operands
-  // are known to fit 17 bits; v_mul_u32_u24 is full rate and exact here.  `a`
-  // is wave-uniform (a kernel parameter) and is read straight from its SGPR.
-  uint32_t r;
-  asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "s"(a), "v"(s));
-  return (r + c) & kMask17;
-}
-
-template <typename V, int NB>
-__device__ __forceinline__ void quant_group(const V v[4], const QuantParams& q, uint32_t s17,
-                                            const Lcg17& k17, uint64_t r[4]) {
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const uint32_t sj = step17(k17.a[j], k17.c[j], s17);  // state s_{4g+j+1}
-    r[j] = quant_floor<V, NB>(v[j], q) + (uint64_t)((~sj >> 16) & 1u);
-  }
-}
-
 // full 32-bit state step (scalar and tail paths)
 __device__ __forceinline__ uint64_t lcg_bit(uint32_t& s) {
   s = kLcgA * s + kLcgC;
   return ((s >> 16) & 1u) == 0u ? 1u : 0u;
 }
 
-// f32 values, num_bytes = 1: one lane's full tile (4 groups x 4 values).
-// Fast floor in f32 (the guard band of quant_fast), with the band test folded
-// into two lane-wide accumulators of frac = t - floor(t) compared as u32 bit
-// patterns (frac >= 0, so the order is the float order, and a NaN frac sorts
-// above 1): the lane is fast when g < min frac and max frac < 1 - g.  NaN and
-// infinite values need no test of their own: med3 returns min_f or max_f for
-// them, whose t is 0 or within 1e-4 of ratio, inside the band.  Codes <=
-// ratio = 254, so the packed LCG bits add without carries.  A lane that fails
-// redoes its 16 values with the reference's double sequence.
+// The rare exact pass of a lane whose band test failed: the values of its
+// valid groups that sit in a guard band (quant_fast's test) get the
+// reference's double sequence.  One rolled loop over the lane's 16 values,
+// each read from its register by the wave-uniform loop index: sixteen unrolled tests and
+// exact sequences held the tile kernels at 73-79 VGPRs (6 waves per SIMD)
+// and cost C3's encode 1 us.
+__device__ __forceinline__ void redo_f32_nb1(const float v[4][4], const QuantParams& q, uint32_t valid,
+                                             uint32_t w[4]) {
+  typedef float f32x16 __attribute__((ext_vector_type(16)));
+  const f32x16 vv = {v[0][0], v[0][1], v[0][2], v[0][3], v[1][0], v[1][1], v[1][2], v[1][3],
+                     v[2][0], v[2][1], v[2][2], v[2][3], v[3][0], v[3][1], v[3][2], v[3][3]};
+#pragma unroll 1
+  for (uint32_t k = 0; k < 16; ++k) {  // k uniform: vv[k] is an indexed register read
+    if (!((valid >> (k >> 2)) & 1u)) continue;
+    const float xv = vv[k];
+    bool ok;
+    (void)quant_fast<float, 1>(xv, q, ok);
+    if (ok) continue;
+    const uint32_t c = quant_exact((double)xv, q);
+    const uint32_t sh = 8u * (k & 3u);
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u)
+      if ((k >> 2) == u) w[u] = (w[u] & ~(0xFFu << sh)) | (c << sh);
+  }
+}
+
+// f32 values, num_bytes = 1: one lane's tile (4 groups x 4 values; `valid`
+// bit u: group u is in the array, all four but in an array's partial last
+// tile).  Fast floor in f32 (the guard band of quant_fast), with the band
+// test folded into two lane-wide accumulators of frac = t - floor(t)
+// compared as u32 bit patterns (frac >= 0, so the order is the float order,
+// and a NaN frac sorts above 1): the lane is fast when g < min frac and max
+// frac < 1 - g.  NaN and infinite values need no test of their own: med3
+// returns min_f or max_f for them, whose t is 0 or within 1e-4 of ratio,
+// inside the band.  Codes <= ratio = 254, so the packed LCG bits add without
+// carries.  A lane that fails takes redo_f32_nb1 (xg: the values of v in
+// memory, group u's at xg + 4 u kBlock).
 template <bool kStored = false>
-__device__ __forceinline__ void encode_tile_f32_nb1(const float v[4][4], const QuantParams& q,
+__device__ __forceinline__ void encode_tile_f32_nb1(const float v[4][4], const float* xg, const QuantParams& q,
                                                     const uint32_t b4[4], uint32_t* __restrict__ out,
-                                                    const StoredLayout* L = nullptr, size_t gs = 0) {
+                                                    const StoredLayout* L = nullptr, size_t gs = 0,
+                                                    uint32_t valid = 0xFu) {
   typedef float f32x2 __attribute__((ext_vector_type(2)));
   const f32x2 mn2 = {q.min_f, q.min_f}, sc2 = {q.scale_f, q.scale_f};
   uint32_t lo = 0x7F800000u, hi = 0u;
   uint32_t w[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
-    uint32_t acc = 0;
+    uint32_t acc = 0, ulo = 0x7F800000u, uhi = 0u;
 #pragma unroll
     for (int j = 0; j < 4; j += 2) {  // value pairs: packed f32 sub/mul (exact per element)
       const f32x2 c = {__builtin_amdgcn_fmed3f(v[u][j], q.min_f, q.max_f),
@@ -603,45 +650,37 @@ __device__ __forceinline__ void encode_tile_f32_nb1(const float v[4][4], const Q
       const f32x2 f = {floorf(t.x), floorf(t.y)};
       const f32x2 fr = t - f;
       const uint32_t a = __float_as_uint(fr.x), b = __float_as_uint(fr.y);
-      lo = __builtin_elementwise_min(__builtin_elementwise_min(lo, a), b);
-      hi = __builtin_elementwise_max(__builtin_elementwise_max(hi, a), b);
+      ulo = __builtin_elementwise_min(__builtin_elementwise_min(ulo, a), b);
+      uhi = __builtin_elementwise_max(__builtin_elementwise_max(uhi, a), b);
       acc = __builtin_amdgcn_cvt_pk_u8_f32(f.x, j, acc);
       acc = __builtin_amdgcn_cvt_pk_u8_f32(f.y, j + 1, acc);
+    }
+    if ((valid >> u) & 1u) {
+      lo = __builtin_elementwise_min(lo, ulo);
+      hi = __builtin_elementwise_max(hi, uhi);
     }
     w[u] = acc;
   }
   const bool fast = q.fast && (lo > __float_as_uint(kGuard32)) && (hi < __float_as_uint(1.0f - kGuard32));
-  if (__builtin_expect(!fast, 0)) {
-    // rare (~0.4 % of lanes): find the values inside the band again and give
-    // only those the exact sequence (an f64 divide each)
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        bool ok;
-        (void)quant_fast<float, 1>(v[u][j], q, ok);
-        if (!ok) {
-          const uint32_t c = quant_exact((double)v[u][j], q);
-          w[u] = (w[u] & ~(0xFFu << (8 * j))) | (c << (8 * j));
-        }
-      }
-  }
+  if (__builtin_expect(!fast, 0)) redo_f32_nb1(v, q, valid, w);  // rare (~0.4 % of lanes)
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
+    if (!((valid >> u) & 1u)) continue;
     const uint32_t c = w[u] + ((b4[u] * 0x204081u) & 0x01010101u);
     if (kStored) store_codes_stored<1>(reinterpret_cast<uint8_t*>(out), *L, gs + u * kBlock, c, 0u);
     else out[u * kBlock] = c;
   }
 }
 
-// One full tile of this lane (groups gb, gb+256, gb+512, gb+768): LCG bits
-// from the cycle table -- group g (elements 4g..4g+3) uses the states
-// s_{4g+1..4g+4} = x_{pos+4g+1..4}, four consecutive table bits (one 8-byte
-// L1/L2-hit load and a funnel shift) -- then quantise, add, pack, store.
+// One tile of this lane (groups gb, gb+256, gb+512, gb+768 of the array x;
+// `valid` as above): LCG bits from the cycle table -- group g (elements 4g..4g+3) uses
+// the states s_{4g+1..4g+4} = x_{pos+4g+1..4}, four consecutive table bits
+// (one 8-byte L1/L2-hit load and a funnel shift) -- then quantise, add, pack,
+// store.
 template <typename V, int NB, bool kStored = false>
-__device__ __forceinline__ void encode_full_tile(const V v[4][4], const QuantParams& q, const EncodeParams& p,
-                                                 uint8_t* __restrict__ out, size_t gb, size_t gs,
-                                                 const StoredLayout* L = nullptr) {
+__device__ __forceinline__ void encode_full_tile(const V v[4][4], const V* x, const QuantParams& q,
+                                                 const EncodeParams& p, uint8_t* __restrict__ out, size_t gb,
+                                                 size_t gs, const StoredLayout* L = nullptr, uint32_t valid = 0xFu) {
   uint32_t b4[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
@@ -650,15 +689,18 @@ __device__ __forceinline__ void encode_full_tile(const V v[4][4], const QuantPar
     b4[u] = __builtin_amdgcn_alignbit(w.y, w.x, k & 31u) & 0xFu;
   }
   if (NB == 1 && sizeof(V) == 4) {
-    if (kStored) encode_tile_f32_nb1<true>(reinterpret_cast<const float(*)[4]>(v), q, b4,
-                                           reinterpret_cast<uint32_t*>(out), L, gs);
-    else encode_tile_f32_nb1(reinterpret_cast<const float(*)[4]>(v), q, b4, reinterpret_cast<uint32_t*>(out) + gs);
+    const float* xg = reinterpret_cast<const float*>(x) + 4 * gb;
+    if (kStored) encode_tile_f32_nb1<true>(reinterpret_cast<const float(*)[4]>(v), xg, q, b4,
+                                           reinterpret_cast<uint32_t*>(out), L, gs, valid);
+    else encode_tile_f32_nb1(reinterpret_cast<const float(*)[4]>(v), xg, q, b4,
+                             reinterpret_cast<uint32_t*>(out) + gs, nullptr, 0, valid);
     return;
   }
   uint32_t fl[4][4];
   quant_tile<V, NB>(v, q, fl);
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
+    if (!((valid >> u) & 1u)) continue;
     uint64_t r[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) r[j] = (uint64_t)(uint32_t)(fl[u][j] + ((b4[u] >> j) & 1u));
@@ -667,29 +709,92 @@ __device__ __forceinline__ void encode_full_tile(const V v[4][4], const QuantPar
   }
 }
 
+// An array's partial last tile (groups past the end masked off): every load
+// issued before any use (they used to go out one group at a time behind a
+// 64-bit LCG jump, and C3's last workgroup finished 2 us after the rest), the
+// LCG bits from the cycle table as in a full tile.
+template <typename V, int NB, bool kStored = false>
+__device__ __forceinline__ void encode_partial_tile(const V* __restrict__ x, bool aligned, size_t ngroups,
+                                                    const QuantParams& q, const EncodeParams& p,
+                                                    uint8_t* __restrict__ out, size_t gb,
+                                                    const StoredLayout* L = nullptr) {
+  V v[4][4];
+  uint32_t valid = 0;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const size_t g = gb + u * kBlock;
+    if (g < ngroups) {
+      valid |= 1u << u;
+      if (aligned) Vec4<V>::load(x + 4 * g, v[u]);
+      else Vec4<V>::loadu(x + 4 * g, v[u]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[u][j] = (V)q.min_f;
+    }
+  }
+  encode_full_tile<V, NB, kStored>(v, x, q, p, out, gb, gb, L, valid);
+}
+
+// A workgroup's first full tile, loaded unconditionally through a buffer
+// descriptor over it (no records when the workgroup has no full tile: the
+// loads return zeros, which nothing reads).  Behind a branch, the loads made
+// the compiler's wait for the partials (issued before them) a vmcnt(0) at the
+// branch's join, i.e. a wait for the tile as well.  Non-temporal, as
+// Vec4::load.
+template <typename V>
+__device__ __forceinline__ void prefetch_tile(const V* x, size_t t0, size_t tf, V v[4][4]) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const bool have = t0 < tf;
+  const V* base = x + (have ? 4 * t0 * kTileGroups : 0);
+  const int bytes = have ? (int)(4 * kTileGroups * sizeof(V)) : 0;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<V*>(base), 0, bytes, 0x00020000);
+  constexpr int kNt = 2;  // gfx950 cache policy bit: nt
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int off = (int)((threadIdx.x + u * kBlock) * 4 * sizeof(V));
+    if (sizeof(V) == 4) {
+      const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, kNt);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[u][j] = (V)__uint_as_float(a[j]);
+    } else {
+      const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, kNt);
+      const u32x4 b = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16, 0, kNt);
+      v[u][0] = (V)__longlong_as_double((long long)((uint64_t)a[1] << 32 | a[0]));
+      v[u][1] = (V)__longlong_as_double((long long)((uint64_t)a[3] << 32 | a[2]));
+      v[u][2] = (V)__longlong_as_double((long long)((uint64_t)b[1] << 32 | b[0]));
+      v[u][3] = (V)__longlong_as_double((long long)((uint64_t)b[3] << 32 | b[2]));
+    }
+  }
+}
+
 template <typename V, int NB, bool kVec>
 __global__ __launch_bounds__(kBlock) void ff_encode(const V* __restrict__ x, size_t n,
                                                      uint8_t* __restrict__ out, EncodeParams p) {
-  // tiles of this workgroup; the first full tile's loads are issued before
-  // the min/max fold so that its latency hides behind them
+  PSF_STAMP(ts0);
+  // tiles of this workgroup; the partials' loads, then the first full
+  // tile's, are issued before the min/max fold so that their latency hides
+  // behind each other (Partials, prefetch_tile)
   const size_t ngroups = n >> 2;
   const size_t ntiles = (ngroups + kTileGroups - 1) / kTileGroups;
   const size_t nfull = ngroups / kTileGroups;
   size_t t0 = 0, t1 = 0;
   if (kVec) {
+    // (workgroup b keeps tile run b: the decode's workgroup b, dealt to the
+    // same XCD, then reads its codes from that XCD's L2.  Rotating the runs by
+    // one, to start the array's partial tile first, cost C3's decode 7.1 ->
+    // 8.4 us for a 0.4 us gain of the encode.)
     tile_range(ntiles, t0, t1, p.reverse ? gridDim.x - 1 - blockIdx.x : blockIdx.x);
   }
   const size_t tf = t1 < nfull ? t1 : nfull;  // full tiles are [t0, tf)
+  Partials<V> parts;
+  if (p.partials != nullptr) parts.load(p.partials, p.nparts);
   V first[4][4];
-  if (kVec && t0 < tf) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u) Vec4<V>::load(x + 4 * (t0 * kTileGroups + threadIdx.x + u * kBlock), first[u]);
-  }
+  if (kVec) prefetch_tile<V>(x, t0, tf, first);
 
   float mn_f = p.preset_min, mx_f = p.preset_max;
   if (p.partials != nullptr) {
     float cmn, cmx;
-    fold_partials<V>(p.partials, p.nparts, cmn, cmx);
+    parts.fold(cmn, cmx);
     if (!p.has_min) mn_f = cmn;
     if (!p.has_max) mx_f = cmx;
   }
@@ -703,6 +808,7 @@ __global__ __launch_bounds__(kBlock) void ff_encode(const V* __restrict__ x, siz
   q.max_f = mx_f;
   q.scale_f = (float)q.scale;
   q.fast = q.bin < __builtin_huge_val();
+  PSF_STAMP(ts1);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     const int status = (q.bin > 0) ? kOk : kErrBin;
     if (p.range_out) { p.range_out[0] = mn_f; p.range_out[1] = mx_f; }
@@ -723,33 +829,18 @@ __global__ __launch_bounds__(kBlock) void ff_encode(const V* __restrict__ x, siz
 
   if (kVec) {
     if (t0 < tf) {
-      encode_full_tile<V, NB>(first, q, p, out, t0 * kTileGroups + threadIdx.x, t0 * kTileGroups + threadIdx.x);
+      encode_full_tile<V, NB>(first, x, q, p, out, t0 * kTileGroups + threadIdx.x, t0 * kTileGroups + threadIdx.x);
       for (size_t t = t0 + 1; t < tf; ++t) {
         const size_t gb = t * kTileGroups + threadIdx.x;
         V v[4][4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) Vec4<V>::load(x + 4 * (gb + u * kBlock), v[u]);
-        encode_full_tile<V, NB>(v, q, p, out, gb, gb);
+        encode_full_tile<V, NB>(v, x, q, p, out, gb, gb);
       }
     }
-    // the partial last tile of the array, if this workgroup owns it: the LCG
-    // state jumps to this lane's first group and steps mod 2^17
-    for (size_t t = (t0 > tf ? t0 : tf); t < t1; ++t) {
-      const size_t gb = t * kTileGroups + threadIdx.x;
-      uint32_t su = lcg_jump(p.seed, 4ull * gb) & kMask17;  // state before element 4gb
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const size_t g = gb + u * kBlock;
-        if (g < ngroups) {
-          V v[4];
-          Vec4<V>::load(x + 4 * g, v);
-          uint64_t r[4];
-          quant_group<V, NB>(v, q, su, p.k17, r);
-          store_codes<NB>(out, g, r);
-        }
-        su = step17(p.a_lane, p.c_lane, su);
-      }
-    }
+    // the partial last tile of the array, if this workgroup owns it
+    for (size_t t = (t0 > tf ? t0 : tf); t < t1; ++t)
+      encode_partial_tile<V, NB>(x, true, ngroups, q, p, out, t * kTileGroups + threadIdx.x);
     // ragged tail (< 4 values): one thread
     const size_t tail = ngroups << 2;
     if (blockIdx.x == 0 && threadIdx.x == 0 && tail < n) {
@@ -771,6 +862,7 @@ __global__ __launch_bounds__(kBlock) void ff_encode(const V* __restrict__ x, siz
       s = p.a_thr * s + p.c_thr;
     }
   }
+  PSF_TRACE_END(ts0, ts1);
 }
 
 // ------------------------------------------------------------- decode ------
@@ -935,8 +1027,6 @@ struct FfBatchT {
   float* range_base;        // encode: device {min, max, status} records of the lazy jobs
   float* ring_base;         // encode: the same records in host-mapped memory
   const uint32_t* lcg_bits;
-  Lcg17 k17;
-  uint32_t a_lane, c_lane;
   uint32_t mm_reverse;     // min/max workgroups dispatched in reverse array order
   uint32_t mm_total_done;  // (host) the min/max pass already ran in a merged launch
   double ratio;
@@ -1332,9 +1422,6 @@ __device__ __forceinline__ int encode_batch_body(const FfBatchT<CAP>& B, uint32_
   EncodeParams p{};  // the per-launch constants the tile code reads
   p.lcg_bits = B.lcg_bits;
   p.lcg_pos = J.u.e.lcg_pos;
-  p.k17 = B.k17;
-  p.a_lane = B.a_lane;
-  p.c_lane = B.c_lane;
   const bool stored = kStored && (NB == 1 || NB == 2) && (J.flags & kFlagStored);
   const StoredLayout L = stored_layout((uint32_t)(n * NB));
   if constexpr (kStored && (NB == 1 || NB == 2)) {
@@ -1344,36 +1431,23 @@ __device__ __forceinline__ int encode_batch_body(const FfBatchT<CAP>& B, uint32_
       for (size_t t = t0; t < tf; ++t) {
         if (t != t0) next_tile(t);
         const size_t gb = t * kTileGroups + threadIdx.x;
-        encode_full_tile<V, NB, true>(v, q, p, out, gb, gb, &L);
+        encode_full_tile<V, NB, true>(v, x, q, p, out, gb, gb, &L);
       }
     }
   }
   if (!stored) {
     for (size_t t = t0; t < tf; ++t) {
       if (t != t0) next_tile(t);
-      encode_full_tile<V, NB>(v, q, p, out, t * kTileGroups + threadIdx.x, t * kTileGroups + threadIdx.x);
+      encode_full_tile<V, NB>(v, x, q, p, out, t * kTileGroups + threadIdx.x, t * kTileGroups + threadIdx.x);
     }
   }
   for (size_t t = (t0 > tf ? t0 : tf); t < t1; ++t) {
     const size_t gb = t * kTileGroups + threadIdx.x;
-    uint32_t su = lcg_jump(J.u.e.seed, 4ull * gb) & kMask17;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const size_t g = gb + u * kBlock;
-      if (g < ngroups) {
-        V v[4];
-        if (al) Vec4<V>::load(x + 4 * g, v);
-        else Vec4<V>::loadu(x + 4 * g, v);
-        uint64_t r[4];
-        quant_group<V, NB>(v, q, su, p.k17, r);
-        if constexpr (kStored && (NB == 1 || NB == 2)) {
-          if (stored) store_codes_stored<NB>(out, L, g, r);
-          else store_codes<NB>(out, g, r);
-        } else {
-          store_codes<NB>(out, g, r);
-        }
-      }
-      su = step17(p.a_lane, p.c_lane, su);
+    if constexpr (kStored && (NB == 1 || NB == 2)) {
+      if (stored) encode_partial_tile<V, NB, true>(x, al, ngroups, q, p, out, gb, &L);
+      else encode_partial_tile<V, NB>(x, al, ngroups, q, p, out, gb);
+    } else {
+      encode_partial_tile<V, NB>(x, al, ngroups, q, p, out, gb);
     }
   }
   const size_t tail = ngroups << 2;
@@ -1479,7 +1553,9 @@ static inline void lcg_affine_pow(uint64_t k, uint32_t& A, uint32_t& Cc) {
   }
 }
 
-// The LCG modulo 2^17 (all the encoder observes, see step17) is one cycle of
+// Only bit 16 of the LCG state is ever observed, and (a*s + c) mod 2^17
+// depends only on s mod 2^17, so the encoder reads its bits off the LCG modulo
+// 2^17, which is one cycle of
 // length 2^17 (a = 1 mod 4, c odd).  Host side: the cycle x_0 = 0,
 // x_{k+1} = a x_k + c, the position of every residue on it, and per device a
 // bit table T[k] = !bit16(x_k) for k < 2^17 + 64 (wrapped), 16 KiB.
@@ -1549,16 +1625,7 @@ static bool enc_perm_mode();
 
 // the LCG jump constants of an encode launch over `grid` workgroups
 static void encode_lcg_params(EncodeParams& p, int grid) {
-  lcg_affine_pow(4ull * kBlock, p.a_lane, p.c_lane);
-  lcg_affine_pow(4ull * kTileGroups, p.a_tile, p.c_tile);
   lcg_affine_pow((uint64_t)grid * kBlock, p.a_thr, p.c_thr);
-  p.a_lane &= kMask17; p.c_lane &= kMask17;
-  p.a_tile &= kMask17; p.c_tile &= kMask17;
-  for (int k = 0; k < 4; ++k) {
-    lcg_affine_pow((uint64_t)k + 1, p.k17.a[k], p.k17.c[k]);
-    p.k17.a[k] &= kMask17;
-    p.k17.c[k] &= kMask17;
-  }
   p.lcg_pos = lcg_cycle().pos[p.seed & kMask17];
 }
 
@@ -1872,14 +1939,6 @@ static int encode_batch_cap(int value_type, int nb, const FfArray* arrs, int cou
   B.lcg_bits = lcg_bits_device();
   if (!B.lcg_bits) return kErrHip;
   B.ratio = ff_ratio(nb);
-  lcg_affine_pow(4ull * kBlock, B.a_lane, B.c_lane);
-  B.a_lane &= kMask17;
-  B.c_lane &= kMask17;
-  for (int k = 0; k < 4; ++k) {
-    lcg_affine_pow((uint64_t)k + 1, B.k17.a[k], B.k17.c[k]);
-    B.k17.a[k] &= kMask17;
-    B.k17.c[k] &= kMask17;
-  }
   uint32_t mm = 0, enc = 0;
   double bytes_mm = 0, bytes_enc = 0;
   const size_t vsz = value_type == kFloat ? 4 : 8;
