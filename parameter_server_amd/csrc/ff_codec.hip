@@ -1682,7 +1682,7 @@ static int encode_typed(const V* x, size_t n, int nb, const FixedPoint& preset, 
     ProfScope ps(prof, kKMinmax, st, (double)n * sizeof(V), true);
     if (vec)
       psf_launch((ff_minmax_partials<V, true>), dim3(grid), dim3(kBlock), 0, st, x, n, partials,
-                         enc_perm_mode() && (double)n * sizeof(V) > 256.0 * (1 << 20) ? 1u : 0u);
+                         1u);  // strided at every size: C3 (40 MB) 3756 -> 3837 GiB/s
     else
       psf_launch((ff_minmax_partials<V, false>), dim3(grid), dim3(kBlock), 0, st, x, n, partials, 0u);
     p.partials = partials;
