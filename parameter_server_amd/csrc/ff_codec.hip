@@ -62,24 +62,38 @@ constexpr uint32_t kMask17 = 0x1FFFFu;   // the LCG bits the encoder uses depend
 
 // ------------------------------------------------------------ helpers ------
 #ifdef PSF_WG_TRACE
-// diagnostic builds only (tools/c3real_probe.hip): per-workgroup s_memrealtime
-// stamps (entry, quantiser ready, last store done) and the XCC / HW ids
-__device__ uint64_t* g_wg_trace;
+// diagnostic builds only (tools/c3real_probe.hip, tools/c1_trace.py):
+// per-workgroup s_memrealtime stamps, 8 words a workgroup: [0] entry, [1]
+// quantiser ready, [2] last store done, [3] XCC id << 32 | HW id; the batched
+// encode also [4] its min/max items done, [5] the hand-off waited out, [6] its
+// own run claimed, [7] its own run published.  Nothing is stamped while the
+// buffer (psf_debug_wg_trace) is unset or past kTraceMax workgroups.
+__device__ uint64_t* g_wg_trace;  // 8 * kTraceMax words
+constexpr uint32_t kTraceMax = 16384;
 #define PSF_STAMP(v) const uint64_t v = __builtin_amdgcn_s_memrealtime()
+#define PSF_STAMP_AT(k)                                                                \
+  do {                                                                                 \
+    if (threadIdx.x == 0 && g_wg_trace && blockIdx.x < kTraceMax)                      \
+      g_wg_trace[8 * blockIdx.x + (k)] = __builtin_amdgcn_s_memrealtime();             \
+  } while (0)
 #define PSF_TRACE_END(a, b)                                                                           \
   do {                                                                                               \
     __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");                                             \
     __syncthreads();                                                                                 \
-    if (threadIdx.x == 0) {                                                                          \
-      uint64_t* tr = g_wg_trace + 4 * blockIdx.x;                                                    \
+    if (threadIdx.x == 0 && g_wg_trace && blockIdx.x < kTraceMax) {                                  \
+      uint64_t* tr = g_wg_trace + 8 * blockIdx.x;                                                    \
       tr[0] = a;                                                                                     \
-      tr[1] = b;                                                                                     \
+      if (b) tr[1] = b;                                                                              \
       tr[2] = __builtin_amdgcn_s_memrealtime();                                                      \
       tr[3] = (uint64_t)__builtin_amdgcn_s_getreg(6164) << 32 | (uint32_t)__builtin_amdgcn_s_getreg(63492); \
     }                                                                                                \
   } while (0)
+extern "C" int psf_debug_wg_trace(void* buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_wg_trace), &buf, sizeof(buf)) == hipSuccess ? 0 : -1;
+}
 #else
 #define PSF_STAMP(v)
+#define PSF_STAMP_AT(k)
 #define PSF_TRACE_END(a, b)
 #endif
 __device__ __forceinline__ uint32_t f32_key(float f) {
@@ -1299,6 +1313,7 @@ __device__ __forceinline__ int encode_batch_body(const FfBatchT<CAP>& B, uint32_
         __syncthreads();
         const bool mine = ((__builtin_amdgcn_readfirstlane(s_item) >> wg) & 1u) == 0;
         __syncthreads();  // (s_item is written again below)
+        PSF_STAMP_AT(6);
         if (mine) {
           own = t0 < t1 && t1 <= tf && t1 - t0 <= 2;
           if (own) {
@@ -1322,6 +1337,7 @@ __device__ __forceinline__ int encode_batch_body(const FfBatchT<CAP>& B, uint32_
             items(min(wg * per, (uint32_t)J.mm_nwg), min(wg * per + per, (uint32_t)J.mm_nwg));
           }
         }
+        PSF_STAMP_AT(7);
         const uint32_t all = nwg == 32 ? ~0u : (1u << nwg) - 1u;
         if (threadIdx.x == 0) s_item = __hip_atomic_fetch_or(&c[0], all, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();
@@ -1339,12 +1355,14 @@ __device__ __forceinline__ int encode_batch_body(const FfBatchT<CAP>& B, uint32_
         const uint32_t i0 = __builtin_amdgcn_readfirstlane(s_item);
         items(i0, i0 + per < (uint32_t)J.mm_nwg ? i0 + per : (uint32_t)J.mm_nwg);
       }
+      PSF_STAMP_AT(4);
       if (threadIdx.x == 0) s_late = wait_ready(&c[1], J.mm_nwg) ? 0u : 1u;
 #ifdef PSF_FUSED_DEBUG
       if (threadIdx.x == 0 && s_late != 0)
         printf("fused: job %d wg %u timed out: claims %u ready %u done %u want %u\n", jb, wg, c[0], c[1], c[2], (uint32_t)J.mm_nwg);
 #endif
       __syncthreads();
+      PSF_STAMP_AT(5);
       late = __builtin_amdgcn_readfirstlane(s_late) != 0;
       for (uint32_t i = threadIdx.x; i < J.mm_nwg; i += kBlock) {
         const K a = __hip_atomic_load(&pp[mm_wg0 + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1383,6 +1401,7 @@ __device__ __forceinline__ int encode_batch_body(const FfBatchT<CAP>& B, uint32_
   q.max_f = mx_f;
   q.scale_f = (float)q.scale;
   q.fast = q.bin < __builtin_huge_val();
+  PSF_STAMP_AT(1);
   if (wg == 0 && threadIdx.x == 0) {
     const int status = late ? kErrHip : (q.bin > 0) ? kOk : kErrBin;
     if (J.lazy != kNoLazy) {
@@ -1523,8 +1542,10 @@ __global__ __launch_bounds__(kBlock) void ff_dec_mm_batch(FfBatchT<kBatchSmall> 
 template <typename V, int NB, bool kStored>
 __global__ __launch_bounds__(kBlock) void ff_fused_batch(FfBatchT<kBatchSmall> D, FfBatchT<kBatchSmall> B, uint32_t* ctl,
                                                          int32_t* sticky) {
+  PSF_STAMP(ts0);
   if (blockIdx.x < D.total) {
     decode_batch_body<V, NB, kBatchSmall>(D, blockIdx.x);
+    PSF_TRACE_END(ts0, 0ull);
     return;
   }
   const int jb = encode_batch_body<V, NB, kBatchSmall, kStored>(B, blockIdx.x - D.total, ctl, sticky);
@@ -1539,6 +1560,7 @@ __global__ __launch_bounds__(kBlock) void ff_fused_batch(FfBatchT<kBatchSmall> D
       }
     }
   }
+  PSF_TRACE_END(ts0, 0ull);
 }
 
 // ------------------------------------------------------------ launchers ----

@@ -155,8 +155,8 @@ int main(int argc, char** argv) {
   CK(hipHostMalloc((void**)&pub, sizeof(psf::PubSlot) * NA, hipHostMallocMapped | hipHostMallocCoherent));
 #ifdef PSF_WG_TRACE
   uint64_t* trace;
-  CK(hipMalloc(&trace, 8 * 4 * 16384));
-  CK(hipMemset(trace, 0, 8 * 4 * 16384));
+  CK(hipMalloc(&trace, 8 * 8 * 16384));
+  CK(hipMemset(trace, 0, 8 * 8 * 16384));
   CK(hipMemcpyToSymbol(HIP_SYMBOL(psf::g_wg_trace), &trace, sizeof(trace)));
 #endif
   hipStream_t st;
@@ -189,8 +189,10 @@ int main(int argc, char** argv) {
   // how long to its quantiser, to its last store; the 12 last to finish
   {
     int grid = (int)((n / 4 + 1023) / 1024);
-    std::vector<uint64_t> tr(4 * (size_t)grid);
-    CK(hipMemcpy(tr.data(), trace, tr.size() * 8, hipMemcpyDeviceToHost));
+    std::vector<uint64_t> tr8(8 * (size_t)grid), tr(4 * (size_t)grid);
+    CK(hipMemcpy(tr8.data(), trace, tr8.size() * 8, hipMemcpyDeviceToHost));
+    for (int b = 0; b < grid; ++b)
+      for (int k = 0; k < 4; ++k) tr[4 * b + k] = tr8[8 * b + k];
     while (grid > 1 && tr[4 * (grid - 1) + 2] == 0) --grid;  // a launch of fewer workgroups
     printf("grid %d\n", grid);
     uint64_t s0 = ~0ull, e1 = 0;

@@ -1,6 +1,7 @@
 set -e
 cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out/r06l
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r06l/gputest.log 2>&1
-tail -2 gpurun_out/r06l/gputest.log
-for c in c3 c3miss c1; do timeout -k 10 300 python bench.py --config $c --no-host-floor > gpurun_out/r06l/bench_$c.json 2> gpurun_out/r06l/bench_$c.err; tail -c 300 gpurun_out/r06l/bench_$c.json; echo; done
+O=gpurun_out/r06o; mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_gpu_batch.py tests/test_gpu_fused.py -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1
+tail -1 $O/tests.log
+PSF_LIBRARY_VARIANT=tools/variants/trace/libpsf.so timeout -k 10 200 python tools/c1_trace.py > $O/trace.txt 2>&1
+ROUNDS=3 CONFIGS="c1" EXTRA="--no-host-floor" timeout -k 10 900 bash tools/ab.sh r06o_c1 base head > $O/ab.log 2>&1
