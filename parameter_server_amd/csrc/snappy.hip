@@ -1088,7 +1088,7 @@ __global__ __launch_bounds__(kScanT) void snappy_scan(const SnappyCJobs J) {
 }
 
 // ---- K-place: one workgroup of 256 per fragment
-constexpr uint32_t kPlaceT = 256;
+constexpr uint32_t kPlaceT = 256;  // (512: C5 + COMPRESSING 1377 -> 1364, 1024: 1281 GiB/s)
 constexpr int kMoveRows = 6;  // rows of 63 16-byte chunks per wave and pass (58 VGPRs: 8 waves per SIMD)
 constexpr uint32_t kMovePass = kMoveRows * (kPlaceT / 64) * 63;  // chunks per pass (23.6 KiB)
 
@@ -1149,11 +1149,15 @@ __device__ void place_moved(uint8_t* d, const uint8_t* tg, uint32_t op, const ui
 
 // Streams of up to kInlineScan fragments need no K-scan: the workgroup of
 // fragment k sums the lengths of the stream's fragments itself (all full but
-// the last), the workgroup of fragment 0 writes the varint header and the last
-// fragment's publishes the stream length.
+// the last); the workgroup of fragment 0 writes the varint header and
+// publishes the stream length and mode -- the first workgroup of the stream
+// to run, so the host, which needs them to finish the compress and launch the
+// decode behind it, has them while K-place still runs (published by the last
+// fragment's workgroup they arrived at its end, and the decode started 12-15
+// us after it: C5 + COMPRESSING's kernel trace).
 constexpr uint32_t kInlineScan = 4096;
 __global__ __launch_bounds__(kPlaceT) void snappy_place(const SnappyCJobs J, const uint8_t* __restrict__ scratch) {
-  __shared__ uint64_t s_part[kPlaceT / 64];
+  __shared__ uint64_t s_part[kPlaceT / 64], s_all[kPlaceT / 64];
   __shared__ int64_t s_tot[kPlaceT / 64];
   __shared__ int64_t s_lo[kPlaceT / 64], s_hi[kPlaceT / 64];
   __shared__ uint32_t s_any[kPlaceT / 64];
@@ -1178,7 +1182,7 @@ __global__ __launch_bounds__(kPlaceT) void snappy_place(const SnappyCJobs J, con
     // stored they come out -- whose prefix sums are the fragments' shifts
     const uint32_t q = (c.nfrag + kPlaceT - 1) / kPlaceT;
     const uint32_t i0 = min(c.nfrag, tid * q), i1 = min(c.nfrag, i0 + q);
-    uint64_t part = 0;
+    uint64_t part = 0, all = 0;
     uint32_t any = 0;
     int64_t tot = 0;
     for (uint32_t i = i0; i < i1; ++i) {
@@ -1186,23 +1190,28 @@ __global__ __launch_bounds__(kPlaceT) void snappy_place(const SnappyCJobs J, con
       const uint32_t li = (uint32_t)min((size_t)kFrag, c.n - (size_t)i * kFrag);
       const uint32_t fl = frag_len(fi, li);
       if (i < k) part += fl;
+      if (k == 0) all += fl;
       any |= fi != 0 ? 1u : 0u;
       tot += (int64_t)fl - (int64_t)frag_len(0, li);
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
       part += __shfl_xor(part, o, 64);
+      all += __shfl_xor(all, o, 64);
       any |= __shfl_xor(any, o, 64);
     }
     if (lane == 0) {
       s_part[wave] = part;
+      s_all[wave] = all;
       s_any[wave] = any;
     }
     __syncthreads();
     off = c.hdr;
+    uint64_t size = c.hdr;  // (fragment 0's workgroup: the stream's length)
     any = 0;
     for (uint32_t w = 0; w < kPlaceT / 64; ++w) {
       off += s_part[w];
+      size += s_all[w];
       any |= s_any[w];
     }
     mode = !c.stored ? kPlaceCopy : !any ? kPlaceStored : kPlaceCopy;
@@ -1242,9 +1251,9 @@ __global__ __launch_bounds__(kPlaceT) void snappy_place(const SnappyCJobs J, con
     }
     if (k == 0 && tid < c.hdr && mode == kPlaceCopy)
       c.dst[tid] = (uint8_t)(((uint32_t)c.n >> (7 * tid)) | (tid + 1 < c.hdr ? 128u : 0u));
-    if (k + 1 == c.nfrag && tid == 0 && J.pub) {
+    if (k == 0 && tid == 0 && J.pub) {
       PubSlot* pub = J.pub + c.slot;
-      pub_store(&pub->size, (uint64_t)(off + frag_len(info, len)));
+      pub_store(&pub->size, size);
       pub_store(&pub->status, (int32_t)kOk);
       pub_store(&pub->pad, mode != kPlaceCopy ? (uint32_t)kStoredInPlace : 0u);
       publish_ticket(pub, c.ticket);
