@@ -122,7 +122,10 @@ void PushRouter::encode_launch(const Message* const* streams, int n, bool origin
 
 void PushRouter::encode_finish(int64_t* sizes) {
   const int64_t t0 = now_ns();
-  pend_.finish();
+  {
+    PSF_HPROF(15);
+    pend_.finish();
+  }
   local_.reserve(local_.size() + slices_.size());
   local_server_.reserve(local_server_.size() + slices_.size());
   std::vector<Message*> remote;

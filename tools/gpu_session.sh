@@ -1,4 +1,6 @@
 set -e
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/r06r; mkdir -p $O
-TESTS="tests/test_gpu_snappy.py tests/test_gpu_stored.py" ROUNDS=3 CONFIGS="c5z c5zm" EXTRA="--no-host-floor" timeout -k 10 1000 bash tools/ab.sh r06r_place base pt512 pt1024 > $O/ab.log 2>&1
+O=gpurun_out/r06t2; mkdir -p $O
+
+
+ROUNDS=4 CONFIGS="c1" EXTRA="--no-host-floor" timeout -k 10 900 bash tools/ab.sh r06t2_c1 base head > $O/ab.log 2>&1

@@ -43,7 +43,7 @@ def main():
     print(f"step {dt:.1f} us")
     if a.config in ("c4", "c5"):
         NAMES.update({0: "router decode_batch", 1: "router prefetch (slice_begin)", 5: "router decode finish",
-                      12: "router slice_end", 13: "router encode_batch"})
+                      12: "router slice_end", 13: "router encode_batch", 15: "router encode finish"})
     for i in range(16):
         if n[i]:
             print(f"{NAMES.get(i, i):28s} {ns[i] / steps / 1e3:8.2f} us/step  calls/step {n[i] / steps:.1f}")
