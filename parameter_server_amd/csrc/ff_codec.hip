@@ -1822,7 +1822,7 @@ static size_t tiles_of(size_t n) { return ((n >> 2) + kTileGroups - 1) / kTileGr
 // the single-array one -- 4096 measured 9 % faster than 1024 on C4's 512 x 1 MiB
 // slices (8192: 4 % more), where 1024 is best for one 1 GiB array (tools/ab_c4.sh, r02)
 #ifndef PSF_BATCH_MINMAX_GRID
-#define PSF_BATCH_MINMAX_GRID 8192
+#define PSF_BATCH_MINMAX_GRID 16384  // r06: 16384 against 8192 on C4, min/max 86.8 -> 83.3 us (4786 -> 4803 GiB/s; 32768: 91.6)
 #endif
 constexpr int kBatchMinmaxGrid = PSF_BATCH_MINMAX_GRID;
 #ifndef PSF_BATCH_STREAM_GRID
