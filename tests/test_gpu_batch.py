@@ -85,6 +85,46 @@ def test_batch_matches_single_and_port(ctx, port, compress):
         F.set_clock(None)
 
 
+@pytest.mark.parametrize("compress", [False, True])
+def test_batch_guard_band_values(ctx, port, compress):
+    """Batched f32 num_bytes=1 encodes (the fused small-batch launch and the
+    stored-stream one) of values on and next to the quantisation grid, where
+    every lane's band test fails and the rolled exact pass decides each code,
+    in arrays whose last tile is partial: codes and decoded values against the
+    C restatement."""
+    from parameter_server_amd import filter as F
+    F.set_clock(2024)
+    try:
+        rng = np.random.default_rng(77)
+        cases = []
+        for n, preset in ((4099, (-1.0, 1.0)), (70_001, None), (262_147, (-3.5, 12.25)), (5, None)):
+            mn, mx = preset if preset else (-2.0, 3.0)
+            k = rng.integers(0, 255, n)
+            g = (np.float64(mn) + k * ((np.float64(mx) - np.float64(mn)) / 254.0)).astype(np.float32)
+            side = rng.integers(0, 3, n)
+            x = np.where(side == 0, g, np.where(side == 1, np.nextafter(g, np.float32(np.inf)),
+                                                np.nextafter(g, np.float32(-np.inf)))).astype(np.float32)
+            cases.append((x, 1, preset, None))
+        snd = [F.RemoteNode(ctx) for _ in cases]
+        rcv = [F.RemoteNode(ctx) for _ in cases]
+        ms = [_message(F, *c, ch=i, compress=compress) for i, c in enumerate(cases)]
+        F.RemoteNode.encode_many(snd, ms)
+        ws = [m.clone() for m in ms]
+        F.RemoteNode.decode_many(rcv, ws)
+        ctx.sync()
+        for i, (x, nb, preset, _) in enumerate(cases):
+            mn = None if preset is None else preset[0]
+            mx = None if preset is None else preset[1]
+            st, codes, pmn, pmx = port.ff_encode(x, nb, 2024, mn, mx)
+            assert st == 0
+            if not compress:
+                assert snd[i].value(ms[i], 0).cpu().numpy().tobytes() == codes.tobytes(), i
+            st, dec = port.ff_decode(codes, nb, pmn, pmx, np.float32)
+            assert rcv[i].value(ws[i], 0).cpu().numpy().tobytes() == dec.tobytes(), i
+    finally:
+        F.set_clock(None)
+
+
 def test_batch_deferred_decode(ctx, port):
     from parameter_server_amd import filter as F
     F.set_clock(55)
