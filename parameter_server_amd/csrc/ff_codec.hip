@@ -304,16 +304,20 @@ __global__ __launch_bounds__(kBlock) void ff_minmax_partials(const V* __restrict
 #pragma unroll
           for (int j = 0; j < 4; ++j) acc_minmax<V, K>(v[u][j], lo, hi);
       } else {
+        // the array's partial last tile: every load issued before any use
+        // (one group at a time, its loads waited one memory latency each)
+        V v[4][4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const size_t g = gb + u * kBlock;
-          if (g < ngroups) {
-            V v[4];
-            Vec4<V>::load(x + 4 * g, v);
+          if (gb + u * kBlock < ngroups) Vec4<V>::load(x + 4 * (gb + u * kBlock), v[u]);
+          else
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc_minmax<V, K>(v[j], lo, hi);
-          }
+            for (int j = 0; j < 4; ++j) v[u][j] = (V)__builtin_nan("");  // skipped by acc_minmax
         }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc_minmax<V, K>(v[u][j], lo, hi);
       }
     }
     if (blockIdx.x == 0)
@@ -1168,19 +1172,24 @@ __device__ __forceinline__ void minmax_item(const FfBatchT<CAP>& B, int jb, uint
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc_minmax<V, K>(v[u][j], lo, hi);
   }
-  for (size_t t = (t0 > tf ? t0 : tf); t < t1; ++t) {  // the partial last tile
+  for (size_t t = (t0 > tf ? t0 : tf); t < t1; ++t) {  // the partial last tile: loads before any use
     const size_t gb = t * kTileGroups + threadIdx.x;
+    V v[4][4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const size_t g = gb + u * kBlock;
       if (g < ngroups) {
-        V v[4];
-        if (al) Vec4<V>::load(x + 4 * g, v);
-        else Vec4<V>::loadu(x + 4 * g, v);
+        if (al) Vec4<V>::load(x + 4 * g, v[u]);
+        else Vec4<V>::loadu(x + 4 * g, v[u]);
+      } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc_minmax<V, K>(v[j], lo, hi);
+        for (int j = 0; j < 4; ++j) v[u][j] = (V)__builtin_nan("");  // skipped by acc_minmax
       }
     }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc_minmax<V, K>(v[u][j], lo, hi);
   }
   if (wg == 0)
     for (size_t i = (ngroups << 2) + threadIdx.x; i < n; i += kBlock) acc_minmax<V, K>(x[i], lo, hi);
