@@ -961,6 +961,25 @@ __device__ __forceinline__ void decode_tile(const uint8_t* __restrict__ code, V*
 template <typename V, int NB, bool kVec>
 __global__ __launch_bounds__(kBlock) void ff_decode(const uint8_t* __restrict__ code, size_t n,
                                                      V* __restrict__ out, DecodeParams p) {
+  // nb = 1: the first tile's code words go out before the range read and the
+  // table build, whose latency they then hide (LDS-only barrier: the table's
+  // __syncthreads would wait for them)
+  uint32_t w0[4];
+  size_t t0 = 0, t1 = 0;
+  const size_t ngroups = n >> 2;
+  if (kVec && NB == 1) {
+    const size_t ntiles = (ngroups + kTileGroups - 1) / kTileGroups;
+    tile_range(ntiles, t0, t1);
+    if (t0 < t1) {
+      const uint32_t* c32 = reinterpret_cast<const uint32_t*>(code);
+      const size_t gb = t0 * kTileGroups + threadIdx.x;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const size_t g = gb + u * kBlock;
+        w0[u] = c32[g < ngroups ? g : ngroups - 1];
+      }
+    }
+  }
   float mn_f = p.mn, mx_f = p.mx;
   if (p.range) { mn_f = p.range[0]; mx_f = p.range[1]; }
   const double min_v = (double)mn_f, max_v = (double)mx_f;
@@ -968,15 +987,25 @@ __global__ __launch_bounds__(kBlock) void ff_decode(const uint8_t* __restrict__ 
   const double ratio = p.ratio;
 
   if (kVec && NB <= 3) {
-    const size_t ngroups = n >> 2;
     const size_t ntiles = (ngroups + kTileGroups - 1) / kTileGroups;
-    size_t t0, t1;
-    tile_range(ntiles, t0, t1);
+    if (NB != 1) tile_range(ntiles, t0, t1);
     __shared__ V lut[256];
     if (NB == 1) {
       // 256-entry table, same formula => bit-identical to the per-element path
       lut[threadIdx.x] = dequant<V>((uint64_t)threadIdx.x, ratio, bin, min_v);
-      __syncthreads();
+      lds_barrier();
+      if (t0 < t1) {  // the prefetched first tile
+        const size_t gb = t0 * kTileGroups + threadIdx.x;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const size_t g = gb + u * kBlock;
+          if (g < ngroups) {
+            V v[4] = {lut[w0[u] & 0xFF], lut[(w0[u] >> 8) & 0xFF], lut[(w0[u] >> 16) & 0xFF], lut[w0[u] >> 24]};
+            Vec4<V>::store(out + 4 * g, v);
+          }
+        }
+        ++t0;
+      }
     }
     for (size_t t = t0; t < t1; ++t)
       decode_tile<V, NB>(code, out, t * kTileGroups + threadIdx.x, ngroups, lut, ratio, bin, min_v);
@@ -1506,19 +1535,43 @@ __device__ __forceinline__ void decode_batch_body(const FfBatchT<CAP>& B, uint32
   V* __restrict__ out = static_cast<V*>(J.out);
   const size_t n = J.n;
   const uint32_t wg = block - B.first[jb];
+  const size_t ngroups = n >> 2;
+  const size_t ntiles = (ngroups + kTileGroups - 1) / kTileGroups;
+  size_t t0, t1;
+  tile_range_of(ntiles, wg, batch_nwg(B, jb), t0, t1);
+  // nb = 1: the first tile's code words before the range read and the table
+  // build (as ff_decode)
+  uint32_t w0[4];
+  if (NB == 1 && t0 < t1) {
+    const uint32_t* c32 = reinterpret_cast<const uint32_t*>(code);
+    const size_t gb = t0 * kTileGroups + threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const size_t g = gb + u * kBlock;
+      w0[u] = c32[g < ngroups ? g : ngroups - 1];
+    }
+  }
   float mn_f = J.mn, mx_f = J.mx;
   if (J.u.range) { mn_f = J.u.range[0]; mx_f = J.u.range[1]; }
   const double min_v = (double)mn_f, max_v = (double)mx_f;
   const double bin = max_v - min_v;
   const double ratio = B.ratio;
-  const size_t ngroups = n >> 2;
-  const size_t ntiles = (ngroups + kTileGroups - 1) / kTileGroups;
-  size_t t0, t1;
-  tile_range_of(ntiles, wg, batch_nwg(B, jb), t0, t1);
   __shared__ V lut[256];
   if (NB == 1) {
     lut[threadIdx.x] = dequant<V>((uint64_t)threadIdx.x, ratio, bin, min_v);
-    __syncthreads();
+    lds_barrier();
+    if (t0 < t1) {
+      const size_t gb = t0 * kTileGroups + threadIdx.x;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const size_t g = gb + u * kBlock;
+        if (g < ngroups) {
+          V v[4] = {lut[w0[u] & 0xFF], lut[(w0[u] >> 8) & 0xFF], lut[(w0[u] >> 16) & 0xFF], lut[w0[u] >> 24]};
+          Vec4<V>::store(out + 4 * g, v);
+        }
+      }
+      ++t0;
+    }
   }
   for (size_t t = t0; t < t1; ++t)
     decode_tile<V, NB>(code, out, t * kTileGroups + threadIdx.x, ngroups, lut, ratio, bin, min_v);
