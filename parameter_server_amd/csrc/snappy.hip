@@ -1147,6 +1147,91 @@ __device__ void place_moved(uint8_t* d, const uint8_t* tg, uint32_t op, const ui
   if (op) copy_bytes<kPlaceT>(d, tg, op, tid);
 }
 
+// A K-place workgroup's view of stream c (no K-scan): the offset of its
+// fragment k, the stream's length and its PlaceMode.  Thread t takes fragments
+// [t q, t q + q): their lengths before fragment k, whether any has tags, and
+// (a stored job) how much longer than stored they come out -- whose prefix
+// sums are the fragments' shifts.
+struct PlaceLds {
+  uint64_t part[kPlaceT / 64], all[kPlaceT / 64];
+  int64_t tot[kPlaceT / 64], lo[kPlaceT / 64], hi[kPlaceT / 64];
+  uint32_t any[kPlaceT / 64];
+};
+__device__ __forceinline__ void place_summary(const SnappyCJobs& J, const CJob& c, uint32_t k, PlaceLds& S,
+                                              uint64_t& off, uint64_t& size, uint32_t& mode) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t q = (c.nfrag + kPlaceT - 1) / kPlaceT;
+  const uint32_t i0 = min(c.nfrag, tid * q), i1 = min(c.nfrag, i0 + q);
+  uint64_t part = 0, all = 0;
+  uint32_t any = 0;
+  int64_t tot = 0;
+  for (uint32_t i = i0; i < i1; ++i) {
+    const uint64_t fi = J.finfo[c.frag0 + i];
+    const uint32_t li = (uint32_t)min((size_t)kFrag, c.n - (size_t)i * kFrag);
+    const uint32_t fl = frag_len(fi, li);
+    if (i < k) part += fl;
+    all += fl;
+    any |= fi != 0 ? 1u : 0u;
+    tot += (int64_t)fl - (int64_t)frag_len(0, li);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    part += __shfl_xor(part, o, 64);
+    all += __shfl_xor(all, o, 64);
+    any |= __shfl_xor(any, o, 64);
+  }
+  if (lane == 0) {
+    S.part[wave] = part;
+    S.all[wave] = all;
+    S.any[wave] = any;
+  }
+  __syncthreads();
+  off = c.hdr;
+  size = c.hdr;
+  any = 0;
+  for (uint32_t w = 0; w < kPlaceT / 64; ++w) {
+    off += S.part[w];
+    size += S.all[w];
+    any |= S.any[w];
+  }
+  mode = !c.stored ? kPlaceCopy : !any ? kPlaceStored : kPlaceCopy;
+  int64_t lo = 0, hi = 0;
+  if (c.stored && any) {
+    int64_t x = tot;  // the shift of fragment i0: the exclusive sum of the totals
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t y = __shfl_up(x, o, 64);
+      if ((int)lane >= o) x += y;
+    }
+    if (lane == 63) S.tot[wave] = x;
+    __syncthreads();
+    int64_t run = x - tot;
+    for (uint32_t w = 0; w < wave; ++w) run += S.tot[w];
+    for (uint32_t i = i0; i < i1; ++i) {
+      const uint32_t li = (uint32_t)min((size_t)kFrag, c.n - (size_t)i * kFrag);
+      run += (int64_t)frag_len(J.finfo[c.frag0 + i], li) - (int64_t)frag_len(0, li);
+      lo = min(lo, run);  // (the shift of fragment i + 1, or the growth at the end)
+      hi = max(hi, run);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      lo = min(lo, (int64_t)__shfl_xor(lo, o, 64));
+      hi = max(hi, (int64_t)__shfl_xor(hi, o, 64));
+    }
+    if (lane == 0) {
+      S.lo[wave] = lo;
+      S.hi[wave] = hi;
+    }
+    __syncthreads();
+    for (uint32_t w = 0; w < kPlaceT / 64; ++w) {
+      lo = min(lo, S.lo[w]);
+      hi = max(hi, S.hi[w]);
+    }
+    if (lo >= -kShiftMax && hi <= kShiftMax) mode = kPlaceShift;
+  }
+  __syncthreads();  // (S is used again by the caller)
+}
+
 // Streams of up to kInlineScan fragments need no K-scan: the workgroup of
 // fragment k sums the lengths of the stream's fragments itself (all full but
 // the last); the workgroup of fragment 0 writes the varint header and
@@ -1157,11 +1242,26 @@ __device__ void place_moved(uint8_t* d, const uint8_t* tg, uint32_t op, const ui
 // us after it: C5 + COMPRESSING's kernel trace).
 constexpr uint32_t kInlineScan = 4096;
 __global__ __launch_bounds__(kPlaceT) void snappy_place(const SnappyCJobs J, const uint8_t* __restrict__ scratch) {
-  __shared__ uint64_t s_part[kPlaceT / 64], s_all[kPlaceT / 64];
-  __shared__ int64_t s_tot[kPlaceT / 64];
-  __shared__ int64_t s_lo[kPlaceT / 64], s_hi[kPlaceT / 64];
-  __shared__ uint32_t s_any[kPlaceT / 64];
-  const uint32_t f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __shared__ PlaceLds S;
+  const uint32_t f = blockIdx.x, tid = threadIdx.x;
+  // no K-scan: block j (among the first to run) publishes stream j's length
+  // and mode, which the host needs to finish the compress and launch the
+  // decode behind it -- it has them while K-place runs (published by the
+  // stream's last, then its first fragment's workgroup, they arrived late in
+  // K-place, and the decode started 12 us after it: kernel trace)
+  if (!J.offset && blockIdx.x < J.njobs && J.pub) {
+    const CJob& cj = J.j[blockIdx.x];
+    uint64_t o, size;
+    uint32_t m;
+    place_summary(J, cj, cj.nfrag, S, o, size, m);
+    if (tid == 0) {
+      PubSlot* pub = J.pub + cj.slot;
+      pub_store(&pub->size, size);
+      pub_store(&pub->status, (int32_t)kOk);
+      pub_store(&pub->pad, m != kPlaceCopy ? (uint32_t)kStoredInPlace : 0u);
+      publish_ticket(pub, cj.ticket);
+    }
+  }
   const uint32_t ji = cjob_index(J, f);
   const CJob& c = J.j[ji];
   const uint32_t k = f - c.frag0;
@@ -1170,94 +1270,16 @@ __global__ __launch_bounds__(kPlaceT) void snappy_place(const SnappyCJobs J, con
   const uint64_t info = J.finfo[f];
   const uint32_t op = (uint32_t)(info >> 32), ne = (uint32_t)info;
   PSF_TRACE(f, 2);
-  uint64_t off;
+  uint64_t off, size;
   uint32_t mode;
   if (J.offset) {
     mode = J.in_place[ji];
     if (mode == kPlaceStored) return;  // K-scan found every fragment stored: the stream is in place
     off = J.offset[f];
   } else {
-    // thread t takes fragments [t q, t q + q): their lengths before this
-    // fragment, whether any has tags, and (a stored job) how much longer than
-    // stored they come out -- whose prefix sums are the fragments' shifts
-    const uint32_t q = (c.nfrag + kPlaceT - 1) / kPlaceT;
-    const uint32_t i0 = min(c.nfrag, tid * q), i1 = min(c.nfrag, i0 + q);
-    uint64_t part = 0, all = 0;
-    uint32_t any = 0;
-    int64_t tot = 0;
-    for (uint32_t i = i0; i < i1; ++i) {
-      const uint64_t fi = J.finfo[c.frag0 + i];
-      const uint32_t li = (uint32_t)min((size_t)kFrag, c.n - (size_t)i * kFrag);
-      const uint32_t fl = frag_len(fi, li);
-      if (i < k) part += fl;
-      if (k == 0) all += fl;
-      any |= fi != 0 ? 1u : 0u;
-      tot += (int64_t)fl - (int64_t)frag_len(0, li);
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      part += __shfl_xor(part, o, 64);
-      all += __shfl_xor(all, o, 64);
-      any |= __shfl_xor(any, o, 64);
-    }
-    if (lane == 0) {
-      s_part[wave] = part;
-      s_all[wave] = all;
-      s_any[wave] = any;
-    }
-    __syncthreads();
-    off = c.hdr;
-    uint64_t size = c.hdr;  // (fragment 0's workgroup: the stream's length)
-    any = 0;
-    for (uint32_t w = 0; w < kPlaceT / 64; ++w) {
-      off += s_part[w];
-      size += s_all[w];
-      any |= s_any[w];
-    }
-    mode = !c.stored ? kPlaceCopy : !any ? kPlaceStored : kPlaceCopy;
-    int64_t lo = 0, hi = 0;
-    if (c.stored && any) {
-      int64_t x = tot;  // the shift of fragment i0: the exclusive sum of the totals
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const int64_t y = __shfl_up(x, o, 64);
-        if ((int)lane >= o) x += y;
-      }
-      if (lane == 63) s_tot[wave] = x;
-      __syncthreads();
-      int64_t run = x - tot;
-      for (uint32_t w = 0; w < wave; ++w) run += s_tot[w];
-      for (uint32_t i = i0; i < i1; ++i) {
-        const uint32_t li = (uint32_t)min((size_t)kFrag, c.n - (size_t)i * kFrag);
-        run += (int64_t)frag_len(J.finfo[c.frag0 + i], li) - (int64_t)frag_len(0, li);
-        lo = min(lo, run);  // (the shift of fragment i + 1, or the growth at the end)
-        hi = max(hi, run);
-      }
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        lo = min(lo, (int64_t)__shfl_xor(lo, o, 64));
-        hi = max(hi, (int64_t)__shfl_xor(hi, o, 64));
-      }
-      if (lane == 0) {
-        s_lo[wave] = lo;
-        s_hi[wave] = hi;
-      }
-      __syncthreads();
-      for (uint32_t w = 0; w < kPlaceT / 64; ++w) {
-        lo = min(lo, s_lo[w]);
-        hi = max(hi, s_hi[w]);
-      }
-      if (lo >= -kShiftMax && hi <= kShiftMax) mode = kPlaceShift;
-    }
+    place_summary(J, c, k, S, off, size, mode);
     if (k == 0 && tid < c.hdr && mode == kPlaceCopy)
       c.dst[tid] = (uint8_t)(((uint32_t)c.n >> (7 * tid)) | (tid + 1 < c.hdr ? 128u : 0u));
-    if (k == 0 && tid == 0 && J.pub) {
-      PubSlot* pub = J.pub + c.slot;
-      pub_store(&pub->size, size);
-      pub_store(&pub->status, (int32_t)kOk);
-      pub_store(&pub->pad, mode != kPlaceCopy ? (uint32_t)kStoredInPlace : 0u);
-      publish_ticket(pub, c.ticket);
-    }
     if (mode == kPlaceStored) return;  // FIXING_FLOAT wrote the stream, header and tags included
   }
   if (mode == kPlaceShift) {
