@@ -144,6 +144,33 @@ template <typename K> __device__ __forceinline__ K wave_max(K v) {
   return v;
 }
 
+// 32-bit keys: the GFX9 DPP reduction -- xor 1 and xor 2 within a quad, the
+// half-row and row mirrors, then row 15 broadcast into rows 1 / 3 and lane 31
+// into rows 2-3 -- leaves the wave's result in lane 63, read out as a scalar.
+// Six DPP-operand min/max instructions against the butterfly's six
+// ds_bpermute round trips and their index arithmetic (~40 VALU per wave in
+// each encode workgroup's prologue fold, on its critical path).  Masked-off
+// rows get the op's identity as `old` (op(v, id) = v), which also lets the
+// compiler fold each DPP move into its min / max (one VALU a step).
+template <int kCtrl, int kRowMask, uint32_t kId>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)kId, (int)v, kCtrl, kRowMask, 0xF, false);
+}
+template <bool kMax>
+__device__ __forceinline__ uint32_t wave_reduce_dpp(uint32_t v) {
+  constexpr uint32_t I = kMax ? 0u : 0xFFFFFFFFu;
+  auto op = [](uint32_t a, uint32_t b) { return kMax ? (a > b ? a : b) : (a < b ? a : b); };
+  v = op(v, dpp_u32<0xB1, 0xF, I>(v));   // quad_perm [1,0,3,2]
+  v = op(v, dpp_u32<0x4E, 0xF, I>(v));   // quad_perm [2,3,0,1]
+  v = op(v, dpp_u32<0x141, 0xF, I>(v));  // row_half_mirror
+  v = op(v, dpp_u32<0x140, 0xF, I>(v));  // row_mirror
+  v = op(v, dpp_u32<0x142, 0xA, I>(v));  // row_bcast:15 -> rows 1, 3
+  v = op(v, dpp_u32<0x143, 0xC, I>(v));  // row_bcast:31 -> rows 2, 3
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+template <> __device__ __forceinline__ uint32_t wave_min<uint32_t>(uint32_t v) { return wave_reduce_dpp<false>(v); }
+template <> __device__ __forceinline__ uint32_t wave_max<uint32_t>(uint32_t v) { return wave_reduce_dpp<true>(v); }
+
 // A workgroup barrier for an LDS hand-off only: it waits for this wave's LDS
 // operations (lgkmcnt), not for its global loads.  __syncthreads' release
 // fence waits for every outstanding load (vmcnt(0)), which held the encode's
