@@ -377,8 +377,26 @@ struct Partials {
   typedef typename KeyOf<V>::K K;
   static constexpr int kPer = (kMinmaxGrid + kBlock - 1) / kBlock;
   K lo[kPer], hi[kPer];
+  int n = 1 << 30;  // records loaded unconditionally: lanes at or past n hold 0
   __device__ __forceinline__ void load(const void* partials, int nparts) {
     const K* p = reinterpret_cast<const K*>(partials);
+    if (sizeof(K) == 4) {
+      // unconditional buffer loads, no exec-masked branches: a record past
+      // nparts reads 0, the max identity; the min's lanes select theirs
+      const int bytes = nparts * 4;
+      const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(const_cast<K*>(p), 0, bytes, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rh =
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<K*>(p + nparts), 0, bytes, 0x00020000);
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) {
+        const int off = ((int)threadIdx.x + k * kBlock) * 4;
+        lo[k] = (K)__builtin_amdgcn_raw_buffer_load_b32(rl, off, 0, 0);
+        hi[k] = (K)__builtin_amdgcn_raw_buffer_load_b32(rh, off, 0, 0);
+      }
+      n = nparts;  // (the min's identity is selected in fold: a select here
+                   // waited for these loads before the tile's were issued)
+      return;
+    }
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
       const int i = (int)threadIdx.x + k * kBlock;
@@ -387,10 +405,12 @@ struct Partials {
     }
   }
   __device__ __forceinline__ void fold(float& mn_f, float& mx_f) const {
-    K l = lo[0], h = hi[0];
+    K l = KeyOf<V>::kLoId, h = hi[0];
 #pragma unroll
-    for (int k = 1; k < kPer; ++k) {
-      l = lo[k] < l ? lo[k] : l;
+    for (int k = 0; k < kPer; ++k) {
+      const K a = (int)threadIdx.x + k * kBlock < n ? lo[k] : KeyOf<V>::kLoId;
+      l = a < l ? a : l;
+      if (k == 0) continue;
       h = hi[k] > h ? hi[k] : h;
     }
     block_minmax(l, h);
@@ -832,7 +852,12 @@ __global__ __launch_bounds__(kBlock) void ff_encode(const V* __restrict__ x, siz
   }
   const size_t tf = t1 < nfull ? t1 : nfull;  // full tiles are [t0, tf)
   Partials<V> parts;
-  if (p.partials != nullptr) parts.load(p.partials, p.nparts);
+  // (f32: loaded unconditionally -- no records without partials -- so that
+  // the loads share the tile's block and nothing consumes them before the
+  // tile's loads are out)
+  if (sizeof(V) == 4) parts.load(p.partials ? p.partials : (const void*)x, p.partials ? p.nparts : 0);
+  else if (p.partials != nullptr) parts.load(p.partials, p.nparts);
+  __builtin_amdgcn_sched_barrier(0);  // the partials' loads stay ahead of the tile's
   V first[4][4];
   if (kVec) prefetch_tile<V>(x, t0, tf, first);
 
