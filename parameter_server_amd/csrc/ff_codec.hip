@@ -177,8 +177,11 @@ template <> __device__ __forceinline__ uint32_t wave_max<uint32_t>(uint32_t v) {
 // partials fold until its first tile had arrived.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// Block-wide (256 threads = 4 waves) min/max of keys; result valid in all threads.
-template <typename K>
+// Block-wide (256 threads = 4 waves) min/max of keys; result valid in all
+// threads (32-bit keys: as scalars).  kOnce: the call site runs once per
+// workgroup, so its LDS slots are never rewritten and the trailing barrier
+// that guards them goes.
+template <typename K, bool kOnce = false>
 __device__ __forceinline__ void block_minmax(K& lo, K& hi) {
   __shared__ K s_lo[kBlock / 64], s_hi[kBlock / 64];
   lo = wave_min(lo);
@@ -192,7 +195,11 @@ __device__ __forceinline__ void block_minmax(K& lo, K& hi) {
     lo = s_lo[w] < lo ? s_lo[w] : lo;
     hi = s_hi[w] > hi ? s_hi[w] : hi;
   }
-  lds_barrier();
+  if constexpr (sizeof(K) == 4) {  // uniform: the key decode that follows runs on the SALU
+    lo = (K)__builtin_amdgcn_readfirstlane((int)lo);
+    hi = (K)__builtin_amdgcn_readfirstlane((int)hi);
+  }
+  if (!kOnce) lds_barrier();
 }
 
 // 4-element vector access of V.  Cache policy (tools/bw_probe3.hip, emulated
@@ -405,15 +412,21 @@ struct Partials {
     }
   }
   __device__ __forceinline__ void fold(float& mn_f, float& mx_f) const {
-    K l = KeyOf<V>::kLoId, h = hi[0];
+    K l = lo[0], h = hi[0];
 #pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      const K a = (int)threadIdx.x + k * kBlock < n ? lo[k] : KeyOf<V>::kLoId;
-      l = a < l ? a : l;
-      if (k == 0) continue;
+    for (int k = 1; k < kPer; ++k) {
+      l = lo[k] < l ? lo[k] : l;
       h = hi[k] > h ? hi[k] : h;
     }
-    block_minmax(l, h);
+    if (n < kPer * kBlock) {  // (uniform) fewer partials than lanes' slots
+      l = KeyOf<V>::kLoId;
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) {
+        const K a = (int)threadIdx.x + k * kBlock < n ? lo[k] : KeyOf<V>::kLoId;
+        l = a < l ? a : l;
+      }
+    }
+    block_minmax<K, true>(l, h);
     if (sizeof(V) == 4) {
       // all-NaN / empty: l stays at the identity, which decodes to a NaN
       float lo_v = key_f32((uint32_t)l), hi_v = key_f32((uint32_t)h);
